@@ -1,0 +1,156 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Criteo-shaped FM training throughput on MI355X.
+
+Metric (BASELINE.json): examples/sec for the whole node, Criteo-shaped FM k=64,
+at 1/2/4/8 MI355X.  One process per GPU (torchrun), RCCL over xGMI.
+
+Workload per step and rank (weak scaling: per-GPU work is fixed as N grows):
+  * B examples x 39 features (13 bucketized integer + 26 categorical Criteo
+    fields, Zipf value popularity), synthetic, generated on the device before
+    timing (a pool of distinct batches is cycled);
+  * FM k=64, fp32 table + fp32 Adagrad slots, hashed vocabulary of
+    125M slots per GPU (1B slots at N=8), row-sharded over the GPUs with RCCL
+    all-to-all for lookups and gradients (mode "shard"); N=1 runs the local
+    single-GPU path;
+  * the timed step is the full training step: id -> key, dedup, (a2a), fused
+    forward + loss, fused backward + Adagrad update, (a2a + owner update).
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] ...
+        (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N)
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+from fast_tffm_amd.data.synthetic import CriteoSynth  # noqa: E402
+from fast_tffm_amd.models.fm import FactorizationMachine, FMConfig  # noqa: E402
+from fast_tffm_amd.ops import kernels as K  # noqa: E402
+from fast_tffm_amd.parallel import dist as fmdist  # noqa: E402
+
+PRESETS = {
+    # BASELINE.json headline: FM k=64 Criteo-shaped, row-sharded 1B slots at N=8
+    "k64": dict(k=64, dtype="fp32", opt="adagrad", mode="auto", slots_per_gpu=125_000_000),
+    # BASELINE config 2: k=16 bf16 table
+    "k16_bf16": dict(k=16, dtype="bf16", opt="adagrad", mode="auto", slots_per_gpu=125_000_000),
+    # BASELINE config 3: k=64 data-parallel, dense all-reduce (small replicated vocabulary)
+    "k64_dp_dense": dict(k=64, dtype="fp32", opt="adagrad", mode="dp_dense", slots_per_gpu=None,
+                         vocab=1_000_000),
+    # BASELINE config 5 (partial: bf16 table, FTRL; fp8 table pending)
+    "k128_ftrl": dict(k=128, dtype="bf16", opt="ftrl", mode="auto", slots_per_gpu=62_500_000),
+}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=131072, help="examples per GPU per step")
+    ap.add_argument("--preset", default="k64", choices=sorted(PRESETS))
+    ap.add_argument("--slots-per-gpu", type=int, default=None, help="override hashed slots per GPU")
+    ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled")
+    ap.add_argument("--alpha", type=float, default=1.1, help="Zipf exponent of field values")
+    ap.add_argument("--mode", default=None, help="override step mode (local|shard|dp|dp_dense)")
+    ap.add_argument("--profile-steps", type=int, default=0, help="also emit a torch.profiler trace")
+    a = ap.parse_args()
+
+    p = dict(PRESETS[a.preset])
+    mode = a.mode or p["mode"]
+    ctx = fmdist.init_distributed(force_pg=mode not in ("auto", "local"))
+    W, rank = ctx.world, ctx.rank
+    if W != a.gpus and rank == 0:
+        print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={W}; using {W}", file=sys.stderr)
+    dev = ctx.device
+    if dev.type != "cuda":
+        print("[bench] no GPU visible: running on CPU (not a valid measurement)", file=sys.stderr)
+    slots = a.slots_per_gpu or p.get("slots_per_gpu")
+    vocab = slots * W if slots else p["vocab"]
+    dtype = torch.bfloat16 if p["dtype"] == "bf16" else torch.float32
+    opt = K.OptConfig(p["opt"], lr=0.01 if p["opt"] == "adagrad" else 0.05, l1=0.001, l2=0.001, beta=1.0,
+                      initial_accumulator=0.1)
+    cfg = FMConfig(vocabulary_size=vocab, factor_num=p["k"], loss_type="logistic", batch_size=a.batch,
+                   init_value_range=0.01, seed=42, dtype=dtype, opt=opt, mode=mode)
+    t0 = time.time()
+    model = FactorizationMachine(cfg, device=dev, dist=ctx if W > 1 or mode not in ("auto", "local") else None)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    if rank == 0:
+        print(f"[bench] {model.table.memory_report()} (init {time.time() - t0:.1f}s), mode={model.mode}, "
+              f"vocab={vocab}, B/gpu={a.batch}", file=sys.stderr)
+
+    gen = CriteoSynth(vocab, alpha=a.alpha, seed=1000 + rank, device=dev)
+    pool = [gen.batch(a.batch) for _ in range(max(1, a.pool))]
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+
+    for i in range(a.warmup):
+        model.train_step(pool[i % len(pool)])
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    ctx.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+
+    t_start = time.perf_counter()
+    last = None
+    for i in range(a.steps):
+        last = model.train_step(pool[i % len(pool)])
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    ctx.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    elapsed = ctx.all_reduce_scalar(elapsed, op="max")
+
+    loss = last.mean_loss() if last is not None else float("nan")
+    if a.profile_steps and rank == 0:
+        from fast_tffm_amd.utils.trace import profile_steps
+
+        profile_steps(lambda i: model.train_step(pool[i % len(pool)]), a.profile_steps,
+                      os.path.join(ROOT, "gpurun_out", "bench_trace.json"))
+
+    ex_total = a.batch * W * a.steps
+    value = ex_total / elapsed
+    ms = elapsed / a.steps * 1e3
+    if rank == 0:
+        par = ("rowshard%d" % W) if model.mode == "shard" else (model.mode + str(W) if W > 1 else "single")
+        print(f"[bench] loss={loss:.5f} ms/step={ms:.3f} ex/s={value:.4g}", file=sys.stderr)
+        print(json.dumps({
+            "metric": "examples/sec (whole node), Criteo-shaped FM k=%d" % p["k"],
+            "value": value,
+            "unit": "examples/s",
+            "n_gpus": W,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": ms,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32" if dtype == torch.float32 else "bf16",
+            "data": "synthetic Criteo-shaped (39 fields, Zipf a=%.2f), random-init weights" % a.alpha,
+            "config": {
+                "model": "FM k=%d, %s table + %s, hashed vocab %d (%d/GPU)" % (
+                    p["k"], p["dtype"], p["opt"], vocab, vocab // W if model.mode == "shard" else vocab),
+                "global_batch": a.batch * W,
+                "seq_len": 39,
+                "parallelism": par,
+            },
+        }), flush=True)
+    fmdist.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,125 @@
+"""Build the native extensions in-tree (fast_tffm_amd/_native/).
+
+* ``_fm_cpu``: host C++ (g++ -O3 -fopenmp): libsvm parser, Hash64, CPU step
+  kernels.  Needed everywhere (CPU tests, data pipeline).
+* ``_fm_hip``: gfx950 HIP (hipcc --offload-arch=gfx950): the GPU hot path.
+
+The reference builds one TF op library with a monkey-patched setuptools
+(reference setup.py:88-201); here each module is one explicit compiler
+invocation, so the build is reproducible from a shell and needs neither
+hipify nor torch's cpp_extension JIT.
+
+Usage:  python -m fast_tffm_amd.build_native [--cpu-only|--hip-only] [--force]
+"""
+
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG, "csrc")
+OUT = os.path.join(PKG, "_native")
+ARCH = os.environ.get("FM_OFFLOAD_ARCH", "gfx950")
+
+CPU_SOURCES = ["cpu/module.cpp", "cpu/parser.cpp", "cpu/kernels.cpp"]
+HIP_SOURCES = ["hip/module.hip"]
+HIP_DEPS = ["hip/fm_kernels.hip", "hip/dedup.hip", "hip/fm_common.h", "hip/step.hip", "hash64.h"]
+
+
+_EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"  # resolved once (lazy init is not thread-safe)
+
+
+def _ext_suffix() -> str:
+    return _EXT_SUFFIX
+
+
+def _py_includes() -> list[str]:
+    import pybind11
+
+    incs = {sysconfig.get_paths()["include"], sysconfig.get_paths()["platinclude"], pybind11.get_include()}
+    return [f"-I{p}" for p in sorted(incs)]
+
+
+def _stale(target: str, sources: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    for s in sources:
+        p = os.path.join(CSRC, s)
+        if os.path.exists(p) and os.path.getmtime(p) > t:
+            return True
+    return False
+
+
+def _run(cmd: list[str]) -> None:
+    print("[build_native]", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def build_cpu(force: bool = False) -> str:
+    os.makedirs(OUT, exist_ok=True)
+    target = os.path.join(OUT, "_fm_cpu" + _ext_suffix())
+    deps = CPU_SOURCES + ["cpu/parser.h", "cpu/kernels.h", "hash64.h"]
+    if force or _stale(target, deps):
+        cxx = os.environ.get("CXX", "g++")
+        tmp = target + ".tmp"
+        cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-fvisibility=hidden",
+               *_py_includes(), *[os.path.join(CSRC, s) for s in CPU_SOURCES], "-o", tmp]
+        _run(cmd)
+        os.replace(tmp, target)
+    return target
+
+
+def hipcc_path() -> str | None:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    return None
+
+
+def build_hip(force: bool = False) -> str:
+    os.makedirs(OUT, exist_ok=True)
+    target = os.path.join(OUT, "_fm_hip" + _ext_suffix())
+    if force or _stale(target, HIP_SOURCES + HIP_DEPS):
+        hipcc = hipcc_path()
+        if hipcc is None:
+            raise RuntimeError("hipcc not found; cannot build the gfx950 extension")
+        tmp = target + ".tmp"
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
+               "-Wno-unused-result", *_py_includes(), f"-I{CSRC}",
+               *[os.path.join(CSRC, s) for s in HIP_SOURCES], "-o", tmp]
+        _run(cmd)
+        os.replace(tmp, target)
+    return target
+
+
+def build_all(force: bool = False, cpu: bool = True, hip: bool = True) -> list[str]:
+    jobs = []
+    with ThreadPoolExecutor(max_workers=2) as ex:
+        if cpu:
+            jobs.append(ex.submit(build_cpu, force))
+        if hip:
+            jobs.append(ex.submit(build_hip, force))
+        return [j.result() for j in jobs]
+
+
+def main(argv: list[str] | None = None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--cpu-only", action="store_true")
+    ap.add_argument("--hip-only", action="store_true")
+    ap.add_argument("--force", action="store_true")
+    a = ap.parse_args(argv)
+    outs = build_all(force=a.force, cpu=not a.hip_only, hip=not a.cpu_only)
+    for o in outs:
+        print("built", o)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

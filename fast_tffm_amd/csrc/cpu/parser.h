@@ -1,0 +1,50 @@
+// libsvm -> CSR parser (host C++), the replacement for the reference's
+// FmParser TF op (cc/fm_parser_op.cc:8-123).
+//
+// Grammar, exactly as the reference's ParseLine (cc/fm_parser_op.cc:58-109):
+//   <label> <fid>[:<fval>] <fid>[:<fval>] ...
+//   * label via strtof; failure -> "Label could not be read in example: <line>"
+//   * every token is preceded by exactly one ' ' (else "Invalid format in
+//     example: <line>"); a single trailing ' ' is accepted;
+//   * non-hash ids: strtoll base 10, must be in [0, vocab_size) (else
+//     "Invalid format in example: ..." / "Invalid feature id. Should be in
+//     range [0, vocabulary_size).<line>");
+//   * hash ids: the token up to ' ', ':' or end is hashed with TF Hash64 and
+//     taken modulo vocab_size (cc/fm_parser_op.cc:82-84);
+//   * optional ":<fval>" via strtof (else "Invalid feature value. <line>"),
+//     default value 1.
+// Unlike the reference (one line at a time on one thread) a batch is split
+// over worker threads; the per-thread CSR pieces are concatenated in line
+// order, so the output is identical to a sequential parse.
+#pragma once
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace fm {
+
+struct ParseError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+struct CsrBatch {
+  std::vector<float> labels;
+  std::vector<int32_t> sizes;
+  std::vector<int64_t> ids;
+  std::vector<float> vals;
+};
+
+// Parse one line (not NUL-terminated: [s, s+len)) and append to `out`.
+void parse_line(const char* s, size_t len, int64_t vocab_size, bool hash_feature_id, CsrBatch& out,
+                std::string& scratch);
+
+// Parse `n` lines given as (pointer, length) spans with up to `threads` threads.
+void parse_lines(const char* const* ptrs, const size_t* lens, size_t n, int64_t vocab_size,
+                 bool hash_feature_id, int threads, CsrBatch& out);
+
+// Parse one float per line (weight files; tf.string_to_number semantics:
+// the whole line must be a number, surrounding whitespace allowed).
+void parse_floats(const char* const* ptrs, const size_t* lens, size_t n, float* out);
+
+}  // namespace fm

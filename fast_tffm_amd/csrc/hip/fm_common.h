@@ -1,0 +1,120 @@
+// Shared device helpers for the gfx950 FM kernels.
+//
+// Conventions used by every kernel in this directory
+//  * wave64: lane = threadIdx.x & 63, 256-thread workgroups (4 waves).
+//  * Factor rows are stored "v-first": a row of the V table holds Kp factor
+//    values (Kp = K rounded up so that one lane moves exactly 16 bytes), the
+//    linear weight w lives in a separate fp32 array (or at column Kp of a packed
+//    exchange row).  The reference keeps w at column 0 of a [V, K+1] block
+//    (fm_model.py:270-284); the checkpoint exporter restores that layout.
+//  * A row is read by LPR lanes ("lanes per row", a power of two) with one
+//    16-byte load each, so one wave instruction moves G = 64/LPR whole rows.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <cstdint>
+
+namespace fm {
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / kWave;
+
+enum LossType : int { kLossNone = 0, kLossMse = 1, kLossLogistic = 2 };
+enum OptType : int { kOptAdagrad = 0, kOptFtrl = 1, kOptSgd = 2 };
+enum DType : int { kF32 = 0, kBF16 = 1 };
+
+// ---- 16-byte row fragments ------------------------------------------------
+template <typename T> struct Frag;
+
+template <> struct Frag<float> {
+  static constexpr int N = 4;  // elements per lane
+  __device__ static inline void load(const float* p, float (&o)[4]) {
+    const float4 v = *reinterpret_cast<const float4*>(p);
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+  }
+  __device__ static inline void store(float* p, const float (&o)[4]) {
+    *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+};
+
+__device__ inline float bf16_bits_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
+// Round-to-nearest-even f32 -> bf16 bits (NaN stays NaN: quiet bit forced).
+__device__ inline uint32_t f32_to_bf16_bits(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (u >> 16) | 0x40u;
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+
+template <> struct Frag<__hip_bfloat16> {
+  static constexpr int N = 8;
+  __device__ static inline void load(const __hip_bfloat16* p, float (&o)[8]) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o[2 * i] = bf16_bits_to_f32(w[i] & 0xffffu);
+      o[2 * i + 1] = bf16_bits_to_f32(w[i] >> 16);
+    }
+  }
+  __device__ static inline void store(__hip_bfloat16* p, const float (&o)[8]) {
+    uint4 v;
+    v.x = f32_to_bf16_bits(o[0]) | (f32_to_bf16_bits(o[1]) << 16);
+    v.y = f32_to_bf16_bits(o[2]) | (f32_to_bf16_bits(o[3]) << 16);
+    v.z = f32_to_bf16_bits(o[4]) | (f32_to_bf16_bits(o[5]) << 16);
+    v.w = f32_to_bf16_bits(o[6]) | (f32_to_bf16_bits(o[7]) << 16);
+    *reinterpret_cast<uint4*>(p) = v;
+  }
+};
+
+// ---- wave reductions (xor butterfly inside a lane group) -------------------
+template <int WIDTH>
+__device__ inline float group_sum(float v) {
+#pragma unroll
+  for (int o = WIDTH / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+// Sum over the row groups of a wave: lanes t, t+LPR, t+2*LPR, ...
+template <int LPR>
+__device__ inline float across_groups_sum(float v) {
+#pragma unroll
+  for (int o = LPR; o < kWave; o <<= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+__device__ inline float softplus_neg_abs(float p) {  // log(1 + exp(-|p|))
+  return log1pf(__expf(-fabsf(p)));
+}
+
+__device__ inline float sigmoidf(float p) { return 1.f / (1.f + __expf(-p)); }
+
+// Optimizer hyper-parameters, passed by value in kernargs.
+struct OptParams {
+  int type;          // OptType
+  float lr;          // learning rate (adagrad / sgd) or alpha (ftrl)
+  float l1, l2;      // ftrl regularisers
+  float beta;        // ftrl beta
+};
+
+// In-place per-element optimizer step on fp32 registers. `s0`/`s1` are the
+// optimizer state values (adagrad: s0 = accumulator; ftrl: s0 = n, s1 = z).
+__device__ inline void opt_step(const OptParams& o, float g, float& p, float& s0, float& s1) {
+  if (o.type == kOptAdagrad) {
+    // TF SparseApplyAdagrad: accum += g^2; var -= lr * g * rsqrt(accum)
+    s0 += g * g;
+    p -= o.lr * g * rsqrtf(s0);
+  } else if (o.type == kOptFtrl) {
+    // TF ApplyFtrl with lr_power = -0.5 (plus optional beta).
+    const float n_new = s0 + g * g;
+    const float sq_old = sqrtf(s0), sq_new = sqrtf(n_new);
+    s1 += g - (sq_new - sq_old) / o.lr * p;
+    s0 = n_new;
+    const float quad = (o.beta + sq_new) / o.lr + 2.f * o.l2;
+    p = fabsf(s1) > o.l1 ? (copysignf(o.l1, s1) - s1) / quad : 0.f;
+  } else {
+    p -= o.lr * g;
+  }
+}
+
+}  // namespace fm

@@ -1,0 +1,179 @@
+// Python binding of the gfx950 kernels (module fast_tffm_amd._native._fm_hip).
+//
+// The binding is deliberately thin: every entry point takes raw device
+// pointers (Python ints from torch.Tensor.data_ptr()) and the HIP stream handle
+// (torch.cuda.current_stream().cuda_stream), launches asynchronously and
+// returns. Shape/dtype validation lives in fast_tffm_amd/ops/kernels.py; no
+// libtorch headers are needed here, which keeps the gfx950 build small and
+// lets the same kernels be called from torch streams, hipGraph captures and
+// the C++ step executor alike.
+#include <pybind11/pybind11.h>
+#include <stdexcept>
+#include <string>
+#include "fm_common.h"
+
+namespace py = pybind11;
+using u64 = std::uintptr_t;
+
+// Unity build: the kernel sources are compiled in this translation unit.
+#include "fm_kernels.hip"
+#include "dedup.hip"
+
+namespace {
+
+template <typename T> T* P(u64 p) { return reinterpret_cast<T*>(p); }
+hipStream_t S(u64 s) { return reinterpret_cast<hipStream_t>(s); }
+
+void check(int code, const char* what) {
+  if (code != 0) {
+    std::string msg = std::string(what) + " failed: ";
+    msg += code > 0 ? hipGetErrorString(static_cast<hipError_t>(code)) : ("code " + std::to_string(code));
+    throw std::runtime_error(msg);
+  }
+}
+
+fm::OptParams opt_params(int type, float lr, float l1, float l2, float beta) {
+  fm::OptParams o;
+  o.type = type; o.lr = lr; o.l1 = l1; o.l2 = l2; o.beta = beta;
+  return o;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_fm_hip, m) {
+  m.doc() = "gfx950 HIP kernels for fast_tffm_amd (FM forward/backward/optimizer, dedup, sharding)";
+  m.attr("ARCH") = "gfx950";
+
+  m.def("fwd_grid", &fm::fwd_grid, py::arg("B"));
+  m.def("lanes_per_row", &fm::lanes_per_row, py::arg("Kp"), py::arg("dtype"));
+
+  m.def(
+      "fwd",
+      [](int B, u64 offsets, u64 rows, u64 vals, u64 v, long long v_stride, u64 w, long long w_stride, int Kp,
+         int dtype, u64 labels, u64 weights, int loss_type, float grad_scale, u64 pred, u64 r1, u64 dpred,
+         u64 loss_partial, u64 reg_partial, int grid, u64 stream) {
+        fm::FwdArgs a;
+        a.B = B; a.offsets = P<const int>(offsets); a.rows = P<const int>(rows);
+        a.vals = P<const float>(vals); a.v = P<const void>(v); a.v_stride = v_stride;
+        a.w = P<const float>(w); a.w_stride = w_stride; a.Kp = Kp;
+        a.labels = P<const float>(labels); a.weights = P<const float>(weights);
+        a.loss_type = loss_type; a.grad_scale = grad_scale; a.pred = P<float>(pred);
+        a.r1 = P<float>(r1); a.dpred = P<float>(dpred); a.loss_partial = P<float>(loss_partial);
+        a.reg_partial = P<float>(reg_partial);
+        check(fm::launch_fwd(a, dtype, grid, S(stream)), "fm_fwd");
+      },
+      py::arg("B"), py::arg("offsets"), py::arg("rows"), py::arg("vals"), py::arg("v"), py::arg("v_stride"),
+      py::arg("w"), py::arg("w_stride"), py::arg("Kp"), py::arg("dtype"), py::arg("labels"), py::arg("weights"),
+      py::arg("loss_type"), py::arg("grad_scale"), py::arg("pred"), py::arg("r1"), py::arg("dpred"),
+      py::arg("loss_partial"), py::arg("reg_partial"), py::arg("grid"), py::arg("stream"));
+
+  m.def(
+      "bwd",
+      [](int mode, u64 num_chunks, u64 chunk_seg, u64 chunk_start, u64 num_unique, u64 seg_start, u64 uniq,
+         u64 sorted_ex, u64 sorted_x, u64 dpred, u64 r1, int Kp, int CH, u64 v, long long v_stride, u64 w,
+         long long w_stride, u64 s0v, u64 s1v, long long s_stride, u64 s0w, u64 s1w, float reg_v, float reg_w,
+         int opt_type, float lr, float l1, float l2, float beta, u64 grad_out, long long g_stride, u64 partial,
+         int dtype, long long max_chunks, long long max_unique, u64 stream) {
+        fm::BwdArgs a;
+        a.mode = mode; a.num_chunks = P<const int>(num_chunks); a.chunk_seg = P<const int>(chunk_seg);
+        a.chunk_start = P<const int>(chunk_start); a.num_unique = P<const int>(num_unique);
+        a.seg_start = P<const int>(seg_start); a.uniq = P<const int>(uniq);
+        a.sorted_ex = P<const int>(sorted_ex); a.sorted_x = P<const float>(sorted_x);
+        a.dpred = P<const float>(dpred); a.r1 = P<const float>(r1); a.Kp = Kp; a.CH = CH;
+        a.v = P<void>(v); a.v_stride = v_stride; a.w = P<float>(w); a.w_stride = w_stride;
+        a.s0v = P<float>(s0v); a.s1v = P<float>(s1v); a.s_stride = s_stride; a.s0w = P<float>(s0w);
+        a.s1w = P<float>(s1w); a.reg_v = reg_v; a.reg_w = reg_w;
+        a.opt = opt_params(opt_type, lr, l1, l2, beta);
+        a.grad_out = P<float>(grad_out); a.g_stride = g_stride; a.partial = P<float>(partial);
+        check(fm::launch_bwd(a, dtype, max_chunks, max_unique, S(stream)), "fm_bwd");
+      },
+      py::arg("mode"), py::arg("num_chunks"), py::arg("chunk_seg"), py::arg("chunk_start"), py::arg("num_unique"),
+      py::arg("seg_start"), py::arg("uniq"), py::arg("sorted_ex"), py::arg("sorted_x"), py::arg("dpred"),
+      py::arg("r1"), py::arg("Kp"), py::arg("CH"), py::arg("v"), py::arg("v_stride"), py::arg("w"),
+      py::arg("w_stride"), py::arg("s0v"), py::arg("s1v"), py::arg("s_stride"), py::arg("s0w"), py::arg("s1w"),
+      py::arg("reg_v"), py::arg("reg_w"), py::arg("opt_type"), py::arg("lr"), py::arg("l1"), py::arg("l2"),
+      py::arg("beta"), py::arg("grad_out"), py::arg("g_stride"), py::arg("partial"), py::arg("dtype"),
+      py::arg("max_chunks"), py::arg("max_unique"), py::arg("stream"));
+
+  m.def("dedup_workspace_bytes", &fm::dedup_workspace_bytes, py::arg("n"));
+
+  m.def(
+      "dedup",
+      [](int n, int end_bit, u64 keys, u64 iota, u64 skeys, u64 perm, u64 uniq, u64 seg_start, u64 num_unique,
+         u64 inv, u64 ex_of_occ, u64 sorted_ex, u64 vals, u64 sorted_x, u64 ws, size_t ws_bytes, u64 stream) {
+        fm::DedupArgs a;
+        a.n = n; a.end_bit = end_bit; a.keys = P<const uint32_t>(keys); a.iota = P<const int>(iota);
+        a.skeys = P<uint32_t>(skeys); a.perm = P<int>(perm); a.uniq = P<uint32_t>(uniq);
+        a.seg_start = P<int>(seg_start); a.num_unique = P<int>(num_unique); a.inv = P<int>(inv);
+        a.ex_of_occ = P<const int>(ex_of_occ); a.sorted_ex = P<int>(sorted_ex); a.vals = P<const float>(vals);
+        a.sorted_x = P<float>(sorted_x); a.ws = P<void>(ws); a.ws_bytes = ws_bytes;
+        check(fm::launch_dedup(a, S(stream)), "dedup");
+      },
+      py::arg("n"), py::arg("end_bit"), py::arg("keys"), py::arg("iota"), py::arg("skeys"), py::arg("perm"),
+      py::arg("uniq"), py::arg("seg_start"), py::arg("num_unique"), py::arg("inv"), py::arg("ex_of_occ"),
+      py::arg("sorted_ex"), py::arg("vals"), py::arg("sorted_x"), py::arg("ws"), py::arg("ws_bytes"),
+      py::arg("stream"));
+
+  m.def(
+      "chunk_plan",
+      [](int n, u64 num_unique, u64 seg_start, int CH, u64 chunk_start, u64 chunk_seg, u64 num_chunks, u64 ws,
+         size_t ws_bytes, u64 stream) {
+        check(fm::launch_chunk_plan(n, P<const int>(num_unique), P<const int>(seg_start), CH, P<int>(chunk_start),
+                                    P<int>(chunk_seg), P<int>(num_chunks), P<void>(ws), ws_bytes, S(stream)),
+              "chunk_plan");
+      },
+      py::arg("n"), py::arg("num_unique"), py::arg("seg_start"), py::arg("CH"), py::arg("chunk_start"),
+      py::arg("chunk_seg"), py::arg("num_chunks"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"));
+
+  m.def(
+      "gather_rows",
+      [](int R, u64 req, u64 v, long long v_stride, u64 w, long long w_stride, int Kp, int dtype, u64 out,
+         long long o_stride, u64 stream) {
+        fm::GatherArgs a;
+        a.R = R; a.req = P<const int>(req); a.v = P<const void>(v); a.v_stride = v_stride;
+        a.w = P<const float>(w); a.w_stride = w_stride; a.Kp = Kp; a.out = P<float>(out); a.o_stride = o_stride;
+        check(fm::launch_gather_rows(a, dtype, S(stream)), "gather_rows");
+      },
+      py::arg("R"), py::arg("req"), py::arg("v"), py::arg("v_stride"), py::arg("w"), py::arg("w_stride"),
+      py::arg("Kp"), py::arg("dtype"), py::arg("out"), py::arg("o_stride"), py::arg("stream"));
+
+  m.def(
+      "apply_rows",
+      [](u64 num_unique, u64 seg_start, u64 uniq, u64 perm, u64 grad_in, long long g_stride, int Kp, u64 v,
+         long long v_stride, u64 w, long long w_stride, u64 s0v, u64 s1v, long long s_stride, u64 s0w, u64 s1w,
+         int opt_type, float lr, float l1, float l2, float beta, int dtype, long long max_unique, u64 stream) {
+        fm::ApplyArgs a;
+        a.num_unique = P<const int>(num_unique); a.seg_start = P<const int>(seg_start);
+        a.uniq = P<const int>(uniq); a.perm = P<const int>(perm); a.grad_in = P<const float>(grad_in);
+        a.g_stride = g_stride; a.Kp = Kp; a.v = P<void>(v); a.v_stride = v_stride; a.w = P<float>(w);
+        a.w_stride = w_stride; a.s0v = P<float>(s0v); a.s1v = P<float>(s1v); a.s_stride = s_stride;
+        a.s0w = P<float>(s0w); a.s1w = P<float>(s1w); a.opt = opt_params(opt_type, lr, l1, l2, beta);
+        check(fm::launch_apply_rows(a, dtype, max_unique, S(stream)), "apply_rows");
+      },
+      py::arg("num_unique"), py::arg("seg_start"), py::arg("uniq"), py::arg("perm"), py::arg("grad_in"),
+      py::arg("g_stride"), py::arg("Kp"), py::arg("v"), py::arg("v_stride"), py::arg("w"), py::arg("w_stride"),
+      py::arg("s0v"), py::arg("s1v"), py::arg("s_stride"), py::arg("s0w"), py::arg("s1w"), py::arg("opt_type"),
+      py::arg("lr"), py::arg("l1"), py::arg("l2"), py::arg("beta"), py::arg("dtype"), py::arg("max_unique"),
+      py::arg("stream"));
+
+  m.def(
+      "init_rows",
+      [](u64 v, long long v_stride, u64 w, long long w_stride, long long rows, int K, int Kp, int dtype,
+         long long gid_mul, long long gid_add, unsigned long long seed, float range, u64 stream) {
+        fm::InitArgs a;
+        a.v = P<void>(v); a.v_stride = v_stride; a.w = P<float>(w); a.w_stride = w_stride; a.rows = rows;
+        a.K = K; a.Kp = Kp; a.dtype = dtype; a.gid_mul = gid_mul; a.gid_add = gid_add; a.seed = seed;
+        a.range = range;
+        check(fm::launch_init_rows(a, S(stream)), "init_rows");
+      },
+      py::arg("v"), py::arg("v_stride"), py::arg("w"), py::arg("w_stride"), py::arg("rows"), py::arg("K"),
+      py::arg("Kp"), py::arg("dtype"), py::arg("gid_mul"), py::arg("gid_add"), py::arg("seed"), py::arg("range"),
+      py::arg("stream"));
+
+  m.def(
+      "csr_rows",
+      [](int B, u64 offsets, u64 ex_of_occ, u64 stream) {
+        check(fm::launch_csr_rows(B, P<const int>(offsets), P<int>(ex_of_occ), S(stream)), "csr_rows");
+      },
+      py::arg("B"), py::arg("offsets"), py::arg("ex_of_occ"), py::arg("stream"));
+}

@@ -1,0 +1,179 @@
+"""The factorization machine and its fused training step.
+
+Reference behaviour (tffm/fm_model.py:267-365): embedding_lookup of the unique
+ids -> FmScorer -> loss (mean of weighted logistic/MSE) -> Adagrad.minimize of
+``loss + reg_score / batch_size`` (``batch_size`` = the configured one).
+
+Here the step is an explicit pipeline of native kernels, no autograd graph:
+
+  local (world == 1):   fwd+loss (direct table gather) | dedup -> bwd+optimizer
+  shard (row-sharded):  dedup -> a2a(ids) -> owner gather -> a2a(rows) -> fwd
+                        -> bwd(emit grads) -> a2a(grads) -> owner sum+optimizer
+  dp    (replicated):   local fwd/bwd(emit) -> all_gather(ids, grads) -> every
+                        rank applies the identical merged update
+  dp_dense:             dense all_reduce of a [vocab, Kp+4] gradient buffer
+
+The reference trains asynchronously (between-graph replication, no
+SyncReplicasOptimizer: run_tffm.py:204-211); these modes are synchronous SPMD.
+``grad_reduce = sum`` (default) adds every rank's mean-loss gradient, which is
+what W asynchronous workers apply per W steps; ``mean`` divides by W.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+
+from ..data.batch import Batch
+from ..ops import kernels as K
+from .table import FMTable, bits_for, rows_per_shard
+
+
+@dataclass
+class FMConfig:
+    vocabulary_size: int
+    factor_num: int
+    loss_type: str = "mse"            # "mse" | "logistic"
+    factor_lambda: float = 0.0
+    bias_lambda: float = 0.0
+    batch_size: int = 50000           # configured batch size: reg_score / batch_size (fm_model.py:345-347)
+    init_value_range: float = 0.01
+    seed: int = 0
+    dtype: torch.dtype = torch.float32
+    opt: K.OptConfig = field(default_factory=K.OptConfig)
+    mode: str = "auto"                # auto | local | shard | dp | dp_dense
+    grad_reduce: str = "sum"          # sum | mean (multi-rank)
+    dedup_chunk: int = 32             # CH of the segmented backward
+    threads: int = 0                  # CPU kernels (0 = OpenMP default)
+
+
+@dataclass
+class StepOut:
+    loss_sum: torch.Tensor            # 0-d, summed weighted loss of this rank's batch
+    n: int                            # examples in this rank's batch
+
+    def mean_loss(self) -> float:
+        return float(self.loss_sum) / max(self.n, 1)
+
+
+class _Workspace:
+    """Per-step buffers, grown on demand and then reused (no per-step allocation)."""
+
+    def __init__(self, device: torch.device, Kp: int, CH: int):
+        self.device, self.Kp, self.CH = device, Kp, CH
+        self.cap_b = self.cap_n = 0
+
+    def ensure(self, B: int, nnz: int) -> None:
+        dev, Kp = self.device, self.Kp
+        if B > self.cap_b:
+            cap = max(B, int(self.cap_b * 1.25))
+            self.pred = torch.empty(cap, dtype=torch.float32, device=dev)
+            self.dpred = torch.empty(cap, dtype=torch.float32, device=dev)
+            self.r1 = torch.empty((cap, Kp), dtype=torch.float32, device=dev)
+            self.cap_b = cap
+        if nnz > self.cap_n:
+            cap = max(nnz, int(self.cap_n * 1.25), 1)
+            self.dd = K.DedupWorkspace(cap, dev, self.CH)
+            self.rows32 = torch.empty(cap, dtype=torch.int32, device=dev)
+            self.bwd_partial = (torch.empty((cap, Kp + 4), dtype=torch.float32, device=dev)
+                                if dev.type == "cuda" else None)
+            self.cap_n = cap
+        if not hasattr(self, "fwd_partial"):
+            self.fwd_partial = torch.zeros(3 * 4096, dtype=torch.float32, device=dev)
+
+
+class FactorizationMachine:
+    """FM model + step executor for one rank."""
+
+    def __init__(self, cfg: FMConfig, device: torch.device | str = "cpu", dist=None):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dist = dist
+        self.world = dist.world if dist is not None else 1
+        self.rank = dist.rank if dist is not None else 0
+        mode = cfg.mode
+        if mode == "auto":
+            mode = "local" if self.world == 1 else "shard"
+        if mode == "local" and self.world > 1:
+            raise ValueError("mode=local needs world_size == 1")
+        self.mode = mode
+        sharded = mode == "shard"
+        self.table = FMTable(cfg.vocabulary_size, cfg.factor_num, world=self.world if sharded else 1,
+                             rank=self.rank if sharded else 0, dtype=cfg.dtype, opt=cfg.opt,
+                             init_range=cfg.init_value_range, seed=cfg.seed, device=self.device)
+        self.K, self.Kp = self.table.K, self.table.Kp
+        self.rps = rows_per_shard(cfg.vocabulary_size, self.world) if sharded else cfg.vocabulary_size
+        self.ws = _Workspace(self.device, self.Kp, cfg.dedup_chunk)
+        self.global_step = 0
+        self._exchange = None
+        if mode in ("shard", "dp", "dp_dense") and self.world >= 1 and dist is not None:
+            from ..parallel.exchange import make_exchange
+
+            self._exchange = make_exchange(self)
+        elif mode != "local":
+            raise ValueError(f"mode={mode} needs a distributed context")
+
+    # ------------------------------------------------------------------
+    @property
+    def reg_coeffs(self) -> tuple[float, float]:
+        """(lambda_f, lambda_b) / configured batch size: d(reg_score / batch_size)/d(params) scale."""
+        s = 1.0 / float(self.cfg.batch_size)
+        if self.world > 1 and self.cfg.grad_reduce == "mean":
+            s /= self.world
+        return self.cfg.factor_lambda * s, self.cfg.bias_lambda * s
+
+    def grad_scale(self, B: int) -> float:
+        s = 1.0 / max(B, 1)
+        if self.world > 1 and self.cfg.grad_reduce == "mean":
+            s /= self.world
+        return s
+
+    def _rows32(self, b: Batch) -> torch.Tensor:
+        out = self.ws.rows32[: b.nnz]
+        out.copy_(b.ids)  # int64 -> int32 (ids < vocabulary_size < 2^31)
+        return out
+
+    # ------------------------------------------------------------------
+    def train_step(self, b: Batch) -> StepOut:
+        self.ws.ensure(b.B, b.nnz)
+        if self._exchange is not None:
+            out = self._exchange.train_step(b)
+        else:
+            out = self._local_train_step(b)
+        self.global_step += 1
+        return out
+
+    def _local_train_step(self, b: Batch) -> StepOut:
+        ws, cfg = self.ws, self.cfg
+        rows = self._rows32(b)
+        ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz)
+        fo = K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,
+                          weights=b.weights, loss=cfg.loss_type, grad_scale=self.grad_scale(b.B), want_r1=True,
+                          pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
+                          threads=cfg.threads)
+        dd = K.dedup(rows, ws=ws.dd, key_bits=bits_for(self.table.rows), ex_of_occ=ex, vals=b.vals)
+        rv, rw = self.reg_coeffs
+        K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
+                      reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads)
+        return StepOut(fo.loss_sum, b.B)
+
+    # ------------------------------------------------------------------
+    @torch.no_grad()
+    def forward(self, b: Batch, *, loss: str = "none", want_reg: bool = False) -> K.FwdOut:
+        """Scores (and optionally the summed loss) without touching parameters."""
+        if self._exchange is not None:
+            return self._exchange.forward(b, loss=loss, want_reg=want_reg)
+        rows = b.ids.to(torch.int32)
+        return K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,
+                            weights=b.weights, loss=loss, grad_scale=1.0, want_r1=False, want_reg=want_reg,
+                            threads=self.cfg.threads)
+
+    def predict(self, b: Batch) -> torch.Tensor:
+        """Raw scores (logits for logistic loss), like the reference's pred_ops (run_tffm.py:10-17)."""
+        return self.forward(b).pred
+
+    def eval_loss(self, b: Batch) -> float:
+        """Weighted mean loss of the configured type (reference valid_op, fm_model.py:317-333)."""
+        fo = self.forward(b, loss=self.cfg.loss_type)
+        return float(fo.loss_sum) / max(b.B, 1)

@@ -1,0 +1,129 @@
+"""Parameter table of the FM: hashed feature id -> (w, v[0..K)).
+
+Reference: ``vocabulary_block_num`` TF variables ``vocab_block_i`` of shape
+``[vocabulary_size // N + 1, K + 1]``, global id ``g`` in block ``g % N`` row
+``g // N``, column 0 = w, columns 1..K = v (tffm/fm_model.py:269-291), plus the
+Adagrad slot per variable.
+
+Here one process owns one *shard* of rows with the same "mod" rule over the
+data-parallel world (``owner = g % world``, ``local row = g // world``).  The
+storage is HBM-friendly rather than reference-shaped:
+
+* ``v``   [rows, Kp]  fp32 or bf16, Kp = K padded to 16-byte rows (pads are 0);
+* ``w``   [rows]      fp32 (linear weight, kept separate so v rows stay aligned);
+* ``s0v``/``s0w``     optimizer slot 0 (Adagrad accumulator / FTRL n), fp32;
+* ``s1v``/``s1w``     optimizer slot 1 (FTRL z), fp32.
+
+The checkpoint module converts to and from the reference layout.
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..ops import kernels as K
+from ..ops import native
+
+
+def rows_per_shard(vocab_size: int, world: int) -> int:
+    return (vocab_size + world - 1) // world
+
+
+def shard_rows(vocab_size: int, world: int, rank: int) -> int:
+    """Rows owned by ``rank``: ids g with g % world == rank and g < vocab_size."""
+    return max(0, (vocab_size - rank + world - 1) // world)
+
+
+class FMTable:
+    def __init__(self, vocab_size: int, factor_num: int, *, world: int = 1, rank: int = 0,
+                 dtype: torch.dtype = torch.float32, opt: K.OptConfig | None = None, init_range: float = 0.01,
+                 seed: int = 0, device: torch.device | str = "cpu", init: bool = True):
+        self.vocab_size = int(vocab_size)
+        self.K = int(factor_num)
+        self.world, self.rank = int(world), int(rank)
+        self.dtype = dtype
+        self.Kp = K.padded_k(self.K, dtype)
+        self.opt = opt or K.OptConfig()
+        self.device = torch.device(device)
+        self.rows = max(1, shard_rows(self.vocab_size, self.world, self.rank))
+        self.init_range = float(init_range)
+        self.seed = int(seed)
+        dev = self.device
+        self.v = torch.zeros((self.rows, self.Kp), dtype=dtype, device=dev)
+        self.w = torch.zeros(self.rows, dtype=torch.float32, device=dev)
+        acc0 = float(self.opt.initial_accumulator)
+        n_state = max(1, self.opt.n_state)  # kernels always address slot 0
+        self.s0v = torch.full((self.rows, self.Kp), acc0 if self.opt.name in ("adagrad", "ftrl") else 0.0,
+                              dtype=torch.float32, device=dev)
+        self.s0w = torch.full((self.rows,), acc0 if self.opt.name in ("adagrad", "ftrl") else 0.0,
+                              dtype=torch.float32, device=dev)
+        self.s1v = torch.zeros((self.rows, self.Kp), dtype=torch.float32, device=dev) if n_state > 1 else None
+        self.s1w = torch.zeros((self.rows,), dtype=torch.float32, device=dev) if n_state > 1 else None
+        if init:
+            self.reinit()
+
+    # ------------------------------------------------------------------
+    @property
+    def state(self) -> K.TableState:
+        return K.TableState(self.v, self.w, self.s0v, self.s1v, self.s0w, self.s1w)
+
+    def reinit(self, seed: int | None = None) -> None:
+        """U(-r, r) over w and v[:K] as a pure function of (seed, global id, column)."""
+        seed = self.seed if seed is None else int(seed)
+        args = dict(v=self.v.data_ptr(), v_stride=self.v.stride(0), w=self.w.data_ptr(), w_stride=1,
+                    rows=self.rows, K=self.K, Kp=self.Kp, dtype=K.dtype_code(self.dtype), gid_mul=self.world,
+                    gid_add=self.rank, seed=seed & 0xFFFFFFFFFFFFFFFF, range=self.init_range)
+        if self.device.type == "cuda":
+            native.hip().init_rows(**args, stream=torch.cuda.current_stream(self.device).cuda_stream)
+        else:
+            native.cpu().init_rows(**args)
+        self._zero_dead_rows()
+
+    def _zero_dead_rows(self) -> None:
+        # the last shard may own fewer real ids than allocated rows (rows >= 1)
+        real = shard_rows(self.vocab_size, self.world, self.rank)
+        if real < self.rows:
+            self.v[real:].zero_()
+            self.w[real:].zero_()
+
+    def global_ids(self) -> torch.Tensor:
+        return torch.arange(self.rows, device=self.device, dtype=torch.int64) * self.world + self.rank
+
+    def nbytes(self) -> int:
+        tot = 0
+        for t in (self.v, self.w, self.s0v, self.s0w, self.s1v, self.s1w):
+            if t is not None:
+                tot += t.numel() * t.element_size()
+        return tot
+
+    # ------------------------------------------------------------------
+    def reference_rows(self, local_rows: torch.Tensor | None = None) -> torch.Tensor:
+        """Rows in the reference layout [n, K+1] (col 0 = w, cols 1..K = v), fp32."""
+        if local_rows is None:
+            v, w = self.v, self.w
+        else:
+            v, w = self.v[local_rows], self.w[local_rows]
+        return torch.cat([w.unsqueeze(1), v[:, : self.K].float()], dim=1)
+
+    def load_reference_rows(self, local_rows: torch.Tensor, rows_ref: torch.Tensor,
+                            acc_ref: torch.Tensor | None = None) -> None:
+        """Write reference-layout rows ([n, K+1]) and optional Adagrad slot rows into this shard."""
+        rows_ref = rows_ref.to(self.device, torch.float32)
+        self.w[local_rows] = rows_ref[:, 0]
+        self.v[local_rows, : self.K] = rows_ref[:, 1:].to(self.dtype)
+        if acc_ref is not None:
+            acc_ref = acc_ref.to(self.device, torch.float32)
+            self.s0w[local_rows] = acc_ref[:, 0]
+            self.s0v[local_rows, : self.K] = acc_ref[:, 1:]
+
+    def memory_report(self) -> str:
+        gb = self.nbytes() / 2**30
+        return (f"table shard rank {self.rank}/{self.world}: {self.rows} rows x K={self.K} (Kp={self.Kp}, "
+                f"{str(self.dtype).replace('torch.', '')}), opt={self.opt.name}: {gb:.2f} GiB")
+
+
+def bits_for(n: int) -> int:
+    """Number of key bits needed to represent values in [0, n)."""
+    return max(1, int(math.ceil(math.log2(max(n, 2)))))

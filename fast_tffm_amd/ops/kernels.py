@@ -1,0 +1,427 @@
+"""Typed, validated wrappers over the native step kernels.
+
+Every wrapper dispatches on the device of its tensors: CUDA (HIP) tensors go to
+the gfx950 kernels of ``_fm_hip``, CPU tensors to ``_fm_cpu``.  Launches are
+asynchronous on the current torch stream; nothing here synchronises the host
+unless ``FM_DEBUG_CHECKS=1`` asks for index range checks.
+
+Row layout contract (see csrc/hip/fm_common.h): a factor table ``v`` is
+``[rows, Kp]`` (fp32 or bf16, Kp padded so that a lane moves 16 bytes), the
+linear weights ``w`` are a separate fp32 vector (or column ``Kp`` of a packed
+``[rows, Kp+4]`` exchange buffer, passed as a strided view).
+"""
+
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+
+from . import native
+
+LOSS_TYPES = {"none": 0, "mse": 1, "logistic": 2}
+OPT_TYPES = {"adagrad": 0, "ftrl": 1, "sgd": 2}
+BWD_LOCAL, BWD_EMIT = 0, 1
+
+_DEBUG = os.environ.get("FM_DEBUG_CHECKS", "0") == "1"
+
+
+def set_debug_checks(on: bool) -> None:
+    global _DEBUG
+    _DEBUG = bool(on)
+
+
+def dtype_code(t: torch.dtype) -> int:
+    if t == torch.float32:
+        return 0
+    if t == torch.bfloat16:
+        return 1
+    raise TypeError(f"unsupported table dtype {t}; use float32 or bfloat16")
+
+
+def elems_per_lane(dtype: torch.dtype) -> int:
+    return 16 // torch.tensor([], dtype=dtype).element_size()
+
+
+def padded_k(K: int, dtype: torch.dtype = torch.float32) -> int:
+    """Factor columns stored per row: K rounded up to a 16-byte multiple (and at least 8)."""
+    e = max(elems_per_lane(dtype), 8) if dtype == torch.bfloat16 else elems_per_lane(dtype)
+    return ((K + e - 1) // e) * e
+
+
+@dataclass
+class OptConfig:
+    name: str = "adagrad"
+    lr: float = 0.01
+    l1: float = 0.0
+    l2: float = 0.0
+    beta: float = 0.0
+    initial_accumulator: float = 0.1
+
+    @property
+    def code(self) -> int:
+        return OPT_TYPES[self.name]
+
+    @property
+    def n_state(self) -> int:
+        return 2 if self.name == "ftrl" else (1 if self.name == "adagrad" else 0)
+
+
+def _p(t: torch.Tensor | None) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def _is_gpu(t: torch.Tensor) -> bool:
+    return t.device.type == "cuda"
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _check(cond: bool, msg: str) -> None:
+    if not cond:
+        raise ValueError(msg)
+
+
+def _chk_vec(t: torch.Tensor | None, dtype: torch.dtype, n: int | None, name: str, dev: torch.device) -> None:
+    if t is None:
+        return
+    _check(t.dtype == dtype, f"{name}: expected {dtype}, got {t.dtype}")
+    _check(t.device == dev, f"{name}: expected device {dev}, got {t.device}")
+    _check(t.is_contiguous(), f"{name}: must be contiguous")
+    if n is not None:
+        _check(t.numel() >= n, f"{name}: needs >= {n} elements, has {t.numel()}")
+
+
+def _chk_rows(v: torch.Tensor, Kp: int, name: str) -> int:
+    """Validate a row-major factor source and return its row stride in elements."""
+    _check(v.dim() == 2, f"{name}: expected 2-D rows")
+    _check(v.stride(1) == 1, f"{name}: rows must be contiguous")
+    epl = elems_per_lane(v.dtype)
+    _check(Kp % epl == 0, f"{name}: Kp={Kp} must be a multiple of {epl} for {v.dtype}")
+    _check(v.shape[1] >= Kp, f"{name}: has {v.shape[1]} columns < Kp={Kp}")
+    _check(v.stride(0) % epl == 0, f"{name}: row stride {v.stride(0)} must be a multiple of {epl}")
+    _check(v.data_ptr() % 16 == 0, f"{name}: base must be 16-byte aligned")
+    return v.stride(0)
+
+
+def _range_check(idx: torch.Tensor, hi: int, name: str) -> None:
+    if _DEBUG and idx.numel() > 0:
+        lo_v, hi_v = int(idx.min()), int(idx.max())
+        _check(lo_v >= 0 and hi_v < hi, f"{name}: index range [{lo_v}, {hi_v}] outside [0, {hi})")
+
+
+# ---------------------------------------------------------------------------
+# forward
+# ---------------------------------------------------------------------------
+class FwdOut:
+    """Outputs of fm_forward. ``loss_sum``/``regv``/``regw`` are 0-d tensors on the op's device."""
+
+    __slots__ = ("pred", "r1", "dpred", "loss_sum", "regv", "regw")
+
+    def __init__(self, pred, r1, dpred, loss_sum, regv, regw):
+        self.pred, self.r1, self.dpred = pred, r1, dpred
+        self.loss_sum, self.regv, self.regw = loss_sum, regv, regw
+
+
+def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | None, v: torch.Tensor,
+               w: torch.Tensor, Kp: int, *, labels: torch.Tensor | None = None,
+               weights: torch.Tensor | None = None, loss: str = "none", grad_scale: float = 1.0,
+               want_r1: bool = True, want_reg: bool = False, pred: torch.Tensor | None = None,
+               r1: torch.Tensor | None = None, dpred: torch.Tensor | None = None,
+               partial: torch.Tensor | None = None, threads: int = 0) -> FwdOut:
+    """FM score of a CSR batch (reference FmScorer, cc/fm_scorer_op.h:101-140), fused with the loss.
+
+    pred_i = sum_j x_j w_j + 1/2 sum_k [(sum_j x_j v_jk)^2 - sum_j x_j^2 v_jk^2]
+    With ``loss`` in {mse, logistic} also returns the summed weighted loss and
+    ``dpred = grad_scale * dL_i/dpred_i``.
+    """
+    dev = rows.device
+    B = offsets.numel() - 1
+    _chk_vec(offsets, torch.int32, B + 1, "offsets", dev)
+    nnz = rows.numel()
+    _chk_vec(rows, torch.int32, nnz, "rows", dev)
+    _chk_vec(vals, torch.float32, nnz, "vals", dev)
+    v_stride = _chk_rows(v, Kp, "v")
+    _check(w.dim() == 1 or (w.dim() == 2 and w.shape[1] == 1), "w: expected a vector (possibly strided)")
+    _check(w.dtype == torch.float32 and w.device == dev, "w: expected float32 on the rows' device")
+    w_stride = w.stride(0)
+    _check(w.shape[0] >= v.shape[0], "w: fewer rows than v")
+    lt = LOSS_TYPES[loss]
+    if lt:
+        _chk_vec(labels, torch.float32, B, "labels", dev)
+        _chk_vec(weights, torch.float32, B, "weights", dev)
+    _range_check(rows, v.shape[0], "rows")
+    if pred is None:
+        pred = torch.empty(B, dtype=torch.float32, device=dev)
+    if want_r1 and r1 is None:
+        r1 = torch.empty((B, Kp), dtype=torch.float32, device=dev)
+    if not want_r1:
+        r1 = None
+    if lt and dpred is None:
+        dpred = torch.empty(B, dtype=torch.float32, device=dev)
+    dt = dtype_code(v.dtype)
+    if _is_gpu(rows):
+        h = native.hip()
+        grid = h.fwd_grid(max(B, 1))
+        if partial is None or partial.numel() < 3 * grid:
+            partial = torch.zeros(3 * grid, dtype=torch.float32, device=dev)
+        lp = partial[:grid]
+        rp = partial[grid:3 * grid]
+        h.fwd(B=B, offsets=_p(offsets), rows=_p(rows), vals=_p(vals), v=_p(v), v_stride=v_stride, w=_p(w),
+              w_stride=w_stride, Kp=Kp, dtype=dt, labels=_p(labels), weights=_p(weights), loss_type=lt,
+              grad_scale=float(grad_scale), pred=_p(pred), r1=_p(r1), dpred=_p(dpred) if lt else 0,
+              loss_partial=_p(lp) if lt else 0, reg_partial=_p(rp) if want_reg else 0, grid=grid,
+              stream=_stream(rows))
+        loss_sum = lp.sum(dtype=torch.float32) if lt else None
+        regv = rp.view(grid, 2)[:, 0].sum() if want_reg else None
+        regw = rp.view(grid, 2)[:, 1].sum() if want_reg else None
+    else:
+        c = native.cpu()
+        ls, rv, rw = c.fwd(B=B, offsets=_p(offsets), rows=_p(rows), vals=_p(vals), v=_p(v), v_stride=v_stride,
+                           w=_p(w), w_stride=w_stride, Kp=Kp, dtype=dt, labels=_p(labels), weights=_p(weights),
+                           loss_type=lt, grad_scale=float(grad_scale), pred=_p(pred), r1=_p(r1),
+                           dpred=_p(dpred) if lt else 0, threads=threads)
+        loss_sum = torch.tensor(ls, dtype=torch.float32) if lt else None
+        regv = torch.tensor(rv, dtype=torch.float32) if want_reg else None
+        regw = torch.tensor(rw, dtype=torch.float32) if want_reg else None
+    return FwdOut(pred, r1, dpred if lt else None, loss_sum, regv, regw)
+
+
+# ---------------------------------------------------------------------------
+# dedup
+# ---------------------------------------------------------------------------
+class DedupOut:
+    """Grouping of a batch's occurrences by key.
+
+    ``num_unique`` is a 1-element int32 device tensor (no host sync);
+    ``U_host`` is set on CPU (and after ``.sync()``).
+    """
+
+    __slots__ = ("n", "skeys", "perm", "uniq", "seg_start", "num_unique", "inv", "sorted_ex", "sorted_x",
+                 "chunk_start", "chunk_seg", "num_chunks", "U_host", "CH")
+
+    def __init__(self, **kw):
+        for k in self.__slots__:
+            setattr(self, k, kw.get(k))
+
+    def sync(self) -> int:
+        if self.U_host is None:
+            self.U_host = int(self.num_unique.item())
+        return self.U_host
+
+    def unique_keys(self) -> torch.Tensor:
+        return self.uniq[: self.sync()]
+
+
+class DedupWorkspace:
+    """Reusable device buffers for dedup + chunk plan of up to ``cap`` occurrences."""
+
+    def __init__(self, cap: int, device: torch.device, CH: int = 32):
+        self.cap, self.device, self.CH = cap, device, CH
+        i32 = dict(dtype=torch.int32, device=device)
+        self.iota = torch.arange(max(cap, 1), **i32)
+        self.skeys = torch.empty(max(cap, 1), **i32)
+        self.perm = torch.empty(max(cap, 1), **i32)
+        self.uniq = torch.empty(max(cap, 1), **i32)
+        self.seg_start = torch.empty(cap + 1, **i32)
+        self.num_unique = torch.zeros(1, **i32)
+        self.inv = torch.empty(max(cap, 1), **i32)
+        self.sorted_ex = torch.empty(max(cap, 1), **i32)
+        self.sorted_x = torch.empty(max(cap, 1), dtype=torch.float32, device=device)
+        self.ex_of_occ = torch.empty(max(cap, 1), **i32)
+        self.chunk_start = torch.empty(cap + 1, **i32)
+        self.chunk_seg = torch.empty(max(cap, 1), **i32)
+        self.num_chunks = torch.zeros(1, **i32)
+        if device.type == "cuda":
+            nbytes = native.hip().dedup_workspace_bytes(max(cap, 1))
+            self.ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        else:
+            self.ws = None
+
+
+def csr_rows(offsets: torch.Tensor, out: torch.Tensor | None = None, nnz: int | None = None) -> torch.Tensor:
+    """Example index of every CSR occurrence (the reference gets it implicitly from feature_poses)."""
+    B = offsets.numel() - 1
+    if nnz is None:
+        nnz = int(offsets[-1])
+    if out is None:
+        out = torch.empty(nnz, dtype=torch.int32, device=offsets.device)
+    if _is_gpu(offsets):
+        native.hip().csr_rows(B=B, offsets=_p(offsets), ex_of_occ=_p(out), stream=_stream(offsets))
+    else:
+        native.cpu().csr_rows(B=B, offsets=_p(offsets), ex_of_occ=_p(out))
+    return out
+
+
+def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int = 32,
+          ex_of_occ: torch.Tensor | None = None, vals: torch.Tensor | None = None, want_inv: bool = False,
+          want_chunks: bool = True, CH: int | None = None) -> DedupOut:
+    """Sort-based unique over non-negative int32 keys (reference tf.unique, fm_model.py:72).
+
+    Unique keys come out in ascending order (the reference's first-occurrence
+    order is an implementation detail no result depends on).
+    """
+    dev = keys.device
+    n = keys.numel()
+    _chk_vec(keys, torch.int32, n, "keys", dev)
+    if ws is None or ws.cap < n:
+        ws = DedupWorkspace(max(n, 1), dev, CH or 32)
+    CH = CH or ws.CH
+    if ex_of_occ is not None:
+        _chk_vec(ex_of_occ, torch.int32, n, "ex_of_occ", dev)
+    if vals is not None:
+        _chk_vec(vals, torch.float32, n, "vals", dev)
+    key_bits = max(1, min(32, int(key_bits)))
+    out = DedupOut(n=n, skeys=ws.skeys, perm=ws.perm, uniq=ws.uniq, seg_start=ws.seg_start,
+                   num_unique=ws.num_unique, inv=ws.inv if want_inv else None,
+                   sorted_ex=ws.sorted_ex if ex_of_occ is not None else None,
+                   sorted_x=ws.sorted_x if vals is not None else None, CH=CH)
+    if _is_gpu(keys):
+        h = native.hip()
+        st = _stream(keys)
+        h.dedup(n=n, end_bit=key_bits, keys=_p(keys), iota=_p(ws.iota), skeys=_p(ws.skeys), perm=_p(ws.perm),
+                uniq=_p(ws.uniq), seg_start=_p(ws.seg_start), num_unique=_p(ws.num_unique), inv=_p(out.inv),
+                ex_of_occ=_p(ex_of_occ), sorted_ex=_p(out.sorted_ex), vals=_p(vals), sorted_x=_p(out.sorted_x),
+                ws=_p(ws.ws), ws_bytes=ws.ws.numel(), stream=st)
+        if want_chunks:
+            h.chunk_plan(n=n, num_unique=_p(ws.num_unique), seg_start=_p(ws.seg_start), CH=CH,
+                         chunk_start=_p(ws.chunk_start), chunk_seg=_p(ws.chunk_seg), num_chunks=_p(ws.num_chunks),
+                         ws=_p(ws.ws), ws_bytes=ws.ws.numel(), stream=st)
+            out.chunk_start, out.chunk_seg, out.num_chunks = ws.chunk_start, ws.chunk_seg, ws.num_chunks
+    else:
+        U = native.cpu().dedup(n=n, keys=_p(keys), skeys=_p(ws.skeys), perm=_p(ws.perm), uniq=_p(ws.uniq),
+                               seg_start=_p(ws.seg_start), inv=_p(out.inv), ex_of_occ=_p(ex_of_occ),
+                               sorted_ex=_p(out.sorted_ex), vals=_p(vals), sorted_x=_p(out.sorted_x))
+        ws.num_unique.fill_(U)
+        out.U_host = U
+    return out
+
+
+# ---------------------------------------------------------------------------
+# backward (+ optimizer)
+# ---------------------------------------------------------------------------
+@dataclass
+class TableState:
+    """Parameters and optimizer slots of one (local) table shard."""
+
+    v: torch.Tensor                 # [rows, Kp] fp32 / bf16
+    w: torch.Tensor                 # [rows] fp32
+    s0v: torch.Tensor | None = None  # adagrad accumulator / ftrl n   [rows, Kp] fp32
+    s1v: torch.Tensor | None = None  # ftrl z                          [rows, Kp] fp32
+    s0w: torch.Tensor | None = None  # [rows]
+    s1w: torch.Tensor | None = None  # [rows]
+
+
+def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *, mode: int,
+                table: TableState | None = None, opt: OptConfig | None = None,
+                src_v: torch.Tensor | None = None, src_w: torch.Tensor | None = None,
+                grad_out: torch.Tensor | None = None, reg_v: float = 0.0, reg_w: float = 0.0,
+                partial: torch.Tensor | None = None, threads: int = 0) -> torch.Tensor | None:
+    """Segmented FM backward over the dedup grouping (reference FmGrad, cc/fm_grad_op.h:59-163).
+
+    Per unique row u with occurrences (i, x):
+      g_v = sum x*dpred_i*(r1_i - x*v) + reg_v * n_u * v
+      g_w = sum x*dpred_i            + reg_w * n_u * w
+    mode=BWD_LOCAL applies ``opt`` in place on ``table`` rows ``uniq[u]``;
+    mode=BWD_EMIT writes [g_v, g_w] rows into ``grad_out[u]`` (``src_v``/``src_w``
+    hold the gathered parameter rows in unique order).
+    """
+    dev = dpred.device
+    _check(dd.sorted_ex is not None, "dedup must be run with ex_of_occ")
+    _chk_vec(dpred, torch.float32, None, "dpred", dev)
+    _check(r1.dtype == torch.float32 and r1.is_contiguous() and r1.shape[1] == Kp, "r1: [B, Kp] fp32 contiguous")
+    if mode == BWD_LOCAL:
+        _check(table is not None and opt is not None, "LOCAL mode needs table + opt")
+        v, w = table.v, table.w
+        dt = dtype_code(v.dtype)
+        _check(opt.name == "sgd" or table.s0v is not None, "optimizer state missing")
+        s_stride = table.s0v.stride(0) if table.s0v is not None else 0
+        s0v, s1v, s0w, s1w = table.s0v, table.s1v, table.s0w, table.s1w
+        if opt.name == "sgd":  # kernels always touch s0: give them scratch
+            s0v, s0w, s_stride = (table.s0v, table.s0w, s_stride)
+        gstride, gptr = 0, 0
+    else:
+        _check(src_v is not None and src_w is not None and grad_out is not None, "EMIT mode needs src + grad_out")
+        v, w = src_v, src_w
+        dt = 0
+        _check(v.dtype == torch.float32, "EMIT source rows must be fp32")
+        s0v = s1v = s0w = s1w = None
+        s_stride = 0
+        _check(grad_out.dtype == torch.float32 and grad_out.stride(1) == 1, "grad_out: fp32 rows")
+        gstride, gptr = grad_out.stride(0), grad_out.data_ptr()
+        _check(gstride >= Kp + 1 and gstride % 4 == 0, "grad_out row stride must be >= Kp+1 and a multiple of 4")
+    v_stride = _chk_rows(v, Kp, "v")
+    o = opt or OptConfig()
+    if _is_gpu(dpred):
+        h = native.hip()
+        if partial is None:
+            partial = torch.empty((max(dd.n, 1), Kp + 4), dtype=torch.float32, device=dev)
+        _check(partial.numel() >= max(dd.n, 1) * (Kp + 4), "partial scratch too small")
+        h.bwd(mode=mode, num_chunks=_p(dd.num_chunks), chunk_seg=_p(dd.chunk_seg), chunk_start=_p(dd.chunk_start),
+              num_unique=_p(dd.num_unique), seg_start=_p(dd.seg_start), uniq=_p(dd.uniq),
+              sorted_ex=_p(dd.sorted_ex), sorted_x=_p(dd.sorted_x), dpred=_p(dpred), r1=_p(r1), Kp=Kp, CH=dd.CH,
+              v=_p(v), v_stride=v_stride, w=_p(w), w_stride=w.stride(0), s0v=_p(s0v), s1v=_p(s1v),
+              s_stride=s_stride, s0w=_p(s0w), s1w=_p(s1w), reg_v=float(reg_v), reg_w=float(reg_w),
+              opt_type=o.code, lr=float(o.lr), l1=float(o.l1), l2=float(o.l2), beta=float(o.beta),
+              grad_out=gptr, g_stride=gstride, partial=_p(partial), dtype=dt, max_chunks=dd.n,
+              max_unique=dd.n, stream=_stream(dpred))
+    else:
+        U = dd.sync()
+        native.cpu().bwd(mode=mode, U=U, seg_start=_p(dd.seg_start), uniq=_p(dd.uniq), sorted_ex=_p(dd.sorted_ex),
+                         sorted_x=_p(dd.sorted_x), dpred=_p(dpred), r1=_p(r1), Kp=Kp, v=_p(v), v_stride=v_stride,
+                         w=_p(w), w_stride=w.stride(0), s0v=_p(s0v), s1v=_p(s1v), s_stride=s_stride, s0w=_p(s0w),
+                         s1w=_p(s1w), reg_v=float(reg_v), reg_w=float(reg_w), opt_type=o.code, lr=float(o.lr),
+                         l1=float(o.l1), l2=float(o.l2), beta=float(o.beta), grad_out=gptr, g_stride=gstride,
+                         dtype=dt, threads=threads)
+    return grad_out
+
+
+# ---------------------------------------------------------------------------
+# row-sharded helpers
+# ---------------------------------------------------------------------------
+def gather_rows(req: torch.Tensor, table: TableState, Kp: int, out: torch.Tensor, threads: int = 0) -> torch.Tensor:
+    """out[p] = [v[req[p]], w[req[p]], 0...] (fp32), the owner side of a sharded lookup."""
+    dev = req.device
+    R = req.numel()
+    _chk_vec(req, torch.int32, R, "req", dev)
+    v_stride = _chk_rows(table.v, Kp, "v")
+    _check(out.dtype == torch.float32 and out.stride(1) == 1 and out.shape[0] >= R, "out: fp32 rows")
+    _check(out.stride(0) >= Kp + 4 and out.stride(0) % 4 == 0, "out row stride")
+    _range_check(req, table.v.shape[0], "req")
+    dt = dtype_code(table.v.dtype)
+    if _is_gpu(req):
+        native.hip().gather_rows(R=R, req=_p(req), v=_p(table.v), v_stride=v_stride, w=_p(table.w),
+                                 w_stride=table.w.stride(0), Kp=Kp, dtype=dt, out=_p(out), o_stride=out.stride(0),
+                                 stream=_stream(req))
+    else:
+        native.cpu().gather_rows(R=R, req=_p(req), v=_p(table.v), v_stride=v_stride, w=_p(table.w),
+                                 w_stride=table.w.stride(0), Kp=Kp, dtype=dt, out=_p(out), o_stride=out.stride(0),
+                                 threads=threads)
+    return out
+
+
+def apply_rows(dd: DedupOut, grad_in: torch.Tensor, table: TableState, opt: OptConfig, Kp: int,
+               threads: int = 0) -> None:
+    """Owner side of a sharded update: sum received grad rows per table row, then one optimizer step."""
+    v_stride = _chk_rows(table.v, Kp, "v")
+    _check(grad_in.dtype == torch.float32 and grad_in.stride(1) == 1, "grad_in: fp32 rows")
+    dt = dtype_code(table.v.dtype)
+    s_stride = table.s0v.stride(0) if table.s0v is not None else 0
+    if _is_gpu(grad_in):
+        native.hip().apply_rows(num_unique=_p(dd.num_unique), seg_start=_p(dd.seg_start), uniq=_p(dd.uniq),
+                                perm=_p(dd.perm), grad_in=_p(grad_in), g_stride=grad_in.stride(0), Kp=Kp,
+                                v=_p(table.v), v_stride=v_stride, w=_p(table.w), w_stride=table.w.stride(0),
+                                s0v=_p(table.s0v), s1v=_p(table.s1v), s_stride=s_stride, s0w=_p(table.s0w),
+                                s1w=_p(table.s1w), opt_type=opt.code, lr=float(opt.lr), l1=float(opt.l1),
+                                l2=float(opt.l2), beta=float(opt.beta), dtype=dt, max_unique=max(dd.n, 1),
+                                stream=_stream(grad_in))
+    else:
+        native.cpu().apply_rows(U=dd.sync(), seg_start=_p(dd.seg_start), uniq=_p(dd.uniq), perm=_p(dd.perm),
+                                grad_in=_p(grad_in), g_stride=grad_in.stride(0), Kp=Kp, v=_p(table.v),
+                                v_stride=v_stride, w=_p(table.w), w_stride=table.w.stride(0), s0v=_p(table.s0v),
+                                s1v=_p(table.s1v), s_stride=s_stride, s0w=_p(table.s0w), s1w=_p(table.s1w),
+                                opt_type=opt.code, lr=float(opt.lr), l1=float(opt.l1), l2=float(opt.l2),
+                                beta=float(opt.beta), dtype=dt, threads=threads)
