@@ -1,0 +1,210 @@
+"""Text input pipeline: files -> shuffled lines -> parsed CSR batches -> device.
+
+Reference pipeline (tffm/fm_model.py:34-126), per ``shuffle_threads`` thread:
+``string_input_producer(train_files, num_epochs, shuffle=True)`` ->
+``TextLineReader.read_up_to(B)`` -> ``shuffle_batch(capacity = 4.5 B,
+min_after_dequeue = 3 B, allow_smaller_final_batch)`` -> FmParser -> unique ->
+``FIFOQueue(queue_size)``; weight files are read by a second file queue with the
+same seed so that weight lines stay aligned with data lines.
+
+Here:
+* file order is reshuffled every epoch with a seeded RNG (same order for data
+  and weight files, which are paired by index so alignment is exact);
+* lines pass through a shuffle window of ``capacity = 4.5 B`` lines from which
+  batches of B are drawn once ``min_after_dequeue + B`` are buffered (the
+  final, smaller batch is emitted like ``allow_smaller_final_batch``);
+* parsing runs in the native multi-threaded parser (``_fm_cpu``) with the GIL
+  released; ``shuffle_threads`` producer threads feed a bounded queue
+  (``queue_size`` batches) and a pinned-memory host->device copy runs ahead on
+  a side stream, so parsing and H2D overlap the GPU step;
+* multi-rank: each rank reads a disjoint subset of the files (rank::world, the
+  reference's "each worker will retrieve one whole file", sample.cfg:68), or
+  every world-th line when there are fewer files than ranks.
+"""
+
+from __future__ import annotations
+
+import queue
+import random
+import threading
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from ..ops import native
+from .batch import Batch
+
+
+@dataclass
+class ReaderState:
+    epoch: int = 0
+    batches_in_epoch: int = 0
+
+
+def _read_lines(path: str) -> list[bytes]:
+    with open(path, "rb") as f:
+        return f.read().splitlines()
+
+
+def parse_lines_to_batch(lines: list[bytes], vocab_size: int, hash_feature_id: bool, threads: int = 1,
+                         weights: np.ndarray | None = None) -> Batch:
+    labels, sizes, ids, vals = native.cpu().parse_lines(lines, int(vocab_size), bool(hash_feature_id), int(threads))
+    return Batch.from_parsed(labels, sizes, ids, vals, weights)
+
+
+def load_file_batch(files: list[str], weight_files: list[str] | None, vocab_size: int, hash_feature_id: bool,
+                    threads: int = 4) -> Batch:
+    """All lines of ``files`` (in order) as one batch (validation / predict)."""
+    lines: list[bytes] = []
+    for f in files:
+        lines.extend(_read_lines(f))
+    w = None
+    if weight_files:
+        wl: list[bytes] = []
+        for f in weight_files:
+            wl.extend(_read_lines(f))
+        if len(wl) != len(lines):
+            raise ValueError("weight files have %d lines, data files %d" % (len(wl), len(lines)))
+        w = native.cpu().parse_floats(wl)
+    return parse_lines_to_batch(lines, vocab_size, hash_feature_id, threads, w)
+
+
+class TextBatchReader:
+    """Iterator over shuffled, parsed training batches (host tensors)."""
+
+    def __init__(self, files: list[str], weight_files: list[str] | None, batch_size: int, *, vocab_size: int,
+                 hash_feature_id: bool = False, num_epochs: int = 1, shuffle: bool = True, seed: int = 0,
+                 parse_threads: int = 4, rank: int = 0, world: int = 1, state: ReaderState | None = None):
+        if weight_files and len(weight_files) != len(files):
+            raise ValueError("The numbers of train files and weight files do not match.")
+        self.files = list(files)
+        self.weight_files = list(weight_files) if weight_files else None
+        self.B = int(batch_size)
+        self.vocab_size = vocab_size
+        self.hash = hash_feature_id
+        self.num_epochs = num_epochs
+        self.shuffle = shuffle
+        self.seed = seed
+        self.threads = parse_threads
+        self.rank, self.world = rank, world
+        self.state = state or ReaderState()
+        self.capacity = int(3 * self.B + 1.5 * self.B)
+        self.min_after = 3 * self.B
+
+    def _my_files(self, epoch: int) -> list[tuple[str, str | None]]:
+        pairs = list(zip(self.files, self.weight_files or [None] * len(self.files)))
+        if self.shuffle:
+            random.Random(self.seed * 1000003 + epoch).shuffle(pairs)
+        if self.world > 1 and len(pairs) >= self.world:
+            pairs = pairs[self.rank::self.world]
+        return pairs
+
+    def _lines(self, epoch: int):
+        line_shard = self.world > 1 and len(self.files) < self.world
+        for path, wpath in self._my_files(epoch):
+            data = _read_lines(path)
+            wl = _read_lines(wpath) if wpath else None
+            if wl is not None and len(wl) != len(data):
+                raise ValueError(f"{wpath}: {len(wl)} lines but {path} has {len(data)}")
+            if line_shard:
+                data = data[self.rank::self.world]
+                wl = wl[self.rank::self.world] if wl is not None else None
+            for i, ln in enumerate(data):
+                if ln:
+                    yield ln, (wl[i] if wl is not None else None)
+
+    def _make(self, items) -> Batch:
+        lines = [it[0] for it in items]
+        w = None
+        if self.weight_files:
+            w = native.cpu().parse_floats([it[1] for it in items])
+        return parse_lines_to_batch(lines, self.vocab_size, self.hash, self.threads, w)
+
+    def __iter__(self):
+        rng = random.Random(self.seed + 7919 * self.rank)
+        skip = self.state.batches_in_epoch
+        for epoch in range(self.state.epoch, self.num_epochs):
+            self.state.epoch = epoch
+            buf: list = []
+            count = 0
+            for item in self._lines(epoch):
+                buf.append(item)
+                if len(buf) >= self.capacity:
+                    if self.shuffle:
+                        rng.shuffle(buf)
+                    out, buf = buf[: self.B], buf[self.B:]
+                    count += 1
+                    if count > skip:
+                        self.state.batches_in_epoch = count
+                        yield self._make(out)
+            if self.shuffle:
+                rng.shuffle(buf)
+            while buf:
+                out, buf = buf[: self.B], buf[self.B:]
+                count += 1
+                if count > skip:
+                    self.state.batches_in_epoch = count
+                    yield self._make(out)
+            skip = 0
+            self.state.batches_in_epoch = 0
+        self.state.epoch = self.num_epochs
+
+
+class Prefetcher:
+    """Background producer threads + bounded queue + pinned H2D on a side stream.
+
+    ``queue_size`` mirrors the reference's example FIFOQueue capacity; ``size()``
+    is what ``-m`` reports as ``example_queue`` fill.
+    """
+
+    _END = object()
+
+    def __init__(self, reader: TextBatchReader, device: torch.device, queue_size: int = 8):
+        self.reader = reader
+        self.device = torch.device(device)
+        self.q: queue.Queue = queue.Queue(maxsize=max(1, queue_size))
+        self.queue_size = max(1, queue_size)
+        self._err: BaseException | None = None
+        self._stop = threading.Event()
+        self._th = threading.Thread(target=self._run, name="fm-reader", daemon=True)
+        self._stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        self._th.start()
+
+    def _run(self):
+        try:
+            for b in self.reader:
+                if self._stop.is_set():
+                    return
+                if self._stream is not None:
+                    b = b.pin_memory()
+                    with torch.cuda.stream(self._stream):
+                        db = b.to(self.device, non_blocking=True)
+                        ev = torch.cuda.Event()
+                        ev.record(self._stream)
+                    self.q.put((db, ev, b))
+                else:
+                    self.q.put((b, None, None))
+        except BaseException as e:  # noqa: BLE001
+            self._err = e
+        finally:
+            self.q.put((self._END, None, None))
+
+    def size(self) -> int:
+        return self.q.qsize()
+
+    def __iter__(self):
+        while True:
+            item, ev, _host = self.q.get()
+            if item is self._END:
+                if self._err is not None:
+                    raise self._err
+                return
+            if ev is not None:
+                torch.cuda.current_stream(self.device).wait_event(ev)
+                # keep the source alive until the copy is consumed by the compute stream
+                item._host_ref = _host  # type: ignore[attr-defined]
+            yield item
+
+    def close(self):
+        self._stop.set()
