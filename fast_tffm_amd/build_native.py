@@ -29,7 +29,8 @@ ARCH = os.environ.get("FM_OFFLOAD_ARCH", "gfx950")
 
 CPU_SOURCES = ["cpu/module.cpp", "cpu/parser.cpp", "cpu/kernels.cpp"]
 HIP_SOURCES = ["hip/module.hip"]
-HIP_DEPS = ["hip/fm_kernels.hip", "hip/dedup.hip", "hip/fm_common.h", "hip/step.hip", "hash64.h"]
+HIP_DEPS = ["hip/fm_fwd.hip", "hip/fm_bwd.hip", "hip/dedup.hip", "hip/shard.hip", "hip/init.hip",
+            "hip/fm_common.h", "hash64.h"]
 
 
 _EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"  # resolved once (lazy init is not thread-safe)

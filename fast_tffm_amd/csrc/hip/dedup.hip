@@ -2,83 +2,86 @@
 // (reference tffm/fm_model.py:72, :133, :173) and for the implicit grouping the
 // reference's FmGrad gets from 168M fp32 atomicAdds (cc/fm_grad_op.h:84-104).
 //
-// Pipeline (all sizes that depend on the data stay on the device, so the whole
-// chain is hipGraph-capturable and needs no host sync):
-//   1. stable LSD radix sort of (key, occurrence) pairs, only over the key bits
-//      actually used (rocPRIM onesweep);
-//   2. head flags + inclusive scan -> segment id of every sorted occurrence;
-//   3. emit: unique keys, segment starts, U, inverse map occurrence->segment,
-//      and the per-sorted-occurrence example index / value the backward reads
-//      contiguously;
-//   4. chunk plan: rows with more than CH occurrences (hot ids) are cut into
-//      CH-sized chunks so that no lane group of the backward runs much longer
-//      than the others.
+// Pipeline (every data-dependent size stays on the device, so the chain needs
+// no host sync and is hipGraph-capturable):
+//   1. stable LSD radix sort of (key, payload) pairs over only the key bits in
+//      use (rocPRIM onesweep).  The payload is the occurrence index, or -- when
+//      the caller needs neither the inverse map nor per-occurrence values --
+//      directly the example index, which saves the gather in step 3;
+//   2. ONE inclusive scan of a packed 64-bit flag per sorted position:
+//      high word = "segment head" (key differs from its left neighbour), low
+//      word = "chunk start" (head, or position % CH == 0).  The flags are
+//      computed on the fly by a transform iterator (no flag array);
+//   3. one emit kernel: unique keys, segment starts, first chunk of each
+//      segment, chunk starts and chunk->segment map, U and #chunks, plus the
+//      optional inverse map and per-sorted-occurrence example index / value.
+// Chunks cut every segment at CH-aligned sorted positions, so no chunk is
+// longer than CH and a hot id (tens of thousands of occurrences in Criteo's
+// low-cardinality fields) is spread over many lane groups in the backward.
 #include "fm_common.h"
 #include <rocprim/rocprim.hpp>
 
 namespace fm {
 
-__global__ __launch_bounds__(kBlock) void mark_heads_kernel(const uint32_t* keys, int n, int* heads) {
-  for (int j = blockIdx.x * kBlock + threadIdx.x; j < n; j += gridDim.x * kBlock)
-    heads[j] = (j == 0 || keys[j] != keys[j - 1]) ? 1 : 0;
-}
+struct FlagOp {
+  const uint32_t* skeys;
+  int CH;
+  __device__ __host__ unsigned long long operator()(int j) const {
+    const bool head = (j == 0) || (skeys[j] != skeys[j - 1]);
+    const bool cstart = head || (j % CH == 0);
+    return ((unsigned long long)(head ? 1u : 0u) << 32) | (cstart ? 1ull : 0ull);
+  }
+};
 
 struct EmitArgs {
-  int n;
-  const uint32_t* skeys;   // sorted keys
-  const int* perm;         // sorted occurrence index
-  const int* incl;         // inclusive scan of heads
-  uint32_t* uniq;          // [n] unique keys (first U valid)
-  int* seg_start;          // [n+1]
-  int* num_unique;         // device scalar
-  int* inv;                // [n] occurrence -> segment (nullable)
-  const int* ex_of_occ;    // [n] example of occurrence (nullable)
-  int* sorted_ex;          // [n] (nullable)
-  const float* vals;       // [n] (nullable)
-  float* sorted_x;         // [n] (nullable)
+  int n, CH;
+  const uint32_t* skeys;          // sorted keys
+  const int* spay;                // sorted payload (occurrence or example index)
+  const unsigned long long* incl; // inclusive scan of packed flags
+  uint32_t* uniq;                 // [n] unique keys (first U valid)
+  int* seg_start;                 // [n+1]
+  int* seg_chunk;                 // [n+1] first chunk of each segment
+  int* chunk_start;               // [n+1]
+  int* chunk_seg;                 // [n]
+  int* counts;                    // device [2]: U, #chunks
+  int* inv;                       // [n] occurrence -> segment (payload = occurrence)
+  const int* ex_of_occ;           // [n] (payload = occurrence)
+  int* sorted_ex;                 // [n] (payload = occurrence)
+  const float* vals;              // [n] (payload = occurrence)
+  float* sorted_x;                // [n] (payload = occurrence)
 };
 
 __global__ __launch_bounds__(kBlock) void rle_emit_kernel(EmitArgs a) {
   for (int j = blockIdx.x * kBlock + threadIdx.x; j < a.n; j += gridDim.x * kBlock) {
-    const int s = a.incl[j] - 1;
-    const bool head = (j == 0) || (a.incl[j - 1] != a.incl[j]);
+    const unsigned long long v = a.incl[j];
+    const unsigned long long vp = j > 0 ? a.incl[j - 1] : 0ull;
+    const int s = (int)(v >> 32) - 1;
+    const int c = (int)(v & 0xffffffffull) - 1;
+    const bool head = (v >> 32) != (vp >> 32);
+    const bool cstart = (v & 0xffffffffull) != (vp & 0xffffffffull);
     if (head) {
       a.uniq[s] = a.skeys[j];
       a.seg_start[s] = j;
+      a.seg_chunk[s] = c;
+    }
+    if (cstart) {
+      a.chunk_start[c] = j;
+      a.chunk_seg[c] = s;
     }
     if (j == a.n - 1) {
-      *a.num_unique = s + 1;
+      a.counts[0] = s + 1;
+      a.counts[1] = c + 1;
       a.seg_start[s + 1] = a.n;
+      a.seg_chunk[s + 1] = c + 1;
+      a.chunk_start[c + 1] = a.n;
     }
-    const int p = a.perm[j];
-    if (a.inv) a.inv[p] = s;
-    if (a.sorted_ex) a.sorted_ex[j] = a.ex_of_occ[p];
-    if (a.sorted_x) a.sorted_x[j] = a.vals[p];
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void chunk_count_kernel(int n, const int* num_unique, const int* seg_start,
-                                                             int CH, int* counts) {
-  const int U = *num_unique;
-  for (int u = blockIdx.x * kBlock + threadIdx.x; u < n; u += gridDim.x * kBlock) {
-    int c = 0;
-    if (u < U) {
-      const int len = seg_start[u + 1] - seg_start[u];
-      c = len > CH ? (len + CH - 1) / CH : 1;
+    if (a.inv || a.sorted_ex || a.sorted_x) {
+      const int p = a.spay[j];
+      if (a.inv) a.inv[p] = s;
+      if (a.sorted_ex) a.sorted_ex[j] = a.ex_of_occ[p];
+      if (a.sorted_x) a.sorted_x[j] = a.vals[p];
     }
-    counts[u] = c;
   }
-}
-
-__global__ __launch_bounds__(kBlock) void chunk_emit_kernel(int n, const int* num_unique, const int* chunk_start,
-                                                            int* chunk_seg, int* num_chunks) {
-  const int U = *num_unique;
-  for (int u = blockIdx.x * kBlock + threadIdx.x; u < U; u += gridDim.x * kBlock) {
-    const int c0 = chunk_start[u], c1 = chunk_start[u + 1];
-    for (int c = c0; c < c1; ++c) chunk_seg[c] = u;
-    if (u == U - 1) *num_chunks = c1;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0 && U == 0) *num_chunks = 0;
 }
 
 static int grid_for(long long n) {
@@ -90,87 +93,70 @@ static int grid_for(long long n) {
 
 static size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
-// Workspace layout: [rocprim temp | int heads/incl(n) | int counts(n)]
-size_t dedup_workspace_bytes(int n) {
-  if (n <= 0) return 256;
+using FlagIter = rocprim::transform_iterator<rocprim::counting_iterator<int>, FlagOp, unsigned long long>;
+
+static size_t temp_bytes(int n, hipStream_t st) {
   size_t sort_bytes = 0, scan_bytes = 0;
   (void)rocprim::radix_sort_pairs((void*)nullptr, sort_bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                            (const int*)nullptr, (int*)nullptr, n, 0, 32, 0);
-  (void)rocprim::inclusive_scan((void*)nullptr, scan_bytes, (const int*)nullptr, (int*)nullptr, (size_t)n,
-                          rocprim::plus<int>(), 0);
-  const size_t tmp = align_up(sort_bytes > scan_bytes ? sort_bytes : scan_bytes);
-  return tmp + 2 * align_up(sizeof(int) * (size_t)n) + align_up(sizeof(int) * ((size_t)n + 1)) + 256;
+                                  (const int*)nullptr, (int*)nullptr, n, 0, 32, st);
+  FlagIter it(rocprim::counting_iterator<int>(0), FlagOp{nullptr, 1});
+  (void)rocprim::inclusive_scan((void*)nullptr, scan_bytes, it, (unsigned long long*)nullptr, (size_t)n,
+                                rocprim::plus<unsigned long long>(), st);
+  return align_up(sort_bytes > scan_bytes ? sort_bytes : scan_bytes);
+}
+
+// Workspace layout: [rocprim temp | u64 incl(n)]
+size_t dedup_workspace_bytes(int n) {
+  if (n <= 0) return 256;
+  return temp_bytes(n, 0) + align_up(sizeof(unsigned long long) * (size_t)n) + 256;
 }
 
 struct DedupArgs {
   int n;
   int end_bit;             // number of key bits to sort on
+  int CH;                  // chunk length of the backward plan
   const uint32_t* keys;    // [n]
-  const int* iota;         // [n] 0..n-1 (values to sort)
+  const int* payload;      // [n] values carried by the sort
   uint32_t* skeys;         // [n]
-  int* perm;               // [n]
+  int* spay;               // [n] sorted payload ("perm")
   uint32_t* uniq;          // [n]
   int* seg_start;          // [n+1]
-  int* num_unique;         // device scalar
+  int* seg_chunk;          // [n+1]
+  int* chunk_start;        // [n+1]
+  int* chunk_seg;          // [n]
+  int* counts;             // device [2]
   int* inv;                // nullable
   const int* ex_of_occ;    // nullable
   int* sorted_ex;          // nullable
   const float* vals;       // nullable
   float* sorted_x;         // nullable
-  void* ws;                // workspace (dedup_workspace_bytes)
+  void* ws;
   size_t ws_bytes;
 };
 
 int launch_dedup(const DedupArgs& a, hipStream_t st) {
   if (a.n <= 0) {
-    (void)hipMemsetAsync(a.num_unique, 0, sizeof(int), st);
+    (void)hipMemsetAsync(a.counts, 0, 2 * sizeof(int), st);
     (void)hipMemsetAsync(a.seg_start, 0, sizeof(int), st);
+    (void)hipMemsetAsync(a.seg_chunk, 0, sizeof(int), st);
+    (void)hipMemsetAsync(a.chunk_start, 0, sizeof(int), st);
     return (int)hipGetLastError();
   }
-  size_t sort_bytes = 0, scan_bytes = 0;
-  (void)rocprim::radix_sort_pairs((void*)nullptr, sort_bytes, a.keys, a.skeys, a.iota, a.perm, a.n, 0, a.end_bit, st);
-  (void)rocprim::inclusive_scan((void*)nullptr, scan_bytes, (const int*)nullptr, (int*)nullptr, (size_t)a.n,
-                          rocprim::plus<int>(), st);
-  const size_t tmp = align_up(sort_bytes > scan_bytes ? sort_bytes : scan_bytes);
-  char* base = static_cast<char*>(a.ws);
-  int* heads = reinterpret_cast<int*>(base + tmp);
-  int* incl = reinterpret_cast<int*>(base + tmp + align_up(sizeof(int) * (size_t)a.n));
-  if (tmp + 2 * align_up(sizeof(int) * (size_t)a.n) > a.ws_bytes) return -2;
+  const size_t tmp = temp_bytes(a.n, st);
+  auto* incl = reinterpret_cast<unsigned long long*>(static_cast<char*>(a.ws) + tmp);
+  if (tmp + sizeof(unsigned long long) * (size_t)a.n > a.ws_bytes) return -2;
 
-  hipError_t e = rocprim::radix_sort_pairs(a.ws, sort_bytes, a.keys, a.skeys, a.iota, a.perm, a.n, 0,
+  size_t sort_bytes = tmp;
+  hipError_t e = rocprim::radix_sort_pairs(a.ws, sort_bytes, a.keys, a.skeys, a.payload, a.spay, a.n, 0,
                                            a.end_bit, st);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(mark_heads_kernel, dim3(grid_for(a.n)), dim3(kBlock), 0, st, a.skeys, a.n, heads);
-  e = rocprim::inclusive_scan(a.ws, scan_bytes, heads, incl, (size_t)a.n, rocprim::plus<int>(), st);
+  FlagIter it(rocprim::counting_iterator<int>(0), FlagOp{a.skeys, a.CH});
+  size_t scan_bytes = tmp;
+  e = rocprim::inclusive_scan(a.ws, scan_bytes, it, incl, (size_t)a.n, rocprim::plus<unsigned long long>(), st);
   if (e != hipSuccess) return (int)e;
-  EmitArgs em{a.n, a.skeys, a.perm, incl, a.uniq, a.seg_start, a.num_unique, a.inv,
-              a.ex_of_occ, a.sorted_ex, a.vals, a.sorted_x};
+  EmitArgs em{a.n, a.CH, a.skeys, a.spay, incl, a.uniq, a.seg_start, a.seg_chunk, a.chunk_start, a.chunk_seg,
+              a.counts, a.inv, a.ex_of_occ, a.sorted_ex, a.vals, a.sorted_x};
   hipLaunchKernelGGL(rle_emit_kernel, dim3(grid_for(a.n)), dim3(kBlock), 0, st, em);
-  return (int)hipGetLastError();
-}
-
-// chunk_start must hold n+1 ints; chunk_seg n ints.
-int launch_chunk_plan(int n, const int* num_unique, const int* seg_start, int CH, int* chunk_start,
-                      int* chunk_seg, int* num_chunks, void* ws, size_t ws_bytes, hipStream_t st) {
-  if (n <= 0) {
-    (void)hipMemsetAsync(num_chunks, 0, sizeof(int), st);
-    (void)hipMemsetAsync(chunk_start, 0, sizeof(int), st);
-    return (int)hipGetLastError();
-  }
-  size_t scan_bytes = 0;
-  (void)rocprim::inclusive_scan((void*)nullptr, scan_bytes, (const int*)nullptr, (int*)nullptr, (size_t)n,
-                          rocprim::plus<int>(), st);
-  const size_t tmp = align_up(scan_bytes);
-  int* counts = reinterpret_cast<int*>(static_cast<char*>(ws) + tmp);
-  if (tmp + align_up(sizeof(int) * (size_t)n) > ws_bytes) return -2;
-  hipLaunchKernelGGL(chunk_count_kernel, dim3(grid_for(n)), dim3(kBlock), 0, st, n, num_unique, seg_start, CH,
-                     counts);
-  (void)hipMemsetAsync(chunk_start, 0, sizeof(int), st);
-  hipError_t e = rocprim::inclusive_scan(ws, scan_bytes, counts, chunk_start + 1, (size_t)n,
-                                         rocprim::plus<int>(), st);
-  if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(chunk_emit_kernel, dim3(grid_for(n)), dim3(kBlock), 0, st, n, num_unique, chunk_start,
-                     chunk_seg, num_chunks);
   return (int)hipGetLastError();
 }
 

@@ -1,0 +1,332 @@
+// Fused FM backward + sparse optimizer step on gfx950.
+//
+// Parity: reference FmGrad (cc/fm_grad_op.h:23-163: FactorSum recompute,
+// zero-fill, ~168M fp32 atomicAdd scatter per sample-cfg step) followed by TF's
+// SparseApplyAdagrad on the parameter servers (tffm/fm_model.py:341-348).
+//
+// Per unique table row u with sorted occurrences (example i, value x):
+//   g_v = sum c * r1_i - v * sum c*x + reg_v * n_u * v,   c = dpred_i * x
+//   g_w = sum c                      + reg_w * n_u * w
+// (d pred / d v = x (r1 - x v), d pred / d w = x; the per-occurrence L2 term of
+// reg_score, cc/fm_grad_op.h:88-103, contributes lambda * reg_grad * param per
+// occurrence).
+//
+// Work decomposition (no float atomics, bitwise run-to-run deterministic):
+//  * dedup.hip cut the sorted occurrence array into chunks of <= CH that never
+//    straddle two rows; one lane group (LPR lanes, 16 B each) reduces a chunk
+//    in registers, after prefetching the chunk's (example, dpred*x) pairs
+//    lane-parallel and broadcasting them with ds_bpermute;
+//  * a row that fits in one chunk (the vast majority) applies the optimizer at
+//    once; otherwise the chunk writes a partial row;
+//  * rows split over <= kSmallChunks chunks are combined by one lane group
+//    (ordered sum), hotter rows (Criteo's 3-value fields: ~40k occurrences per
+//    row at B=128k) are queued to a second kernel where a whole workgroup sums
+//    the partials in a fixed interleaved order and reduces through LDS.
+#include "fm_common.h"
+
+namespace fm {
+
+enum BwdMode : int { kBwdLocal = 0, kBwdEmit = 1 };
+constexpr int kMaxCH = 32;        // chunk length cap (prefetch registers)
+constexpr int kSmallChunks = 16;  // rows with more chunks go to the workgroup combine
+
+struct BwdArgs {
+  int mode;                 // BwdMode
+  const int* counts;        // device [2]: U, #chunks
+  const int* chunk_start;   // [#chunks+1] into the sorted occurrence arrays
+  const int* chunk_seg;     // [#chunks] -> segment (row) id
+  const int* seg_start;     // [U+1]
+  const int* seg_chunk;     // [U+1] first chunk of each segment
+  const int* uniq;          // [U] table row of each segment (LOCAL)
+  const int* sorted_ex;     // [nnz] example index of each sorted occurrence
+  const float* sorted_x;    // [nnz] value of each sorted occurrence or nullptr (=1)
+  const float* dpred;       // [B]
+  const float* r1;          // [B, Kp]
+  int Kp;
+  void* v;                  // LOCAL: table (read/write); EMIT: gathered rows (read)
+  long long v_stride;
+  float* w;
+  long long w_stride;
+  float* s0v;               // optimizer state, same row layout as v (fp32)
+  float* s1v;
+  long long s_stride;
+  float* s0w;
+  float* s1w;
+  float reg_v, reg_w;       // lambda_f * reg_grad, lambda_b * reg_grad
+  OptParams opt;
+  float* grad_out;          // EMIT: [U, g_stride], w-grad at column Kp
+  long long g_stride;
+  float* partial;           // [#chunks, Kp + 4]
+  int* big_list;            // [U] rows for the workgroup combine
+  int* big_count;           // device scalar, zeroed by the launcher
+};
+
+template <typename TV, int EPL>
+__device__ inline void bwd_finalize(const BwdArgs& a, int u, int t, bool tact, int tE,
+                                    const float (&A)[EPL], float Scx, float Sc, int n_u) {
+  using F = Frag<TV>;
+  const long long row = (a.mode == kBwdLocal) ? (long long)a.uniq[u] : (long long)u;
+  TV* vrow = reinterpret_cast<TV*>(a.v) + row * a.v_stride + tE * EPL;
+  float vv[EPL];
+  F::load(vrow, vv);
+  float* wp = a.w + row * a.w_stride;
+  const float wv = *wp;
+  const float nreg_v = a.reg_v * (float)n_u, nreg_w = a.reg_w * (float)n_u;
+  float gr[EPL];
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) gr[k] = A[k] - Scx * vv[k] + nreg_v * vv[k];
+  const float gw = Sc + nreg_w * wv;
+  if (a.mode == kBwdEmit) {
+    float* dst = a.grad_out + (long long)u * a.g_stride;
+    if (tact) {
+#pragma unroll
+      for (int k = 0; k < EPL; k += 4)
+        *reinterpret_cast<float4*>(dst + t * EPL + k) = make_float4(gr[k], gr[k + 1], gr[k + 2], gr[k + 3]);
+    }
+    if (t == 0) dst[a.Kp] = gw;
+    return;
+  }
+  float* s0 = a.s0v + row * a.s_stride + tE * EPL;
+  float* s1 = a.s1v ? a.s1v + row * a.s_stride + tE * EPL : nullptr;
+  float st0[EPL], st1[EPL];
+#pragma unroll
+  for (int k = 0; k < EPL; k += 4) {
+    const float4 q = *reinterpret_cast<const float4*>(s0 + k);
+    st0[k] = q.x; st0[k + 1] = q.y; st0[k + 2] = q.z; st0[k + 3] = q.w;
+    if (s1) {
+      const float4 z = *reinterpret_cast<const float4*>(s1 + k);
+      st1[k] = z.x; st1[k + 1] = z.y; st1[k + 2] = z.z; st1[k + 3] = z.w;
+    } else {
+      st1[k] = st1[k + 1] = st1[k + 2] = st1[k + 3] = 0.f;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) opt_step(a.opt, gr[k], vv[k], st0[k], st1[k]);
+  if (tact) {
+    F::store(vrow, vv);
+#pragma unroll
+    for (int k = 0; k < EPL; k += 4) {
+      *reinterpret_cast<float4*>(s0 + k) = make_float4(st0[k], st0[k + 1], st0[k + 2], st0[k + 3]);
+      if (s1) *reinterpret_cast<float4*>(s1 + k) = make_float4(st1[k], st1[k + 1], st1[k + 2], st1[k + 3]);
+    }
+  }
+  if (t == 0) {
+    float p = wv, q0 = a.s0w[row], q1 = a.s1w ? a.s1w[row] : 0.f;
+    opt_step(a.opt, gw, p, q0, q1);
+    *wp = p;
+    a.s0w[row] = q0;
+    if (a.s1w) a.s1w[row] = q1;
+  }
+}
+
+// One lane group per chunk of <= CH (<= kMaxCH) sorted occurrences of one row.
+template <int LPR, typename TV>
+__global__ __launch_bounds__(kBlock) void fm_bwd_chunk_kernel(BwdArgs a) {
+  constexpr int EPL = Frag<TV>::N;  // elements per lane of the table dtype
+  constexpr int G = kWave / LPR;
+  constexpr int PF = (kMaxCH + LPR - 1) / LPR;  // prefetched occurrences per lane
+  constexpr int UNR = LPR < 8 ? LPR : 8;         // r1 rows in flight per lane
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPR, t = lane % LPR;
+  const int gbase = g * LPR;
+  const int nv = a.Kp / EPL;
+  const bool tact = t < nv;
+  const int tE = tact ? t : nv - 1;
+  const int nchunks = a.counts[1];
+  const int ngroups = gridDim.x * kWavesPerBlock * G;
+  const int wave_group0 = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G;
+  for (int cbase = wave_group0; cbase < nchunks; cbase += ngroups) {
+    const int c = cbase + g;
+    if (c >= nchunks) continue;
+    const int u = a.chunk_seg[c];
+    const int j0 = a.chunk_start[c], j1 = a.chunk_start[c + 1];
+    const int len = j1 - j0;
+    // lane-parallel prefetch of the chunk's (example, dpred*x, x)
+    int pex[PF];
+    float pc[PF], px[PF];
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int jj = j0 + q * LPR + t;
+      const bool ok = jj < j1;
+      const int jc = ok ? jj : j0;
+      const int ex = a.sorted_ex[jc];
+      const float x = a.sorted_x ? a.sorted_x[jc] : 1.f;
+      pex[q] = ex;
+      px[q] = x;
+      pc[q] = ok ? a.dpred[ex] * x : 0.f;
+    }
+    float A[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) A[k] = 0.f;
+    float Scx = 0.f, Sc = 0.f;
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      if (q * LPR < len) {
+        for (int l = 0; l < LPR && q * LPR + l < len; l += UNR) {
+          float rr[UNR][EPL], cc[UNR], xx[UNR];
+#pragma unroll
+          for (int uu = 0; uu < UNR; ++uu) {
+            const int li = l + uu;
+            const bool ok = li < LPR && q * LPR + li < len;
+            const int src = gbase + (ok ? li : 0);
+            // shuffles are unconditional (every lane of the group takes part); mask after
+            const int ex = __shfl(pex[q], src, kWave);
+            const float cs = __shfl(pc[q], src, kWave);
+            cc[uu] = ok ? cs : 0.f;
+            xx[uu] = __shfl(px[q], src, kWave);
+            const float* rp = a.r1 + (long long)ex * a.Kp + tE * EPL;
+#pragma unroll
+            for (int k = 0; k < EPL; k += 4) {
+              const float4 f = *reinterpret_cast<const float4*>(rp + k);
+              rr[uu][k] = f.x; rr[uu][k + 1] = f.y; rr[uu][k + 2] = f.z; rr[uu][k + 3] = f.w;
+            }
+          }
+#pragma unroll
+          for (int uu = 0; uu < UNR; ++uu) {
+#pragma unroll
+            for (int k = 0; k < EPL; ++k) A[k] += cc[uu] * rr[uu][k];
+            Scx += cc[uu] * xx[uu];
+            Sc += cc[uu];
+          }
+        }
+      }
+    }
+    const int cs0 = a.seg_chunk[u], cs1 = a.seg_chunk[u + 1];
+    if (cs1 - cs0 == 1) {
+      bwd_finalize<TV, EPL>(a, u, t, tact, tE, A, Scx, Sc, len);
+    } else {
+      float* dst = a.partial + (long long)c * (a.Kp + 4);
+      if (tact) {
+#pragma unroll
+        for (int k = 0; k < EPL; k += 4)
+          *reinterpret_cast<float4*>(dst + t * EPL + k) = make_float4(A[k], A[k + 1], A[k + 2], A[k + 3]);
+      }
+      if (t == 0) { dst[a.Kp] = Scx; dst[a.Kp + 1] = Sc; }
+    }
+  }
+}
+
+// Rows split over 2..kSmallChunks chunks: one lane group, ordered sum of the partials.
+// Hotter rows are appended to big_list for fm_bwd_big_kernel.
+template <int LPR, typename TV>
+__global__ __launch_bounds__(kBlock) void fm_bwd_combine_kernel(BwdArgs a) {
+  constexpr int EPL = Frag<TV>::N;
+  constexpr int G = kWave / LPR;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPR, t = lane % LPR;
+  const int nv = a.Kp / EPL;
+  const bool tact = t < nv;
+  const int tE = tact ? t : nv - 1;
+  const int U = a.counts[0];
+  const int ngroups = gridDim.x * kWavesPerBlock * G;
+  for (int u = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g; u < U; u += ngroups) {
+    const int c0 = a.seg_chunk[u], c1 = a.seg_chunk[u + 1];
+    const int nc = c1 - c0;
+    if (nc <= 1) continue;
+    if (nc > kSmallChunks) {
+      if (t == 0) a.big_list[atomicAdd(a.big_count, 1)] = u;
+      continue;
+    }
+    float A[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) A[k] = 0.f;
+    float Scx = 0.f, Sc = 0.f;
+    for (int c = c0; c < c1; c += 4) {
+      float pr[4][EPL], ps[4], pt[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = c + q < c1;
+        const float* src = a.partial + (long long)(ok ? c + q : c0) * (a.Kp + 4);
+#pragma unroll
+        for (int k = 0; k < EPL; k += 4) {
+          const float4 f = *reinterpret_cast<const float4*>(src + tE * EPL + k);
+          pr[q][k] = f.x; pr[q][k + 1] = f.y; pr[q][k + 2] = f.z; pr[q][k + 3] = f.w;
+        }
+        ps[q] = ok ? src[a.Kp] : 0.f;
+        pt[q] = ok ? src[a.Kp + 1] : 0.f;
+        if (!ok) {
+#pragma unroll
+          for (int k = 0; k < EPL; ++k) pr[q][k] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int k = 0; k < EPL; ++k) A[k] += pr[q][k];
+        Scx += ps[q];
+        Sc += pt[q];
+      }
+    }
+    bwd_finalize<TV, EPL>(a, u, t, tact, tE, A, Scx, Sc, a.seg_start[u + 1] - a.seg_start[u]);
+  }
+}
+
+// Hot rows: one workgroup per row. Lane group q of the workgroup sums chunks
+// c0+q, c0+q+NG, ... ; the NG group sums are reduced in LDS in group order.
+template <int LPR, typename TV>
+__global__ __launch_bounds__(kBlock) void fm_bwd_big_kernel(BwdArgs a) {
+  constexpr int EPL = Frag<TV>::N;
+  constexpr int G = kWave / LPR;
+  constexpr int NG = kWavesPerBlock * G;
+  constexpr int ROW = LPR * EPL + 4;  // LDS floats per group sum (>= Kp + 2)
+  __shared__ float lds[NG * ROW];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPR, t = lane % LPR;
+  const int grp = (threadIdx.x >> 6) * G + g;
+  const int nv = a.Kp / EPL;
+  const bool tact = t < nv;
+  const int tE = tact ? t : nv - 1;
+  const int nbig = *a.big_count;
+  for (int bi = blockIdx.x; bi < nbig; bi += gridDim.x) {
+    const int u = a.big_list[bi];
+    const int c0 = a.seg_chunk[u], c1 = a.seg_chunk[u + 1];
+    float A[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) A[k] = 0.f;
+    float Scx = 0.f, Sc = 0.f;
+    for (int c = c0 + grp; c < c1; c += NG) {
+      const float* src = a.partial + (long long)c * (a.Kp + 4);
+#pragma unroll
+      for (int k = 0; k < EPL; k += 4) {
+        const float4 f = *reinterpret_cast<const float4*>(src + tE * EPL + k);
+        A[k] += f.x; A[k + 1] += f.y; A[k + 2] += f.z; A[k + 3] += f.w;
+      }
+      Scx += src[a.Kp];
+      Sc += src[a.Kp + 1];
+    }
+    float* my = lds + grp * ROW;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) my[t * EPL + k] = A[k];
+    if (t == 0) { my[LPR * EPL] = Scx; my[LPR * EPL + 1] = Sc; }
+    __syncthreads();
+    if (grp == 0) {
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) A[k] = 0.f;
+      Scx = Sc = 0.f;
+      for (int q = 0; q < NG; ++q) {
+        const float* o = lds + q * ROW;
+#pragma unroll
+        for (int k = 0; k < EPL; ++k) A[k] += o[t * EPL + k];
+        Scx += o[LPR * EPL];
+        Sc += o[LPR * EPL + 1];
+      }
+      bwd_finalize<TV, EPL>(a, u, t, tact, tE, A, Scx, Sc, a.seg_start[u + 1] - a.seg_start[u]);
+    }
+    __syncthreads();
+  }
+}
+
+int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_unique, hipStream_t st) {
+  if (max_chunks <= 0) return 0;
+  const int lpr = lanes_per_row(a.Kp, dtype);
+  const int G = kWave / lpr;
+  (void)hipMemsetAsync(a.big_count, 0, sizeof(int), st);
+  const int g1 = fill_grid(max_chunks, kWavesPerBlock * G);
+  FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, a);
+  const int g2 = fill_grid(max_unique, kWavesPerBlock * G, 2048);
+  FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, a);
+  FM_DISPATCH(dtype, lpr, fm_bwd_big_kernel, 1024, st, a);
+  return (int)hipGetLastError();
+}
+
+}  // namespace fm

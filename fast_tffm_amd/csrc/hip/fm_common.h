@@ -117,4 +117,38 @@ __device__ inline void opt_step(const OptParams& o, float g, float& p, float& s0
   }
 }
 
+// ---- host-side launch helpers ----------------------------------------------
+inline int next_pow2(int x) { int p = 1; while (p < x) p <<= 1; return p; }
+
+inline int lanes_per_row(int Kp, int dtype) {
+  const int epl = dtype == kBF16 ? 8 : 4;
+  return next_pow2((Kp + epl - 1) / epl);
+}
+
+inline int fill_grid(long long work_groups, int groups_per_block, int cap = 8192) {
+  long long blocks = (work_groups + groups_per_block - 1) / groups_per_block;
+  if (blocks < 1) blocks = 1;
+  if (blocks > cap) blocks = cap;
+  return (int)blocks;
+}
+
+#define FM_DISPATCH_LPR(LPR_VAL, KERNEL, TV, GRID, STREAM, ARGS)                                   \
+  switch (LPR_VAL) {                                                                                \
+    case 1: hipLaunchKernelGGL((KERNEL<1, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break;  \
+    case 2: hipLaunchKernelGGL((KERNEL<2, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break;  \
+    case 4: hipLaunchKernelGGL((KERNEL<4, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break;  \
+    case 8: hipLaunchKernelGGL((KERNEL<8, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break;  \
+    case 16: hipLaunchKernelGGL((KERNEL<16, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break; \
+    case 32: hipLaunchKernelGGL((KERNEL<32, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break; \
+    case 64: hipLaunchKernelGGL((KERNEL<64, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break; \
+    default: return -1;                                                                             \
+  }
+
+#define FM_DISPATCH(DTYPE, LPR_VAL, KERNEL, GRID, STREAM, ARGS)                       \
+  if ((DTYPE) == kBF16) {                                                            \
+    FM_DISPATCH_LPR(LPR_VAL, KERNEL, __hip_bfloat16, GRID, STREAM, ARGS)             \
+  } else {                                                                           \
+    FM_DISPATCH_LPR(LPR_VAL, KERNEL, float, GRID, STREAM, ARGS)                      \
+  }
+
 }  // namespace fm

@@ -1,0 +1,184 @@
+// Fused FM forward + loss on gfx950 (see the design notes below).
+//
+// Parity: reference FmScorer (cc/fm_scorer_op.h:8-140: BiasGenerator,
+// FeatureRankGenerator, pred/reg reductions) fused with the loss ops of
+// tffm/fm_model.py:311-333.
+//
+// Design: one wave64 per example; the example's (row, value) pairs are loaded
+// once, lane-parallel, and broadcast with ds_bpermute; factor rows are fetched
+// 16 B per lane, G = 64/LPR rows per wave instruction, UNR row groups in flight
+// per lane; r1 = sum x*v is cached for the backward (the reference recomputes
+// it, G5) and the loss gradient dpred is emitted by the same kernel (T6).
+#include "fm_common.h"
+
+namespace fm {
+
+struct FwdArgs {
+  int B;
+  const int* offsets;   // [B+1] CSR offsets into rows/vals
+  const int* rows;      // [nnz] row index into the v/w sources
+  const float* vals;    // [nnz] feature values, nullptr => all 1
+  const void* v;        // factor rows (TV), v_stride elements apart
+  long long v_stride;
+  const float* w;       // linear weights, w_stride elements apart
+  long long w_stride;
+  int Kp;               // padded factor count (multiple of 16B / sizeof(TV))
+  const float* labels;  // [B] (loss only)
+  const float* weights; // [B] or nullptr => 1
+  int loss_type;        // LossType
+  float grad_scale;     // dL/dpred scale (1/B for a batch mean)
+  float* pred;          // [B]
+  float* r1;            // [B, Kp] fp32 or nullptr
+  float* dpred;         // [B] or nullptr
+  float* loss_partial;  // [gridDim.x] or nullptr
+  float* reg_partial;   // [2*gridDim.x] (sum |v|^2, sum w^2) or nullptr
+};
+
+template <int LPR, typename TV>
+__global__ __launch_bounds__(kBlock) void fm_fwd_kernel(FwdArgs a) {
+  using F = Frag<TV>;
+  constexpr int EPL = F::N;
+  constexpr int G = kWave / LPR;
+  constexpr int UNR = (16 / G) > 1 ? (16 / G) : 1;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPR, t = lane % LPR;
+  const int nv = a.Kp / EPL;
+  const bool tact = t < nv;
+  const int tE = tact ? t : nv - 1;        // clamped: loads never leave the row
+  const float tmask = tact ? 1.f : 0.f;
+  const float wmask = (t == 0) ? 1.f : 0.f;
+  const TV* vbase = reinterpret_cast<const TV*>(a.v) + tE * EPL;
+  const int wave = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int nwaves = gridDim.x * kWavesPerBlock;
+
+  float loss_acc = 0.f, regv_acc = 0.f, regw_acc = 0.f;
+  for (int i = wave; i < a.B; i += nwaves) {
+    const int s = a.offsets[i], e = a.offsets[i + 1];
+    float s1[EPL], s2[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
+    float lin = 0.f, rv = 0.f, rw = 0.f;
+    for (int base = s; base < e; base += kWave) {
+      const int m = min(kWave, e - base);
+      int my_row = 0;
+      float my_x = 0.f;
+      if (lane < m) {
+        my_row = a.rows[base + lane];
+        my_x = a.vals ? a.vals[base + lane] : 1.f;
+      }
+      for (int q = 0; q < m; q += G * UNR) {
+        float fr[UNR][EPL], fw[UNR], fx[UNR], fm[UNR];
+        // Unconditional loads (invalid slots re-read a valid row and are masked
+        // to zero): keeps all UNR loads in flight before the first use.
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          const int f = q + u * G + g;
+          const int row = __shfl(my_row, f & (kWave - 1), kWave);
+          const float x = __shfl(my_x, f & (kWave - 1), kWave);
+          fm[u] = f < m ? 1.f : 0.f;
+          fx[u] = x * fm[u];
+          F::load(vbase + (long long)row * a.v_stride, fr[u]);
+          fw[u] = a.w[(long long)row * a.w_stride];
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          const float xm = fx[u] * tmask;
+          const float rm = fm[u] * tmask;
+#pragma unroll
+          for (int k = 0; k < EPL; ++k) {
+            const float xv = xm * fr[u][k];
+            s1[k] += xv;
+            s2[k] += xv * xv;
+            rv += rm * fr[u][k] * fr[u][k];
+          }
+          lin += wmask * fx[u] * fw[u];
+          rw += wmask * fm[u] * fw[u] * fw[u];
+        }
+      }
+    }
+    float part = 0.f;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      s1[k] = across_groups_sum<LPR>(s1[k]);
+      s2[k] = across_groups_sum<LPR>(s2[k]);
+      part += s1[k] * s1[k] - s2[k];
+    }
+    part = group_sum<LPR>(part);
+    lin = group_sum<kWave>(lin);
+    const float pred = lin + 0.5f * part;
+    if (a.r1 != nullptr && g == 0 && tact) {
+      float* dst = a.r1 + (long long)i * a.Kp + t * EPL;
+#pragma unroll
+      for (int k = 0; k < EPL; k += 4)
+        *reinterpret_cast<float4*>(dst + k) = make_float4(s1[k], s1[k + 1], s1[k + 2], s1[k + 3]);
+    }
+    if (a.reg_partial != nullptr) {
+      rv = group_sum<kWave>(rv);
+      rw = group_sum<kWave>(rw);
+      regv_acc += rv;
+      regw_acc += rw;
+    }
+    if (lane == 0) {
+      a.pred[i] = pred;
+      if (a.loss_type != kLossNone) {
+        const float y = a.labels[i];
+        const float wt = a.weights ? a.weights[i] : 1.f;
+        float l, d;
+        if (a.loss_type == kLossMse) {
+          const float diff = pred - y;
+          l = wt * diff * diff;
+          d = 2.f * wt * diff;
+        } else {
+          // sigmoid_cross_entropy_with_logits, numerically stable form
+          l = wt * (fmaxf(pred, 0.f) - pred * y + softplus_neg_abs(pred));
+          d = wt * (sigmoidf(pred) - y);
+        }
+        loss_acc += l;
+        if (a.dpred) a.dpred[i] = d * a.grad_scale;
+      }
+    }
+  }
+  if (a.loss_partial == nullptr && a.reg_partial == nullptr) return;
+  __shared__ float red[3][kWavesPerBlock];
+  const int wv = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wv] = loss_acc;
+    red[1][wv] = regv_acc;
+    red[2][wv] = regw_acc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float l = 0.f, r0 = 0.f, r1v = 0.f;
+    for (int k = 0; k < kWavesPerBlock; ++k) { l += red[0][k]; r0 += red[1][k]; r1v += red[2][k]; }
+    if (a.loss_partial) a.loss_partial[blockIdx.x] = l;
+    if (a.reg_partial) { a.reg_partial[2 * blockIdx.x] = r0; a.reg_partial[2 * blockIdx.x + 1] = r1v; }
+  }
+}
+
+// Expand CSR offsets into the example index of every occurrence.
+__global__ __launch_bounds__(kBlock) void csr_rows_kernel(int B, const int* offsets, int* ex_of_occ) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int nwaves = gridDim.x * kWavesPerBlock;
+  for (int i = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); i < B; i += nwaves) {
+    const int s = offsets[i], e = offsets[i + 1];
+    for (int j = s + lane; j < e; j += kWave) ex_of_occ[j] = i;
+  }
+}
+
+int fwd_grid(int B) { return fill_grid(B, kWavesPerBlock, 4096); }
+
+int launch_fwd(const FwdArgs& a, int dtype, int grid, hipStream_t st) {
+  if (a.B <= 0) return 0;
+  const int lpr = lanes_per_row(a.Kp, dtype);
+  FM_DISPATCH(dtype, lpr, fm_fwd_kernel, grid, st, a);
+  return (int)hipGetLastError();
+}
+
+int launch_csr_rows(int B, const int* offsets, int* ex_of_occ, hipStream_t st) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(csr_rows_kernel, dim3(fill_grid(B, kWavesPerBlock, 4096)), dim3(kBlock), 0, st, B,
+                     offsets, ex_of_occ);
+  return (int)hipGetLastError();
+}
+
+}  // namespace fm

@@ -1,0 +1,53 @@
+#include "fm_common.h"
+#include "../hash64.h"
+
+namespace fm {
+
+// ---------------------------------------------------------------------------
+// Table init (reference fm_model.py:278-281: U(-r, r) over all K+1 columns).
+// Counter-based: the value of (global id g, reference column c) depends only on
+// (seed, g, c), so a table sharded over any world size -- or restored into
+// another layout -- starts from bit-identical parameters.
+// ---------------------------------------------------------------------------
+__device__ inline float init_uniform(unsigned long long seed, long long gid, int col, float range) {
+  const unsigned long long h = mix64(seed ^ mix64((unsigned long long)gid * 0x100000001b3ull + (unsigned long long)col));
+  const float u = (float)(h >> 40) * (1.0f / 16777216.0f);  // [0, 1)
+  return range * (2.f * u - 1.f);
+}
+
+struct InitArgs {
+  void* v; long long v_stride; float* w; long long w_stride;
+  long long rows; int K, Kp, dtype;
+  long long gid_mul, gid_add;    // global id of local row r = r * gid_mul + gid_add
+  unsigned long long seed; float range;
+};
+
+__global__ __launch_bounds__(kBlock) void init_rows_kernel(InitArgs a) {
+  const long long total = a.rows * (long long)(a.Kp + 1);
+  for (long long e = (long long)blockIdx.x * kBlock + threadIdx.x; e < total; e += (long long)gridDim.x * kBlock) {
+    const long long r = e / (a.Kp + 1);
+    const int c = (int)(e - r * (a.Kp + 1));
+    const long long gid = r * a.gid_mul + a.gid_add;
+    if (c < a.Kp) {
+      const float val = c < a.K ? init_uniform(a.seed, gid, c + 1, a.range) : 0.f;
+      if (a.dtype == kBF16)
+        reinterpret_cast<uint16_t*>(a.v)[r * a.v_stride + c] = (uint16_t)f32_to_bf16_bits(val);
+      else
+        reinterpret_cast<float*>(a.v)[r * a.v_stride + c] = val;
+    } else {
+      a.w[r * a.w_stride] = init_uniform(a.seed, gid, 0, a.range);
+    }
+  }
+}
+
+int launch_init_rows(const InitArgs& a, hipStream_t st) {
+  if (a.rows <= 0) return 0;
+  const long long total = a.rows * (long long)(a.Kp + 1);
+  long long blocks = (total + kBlock - 1) / kBlock;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(init_rows_kernel, dim3((int)blocks), dim3(kBlock), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+}  // namespace fm
+

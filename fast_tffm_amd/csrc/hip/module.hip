@@ -15,9 +15,12 @@
 namespace py = pybind11;
 using u64 = std::uintptr_t;
 
-// Unity build: the kernel sources are compiled in this translation unit.
-#include "fm_kernels.hip"
+// Unity build: all kernel sources are compiled in this translation unit.
+#include "fm_fwd.hip"
+#include "fm_bwd.hip"
 #include "dedup.hip"
+#include "shard.hip"
+#include "init.hip"
 
 namespace {
 
@@ -43,6 +46,7 @@ fm::OptParams opt_params(int type, float lr, float l1, float l2, float beta) {
 PYBIND11_MODULE(_fm_hip, m) {
   m.doc() = "gfx950 HIP kernels for fast_tffm_amd (FM forward/backward/optimizer, dedup, sharding)";
   m.attr("ARCH") = "gfx950";
+  m.attr("MAX_CH") = fm::kMaxCH;
 
   m.def("fwd_grid", &fm::fwd_grid, py::arg("B"));
   m.def("lanes_per_row", &fm::lanes_per_row, py::arg("Kp"), py::arg("dtype"));
@@ -69,61 +73,55 @@ PYBIND11_MODULE(_fm_hip, m) {
 
   m.def(
       "bwd",
-      [](int mode, u64 num_chunks, u64 chunk_seg, u64 chunk_start, u64 num_unique, u64 seg_start, u64 uniq,
-         u64 sorted_ex, u64 sorted_x, u64 dpred, u64 r1, int Kp, int CH, u64 v, long long v_stride, u64 w,
+      [](int mode, u64 counts, u64 chunk_start, u64 chunk_seg, u64 seg_start, u64 seg_chunk, u64 uniq,
+         u64 sorted_ex, u64 sorted_x, u64 dpred, u64 r1, int Kp, u64 v, long long v_stride, u64 w,
          long long w_stride, u64 s0v, u64 s1v, long long s_stride, u64 s0w, u64 s1w, float reg_v, float reg_w,
          int opt_type, float lr, float l1, float l2, float beta, u64 grad_out, long long g_stride, u64 partial,
-         int dtype, long long max_chunks, long long max_unique, u64 stream) {
+         u64 big_list, u64 big_count, int dtype, long long max_chunks, long long max_unique, u64 stream) {
         fm::BwdArgs a;
-        a.mode = mode; a.num_chunks = P<const int>(num_chunks); a.chunk_seg = P<const int>(chunk_seg);
-        a.chunk_start = P<const int>(chunk_start); a.num_unique = P<const int>(num_unique);
-        a.seg_start = P<const int>(seg_start); a.uniq = P<const int>(uniq);
+        a.mode = mode; a.counts = P<const int>(counts); a.chunk_start = P<const int>(chunk_start);
+        a.chunk_seg = P<const int>(chunk_seg); a.seg_start = P<const int>(seg_start);
+        a.seg_chunk = P<const int>(seg_chunk); a.uniq = P<const int>(uniq);
         a.sorted_ex = P<const int>(sorted_ex); a.sorted_x = P<const float>(sorted_x);
-        a.dpred = P<const float>(dpred); a.r1 = P<const float>(r1); a.Kp = Kp; a.CH = CH;
+        a.dpred = P<const float>(dpred); a.r1 = P<const float>(r1); a.Kp = Kp;
         a.v = P<void>(v); a.v_stride = v_stride; a.w = P<float>(w); a.w_stride = w_stride;
         a.s0v = P<float>(s0v); a.s1v = P<float>(s1v); a.s_stride = s_stride; a.s0w = P<float>(s0w);
         a.s1w = P<float>(s1w); a.reg_v = reg_v; a.reg_w = reg_w;
         a.opt = opt_params(opt_type, lr, l1, l2, beta);
         a.grad_out = P<float>(grad_out); a.g_stride = g_stride; a.partial = P<float>(partial);
+        a.big_list = P<int>(big_list); a.big_count = P<int>(big_count);
         check(fm::launch_bwd(a, dtype, max_chunks, max_unique, S(stream)), "fm_bwd");
       },
-      py::arg("mode"), py::arg("num_chunks"), py::arg("chunk_seg"), py::arg("chunk_start"), py::arg("num_unique"),
-      py::arg("seg_start"), py::arg("uniq"), py::arg("sorted_ex"), py::arg("sorted_x"), py::arg("dpred"),
-      py::arg("r1"), py::arg("Kp"), py::arg("CH"), py::arg("v"), py::arg("v_stride"), py::arg("w"),
-      py::arg("w_stride"), py::arg("s0v"), py::arg("s1v"), py::arg("s_stride"), py::arg("s0w"), py::arg("s1w"),
-      py::arg("reg_v"), py::arg("reg_w"), py::arg("opt_type"), py::arg("lr"), py::arg("l1"), py::arg("l2"),
-      py::arg("beta"), py::arg("grad_out"), py::arg("g_stride"), py::arg("partial"), py::arg("dtype"),
-      py::arg("max_chunks"), py::arg("max_unique"), py::arg("stream"));
+      py::arg("mode"), py::arg("counts"), py::arg("chunk_start"), py::arg("chunk_seg"), py::arg("seg_start"),
+      py::arg("seg_chunk"), py::arg("uniq"), py::arg("sorted_ex"), py::arg("sorted_x"), py::arg("dpred"),
+      py::arg("r1"), py::arg("Kp"), py::arg("v"), py::arg("v_stride"), py::arg("w"), py::arg("w_stride"),
+      py::arg("s0v"), py::arg("s1v"), py::arg("s_stride"), py::arg("s0w"), py::arg("s1w"), py::arg("reg_v"),
+      py::arg("reg_w"), py::arg("opt_type"), py::arg("lr"), py::arg("l1"), py::arg("l2"), py::arg("beta"),
+      py::arg("grad_out"), py::arg("g_stride"), py::arg("partial"), py::arg("big_list"), py::arg("big_count"),
+      py::arg("dtype"), py::arg("max_chunks"), py::arg("max_unique"), py::arg("stream"));
 
   m.def("dedup_workspace_bytes", &fm::dedup_workspace_bytes, py::arg("n"));
 
   m.def(
       "dedup",
-      [](int n, int end_bit, u64 keys, u64 iota, u64 skeys, u64 perm, u64 uniq, u64 seg_start, u64 num_unique,
-         u64 inv, u64 ex_of_occ, u64 sorted_ex, u64 vals, u64 sorted_x, u64 ws, size_t ws_bytes, u64 stream) {
+      [](int n, int end_bit, int CH, u64 keys, u64 payload, u64 skeys, u64 spay, u64 uniq, u64 seg_start,
+         u64 seg_chunk, u64 chunk_start, u64 chunk_seg, u64 counts, u64 inv, u64 ex_of_occ, u64 sorted_ex,
+         u64 vals, u64 sorted_x, u64 ws, size_t ws_bytes, u64 stream) {
+        if (CH < 1 || CH > fm::kMaxCH) throw std::invalid_argument("CH must be in [1, MAX_CH]");
         fm::DedupArgs a;
-        a.n = n; a.end_bit = end_bit; a.keys = P<const uint32_t>(keys); a.iota = P<const int>(iota);
-        a.skeys = P<uint32_t>(skeys); a.perm = P<int>(perm); a.uniq = P<uint32_t>(uniq);
-        a.seg_start = P<int>(seg_start); a.num_unique = P<int>(num_unique); a.inv = P<int>(inv);
-        a.ex_of_occ = P<const int>(ex_of_occ); a.sorted_ex = P<int>(sorted_ex); a.vals = P<const float>(vals);
-        a.sorted_x = P<float>(sorted_x); a.ws = P<void>(ws); a.ws_bytes = ws_bytes;
+        a.n = n; a.end_bit = end_bit; a.CH = CH; a.keys = P<const uint32_t>(keys);
+        a.payload = P<const int>(payload); a.skeys = P<uint32_t>(skeys); a.spay = P<int>(spay);
+        a.uniq = P<uint32_t>(uniq); a.seg_start = P<int>(seg_start); a.seg_chunk = P<int>(seg_chunk);
+        a.chunk_start = P<int>(chunk_start); a.chunk_seg = P<int>(chunk_seg); a.counts = P<int>(counts);
+        a.inv = P<int>(inv); a.ex_of_occ = P<const int>(ex_of_occ); a.sorted_ex = P<int>(sorted_ex);
+        a.vals = P<const float>(vals); a.sorted_x = P<float>(sorted_x); a.ws = P<void>(ws);
+        a.ws_bytes = ws_bytes;
         check(fm::launch_dedup(a, S(stream)), "dedup");
       },
-      py::arg("n"), py::arg("end_bit"), py::arg("keys"), py::arg("iota"), py::arg("skeys"), py::arg("perm"),
-      py::arg("uniq"), py::arg("seg_start"), py::arg("num_unique"), py::arg("inv"), py::arg("ex_of_occ"),
-      py::arg("sorted_ex"), py::arg("vals"), py::arg("sorted_x"), py::arg("ws"), py::arg("ws_bytes"),
-      py::arg("stream"));
-
-  m.def(
-      "chunk_plan",
-      [](int n, u64 num_unique, u64 seg_start, int CH, u64 chunk_start, u64 chunk_seg, u64 num_chunks, u64 ws,
-         size_t ws_bytes, u64 stream) {
-        check(fm::launch_chunk_plan(n, P<const int>(num_unique), P<const int>(seg_start), CH, P<int>(chunk_start),
-                                    P<int>(chunk_seg), P<int>(num_chunks), P<void>(ws), ws_bytes, S(stream)),
-              "chunk_plan");
-      },
-      py::arg("n"), py::arg("num_unique"), py::arg("seg_start"), py::arg("CH"), py::arg("chunk_start"),
-      py::arg("chunk_seg"), py::arg("num_chunks"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"));
+      py::arg("n"), py::arg("end_bit"), py::arg("CH"), py::arg("keys"), py::arg("payload"), py::arg("skeys"),
+      py::arg("spay"), py::arg("uniq"), py::arg("seg_start"), py::arg("seg_chunk"), py::arg("chunk_start"),
+      py::arg("chunk_seg"), py::arg("counts"), py::arg("inv"), py::arg("ex_of_occ"), py::arg("sorted_ex"),
+      py::arg("vals"), py::arg("sorted_x"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"));
 
   m.def(
       "gather_rows",

@@ -1,0 +1,135 @@
+// Owner-side kernels of the row-sharded exchange (parallel/exchange.py):
+// gather requested table rows into a packed [v | w | pad] send buffer, and sum
+// the gradient rows every peer returned for one table row before applying the
+// optimizer once (replaces the PS-side embedding gather and SparseApplyAdagrad
+// that the reference gets from TF's gRPC runtime, tffm/fm_model.py:291, :341-348).
+#include "fm_common.h"
+
+namespace fm {
+
+// ---------------------------------------------------------------------------
+// Row-sharded helpers
+// ---------------------------------------------------------------------------
+struct GatherArgs {
+  int R;
+  const int* req;           // [R] local table rows requested by peers
+  const void* v; long long v_stride;
+  const float* w; long long w_stride;
+  int Kp;
+  float* out; long long o_stride;   // [R, o_stride]: v at [0,Kp), w at Kp
+};
+
+template <int LPR, typename TV>
+__global__ __launch_bounds__(kBlock) void gather_rows_kernel(GatherArgs a) {
+  using F = Frag<TV>;
+  constexpr int EPL = F::N;
+  constexpr int G = kWave / LPR;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPR, t = lane % LPR;
+  const int nv = a.Kp / EPL;
+  const bool tact = t < nv;
+  const int tE = tact ? t : nv - 1;
+  const int ngroups = gridDim.x * kWavesPerBlock * G;
+  for (int p = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g; p < a.R; p += ngroups) {
+    const long long row = a.req[p];
+    float vv[EPL];
+    F::load(reinterpret_cast<const TV*>(a.v) + row * a.v_stride + tE * EPL, vv);
+    float* dst = a.out + (long long)p * a.o_stride;
+    if (tact) {
+#pragma unroll
+      for (int k = 0; k < EPL; k += 4)
+        *reinterpret_cast<float4*>(dst + t * EPL + k) = make_float4(vv[k], vv[k + 1], vv[k + 2], vv[k + 3]);
+    }
+    if (t == 0) {
+      dst[a.Kp] = a.w[row * a.w_stride];
+      dst[a.Kp + 1] = 0.f; dst[a.Kp + 2] = 0.f; dst[a.Kp + 3] = 0.f;
+    }
+  }
+}
+
+struct ApplyArgs {
+  const int* num_unique;    // device scalar: number of distinct rows received
+  const int* seg_start;     // [U+1] into perm
+  const int* uniq;          // [U] local table row
+  const int* perm;          // [R] position in grad_in of each sorted entry
+  const float* grad_in; long long g_stride;  // [R, g_stride], w-grad at column Kp
+  int Kp;
+  void* v; long long v_stride;
+  float* w; long long w_stride;
+  float* s0v; float* s1v; long long s_stride;
+  float* s0w; float* s1w;
+  OptParams opt;
+};
+
+// Owner-side: sum the gradient rows every peer sent for one table row (in
+// source-rank order: the sort is stable and the receive buffer is rank-major)
+// and apply the optimizer once.
+template <int LPR, typename TV>
+__global__ __launch_bounds__(kBlock) void apply_rows_kernel(ApplyArgs a) {
+  using F = Frag<TV>;
+  constexpr int EPL = F::N;
+  constexpr int G = kWave / LPR;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPR, t = lane % LPR;
+  const int nv = a.Kp / EPL;
+  const bool tact = t < nv;
+  const int tE = tact ? t : nv - 1;
+  const int U = *a.num_unique;
+  const int ngroups = gridDim.x * kWavesPerBlock * G;
+  for (int u = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g; u < U; u += ngroups) {
+    float gr[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) gr[k] = 0.f;
+    float gw = 0.f;
+    for (int j = a.seg_start[u]; j < a.seg_start[u + 1]; ++j) {
+      const float* src = a.grad_in + (long long)a.perm[j] * a.g_stride;
+#pragma unroll
+      for (int k = 0; k < EPL; k += 4) {
+        const float4 f = *reinterpret_cast<const float4*>(src + tE * EPL + k);
+        gr[k] += f.x; gr[k + 1] += f.y; gr[k + 2] += f.z; gr[k + 3] += f.w;
+      }
+      gw += src[a.Kp];
+    }
+    const long long row = a.uniq[u];
+    TV* vrow = reinterpret_cast<TV*>(a.v) + row * a.v_stride + tE * EPL;
+    float vv[EPL], st0[EPL], st1[EPL];
+    F::load(vrow, vv);
+    float* s0 = a.s0v + row * a.s_stride + tE * EPL;
+    float* s1 = a.s1v ? a.s1v + row * a.s_stride + tE * EPL : nullptr;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) { st0[k] = s0[k]; st1[k] = s1 ? s1[k] : 0.f; }
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) opt_step(a.opt, gr[k], vv[k], st0[k], st1[k]);
+    if (tact) {
+      F::store(vrow, vv);
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) { s0[k] = st0[k]; if (s1) s1[k] = st1[k]; }
+    }
+    if (t == 0) {
+      float* wp = a.w + row * a.w_stride;
+      float p = *wp, q0 = a.s0w[row], q1 = a.s1w ? a.s1w[row] : 0.f;
+      opt_step(a.opt, gw, p, q0, q1);
+      *wp = p;
+      a.s0w[row] = q0;
+      if (a.s1w) a.s1w[row] = q1;
+    }
+  }
+}
+
+int launch_gather_rows(const GatherArgs& a, int dtype, hipStream_t st) {
+  if (a.R <= 0) return 0;
+  const int lpr = lanes_per_row(a.Kp, dtype);
+  const int grid = fill_grid(a.R, kWavesPerBlock * (kWave / lpr));
+  FM_DISPATCH(dtype, lpr, gather_rows_kernel, grid, st, a);
+  return (int)hipGetLastError();
+}
+
+int launch_apply_rows(const ApplyArgs& a, int dtype, long long max_unique, hipStream_t st) {
+  if (max_unique <= 0) return 0;
+  const int lpr = lanes_per_row(a.Kp, dtype);
+  const int grid = fill_grid(max_unique, kWavesPerBlock * (kWave / lpr));
+  FM_DISPATCH(dtype, lpr, apply_rows_kernel, grid, st, a);
+  return (int)hipGetLastError();
+}
+
+}  // namespace fm

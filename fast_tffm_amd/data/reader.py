@@ -201,8 +201,14 @@ class Prefetcher:
                     raise self._err
                 return
             if ev is not None:
-                torch.cuda.current_stream(self.device).wait_event(ev)
-                # keep the source alive until the copy is consumed by the compute stream
+                cur = torch.cuda.current_stream(self.device)
+                cur.wait_event(ev)
+                # the batch was allocated on the side stream: tell the caching allocator
+                # it is in use on the compute stream too
+                for t in (item.labels, item.offsets, item.ids, item.vals, item.weights):
+                    if t is not None:
+                        t.record_stream(cur)
+                # keep the pinned source alive until the copy has been consumed
                 item._host_ref = _host  # type: ignore[attr-defined]
             yield item
 

@@ -76,7 +76,7 @@ class _Workspace:
             cap = max(nnz, int(self.cap_n * 1.25), 1)
             self.dd = K.DedupWorkspace(cap, dev, self.CH)
             self.rows32 = torch.empty(cap, dtype=torch.int32, device=dev)
-            self.bwd_partial = (torch.empty((cap, Kp + 4), dtype=torch.float32, device=dev)
+            self.bwd_partial = (torch.empty((K.partial_rows(cap, self.CH), Kp + 4), dtype=torch.float32, device=dev)
                                 if dev.type == "cuda" else None)
             self.cap_n = cap
         if not hasattr(self, "fwd_partial"):

@@ -194,14 +194,16 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
 # dedup
 # ---------------------------------------------------------------------------
 class DedupOut:
-    """Grouping of a batch's occurrences by key.
+    """Grouping of a batch's occurrences by key (sorted unique keys = segments).
 
-    ``num_unique`` is a 1-element int32 device tensor (no host sync);
-    ``U_host`` is set on CPU (and after ``.sync()``).
+    ``counts`` is a 2-element int32 device tensor (U, #chunks) -- no host sync;
+    ``num_unique`` is a view of counts[0]; ``U_host`` is set on CPU and after
+    ``.sync()``.  ``perm`` is the sorted payload: the occurrence index, unless
+    the dedup ran with the example index as payload (then ``sorted_ex is perm``).
     """
 
-    __slots__ = ("n", "skeys", "perm", "uniq", "seg_start", "num_unique", "inv", "sorted_ex", "sorted_x",
-                 "chunk_start", "chunk_seg", "num_chunks", "U_host", "CH")
+    __slots__ = ("n", "skeys", "perm", "uniq", "seg_start", "seg_chunk", "chunk_start", "chunk_seg", "counts",
+                 "num_unique", "inv", "sorted_ex", "sorted_x", "U_host", "CH", "big_list", "big_count")
 
     def __init__(self, **kw):
         for k in self.__slots__:
@@ -221,22 +223,25 @@ class DedupWorkspace:
 
     def __init__(self, cap: int, device: torch.device, CH: int = 32):
         self.cap, self.device, self.CH = cap, device, CH
+        n1 = max(cap, 1)
         i32 = dict(dtype=torch.int32, device=device)
-        self.iota = torch.arange(max(cap, 1), **i32)
-        self.skeys = torch.empty(max(cap, 1), **i32)
-        self.perm = torch.empty(max(cap, 1), **i32)
-        self.uniq = torch.empty(max(cap, 1), **i32)
-        self.seg_start = torch.empty(cap + 1, **i32)
-        self.num_unique = torch.zeros(1, **i32)
-        self.inv = torch.empty(max(cap, 1), **i32)
-        self.sorted_ex = torch.empty(max(cap, 1), **i32)
-        self.sorted_x = torch.empty(max(cap, 1), dtype=torch.float32, device=device)
-        self.ex_of_occ = torch.empty(max(cap, 1), **i32)
-        self.chunk_start = torch.empty(cap + 1, **i32)
-        self.chunk_seg = torch.empty(max(cap, 1), **i32)
-        self.num_chunks = torch.zeros(1, **i32)
+        self.iota = torch.arange(n1, **i32)
+        self.skeys = torch.empty(n1, **i32)
+        self.perm = torch.empty(n1, **i32)
+        self.uniq = torch.empty(n1, **i32)
+        self.seg_start = torch.empty(n1 + 1, **i32)
+        self.seg_chunk = torch.empty(n1 + 1, **i32)
+        self.chunk_start = torch.empty(n1 + 1, **i32)
+        self.chunk_seg = torch.empty(n1, **i32)
+        self.counts = torch.zeros(2, **i32)
+        self.inv = torch.empty(n1, **i32)
+        self.sorted_ex = torch.empty(n1, **i32)
+        self.sorted_x = torch.empty(n1, dtype=torch.float32, device=device)
+        self.ex_of_occ = torch.empty(n1, **i32)
+        self.big_list = torch.empty(n1, **i32)
+        self.big_count = torch.zeros(1, **i32)
         if device.type == "cuda":
-            nbytes = native.hip().dedup_workspace_bytes(max(cap, 1))
+            nbytes = native.hip().dedup_workspace_bytes(n1)
             self.ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
         else:
             self.ws = None
@@ -258,11 +263,14 @@ def csr_rows(offsets: torch.Tensor, out: torch.Tensor | None = None, nnz: int | 
 
 def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int = 32,
           ex_of_occ: torch.Tensor | None = None, vals: torch.Tensor | None = None, want_inv: bool = False,
-          want_chunks: bool = True, CH: int | None = None) -> DedupOut:
+          CH: int | None = None, want_perm: bool = False) -> DedupOut:
     """Sort-based unique over non-negative int32 keys (reference tf.unique, fm_model.py:72).
 
     Unique keys come out in ascending order (the reference's first-occurrence
-    order is an implementation detail no result depends on).
+    order is an implementation detail no result depends on).  On the GPU the
+    result also carries the backward's chunk plan.  When neither the inverse
+    map, per-occurrence values nor the occurrence permutation are needed, the
+    sort carries the example index directly (one gather pass less).
     """
     dev = keys.device
     n = keys.numel()
@@ -275,27 +283,27 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
     if vals is not None:
         _chk_vec(vals, torch.float32, n, "vals", dev)
     key_bits = max(1, min(32, int(key_bits)))
+    ex_payload = ex_of_occ is not None and vals is None and not want_inv and not want_perm and _is_gpu(keys)
     out = DedupOut(n=n, skeys=ws.skeys, perm=ws.perm, uniq=ws.uniq, seg_start=ws.seg_start,
-                   num_unique=ws.num_unique, inv=ws.inv if want_inv else None,
-                   sorted_ex=ws.sorted_ex if ex_of_occ is not None else None,
-                   sorted_x=ws.sorted_x if vals is not None else None, CH=CH)
+                   seg_chunk=ws.seg_chunk, chunk_start=ws.chunk_start, chunk_seg=ws.chunk_seg, counts=ws.counts,
+                   num_unique=ws.counts[:1], inv=ws.inv if want_inv else None,
+                   sorted_ex=(ws.perm if ex_payload else ws.sorted_ex) if ex_of_occ is not None else None,
+                   sorted_x=ws.sorted_x if vals is not None else None, CH=CH, big_list=ws.big_list,
+                   big_count=ws.big_count)
     if _is_gpu(keys):
         h = native.hip()
-        st = _stream(keys)
-        h.dedup(n=n, end_bit=key_bits, keys=_p(keys), iota=_p(ws.iota), skeys=_p(ws.skeys), perm=_p(ws.perm),
-                uniq=_p(ws.uniq), seg_start=_p(ws.seg_start), num_unique=_p(ws.num_unique), inv=_p(out.inv),
-                ex_of_occ=_p(ex_of_occ), sorted_ex=_p(out.sorted_ex), vals=_p(vals), sorted_x=_p(out.sorted_x),
-                ws=_p(ws.ws), ws_bytes=ws.ws.numel(), stream=st)
-        if want_chunks:
-            h.chunk_plan(n=n, num_unique=_p(ws.num_unique), seg_start=_p(ws.seg_start), CH=CH,
-                         chunk_start=_p(ws.chunk_start), chunk_seg=_p(ws.chunk_seg), num_chunks=_p(ws.num_chunks),
-                         ws=_p(ws.ws), ws_bytes=ws.ws.numel(), stream=st)
-            out.chunk_start, out.chunk_seg, out.num_chunks = ws.chunk_start, ws.chunk_seg, ws.num_chunks
+        _check(1 <= CH <= h.MAX_CH, f"CH must be in [1, {h.MAX_CH}]")
+        h.dedup(n=n, end_bit=key_bits, CH=CH, keys=_p(keys), payload=_p(ex_of_occ if ex_payload else ws.iota),
+                skeys=_p(ws.skeys), spay=_p(ws.perm), uniq=_p(ws.uniq), seg_start=_p(ws.seg_start),
+                seg_chunk=_p(ws.seg_chunk), chunk_start=_p(ws.chunk_start), chunk_seg=_p(ws.chunk_seg),
+                counts=_p(ws.counts), inv=_p(out.inv), ex_of_occ=0 if ex_payload else _p(ex_of_occ),
+                sorted_ex=0 if ex_payload else _p(out.sorted_ex), vals=_p(vals), sorted_x=_p(out.sorted_x),
+                ws=_p(ws.ws), ws_bytes=ws.ws.numel(), stream=_stream(keys))
     else:
         U = native.cpu().dedup(n=n, keys=_p(keys), skeys=_p(ws.skeys), perm=_p(ws.perm), uniq=_p(ws.uniq),
                                seg_start=_p(ws.seg_start), inv=_p(out.inv), ex_of_occ=_p(ex_of_occ),
                                sorted_ex=_p(out.sorted_ex), vals=_p(vals), sorted_x=_p(out.sorted_x))
-        ws.num_unique.fill_(U)
+        ws.counts[0] = U
         out.U_host = U
     return out
 
@@ -313,6 +321,11 @@ class TableState:
     s1v: torch.Tensor | None = None  # ftrl z                          [rows, Kp] fp32
     s0w: torch.Tensor | None = None  # [rows]
     s1w: torch.Tensor | None = None  # [rows]
+
+
+def partial_rows(n: int, CH: int) -> int:
+    """Upper bound on backward chunks (= partial rows) for n occurrences: U + n / CH."""
+    return max(n, 1) + max(n, 1) // max(CH, 1) + 1
 
 
 def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *, mode: int,
@@ -358,16 +371,16 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
     if _is_gpu(dpred):
         h = native.hip()
         if partial is None:
-            partial = torch.empty((max(dd.n, 1), Kp + 4), dtype=torch.float32, device=dev)
-        _check(partial.numel() >= max(dd.n, 1) * (Kp + 4), "partial scratch too small")
-        h.bwd(mode=mode, num_chunks=_p(dd.num_chunks), chunk_seg=_p(dd.chunk_seg), chunk_start=_p(dd.chunk_start),
-              num_unique=_p(dd.num_unique), seg_start=_p(dd.seg_start), uniq=_p(dd.uniq),
-              sorted_ex=_p(dd.sorted_ex), sorted_x=_p(dd.sorted_x), dpred=_p(dpred), r1=_p(r1), Kp=Kp, CH=dd.CH,
+            partial = torch.empty((partial_rows(dd.n, dd.CH), Kp + 4), dtype=torch.float32, device=dev)
+        _check(partial.numel() >= partial_rows(dd.n, dd.CH) * (Kp + 4), "partial scratch too small")
+        h.bwd(mode=mode, counts=_p(dd.counts), chunk_start=_p(dd.chunk_start), chunk_seg=_p(dd.chunk_seg),
+              seg_start=_p(dd.seg_start), seg_chunk=_p(dd.seg_chunk), uniq=_p(dd.uniq),
+              sorted_ex=_p(dd.sorted_ex), sorted_x=_p(dd.sorted_x), dpred=_p(dpred), r1=_p(r1), Kp=Kp,
               v=_p(v), v_stride=v_stride, w=_p(w), w_stride=w.stride(0), s0v=_p(s0v), s1v=_p(s1v),
               s_stride=s_stride, s0w=_p(s0w), s1w=_p(s1w), reg_v=float(reg_v), reg_w=float(reg_w),
               opt_type=o.code, lr=float(o.lr), l1=float(o.l1), l2=float(o.l2), beta=float(o.beta),
-              grad_out=gptr, g_stride=gstride, partial=_p(partial), dtype=dt, max_chunks=dd.n,
-              max_unique=dd.n, stream=_stream(dpred))
+              grad_out=gptr, g_stride=gstride, partial=_p(partial), big_list=_p(dd.big_list),
+              big_count=_p(dd.big_count), dtype=dt, max_chunks=dd.n, max_unique=dd.n, stream=_stream(dpred))
     else:
         U = dd.sync()
         native.cpu().bwd(mode=mode, U=U, seg_start=_p(dd.seg_start), uniq=_p(dd.uniq), sorted_ex=_p(dd.sorted_ex),

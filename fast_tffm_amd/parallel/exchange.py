@@ -86,7 +86,7 @@ class ShardExchange(_Base):
         ws = self.m.ws
         keys = self._keys(b)
         dd = K.dedup(keys, ws=ws.dd, key_bits=self.key_bits, ex_of_occ=ex, vals=b.vals if ex is not None else None,
-                     want_inv=True, want_chunks=ex is not None)
+                     want_inv=True)
         U = dd.sync()
         uniq = dd.uniq[:U].to(torch.int64)
         owner = torch.div(uniq, self.Rps, rounding_mode="floor")
@@ -124,7 +124,7 @@ class ShardExchange(_Base):
         R = req_recv.numel()
         grad_recv = torch.empty((R, self.gs), dtype=torch.float32, device=self.dev)
         _a2a(grad_recv, grad, rc, sc, self.group)
-        dd2 = K.dedup(req_recv, ws=self._dd2(R), key_bits=bits_for(self.Rps), want_chunks=False)
+        dd2 = K.dedup(req_recv, ws=self._dd2(R), key_bits=bits_for(self.Rps), want_perm=True)
         K.apply_rows(dd2, grad_recv, m.table.state, cfg.opt, Kp, threads=cfg.threads)
         return StepOut(fo.loss_sum, b.B)
 
@@ -179,7 +179,7 @@ class DPExchange(_Base):
         ids_cat = torch.cat([ids_all[r][: sizes[r]] for r in range(self.W)])
         g_cat = torch.cat([g_all[r][: sizes[r]] for r in range(self.W)])
         n = ids_cat.numel()
-        dd2 = K.dedup(ids_cat, ws=self._dd2(n), key_bits=bits_for(self.m.table.rows), want_chunks=False)
+        dd2 = K.dedup(ids_cat, ws=self._dd2(n), key_bits=bits_for(self.m.table.rows), want_perm=True)
         K.apply_rows(dd2, g_cat, self.m.table.state, self.m.cfg.opt, self.Kp, threads=self.m.cfg.threads)
         return StepOut(fo.loss_sum, b.B)
 

@@ -1,0 +1,252 @@
+"""Checkpoint / resume, and conversion to the reference's table layout.
+
+Reference: ``tf.train.Saver`` bundles in ``log_dir`` written by
+``CheckpointSaverHook(save_steps)`` (run_tffm.py:213-216); variables
+``vocab_block_{i}`` ``[V // N + 1, K + 1]`` (column 0 = w), their Adagrad slots
+and ``global_step``; ``MonitoredTrainingSession`` restores the latest
+checkpoint automatically; ``generate`` uses ``get_checkpoint_state(log_dir)``.
+
+Layout here (one directory per step, one file per table shard)::
+
+    log_dir/checkpoint                         TF-style index: model_checkpoint_path: "model.ckpt-<step>"
+    log_dir/model.ckpt-<step>/meta.json        step, shapes, optimizer, world, reader position
+    log_dir/model.ckpt-<step>/shard-RRRRR-of-WWWWW.safetensors
+        w [rows] fp32, v [rows, K] (table dtype), s0w/s0v (Adagrad acc / FTRL n),
+        s1w/s1v (FTRL z); local row r of shard s holds global id r * W + s.
+
+Every rank writes only its own shard (replicated modes: rank 0 writes the
+single table); rank 0 writes meta.json and the index after a barrier, so the
+index never points at a partial checkpoint.  Restore re-shards on the fly when
+the world size changed.  ``export_reference_blocks``/``import_reference_blocks``
+convert to/from ``vocab_block_{i}`` arrays in the reference's mod layout.
+"""
+
+from __future__ import annotations
+
+import glob
+import json
+import os
+import re
+import shutil
+
+import numpy as np
+import torch
+from safetensors.torch import load_file, save_file
+
+FORMAT = "fast_tffm_amd/ckpt-v1"
+INDEX = "checkpoint"
+
+
+def _shard_name(rank: int, world: int) -> str:
+    return f"shard-{rank:05d}-of-{world:05d}.safetensors"
+
+
+def latest_checkpoint(log_dir: str | None) -> str | None:
+    """Path of the newest complete checkpoint directory in ``log_dir`` (or None)."""
+    if not log_dir or not os.path.isdir(log_dir):
+        return None
+    idx = os.path.join(log_dir, INDEX)
+    if os.path.exists(idx):
+        with open(idx) as f:
+            for line in f:
+                m = re.match(r'model_checkpoint_path:\s*"(.*)"', line.strip())
+                if m:
+                    p = m.group(1)
+                    p = p if os.path.isabs(p) else os.path.join(log_dir, p)
+                    if os.path.exists(os.path.join(p, "meta.json")):
+                        return p
+    cands = sorted(glob.glob(os.path.join(log_dir, "model.ckpt-*", "meta.json")),
+                   key=lambda p: int(re.search(r"model\.ckpt-(\d+)", p).group(1)))
+    return os.path.dirname(cands[-1]) if cands else None
+
+
+def _table_tensors(table) -> dict[str, torch.Tensor]:
+    K = table.K
+    t = {"w": table.w, "v": table.v[:, :K], "s0w": table.s0w, "s0v": table.s0v[:, :K]}
+    if table.s1v is not None:
+        t["s1w"] = table.s1w
+        t["s1v"] = table.s1v[:, :K]
+    return {k: v.detach().to("cpu").contiguous() for k, v in t.items()}
+
+
+def save_checkpoint(model, log_dir: str, step: int, *, reader_state: dict | None = None, ctx=None,
+                    max_to_keep: int = 5) -> str:
+    """Write a checkpoint of ``model`` (a FactorizationMachine) at ``step``; returns its directory."""
+    table = model.table
+    rank = ctx.rank if ctx is not None else 0
+    world = ctx.world if ctx is not None else 1
+    sharded = model.mode == "shard"
+    path = os.path.join(log_dir, f"model.ckpt-{step}")
+    os.makedirs(path, exist_ok=True)
+    if sharded or rank == 0:
+        shard_rank, shard_world = (table.rank, table.world)
+        tmp = os.path.join(path, _shard_name(shard_rank, shard_world) + ".tmp")
+        save_file(_table_tensors(table), tmp, metadata={"format": FORMAT, "rank": str(shard_rank),
+                                                          "world": str(shard_world)})
+        os.replace(tmp, os.path.join(path, _shard_name(shard_rank, shard_world)))
+    if ctx is not None and world > 1:
+        ctx.barrier()
+    if rank == 0:
+        meta = {
+            "format": FORMAT,
+            "global_step": int(step),
+            "vocabulary_size": table.vocab_size,
+            "factor_num": table.K,
+            "dtype": str(table.dtype).replace("torch.", ""),
+            "optimizer": table.opt.name,
+            "shard_world": table.world,
+            "mode": model.mode,
+            "loss_type": model.cfg.loss_type,
+            "reader_state": reader_state or {},
+        }
+        with open(os.path.join(path, "meta.json.tmp"), "w") as f:
+            json.dump(meta, f, indent=1)
+        os.replace(os.path.join(path, "meta.json.tmp"), os.path.join(path, "meta.json"))
+        _write_index(log_dir, os.path.basename(path), max_to_keep)
+    if ctx is not None and world > 1:
+        ctx.barrier()
+    return path
+
+
+def _write_index(log_dir: str, newest: str, max_to_keep: int) -> None:
+    ckpts = sorted(glob.glob(os.path.join(log_dir, "model.ckpt-*")),
+                   key=lambda p: int(re.search(r"model\.ckpt-(\d+)$", p).group(1)) if re.search(
+                       r"model\.ckpt-(\d+)$", p) else -1)
+    ckpts = [c for c in ckpts if os.path.exists(os.path.join(c, "meta.json"))]
+    if max_to_keep and len(ckpts) > max_to_keep:
+        for old in ckpts[:-max_to_keep]:
+            shutil.rmtree(old, ignore_errors=True)
+        ckpts = ckpts[-max_to_keep:]
+    lines = [f'model_checkpoint_path: "{newest}"']
+    lines += [f'all_model_checkpoint_paths: "{os.path.basename(c)}"' for c in ckpts]
+    tmp = os.path.join(log_dir, INDEX + ".tmp")
+    with open(tmp, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    os.replace(tmp, os.path.join(log_dir, INDEX))
+
+
+def read_meta(ckpt_dir: str) -> dict:
+    with open(os.path.join(ckpt_dir, "meta.json")) as f:
+        return json.load(f)
+
+
+def _iter_shards(ckpt_dir: str):
+    for p in sorted(glob.glob(os.path.join(ckpt_dir, "shard-*-of-*.safetensors"))):
+        m = re.search(r"shard-(\d+)-of-(\d+)\.safetensors$", p)
+        yield int(m.group(1)), int(m.group(2)), p
+
+
+def restore_checkpoint(model, ckpt_dir: str) -> dict:
+    """Load ``ckpt_dir`` into ``model``'s (local) table, re-sharding if needed. Returns meta."""
+    meta = read_meta(ckpt_dir)
+    table = model.table
+    if meta["factor_num"] != table.K or meta["vocabulary_size"] != table.vocab_size:
+        raise ValueError(f"checkpoint shape (V={meta['vocabulary_size']}, K={meta['factor_num']}) does not match "
+                         f"the model (V={table.vocab_size}, K={table.K})")
+    K = table.K
+    dev = table.device
+    direct = os.path.join(ckpt_dir, _shard_name(table.rank, table.world))
+    if os.path.exists(direct):
+        t = load_file(direct)
+        _copy_rows(table, None, t, K, dev)
+    else:
+        for s_rank, s_world, path in _iter_shards(ckpt_dir):
+            t = load_file(path)
+            n = t["w"].shape[0]
+            gid = torch.arange(n, dtype=torch.int64) * s_world + s_rank
+            mine = (gid % table.world == table.rank) & (gid < table.vocab_size)
+            if not bool(mine.any()):
+                continue
+            sel = torch.nonzero(mine).flatten()
+            local = torch.div(gid[sel], table.world, rounding_mode="floor")
+            _copy_rows(table, local.to(dev), {k: v[sel] for k, v in t.items()}, K, dev)
+    model.global_step = int(meta["global_step"])
+    return meta
+
+
+def _copy_rows(table, local_rows, t: dict, K: int, dev) -> None:
+    def put(dst, src, cols=False):
+        if dst is None or src is None:
+            return
+        src = src.to(dev, dst.dtype)
+        if local_rows is None:
+            n = src.shape[0]
+            if cols:
+                dst[:n, :K] = src
+            else:
+                dst[:n] = src
+        else:
+            if cols:
+                dst[local_rows, :K] = src
+            else:
+                dst[local_rows] = src
+
+    put(table.w, t.get("w"))
+    put(table.v, t.get("v"), cols=True)
+    put(table.s0w, t.get("s0w"))
+    put(table.s0v, t.get("s0v"), cols=True)
+    put(table.s1w, t.get("s1w"))
+    put(table.s1v, t.get("s1v"), cols=True)
+
+
+# ---------------------------------------------------------------------------
+# reference layout: vocab_block_{i} [V // N + 1, K + 1], id g -> block g % N, row g // N
+# ---------------------------------------------------------------------------
+def export_reference_blocks(ckpt_dir: str, out_dir: str, block_num: int, *, with_slots: bool = True) -> list[str]:
+    """Write ``vocab_block_{i}.npy`` (+ ``vocab_block_{i}_Adagrad.npy``) in the reference's layout."""
+    meta = read_meta(ckpt_dir)
+    V, K = meta["vocabulary_size"], meta["factor_num"]
+    rows_per_block = V // block_num + 1
+    os.makedirs(out_dir, exist_ok=True)
+    blocks, slots = [], []
+    for i in range(block_num):
+        blocks.append(np.lib.format.open_memmap(os.path.join(out_dir, f"vocab_block_{i}.npy"), mode="w+",
+                                                dtype=np.float32, shape=(rows_per_block, K + 1)))
+        if with_slots:
+            slots.append(np.lib.format.open_memmap(os.path.join(out_dir, f"vocab_block_{i}_Adagrad.npy"),
+                                                   mode="w+", dtype=np.float32, shape=(rows_per_block, K + 1)))
+    for s_rank, s_world, path in _iter_shards(ckpt_dir):
+        t = load_file(path)
+        n = t["w"].shape[0]
+        gid = np.arange(n, dtype=np.int64) * s_world + s_rank
+        ok = gid < V
+        gid = gid[ok]
+        ref = np.concatenate([t["w"].float().numpy()[ok, None], t["v"].float().numpy()[ok]], axis=1)
+        acc = np.concatenate([t["s0w"].numpy()[ok, None], t["s0v"].numpy()[ok]], axis=1)
+        b, r = gid % block_num, gid // block_num
+        for i in range(block_num):
+            m = b == i
+            blocks[i][r[m]] = ref[m]
+            if with_slots:
+                slots[i][r[m]] = acc[m]
+    files = []
+    for i, arr in enumerate(blocks):
+        arr.flush()
+        files.append(os.path.join(out_dir, f"vocab_block_{i}.npy"))
+    for arr in slots:
+        arr.flush()
+    with open(os.path.join(out_dir, "global_step.json"), "w") as f:
+        json.dump({"global_step": meta["global_step"], "vocabulary_size": V, "factor_num": K,
+                   "vocabulary_block_num": block_num}, f)
+    return files
+
+
+def import_reference_blocks(model, in_dir: str, block_num: int) -> None:
+    """Load ``vocab_block_{i}.npy`` (reference layout) into the model's local table shard."""
+    table = model.table
+    gids = table.global_ids().cpu()
+    ok = gids < table.vocab_size
+    gids = gids[ok]
+    local = torch.nonzero(ok).flatten()
+    b, r = gids % block_num, torch.div(gids, block_num, rounding_mode="floor")
+    for i in range(block_num):
+        arr = np.load(os.path.join(in_dir, f"vocab_block_{i}.npy"), mmap_mode="r", allow_pickle=False)
+        sp = os.path.join(in_dir, f"vocab_block_{i}_Adagrad.npy")
+        acc = np.load(sp, mmap_mode="r", allow_pickle=False) if os.path.exists(sp) else None
+        m = b == i
+        if not bool(m.any()):
+            continue
+        rows = r[m].numpy()
+        ref = torch.from_numpy(np.ascontiguousarray(arr[rows]))
+        a = torch.from_numpy(np.ascontiguousarray(acc[rows])) if acc is not None else None
+        table.load_reference_rows(local[m].to(table.device), ref, a)

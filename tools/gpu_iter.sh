@@ -1,0 +1,17 @@
+#!/bin/bash
+# Iteration loop on the GPU box: numerics tests -> bench -> kernel profile.
+# usage: tools/gpu_iter.sh <tag> [extra bench args...]
+set -o pipefail
+TAG=${1:-iter}; shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/$TAG
+mkdir -p $OUT
+export FM_NO_AUTOBUILD=1
+cd $R
+timeout -k 10 400 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1 || { echo "pytest gpu failed"; tail -40 $OUT/pytest_gpu.log; exit 1; }
+tail -1 $OUT/pytest_gpu.log
+timeout -k 10 300 python bench.py --steps 30 --warmup 5 "$@" > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -30 $OUT/bench.err; exit 1; }
+tail -2 $OUT/bench.err
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $R/bench.py --steps 20 --warmup 5 "$@" > $OUT/prof.log 2>&1 || { echo "rocprof failed"; tail -30 $OUT/prof.log; exit 1; }
+python3 $R/tools/kstats.py $OUT/prof/run_kernel_stats.csv 25 | tee $OUT/kernel_summary.txt
