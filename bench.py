@@ -63,6 +63,7 @@ def main() -> int:
     ap.add_argument("--alpha", type=float, default=1.1, help="Zipf exponent of field values")
     ap.add_argument("--mode", default=None, help="override step mode (local|shard|dp|dp_dense)")
     ap.add_argument("--profile-steps", type=int, default=0, help="also emit a torch.profiler trace")
+    ap.add_argument("--graph", type=int, default=1, help="capture the local step in a hipGraph (1/0)")
     a = ap.parse_args()
 
     p = dict(PRESETS[a.preset])
@@ -93,6 +94,15 @@ def main() -> int:
     pool = [gen.batch(a.batch) for _ in range(max(1, a.pool))]
     if dev.type == "cuda":
         torch.cuda.synchronize()
+    graphed = False
+    if a.graph and dev.type == "cuda" and model.mode == "local":
+        model.capture_graph(pool[0])  # replays copy each pool batch into the graph's static inputs
+        graphed = True
+    if rank == 0:
+        from fast_tffm_amd.ops import kernels as Kd
+
+        dd = Kd.dedup(pool[0].ids if pool[0].ids.dtype == torch.int32 else pool[0].ids.int(), key_bits=32)
+        print(f"[bench] batch stats: nnz={pool[0].nnz} unique={dd.sync()} graph={graphed}", file=sys.stderr)
 
     for i in range(a.warmup):
         model.train_step(pool[i % len(pool)])

@@ -56,10 +56,13 @@ class Batch:
         v = torch.from_numpy(np.ascontiguousarray(vals, dtype=np.float32))
         if drop_unit_vals and v.numel() > 0 and bool((v == 1).all()):
             v = None  # all-ones values: the kernels take the x=1 fast path
+        ids = np.ascontiguousarray(ids, dtype=np.int64)
+        if ids.size == 0 or int(ids.max()) < 2**31:
+            ids = ids.astype(np.int32)  # table rows are int32 on the device
         return Batch(
             labels=torch.from_numpy(np.ascontiguousarray(labels, dtype=np.float32)),
             offsets=torch.from_numpy(offsets),
-            ids=torch.from_numpy(np.ascontiguousarray(ids, dtype=np.int64)),
+            ids=torch.from_numpy(ids),
             vals=v,
             weights=None if weights is None else torch.from_numpy(np.ascontiguousarray(weights, dtype=np.float32)),
             nnz=int(offsets[-1]),

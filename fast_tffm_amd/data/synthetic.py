@@ -66,7 +66,8 @@ class CriteoSynth:
             val = zipf_sample(B, card, self.alpha, self.gen, dev)
             h = _mix64(val * 64 + f)
             cols.append(torch.remainder(h, self.vocab_size))
-        ids = torch.stack(cols, dim=1).reshape(-1).contiguous()
+        ids = torch.stack(cols, dim=1).reshape(-1)
+        ids = (ids.to(torch.int32) if self.vocab_size < 2**31 else ids).contiguous()
         offsets = torch.arange(0, (B + 1) * self.F, self.F, dtype=torch.int32, device=dev)
         labels = (torch.rand(B, generator=self.gen, device=dev) < self.ctr).to(torch.float32)
         return Batch(labels=labels, offsets=offsets, ids=ids, vals=None, weights=None, nnz=B * self.F)

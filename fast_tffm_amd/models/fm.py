@@ -83,6 +83,54 @@ class _Workspace:
             self.fwd_partial = torch.zeros(3 * 4096, dtype=torch.float32, device=dev)
 
 
+class _GraphedStep:
+    """A hipGraph of the local training step over static input buffers."""
+
+    def __init__(self, model: "FactorizationMachine", ex: Batch, warmup: int):
+        self.m = model
+        dev = model.device
+        self.sig = self._sig(ex)
+
+        def static(t):
+            return None if t is None else torch.empty_like(t, device=dev)
+
+        ids = ex.ids if ex.ids.dtype == torch.int32 else ex.ids.to(torch.int32)
+        self.inp = Batch(static(ex.labels), static(ex.offsets), static(ids), static(ex.vals), static(ex.weights),
+                         ex.nnz)
+        self._load(ex)
+        model.ws.ensure(ex.B, ex.nnz)
+        # warm up on a side stream (allocations, lazy module loads), then capture
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                model._local_train_step(self.inp)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize(dev)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = model._local_train_step(self.inp)
+        torch.cuda.synchronize(dev)
+
+    @staticmethod
+    def _sig(b: Batch):
+        return (b.B, b.nnz, b.vals is not None, b.weights is not None)
+
+    def matches(self, b: Batch) -> bool:
+        return self._sig(b) == self.sig
+
+    def _load(self, b: Batch) -> None:
+        for dst, src in ((self.inp.labels, b.labels), (self.inp.offsets, b.offsets), (self.inp.ids, b.ids),
+                         (self.inp.vals, b.vals), (self.inp.weights, b.weights)):
+            if dst is not None and src is not None and dst.data_ptr() != src.data_ptr():
+                dst.copy_(src, non_blocking=True)
+
+    def replay(self, b: Batch) -> StepOut:
+        self._load(b)
+        self.graph.replay()
+        return StepOut(self.out.loss_sum.clone(), b.B)
+
+
 class FactorizationMachine:
     """FM model + step executor for one rank."""
 
@@ -106,6 +154,8 @@ class FactorizationMachine:
         self.rps = rows_per_shard(cfg.vocabulary_size, self.world) if sharded else cfg.vocabulary_size
         self.ws = _Workspace(self.device, self.Kp, cfg.dedup_chunk)
         self.global_step = 0
+        self._side = None
+        self._graph = None
         self._exchange = None
         if mode in ("shard", "dp", "dp_dense") and self.world >= 1 and dist is not None:
             from ..parallel.exchange import make_exchange
@@ -130,33 +180,70 @@ class FactorizationMachine:
         return s
 
     def _rows32(self, b: Batch) -> torch.Tensor:
+        if b.ids.dtype == torch.int32:
+            return b.ids
         out = self.ws.rows32[: b.nnz]
         out.copy_(b.ids)  # int64 -> int32 (ids < vocabulary_size < 2^31)
         return out
 
     # ------------------------------------------------------------------
     def train_step(self, b: Batch) -> StepOut:
-        self.ws.ensure(b.B, b.nnz)
-        if self._exchange is not None:
-            out = self._exchange.train_step(b)
+        if self._graph is not None and self._graph.matches(b):
+            out = self._graph.replay(b)
         else:
-            out = self._local_train_step(b)
+            self.ws.ensure(b.B, b.nnz)
+            if self._exchange is not None:
+                out = self._exchange.train_step(b)
+            else:
+                out = self._local_train_step(b)
         self.global_step += 1
         return out
 
+    def _side_stream(self):
+        if self._side is None:
+            self._side = torch.cuda.Stream(self.device)
+        return self._side
+
     def _local_train_step(self, b: Batch) -> StepOut:
+        """fwd+loss on the current stream, concurrently with dedup on a side stream, then bwd+update.
+
+        The two branches only share read-only inputs; the join is an event, so
+        the step stays asynchronous (and graph-capturable).
+        """
         ws, cfg = self.ws, self.cfg
         rows = self._rows32(b)
         ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz)
+        gpu = self.device.type == "cuda"
+        if gpu:
+            main = torch.cuda.current_stream(self.device)
+            side = self._side_stream()
+            side.wait_stream(main)  # inputs ready; previous step's readers of ws.dd are enqueued before
+            with torch.cuda.stream(side):
+                dd = K.dedup(rows, ws=ws.dd, key_bits=bits_for(self.table.rows), ex_of_occ=ex, vals=b.vals)
         fo = K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,
                           weights=b.weights, loss=cfg.loss_type, grad_scale=self.grad_scale(b.B), want_r1=True,
                           pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
                           threads=cfg.threads)
-        dd = K.dedup(rows, ws=ws.dd, key_bits=bits_for(self.table.rows), ex_of_occ=ex, vals=b.vals)
+        if gpu:
+            main.wait_stream(side)
+        else:
+            dd = K.dedup(rows, ws=ws.dd, key_bits=bits_for(self.table.rows), ex_of_occ=ex, vals=b.vals)
         rv, rw = self.reg_coeffs
         K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
                       reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads)
         return StepOut(fo.loss_sum, b.B)
+
+    # ------------------------------------------------------------------
+    def capture_graph(self, example: Batch, warmup: int = 2) -> None:
+        """Capture the local training step for batches shaped like ``example`` into a hipGraph.
+
+        Subsequent ``train_step`` calls with the same (B, nnz, has vals/weights)
+        copy the batch into the graph's static buffers and replay the whole
+        step (~10 kernels + the stream fork/join) with one launch.
+        """
+        if self.device.type != "cuda" or self._exchange is not None:
+            raise RuntimeError("graph capture is available for the local GPU step")
+        self._graph = _GraphedStep(self, example, warmup)
 
     # ------------------------------------------------------------------
     @torch.no_grad()

@@ -108,7 +108,7 @@ def _chk_rows(v: torch.Tensor, Kp: int, name: str) -> int:
 
 
 def _range_check(idx: torch.Tensor, hi: int, name: str) -> None:
-    if _DEBUG and idx.numel() > 0:
+    if _DEBUG and idx.numel() > 0 and not (idx.is_cuda and torch.cuda.is_current_stream_capturing()):
         lo_v, hi_v = int(idx.min()), int(idx.max())
         _check(lo_v >= 0 and hi_v < hi, f"{name}: index range [{lo_v}, {hi_v}] outside [0, {hi})")
 

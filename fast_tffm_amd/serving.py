@@ -1,0 +1,161 @@
+"""Serving export (``run.py generate``) and a standalone predictor.
+
+Reference: ``generate`` restores the latest checkpoint and writes a TF
+SavedModel (tag ``serve``, signature ``serving_default``, input ``data_lines``
+(string), output ``scores``, method PREDICT; run_tffm.py:93-120) whose graph is
+pure TF: ``serving_parser`` splits feature-only lines ``id:val id:val ...``
+(``:val`` mandatory, no label column), ``serving_scorer`` looks the ids up in
+``vocab_block_i`` with the "mod" partition and evaluates the FM densely
+(tffm/fm_model.py:195-265).  The export path must not exist yet.
+
+Here the export is a self-contained directory::
+
+    export_path/saved_model.json        signature + model metadata
+    export_path/variables/vocab_block_{i}.npy   reference layout [V // N + 1, K + 1]
+
+``ServingModel.load(export_path).predict(data_lines)`` reproduces the
+signature (lines -> scores) with the native scorer (CPU or gfx950), and
+``python -m fast_tffm_amd.serving --dir export_path --inputs data.npy`` mirrors
+``saved_model_cli run ... --inputs data_lines=data.npy``.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+SIGNATURE = {
+    "tag_set": "serve",
+    "signature_def": "serving_default",
+    "method_name": "tensorflow/serving/predict",
+    "inputs": {"data_lines": {"dtype": "string", "shape": [-1]}},
+    "outputs": {"scores": {"dtype": "float32", "shape": [-1]}},
+}
+
+
+def export_model(ckpt_dir: str, export_path: str, *, vocabulary_block_num: int, hash_feature_id: bool = False,
+                 loss_type: str = "mse") -> str:
+    """Write a serving export of checkpoint ``ckpt_dir`` to the (new) directory ``export_path``."""
+    from .utils.checkpoint import export_reference_blocks, read_meta
+
+    if os.path.exists(export_path):
+        raise FileExistsError(f"export path {export_path} already exists (it must not be a pre-existing directory)")
+    meta = read_meta(ckpt_dir)
+    tmp = export_path.rstrip("/") + ".tmp-export"
+    os.makedirs(os.path.join(tmp, "variables"), exist_ok=True)
+    export_reference_blocks(ckpt_dir, os.path.join(tmp, "variables"), vocabulary_block_num, with_slots=False)
+    doc = dict(SIGNATURE)
+    doc.update({
+        "format": "fast_tffm_amd/serving-v1",
+        "vocabulary_size": meta["vocabulary_size"],
+        "vocabulary_block_num": vocabulary_block_num,
+        "factor_num": meta["factor_num"],
+        "hash_feature_id": bool(hash_feature_id),
+        "loss_type": loss_type,
+        "global_step": meta["global_step"],
+        "score": "raw FM score (logit for logistic loss), no global bias",
+    })
+    with open(os.path.join(tmp, "saved_model.json"), "w") as f:
+        json.dump(doc, f, indent=1)
+    os.replace(tmp, export_path)
+    return export_path
+
+
+def parse_serving_lines(lines, vocab_size: int, hash_feature_id: bool = False):
+    """Feature-only lines ``id:val id:val ...`` -> (offsets, ids, vals) (reference serving_parser)."""
+    offsets = [0]
+    ids: list[int] = []
+    vals: list[float] = []
+    from .ops import native
+
+    for ln in lines:
+        if isinstance(ln, bytes):
+            ln = ln.decode()
+        toks = ln.split()
+        for tok in toks:
+            fid, sep, fv = tok.rpartition(":")
+            if not sep:
+                raise ValueError(f"serving input needs id:val tokens, got {tok!r}")
+            if hash_feature_id:
+                ids.append(int(native.cpu().hash_bucket([fid], vocab_size)[0]))
+            else:
+                i = int(fid)
+                if not 0 <= i < vocab_size:
+                    raise ValueError(f"feature id {i} outside [0, {vocab_size})")
+                ids.append(i)
+            vals.append(float(fv))
+        offsets.append(len(ids))
+    return (torch.tensor(offsets, dtype=torch.int32), torch.tensor(ids, dtype=torch.int64),
+            torch.tensor(vals, dtype=torch.float32))
+
+
+class ServingModel:
+    """Loaded serving export: ``predict(data_lines) -> scores``."""
+
+    def __init__(self, meta: dict, v: torch.Tensor, w: torch.Tensor, device: torch.device):
+        self.meta, self.v, self.w, self.device = meta, v, w, device
+        self.K = meta["factor_num"]
+        self.Kp = v.shape[1]
+
+    @classmethod
+    def load(cls, export_path: str, device: str | None = None) -> "ServingModel":
+        from .ops.kernels import padded_k
+
+        with open(os.path.join(export_path, "saved_model.json")) as f:
+            meta = json.load(f)
+        V, K, N = meta["vocabulary_size"], meta["factor_num"], meta["vocabulary_block_num"]
+        dev = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
+        Kp = padded_k(K)
+        v = torch.zeros((V, Kp), dtype=torch.float32)
+        w = torch.zeros(V, dtype=torch.float32)
+        gid = torch.arange(V)
+        for i in range(N):
+            blk = np.load(os.path.join(export_path, "variables", f"vocab_block_{i}.npy"), mmap_mode="r",
+                          allow_pickle=False)
+            sel = gid[gid % N == i]
+            rows = torch.from_numpy(np.ascontiguousarray(blk[(sel // N).numpy()]))
+            w[sel] = rows[:, 0]
+            v[sel, :K] = rows[:, 1:]
+        return cls(meta, v.to(dev), w.to(dev), dev)
+
+    def predict(self, data_lines) -> np.ndarray:
+        from .ops import kernels as Kn
+
+        flat = np.asarray(data_lines).reshape(-1).tolist()
+        offsets, ids, vals = parse_serving_lines(flat, self.meta["vocabulary_size"], self.meta["hash_feature_id"])
+        d = self.device
+        fo = Kn.fm_forward(offsets.to(d), ids.to(torch.int32).to(d), vals.to(d), self.v, self.w, self.Kp,
+                           want_r1=False)
+        return fo.pred.cpu().numpy()
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description="Run a fast_tffm_amd serving export (saved_model_cli run equivalent)")
+    ap.add_argument("--dir", required=True)
+    ap.add_argument("--inputs", required=True, help="data_lines=FILE.npy | FILE.npy | FILE.txt (one line each)")
+    ap.add_argument("--outdir", default=None)
+    ap.add_argument("--device", default=None)
+    a = ap.parse_args(argv)
+    path = a.inputs.split("=", 1)[1] if "=" in a.inputs else a.inputs
+    if path.endswith(".npy"):
+        lines = np.load(path, allow_pickle=False)
+    else:
+        with open(path) as f:
+            lines = [ln.rstrip("\n") for ln in f]
+    m = ServingModel.load(a.dir, a.device)
+    scores = m.predict(lines)
+    if a.outdir:
+        os.makedirs(a.outdir, exist_ok=True)
+        np.save(os.path.join(a.outdir, "scores.npy"), scores)
+    print("Result for output key scores:")
+    print(scores)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
