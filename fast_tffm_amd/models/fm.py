@@ -86,7 +86,7 @@ class _Workspace:
 class _GraphedStep:
     """A hipGraph of the local training step over static input buffers."""
 
-    def __init__(self, model: "FactorizationMachine", ex: Batch, warmup: int):
+    def __init__(self, model: "FactorizationMachine", ex: Batch, warmup: int = 1):
         self.m = model
         dev = model.device
         self.sig = self._sig(ex)
@@ -97,20 +97,16 @@ class _GraphedStep:
         ids = ex.ids if ex.ids.dtype == torch.int32 else ex.ids.to(torch.int32)
         self.inp = Batch(static(ex.labels), static(ex.offsets), static(ids), static(ex.vals), static(ex.weights),
                          ex.nnz)
-        self._load(ex)
-        model.ws.ensure(ex.B, ex.nnz)
-        # warm up on a side stream (allocations, lazy module loads), then capture
-        s = torch.cuda.Stream(dev)
-        s.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(s):
-            for _ in range(warmup):
-                model._local_train_step(self.inp)
-        torch.cuda.current_stream(dev).wait_stream(s)
+        self.eager_left = max(1, warmup)  # real (eager) steps before capture: lazy loads, workspace sizing
+        self.graph = None
+        self.out = None
+
+    def _capture(self) -> None:
+        dev = self.m.device
         torch.cuda.synchronize(dev)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            self.out = model._local_train_step(self.inp)
-        torch.cuda.synchronize(dev)
+            self.out = self.m._local_train_step(self.inp)
 
     @staticmethod
     def _sig(b: Batch):
@@ -126,7 +122,13 @@ class _GraphedStep:
                 dst.copy_(src, non_blocking=True)
 
     def replay(self, b: Batch) -> StepOut:
+        if self.eager_left > 0:
+            self.eager_left -= 1
+            self.m.ws.ensure(b.B, b.nnz)
+            return self.m._local_train_step(b)
         self._load(b)
+        if self.graph is None:
+            self._capture()  # capture does not execute: the replay below runs this step
         self.graph.replay()
         return StepOut(self.out.loss_sum.clone(), b.B)
 
@@ -234,12 +236,14 @@ class FactorizationMachine:
         return StepOut(fo.loss_sum, b.B)
 
     # ------------------------------------------------------------------
-    def capture_graph(self, example: Batch, warmup: int = 2) -> None:
-        """Capture the local training step for batches shaped like ``example`` into a hipGraph.
+    def capture_graph(self, example: Batch, warmup: int = 1) -> None:
+        """Arm hipGraph execution of the local training step for batches shaped like ``example``.
 
-        Subsequent ``train_step`` calls with the same (B, nnz, has vals/weights)
-        copy the batch into the graph's static buffers and replay the whole
-        step (~10 kernels + the stream fork/join) with one launch.
+        The next ``warmup`` matching ``train_step`` calls run eagerly; the one
+        after captures the step (capture executes nothing) and every matching
+        call from then on copies its batch into the graph's static buffers and
+        replays the whole step (~10 kernels + the stream fork/join) with one
+        launch.  Results are identical to eager execution.
         """
         if self.device.type != "cuda" or self._exchange is not None:
             raise RuntimeError("graph capture is available for the local GPU step")
