@@ -23,6 +23,7 @@ class Batch:
     vals: torch.Tensor | None       # [nnz] float32, None => all ones
     weights: torch.Tensor | None = None  # [B] float32, None => all ones
     nnz: int = -1                   # host copy of offsets[-1] (avoids a device sync)
+    reader_pos: tuple | None = None  # (epoch, batches consumed in epoch) after this batch
 
     def __post_init__(self):
         if self.nnz < 0:
@@ -40,13 +41,15 @@ class Batch:
         def mv(t):
             return None if t is None else t.to(device, non_blocking=non_blocking)
 
-        return Batch(mv(self.labels), mv(self.offsets), mv(self.ids), mv(self.vals), mv(self.weights), self.nnz)
+        return Batch(mv(self.labels), mv(self.offsets), mv(self.ids), mv(self.vals), mv(self.weights), self.nnz,
+                     self.reader_pos)
 
     def pin_memory(self) -> "Batch":
         def pn(t):
             return None if t is None else t.pin_memory()
 
-        return Batch(pn(self.labels), pn(self.offsets), pn(self.ids), pn(self.vals), pn(self.weights), self.nnz)
+        return Batch(pn(self.labels), pn(self.offsets), pn(self.ids), pn(self.vals), pn(self.weights), self.nnz,
+                     self.reader_pos)
 
     @staticmethod
     def from_parsed(labels: np.ndarray, sizes: np.ndarray, ids: np.ndarray, vals: np.ndarray,

@@ -114,6 +114,12 @@ class TextBatchReader:
                 if ln:
                     yield ln, (wl[i] if wl is not None else None)
 
+    @staticmethod
+    def _tag(b: Batch, epoch: int, count: int) -> Batch:
+        # position AFTER this batch: what a checkpoint taken after consuming it must store
+        b.reader_pos = (epoch, count)  # type: ignore[attr-defined]
+        return b
+
     def _make(self, items) -> Batch:
         lines = [it[0] for it in items]
         w = None
@@ -137,7 +143,7 @@ class TextBatchReader:
                     count += 1
                     if count > skip:
                         self.state.batches_in_epoch = count
-                        yield self._make(out)
+                        yield self._tag(self._make(out), epoch, count)
             if self.shuffle:
                 rng.shuffle(buf)
             while buf:
@@ -145,7 +151,7 @@ class TextBatchReader:
                 count += 1
                 if count > skip:
                     self.state.batches_in_epoch = count
-                    yield self._make(out)
+                    yield self._tag(self._make(out), epoch, count)
             skip = 0
             self.state.batches_in_epoch = 0
         self.state.epoch = self.num_epochs

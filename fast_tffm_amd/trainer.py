@@ -118,7 +118,7 @@ class Trainer:
         reader = TextBatchReader(c.train_files, c.weight_files or None, c.batch_size, vocab_size=c.vocabulary_size,
                                  hash_feature_id=c.hash_feature_id, num_epochs=c.num_epochs, shuffle=c.shuffle,
                                  seed=c.seed, parse_threads=c.parse_threads, rank=self.rank, world=self.world,
-                                 state=self.reader_state)
+                                 state=ReaderState(self.reader_state.epoch, self.reader_state.batches_in_epoch))
         pf = Prefetcher(reader, self.device, queue_size=max(1, min(c.queue_size, 64)))
         metrics = MetricsLogger(c.log_dir if self.rank == 0 else None, every=c.save_summaries_steps)
         self.print("========", "train", "========")
@@ -142,6 +142,8 @@ class Trainer:
             cur = time.time()
             out = self.model.train_step(batch)
             step_num = self.model.global_step
+            if batch.reader_pos is not None:  # position of the last CONSUMED batch (the reader runs ahead)
+                self.reader_state.epoch, self.reader_state.batches_in_epoch = batch.reader_pos
             loss = out.mean_loss()  # host sync: the reference fetches the loss every step
             last_loss = loss
             tend = time.time()
