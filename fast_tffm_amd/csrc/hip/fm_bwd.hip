@@ -61,21 +61,53 @@ struct BwdArgs {
   int* big_count;           // device scalar, zeroed by the launcher
 };
 
+// Parameter row + optimizer slots of one segment, read before its gradient is
+// known so that the loads overlap the occurrence reduction.
+template <int EPL>
+struct RowState {
+  long long row;
+  float vv[EPL], st0[EPL], st1[EPL];
+  float wv, q0, q1;
+};
+
 template <typename TV, int EPL>
-__device__ inline void bwd_finalize(const BwdArgs& a, int u, int t, bool tact, int tE,
-                                    const float (&A)[EPL], float Scx, float Sc, int n_u) {
+__device__ inline void bwd_load_row(const BwdArgs& a, int u, int tE, RowState<EPL>& r) {
   using F = Frag<TV>;
-  const long long row = (a.mode == kBwdLocal) ? (long long)a.uniq[u] : (long long)u;
-  TV* vrow = reinterpret_cast<TV*>(a.v) + row * a.v_stride + tE * EPL;
-  float vv[EPL];
-  F::load(vrow, vv);
-  float* wp = a.w + row * a.w_stride;
-  const float wv = *wp;
+  r.row = (a.mode == kBwdLocal) ? (long long)a.uniq[u] : (long long)u;
+  F::load(reinterpret_cast<const TV*>(a.v) + r.row * a.v_stride + tE * EPL, r.vv);
+  r.wv = a.w[r.row * a.w_stride];
+  if (a.mode == kBwdEmit) return;
+  const float* s0 = a.s0v + r.row * a.s_stride + tE * EPL;
+#pragma unroll
+  for (int k = 0; k < EPL; k += 4) {
+    const float4 q = *reinterpret_cast<const float4*>(s0 + k);
+    r.st0[k] = q.x; r.st0[k + 1] = q.y; r.st0[k + 2] = q.z; r.st0[k + 3] = q.w;
+  }
+  r.q0 = a.s0w[r.row];
+  if (a.s1v) {
+    const float* s1 = a.s1v + r.row * a.s_stride + tE * EPL;
+#pragma unroll
+    for (int k = 0; k < EPL; k += 4) {
+      const float4 z = *reinterpret_cast<const float4*>(s1 + k);
+      r.st1[k] = z.x; r.st1[k + 1] = z.y; r.st1[k + 2] = z.z; r.st1[k + 3] = z.w;
+    }
+    r.q1 = a.s1w[r.row];
+  } else {
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) r.st1[k] = 0.f;
+    r.q1 = 0.f;
+  }
+}
+
+template <typename TV, int EPL>
+__device__ inline void bwd_finish(const BwdArgs& a, int u, int t, bool tact, RowState<EPL>& r,
+                                  const float (&A)[EPL], float Scx, float Sc, int n_u) {
+  using F = Frag<TV>;
   const float nreg_v = a.reg_v * (float)n_u, nreg_w = a.reg_w * (float)n_u;
   float gr[EPL];
 #pragma unroll
-  for (int k = 0; k < EPL; ++k) gr[k] = A[k] - Scx * vv[k] + nreg_v * vv[k];
-  const float gw = Sc + nreg_w * wv;
+  for (int k = 0; k < EPL; ++k) gr[k] = A[k] - Scx * r.vv[k] + nreg_v * r.vv[k];
+  const float gw = Sc + nreg_w * r.wv;
   if (a.mode == kBwdEmit) {
     float* dst = a.grad_out + (long long)u * a.g_stride;
     if (tact) {
@@ -86,37 +118,35 @@ __device__ inline void bwd_finalize(const BwdArgs& a, int u, int t, bool tact, i
     if (t == 0) dst[a.Kp] = gw;
     return;
   }
-  float* s0 = a.s0v + row * a.s_stride + tE * EPL;
-  float* s1 = a.s1v ? a.s1v + row * a.s_stride + tE * EPL : nullptr;
-  float st0[EPL], st1[EPL];
 #pragma unroll
-  for (int k = 0; k < EPL; k += 4) {
-    const float4 q = *reinterpret_cast<const float4*>(s0 + k);
-    st0[k] = q.x; st0[k + 1] = q.y; st0[k + 2] = q.z; st0[k + 3] = q.w;
-    if (s1) {
-      const float4 z = *reinterpret_cast<const float4*>(s1 + k);
-      st1[k] = z.x; st1[k + 1] = z.y; st1[k + 2] = z.z; st1[k + 3] = z.w;
-    } else {
-      st1[k] = st1[k + 1] = st1[k + 2] = st1[k + 3] = 0.f;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < EPL; ++k) opt_step(a.opt, gr[k], vv[k], st0[k], st1[k]);
+  for (int k = 0; k < EPL; ++k) opt_step(a.opt, gr[k], r.vv[k], r.st0[k], r.st1[k]);
   if (tact) {
-    F::store(vrow, vv);
+    F::store(reinterpret_cast<TV*>(a.v) + r.row * a.v_stride + t * EPL, r.vv);
+    float* s0 = a.s0v + r.row * a.s_stride + t * EPL;
 #pragma unroll
-    for (int k = 0; k < EPL; k += 4) {
-      *reinterpret_cast<float4*>(s0 + k) = make_float4(st0[k], st0[k + 1], st0[k + 2], st0[k + 3]);
-      if (s1) *reinterpret_cast<float4*>(s1 + k) = make_float4(st1[k], st1[k + 1], st1[k + 2], st1[k + 3]);
+    for (int k = 0; k < EPL; k += 4)
+      *reinterpret_cast<float4*>(s0 + k) = make_float4(r.st0[k], r.st0[k + 1], r.st0[k + 2], r.st0[k + 3]);
+    if (a.s1v) {
+      float* s1 = a.s1v + r.row * a.s_stride + t * EPL;
+#pragma unroll
+      for (int k = 0; k < EPL; k += 4)
+        *reinterpret_cast<float4*>(s1 + k) = make_float4(r.st1[k], r.st1[k + 1], r.st1[k + 2], r.st1[k + 3]);
     }
   }
   if (t == 0) {
-    float p = wv, q0 = a.s0w[row], q1 = a.s1w ? a.s1w[row] : 0.f;
-    opt_step(a.opt, gw, p, q0, q1);
-    *wp = p;
-    a.s0w[row] = q0;
-    if (a.s1w) a.s1w[row] = q1;
+    opt_step(a.opt, gw, r.wv, r.q0, r.q1);
+    a.w[r.row * a.w_stride] = r.wv;
+    a.s0w[r.row] = r.q0;
+    if (a.s1w) a.s1w[r.row] = r.q1;
   }
+}
+
+template <typename TV, int EPL>
+__device__ inline void bwd_finalize(const BwdArgs& a, int u, int t, bool tact, int tE,
+                                    const float (&A)[EPL], float Scx, float Sc, int n_u) {
+  RowState<EPL> r;
+  bwd_load_row<TV, EPL>(a, u, tE, r);
+  bwd_finish<TV, EPL>(a, u, t, tact, r, A, Scx, Sc, n_u);
 }
 
 // One lane group per chunk of <= CH (<= kMaxCH) sorted occurrences of one row.
@@ -141,6 +171,9 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_chunk_kernel(BwdArgs a) {
     const int u = a.chunk_seg[c];
     const int j0 = a.chunk_start[c], j1 = a.chunk_start[c + 1];
     const int len = j1 - j0;
+    const bool single = a.seg_chunk[u + 1] - a.seg_chunk[u] == 1;
+    RowState<EPL> rs;
+    if (single) bwd_load_row<TV, EPL>(a, u, tE, rs);  // overlaps the r1 reduction below
     // lane-parallel prefetch of the chunk's (example, dpred*x, x)
     int pex[PF];
     float pc[PF], px[PF];
@@ -191,9 +224,8 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_chunk_kernel(BwdArgs a) {
         }
       }
     }
-    const int cs0 = a.seg_chunk[u], cs1 = a.seg_chunk[u + 1];
-    if (cs1 - cs0 == 1) {
-      bwd_finalize<TV, EPL>(a, u, t, tact, tE, A, Scx, Sc, len);
+    if (single) {
+      bwd_finish<TV, EPL>(a, u, t, tact, rs, A, Scx, Sc, len);
     } else {
       float* dst = a.partial + (long long)c * (a.Kp + 4);
       if (tact) {
@@ -284,15 +316,32 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_big_kernel(BwdArgs a) {
 #pragma unroll
     for (int k = 0; k < EPL; ++k) A[k] = 0.f;
     float Scx = 0.f, Sc = 0.f;
-    for (int c = c0 + grp; c < c1; c += NG) {
-      const float* src = a.partial + (long long)c * (a.Kp + 4);
+    // 4 partial rows in flight per group; fixed order (c0+grp, +NG, ...) keeps the sum deterministic
+    for (int c = c0 + grp; c < c1; c += 4 * NG) {
+      float pr[4][EPL], ps[4], pt[4];
 #pragma unroll
-      for (int k = 0; k < EPL; k += 4) {
-        const float4 f = *reinterpret_cast<const float4*>(src + tE * EPL + k);
-        A[k] += f.x; A[k + 1] += f.y; A[k + 2] += f.z; A[k + 3] += f.w;
+      for (int q = 0; q < 4; ++q) {
+        const int cc = c + q * NG;
+        const bool ok = cc < c1;
+        const float* src = a.partial + (long long)(ok ? cc : c) * (a.Kp + 4);
+#pragma unroll
+        for (int k = 0; k < EPL; k += 4) {
+          const float4 f = *reinterpret_cast<const float4*>(src + tE * EPL + k);
+          pr[q][k] = f.x; pr[q][k + 1] = f.y; pr[q][k + 2] = f.z; pr[q][k + 3] = f.w;
+        }
+        const float m = ok ? 1.f : 0.f;
+        ps[q] = m * src[a.Kp];
+        pt[q] = m * src[a.Kp + 1];
+#pragma unroll
+        for (int k = 0; k < EPL; ++k) pr[q][k] *= m;
       }
-      Scx += src[a.Kp];
-      Sc += src[a.Kp + 1];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int k = 0; k < EPL; ++k) A[k] += pr[q][k];
+        Scx += ps[q];
+        Sc += pt[q];
+      }
     }
     float* my = lds + grp * ROW;
 #pragma unroll

@@ -34,12 +34,20 @@ struct FwdArgs {
   float* reg_partial;   // [2*gridDim.x] (sum |v|^2, sum w^2) or nullptr
 };
 
+// Rows of one example kept in flight per lane group: enough to cover a
+// Criteo-shaped example (39 features) in one round for K=64 (G=4 -> 10 row
+// loads per lane) while bounding VGPRs for large K.
+template <int G>
+struct FwdUnroll {
+  static constexpr int v = (40 / G) < 1 ? 1 : ((40 / G) > 12 ? 12 : (40 / G));
+};
+
 template <int LPR, typename TV>
 __global__ __launch_bounds__(kBlock) void fm_fwd_kernel(FwdArgs a) {
   using F = Frag<TV>;
   constexpr int EPL = F::N;
   constexpr int G = kWave / LPR;
-  constexpr int UNR = (16 / G) > 1 ? (16 / G) : 1;
+  constexpr int UNR = FwdUnroll<G>::v;
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR, t = lane % LPR;
   const int nv = a.Kp / EPL;
@@ -50,6 +58,7 @@ __global__ __launch_bounds__(kBlock) void fm_fwd_kernel(FwdArgs a) {
   const TV* vbase = reinterpret_cast<const TV*>(a.v) + tE * EPL;
   const int wave = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   const int nwaves = gridDim.x * kWavesPerBlock;
+  const bool want_reg = a.reg_partial != nullptr;
 
   float loss_acc = 0.f, regv_acc = 0.f, regw_acc = 0.f;
   for (int i = wave; i < a.B; i += nwaves) {
@@ -67,32 +76,36 @@ __global__ __launch_bounds__(kBlock) void fm_fwd_kernel(FwdArgs a) {
         my_x = a.vals ? a.vals[base + lane] : 1.f;
       }
       for (int q = 0; q < m; q += G * UNR) {
-        float fr[UNR][EPL], fw[UNR], fx[UNR], fm[UNR];
-        // Unconditional loads (invalid slots re-read a valid row and are masked
-        // to zero): keeps all UNR loads in flight before the first use.
+        float fr[UNR][EPL], fw[UNR], fx[UNR];
+        // Issue every row load of the round before the first use.  Loads are
+        // unconditional (slots past the example re-read a valid row of it and are
+        // masked to zero afterwards), so hipcc keeps all UNR loads in flight.
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
           const int f = q + u * G + g;
-          const int row = __shfl(my_row, f & (kWave - 1), kWave);
-          const float x = __shfl(my_x, f & (kWave - 1), kWave);
-          fm[u] = f < m ? 1.f : 0.f;
-          fx[u] = x * fm[u];
+          const int src = f < m ? f : 0;
+          const int row = __shfl(my_row, src, kWave);
+          const float x = __shfl(my_x, src, kWave);
+          fx[u] = f < m ? x : 0.f;
           F::load(vbase + (long long)row * a.v_stride, fr[u]);
           fw[u] = a.w[(long long)row * a.w_stride];
         }
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
           const float xm = fx[u] * tmask;
-          const float rm = fm[u] * tmask;
 #pragma unroll
           for (int k = 0; k < EPL; ++k) {
             const float xv = xm * fr[u][k];
             s1[k] += xv;
             s2[k] += xv * xv;
-            rv += rm * fr[u][k] * fr[u][k];
           }
           lin += wmask * fx[u] * fw[u];
-          rw += wmask * fm[u] * fw[u] * fw[u];
+          if (want_reg) {
+            const float ok = (q + u * G + g) < m ? 1.f : 0.f;
+#pragma unroll
+            for (int k = 0; k < EPL; ++k) rv += ok * tmask * fr[u][k] * fr[u][k];
+            rw += ok * wmask * fw[u] * fw[u];
+          }
         }
       }
     }
@@ -112,7 +125,7 @@ __global__ __launch_bounds__(kBlock) void fm_fwd_kernel(FwdArgs a) {
       for (int k = 0; k < EPL; k += 4)
         *reinterpret_cast<float4*>(dst + k) = make_float4(s1[k], s1[k + 1], s1[k + 2], s1[k + 3]);
     }
-    if (a.reg_partial != nullptr) {
+    if (want_reg) {
       rv = group_sum<kWave>(rv);
       rw = group_sum<kWave>(rw);
       regv_acc += rv;
