@@ -1,0 +1,125 @@
+"""Multi-rank correctness on CPU (gloo, world_size 2): every exchange mode is a
+drop-in replacement for the single-process step.
+
+* ``shard`` (row-sharded table, all-to-all lookups/grads), ``dp`` (replicated,
+  sparse all-gather) and ``dp_dense`` (replicated, dense all-reduce) with
+  ``grad_reduce = mean`` must equal ONE process training on the concatenated
+  global batch (batch_size_cfg scaled by the world size);
+* ``shard`` with ``grad_reduce = sum`` equals one process whose example weights
+  are multiplied by the world size (the summed per-rank mean losses);
+* a checkpoint written by 2 shards restores into a 1-process table (re-shard)
+  and into the reference vocab_block layout.
+"""
+
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from fast_tffm_amd.data.batch import Batch
+from fast_tffm_amd.data.synthetic import random_batch
+from fast_tffm_amd.models.fm import FactorizationMachine, FMConfig
+from fast_tffm_amd.ops import kernels as K
+from fast_tffm_amd.utils import checkpoint as ckpt
+
+V, KF, B, STEPS, WORLD = 997, 8, 24, 3, 2
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _cfg(mode, grad_reduce, bcfg):
+    return FMConfig(vocabulary_size=V, factor_num=KF, loss_type="logistic", factor_lambda=0.05, bias_lambda=0.02,
+                    batch_size=bcfg, init_value_range=0.1, seed=11, mode=mode, grad_reduce=grad_reduce,
+                    opt=K.OptConfig("adagrad", lr=0.1, initial_accumulator=0.1), threads=1)
+
+
+def _batch(step, rank):
+    return random_batch(B, V, max_feats=10, seed=1000 * step + rank)
+
+
+def _worker(rank, world, port, mode, grad_reduce, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    from fast_tffm_amd.parallel import dist as fmdist
+
+    ctx = fmdist.init_distributed(backend="gloo", rank=rank, world=world, device="cpu")
+    m = FactorizationMachine(_cfg(mode, grad_reduce, 16), device="cpu", dist=ctx)
+    losses = [m.train_step(_batch(s, rank)).mean_loss() for s in range(STEPS)]
+    pred = m.predict(_batch(99, rank))
+    torch.save({"gids": m.table.global_ids(), "rows": m.table.reference_rows(), "acc": m.table.s0v[:, :KF].clone(),
+                "losses": losses, "pred": pred}, os.path.join(out_dir, f"rank{rank}.pt"))
+    ckpt.save_checkpoint(m, os.path.join(out_dir, "log"), m.global_step, ctx=ctx)
+    fmdist.shutdown()
+
+
+def _run_world(tmp_path, mode, grad_reduce):
+    port = _free_port()
+    mp.spawn(_worker, args=(WORLD, port, mode, grad_reduce, str(tmp_path)), nprocs=WORLD, join=True)
+    return [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(WORLD)]
+
+
+def _concat(batches, weight_mult=1.0):
+    offs, ids, vals, labels, weights, base = [torch.zeros(1, dtype=torch.int32)], [], [], [], [], 0
+    for b in batches:
+        offs.append(b.offsets[1:] + base)
+        base += b.nnz
+        ids.append(b.ids)
+        vals.append(b.vals)
+        labels.append(b.labels)
+        weights.append(b.weights * weight_mult)
+    return Batch(torch.cat(labels), torch.cat(offs), torch.cat(ids), torch.cat(vals), torch.cat(weights), base)
+
+
+def _single(grad_reduce):
+    bcfg = 16 * WORLD if grad_reduce == "mean" else 16
+    m = FactorizationMachine(_cfg("local", "sum", bcfg), device="cpu")
+    wm = 1.0 if grad_reduce == "mean" else float(WORLD)
+    for s in range(STEPS):
+        m.train_step(_concat([_batch(s, r) for r in range(WORLD)], wm))
+    return m
+
+
+def _assemble(res):
+    rows = torch.zeros(V, KF + 1)
+    for r in res:
+        g = r["gids"]
+        ok = g < V
+        rows[g[ok]] = r["rows"][ok]
+    return rows
+
+
+@pytest.mark.parametrize("mode,grad_reduce", [("shard", "mean"), ("shard", "sum"), ("dp", "mean"),
+                                              ("dp_dense", "mean")])
+def test_multi_rank_equals_single_process(tmp_path, mode, grad_reduce):
+    res = _run_world(tmp_path, mode, grad_reduce)
+    ref = _single(grad_reduce)
+    ref_rows = ref.table.reference_rows()
+    if mode == "shard":
+        got = _assemble(res)
+        torch.testing.assert_close(got, ref_rows, rtol=1e-5, atol=1e-7)
+    else:  # replicated: every rank holds the full, identical table
+        for r in res:
+            torch.testing.assert_close(r["rows"], ref_rows, rtol=1e-5, atol=1e-7)
+        assert torch.equal(res[0]["rows"], res[1]["rows"])
+    # predictions of rank r's eval batch match the single model's
+    for rank, r in enumerate(res):
+        torch.testing.assert_close(r["pred"], ref.predict(_batch(99, rank)), rtol=1e-5, atol=1e-6)
+
+    if mode == "shard" and grad_reduce == "mean":
+        # re-shard: 2-shard checkpoint -> 1-process table
+        m1 = FactorizationMachine(_cfg("local", "sum", 16), device="cpu")
+        meta = ckpt.restore_checkpoint(m1, ckpt.latest_checkpoint(str(tmp_path / "log")))
+        assert meta["shard_world"] == WORLD and m1.global_step == STEPS
+        torch.testing.assert_close(m1.table.reference_rows(), ref_rows, rtol=1e-5, atol=1e-7)
+        # reference layout export/import round trip
+        files = ckpt.export_reference_blocks(ckpt.latest_checkpoint(str(tmp_path / "log")), str(tmp_path / "ref"), 4)
+        assert len(files) == 4
+        m2 = FactorizationMachine(_cfg("local", "sum", 16), device="cpu")
+        ckpt.import_reference_blocks(m2, str(tmp_path / "ref"), 4)
+        assert torch.equal(m2.table.reference_rows(), _assemble(res))  # bit-exact round trip of the shards
