@@ -8,13 +8,16 @@
 //      use (rocPRIM onesweep).  The payload is the occurrence index, or -- when
 //      the caller needs neither the inverse map nor per-occurrence values --
 //      directly the example index, which saves the gather in step 3;
-//   2. ONE inclusive scan of a packed 64-bit flag per sorted position:
-//      high word = "segment head" (key differs from its left neighbour), low
-//      word = "chunk start" (head, or position % CH == 0).  The flags are
-//      computed on the fly by a transform iterator (no flag array);
-//   3. one emit kernel: unique keys, segment starts, first chunk of each
-//      segment, chunk starts and chunk->segment map, U and #chunks, plus the
-//      optional inverse map and per-sorted-occurrence example index / value.
+//   2. run-length encoding with a 3-kernel tile scan of two flags per sorted
+//      position: "segment head" (key differs from its left neighbour) and
+//      "chunk start" (head, or position % CH == 0):
+//        tile_count  -- per 2048-element tile: #heads, #chunk starts
+//        tile_scan   -- one workgroup scans the tile totals (U, #chunks)
+//        tile_emit   -- re-reads its tile, block-scans the flags and writes
+//                       unique keys, segment starts, first chunk of each
+//                       segment, chunk starts, chunk->segment, the optional
+//                       inverse map / per-sorted-occurrence example index and
+//                       value, and the list of rows that span several chunks;
 // Chunks cut every segment at CH-aligned sorted positions, so no chunk is
 // longer than CH and a hot id (tens of thousands of occurrences in Criteo's
 // low-cardinality fields) is spread over many lane groups in the backward.
@@ -23,27 +26,23 @@
 
 namespace fm {
 
-struct FlagOp {
-  const uint32_t* skeys;
-  int CH;
-  __device__ __host__ unsigned long long operator()(int j) const {
-    const bool head = (j == 0) || (skeys[j] != skeys[j - 1]);
-    const bool cstart = head || (j % CH == 0);
-    return ((unsigned long long)(head ? 1u : 0u) << 32) | (cstart ? 1ull : 0ull);
-  }
-};
+constexpr int kRleItems = 8;                     // elements per thread
+constexpr int kRleTile = kBlock * kRleItems;     // 2048 elements per tile
+constexpr int kMaxTiles = 1024 * 64;             // single-workgroup tile scan limit (n < 134M)
 
-struct EmitArgs {
-  int n, CH;
+struct RleArgs {
+  int n, CH, ntiles;
   const uint32_t* skeys;          // sorted keys
   const int* spay;                // sorted payload (occurrence or example index)
-  const unsigned long long* incl; // inclusive scan of packed flags
+  unsigned* tile_cnt;             // [2][ntiles] heads, chunk starts per tile
+  unsigned* tile_off;             // [2][ntiles] exclusive offsets
   uint32_t* uniq;                 // [n] unique keys (first U valid)
   int* seg_start;                 // [n+1]
   int* seg_chunk;                 // [n+1] first chunk of each segment
   int* chunk_start;               // [n+1]
   int* chunk_seg;                 // [n]
-  int* counts;                    // device [2]: U, #chunks
+  int* counts;                    // device [4]: U, #chunks, #multi-chunk rows, (spare)
+  int* multi;                     // [n] rows spanning > 1 chunk (unordered)
   int* inv;                       // [n] occurrence -> segment (payload = occurrence)
   const int* ex_of_occ;           // [n] (payload = occurrence)
   int* sorted_ex;                 // [n] (payload = occurrence)
@@ -51,29 +50,138 @@ struct EmitArgs {
   float* sorted_x;                // [n] (payload = occurrence)
 };
 
-__global__ __launch_bounds__(kBlock) void rle_emit_kernel(EmitArgs a) {
-  for (int j = blockIdx.x * kBlock + threadIdx.x; j < a.n; j += gridDim.x * kBlock) {
-    const unsigned long long v = a.incl[j];
-    const unsigned long long vp = j > 0 ? a.incl[j - 1] : 0ull;
-    const int s = (int)(v >> 32) - 1;
-    const int c = (int)(v & 0xffffffffull) - 1;
-    const bool head = (v >> 32) != (vp >> 32);
-    const bool cstart = (v & 0xffffffffull) != (vp & 0xffffffffull);
-    if (head) {
+__device__ inline void rle_flags(const RleArgs& a, int j, bool& head, bool& cstart) {
+  head = (j == 0) || (a.skeys[j] != a.skeys[j - 1]);
+  cstart = head || (j % a.CH == 0);
+}
+
+// Block-wide exclusive scan of two per-thread counts (packed in one u32 pair).
+__device__ inline void block_excl_scan2(unsigned h, unsigned c, unsigned& h_ex, unsigned& c_ex, unsigned& h_tot,
+                                        unsigned& c_tot) {
+  __shared__ unsigned sh[2][kWavesPerBlock];
+  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x >> 6;
+  unsigned hi = h, ci = c;  // inclusive wave scan
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const unsigned hs = __shfl_up(hi, o, kWave), cs = __shfl_up(ci, o, kWave);
+    if (lane >= o) { hi += hs; ci += cs; }
+  }
+  if (lane == kWave - 1) { sh[0][wv] = hi; sh[1][wv] = ci; }
+  __syncthreads();
+  unsigned hb = 0, cb = 0;
+  h_tot = c_tot = 0;
+#pragma unroll
+  for (int w = 0; w < kWavesPerBlock; ++w) {
+    if (w < wv) { hb += sh[0][w]; cb += sh[1][w]; }
+    h_tot += sh[0][w];
+    c_tot += sh[1][w];
+  }
+  h_ex = hb + hi - h;
+  c_ex = cb + ci - c;
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kBlock) void rle_tile_count_kernel(RleArgs a) {
+  const int tile = blockIdx.x;
+  const int j0 = tile * kRleTile + threadIdx.x * kRleItems;
+  unsigned h = 0, c = 0;
+#pragma unroll
+  for (int q = 0; q < kRleItems; ++q) {
+    const int j = j0 + q;
+    if (j < a.n) {
+      bool hd, cs;
+      rle_flags(a, j, hd, cs);
+      h += hd;
+      c += cs;
+    }
+  }
+  unsigned he, ce, ht, ct;
+  block_excl_scan2(h, c, he, ce, ht, ct);
+  if (threadIdx.x == 0) {
+    a.tile_cnt[tile] = ht;
+    a.tile_cnt[a.ntiles + tile] = ct;
+  }
+}
+
+// One workgroup of 1024 threads: exclusive scan of the tile totals.
+__global__ __launch_bounds__(1024) void rle_tile_scan_kernel(RleArgs a) {
+  __shared__ unsigned carry[2];
+  __shared__ unsigned wsum[2][16];
+  if (threadIdx.x == 0) { carry[0] = 0; carry[1] = 0; }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int base = 0; base < a.ntiles; base += 1024) {
+    const int t = base + threadIdx.x;
+    const unsigned h = t < a.ntiles ? a.tile_cnt[t] : 0u;
+    const unsigned c = t < a.ntiles ? a.tile_cnt[a.ntiles + t] : 0u;
+    unsigned hi = h, ci = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned hs = __shfl_up(hi, o, 64), cs = __shfl_up(ci, o, 64);
+      if (lane >= o) { hi += hs; ci += cs; }
+    }
+    if (lane == 63) { wsum[0][wv] = hi; wsum[1][wv] = ci; }
+    __syncthreads();
+    unsigned hb = carry[0], cb = carry[1], ht = 0, ct = 0;
+    for (int w = 0; w < 16; ++w) {
+      if (w < wv) { hb += wsum[0][w]; cb += wsum[1][w]; }
+      ht += wsum[0][w];
+      ct += wsum[1][w];
+    }
+    if (t < a.ntiles) {
+      a.tile_off[t] = hb + hi - h;
+      a.tile_off[a.ntiles + t] = cb + ci - c;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) { carry[0] += ht; carry[1] += ct; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    a.counts[0] = (int)carry[0];
+    a.counts[1] = (int)carry[1];
+    a.seg_start[carry[0]] = a.n;
+    a.seg_chunk[carry[0]] = (int)carry[1];
+    a.chunk_start[carry[1]] = a.n;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void rle_tile_emit_kernel(RleArgs a) {
+  const int tile = blockIdx.x;
+  const int j0 = tile * kRleTile + threadIdx.x * kRleItems;
+  bool hd[kRleItems], cs[kRleItems];
+  unsigned h = 0, c = 0;
+#pragma unroll
+  for (int q = 0; q < kRleItems; ++q) {
+    const int j = j0 + q;
+    hd[q] = cs[q] = false;
+    if (j < a.n) rle_flags(a, j, hd[q], cs[q]);
+    h += hd[q];
+    c += cs[q];
+  }
+  unsigned he, ce, ht, ct;
+  block_excl_scan2(h, c, he, ce, ht, ct);
+  // running (inclusive) segment / chunk ids of this thread's elements
+  int s = (int)(a.tile_off[tile] + he) - 1;
+  int ch = (int)(a.tile_off[a.ntiles + tile] + ce) - 1;
+#pragma unroll
+  for (int q = 0; q < kRleItems; ++q) {
+    const int j = j0 + q;
+    if (j >= a.n) break;
+    s += hd[q];
+    ch += cs[q];
+    if (hd[q]) {
       a.uniq[s] = a.skeys[j];
       a.seg_start[s] = j;
-      a.seg_chunk[s] = c;
+      a.seg_chunk[s] = ch;
     }
-    if (cstart) {
-      a.chunk_start[c] = j;
-      a.chunk_seg[c] = s;
-    }
-    if (j == a.n - 1) {
-      a.counts[0] = s + 1;
-      a.counts[1] = c + 1;
-      a.seg_start[s + 1] = a.n;
-      a.seg_chunk[s + 1] = c + 1;
-      a.chunk_start[c + 1] = a.n;
+    if (cs[q]) {
+      a.chunk_start[ch] = j;
+      a.chunk_seg[ch] = s;
+      // a non-head chunk start j is the segment's SECOND chunk iff the head lies in [j - CH, j)
+      if (!hd[q]) {
+        const int prev = j - a.CH - 1;
+        if (prev < 0 || a.skeys[prev] != a.skeys[j]) a.multi[atomicAdd(&a.counts[2], 1)] = s;
+      }
     }
     if (a.inv || a.sorted_ex || a.sorted_x) {
       const int p = a.spay[j];
@@ -84,31 +192,58 @@ __global__ __launch_bounds__(kBlock) void rle_emit_kernel(EmitArgs a) {
   }
 }
 
-static int grid_for(long long n) {
-  long long b = (n + kBlock - 1) / kBlock;
-  if (b < 1) b = 1;
-  if (b > 4096) b = 4096;
-  return (int)b;
-}
-
 static size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
-using FlagIter = rocprim::transform_iterator<rocprim::counting_iterator<int>, FlagOp, unsigned long long>;
+// Onesweep configuration measured on MI355X for 5.1M (key, int32) pairs with
+// 27-bit keys (tools/bench_sort.hip, interleaved rounds): rocPRIM's default
+// 260 us; 1024x8 "match" ranking with 8-bit digits 203 us, 9-bit 150 us,
+// 10-bit 164 us, 11-bit 273 us.  The digit width is chosen so that the key bits
+// are covered in the fewest passes of 9-10 bits.
+template <unsigned BITS>
+using OnesweepCfg = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>, BITS,
+                                        rocprim::block_radix_rank_algorithm::match>,
+    0>;
 
-static size_t temp_bytes(int n, hipStream_t st) {
-  size_t sort_bytes = 0, scan_bytes = 0;
-  (void)rocprim::radix_sort_pairs((void*)nullptr, sort_bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                  (const int*)nullptr, (int*)nullptr, n, 0, 32, st);
-  FlagIter it(rocprim::counting_iterator<int>(0), FlagOp{nullptr, 1});
-  (void)rocprim::inclusive_scan((void*)nullptr, scan_bytes, it, (unsigned long long*)nullptr, (size_t)n,
-                                rocprim::plus<unsigned long long>(), st);
-  return align_up(sort_bytes > scan_bytes ? sort_bytes : scan_bytes);
+static int digit_bits(int key_bits) {
+  if (key_bits <= 18) return 9;   // 2 passes
+  if (key_bits <= 20) return 10;  // 2 passes
+  if (key_bits <= 27) return 9;   // 3 passes
+  if (key_bits <= 30) return 10;  // 3 passes
+  return 8;                       // 4 passes
 }
 
-// Workspace layout: [rocprim temp | u64 incl(n)]
+template <unsigned BITS>
+static hipError_t sort_pairs_bits(void* tmp, size_t& bytes, const uint32_t* k, uint32_t* ko, const int* v, int* vo,
+                                  int n, int end_bit, hipStream_t st) {
+  return rocprim::radix_sort_pairs<OnesweepCfg<BITS>>(tmp, bytes, k, ko, v, vo, n, 0, end_bit, st);
+}
+
+static hipError_t sort_pairs(void* tmp, size_t& bytes, const uint32_t* k, uint32_t* ko, const int* v, int* vo,
+                             int n, int end_bit, hipStream_t st) {
+  switch (digit_bits(end_bit)) {
+    case 10: return sort_pairs_bits<10>(tmp, bytes, k, ko, v, vo, n, end_bit, st);
+    case 8: return sort_pairs_bits<8>(tmp, bytes, k, ko, v, vo, n, end_bit, st);
+    default: return sort_pairs_bits<9>(tmp, bytes, k, ko, v, vo, n, end_bit, st);
+  }
+}
+
+static size_t sort_temp_bytes(int n, hipStream_t st) {
+  size_t best = 0;
+  for (int bits : {16, 20, 27, 30, 32}) {  // the largest requirement over all dispatch targets
+    size_t b = 0;
+    (void)sort_pairs(nullptr, b, nullptr, nullptr, nullptr, nullptr, n, bits, st);
+    if (b > best) best = b;
+  }
+  return align_up(best);
+}
+
+// Workspace layout: [rocprim sort temp | tile_cnt(2*ntiles) | tile_off(2*ntiles)]
 size_t dedup_workspace_bytes(int n) {
   if (n <= 0) return 256;
-  return temp_bytes(n, 0) + align_up(sizeof(unsigned long long) * (size_t)n) + 256;
+  const size_t ntiles = ((size_t)n + kRleTile - 1) / kRleTile;
+  return sort_temp_bytes(n, 0) + 2 * align_up(2 * ntiles * sizeof(unsigned)) + 256;
 }
 
 struct DedupArgs {
@@ -124,7 +259,8 @@ struct DedupArgs {
   int* seg_chunk;          // [n+1]
   int* chunk_start;        // [n+1]
   int* chunk_seg;          // [n]
-  int* counts;             // device [2]
+  int* counts;             // device [4]
+  int* multi;              // [n]
   int* inv;                // nullable
   const int* ex_of_occ;    // nullable
   int* sorted_ex;          // nullable
@@ -135,28 +271,29 @@ struct DedupArgs {
 };
 
 int launch_dedup(const DedupArgs& a, hipStream_t st) {
+  (void)hipMemsetAsync(a.counts, 0, 4 * sizeof(int), st);
   if (a.n <= 0) {
-    (void)hipMemsetAsync(a.counts, 0, 2 * sizeof(int), st);
     (void)hipMemsetAsync(a.seg_start, 0, sizeof(int), st);
     (void)hipMemsetAsync(a.seg_chunk, 0, sizeof(int), st);
     (void)hipMemsetAsync(a.chunk_start, 0, sizeof(int), st);
     return (int)hipGetLastError();
   }
-  const size_t tmp = temp_bytes(a.n, st);
-  auto* incl = reinterpret_cast<unsigned long long*>(static_cast<char*>(a.ws) + tmp);
-  if (tmp + sizeof(unsigned long long) * (size_t)a.n > a.ws_bytes) return -2;
+  const int ntiles = (a.n + kRleTile - 1) / kRleTile;
+  if (ntiles > kMaxTiles) return -3;
+  const size_t tmp = sort_temp_bytes(a.n, st);
+  char* base = static_cast<char*>(a.ws);
+  unsigned* tile_cnt = reinterpret_cast<unsigned*>(base + tmp);
+  unsigned* tile_off = reinterpret_cast<unsigned*>(base + tmp + align_up(2 * (size_t)ntiles * sizeof(unsigned)));
+  if (tmp + 2 * align_up(2 * (size_t)ntiles * sizeof(unsigned)) > a.ws_bytes) return -2;
 
   size_t sort_bytes = tmp;
-  hipError_t e = rocprim::radix_sort_pairs(a.ws, sort_bytes, a.keys, a.skeys, a.payload, a.spay, a.n, 0,
-                                           a.end_bit, st);
+  hipError_t e = sort_pairs(a.ws, sort_bytes, a.keys, a.skeys, a.payload, a.spay, a.n, a.end_bit, st);
   if (e != hipSuccess) return (int)e;
-  FlagIter it(rocprim::counting_iterator<int>(0), FlagOp{a.skeys, a.CH});
-  size_t scan_bytes = tmp;
-  e = rocprim::inclusive_scan(a.ws, scan_bytes, it, incl, (size_t)a.n, rocprim::plus<unsigned long long>(), st);
-  if (e != hipSuccess) return (int)e;
-  EmitArgs em{a.n, a.CH, a.skeys, a.spay, incl, a.uniq, a.seg_start, a.seg_chunk, a.chunk_start, a.chunk_seg,
-              a.counts, a.inv, a.ex_of_occ, a.sorted_ex, a.vals, a.sorted_x};
-  hipLaunchKernelGGL(rle_emit_kernel, dim3(grid_for(a.n)), dim3(kBlock), 0, st, em);
+  RleArgs r{a.n, a.CH, ntiles, a.skeys, a.spay, tile_cnt, tile_off, a.uniq, a.seg_start, a.seg_chunk,
+            a.chunk_start, a.chunk_seg, a.counts, a.multi, a.inv, a.ex_of_occ, a.sorted_ex, a.vals, a.sorted_x};
+  hipLaunchKernelGGL(rle_tile_count_kernel, dim3(ntiles), dim3(kBlock), 0, st, r);
+  hipLaunchKernelGGL(rle_tile_scan_kernel, dim3(1), dim3(1024), 0, st, r);
+  hipLaunchKernelGGL(rle_tile_emit_kernel, dim3(ntiles), dim3(kBlock), 0, st, r);
   return (int)hipGetLastError();
 }
 

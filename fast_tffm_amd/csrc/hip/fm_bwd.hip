@@ -59,6 +59,7 @@ struct BwdArgs {
   float* partial;           // [#chunks, Kp + 4]
   int* big_list;            // [U] rows for the workgroup combine
   int* big_count;           // device scalar, zeroed by the launcher
+  const int* multi;         // [counts[2]] rows spanning more than one chunk
 };
 
 // Parameter row + optimizer slots of one segment, read before its gradient is
@@ -249,12 +250,12 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_combine_kernel(BwdArgs a) {
   const int nv = a.Kp / EPL;
   const bool tact = t < nv;
   const int tE = tact ? t : nv - 1;
-  const int U = a.counts[0];
+  const int nmulti = a.counts[2];  // rows spanning > 1 chunk, listed by the dedup
   const int ngroups = gridDim.x * kWavesPerBlock * G;
-  for (int u = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g; u < U; u += ngroups) {
+  for (int i = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g; i < nmulti; i += ngroups) {
+    const int u = a.multi[i];
     const int c0 = a.seg_chunk[u], c1 = a.seg_chunk[u + 1];
     const int nc = c1 - c0;
-    if (nc <= 1) continue;
     if (nc > kSmallChunks) {
       if (t == 0) a.big_list[atomicAdd(a.big_count, 1)] = u;
       continue;

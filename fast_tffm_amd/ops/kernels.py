@@ -203,7 +203,7 @@ class DedupOut:
     """
 
     __slots__ = ("n", "skeys", "perm", "uniq", "seg_start", "seg_chunk", "chunk_start", "chunk_seg", "counts",
-                 "num_unique", "inv", "sorted_ex", "sorted_x", "U_host", "CH", "big_list", "big_count")
+                 "num_unique", "inv", "sorted_ex", "sorted_x", "U_host", "CH", "big_list", "big_count", "multi")
 
     def __init__(self, **kw):
         for k in self.__slots__:
@@ -233,7 +233,8 @@ class DedupWorkspace:
         self.seg_chunk = torch.empty(n1 + 1, **i32)
         self.chunk_start = torch.empty(n1 + 1, **i32)
         self.chunk_seg = torch.empty(n1, **i32)
-        self.counts = torch.zeros(2, **i32)
+        self.counts = torch.zeros(4, **i32)   # U, #chunks, #multi-chunk rows, spare
+        self.multi = torch.empty(n1, **i32)
         self.inv = torch.empty(n1, **i32)
         self.sorted_ex = torch.empty(n1, **i32)
         self.sorted_x = torch.empty(n1, dtype=torch.float32, device=device)
@@ -289,14 +290,15 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
                    num_unique=ws.counts[:1], inv=ws.inv if want_inv else None,
                    sorted_ex=(ws.perm if ex_payload else ws.sorted_ex) if ex_of_occ is not None else None,
                    sorted_x=ws.sorted_x if vals is not None else None, CH=CH, big_list=ws.big_list,
-                   big_count=ws.big_count)
+                   big_count=ws.big_count, multi=ws.multi)
     if _is_gpu(keys):
         h = native.hip()
         _check(1 <= CH <= h.MAX_CH, f"CH must be in [1, {h.MAX_CH}]")
         h.dedup(n=n, end_bit=key_bits, CH=CH, keys=_p(keys), payload=_p(ex_of_occ if ex_payload else ws.iota),
                 skeys=_p(ws.skeys), spay=_p(ws.perm), uniq=_p(ws.uniq), seg_start=_p(ws.seg_start),
                 seg_chunk=_p(ws.seg_chunk), chunk_start=_p(ws.chunk_start), chunk_seg=_p(ws.chunk_seg),
-                counts=_p(ws.counts), inv=_p(out.inv), ex_of_occ=0 if ex_payload else _p(ex_of_occ),
+                counts=_p(ws.counts), multi=_p(ws.multi), inv=_p(out.inv),
+                ex_of_occ=0 if ex_payload else _p(ex_of_occ),
                 sorted_ex=0 if ex_payload else _p(out.sorted_ex), vals=_p(vals), sorted_x=_p(out.sorted_x),
                 ws=_p(ws.ws), ws_bytes=ws.ws.numel(), stream=_stream(keys))
     else:
@@ -380,7 +382,8 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               s_stride=s_stride, s0w=_p(s0w), s1w=_p(s1w), reg_v=float(reg_v), reg_w=float(reg_w),
               opt_type=o.code, lr=float(o.lr), l1=float(o.l1), l2=float(o.l2), beta=float(o.beta),
               grad_out=gptr, g_stride=gstride, partial=_p(partial), big_list=_p(dd.big_list),
-              big_count=_p(dd.big_count), dtype=dt, max_chunks=dd.n, max_unique=dd.n, stream=_stream(dpred))
+              big_count=_p(dd.big_count), multi=_p(dd.multi), dtype=dt, max_chunks=dd.n, max_unique=dd.n,
+              stream=_stream(dpred))
     else:
         U = dd.sync()
         native.cpu().bwd(mode=mode, U=U, seg_start=_p(dd.seg_start), uniq=_p(dd.uniq), sorted_ex=_p(dd.sorted_ex),
