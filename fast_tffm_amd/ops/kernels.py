@@ -419,6 +419,18 @@ def gather_rows(req: torch.Tensor, table: TableState, Kp: int, out: torch.Tensor
     return out
 
 
+def owner_counts(dd: DedupOut, rows_per_shard: int, world: int) -> torch.Tensor:
+    """int64[world]: unique keys (owner * rows_per_shard + row) per owner, computed without a host sync."""
+    out = torch.empty(world, dtype=torch.int64, device=dd.uniq.device)
+    if dd.uniq.device.type == "cuda":
+        native.hip().owner_counts(uniq=_p(dd.uniq), num_unique=_p(dd.num_unique), Rps=int(rows_per_shard), W=world,
+                                  out=_p(out), stream=_stream(dd.uniq))
+    else:
+        owner = torch.div(dd.uniq[: dd.sync()].to(torch.int64), rows_per_shard, rounding_mode="floor")
+        out.copy_(torch.bincount(owner, minlength=world))
+    return out
+
+
 def apply_rows(dd: DedupOut, grad_in: torch.Tensor, table: TableState, opt: OptConfig, Kp: int,
                threads: int = 0) -> None:
     """Owner side of a sharded update: sum received grad rows per table row, then one optimizer step."""

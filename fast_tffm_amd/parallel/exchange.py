@@ -87,16 +87,17 @@ class ShardExchange(_Base):
         keys = self._keys(b)
         dd = K.dedup(keys, ws=ws.dd, key_bits=self.key_bits, ex_of_occ=ex, vals=b.vals if ex is not None else None,
                      want_inv=True)
-        U = dd.sync()
-        uniq = dd.uniq[:U].to(torch.int64)
-        owner = torch.div(uniq, self.Rps, rounding_mode="floor")
-        send_counts = torch.bincount(owner, minlength=self.W).to(torch.int64)
-        recv_counts = torch.empty_like(send_counts)
-        dist.all_to_all_single(recv_counts, send_counts, group=self.group)
-        sc = send_counts.tolist()
-        rc = recv_counts.tolist()
+        # per-owner counts on the device, one count all-to-all, ONE host sync for both split lists
+        counts = torch.empty(2 * self.W, dtype=torch.int64, device=self.dev)
+        counts[: self.W] = K.owner_counts(dd, self.Rps, self.W)
+        dist.all_to_all_single(counts[self.W:], counts[: self.W], group=self.group)
+        both = counts.tolist()
+        sc, rc = both[: self.W], both[self.W:]
+        U = int(sum(sc))
+        dd.U_host = U
         R = int(sum(rc))
-        req_send = (uniq - owner * self.Rps).to(torch.int32)
+        uniq = dd.uniq[:U]
+        req_send = torch.remainder(uniq, self.Rps)  # keys are owner * Rps + local row
         req_recv = torch.empty(R, dtype=torch.int32, device=self.dev)
         _a2a(req_recv, req_send, rc, sc, self.group)
         rows_send = torch.empty((R, self.gs), dtype=torch.float32, device=self.dev)
