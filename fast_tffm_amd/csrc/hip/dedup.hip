@@ -17,7 +17,9 @@
 //                       unique keys, segment starts, first chunk of each
 //                       segment, chunk starts, chunk->segment, the optional
 //                       inverse map / per-sorted-occurrence example index and
-//                       value, and the list of rows that span several chunks;
+//                       value, and (sliced schedule) per-slice chunk counts;
+//   3. (sliced schedule) scan of the per-(slice, tile) counts and a scatter of
+//      the chunk ids into per-example-slice lists for the backward.
 // Chunks cut every segment at CH-aligned sorted positions, so no chunk is
 // longer than CH and a hot id (tens of thousands of occurrences in Criteo's
 // low-cardinality fields) is spread over many lane groups in the backward.
@@ -29,20 +31,26 @@ namespace fm {
 constexpr int kRleItems = 8;                     // elements per thread
 constexpr int kRleTile = kBlock * kRleItems;     // 2048 elements per tile
 constexpr int kMaxTiles = 1024 * 64;             // single-workgroup tile scan limit (n < 134M)
+constexpr int kMaxSlices = 64;
 
 struct RleArgs {
   int n, CH, ntiles;
+  int slice_shift;                // example slice = ex >> slice_shift; < 0: no slicing
+  int nslices;                    // example slices (<= kMaxSlices)
+  int hot;                        // a row is "hot" at j when skeys[j -/+ hot] has its key (multiple of 8)
   const uint32_t* skeys;          // sorted keys
   const int* spay;                // sorted payload (occurrence or example index)
+  const int* sex;                 // sorted example index (== spay when the payload is the example), or null
   unsigned* tile_cnt;             // [2][ntiles] heads, chunk starts per tile
   unsigned* tile_off;             // [2][ntiles] exclusive offsets
+  unsigned* slice_cnt;            // [nslices][ntiles] chunks per (slice, tile)
   uint32_t* uniq;                 // [n] unique keys (first U valid)
   int* seg_start;                 // [n+1]
   int* seg_chunk;                 // [n+1] first chunk of each segment
   int* chunk_start;               // [n+1]
-  int* chunk_seg;                 // [n]
+  int* chunk_seg;                 // [n] segment id | kChunkFirst | kChunkSingle
+  int* chunk_key;                 // [n] key of the chunk's segment
   int* counts;                    // device [4]: U, #chunks, #multi-chunk rows, (spare)
-  int* multi;                     // [n] rows spanning > 1 chunk (unordered)
   int* inv;                       // [n] occurrence -> segment (payload = occurrence)
   const int* ex_of_occ;           // [n] (payload = occurrence)
   int* sorted_ex;                 // [n] (payload = occurrence)
@@ -50,9 +58,73 @@ struct RleArgs {
   float* sorted_x;                // [n] (payload = occurrence)
 };
 
-__device__ inline void rle_flags(const RleArgs& a, int j, bool& head, bool& cstart) {
-  head = (j == 0) || (a.skeys[j] != a.skeys[j - 1]);
-  cstart = head || (j % a.CH == 0);
+__device__ inline int sorted_example(const RleArgs& a, int j) {
+  return a.sex ? a.sex[j] : a.ex_of_occ[a.spay[j]];
+}
+
+// v[q] = p[j0 + q] (fill outside [0, n)); two 16-byte loads when in range (j0 % 8 == 0).
+template <typename T>
+__device__ inline void load8(const T* p, int j0, int n, T (&v)[8], T fill) {
+  if (j0 >= 0 && j0 + 8 <= n) {
+    const uint4 x = *reinterpret_cast<const uint4*>(p + j0);
+    const uint4 y = *reinterpret_cast<const uint4*>(p + j0 + 4);
+    v[0] = (T)x.x; v[1] = (T)x.y; v[2] = (T)x.z; v[3] = (T)x.w;
+    v[4] = (T)y.x; v[5] = (T)y.y; v[6] = (T)y.z; v[7] = (T)y.w;
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = (j0 + q >= 0 && j0 + q < n) ? p[j0 + q] : fill;
+  }
+}
+
+// Flags of one thread's 8 consecutive sorted positions j0..j0+7.
+//   head:   first occurrence of a key;
+//   cstart: chunk boundary = head, CH-aligned position, or -- for hot rows --
+//           a change of example slice (a hot row's occurrences are sorted by
+//           example, so each of its chunks reads r1 from one slice; see
+//           fm_bwd.hip, XCD-sliced schedule);
+//   slice:  (chunk starts) list the chunk goes to: its example slice for a
+//           hot row, chunk id mod nslices otherwise (no locality to exploit:
+//           spread evenly).
+struct Rle8 {
+  uint32_t k[8];
+  bool hd[8], cs[8], hot[8];
+  int ex[8];
+};
+
+__device__ inline void rle_flags8(const RleArgs& a, int j0, Rle8& r) {
+  constexpr uint32_t kNone = 0xffffffffu;  // keys are non-negative int32: never a key
+  load8(a.skeys, j0, a.n, r.k, kNone);
+  const uint32_t kp = (j0 > 0 && j0 <= a.n) ? a.skeys[j0 - 1] : kNone;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int j = j0 + q;
+    const bool ok = j < a.n;
+    r.hd[q] = ok && (j == 0 || r.k[q] != (q ? r.k[q - 1] : kp));
+    r.cs[q] = r.hd[q] || (ok && j % a.CH == 0);
+    r.hot[q] = false;
+    r.ex[q] = 0;
+  }
+  if (a.slice_shift < 0) return;
+  uint32_t kl[8], kr[8];
+  load8(a.skeys, j0 - a.hot, a.n, kl, kNone);
+  load8(a.skeys, j0 + a.hot, a.n, kr, kNone);
+  if (a.sex) {
+    load8(a.sex, j0, a.n, r.ex, 0);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) r.ex[q] = j0 + q < a.n ? sorted_example(a, j0 + q) : 0;
+  }
+  const int ep = (j0 > 0 && j0 <= a.n) ? sorted_example(a, j0 - 1) : 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    r.hot[q] = r.k[q] != kNone && (kl[q] == r.k[q] || kr[q] == r.k[q]);
+    if (r.hot[q] && !r.cs[q])  // not a head: j > 0
+      r.cs[q] = (r.ex[q] >> a.slice_shift) != ((q ? r.ex[q - 1] : ep) >> a.slice_shift);
+  }
+}
+
+__device__ inline int chunk_slice(const RleArgs& a, bool hot, int ex, int c) {
+  return hot ? min(ex >> a.slice_shift, a.nslices - 1) : c % a.nslices;
 }
 
 // Block-wide exclusive scan of two per-thread counts (packed in one u32 pair).
@@ -83,18 +155,11 @@ __device__ inline void block_excl_scan2(unsigned h, unsigned c, unsigned& h_ex, 
 
 __global__ __launch_bounds__(kBlock) void rle_tile_count_kernel(RleArgs a) {
   const int tile = blockIdx.x;
-  const int j0 = tile * kRleTile + threadIdx.x * kRleItems;
+  Rle8 r;
+  rle_flags8(a, tile * kRleTile + threadIdx.x * kRleItems, r);
   unsigned h = 0, c = 0;
 #pragma unroll
-  for (int q = 0; q < kRleItems; ++q) {
-    const int j = j0 + q;
-    if (j < a.n) {
-      bool hd, cs;
-      rle_flags(a, j, hd, cs);
-      h += hd;
-      c += cs;
-    }
-  }
+  for (int q = 0; q < kRleItems; ++q) { h += r.hd[q]; c += r.cs[q]; }
   unsigned he, ce, ht, ct;
   block_excl_scan2(h, c, he, ce, ht, ct);
   if (threadIdx.x == 0) {
@@ -146,20 +211,19 @@ __global__ __launch_bounds__(1024) void rle_tile_scan_kernel(RleArgs a) {
 }
 
 __global__ __launch_bounds__(kBlock) void rle_tile_emit_kernel(RleArgs a) {
+  __shared__ unsigned sc[kMaxSlices];
   const int tile = blockIdx.x;
   const int j0 = tile * kRleTile + threadIdx.x * kRleItems;
-  bool hd[kRleItems], cs[kRleItems];
+  const bool sliced = a.slice_shift >= 0;
+  if (sliced)
+    for (int sl = threadIdx.x; sl < kMaxSlices; sl += kBlock) sc[sl] = 0;
+  Rle8 r;
+  rle_flags8(a, j0, r);
   unsigned h = 0, c = 0;
 #pragma unroll
-  for (int q = 0; q < kRleItems; ++q) {
-    const int j = j0 + q;
-    hd[q] = cs[q] = false;
-    if (j < a.n) rle_flags(a, j, hd[q], cs[q]);
-    h += hd[q];
-    c += cs[q];
-  }
+  for (int q = 0; q < kRleItems; ++q) { h += r.hd[q]; c += r.cs[q]; }
   unsigned he, ce, ht, ct;
-  block_excl_scan2(h, c, he, ce, ht, ct);
+  block_excl_scan2(h, c, he, ce, ht, ct);  // (its barriers also order the sc[] reset)
   // running (inclusive) segment / chunk ids of this thread's elements
   int s = (int)(a.tile_off[tile] + he) - 1;
   int ch = (int)(a.tile_off[a.ntiles + tile] + ce) - 1;
@@ -167,21 +231,22 @@ __global__ __launch_bounds__(kBlock) void rle_tile_emit_kernel(RleArgs a) {
   for (int q = 0; q < kRleItems; ++q) {
     const int j = j0 + q;
     if (j >= a.n) break;
-    s += hd[q];
-    ch += cs[q];
-    if (hd[q]) {
-      a.uniq[s] = a.skeys[j];
+    s += r.hd[q];
+    ch += r.cs[q];
+    if (r.hd[q]) {
+      a.uniq[s] = r.k[q];
       a.seg_start[s] = j;
       a.seg_chunk[s] = ch;
     }
-    if (cs[q]) {
+    if (r.cs[q]) {
+      // a head chunk is the row's only one iff the row ends before the next CH-aligned cut
+      // (slice cuts only split rows longer than 8 CH)
+      const int b = (j / a.CH + 1) * a.CH;
+      const bool single = r.hd[q] && (b >= a.n || a.skeys[b] != r.k[q]);
       a.chunk_start[ch] = j;
-      a.chunk_seg[ch] = s;
-      // a non-head chunk start j is the segment's SECOND chunk iff the head lies in [j - CH, j)
-      if (!hd[q]) {
-        const int prev = j - a.CH - 1;
-        if (prev < 0 || a.skeys[prev] != a.skeys[j]) a.multi[atomicAdd(&a.counts[2], 1)] = s;
-      }
+      a.chunk_seg[ch] = (int)((unsigned)s | (r.hd[q] ? (unsigned)kChunkFirst : 0u) | (single ? kChunkSingle : 0u));
+      a.chunk_key[ch] = (int)r.k[q];
+      if (sliced) atomicAdd(&sc[chunk_slice(a, r.hot[q], r.ex[q], ch)], 1u);
     }
     if (a.inv || a.sorted_ex || a.sorted_x) {
       const int p = a.spay[j];
@@ -190,9 +255,49 @@ __global__ __launch_bounds__(kBlock) void rle_tile_emit_kernel(RleArgs a) {
       if (a.sorted_x) a.sorted_x[j] = a.vals[p];
     }
   }
+  if (sliced) {
+    __syncthreads();
+    for (int sl = threadIdx.x; sl < a.nslices; sl += kBlock) a.slice_cnt[sl * a.ntiles + tile] = sc[sl];
+  }
 }
 
 static size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+
+// ---------------------------------------------------------------------------
+// Per-slice chunk lists for the XCD-sliced backward schedule.  The emit kernel
+// counted the chunks of every (slice, RLE tile); after an exclusive scan of
+// those counts (slice-major) each tile scatters its chunk ids into the lists.
+// Order inside a list is irrelevant to the results.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void slice_scatter_kernel(RleArgs a, const unsigned* off, int* list,
+                                                               int* slice_start) {
+  __shared__ unsigned cur[kMaxSlices];
+  for (int s = threadIdx.x; s < kMaxSlices; s += kBlock) cur[s] = 0;
+  __syncthreads();
+  const int tile = blockIdx.x;
+  const int C = a.counts[1];
+  const int c0 = (int)a.tile_off[a.ntiles + tile];
+  const int c1 = tile + 1 < a.ntiles ? (int)a.tile_off[a.ntiles + tile + 1] : C;
+  for (int c = c0 + threadIdx.x; c < c1; c += kBlock) {
+    const int j = a.chunk_start[c];
+    const uint32_t k = a.skeys[j];
+    const bool hot = (j >= a.hot && a.skeys[j - a.hot] == k) || (j + a.hot < a.n && a.skeys[j + a.hot] == k);
+    const int s = chunk_slice(a, hot, hot ? sorted_example(a, j) : 0, c);
+    list[off[s * a.ntiles + tile] + atomicAdd(&cur[s], 1u)] = c;
+  }
+  if (tile == 0) {
+    for (int s = threadIdx.x; s < a.nslices; s += kBlock) slice_start[s] = (int)off[s * a.ntiles];
+    if (threadIdx.x == 0) slice_start[a.nslices] = C;
+  }
+}
+
+static size_t slice_scan_bytes(int n) {
+  const size_t m = (size_t)kMaxSlices * (((size_t)n + kRleTile - 1) / kRleTile);
+  size_t b = 0;
+  (void)rocprim::exclusive_scan((void*)nullptr, b, (const unsigned*)nullptr, (unsigned*)nullptr, 0u, m,
+                                rocprim::plus<unsigned>(), 0);
+  return align_up(b) + 2 * align_up(m * sizeof(unsigned));
+}
 
 // Onesweep configuration measured on MI355X for 5.1M (key, int32) pairs with
 // 27-bit keys (tools/bench_sort.hip, interleaved rounds): rocPRIM's default
@@ -239,11 +344,11 @@ static size_t sort_temp_bytes(int n, hipStream_t st) {
   return align_up(best);
 }
 
-// Workspace layout: [rocprim sort temp | tile_cnt(2*ntiles) | tile_off(2*ntiles)]
+// Workspace layout: [rocprim sort temp | tile_cnt(2*ntiles) | tile_off(2*ntiles) | slice scan temp | cnt | off]
 size_t dedup_workspace_bytes(int n) {
   if (n <= 0) return 256;
   const size_t ntiles = ((size_t)n + kRleTile - 1) / kRleTile;
-  return sort_temp_bytes(n, 0) + 2 * align_up(2 * ntiles * sizeof(unsigned)) + 256;
+  return sort_temp_bytes(n, 0) + 2 * align_up(2 * ntiles * sizeof(unsigned)) + slice_scan_bytes(n) + 256;
 }
 
 struct DedupArgs {
@@ -259,13 +364,18 @@ struct DedupArgs {
   int* seg_chunk;          // [n+1]
   int* chunk_start;        // [n+1]
   int* chunk_seg;          // [n]
+  int* chunk_key;          // [n]
   int* counts;             // device [4]
-  int* multi;              // [n]
   int* inv;                // nullable
   const int* ex_of_occ;    // nullable
   int* sorted_ex;          // nullable
   const float* vals;       // nullable
   float* sorted_x;         // nullable
+  int payload_is_ex;       // payload carries the example index (sorted payload == sorted example)
+  int slice_shift;         // < 0: no slicing; else example slice = ex >> slice_shift
+  int nslices;             // slices (<= kMaxSlices)
+  int* slice_list;         // [n] chunk ids grouped by slice
+  int* slice_start;        // [nslices + 1]
   void* ws;
   size_t ws_bytes;
 };
@@ -284,16 +394,36 @@ int launch_dedup(const DedupArgs& a, hipStream_t st) {
   char* base = static_cast<char*>(a.ws);
   unsigned* tile_cnt = reinterpret_cast<unsigned*>(base + tmp);
   unsigned* tile_off = reinterpret_cast<unsigned*>(base + tmp + align_up(2 * (size_t)ntiles * sizeof(unsigned)));
-  if (tmp + 2 * align_up(2 * (size_t)ntiles * sizeof(unsigned)) > a.ws_bytes) return -2;
+  if (tmp + 2 * align_up(2 * (size_t)ntiles * sizeof(unsigned)) + slice_scan_bytes(a.n) > a.ws_bytes) return -2;
 
   size_t sort_bytes = tmp;
   hipError_t e = sort_pairs(a.ws, sort_bytes, a.keys, a.skeys, a.payload, a.spay, a.n, a.end_bit, st);
   if (e != hipSuccess) return (int)e;
-  RleArgs r{a.n, a.CH, ntiles, a.skeys, a.spay, tile_cnt, tile_off, a.uniq, a.seg_start, a.seg_chunk,
-            a.chunk_start, a.chunk_seg, a.counts, a.multi, a.inv, a.ex_of_occ, a.sorted_ex, a.vals, a.sorted_x};
+  const bool sliced = a.slice_shift >= 0 && a.nslices > 0 && a.nslices <= kMaxSlices && a.slice_list;
+  // slice scan scratch: [rocprim temp | cnt | off], m = nslices * ntiles
+  const size_t m = (size_t)kMaxSlices * (size_t)ntiles;
+  char* sbase = base + tmp + 2 * align_up(2 * (size_t)ntiles * sizeof(unsigned));
+  const size_t scan_cap = slice_scan_bytes(a.n) - 2 * align_up(m * sizeof(unsigned));
+  unsigned* cnt = reinterpret_cast<unsigned*>(sbase + scan_cap);
+  unsigned* off = reinterpret_cast<unsigned*>(sbase + scan_cap + align_up(m * sizeof(unsigned)));
+  RleArgs r{a.n, a.CH, ntiles, sliced ? a.slice_shift : -1, sliced ? a.nslices : 0, 8 * a.CH, a.skeys, a.spay,
+            a.payload_is_ex ? a.spay : nullptr, tile_cnt, tile_off, cnt, a.uniq, a.seg_start, a.seg_chunk,
+            a.chunk_start, a.chunk_seg, a.chunk_key, a.counts, a.inv, a.ex_of_occ, a.sorted_ex, a.vals, a.sorted_x};
   hipLaunchKernelGGL(rle_tile_count_kernel, dim3(ntiles), dim3(kBlock), 0, st, r);
   hipLaunchKernelGGL(rle_tile_scan_kernel, dim3(1), dim3(1024), 0, st, r);
   hipLaunchKernelGGL(rle_tile_emit_kernel, dim3(ntiles), dim3(kBlock), 0, st, r);
+  if (!sliced) return (int)hipGetLastError();
+
+  // per-slice chunk lists
+  const size_t ms = (size_t)a.nslices * ntiles;
+  size_t scan_bytes = 0;
+  (void)rocprim::exclusive_scan((void*)nullptr, scan_bytes, (const unsigned*)nullptr, (unsigned*)nullptr, 0u, ms,
+                                rocprim::plus<unsigned>(), st);
+  if (scan_bytes > scan_cap) return -4;
+  e = rocprim::exclusive_scan(sbase, scan_bytes, cnt, off, 0u, ms, rocprim::plus<unsigned>(), st);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(slice_scatter_kernel, dim3(ntiles), dim3(kBlock), 0, st, r, off, a.slice_list,
+                     a.slice_start);
   return (int)hipGetLastError();
 }
 

@@ -34,7 +34,8 @@ struct BwdArgs {
   int mode;                 // BwdMode
   const int* counts;        // device [2]: U, #chunks
   const int* chunk_start;   // [#chunks+1] into the sorted occurrence arrays
-  const int* chunk_seg;     // [#chunks] -> segment (row) id
+  const int* chunk_seg;     // [#chunks] segment (row) id | kChunkFirst | kChunkSingle
+  const int* chunk_key;     // [#chunks] key (= table row in LOCAL mode) of the chunk's segment
   const int* seg_start;     // [U+1]
   const int* seg_chunk;     // [U+1] first chunk of each segment
   const int* uniq;          // [U] table row of each segment (LOCAL)
@@ -59,7 +60,11 @@ struct BwdArgs {
   float* partial;           // [#chunks, Kp + 4]
   int* big_list;            // [U] rows for the workgroup combine
   int* big_count;           // device scalar, zeroed by the launcher
-  const int* multi;         // [counts[2]] rows spanning more than one chunk
+  int* multi;               // [counts[2]] rows spanning more than one chunk (filled by the chunk kernel)
+  int* counts_rw;           // == counts, writable (counts[2] = #multi, zeroed by the launcher)
+  const int* slice_list;    // chunk ids grouped by example slice, or null
+  const int* slice_start;   // [nslices + 1]
+  int nslices;
 };
 
 // Parameter row + optimizer slots of one segment, read before its gradient is
@@ -71,10 +76,11 @@ struct RowState {
   float wv, q0, q1;
 };
 
+// row: the table row (LOCAL) or the gathered row u (EMIT).
 template <typename TV, int EPL>
-__device__ inline void bwd_load_row(const BwdArgs& a, int u, int tE, RowState<EPL>& r) {
+__device__ inline void bwd_load_row(const BwdArgs& a, long long row, int tE, RowState<EPL>& r) {
   using F = Frag<TV>;
-  r.row = (a.mode == kBwdLocal) ? (long long)a.uniq[u] : (long long)u;
+  r.row = row;
   F::load(reinterpret_cast<const TV*>(a.v) + r.row * a.v_stride + tE * EPL, r.vv);
   r.wv = a.w[r.row * a.w_stride];
   if (a.mode == kBwdEmit) return;
@@ -146,7 +152,7 @@ template <typename TV, int EPL>
 __device__ inline void bwd_finalize(const BwdArgs& a, int u, int t, bool tact, int tE,
                                     const float (&A)[EPL], float Scx, float Sc, int n_u) {
   RowState<EPL> r;
-  bwd_load_row<TV, EPL>(a, u, tE, r);
+  bwd_load_row<TV, EPL>(a, a.mode == kBwdLocal ? (long long)a.uniq[u] : (long long)u, tE, r);
   bwd_finish<TV, EPL>(a, u, t, tact, r, A, Scx, Sc, n_u);
 }
 
@@ -164,17 +170,41 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_chunk_kernel(BwdArgs a) {
   const bool tact = t < nv;
   const int tE = tact ? t : nv - 1;
   const int nchunks = a.counts[1];
-  const int ngroups = gridDim.x * kWavesPerBlock * G;
-  const int wave_group0 = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G;
-  for (int cbase = wave_group0; cbase < nchunks; cbase += ngroups) {
-    const int c = cbase + g;
-    if (c >= nchunks) continue;
-    const int u = a.chunk_seg[c];
-    const int j0 = a.chunk_start[c], j1 = a.chunk_start[c + 1];
+  // XCD-sliced schedule: workgroups b = x (mod 8) share an XCD under the observed
+  // round-robin dispatch (speed only, never correctness) and walk the chunk lists
+  // of example slices x, x+8, ... in order, so the r1 rows they gather stay in
+  // that XCD's L2.  Unsliced: one linear walk over all chunks.
+  const int nslc = a.slice_list ? a.nslices : 0;
+  const int nx = nslc ? 8 : 1;
+  const int wave_in_x = (blockIdx.x / nx) * kWavesPerBlock + (threadIdx.x >> 6);
+  const int stride = (gridDim.x / nx) * kWavesPerBlock * G;
+  for (int s = nslc ? (int)(blockIdx.x % nx) : 0; s < (nslc ? nslc : 1); s += nx) {
+  const int i0 = nslc ? a.slice_start[s] : 0;
+  const int i1 = nslc ? a.slice_start[s + 1] : nchunks;
+  // Software pipeline over this lane group's chunks: the descriptor of the next
+  // chunk (and the list entry of the one after) load while the current one is
+  // reduced, so the dependent metadata chain is off the critical path.
+  int ii = i0 + wave_in_x * G + g;
+  auto chunk_at = [&](int i) { return nslc ? a.slice_list[i] : i; };
+  int c = ii < i1 ? chunk_at(ii) : 0;
+  int cn = ii + stride < i1 ? chunk_at(ii + stride) : 0;
+  int d_j0 = 0, d_j1 = 0, d_seg = 0, d_key = 0;
+  if (ii < i1) {
+    d_j0 = a.chunk_start[c]; d_j1 = a.chunk_start[c + 1]; d_seg = a.chunk_seg[c]; d_key = a.chunk_key[c];
+  }
+  for (; ii < i1; ii += stride) {
+    const int cc = c, j0 = d_j0, j1 = d_j1, key = d_key;
+    const int u = d_seg & kChunkSegMask;
+    const bool single = (unsigned)d_seg & kChunkSingle;
+    const bool first = d_seg & kChunkFirst;
+    if (ii + stride < i1) {
+      c = cn;
+      d_j0 = a.chunk_start[c]; d_j1 = a.chunk_start[c + 1]; d_seg = a.chunk_seg[c]; d_key = a.chunk_key[c];
+      cn = ii + 2 * stride < i1 ? chunk_at(ii + 2 * stride) : 0;
+    }
     const int len = j1 - j0;
-    const bool single = a.seg_chunk[u + 1] - a.seg_chunk[u] == 1;
     RowState<EPL> rs;
-    if (single) bwd_load_row<TV, EPL>(a, u, tE, rs);  // overlaps the r1 reduction below
+    if (single) bwd_load_row<TV, EPL>(a, a.mode == kBwdLocal ? (long long)key : (long long)u, tE, rs);
     // lane-parallel prefetch of the chunk's (example, dpred*x, x)
     int pex[PF];
     float pc[PF], px[PF];
@@ -228,14 +258,20 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_chunk_kernel(BwdArgs a) {
     if (single) {
       bwd_finish<TV, EPL>(a, u, t, tact, rs, A, Scx, Sc, len);
     } else {
-      float* dst = a.partial + (long long)c * (a.Kp + 4);
+      float* dst = a.partial + (long long)cc * (a.Kp + 4);
       if (tact) {
 #pragma unroll
         for (int k = 0; k < EPL; k += 4)
           *reinterpret_cast<float4*>(dst + t * EPL + k) = make_float4(A[k], A[k + 1], A[k + 2], A[k + 3]);
       }
-      if (t == 0) { dst[a.Kp] = Scx; dst[a.Kp + 1] = Sc; }
+      if (t == 0) {
+        dst[a.Kp] = Scx;
+        dst[a.Kp + 1] = Sc;
+        // the row's first chunk registers the row for the combine kernels
+        if (first) a.multi[atomicAdd(&a.counts_rw[2], 1)] = u;
+      }
     }
+  }
   }
 }
 
@@ -250,7 +286,7 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_combine_kernel(BwdArgs a) {
   const int nv = a.Kp / EPL;
   const bool tact = t < nv;
   const int tE = tact ? t : nv - 1;
-  const int nmulti = a.counts[2];  // rows spanning > 1 chunk, listed by the dedup
+  const int nmulti = a.counts[2];  // rows spanning > 1 chunk, listed by the chunk kernel
   const int ngroups = gridDim.x * kWavesPerBlock * G;
   for (int i = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g; i < nmulti; i += ngroups) {
     const int u = a.multi[i];
@@ -371,7 +407,8 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   const int lpr = lanes_per_row(a.Kp, dtype);
   const int G = kWave / lpr;
   (void)hipMemsetAsync(a.big_count, 0, sizeof(int), st);
-  const int g1 = fill_grid(max_chunks, kWavesPerBlock * G);
+  (void)hipMemsetAsync(a.counts_rw + 2, 0, sizeof(int), st);  // #multi-chunk rows, appended by the chunk kernel
+  const int g1 = (fill_grid(max_chunks, kWavesPerBlock * G) + 7) / 8 * 8;  // multiple of 8: XCD groups
   FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, a);
   const int g2 = fill_grid(max_unique, kWavesPerBlock * G, 2048);
   FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, a);

@@ -73,15 +73,16 @@ PYBIND11_MODULE(_fm_hip, m) {
 
   m.def(
       "bwd",
-      [](int mode, u64 counts, u64 chunk_start, u64 chunk_seg, u64 seg_start, u64 seg_chunk, u64 uniq,
+      [](int mode, u64 counts, u64 chunk_start, u64 chunk_seg, u64 chunk_key, u64 seg_start, u64 seg_chunk, u64 uniq,
          u64 sorted_ex, u64 sorted_x, u64 dpred, u64 r1, int Kp, u64 v, long long v_stride, u64 w,
          long long w_stride, u64 s0v, u64 s1v, long long s_stride, u64 s0w, u64 s1w, float reg_v, float reg_w,
          int opt_type, float lr, float l1, float l2, float beta, u64 grad_out, long long g_stride, u64 partial,
-         u64 big_list, u64 big_count, u64 multi, int dtype, long long max_chunks, long long max_unique,
-         u64 stream) {
+         u64 big_list, u64 big_count, u64 multi, u64 slice_list, u64 slice_start, int nslices, int dtype,
+         long long max_chunks, long long max_unique, u64 stream) {
         fm::BwdArgs a;
         a.mode = mode; a.counts = P<const int>(counts); a.chunk_start = P<const int>(chunk_start);
-        a.chunk_seg = P<const int>(chunk_seg); a.seg_start = P<const int>(seg_start);
+        a.chunk_seg = P<const int>(chunk_seg); a.chunk_key = P<const int>(chunk_key);
+        a.seg_start = P<const int>(seg_start);
         a.seg_chunk = P<const int>(seg_chunk); a.uniq = P<const int>(uniq);
         a.sorted_ex = P<const int>(sorted_ex); a.sorted_x = P<const float>(sorted_x);
         a.dpred = P<const float>(dpred); a.r1 = P<const float>(r1); a.Kp = Kp;
@@ -90,41 +91,50 @@ PYBIND11_MODULE(_fm_hip, m) {
         a.s1w = P<float>(s1w); a.reg_v = reg_v; a.reg_w = reg_w;
         a.opt = opt_params(opt_type, lr, l1, l2, beta);
         a.grad_out = P<float>(grad_out); a.g_stride = g_stride; a.partial = P<float>(partial);
-        a.big_list = P<int>(big_list); a.big_count = P<int>(big_count); a.multi = P<const int>(multi);
+        a.big_list = P<int>(big_list); a.big_count = P<int>(big_count); a.multi = P<int>(multi);
+        a.counts_rw = P<int>(counts); a.slice_list = P<const int>(slice_list);
+        a.slice_start = P<const int>(slice_start); a.nslices = nslices;
         check(fm::launch_bwd(a, dtype, max_chunks, max_unique, S(stream)), "fm_bwd");
       },
-      py::arg("mode"), py::arg("counts"), py::arg("chunk_start"), py::arg("chunk_seg"), py::arg("seg_start"),
+      py::arg("mode"), py::arg("counts"), py::arg("chunk_start"), py::arg("chunk_seg"), py::arg("chunk_key"),
+      py::arg("seg_start"),
       py::arg("seg_chunk"), py::arg("uniq"), py::arg("sorted_ex"), py::arg("sorted_x"), py::arg("dpred"),
       py::arg("r1"), py::arg("Kp"), py::arg("v"), py::arg("v_stride"), py::arg("w"), py::arg("w_stride"),
       py::arg("s0v"), py::arg("s1v"), py::arg("s_stride"), py::arg("s0w"), py::arg("s1w"), py::arg("reg_v"),
       py::arg("reg_w"), py::arg("opt_type"), py::arg("lr"), py::arg("l1"), py::arg("l2"), py::arg("beta"),
       py::arg("grad_out"), py::arg("g_stride"), py::arg("partial"), py::arg("big_list"), py::arg("big_count"),
-      py::arg("multi"), py::arg("dtype"), py::arg("max_chunks"), py::arg("max_unique"), py::arg("stream"));
+      py::arg("multi"), py::arg("slice_list"), py::arg("slice_start"), py::arg("nslices"), py::arg("dtype"),
+      py::arg("max_chunks"), py::arg("max_unique"), py::arg("stream"));
 
   m.def("dedup_workspace_bytes", &fm::dedup_workspace_bytes, py::arg("n"));
 
   m.def(
       "dedup",
       [](int n, int end_bit, int CH, u64 keys, u64 payload, u64 skeys, u64 spay, u64 uniq, u64 seg_start,
-         u64 seg_chunk, u64 chunk_start, u64 chunk_seg, u64 counts, u64 multi, u64 inv, u64 ex_of_occ,
-         u64 sorted_ex, u64 vals, u64 sorted_x, u64 ws, size_t ws_bytes, u64 stream) {
+         u64 seg_chunk, u64 chunk_start, u64 chunk_seg, u64 chunk_key, u64 counts, u64 inv, u64 ex_of_occ,
+         u64 sorted_ex, u64 vals, u64 sorted_x, int payload_is_ex, int slice_shift, int nslices, u64 slice_list,
+         u64 slice_start, u64 ws, size_t ws_bytes, u64 stream) {
         if (CH < 1 || CH > fm::kMaxCH) throw std::invalid_argument("CH must be in [1, MAX_CH]");
         fm::DedupArgs a;
         a.n = n; a.end_bit = end_bit; a.CH = CH; a.keys = P<const uint32_t>(keys);
         a.payload = P<const int>(payload); a.skeys = P<uint32_t>(skeys); a.spay = P<int>(spay);
         a.uniq = P<uint32_t>(uniq); a.seg_start = P<int>(seg_start); a.seg_chunk = P<int>(seg_chunk);
         a.chunk_start = P<int>(chunk_start); a.chunk_seg = P<int>(chunk_seg); a.counts = P<int>(counts);
-        a.multi = P<int>(multi);
+        a.chunk_key = P<int>(chunk_key);
         a.inv = P<int>(inv); a.ex_of_occ = P<const int>(ex_of_occ); a.sorted_ex = P<int>(sorted_ex);
         a.vals = P<const float>(vals); a.sorted_x = P<float>(sorted_x); a.ws = P<void>(ws);
+        a.payload_is_ex = payload_is_ex; a.slice_shift = slice_shift; a.nslices = nslices;
+        a.slice_list = P<int>(slice_list); a.slice_start = P<int>(slice_start);
         a.ws_bytes = ws_bytes;
         check(fm::launch_dedup(a, S(stream)), "dedup");
       },
       py::arg("n"), py::arg("end_bit"), py::arg("CH"), py::arg("keys"), py::arg("payload"), py::arg("skeys"),
       py::arg("spay"), py::arg("uniq"), py::arg("seg_start"), py::arg("seg_chunk"), py::arg("chunk_start"),
-      py::arg("chunk_seg"), py::arg("counts"), py::arg("multi"), py::arg("inv"), py::arg("ex_of_occ"),
+      py::arg("chunk_seg"), py::arg("chunk_key"), py::arg("counts"), py::arg("inv"), py::arg("ex_of_occ"),
       py::arg("sorted_ex"),
-      py::arg("vals"), py::arg("sorted_x"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"));
+      py::arg("vals"), py::arg("sorted_x"), py::arg("payload_is_ex"), py::arg("slice_shift"), py::arg("nslices"),
+      py::arg("slice_list"), py::arg("slice_start"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"));
+  m.attr("MAX_SLICES") = fm::kMaxSlices;
 
   m.def(
       "gather_rows",

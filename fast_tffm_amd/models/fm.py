@@ -231,7 +231,8 @@ class FactorizationMachine:
             side.wait_stream(main)  # inputs ready; previous step's readers of ws.dd are enqueued before
             with torch.cuda.stream(side):
                 ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz)
-                dd = K.dedup(rows, ws=ws.dd, key_bits=bits_for(self.table.rows), ex_of_occ=ex, vals=b.vals)
+                dd = K.dedup(rows, ws=ws.dd, key_bits=bits_for(self.table.rows), ex_of_occ=ex, vals=b.vals,
+                             num_examples=b.B, Kp=self.Kp)
         else:
             ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz)
         fo = K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,

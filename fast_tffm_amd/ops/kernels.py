@@ -202,8 +202,9 @@ class DedupOut:
     the dedup ran with the example index as payload (then ``sorted_ex is perm``).
     """
 
-    __slots__ = ("n", "skeys", "perm", "uniq", "seg_start", "seg_chunk", "chunk_start", "chunk_seg", "counts",
-                 "num_unique", "inv", "sorted_ex", "sorted_x", "U_host", "CH", "big_list", "big_count", "multi")
+    __slots__ = ("n", "skeys", "perm", "uniq", "seg_start", "seg_chunk", "chunk_start", "chunk_seg", "chunk_key", "counts",
+                 "num_unique", "inv", "sorted_ex", "sorted_x", "U_host", "CH", "big_list", "big_count", "multi",
+                 "slice_list", "slice_start", "nslices")
 
     def __init__(self, **kw):
         for k in self.__slots__:
@@ -232,7 +233,8 @@ class DedupWorkspace:
         self.seg_start = torch.empty(n1 + 1, **i32)
         self.seg_chunk = torch.empty(n1 + 1, **i32)
         self.chunk_start = torch.empty(n1 + 1, **i32)
-        self.chunk_seg = torch.empty(n1, **i32)
+        self.chunk_seg = torch.empty(n1, **i32)   # segment id | first (bit 30) | single (bit 31)
+        self.chunk_key = torch.empty(n1, **i32)
         self.counts = torch.zeros(4, **i32)   # U, #chunks, #multi-chunk rows, spare
         self.multi = torch.empty(n1, **i32)
         self.inv = torch.empty(n1, **i32)
@@ -241,6 +243,8 @@ class DedupWorkspace:
         self.ex_of_occ = torch.empty(n1, **i32)
         self.big_list = torch.empty(n1, **i32)
         self.big_count = torch.zeros(1, **i32)
+        self.slice_list = torch.empty(n1, **i32)
+        self.slice_start = torch.empty(MAX_SLICES + 1, **i32)
         if device.type == "cuda":
             nbytes = native.hip().dedup_workspace_bytes(n1)
             self.ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
@@ -262,14 +266,41 @@ def csr_rows(offsets: torch.Tensor, out: torch.Tensor | None = None, nnz: int | 
     return out
 
 
+MAX_SLICES = 64            # = fm::kMaxSlices (dedup.hip)
+SLICE_BYTES = 2 << 20      # r1 bytes per example slice of the XCD-sliced backward (XCD L2 = 4 MB)
+
+
+def slice_plan(num_examples: int, Kp: int) -> tuple[int, int]:
+    """(slice_shift, nslices) of the XCD-sliced backward schedule, or (-1, 0) when not worth it.
+
+    Example slice = ex >> slice_shift.  The backward's chunks are listed per
+    slice and workgroup b walks the lists of slices b%8, b%8+8, ...: the r1
+    rows (Kp fp32 per example) a slice's chunks gather stay in one XCD's L2.
+    """
+    row = Kp * 4
+    # measured on MI355X (B=131072, K=64, profiles/README.md): sliced 0.782 ms/step vs
+    # linear 0.726 -- the L2 hit rate of the chunk kernel rises 34% -> 48% but the list
+    # indirection and the extra hot-row chunks cost more; opt-in via FM_BWD_SLICES=1
+    if os.environ.get("FM_BWD_SLICES", "0") != "1" or num_examples * row <= 8 * SLICE_BYTES:
+        return -1, 0
+    shift = max(0, (SLICE_BYTES // row).bit_length() - 1)
+    while shift > 0 and -(-num_examples >> shift) < 8:
+        shift -= 1
+    while -(-num_examples >> shift) > MAX_SLICES:
+        shift += 1
+    return shift, -(-num_examples >> shift)
+
+
 def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int = 32,
           ex_of_occ: torch.Tensor | None = None, vals: torch.Tensor | None = None, want_inv: bool = False,
-          CH: int | None = None, want_perm: bool = False) -> DedupOut:
+          CH: int | None = None, want_perm: bool = False, num_examples: int | None = None,
+          Kp: int | None = None) -> DedupOut:
     """Sort-based unique over non-negative int32 keys (reference tf.unique, fm_model.py:72).
 
     Unique keys come out in ascending order (the reference's first-occurrence
     order is an implementation detail no result depends on).  On the GPU the
-    result also carries the backward's chunk plan.  When neither the inverse
+    result also carries the backward's chunk plan (per example slice when
+    ``num_examples`` and ``Kp`` are given, see ``slice_plan``).  When neither the inverse
     map, per-occurrence values nor the occurrence permutation are needed, the
     sort carries the example index directly (one gather pass less).
     """
@@ -285,22 +316,29 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
         _chk_vec(vals, torch.float32, n, "vals", dev)
     key_bits = max(1, min(32, int(key_bits)))
     ex_payload = ex_of_occ is not None and vals is None and not want_inv and not want_perm and _is_gpu(keys)
+    shift, nsl = -1, 0
+    if ex_of_occ is not None and num_examples and Kp and _is_gpu(keys):
+        shift, nsl = slice_plan(int(num_examples), int(Kp))
     out = DedupOut(n=n, skeys=ws.skeys, perm=ws.perm, uniq=ws.uniq, seg_start=ws.seg_start,
-                   seg_chunk=ws.seg_chunk, chunk_start=ws.chunk_start, chunk_seg=ws.chunk_seg, counts=ws.counts,
+                   seg_chunk=ws.seg_chunk, chunk_start=ws.chunk_start, chunk_seg=ws.chunk_seg,
+                   chunk_key=ws.chunk_key, counts=ws.counts,
                    num_unique=ws.counts[:1], inv=ws.inv if want_inv else None,
                    sorted_ex=(ws.perm if ex_payload else ws.sorted_ex) if ex_of_occ is not None else None,
                    sorted_x=ws.sorted_x if vals is not None else None, CH=CH, big_list=ws.big_list,
-                   big_count=ws.big_count, multi=ws.multi)
+                   big_count=ws.big_count, multi=ws.multi, slice_list=ws.slice_list if nsl else None,
+                   slice_start=ws.slice_start, nslices=nsl)
     if _is_gpu(keys):
         h = native.hip()
         _check(1 <= CH <= h.MAX_CH, f"CH must be in [1, {h.MAX_CH}]")
         h.dedup(n=n, end_bit=key_bits, CH=CH, keys=_p(keys), payload=_p(ex_of_occ if ex_payload else ws.iota),
                 skeys=_p(ws.skeys), spay=_p(ws.perm), uniq=_p(ws.uniq), seg_start=_p(ws.seg_start),
                 seg_chunk=_p(ws.seg_chunk), chunk_start=_p(ws.chunk_start), chunk_seg=_p(ws.chunk_seg),
-                counts=_p(ws.counts), multi=_p(ws.multi), inv=_p(out.inv),
+                chunk_key=_p(ws.chunk_key),
+                counts=_p(ws.counts), inv=_p(out.inv),
                 ex_of_occ=0 if ex_payload else _p(ex_of_occ),
                 sorted_ex=0 if ex_payload else _p(out.sorted_ex), vals=_p(vals), sorted_x=_p(out.sorted_x),
-                ws=_p(ws.ws), ws_bytes=ws.ws.numel(), stream=_stream(keys))
+                payload_is_ex=int(ex_payload), slice_shift=shift, nslices=nsl,
+                slice_list=_p(out.slice_list), slice_start=_p(ws.slice_start), ws=_p(ws.ws), ws_bytes=ws.ws.numel(), stream=_stream(keys))
     else:
         U = native.cpu().dedup(n=n, keys=_p(keys), skeys=_p(ws.skeys), perm=_p(ws.perm), uniq=_p(ws.uniq),
                                seg_start=_p(ws.seg_start), inv=_p(out.inv), ex_of_occ=_p(ex_of_occ),
@@ -376,13 +414,15 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
             partial = torch.empty((partial_rows(dd.n, dd.CH), Kp + 4), dtype=torch.float32, device=dev)
         _check(partial.numel() >= partial_rows(dd.n, dd.CH) * (Kp + 4), "partial scratch too small")
         h.bwd(mode=mode, counts=_p(dd.counts), chunk_start=_p(dd.chunk_start), chunk_seg=_p(dd.chunk_seg),
+              chunk_key=_p(dd.chunk_key),
               seg_start=_p(dd.seg_start), seg_chunk=_p(dd.seg_chunk), uniq=_p(dd.uniq),
               sorted_ex=_p(dd.sorted_ex), sorted_x=_p(dd.sorted_x), dpred=_p(dpred), r1=_p(r1), Kp=Kp,
               v=_p(v), v_stride=v_stride, w=_p(w), w_stride=w.stride(0), s0v=_p(s0v), s1v=_p(s1v),
               s_stride=s_stride, s0w=_p(s0w), s1w=_p(s1w), reg_v=float(reg_v), reg_w=float(reg_w),
               opt_type=o.code, lr=float(o.lr), l1=float(o.l1), l2=float(o.l2), beta=float(o.beta),
               grad_out=gptr, g_stride=gstride, partial=_p(partial), big_list=_p(dd.big_list),
-              big_count=_p(dd.big_count), multi=_p(dd.multi), dtype=dt, max_chunks=dd.n, max_unique=dd.n,
+              big_count=_p(dd.big_count), multi=_p(dd.multi), slice_list=_p(dd.slice_list),
+              slice_start=_p(dd.slice_start), nslices=int(dd.nslices or 0), dtype=dt, max_chunks=dd.n, max_unique=dd.n,
               stream=_stream(dpred))
     else:
         U = dd.sync()

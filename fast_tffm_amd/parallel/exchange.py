@@ -86,7 +86,7 @@ class ShardExchange(_Base):
         ws = self.m.ws
         keys = self._keys(b)
         dd = K.dedup(keys, ws=ws.dd, key_bits=self.key_bits, ex_of_occ=ex, vals=b.vals if ex is not None else None,
-                     want_inv=True)
+                     want_inv=True, num_examples=b.B, Kp=self.m.Kp)
         # per-owner counts on the device, one count all-to-all, ONE host sync for both split lists
         counts = torch.empty(2 * self.W, dtype=torch.int64, device=self.dev)
         counts[: self.W] = K.owner_counts(dd, self.Rps, self.W)
@@ -148,7 +148,8 @@ class DPExchange(_Base):
         fo = K.fm_forward(b.offsets, rows, b.vals, m.table.v, m.table.w, Kp, labels=b.labels, weights=b.weights,
                           loss=cfg.loss_type, grad_scale=m.grad_scale(b.B), want_r1=True, pred=ws.pred[: b.B],
                           r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial, threads=cfg.threads)
-        dd = K.dedup(rows, ws=ws.dd, key_bits=bits_for(m.table.rows), ex_of_occ=ex, vals=b.vals)
+        dd = K.dedup(rows, ws=ws.dd, key_bits=bits_for(m.table.rows), ex_of_occ=ex, vals=b.vals,
+                     num_examples=b.B, Kp=Kp)
         U = dd.sync()
         uniq = dd.uniq[:U]
         src = torch.empty((U, self.gs), dtype=torch.float32, device=self.dev)

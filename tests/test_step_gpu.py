@@ -69,3 +69,26 @@ def test_bf16_table_step_close_to_fp32():
     m32.train_step(b)
     m16.train_step(b)
     torch.testing.assert_close(m16.table.reference_rows(), m32.table.reference_rows(), rtol=2e-2, atol=2e-3)
+
+
+@pytest.mark.parametrize("k", [16, 64])
+def test_xcd_sliced_schedule_matches_oracle(monkeypatch, k):
+    """Per-slice chunk lists + slice-cut hot rows (the large-batch schedule) forced on a small batch."""
+    monkeypatch.setattr(K, "SLICE_BYTES", 4096)
+    monkeypatch.setenv("FM_BWD_SLICES", "1")
+    V = 5000
+    gen = CriteoSynth(V, device="cuda", seed=8)
+    b = gen.batch(2048)
+    m = _model(V=V, k=k)
+    assert K.slice_plan(b.B, m.Kp)[1] > 8
+    p0 = m.table.reference_rows().double().cpu()
+    m.train_step(b)
+    p1, _, _ = reference_train_step(p0, torch.full_like(p0, 0.1), b.to("cpu"), "logistic", 0.05, 0.01, 0.01, 512)
+    torch.testing.assert_close(m.table.reference_rows().double().cpu(), p1, rtol=2e-4, atol=5e-6)
+    # the plan: every chunk listed exactly once, slice lists cover [0, #chunks)
+    dd = K.dedup(m._rows32(b), key_bits=32, ex_of_occ=K.csr_rows(b.offsets), num_examples=b.B, Kp=m.Kp)
+    C = int(dd.counts[1])
+    lst = dd.slice_list[:C].sort().values.cpu()
+    assert torch.equal(lst, torch.arange(C, dtype=torch.int32))
+    st = dd.slice_start[: dd.nslices + 1].cpu()
+    assert int(st[0]) == 0 and int(st[-1]) == C and bool((st[1:] >= st[:-1]).all())
