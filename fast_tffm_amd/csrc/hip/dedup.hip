@@ -41,6 +41,8 @@ struct RleArgs {
   const uint32_t* skeys;          // sorted keys
   const int* spay;                // sorted payload (occurrence or example index)
   const int* sex;                 // sorted example index (== spay when the payload is the example), or null
+  int ex_shift;                   // > 0: payload / ex_of_occ hold packed codes (example << ex_shift | slot)
+  const int* offsets;             // [B+1] CSR offsets (packed codes -> occurrence index)
   unsigned* tile_cnt;             // [2][ntiles] heads, chunk starts per tile
   unsigned* tile_off;             // [2][ntiles] exclusive offsets
   unsigned* slice_cnt;            // [nslices][ntiles] chunks per (slice, tile)
@@ -59,7 +61,7 @@ struct RleArgs {
 };
 
 __device__ inline int sorted_example(const RleArgs& a, int j) {
-  return a.sex ? a.sex[j] : a.ex_of_occ[a.spay[j]];
+  return (a.sex ? a.sex[j] : a.ex_of_occ[a.spay[j]]) >> a.ex_shift;
 }
 
 // v[q] = p[j0 + q] (fill outside [0, n)); two 16-byte loads when in range (j0 % 8 == 0).
@@ -110,6 +112,8 @@ __device__ inline void rle_flags8(const RleArgs& a, int j0, Rle8& r) {
   load8(a.skeys, j0 + a.hot, a.n, kr, kNone);
   if (a.sex) {
     load8(a.sex, j0, a.n, r.ex, 0);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) r.ex[q] >>= a.ex_shift;
   } else {
 #pragma unroll
     for (int q = 0; q < 8; ++q) r.ex[q] = j0 + q < a.n ? sorted_example(a, j0 + q) : 0;
@@ -227,12 +231,14 @@ __global__ __launch_bounds__(kBlock) void rle_tile_emit_kernel(RleArgs a) {
   // running (inclusive) segment / chunk ids of this thread's elements
   int s = (int)(a.tile_off[tile] + he) - 1;
   int ch = (int)(a.tile_off[a.ntiles + tile] + ce) - 1;
+  int sq[kRleItems];
 #pragma unroll
   for (int q = 0; q < kRleItems; ++q) {
     const int j = j0 + q;
-    if (j >= a.n) break;
     s += r.hd[q];
     ch += r.cs[q];
+    sq[q] = s;
+    if (j >= a.n) continue;
     if (r.hd[q]) {
       a.uniq[s] = r.k[q];
       a.seg_start[s] = j;
@@ -248,11 +254,30 @@ __global__ __launch_bounds__(kBlock) void rle_tile_emit_kernel(RleArgs a) {
       a.chunk_key[ch] = (int)r.k[q];
       if (sliced) atomicAdd(&sc[chunk_slice(a, r.hot[q], r.ex[q], ch)], 1u);
     }
-    if (a.inv || a.sorted_ex || a.sorted_x) {
-      const int p = a.spay[j];
-      if (a.inv) a.inv[p] = s;
-      if (a.sorted_ex) a.sorted_ex[j] = a.ex_of_occ[p];
-      if (a.sorted_x) a.sorted_x[j] = a.vals[p];
+  }
+  if (a.inv || a.sorted_ex || a.sorted_x) {
+    // payload = occurrence (or packed code): all 8 random gathers / scatters of the thread in flight at once
+    int p[kRleItems];
+    load8(a.spay, j0, a.n, p, 0);
+    if (a.ex_shift > 0) {  // packed code -> occurrence index (offsets is small and L2-resident)
+      const int mask = (1 << a.ex_shift) - 1;
+#pragma unroll
+      for (int q = 0; q < kRleItems; ++q) p[q] = j0 + q < a.n ? a.offsets[p[q] >> a.ex_shift] + (p[q] & mask) : 0;
+    }
+    int exv[kRleItems];
+    float xv[kRleItems];
+#pragma unroll
+    for (int q = 0; q < kRleItems; ++q) {
+      const bool ok = j0 + q < a.n;
+      exv[q] = (a.sorted_ex && ok) ? a.ex_of_occ[p[q]] : 0;
+      xv[q] = (a.sorted_x && ok) ? a.vals[p[q]] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < kRleItems; ++q) {
+      if (j0 + q >= a.n) break;
+      if (a.inv) a.inv[p[q]] = sq[q];
+      if (a.sorted_ex) a.sorted_ex[j0 + q] = exv[q];
+      if (a.sorted_x) a.sorted_x[j0 + q] = xv[q];
     }
   }
   if (sliced) {
@@ -372,6 +397,8 @@ struct DedupArgs {
   const float* vals;       // nullable
   float* sorted_x;         // nullable
   int payload_is_ex;       // payload carries the example index (sorted payload == sorted example)
+  int ex_shift;            // > 0: the payload is the packed code (example << ex_shift | slot), see csr_rows
+  const int* offsets;      // [B+1] (ex_shift > 0)
   int slice_shift;         // < 0: no slicing; else example slice = ex >> slice_shift
   int nslices;             // slices (<= kMaxSlices)
   int* slice_list;         // [n] chunk ids grouped by slice
@@ -407,7 +434,7 @@ int launch_dedup(const DedupArgs& a, hipStream_t st) {
   unsigned* cnt = reinterpret_cast<unsigned*>(sbase + scan_cap);
   unsigned* off = reinterpret_cast<unsigned*>(sbase + scan_cap + align_up(m * sizeof(unsigned)));
   RleArgs r{a.n, a.CH, ntiles, sliced ? a.slice_shift : -1, sliced ? a.nslices : 0, 8 * a.CH, a.skeys, a.spay,
-            a.payload_is_ex ? a.spay : nullptr, tile_cnt, tile_off, cnt, a.uniq, a.seg_start, a.seg_chunk,
+            a.payload_is_ex ? a.spay : nullptr, a.ex_shift, a.offsets, tile_cnt, tile_off, cnt, a.uniq, a.seg_start, a.seg_chunk,
             a.chunk_start, a.chunk_seg, a.chunk_key, a.counts, a.inv, a.ex_of_occ, a.sorted_ex, a.vals, a.sorted_x};
   hipLaunchKernelGGL(rle_tile_count_kernel, dim3(ntiles), dim3(kBlock), 0, st, r);
   hipLaunchKernelGGL(rle_tile_scan_kernel, dim3(1), dim3(1024), 0, st, r);

@@ -39,7 +39,8 @@ struct BwdArgs {
   const int* seg_start;     // [U+1]
   const int* seg_chunk;     // [U+1] first chunk of each segment
   const int* uniq;          // [U] table row of each segment (LOCAL)
-  const int* sorted_ex;     // [nnz] example index of each sorted occurrence
+  const int* sorted_ex;     // [nnz] example index of each sorted occurrence (<< ex_shift when packed)
+  int ex_shift;             // > 0: sorted_ex holds packed codes (example << ex_shift | slot)
   const float* sorted_x;    // [nnz] value of each sorted occurrence or nullptr (=1)
   const float* dpred;       // [B]
   const float* r1;          // [B, Kp]
@@ -213,7 +214,7 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_chunk_kernel(BwdArgs a) {
       const int jj = j0 + q * LPR + t;
       const bool ok = jj < j1;
       const int jc = ok ? jj : j0;
-      const int ex = a.sorted_ex[jc];
+      const int ex = a.sorted_ex[jc] >> a.ex_shift;
       const float x = a.sorted_x ? a.sorted_x[jc] : 1.f;
       pex[q] = ex;
       px[q] = x;

@@ -169,12 +169,16 @@ __global__ __launch_bounds__(kBlock) void fm_fwd_kernel(FwdArgs a) {
 }
 
 // Expand CSR offsets into the example index of every occurrence.
-__global__ __launch_bounds__(kBlock) void csr_rows_kernel(int B, const int* offsets, int* ex_of_occ) {
+// Example of every CSR occurrence; with slot_bits > 0 the packed occurrence code
+// (example << slot_bits) | (position inside the example), which the dedup sort
+// carries as its payload: the example and, through offsets, the occurrence
+// index both decode from it without a gather.
+__global__ __launch_bounds__(kBlock) void csr_rows_kernel(int B, const int* offsets, int* ex_of_occ, int slot_bits) {
   const int lane = threadIdx.x & (kWave - 1);
   const int nwaves = gridDim.x * kWavesPerBlock;
   for (int i = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); i < B; i += nwaves) {
     const int s = offsets[i], e = offsets[i + 1];
-    for (int j = s + lane; j < e; j += kWave) ex_of_occ[j] = i;
+    for (int j = s + lane; j < e; j += kWave) ex_of_occ[j] = slot_bits > 0 ? (i << slot_bits) | (j - s) : i;
   }
 }
 
@@ -187,10 +191,10 @@ int launch_fwd(const FwdArgs& a, int dtype, int grid, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-int launch_csr_rows(int B, const int* offsets, int* ex_of_occ, hipStream_t st) {
+int launch_csr_rows(int B, const int* offsets, int* ex_of_occ, int slot_bits, hipStream_t st) {
   if (B <= 0) return 0;
   hipLaunchKernelGGL(csr_rows_kernel, dim3(fill_grid(B, kWavesPerBlock, 4096)), dim3(kBlock), 0, st, B,
-                     offsets, ex_of_occ);
+                     offsets, ex_of_occ, slot_bits);
   return (int)hipGetLastError();
 }
 

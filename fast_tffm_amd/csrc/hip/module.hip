@@ -74,7 +74,7 @@ PYBIND11_MODULE(_fm_hip, m) {
   m.def(
       "bwd",
       [](int mode, u64 counts, u64 chunk_start, u64 chunk_seg, u64 chunk_key, u64 seg_start, u64 seg_chunk, u64 uniq,
-         u64 sorted_ex, u64 sorted_x, u64 dpred, u64 r1, int Kp, u64 v, long long v_stride, u64 w,
+         u64 sorted_ex, int ex_shift, u64 sorted_x, u64 dpred, u64 r1, int Kp, u64 v, long long v_stride, u64 w,
          long long w_stride, u64 s0v, u64 s1v, long long s_stride, u64 s0w, u64 s1w, float reg_v, float reg_w,
          int opt_type, float lr, float l1, float l2, float beta, u64 grad_out, long long g_stride, u64 partial,
          u64 big_list, u64 big_count, u64 multi, u64 slice_list, u64 slice_start, int nslices, int dtype,
@@ -84,7 +84,7 @@ PYBIND11_MODULE(_fm_hip, m) {
         a.chunk_seg = P<const int>(chunk_seg); a.chunk_key = P<const int>(chunk_key);
         a.seg_start = P<const int>(seg_start);
         a.seg_chunk = P<const int>(seg_chunk); a.uniq = P<const int>(uniq);
-        a.sorted_ex = P<const int>(sorted_ex); a.sorted_x = P<const float>(sorted_x);
+        a.sorted_ex = P<const int>(sorted_ex); a.ex_shift = ex_shift; a.sorted_x = P<const float>(sorted_x);
         a.dpred = P<const float>(dpred); a.r1 = P<const float>(r1); a.Kp = Kp;
         a.v = P<void>(v); a.v_stride = v_stride; a.w = P<float>(w); a.w_stride = w_stride;
         a.s0v = P<float>(s0v); a.s1v = P<float>(s1v); a.s_stride = s_stride; a.s0w = P<float>(s0w);
@@ -98,7 +98,7 @@ PYBIND11_MODULE(_fm_hip, m) {
       },
       py::arg("mode"), py::arg("counts"), py::arg("chunk_start"), py::arg("chunk_seg"), py::arg("chunk_key"),
       py::arg("seg_start"),
-      py::arg("seg_chunk"), py::arg("uniq"), py::arg("sorted_ex"), py::arg("sorted_x"), py::arg("dpred"),
+      py::arg("seg_chunk"), py::arg("uniq"), py::arg("sorted_ex"), py::arg("ex_shift"), py::arg("sorted_x"), py::arg("dpred"),
       py::arg("r1"), py::arg("Kp"), py::arg("v"), py::arg("v_stride"), py::arg("w"), py::arg("w_stride"),
       py::arg("s0v"), py::arg("s1v"), py::arg("s_stride"), py::arg("s0w"), py::arg("s1w"), py::arg("reg_v"),
       py::arg("reg_w"), py::arg("opt_type"), py::arg("lr"), py::arg("l1"), py::arg("l2"), py::arg("beta"),
@@ -112,7 +112,7 @@ PYBIND11_MODULE(_fm_hip, m) {
       "dedup",
       [](int n, int end_bit, int CH, u64 keys, u64 payload, u64 skeys, u64 spay, u64 uniq, u64 seg_start,
          u64 seg_chunk, u64 chunk_start, u64 chunk_seg, u64 chunk_key, u64 counts, u64 inv, u64 ex_of_occ,
-         u64 sorted_ex, u64 vals, u64 sorted_x, int payload_is_ex, int slice_shift, int nslices, u64 slice_list,
+         u64 sorted_ex, u64 vals, u64 sorted_x, int payload_is_ex, int ex_shift, u64 offsets, int slice_shift, int nslices, u64 slice_list,
          u64 slice_start, u64 ws, size_t ws_bytes, u64 stream) {
         if (CH < 1 || CH > fm::kMaxCH) throw std::invalid_argument("CH must be in [1, MAX_CH]");
         fm::DedupArgs a;
@@ -123,7 +123,8 @@ PYBIND11_MODULE(_fm_hip, m) {
         a.chunk_key = P<int>(chunk_key);
         a.inv = P<int>(inv); a.ex_of_occ = P<const int>(ex_of_occ); a.sorted_ex = P<int>(sorted_ex);
         a.vals = P<const float>(vals); a.sorted_x = P<float>(sorted_x); a.ws = P<void>(ws);
-        a.payload_is_ex = payload_is_ex; a.slice_shift = slice_shift; a.nslices = nslices;
+        a.payload_is_ex = payload_is_ex; a.ex_shift = ex_shift; a.offsets = P<const int>(offsets);
+        a.slice_shift = slice_shift; a.nslices = nslices;
         a.slice_list = P<int>(slice_list); a.slice_start = P<int>(slice_start);
         a.ws_bytes = ws_bytes;
         check(fm::launch_dedup(a, S(stream)), "dedup");
@@ -132,7 +133,8 @@ PYBIND11_MODULE(_fm_hip, m) {
       py::arg("spay"), py::arg("uniq"), py::arg("seg_start"), py::arg("seg_chunk"), py::arg("chunk_start"),
       py::arg("chunk_seg"), py::arg("chunk_key"), py::arg("counts"), py::arg("inv"), py::arg("ex_of_occ"),
       py::arg("sorted_ex"),
-      py::arg("vals"), py::arg("sorted_x"), py::arg("payload_is_ex"), py::arg("slice_shift"), py::arg("nslices"),
+      py::arg("vals"), py::arg("sorted_x"), py::arg("payload_is_ex"), py::arg("ex_shift"), py::arg("offsets"),
+      py::arg("slice_shift"), py::arg("nslices"),
       py::arg("slice_list"), py::arg("slice_start"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"));
   m.attr("MAX_SLICES") = fm::kMaxSlices;
 
@@ -191,9 +193,16 @@ PYBIND11_MODULE(_fm_hip, m) {
       py::arg("uniq"), py::arg("num_unique"), py::arg("Rps"), py::arg("W"), py::arg("out"), py::arg("stream"));
 
   m.def(
-      "csr_rows",
-      [](int B, u64 offsets, u64 ex_of_occ, u64 stream) {
-        check(fm::launch_csr_rows(B, P<const int>(offsets), P<int>(ex_of_occ), S(stream)), "csr_rows");
+      "shard_keys",
+      [](int n, u64 ids, int W, int Rps, u64 keys, u64 stream) {
+        check(fm::launch_shard_keys(n, P<const int>(ids), W, Rps, P<int>(keys), S(stream)), "shard_keys");
       },
-      py::arg("B"), py::arg("offsets"), py::arg("ex_of_occ"), py::arg("stream"));
+      py::arg("n"), py::arg("ids"), py::arg("W"), py::arg("Rps"), py::arg("keys"), py::arg("stream"));
+
+  m.def(
+      "csr_rows",
+      [](int B, u64 offsets, u64 ex_of_occ, int slot_bits, u64 stream) {
+        check(fm::launch_csr_rows(B, P<const int>(offsets), P<int>(ex_of_occ), slot_bits, S(stream)), "csr_rows");
+      },
+      py::arg("B"), py::arg("offsets"), py::arg("ex_of_occ"), py::arg("slot_bits"), py::arg("stream"));
 }

@@ -77,11 +77,28 @@ __global__ __launch_bounds__(kBlock) void apply_rows_kernel(ApplyArgs a) {
   const int U = *a.num_unique;
   const int ngroups = gridDim.x * kWavesPerBlock * G;
   for (int u = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g; u < U; u += ngroups) {
+    // table row + optimizer state first: their loads overlap the gradient sum below
+    const long long row = a.uniq[u];
+    TV* vrow = reinterpret_cast<TV*>(a.v) + row * a.v_stride + tE * EPL;
+    float vv[EPL], st0[EPL], st1[EPL];
+    F::load(vrow, vv);
+    float* s0 = a.s0v + row * a.s_stride + tE * EPL;
+    float* s1 = a.s1v ? a.s1v + row * a.s_stride + tE * EPL : nullptr;
+#pragma unroll
+    for (int k = 0; k < EPL; k += 4) {
+      const float4 q = *reinterpret_cast<const float4*>(s0 + k);
+      st0[k] = q.x; st0[k + 1] = q.y; st0[k + 2] = q.z; st0[k + 3] = q.w;
+      const float4 z = s1 ? *reinterpret_cast<const float4*>(s1 + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      st1[k] = z.x; st1[k + 1] = z.y; st1[k + 2] = z.z; st1[k + 3] = z.w;
+    }
+    float* wp = a.w + row * a.w_stride;
+    float pw = *wp, q0 = a.s0w[row], q1 = a.s1w ? a.s1w[row] : 0.f;
     float gr[EPL];
 #pragma unroll
     for (int k = 0; k < EPL; ++k) gr[k] = 0.f;
     float gw = 0.f;
-    for (int j = a.seg_start[u]; j < a.seg_start[u + 1]; ++j) {
+    const int j1 = a.seg_start[u + 1];
+    for (int j = a.seg_start[u]; j < j1; ++j) {
       const float* src = a.grad_in + (long long)a.perm[j] * a.g_stride;
 #pragma unroll
       for (int k = 0; k < EPL; k += 4) {
@@ -90,26 +107,19 @@ __global__ __launch_bounds__(kBlock) void apply_rows_kernel(ApplyArgs a) {
       }
       gw += src[a.Kp];
     }
-    const long long row = a.uniq[u];
-    TV* vrow = reinterpret_cast<TV*>(a.v) + row * a.v_stride + tE * EPL;
-    float vv[EPL], st0[EPL], st1[EPL];
-    F::load(vrow, vv);
-    float* s0 = a.s0v + row * a.s_stride + tE * EPL;
-    float* s1 = a.s1v ? a.s1v + row * a.s_stride + tE * EPL : nullptr;
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) { st0[k] = s0[k]; st1[k] = s1 ? s1[k] : 0.f; }
 #pragma unroll
     for (int k = 0; k < EPL; ++k) opt_step(a.opt, gr[k], vv[k], st0[k], st1[k]);
     if (tact) {
       F::store(vrow, vv);
 #pragma unroll
-      for (int k = 0; k < EPL; ++k) { s0[k] = st0[k]; if (s1) s1[k] = st1[k]; }
+      for (int k = 0; k < EPL; k += 4) {
+        *reinterpret_cast<float4*>(s0 + k) = make_float4(st0[k], st0[k + 1], st0[k + 2], st0[k + 3]);
+        if (s1) *reinterpret_cast<float4*>(s1 + k) = make_float4(st1[k], st1[k + 1], st1[k + 2], st1[k + 3]);
+      }
     }
     if (t == 0) {
-      float* wp = a.w + row * a.w_stride;
-      float p = *wp, q0 = a.s0w[row], q1 = a.s1w ? a.s1w[row] : 0.f;
-      opt_step(a.opt, gw, p, q0, q1);
-      *wp = p;
+      opt_step(a.opt, gw, pw, q0, q1);
+      *wp = pw;
       a.s0w[row] = q0;
       if (a.s1w) a.s1w[row] = q1;
     }
@@ -154,6 +164,21 @@ __global__ void owner_counts_kernel(const uint32_t* uniq, const int* num_unique,
     return lo;
   };
   out[w] = lower((unsigned long long)(w + 1) * Rps) - lower((unsigned long long)w * Rps);
+}
+
+// Sharded key of every occurrence: owner (id % W) major, local row (id / W) minor,
+// so that a sort groups each owner's requests contiguously.
+__global__ void shard_keys_kernel(int n, const int* ids, int W, int Rps, int* keys) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int id = ids[i];
+    keys[i] = (id % W) * Rps + id / W;
+  }
+}
+
+int launch_shard_keys(int n, const int* ids, int W, int Rps, int* keys, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(shard_keys_kernel, dim3(fill_grid(n, kBlock, 4096)), dim3(kBlock), 0, st, n, ids, W, Rps, keys);
+  return (int)hipGetLastError();
 }
 
 int launch_owner_counts(const uint32_t* uniq, const int* num_unique, long long Rps, int W, long long* out,

@@ -24,6 +24,7 @@ class Batch:
     weights: torch.Tensor | None = None  # [B] float32, None => all ones
     nnz: int = -1                   # host copy of offsets[-1] (avoids a device sync)
     reader_pos: tuple | None = None  # (epoch, batches consumed in epoch) after this batch
+    max_feats: int = -1             # host-known max features per example (-1: unknown)
 
     def __post_init__(self):
         if self.nnz < 0:
@@ -42,14 +43,14 @@ class Batch:
             return None if t is None else t.to(device, non_blocking=non_blocking)
 
         return Batch(mv(self.labels), mv(self.offsets), mv(self.ids), mv(self.vals), mv(self.weights), self.nnz,
-                     self.reader_pos)
+                     self.reader_pos, self.max_feats)
 
     def pin_memory(self) -> "Batch":
         def pn(t):
             return None if t is None else t.pin_memory()
 
         return Batch(pn(self.labels), pn(self.offsets), pn(self.ids), pn(self.vals), pn(self.weights), self.nnz,
-                     self.reader_pos)
+                     self.reader_pos, self.max_feats)
 
     @staticmethod
     def from_parsed(labels: np.ndarray, sizes: np.ndarray, ids: np.ndarray, vals: np.ndarray,
@@ -69,6 +70,7 @@ class Batch:
             vals=v,
             weights=None if weights is None else torch.from_numpy(np.ascontiguousarray(weights, dtype=np.float32)),
             nnz=int(offsets[-1]),
+            max_feats=int(sizes.max()) if len(sizes) else 0,
         )
 
     def slice(self, start: int, end: int) -> "Batch":
@@ -77,4 +79,4 @@ class Batch:
         a, b = int(o[start]), int(o[end])
         return Batch(self.labels[start:end], (o[start:end + 1] - a).contiguous(), self.ids[a:b],
                      None if self.vals is None else self.vals[a:b],
-                     None if self.weights is None else self.weights[start:end], b - a)
+                     None if self.weights is None else self.weights[start:end], b - a, max_feats=self.max_feats)

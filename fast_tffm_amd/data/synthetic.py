@@ -70,7 +70,8 @@ class CriteoSynth:
         ids = (ids.to(torch.int32) if self.vocab_size < 2**31 else ids).contiguous()
         offsets = torch.arange(0, (B + 1) * self.F, self.F, dtype=torch.int32, device=dev)
         labels = (torch.rand(B, generator=self.gen, device=dev) < self.ctr).to(torch.float32)
-        return Batch(labels=labels, offsets=offsets, ids=ids, vals=None, weights=None, nnz=B * self.F)
+        return Batch(labels=labels, offsets=offsets, ids=ids, vals=None, weights=None, nnz=B * self.F,
+                     max_feats=self.F)
 
 
 def random_batch(B: int, vocab_size: int, max_feats: int = 8, *, seed: int = 0, device="cpu",
@@ -89,4 +90,4 @@ def random_batch(B: int, vocab_size: int, max_feats: int = 8, *, seed: int = 0, 
     else:
         labels = torch.randn(B, generator=g)
     weights = (torch.rand(B, generator=g) + 0.5) if with_weights else None
-    return Batch(labels, offsets, ids, vals, weights, nnz).to(device)
+    return Batch(labels, offsets, ids, vals, weights, nnz, max_feats=int(sizes.max()) if B else 0).to(device)

@@ -96,7 +96,7 @@ class _GraphedStep:
 
         ids = ex.ids if ex.ids.dtype == torch.int32 else ex.ids.to(torch.int32)
         self.inp = Batch(static(ex.labels), static(ex.offsets), static(ids), static(ex.vals), static(ex.weights),
-                         ex.nnz)
+                         ex.nnz, max_feats=ex.max_feats)
         self.eager_left = max(1, warmup)  # real (eager) steps before capture: lazy loads, workspace sizing
         self.graph = None
         self.out = None
@@ -110,7 +110,7 @@ class _GraphedStep:
 
     @staticmethod
     def _sig(b: Batch):
-        return (b.B, b.nnz, b.vals is not None, b.weights is not None)
+        return (b.B, b.nnz, b.vals is not None, b.weights is not None, FactorizationMachine._slot_bits(b))
 
     def matches(self, b: Batch) -> bool:
         return self._sig(b) == self.sig
@@ -185,6 +185,14 @@ class FactorizationMachine:
             s /= self.world
         return s
 
+    @staticmethod
+    def _slot_bits(b: Batch, always: bool = False) -> int:
+        """Packed occurrence codes (csr_rows slot_bits) for GPU batches whose dedup needs the
+        occurrence index (per-occurrence values, or ``always``: the sharded inverse map)."""
+        if b.ids.device.type != "cuda" or not (always or b.vals is not None):
+            return 0
+        return K.slot_bits_for(b.B, b.max_feats)
+
     def _rows32(self, b: Batch) -> torch.Tensor:
         if b.ids.dtype == torch.int32:
             return b.ids
@@ -230,9 +238,10 @@ class FactorizationMachine:
             side = self._side_stream()
             side.wait_stream(main)  # inputs ready; previous step's readers of ws.dd are enqueued before
             with torch.cuda.stream(side):
-                ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz)
+                sb = self._slot_bits(b)
+                ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz, slot_bits=sb)
                 dd = K.dedup(rows, ws=ws.dd, key_bits=bits_for(self.table.rows), ex_of_occ=ex, vals=b.vals,
-                             num_examples=b.B, Kp=self.Kp)
+                             num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets)
         else:
             ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz)
         fo = K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,

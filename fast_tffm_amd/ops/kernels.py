@@ -204,7 +204,7 @@ class DedupOut:
 
     __slots__ = ("n", "skeys", "perm", "uniq", "seg_start", "seg_chunk", "chunk_start", "chunk_seg", "chunk_key", "counts",
                  "num_unique", "inv", "sorted_ex", "sorted_x", "U_host", "CH", "big_list", "big_count", "multi",
-                 "slice_list", "slice_start", "nslices")
+                 "slice_list", "slice_start", "nslices", "ex_shift")
 
     def __init__(self, **kw):
         for k in self.__slots__:
@@ -252,16 +252,31 @@ class DedupWorkspace:
             self.ws = None
 
 
-def csr_rows(offsets: torch.Tensor, out: torch.Tensor | None = None, nnz: int | None = None) -> torch.Tensor:
-    """Example index of every CSR occurrence (the reference gets it implicitly from feature_poses)."""
+def slot_bits_for(B: int, max_feats: int) -> int:
+    """Bits of the in-example slot of a packed occurrence code, or 0 when codes do not fit int32."""
+    if max_feats is None or max_feats < 1:
+        return 0
+    sb = max(1, (max_feats - 1).bit_length())
+    return sb if (B << sb) < 2**31 else 0
+
+
+def csr_rows(offsets: torch.Tensor, out: torch.Tensor | None = None, nnz: int | None = None,
+             slot_bits: int = 0) -> torch.Tensor:
+    """Example index of every CSR occurrence (the reference gets it implicitly from feature_poses).
+
+    With ``slot_bits > 0`` (GPU) the packed code ``example << slot_bits | slot`` instead:
+    the dedup sort carries it and decodes example and occurrence index from it.
+    """
     B = offsets.numel() - 1
     if nnz is None:
         nnz = int(offsets[-1])
     if out is None:
         out = torch.empty(nnz, dtype=torch.int32, device=offsets.device)
     if _is_gpu(offsets):
-        native.hip().csr_rows(B=B, offsets=_p(offsets), ex_of_occ=_p(out), stream=_stream(offsets))
+        native.hip().csr_rows(B=B, offsets=_p(offsets), ex_of_occ=_p(out), slot_bits=int(slot_bits),
+                              stream=_stream(offsets))
     else:
+        _check(slot_bits == 0, "packed occurrence codes are a GPU path")
         native.cpu().csr_rows(B=B, offsets=_p(offsets), ex_of_occ=_p(out))
     return out
 
@@ -294,7 +309,7 @@ def slice_plan(num_examples: int, Kp: int) -> tuple[int, int]:
 def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int = 32,
           ex_of_occ: torch.Tensor | None = None, vals: torch.Tensor | None = None, want_inv: bool = False,
           CH: int | None = None, want_perm: bool = False, num_examples: int | None = None,
-          Kp: int | None = None) -> DedupOut:
+          Kp: int | None = None, ex_shift: int = 0, offsets: torch.Tensor | None = None) -> DedupOut:
     """Sort-based unique over non-negative int32 keys (reference tf.unique, fm_model.py:72).
 
     Unique keys come out in ascending order (the reference's first-occurrence
@@ -315,7 +330,12 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
     if vals is not None:
         _chk_vec(vals, torch.float32, n, "vals", dev)
     key_bits = max(1, min(32, int(key_bits)))
-    ex_payload = ex_of_occ is not None and vals is None and not want_inv and not want_perm and _is_gpu(keys)
+    packed = ex_shift > 0
+    if packed:  # ex_of_occ holds packed codes (csr_rows slot_bits): the payload decodes to example + occurrence
+        _check(_is_gpu(keys) and ex_of_occ is not None and offsets is not None and not want_perm,
+               "packed occurrence codes need the GPU, codes and offsets")
+    ex_payload = ex_of_occ is not None and _is_gpu(keys) and not want_perm and (
+        packed or (vals is None and not want_inv))
     shift, nsl = -1, 0
     if ex_of_occ is not None and num_examples and Kp and _is_gpu(keys):
         shift, nsl = slice_plan(int(num_examples), int(Kp))
@@ -326,7 +346,7 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
                    sorted_ex=(ws.perm if ex_payload else ws.sorted_ex) if ex_of_occ is not None else None,
                    sorted_x=ws.sorted_x if vals is not None else None, CH=CH, big_list=ws.big_list,
                    big_count=ws.big_count, multi=ws.multi, slice_list=ws.slice_list if nsl else None,
-                   slice_start=ws.slice_start, nslices=nsl)
+                   slice_start=ws.slice_start, nslices=nsl, ex_shift=int(ex_shift))
     if _is_gpu(keys):
         h = native.hip()
         _check(1 <= CH <= h.MAX_CH, f"CH must be in [1, {h.MAX_CH}]")
@@ -337,8 +357,10 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
                 counts=_p(ws.counts), inv=_p(out.inv),
                 ex_of_occ=0 if ex_payload else _p(ex_of_occ),
                 sorted_ex=0 if ex_payload else _p(out.sorted_ex), vals=_p(vals), sorted_x=_p(out.sorted_x),
-                payload_is_ex=int(ex_payload), slice_shift=shift, nslices=nsl,
-                slice_list=_p(out.slice_list), slice_start=_p(ws.slice_start), ws=_p(ws.ws), ws_bytes=ws.ws.numel(), stream=_stream(keys))
+                payload_is_ex=int(ex_payload), ex_shift=int(ex_shift), offsets=_p(offsets),
+                slice_shift=shift, nslices=nsl,
+                slice_list=_p(out.slice_list), slice_start=_p(ws.slice_start), ws=_p(ws.ws),
+                ws_bytes=ws.ws.numel(), stream=_stream(keys))
     else:
         U = native.cpu().dedup(n=n, keys=_p(keys), skeys=_p(ws.skeys), perm=_p(ws.perm), uniq=_p(ws.uniq),
                                seg_start=_p(ws.seg_start), inv=_p(out.inv), ex_of_occ=_p(ex_of_occ),
@@ -416,7 +438,8 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
         h.bwd(mode=mode, counts=_p(dd.counts), chunk_start=_p(dd.chunk_start), chunk_seg=_p(dd.chunk_seg),
               chunk_key=_p(dd.chunk_key),
               seg_start=_p(dd.seg_start), seg_chunk=_p(dd.seg_chunk), uniq=_p(dd.uniq),
-              sorted_ex=_p(dd.sorted_ex), sorted_x=_p(dd.sorted_x), dpred=_p(dpred), r1=_p(r1), Kp=Kp,
+              sorted_ex=_p(dd.sorted_ex), ex_shift=int(dd.ex_shift or 0), sorted_x=_p(dd.sorted_x),
+              dpred=_p(dpred), r1=_p(r1), Kp=Kp,
               v=_p(v), v_stride=v_stride, w=_p(w), w_stride=w.stride(0), s0v=_p(s0v), s1v=_p(s1v),
               s_stride=s_stride, s0w=_p(s0w), s1w=_p(s1w), reg_v=float(reg_v), reg_w=float(reg_w),
               opt_type=o.code, lr=float(o.lr), l1=float(o.l1), l2=float(o.l2), beta=float(o.beta),
@@ -457,6 +480,21 @@ def gather_rows(req: torch.Tensor, table: TableState, Kp: int, out: torch.Tensor
                                  w_stride=table.w.stride(0), Kp=Kp, dtype=dt, out=_p(out), o_stride=out.stride(0),
                                  threads=threads)
     return out
+
+
+def shard_keys(ids: torch.Tensor, world: int, rows_per_shard: int, out: torch.Tensor) -> torch.Tensor:
+    """Sharded key of every occurrence: (id % world) * rows_per_shard + id // world (int32)."""
+    n = ids.numel()
+    _check(world * rows_per_shard < 2**31, "sharded keys must fit int32")
+    if _is_gpu(ids) and ids.dtype == torch.int32:
+        _chk_vec(out, torch.int32, None, "out", ids.device)
+        _check(out.numel() >= n, "out too small")
+        native.hip().shard_keys(n=n, ids=_p(ids), W=int(world), Rps=int(rows_per_shard), keys=_p(out),
+                                stream=_stream(ids))
+        return out[:n]
+    keys = (ids % world) * rows_per_shard + torch.div(ids, world, rounding_mode="floor")
+    out[:n].copy_(keys)
+    return out[:n]
 
 
 def owner_counts(dd: DedupOut, rows_per_shard: int, world: int) -> torch.Tensor:

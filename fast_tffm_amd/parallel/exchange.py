@@ -75,18 +75,17 @@ class ShardExchange(_Base):
         self.key_bits = bits_for(self.W * self.Rps)
 
     def _keys(self, b: Batch) -> torch.Tensor:
-        ids = b.ids
-        keys = (ids % self.W) * self.Rps + torch.div(ids, self.W, rounding_mode="floor")
-        out = self.m.ws.rows32[: b.nnz]
-        out.copy_(keys)
-        return out
+        return K.shard_keys(b.ids, self.W, self.Rps, self.m.ws.rows32)
 
-    def _lookup(self, b: Batch, ex: torch.Tensor | None):
-        """dedup + a2a(ids) + owner gather + a2a(rows). Returns (dd, gathered, splits, req_recv)."""
+    def _lookup(self, b: Batch, ex: torch.Tensor | None, sb: int = 0):
+        """dedup + a2a(ids) + owner gather + a2a(rows). Returns (dd, gathered, splits, req_recv).
+
+        ``sb`` > 0: ``ex`` holds packed occurrence codes (csr_rows slot_bits)."""
         ws = self.m.ws
         keys = self._keys(b)
         dd = K.dedup(keys, ws=ws.dd, key_bits=self.key_bits, ex_of_occ=ex, vals=b.vals if ex is not None else None,
-                     want_inv=True, num_examples=b.B, Kp=self.m.Kp)
+                     want_inv=True, num_examples=b.B, Kp=self.m.Kp, ex_shift=sb,
+                     offsets=b.offsets if sb else None)
         # per-owner counts on the device, one count all-to-all, ONE host sync for both split lists
         counts = torch.empty(2 * self.W, dtype=torch.int64, device=self.dev)
         counts[: self.W] = K.owner_counts(dd, self.Rps, self.W)
@@ -110,9 +109,22 @@ class ShardExchange(_Base):
         from ..models.fm import StepOut
 
         m, ws, cfg, Kp = self.m, self.m.ws, self.m.cfg, self.Kp
-        ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz)
-        dd, gathered, (sc, rc), req_recv = self._lookup(b, ex)
+        sb = m._slot_bits(b, always=True)
+        ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz, slot_bits=sb)
+        dd, gathered, (sc, rc), req_recv = self._lookup(b, ex, sb)
         U = dd.U_host
+        R = req_recv.numel()
+        # owner side: group the received requests by table row now, on a side stream,
+        # concurrently with this rank's forward/backward (it only needs req_recv)
+        gpu = self.dev.type == "cuda"
+        if gpu:
+            main = torch.cuda.current_stream(self.dev)
+            side = m._side_stream()
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                dd2 = K.dedup(req_recv, ws=self._dd2(R), key_bits=bits_for(self.Rps), want_perm=True)
+        else:
+            dd2 = K.dedup(req_recv, ws=self._dd2(R), key_bits=bits_for(self.Rps), want_perm=True)
         src_v, src_w = gathered[:, :Kp], gathered[:, Kp]
         fo = K.fm_forward(b.offsets, dd.inv[: b.nnz], b.vals, src_v, src_w, Kp, labels=b.labels,
                           weights=b.weights, loss=cfg.loss_type, grad_scale=m.grad_scale(b.B), want_r1=True,
@@ -122,10 +134,10 @@ class ShardExchange(_Base):
         rv, rw = m.reg_coeffs
         K.fm_backward(dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT, src_v=src_v, src_w=src_w, grad_out=grad, reg_v=rv,
                       reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads)
-        R = req_recv.numel()
         grad_recv = torch.empty((R, self.gs), dtype=torch.float32, device=self.dev)
         _a2a(grad_recv, grad, rc, sc, self.group)
-        dd2 = K.dedup(req_recv, ws=self._dd2(R), key_bits=bits_for(self.Rps), want_perm=True)
+        if gpu:
+            main.wait_stream(side)
         K.apply_rows(dd2, grad_recv, m.table.state, cfg.opt, Kp, threads=cfg.threads)
         return StepOut(fo.loss_sum, b.B)
 

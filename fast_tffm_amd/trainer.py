@@ -229,7 +229,7 @@ def _take(b, idx: torch.Tensor):
     offs = torch.zeros(idx.numel() + 1, dtype=torch.int32)
     offs[1:] = torch.cumsum(sizes, 0)
     return Batch(b.labels[idx], offs, b.ids[gather], None if b.vals is None else b.vals[gather],
-                 None if b.weights is None else b.weights[idx], int(offs[-1]))
+                 None if b.weights is None else b.weights[idx], int(offs[-1]), max_feats=b.max_feats)
 
 
 def _start_profiler():
