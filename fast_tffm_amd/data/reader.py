@@ -216,6 +216,7 @@ class Prefetcher:
                         t.record_stream(cur)
                 # keep the pinned source alive until the copy has been consumed
                 item._host_ref = _host  # type: ignore[attr-defined]
+                item.ready = ev  # type: ignore[attr-defined]  # other streams (lookahead plans) wait on it
             yield item
 
     def close(self):

@@ -201,7 +201,12 @@ class FactorizationMachine:
         return out
 
     # ------------------------------------------------------------------
-    def train_step(self, b: Batch) -> StepOut:
+    def train_step(self, b: Batch, next_batch: Batch | None = None) -> StepOut:
+        """One synchronous training step on ``b``.
+
+        ``next_batch`` (optional lookahead): the batch of the following call;
+        multi-rank executors prepare its table-independent work (dedup, id
+        exchange) concurrently with this step."""
         if self._graph is not None and self._graph.matches(b):
             g = self._graph
             # a batch that already lives in a captured graph's input buffers replays that graph, no copy
@@ -212,7 +217,9 @@ class FactorizationMachine:
             out = g.replay(b)
         else:
             self.ws.ensure(b.B, b.nnz)
-            if self._exchange is not None:
+            if getattr(self._exchange, "supports_lookahead", False):
+                out = self._exchange.train_step(b, next_batch)
+            elif self._exchange is not None:
                 out = self._exchange.train_step(b)
             else:
                 out = self._local_train_step(b)

@@ -68,86 +68,193 @@ class _Base:
         return self.dd2ws
 
 
+class _ShardPlan:
+    """The table-independent half of one batch's sharded step: dedup, owner counts,
+    id all-to-all and the owner-side grouping of the received requests."""
+
+    __slots__ = ("b", "slot", "dd", "sc", "rc", "U", "R", "req_recv", "dd2", "ready")
+
+
+class _PlanSlot:
+    """Double-buffered device workspaces of a plan (a plan for batch t+1 is built
+    while step t still reads the buffers of plan t)."""
+
+    def __init__(self):
+        self.dd: K.DedupWorkspace | None = None
+        self.dd2: K.DedupWorkspace | None = None
+        self.keys: torch.Tensor | None = None
+        self.done: torch.cuda.Event | None = None  # main-stream event: last step using this slot finished
+
+    def ensure(self, nnz: int, dev, CH: int) -> None:
+        if self.dd is None or self.dd.cap < nnz:
+            cap = max(nnz, 1, int(1.25 * (self.dd.cap if self.dd else 0)))
+            self.dd = K.DedupWorkspace(cap, dev, CH)
+            self.keys = torch.empty(cap, dtype=torch.int32, device=dev)
+
+    def ensure2(self, n: int, dev) -> K.DedupWorkspace:
+        if self.dd2 is None or self.dd2.cap < n:
+            self.dd2 = K.DedupWorkspace(max(n, 1, int(1.25 * (self.dd2.cap if self.dd2 else 0))), dev)
+        return self.dd2
+
+
 class ShardExchange(_Base):
+    """Row-sharded step.  ``train_step(b, next_batch)`` builds the plan of the next
+    batch (everything that does not read the table: dedup, counts + id a2a with its
+    one host sync, owner-side grouping) on a side stream while this step's
+    forward/backward run, so only gather -> a2a(rows) -> fwd -> bwd -> a2a(grads)
+    -> apply stay on the critical path.  Synchronous semantics are unchanged: the
+    rows of step t+1 are gathered after step t's update."""
+
+    supports_lookahead = True
+
     def __init__(self, model):
         super().__init__(model)
         self.Rps = model.rps
         self.key_bits = bits_for(self.W * self.Rps)
+        self.slots = [_PlanSlot(), _PlanSlot()]
+        # lookahead plans talk on their own communicator (own RCCL stream): the id
+        # all-to-all of batch t+1 does not queue behind step t's row / grad all-to-alls
+        self.plan_group = (dist.new_group(ranks=list(range(self.W)), backend=dist.get_backend(self.group))
+                           if self.W > 1 else self.group)
+        self.cpu_group = self.ctx.cpu_group or self.group
+        self.last_slot = 1
+        self.pending: _ShardPlan | None = None
+        self._prep = None
 
-    def _keys(self, b: Batch) -> torch.Tensor:
-        return K.shard_keys(b.ids, self.W, self.Rps, self.m.ws.rows32)
+    def _keys(self, b: Batch, out: torch.Tensor) -> torch.Tensor:
+        return K.shard_keys(b.ids, self.W, self.Rps, out)
 
-    def _lookup(self, b: Batch, ex: torch.Tensor | None, sb: int = 0):
-        """dedup + a2a(ids) + owner gather + a2a(rows). Returns (dd, gathered, splits, req_recv).
+    def _prep_stream(self):
+        if self._prep is None:
+            self._prep = torch.cuda.Stream(self.dev)
+        return self._prep
 
-        ``sb`` > 0: ``ex`` holds packed occurrence codes (csr_rows slot_bits)."""
-        ws = self.m.ws
-        keys = self._keys(b)
-        dd = K.dedup(keys, ws=ws.dd, key_bits=self.key_bits, ex_of_occ=ex, vals=b.vals if ex is not None else None,
-                     want_inv=True, num_examples=b.B, Kp=self.m.Kp, ex_shift=sb,
-                     offsets=b.offsets if sb else None)
-        # per-owner counts on the device, one count all-to-all, ONE host sync for both split lists
-        counts = torch.empty(2 * self.W, dtype=torch.int64, device=self.dev)
-        counts[: self.W] = K.owner_counts(dd, self.Rps, self.W)
-        dist.all_to_all_single(counts[self.W:], counts[: self.W], group=self.group)
-        both = counts.tolist()
-        sc, rc = both[: self.W], both[self.W:]
-        U = int(sum(sc))
-        dd.U_host = U
-        R = int(sum(rc))
-        uniq = dd.uniq[:U]
-        req_send = torch.remainder(uniq, self.Rps)  # keys are owner * Rps + local row
-        req_recv = torch.empty(R, dtype=torch.int32, device=self.dev)
-        _a2a(req_recv, req_send, rc, sc, self.group)
-        rows_send = torch.empty((R, self.gs), dtype=torch.float32, device=self.dev)
-        K.gather_rows(req_recv, self.m.table.state, self.Kp, rows_send, threads=self.m.cfg.threads)
-        gathered = torch.empty((U, self.gs), dtype=torch.float32, device=self.dev)
-        _a2a(gathered, rows_send, sc, rc, self.group)
-        return dd, gathered, (sc, rc), req_recv
+    def _plan(self, b: Batch, train: bool, inputs_ready=None) -> _ShardPlan:
+        """Build the plan of ``b`` (on the side stream when on the GPU).
 
-    def train_step(self, b: Batch):
+        ``inputs_ready``: main-stream event after which ``b``'s tensors are valid
+        (default: everything enqueued on the current stream so far)."""
+        m = self.m
+        # never the slot of a pending (not yet consumed) plan; the other slot's last user
+        # step is waited for through its done event
+        idx = (self.pending.slot ^ 1) if self.pending is not None else (self.last_slot ^ 1)
+        self.last_slot = idx
+        slot = self.slots[idx]
+        pl = _ShardPlan()
+        pl.b, pl.slot = b, idx
+        gpu = self.dev.type == "cuda"
+        if gpu:
+            st = self._prep_stream()
+            if slot.done is not None:
+                st.wait_event(slot.done)      # the last step that used these buffers is over
+            ready = getattr(b, "ready", None) or inputs_ready
+            if ready is not None:
+                st.wait_event(ready)           # H2D copy of the batch (Prefetcher) / its producer
+            else:
+                st.wait_stream(torch.cuda.current_stream(self.dev))
+            for t in (b.labels, b.offsets, b.ids, b.vals, b.weights):
+                if t is not None:
+                    t.record_stream(st)
+            ctx = torch.cuda.stream(st)
+        else:
+            import contextlib
+
+            ctx = contextlib.nullcontext()
+        with ctx:
+            slot.ensure(b.nnz, self.dev, m.cfg.dedup_chunk)
+            keys = self._keys(b, slot.keys)
+            ex, sb = None, 0
+            if train:
+                sb = m._slot_bits(b, always=True)
+                ex = K.csr_rows(b.offsets, out=slot.dd.ex_of_occ[: b.nnz], nnz=b.nnz, slot_bits=sb)
+            dd = K.dedup(keys, ws=slot.dd, key_bits=self.key_bits, ex_of_occ=ex,
+                         vals=b.vals if ex is not None else None, want_inv=True, num_examples=b.B, Kp=self.m.Kp,
+                         ex_shift=sb, offsets=b.offsets if sb else None)
+            # per-owner counts: one small D2H on this (side) stream -- the only host sync of the
+            # step, it waits for this dedup only -- then the count exchange on the CPU group
+            sc = K.owner_counts(dd, self.Rps, self.W).cpu()
+            rc = torch.empty_like(sc)
+            dist.all_to_all_single(rc, sc, group=self.cpu_group)
+            pl.sc, pl.rc = sc.tolist(), rc.tolist()
+            pl.U, pl.R = int(sum(pl.sc)), int(sum(pl.rc))
+            dd.U_host = pl.U
+            req_send = torch.remainder(dd.uniq[: pl.U], self.Rps)  # keys are owner * Rps + local row
+            pl.req_recv = torch.empty(pl.R, dtype=torch.int32, device=self.dev)
+            _a2a(pl.req_recv, req_send, pl.rc, pl.sc, self.plan_group)
+            pl.dd = dd
+            pl.dd2 = (K.dedup(pl.req_recv, ws=slot.ensure2(pl.R, self.dev), key_bits=bits_for(self.Rps),
+                              want_perm=True) if train else None)
+            if gpu:
+                pl.ready = torch.cuda.Event()
+                pl.ready.record(st)
+            else:
+                pl.ready = None
+        return pl
+
+    def _take_plan(self, b: Batch, train: bool) -> _ShardPlan:
+        pl = self.pending
+        if pl is not None and pl.b is b:
+            self.pending = None
+        else:  # (a pending plan for another batch, e.g. the next training batch, stays pending)
+            pl = self._plan(b, train)
+        if pl.ready is not None:
+            main = torch.cuda.current_stream(self.dev)
+            main.wait_event(pl.ready)
+            pl.req_recv.record_stream(main)  # allocated on the side stream, read on main
+        return pl
+
+    def _gather(self, pl: _ShardPlan) -> torch.Tensor:
+        """Owner gather of the requested rows + a2a back: [U, Kp+4] rows in unique order."""
+        rows_send = torch.empty((pl.R, self.gs), dtype=torch.float32, device=self.dev)
+        K.gather_rows(pl.req_recv, self.m.table.state, self.Kp, rows_send, threads=self.m.cfg.threads)
+        gathered = torch.empty((pl.U, self.gs), dtype=torch.float32, device=self.dev)
+        _a2a(gathered, rows_send, pl.sc, pl.rc, self.group)
+        return gathered
+
+    def train_step(self, b: Batch, next_batch: Batch | None = None):
         from ..models.fm import StepOut
 
         m, ws, cfg, Kp = self.m, self.m.ws, self.m.cfg, self.Kp
-        sb = m._slot_bits(b, always=True)
-        ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz, slot_bits=sb)
-        dd, gathered, (sc, rc), req_recv = self._lookup(b, ex, sb)
-        U = dd.U_host
-        R = req_recv.numel()
-        # owner side: group the received requests by table row now, on a side stream,
-        # concurrently with this rank's forward/backward (it only needs req_recv)
-        gpu = self.dev.type == "cuda"
-        if gpu:
-            main = torch.cuda.current_stream(self.dev)
-            side = m._side_stream()
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                dd2 = K.dedup(req_recv, ws=self._dd2(R), key_bits=bits_for(self.Rps), want_perm=True)
-        else:
-            dd2 = K.dedup(req_recv, ws=self._dd2(R), key_bits=bits_for(self.Rps), want_perm=True)
+        nb_ready = None
+        if next_batch is not None and self.dev.type == "cuda" and getattr(next_batch, "ready", None) is None:
+            nb_ready = torch.cuda.Event()  # next_batch's producers: all work enqueued before this step
+            nb_ready.record(torch.cuda.current_stream(self.dev))
+        pl = self._take_plan(b, True)
+        dd = pl.dd
+        gathered = self._gather(pl)
         src_v, src_w = gathered[:, :Kp], gathered[:, Kp]
         fo = K.fm_forward(b.offsets, dd.inv[: b.nnz], b.vals, src_v, src_w, Kp, labels=b.labels,
                           weights=b.weights, loss=cfg.loss_type, grad_scale=m.grad_scale(b.B), want_r1=True,
                           pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
                           threads=cfg.threads)
-        grad = torch.empty((U, self.gs), dtype=torch.float32, device=self.dev)
+        grad = torch.empty((pl.U, self.gs), dtype=torch.float32, device=self.dev)
         rv, rw = m.reg_coeffs
         K.fm_backward(dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT, src_v=src_v, src_w=src_w, grad_out=grad, reg_v=rv,
                       reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads)
-        grad_recv = torch.empty((R, self.gs), dtype=torch.float32, device=self.dev)
-        _a2a(grad_recv, grad, rc, sc, self.group)
-        if gpu:
-            main.wait_stream(side)
-        K.apply_rows(dd2, grad_recv, m.table.state, cfg.opt, Kp, threads=cfg.threads)
+        grad_recv = torch.empty((pl.R, self.gs), dtype=torch.float32, device=self.dev)
+        _a2a(grad_recv, grad, pl.rc, pl.sc, self.group)
+        K.apply_rows(pl.dd2, grad_recv, m.table.state, cfg.opt, Kp, threads=cfg.threads)
+        if self.dev.type == "cuda":
+            done = torch.cuda.Event()
+            done.record(torch.cuda.current_stream(self.dev))
+            self.slots[pl.slot].done = done
+        if next_batch is not None:
+            self.pending = self._plan(next_batch, True, nb_ready)
         return StepOut(fo.loss_sum, b.B)
 
     @torch.no_grad()
     def forward(self, b: Batch, *, loss: str = "none", want_reg: bool = False) -> K.FwdOut:
         self.m.ws.ensure(b.B, b.nnz)
-        dd, gathered, _, _ = self._lookup(b, None)
-        return K.fm_forward(b.offsets, dd.inv[: b.nnz], b.vals, gathered[:, : self.Kp], gathered[:, self.Kp],
-                            self.Kp, labels=b.labels, weights=b.weights, loss=loss, grad_scale=1.0, want_r1=False,
-                            want_reg=want_reg, threads=self.m.cfg.threads)
+        pl = self._take_plan(b, False)
+        gathered = self._gather(pl)
+        out = K.fm_forward(b.offsets, pl.dd.inv[: b.nnz], b.vals, gathered[:, : self.Kp], gathered[:, self.Kp],
+                           self.Kp, labels=b.labels, weights=b.weights, loss=loss, grad_scale=1.0, want_r1=False,
+                           want_reg=want_reg, threads=self.m.cfg.threads)
+        if self.dev.type == "cuda":
+            done = torch.cuda.Event()
+            done.record(torch.cuda.current_stream(self.dev))
+            self.slots[pl.slot].done = done
+        return out
 
 
 class DPExchange(_Base):

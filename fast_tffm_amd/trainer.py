@@ -129,18 +129,23 @@ class Trainer:
         prof = None
         ended_early = False
         last_loss = float("nan")
-        while True:
+
+        def fetch():
             try:
-                batch = next(it)
-                have = True
+                nb = next(it)
             except StopIteration:
-                batch, have = None, False
-            if not self._all_have_batch(have):
-                break
+                nb = None
+            return nb, self._all_have_batch(nb is not None)
+
+        batch, have = fetch()
+        while have:
+            # lookahead: the next batch (when every rank has one) lets the sharded executor
+            # build its dedup / id exchange while this step computes
+            nxt, nhave = fetch()
             if self.trace and prof is None and step_num == start_step + 1:
                 prof = _start_profiler()
             cur = time.time()
-            out = self.model.train_step(batch)
+            out = self.model.train_step(batch, nxt if nhave else None)
             step_num = self.model.global_step
             if batch.reader_pos is not None:  # position of the last CONSUMED batch (the reader runs ahead)
                 self.reader_state.epoch, self.reader_state.batches_in_epoch = batch.reader_pos
@@ -171,6 +176,7 @@ class Trainer:
                     self.save()
             if ended_early or (c.max_steps is not None and step_num - start_step >= c.max_steps):
                 break
+            batch, have = nxt, nhave
         if prof is not None:
             _stop_profiler(prof, self.trace)
         pf.close()

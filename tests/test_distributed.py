@@ -50,7 +50,10 @@ def _worker(rank, world, port, mode, grad_reduce, out_dir):
 
     ctx = fmdist.init_distributed(backend="gloo", rank=rank, world=world, device="cpu")
     m = FactorizationMachine(_cfg(mode, grad_reduce, 16), device="cpu", dist=ctx)
-    losses = [m.train_step(_batch(s, rank)).mean_loss() for s in range(STEPS)]
+    bs = [_batch(s, rank) for s in range(STEPS)]
+    # shard mode also exercises the lookahead plan (next batch's dedup + id exchange built early)
+    losses = [m.train_step(bs[s], bs[s + 1] if s + 1 < STEPS and mode == "shard" else None).mean_loss()
+              for s in range(STEPS)]
     pred = m.predict(_batch(99, rank))
     torch.save({"gids": m.table.global_ids(), "rows": m.table.reference_rows(), "acc": m.table.s0v[:, :KF].clone(),
                 "losses": losses, "pred": pred}, os.path.join(out_dir, f"rank{rank}.pt"))
