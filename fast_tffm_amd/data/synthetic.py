@@ -91,3 +91,48 @@ def random_batch(B: int, vocab_size: int, max_feats: int = 8, *, seed: int = 0, 
         labels = torch.randn(B, generator=g)
     weights = (torch.rand(B, generator=g) + 0.5) if with_weights else None
     return Batch(labels, offsets, ids, vals, weights, nnz, max_feats=int(sizes.max()) if B else 0).to(device)
+
+
+def write_libsvm(path: str, n_lines: int, *, shape: str = "criteo", vocab_size: int = 1_000_000, seed: int = 0,
+                 weights_path: str | None = None, with_values: bool = False) -> None:
+    """Write a synthetic libsvm text file in the reference's input format
+    (``<label> <fid>[:<val>] ...``, README.md:44-50).
+
+    shape="criteo": 39 fields (13 bucketized integer + 26 categorical, Zipf
+    popularity), 16-39 features per line like the reference's sample data
+    (SURVEY.md §6.3); shape="a1a": LIBSVM a1a-shaped (123 binary features,
+    ~14 active per line).  ``weights_path`` gets one weight per line (2 for
+    label 1, 1 for label 0, like the reference's data/weight_*).
+    """
+    import numpy as np
+
+    rng = np.random.default_rng(seed)
+    lines, wl = [], []
+    if shape == "a1a":
+        base = rng.random(123) ** 3
+        for _ in range(n_lines):
+            k = int(rng.integers(11, 15))
+            feats = np.sort(rng.choice(123, size=k, replace=False, p=base / base.sum()))
+            label = int(rng.random() < 0.24 + 0.5 * (feats[0] < 10))
+            toks = [f"{int(f) + 1}:1" if with_values else str(int(f) + 1) for f in feats]
+            lines.append(f"{label} " + " ".join(toks))
+            wl.append("2" if label else "1")
+    else:
+        cards = CRITEO_FIELD_CARD
+        for _ in range(n_lines):
+            nf = int(rng.integers(16, 40))
+            fields = np.sort(rng.choice(39, size=nf, replace=False))
+            toks = []
+            for f in fields:
+                card = cards[f]
+                val = min(int(rng.zipf(1.3)) - 1, card - 1)
+                fid = (f * 1_000_003 + val * 7919) % vocab_size
+                toks.append(f"{fid}:{rng.random():.3f}" if with_values else str(fid))
+            label = int(rng.random() < 0.25)
+            lines.append(f"{label} " + " ".join(toks))
+            wl.append("2" if label else "1")
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    if weights_path:
+        with open(weights_path, "w") as f:
+            f.write("\n".join(wl) + "\n")

@@ -27,6 +27,7 @@ import torch
 
 from ..data.batch import Batch
 from ..ops import kernels as K
+from ..utils.trace import roctx_range
 from .table import FMTable, bits_for, rows_per_shard
 
 
@@ -244,24 +245,26 @@ class FactorizationMachine:
             main = torch.cuda.current_stream(self.device)
             side = self._side_stream()
             side.wait_stream(main)  # inputs ready; previous step's readers of ws.dd are enqueued before
-            with torch.cuda.stream(side):
+            with torch.cuda.stream(side), roctx_range("dedup"):
                 sb = self._slot_bits(b)
                 ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz, slot_bits=sb)
                 dd = K.dedup(rows, ws=ws.dd, key_bits=bits_for(self.table.rows), ex_of_occ=ex, vals=b.vals,
                              num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets)
         else:
             ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz)
-        fo = K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,
-                          weights=b.weights, loss=cfg.loss_type, grad_scale=self.grad_scale(b.B), want_r1=True,
-                          pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
-                          threads=cfg.threads)
+        with roctx_range("fwd"):
+            fo = K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,
+                              weights=b.weights, loss=cfg.loss_type, grad_scale=self.grad_scale(b.B), want_r1=True,
+                              pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
+                              threads=cfg.threads)
         if gpu:
             main.wait_stream(side)
         else:
             dd = K.dedup(rows, ws=ws.dd, key_bits=bits_for(self.table.rows), ex_of_occ=ex, vals=b.vals)
         rv, rw = self.reg_coeffs
-        K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
-                      reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads)
+        with roctx_range("bwd+update"):
+            K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
+                          reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads)
         return StepOut(fo.loss_sum, b.B)
 
     # ------------------------------------------------------------------

@@ -103,8 +103,14 @@ def init_distributed(*, backend: str | None = None, rank: int | None = None, wor
         os.environ.setdefault("MASTER_PORT", "29500")
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")  # hang -> error, not a stuck job
         if not dist.is_initialized():
-            kw = dict(backend=backend, rank=rank, world_size=world,
-                      timeout=datetime.timedelta(seconds=timeout_s))
+            timeout = datetime.timedelta(seconds=timeout_s)
+            # torchrun --max-restarts re-runs every rank against the SAME rendezvous store;
+            # keys of the failed attempt (e.g. the address of a sub-group's rank 0) would be
+            # read back by the new processes, so each attempt gets its own key prefix
+            store, _, _ = next(dist.rendezvous("env://", rank=rank, world_size=world, timeout=timeout))
+            attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
+            store = dist.PrefixStore(f"fm_attempt_{attempt}", store)
+            kw = dict(backend=backend, rank=rank, world_size=world, timeout=timeout, store=store)
             if backend == "nccl":
                 kw["device_id"] = dev
             dist.init_process_group(**kw)

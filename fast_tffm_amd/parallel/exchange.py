@@ -35,6 +35,7 @@ import torch.distributed as dist
 from ..data.batch import Batch
 from ..ops import kernels as K
 from ..models.table import bits_for
+from ..utils.trace import roctx_range
 
 
 def make_exchange(model):
@@ -219,27 +220,34 @@ class ShardExchange(_Base):
         if next_batch is not None and self.dev.type == "cuda" and getattr(next_batch, "ready", None) is None:
             nb_ready = torch.cuda.Event()  # next_batch's producers: all work enqueued before this step
             nb_ready.record(torch.cuda.current_stream(self.dev))
-        pl = self._take_plan(b, True)
+        with roctx_range("plan"):
+            pl = self._take_plan(b, True)
         dd = pl.dd
-        gathered = self._gather(pl)
+        with roctx_range("gather+a2a_rows"):
+            gathered = self._gather(pl)
         src_v, src_w = gathered[:, :Kp], gathered[:, Kp]
-        fo = K.fm_forward(b.offsets, dd.inv[: b.nnz], b.vals, src_v, src_w, Kp, labels=b.labels,
-                          weights=b.weights, loss=cfg.loss_type, grad_scale=m.grad_scale(b.B), want_r1=True,
-                          pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
-                          threads=cfg.threads)
+        with roctx_range("fwd"):
+            fo = K.fm_forward(b.offsets, dd.inv[: b.nnz], b.vals, src_v, src_w, Kp, labels=b.labels,
+                              weights=b.weights, loss=cfg.loss_type, grad_scale=m.grad_scale(b.B), want_r1=True,
+                              pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B],
+                              partial=ws.fwd_partial, threads=cfg.threads)
         grad = torch.empty((pl.U, self.gs), dtype=torch.float32, device=self.dev)
         rv, rw = m.reg_coeffs
-        K.fm_backward(dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT, src_v=src_v, src_w=src_w, grad_out=grad, reg_v=rv,
-                      reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads)
+        with roctx_range("bwd"):
+            K.fm_backward(dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT, src_v=src_v, src_w=src_w, grad_out=grad,
+                          reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads)
         grad_recv = torch.empty((pl.R, self.gs), dtype=torch.float32, device=self.dev)
-        _a2a(grad_recv, grad, pl.rc, pl.sc, self.group)
-        K.apply_rows(pl.dd2, grad_recv, m.table.state, cfg.opt, Kp, threads=cfg.threads)
+        with roctx_range("a2a_grads"):
+            _a2a(grad_recv, grad, pl.rc, pl.sc, self.group)
+        with roctx_range("apply"):
+            K.apply_rows(pl.dd2, grad_recv, m.table.state, cfg.opt, Kp, threads=cfg.threads)
         if self.dev.type == "cuda":
             done = torch.cuda.Event()
             done.record(torch.cuda.current_stream(self.dev))
             self.slots[pl.slot].done = done
         if next_batch is not None:
-            self.pending = self._plan(next_batch, True, nb_ready)
+            with roctx_range("plan_next"):
+                self.pending = self._plan(next_batch, True, nb_ready)
         return StepOut(fo.loss_sum, b.B)
 
     @torch.no_grad()

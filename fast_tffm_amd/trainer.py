@@ -27,6 +27,8 @@ import torch
 import torch.distributed as dist
 
 from .config import FMRunConfig
+from .utils.fault import maybe_inject
+from .utils.trace import roctx_range
 from .data.reader import Prefetcher, ReaderState, TextBatchReader, load_file_batch
 from .models.fm import FactorizationMachine
 from .parallel.dist import DistContext
@@ -131,10 +133,11 @@ class Trainer:
         last_loss = float("nan")
 
         def fetch():
-            try:
-                nb = next(it)
-            except StopIteration:
-                nb = None
+            with roctx_range("input_wait"):
+                try:
+                    nb = next(it)
+                except StopIteration:
+                    nb = None
             return nb, self._all_have_batch(nb is not None)
 
         batch, have = fetch()
@@ -145,7 +148,8 @@ class Trainer:
             if self.trace and prof is None and step_num == start_step + 1:
                 prof = _start_profiler()
             cur = time.time()
-            out = self.model.train_step(batch, nxt if nhave else None)
+            with roctx_range("train_step"):
+                out = self.model.train_step(batch, nxt if nhave else None)
             step_num = self.model.global_step
             if batch.reader_pos is not None:  # position of the last CONSUMED batch (the reader runs ahead)
                 self.reader_state.epoch, self.reader_state.batches_in_epoch = batch.reader_pos
@@ -174,6 +178,7 @@ class Trainer:
                         ended_early = True
                 if c.log_dir:
                     self.save()
+            maybe_inject(step_num, self.rank)
             if ended_early or (c.max_steps is not None and step_num - start_step >= c.max_steps):
                 break
             batch, have = nxt, nhave

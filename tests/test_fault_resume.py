@@ -1,0 +1,96 @@
+"""Failure recovery: torchrun ``--max-restarts`` + auto-resume
+from the latest checkpoint must give the same final model as an uninterrupted
+run.  A rank is killed by the env-driven fault injector (utils/fault.py) right
+after a step that follows a checkpoint; torchrun restarts both ranks, which
+restore table, optimizer slots, global step and reader position and redo the
+lost steps.  CPU / gloo, world size 2, row-sharded table.
+"""
+
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+from safetensors.torch import load_file
+
+from fast_tffm_amd.data.synthetic import write_libsvm
+from fast_tffm_amd.utils import checkpoint as ckpt
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _cfg(tmp, log_dir):
+    text = f"""[General]
+vocabulary_size = 50000
+vocabulary_block_num = 2
+factor_num = 8
+hash_feature_id = false
+log_dir = {log_dir}
+device = cpu
+
+[Train]
+batch_size = 100
+init_value_range = 0.01
+factor_lambda = 0.0001
+bias_lambda = 0.0001
+epoch_num = 2
+learning_rate = 0.05
+adagrad.initial_accumulator = 0.1
+save_steps = 2
+loss_type = logistic
+train_files = {tmp}/data/train_*
+weight_files = {tmp}/data/weight_*
+"""
+    p = os.path.join(tmp, os.path.basename(log_dir) + ".cfg")
+    with open(p, "w") as f:
+        f.write(text)
+    return p
+
+
+def _torchrun(cfg, env_extra, timeout=240):
+    env = dict(os.environ)
+    env.update(env_extra)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--max-restarts", "1", "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "run.py"), "train", cfg, "--device", "cpu"]
+    return subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+def _final_state(log_dir):
+    path = ckpt.latest_checkpoint(log_dir)  # log_dir/model.ckpt-<step>
+    assert path is not None
+    shards = sorted(f for f in os.listdir(path) if f.endswith(".safetensors"))
+    return path, {f: load_file(os.path.join(path, f)) for f in shards}
+
+
+@pytest.mark.timeout(600)
+def test_killed_rank_restarts_and_resumes_exactly(tmp_path):
+    tmp = str(tmp_path)
+    os.makedirs(os.path.join(tmp, "data"))
+    for i in range(2):
+        write_libsvm(os.path.join(tmp, "data", f"train_{i}"), 600, vocab_size=50000, seed=i,
+                     weights_path=os.path.join(tmp, "data", f"weight_{i}"))
+    marker = os.path.join(tmp, "fault.marker")
+    faulty = _torchrun(_cfg(tmp, os.path.join(tmp, "log_fault")),
+                       {"FM_FAULT_STEP": "3", "FM_FAULT_RANK": "1", "FM_FAULT_MARKER": marker})
+    assert faulty.returncode == 0, faulty.stdout[-3000:] + faulty.stderr[-3000:]
+    assert os.path.exists(marker), "the fault was never injected"
+    assert "injected failure after step 3 on rank 1" in faulty.stderr
+    clean = _torchrun(_cfg(tmp, os.path.join(tmp, "log_clean")), {})
+    assert clean.returncode == 0, clean.stdout[-3000:] + clean.stderr[-3000:]
+
+    pf, sf = _final_state(os.path.join(tmp, "log_fault"))
+    pc, sc = _final_state(os.path.join(tmp, "log_clean"))
+    assert os.path.basename(pf) == os.path.basename(pc)  # same final global step
+    assert sf.keys() == sc.keys() and len(sf) > 0
+    for name in sf:
+        for k in sf[name]:
+            assert (sf[name][k] == sc[name][k]).all(), (name, k)
