@@ -27,6 +27,11 @@ BWD_LOCAL, BWD_EMIT = 0, 1
 _DEBUG = os.environ.get("FM_DEBUG_CHECKS", "0") == "1"
 
 
+def debug_checks() -> bool:
+    """FM_DEBUG_CHECKS=1: index range checks in the kernel wrappers and exchange split checks."""
+    return _DEBUG
+
+
 def set_debug_checks(on: bool) -> None:
     global _DEBUG
     _DEBUG = bool(on)

@@ -178,6 +178,8 @@ class ShardExchange(_Base):
             dist.all_to_all_single(rc, sc, group=self.cpu_group)
             pl.sc, pl.rc = sc.tolist(), rc.tolist()
             pl.U, pl.R = int(sum(pl.sc)), int(sum(pl.rc))
+            if K.debug_checks():
+                self._check_splits(pl, dd)
             dd.U_host = pl.U
             req_send = torch.remainder(dd.uniq[: pl.U], self.Rps)  # keys are owner * Rps + local row
             pl.req_recv = torch.empty(pl.R, dtype=torch.int32, device=self.dev)
@@ -191,6 +193,22 @@ class ShardExchange(_Base):
             else:
                 pl.ready = None
         return pl
+
+    def _check_splits(self, pl: _ShardPlan, dd) -> None:
+        """FM_DEBUG_CHECKS=1: the split lists of every rank must form a consistent W x W
+        exchange (what rank s sends to r is what r expects from s) and cover all unique ids."""
+        mats = [None] * self.W
+        dist.all_gather_object(mats, (pl.sc, pl.rc), group=self.cpu_group)
+        for r in range(self.W):
+            for q in range(self.W):
+                if mats[q][0][r] != mats[r][1][q]:
+                    raise RuntimeError(f"a2a split mismatch: rank {q} sends {mats[q][0][r]} ids to rank {r}, "
+                                       f"which expects {mats[r][1][q]}")
+        u = int(dd.num_unique.item())
+        if u != pl.U:
+            raise RuntimeError(f"owner counts cover {pl.U} ids, dedup found {u}")
+        if pl.U and int(dd.uniq[pl.U - 1].item()) >= self.W * self.Rps:
+            raise RuntimeError("sharded key out of range")
 
     def _take_plan(self, b: Batch, train: bool) -> _ShardPlan:
         pl = self.pending
