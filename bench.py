@@ -46,7 +46,9 @@ PRESETS = {
     # BASELINE config 3: k=64 data-parallel, dense all-reduce (small replicated vocabulary)
     "k64_dp_dense": dict(k=64, dtype="fp32", opt="adagrad", mode="dp_dense", slots_per_gpu=None,
                          vocab=1_000_000),
-    # BASELINE config 5 (partial: bf16 table, FTRL; fp8 table pending)
+    # BASELINE config 5: k=128 fp8 factor table (OCP e4m3 + per-row scale) + fused FTRL
+    "k128_fp8_ftrl": dict(k=128, dtype="fp8", opt="ftrl", mode="auto", slots_per_gpu=62_500_000),
+    # same with a bf16 table (reference point for the fp8 one)
     "k128_ftrl": dict(k=128, dtype="bf16", opt="ftrl", mode="auto", slots_per_gpu=62_500_000),
 }
 
@@ -84,7 +86,7 @@ def main() -> int:
         print("[bench] no GPU visible: running on CPU (not a valid measurement)", file=sys.stderr)
     slots = a.slots_per_gpu or p.get("slots_per_gpu")
     vocab = slots * W if slots else p["vocab"]
-    dtype = torch.bfloat16 if p["dtype"] == "bf16" else torch.float32
+    dtype = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp8": torch.float8_e4m3fn}[p["dtype"]]
     opt = K.OptConfig(p["opt"], lr=0.01 if p["opt"] == "adagrad" else 0.05, l1=0.001, l2=0.001, beta=1.0,
                       initial_accumulator=0.1)
     cfg = FMConfig(vocabulary_size=vocab, factor_num=p["k"], loss_type="logistic", batch_size=a.batch,
@@ -168,7 +170,8 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32" if dtype == torch.float32 else "bf16",
+            # compute dtype: fp32 arithmetic throughout; the table is stored as p["dtype"]
+            "dtype": p["dtype"],
             "data": "synthetic Criteo-shaped (39 fields, Zipf a=%.2f), random-init weights" % a.alpha,
             "config": {
                 "model": "FM k=%d, %s table + %s, hashed vocab %d (%d/GPU)" % (

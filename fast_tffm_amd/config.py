@@ -16,7 +16,7 @@ Decisions on reference quirks:
 * ``model_file`` is read and kept, unused, like the reference (:405-407).
 
 Extensions (new keys, all optional):
-  [General]     seed, dtype = fp32|bf16, device = auto|cpu|cuda
+  [General]     seed, dtype = fp32|bf16|fp8 (fp8: OCP e4m3 + per-row scale, GPU), device = auto|cpu|cuda
   [Train]       optimizer = adagrad|ftrl|sgd, ftrl.l1, ftrl.l2, ftrl.beta,
                 ftrl.initial_accumulator, parse_threads, shuffle = true|false,
                 max_steps, dedup_chunk, log_steps
@@ -32,6 +32,8 @@ from dataclasses import dataclass, field
 
 GENERAL, TRAIN, PREDICT, DISTRIBUTED = "General", "Train", "Predict", "Distributed"
 
+
+_TABLE_DTYPES = ("fp32", "bf16", "fp8")  # -> torch.float32 / bfloat16 / float8_e4m3fn
 
 class ConfigError(ValueError):
     pass
@@ -110,7 +112,8 @@ class FMRunConfig:
         return FMConfig(vocabulary_size=self.vocabulary_size, factor_num=self.factor_num, loss_type=self.loss_type,
                         factor_lambda=self.factor_lambda, bias_lambda=self.bias_lambda, batch_size=self.batch_size,
                         init_value_range=self.init_value_range, seed=self.seed,
-                        dtype=torch.bfloat16 if self.dtype == "bf16" else torch.float32, opt=opt, mode=self.mode,
+                        dtype={"fp32": torch.float32, "bf16": torch.bfloat16,
+                               "fp8": torch.float8_e4m3fn}[self.dtype], opt=opt, mode=self.mode,
                         grad_reduce=self.grad_reduce, dedup_chunk=self.dedup_chunk)
 
 
@@ -184,8 +187,8 @@ def load_config(config_file: str, *, echo: bool = True, printer=print) -> FMRunC
         raise ConfigError("loss_type must be 'logistic' or 'mse', got %r" % c.loss_type)
     if c.optimizer not in ("adagrad", "ftrl", "sgd"):
         raise ConfigError("optimizer must be adagrad|ftrl|sgd, got %r" % c.optimizer)
-    if c.dtype not in ("fp32", "bf16"):
-        raise ConfigError("dtype must be fp32|bf16, got %r" % c.dtype)
+    if c.dtype not in _TABLE_DTYPES:
+        raise ConfigError("dtype must be fp32|bf16|fp8, got %r" % c.dtype)
 
     c.train_files = _expand(read_list(TRAIN, "train_files"), base_dir)
     wf = read_list(TRAIN, "weight_files", required=False)

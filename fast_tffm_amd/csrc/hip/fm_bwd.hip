@@ -84,6 +84,11 @@ __device__ inline void bwd_load_row(const BwdArgs& a, long long row, int tE, Row
   r.row = row;
   F::load(reinterpret_cast<const TV*>(a.v) + r.row * a.v_stride + tE * EPL, r.vv);
   r.wv = a.w[r.row * a.w_stride];
+  if constexpr (F::kScaled) {
+    const float s = row_scale<TV>(a.w, r.row, a.w_stride);
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) r.vv[k] *= s;
+  }
   if (a.mode == kBwdEmit) return;
   const float* s0 = a.s0v + r.row * a.s_stride + tE * EPL;
 #pragma unroll
@@ -107,7 +112,7 @@ __device__ inline void bwd_load_row(const BwdArgs& a, long long row, int tE, Row
   }
 }
 
-template <typename TV, int EPL>
+template <int LPR, typename TV, int EPL>
 __device__ inline void bwd_finish(const BwdArgs& a, int u, int t, bool tact, RowState<EPL>& r,
                                   const float (&A)[EPL], float Scx, float Sc, int n_u) {
   using F = Frag<TV>;
@@ -128,8 +133,9 @@ __device__ inline void bwd_finish(const BwdArgs& a, int u, int t, bool tact, Row
   }
 #pragma unroll
   for (int k = 0; k < EPL; ++k) opt_step(a.opt, gr[k], r.vv[k], r.st0[k], r.st1[k]);
+  store_row<LPR, TV>(reinterpret_cast<TV*>(a.v) + r.row * a.v_stride + t * EPL, r.vv, a.w, r.row, a.w_stride, t,
+                     tact);
   if (tact) {
-    F::store(reinterpret_cast<TV*>(a.v) + r.row * a.v_stride + t * EPL, r.vv);
     float* s0 = a.s0v + r.row * a.s_stride + t * EPL;
 #pragma unroll
     for (int k = 0; k < EPL; k += 4)
@@ -149,12 +155,12 @@ __device__ inline void bwd_finish(const BwdArgs& a, int u, int t, bool tact, Row
   }
 }
 
-template <typename TV, int EPL>
+template <int LPR, typename TV, int EPL>
 __device__ inline void bwd_finalize(const BwdArgs& a, int u, int t, bool tact, int tE,
                                     const float (&A)[EPL], float Scx, float Sc, int n_u) {
   RowState<EPL> r;
   bwd_load_row<TV, EPL>(a, a.mode == kBwdLocal ? (long long)a.uniq[u] : (long long)u, tE, r);
-  bwd_finish<TV, EPL>(a, u, t, tact, r, A, Scx, Sc, n_u);
+  bwd_finish<LPR, TV, EPL>(a, u, t, tact, r, A, Scx, Sc, n_u);
 }
 
 // One lane group per chunk of <= CH (<= kMaxCH) sorted occurrences of one row.
@@ -257,7 +263,7 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_chunk_kernel(BwdArgs a) {
       }
     }
     if (single) {
-      bwd_finish<TV, EPL>(a, u, t, tact, rs, A, Scx, Sc, len);
+      bwd_finish<LPR, TV, EPL>(a, u, t, tact, rs, A, Scx, Sc, len);
     } else {
       float* dst = a.partial + (long long)cc * (a.Kp + 4);
       if (tact) {
@@ -327,7 +333,7 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_combine_kernel(BwdArgs a) {
         Sc += pt[q];
       }
     }
-    bwd_finalize<TV, EPL>(a, u, t, tact, tE, A, Scx, Sc, a.seg_start[u + 1] - a.seg_start[u]);
+    bwd_finalize<LPR, TV, EPL>(a, u, t, tact, tE, A, Scx, Sc, a.seg_start[u + 1] - a.seg_start[u]);
   }
 }
 
@@ -397,7 +403,7 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_big_kernel(BwdArgs a) {
         Scx += o[LPR * EPL];
         Sc += o[LPR * EPL + 1];
       }
-      bwd_finalize<TV, EPL>(a, u, t, tact, tE, A, Scx, Sc, a.seg_start[u + 1] - a.seg_start[u]);
+      bwd_finalize<LPR, TV, EPL>(a, u, t, tact, tE, A, Scx, Sc, a.seg_start[u + 1] - a.seg_start[u]);
     }
     __syncthreads();
   }

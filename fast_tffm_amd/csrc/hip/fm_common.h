@@ -27,13 +27,21 @@ constexpr unsigned kChunkSingle = 1u << 31;  // the segment's only chunk
 
 enum LossType : int { kLossNone = 0, kLossMse = 1, kLossLogistic = 2 };
 enum OptType : int { kOptAdagrad = 0, kOptFtrl = 1, kOptSgd = 2 };
-enum DType : int { kF32 = 0, kBF16 = 1 };
+enum DType : int { kF32 = 0, kBF16 = 1, kFP8 = 2 };
+
+// fp8 table storage: OCP e4m3 (gfx950 v_cvt_pk_*_fp8) with one fp32 scale per
+// row, stored next to the row's linear weight (w[row * w_stride + 1], w_stride
+// = 2), so the scale arrives with the w load.  A row is quantised as
+// q = v / s with s = max|v| / kFp8Max (round to nearest even).
+struct fp8e4m3 { uint8_t bits; };
+constexpr float kFp8Max = 448.f;
 
 // ---- 16-byte row fragments ------------------------------------------------
 template <typename T> struct Frag;
 
 template <> struct Frag<float> {
   static constexpr int N = 4;  // elements per lane
+  static constexpr bool kScaled = false;
   __device__ static inline void load(const float* p, float (&o)[4]) {
     const float4 v = *reinterpret_cast<const float4*>(p);
     o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
@@ -53,6 +61,7 @@ __device__ inline uint32_t f32_to_bf16_bits(float f) {
 
 template <> struct Frag<__hip_bfloat16> {
   static constexpr int N = 8;
+  static constexpr bool kScaled = false;
   __device__ static inline void load(const __hip_bfloat16* p, float (&o)[8]) {
     const uint4 v = *reinterpret_cast<const uint4*>(p);
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -72,12 +81,67 @@ template <> struct Frag<__hip_bfloat16> {
   }
 };
 
+// 4 fp8 per lane (a 4-byte load: a K=128 row is one 32-lane instruction, the
+// same lane mapping and register footprint as fp32); values are unscaled here.
+template <> struct Frag<fp8e4m3> {
+  static constexpr int N = 4;
+  static constexpr bool kScaled = true;
+  __device__ static inline void load(const fp8e4m3* p, float (&o)[4]) {
+    const int u = *reinterpret_cast<const int*>(p);
+    const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8(u, false);
+    const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8(u, true);
+    o[0] = lo[0]; o[1] = lo[1]; o[2] = hi[0]; o[3] = hi[1];
+  }
+  __device__ static inline void store(fp8e4m3* p, const float (&o)[4]) {
+    int u = __builtin_amdgcn_cvt_pk_fp8_f32(o[0], o[1], 0, false);
+    u = __builtin_amdgcn_cvt_pk_fp8_f32(o[2], o[3], u, true);
+    *reinterpret_cast<int*>(p) = u;
+  }
+};
+
 // ---- wave reductions (xor butterfly inside a lane group) -------------------
 template <int WIDTH>
 __device__ inline float group_sum(float v) {
 #pragma unroll
   for (int o = WIDTH / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
   return v;
+}
+
+template <int WIDTH>
+__device__ inline float group_max(float v) {
+#pragma unroll
+  for (int o = WIDTH / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+// Dequantisation factor of a table row (1 for unscaled dtypes).
+template <typename TV>
+__device__ inline float row_scale(const float* w, long long row, long long w_stride) {
+  if constexpr (Frag<TV>::kScaled) return w[row * w_stride + 1];
+  return 1.f;
+}
+
+// Store this lane's EPL fp32 values of a row (every lane of the LPR group must
+// call: scaled dtypes reduce the row's max |v| over the group first).
+template <int LPR, typename TV>
+__device__ inline void store_row(TV* lane_ptr, const float (&o)[Frag<TV>::N], float* w, long long row,
+                                 long long w_stride, int t, bool tact) {
+  using F = Frag<TV>;
+  if constexpr (F::kScaled) {
+    float m = 0.f;
+#pragma unroll
+    for (int k = 0; k < F::N; ++k) m = fmaxf(m, fabsf(o[k]));
+    m = group_max<LPR>(m);
+    const float s = m > 0.f ? m / kFp8Max : 1.f;
+    const float inv = 1.f / s;
+    float q[F::N];
+#pragma unroll
+    for (int k = 0; k < F::N; ++k) q[k] = fminf(fmaxf(o[k] * inv, -kFp8Max), kFp8Max);
+    if (tact) F::store(lane_ptr, q);
+    if (t == 0) w[row * w_stride + 1] = s;
+  } else {
+    if (tact) F::store(lane_ptr, o);
+  }
 }
 
 // Sum over the row groups of a wave: lanes t, t+LPR, t+2*LPR, ...
@@ -126,7 +190,7 @@ __device__ inline void opt_step(const OptParams& o, float g, float& p, float& s0
 inline int next_pow2(int x) { int p = 1; while (p < x) p <<= 1; return p; }
 
 inline int lanes_per_row(int Kp, int dtype) {
-  const int epl = dtype == kBF16 ? 8 : 4;
+  const int epl = dtype == kBF16 ? 8 : 4;  // fp32: 16 B, bf16: 16 B, fp8: 4 B per lane
   return next_pow2((Kp + epl - 1) / epl);
 }
 
@@ -152,6 +216,8 @@ inline int fill_grid(long long work_groups, int groups_per_block, int cap = 8192
 #define FM_DISPATCH(DTYPE, LPR_VAL, KERNEL, GRID, STREAM, ARGS)                       \
   if ((DTYPE) == kBF16) {                                                            \
     FM_DISPATCH_LPR(LPR_VAL, KERNEL, __hip_bfloat16, GRID, STREAM, ARGS)             \
+  } else if ((DTYPE) == kFP8) {                                                      \
+    FM_DISPATCH_LPR(LPR_VAL, KERNEL, fp8e4m3, GRID, STREAM, ARGS)                    \
   } else {                                                                           \
     FM_DISPATCH_LPR(LPR_VAL, KERNEL, float, GRID, STREAM, ARGS)                      \
   }

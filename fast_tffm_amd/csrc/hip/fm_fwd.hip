@@ -76,7 +76,7 @@ __global__ __launch_bounds__(kBlock) void fm_fwd_kernel(FwdArgs a) {
         my_x = a.vals ? a.vals[base + lane] : 1.f;
       }
       for (int q = 0; q < m; q += G * UNR) {
-        float fr[UNR][EPL], fw[UNR], fx[UNR];
+        float fr[UNR][EPL], fw[UNR], fx[UNR], fs[UNR];
         // Issue every row load of the round before the first use.  Loads are
         // unconditional (slots past the example re-read a valid row of it and are
         // masked to zero afterwards), so hipcc keeps all UNR loads in flight.
@@ -89,9 +89,14 @@ __global__ __launch_bounds__(kBlock) void fm_fwd_kernel(FwdArgs a) {
           fx[u] = f < m ? x : 0.f;
           F::load(vbase + (long long)row * a.v_stride, fr[u]);
           fw[u] = a.w[(long long)row * a.w_stride];
+          fs[u] = row_scale<TV>(a.w, row, a.w_stride);  // (fp8: same cache line as w)
         }
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
+          if constexpr (F::kScaled) {
+#pragma unroll
+            for (int k = 0; k < EPL; ++k) fr[u][k] *= fs[u];
+          }
           const float xm = fx[u] * tmask;
 #pragma unroll
           for (int k = 0; k < EPL; ++k) {

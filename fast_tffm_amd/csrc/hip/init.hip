@@ -40,8 +40,37 @@ __global__ __launch_bounds__(kBlock) void init_rows_kernel(InitArgs a) {
   }
 }
 
+// fp8 rows: one thread per row (the row's scale needs its max |v| first, so
+// the values are generated twice; init runs once).
+__global__ __launch_bounds__(kBlock) void init_rows_fp8_kernel(InitArgs a) {
+  for (long long r = (long long)blockIdx.x * kBlock + threadIdx.x; r < a.rows; r += (long long)gridDim.x * kBlock) {
+    const long long gid = r * a.gid_mul + a.gid_add;
+    float m = 0.f;
+    for (int c = 0; c < a.K; ++c) m = fmaxf(m, fabsf(init_uniform(a.seed, gid, c + 1, a.range)));
+    const float s = m > 0.f ? m / kFp8Max : 1.f;
+    int* dst = reinterpret_cast<int*>(reinterpret_cast<uint8_t*>(a.v) + r * a.v_stride);
+    for (int c = 0; c < a.Kp; c += 4) {
+      float q[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        q[k] = c + k < a.K ? fminf(fmaxf(init_uniform(a.seed, gid, c + k + 1, a.range) / s, -kFp8Max), kFp8Max) : 0.f;
+      int u = __builtin_amdgcn_cvt_pk_fp8_f32(q[0], q[1], 0, false);
+      dst[c / 4] = __builtin_amdgcn_cvt_pk_fp8_f32(q[2], q[3], u, true);
+    }
+    a.w[r * a.w_stride] = init_uniform(a.seed, gid, 0, a.range);
+    a.w[r * a.w_stride + 1] = s;
+  }
+}
+
 int launch_init_rows(const InitArgs& a, hipStream_t st) {
   if (a.rows <= 0) return 0;
+  if (a.dtype == kFP8) {
+    if (a.Kp % 4 != 0 || a.w_stride < 2) return -1;
+    long long blocks = (a.rows + kBlock - 1) / kBlock;
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(init_rows_fp8_kernel, dim3((int)blocks), dim3(kBlock), 0, st, a);
+    return (int)hipGetLastError();
+  }
   const long long total = a.rows * (long long)(a.Kp + 1);
   long long blocks = (total + kBlock - 1) / kBlock;
   if (blocks > 16384) blocks = 16384;

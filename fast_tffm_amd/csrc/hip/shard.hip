@@ -34,6 +34,11 @@ __global__ __launch_bounds__(kBlock) void gather_rows_kernel(GatherArgs a) {
     const long long row = a.req[p];
     float vv[EPL];
     F::load(reinterpret_cast<const TV*>(a.v) + row * a.v_stride + tE * EPL, vv);
+    if constexpr (F::kScaled) {
+      const float s = row_scale<TV>(a.w, row, a.w_stride);
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) vv[k] *= s;
+    }
     float* dst = a.out + (long long)p * a.o_stride;
     if (tact) {
 #pragma unroll
@@ -82,6 +87,11 @@ __global__ __launch_bounds__(kBlock) void apply_rows_kernel(ApplyArgs a) {
     TV* vrow = reinterpret_cast<TV*>(a.v) + row * a.v_stride + tE * EPL;
     float vv[EPL], st0[EPL], st1[EPL];
     F::load(vrow, vv);
+    if constexpr (F::kScaled) {
+      const float s = row_scale<TV>(a.w, row, a.w_stride);
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) vv[k] *= s;
+    }
     float* s0 = a.s0v + row * a.s_stride + tE * EPL;
     float* s1 = a.s1v ? a.s1v + row * a.s_stride + tE * EPL : nullptr;
 #pragma unroll
@@ -109,8 +119,8 @@ __global__ __launch_bounds__(kBlock) void apply_rows_kernel(ApplyArgs a) {
     }
 #pragma unroll
     for (int k = 0; k < EPL; ++k) opt_step(a.opt, gr[k], vv[k], st0[k], st1[k]);
+    store_row<LPR, TV>(vrow, vv, a.w, row, a.w_stride, t, tact);
     if (tact) {
-      F::store(vrow, vv);
 #pragma unroll
       for (int k = 0; k < EPL; k += 4) {
         *reinterpret_cast<float4*>(s0 + k) = make_float4(st0[k], st0[k + 1], st0[k + 2], st0[k + 3]);

@@ -9,8 +9,11 @@ Here one process owns one *shard* of rows with the same "mod" rule over the
 data-parallel world (``owner = g % world``, ``local row = g // world``).  The
 storage is HBM-friendly rather than reference-shaped:
 
-* ``v``   [rows, Kp]  fp32 or bf16, Kp = K padded to 16-byte rows (pads are 0);
+* ``v``   [rows, Kp]  fp32, bf16 or fp8 (OCP e4m3, GPU only), Kp = K padded to
+  whole lanes (pads are 0);
 * ``w``   [rows]      fp32 (linear weight, kept separate so v rows stay aligned);
+  fp8 tables store [w, scale] pairs (``wx`` [rows, 2], ``w`` = wx[:, 0]) so the
+  row's dequantisation scale arrives with w;
 * ``s0v``/``s0w``     optimizer slot 0 (Adagrad accumulator / FTRL n), fp32;
 * ``s1v``/``s1w``     optimizer slot 1 (FTRL z), fp32.
 
@@ -51,8 +54,19 @@ class FMTable:
         self.init_range = float(init_range)
         self.seed = int(seed)
         dev = self.device
+        self.fp8 = dtype == K.FP8
+        if self.fp8 and self.device.type != "cuda":
+            raise ValueError("fp8 tables run on the GPU kernels only")
         self.v = torch.zeros((self.rows, self.Kp), dtype=dtype, device=dev)
-        self.w = torch.zeros(self.rows, dtype=torch.float32, device=dev)
+        if self.fp8:
+            self.wx = torch.zeros((self.rows, 2), dtype=torch.float32, device=dev)
+            self.wx[:, 1] = 1.0
+            self.w = self.wx[:, 0]          # stride 2: the kernels read the scale at w[row * 2 + 1]
+            self.scale = self.wx[:, 1]
+        else:
+            self.wx = None
+            self.w = torch.zeros(self.rows, dtype=torch.float32, device=dev)
+            self.scale = None
         acc0 = float(self.opt.initial_accumulator)
         n_state = max(1, self.opt.n_state)  # kernels always address slot 0
         self.s0v = torch.full((self.rows, self.Kp), acc0 if self.opt.name in ("adagrad", "ftrl") else 0.0,
@@ -72,7 +86,7 @@ class FMTable:
     def reinit(self, seed: int | None = None) -> None:
         """U(-r, r) over w and v[:K] as a pure function of (seed, global id, column)."""
         seed = self.seed if seed is None else int(seed)
-        args = dict(v=self.v.data_ptr(), v_stride=self.v.stride(0), w=self.w.data_ptr(), w_stride=1,
+        args = dict(v=self.v.data_ptr(), v_stride=self.v.stride(0), w=self.w.data_ptr(), w_stride=self.w.stride(0),
                     rows=self.rows, K=self.K, Kp=self.Kp, dtype=K.dtype_code(self.dtype), gid_mul=self.world,
                     gid_add=self.rank, seed=seed & 0xFFFFFFFFFFFFFFFF, range=self.init_range)
         if self.device.type == "cuda":
@@ -87,13 +101,15 @@ class FMTable:
         if real < self.rows:
             self.v[real:].zero_()
             self.w[real:].zero_()
+            if self.scale is not None:
+                self.scale[real:] = 1.0
 
     def global_ids(self) -> torch.Tensor:
         return torch.arange(self.rows, device=self.device, dtype=torch.int64) * self.world + self.rank
 
     def nbytes(self) -> int:
         tot = 0
-        for t in (self.v, self.w, self.s0v, self.s0w, self.s1v, self.s1w):
+        for t in (self.v, self.wx if self.fp8 else self.w, self.s0v, self.s0w, self.s1v, self.s1w):
             if t is not None:
                 tot += t.numel() * t.element_size()
         return tot
@@ -102,17 +118,43 @@ class FMTable:
     def reference_rows(self, local_rows: torch.Tensor | None = None) -> torch.Tensor:
         """Rows in the reference layout [n, K+1] (col 0 = w, cols 1..K = v), fp32."""
         if local_rows is None:
-            v, w = self.v, self.w
+            v, w = self.dense_v(), self.w
         else:
-            v, w = self.v[local_rows], self.w[local_rows]
+            v, w = self.dense_v(local_rows), self.w[local_rows]
         return torch.cat([w.unsqueeze(1), v[:, : self.K].float()], dim=1)
+
+    def dense_v(self, local_rows: torch.Tensor | None = None) -> torch.Tensor:
+        """v rows as fp32 values (fp8: dequantised with the row scales)."""
+        v = self.v if local_rows is None else self.v[local_rows]
+        if not self.fp8:
+            return v
+        s = self.scale if local_rows is None else self.scale[local_rows]
+        return v.float() * s[:, None]
+
+    def set_v(self, local_rows: torch.Tensor | None, vals: torch.Tensor) -> None:
+        """Write fp32 values into v[:, :K] (fp8: re-quantised per row, pads stay 0)."""
+        if self.fp8:
+            n = vals.shape[0]
+            full = torch.zeros((n, self.Kp), dtype=torch.float32, device=self.device)
+            full[:, : self.K] = vals.to(self.device, torch.float32)
+            q, s = K.quantize_fp8_rows(full)
+            if local_rows is None:
+                self.v[:n], self.scale[:n] = q, s
+            else:
+                self.v[local_rows], self.scale[local_rows] = q, s
+            return
+        vals = vals.to(self.device, self.dtype)
+        if local_rows is None:
+            self.v[: vals.shape[0], : self.K] = vals
+        else:
+            self.v[local_rows, : self.K] = vals
 
     def load_reference_rows(self, local_rows: torch.Tensor, rows_ref: torch.Tensor,
                             acc_ref: torch.Tensor | None = None) -> None:
         """Write reference-layout rows ([n, K+1]) and optional Adagrad slot rows into this shard."""
         rows_ref = rows_ref.to(self.device, torch.float32)
         self.w[local_rows] = rows_ref[:, 0]
-        self.v[local_rows, : self.K] = rows_ref[:, 1:].to(self.dtype)
+        self.set_v(local_rows, rows_ref[:, 1:])
         if acc_ref is not None:
             acc_ref = acc_ref.to(self.device, torch.float32)
             self.s0w[local_rows] = acc_ref[:, 0]

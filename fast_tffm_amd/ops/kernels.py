@@ -37,22 +37,38 @@ def set_debug_checks(on: bool) -> None:
     _DEBUG = bool(on)
 
 
+FP8 = torch.float8_e4m3fn   # OCP e4m3 table storage (+ fp32 scale per row), GPU only
+FP8_MAX = 448.0
+
+
 def dtype_code(t: torch.dtype) -> int:
     if t == torch.float32:
         return 0
     if t == torch.bfloat16:
         return 1
-    raise TypeError(f"unsupported table dtype {t}; use float32 or bfloat16")
+    if t == FP8:
+        return 2
+    raise TypeError(f"unsupported table dtype {t}; use float32, bfloat16 or float8_e4m3fn")
 
 
 def elems_per_lane(dtype: torch.dtype) -> int:
-    return 16 // torch.tensor([], dtype=dtype).element_size()
+    """Table elements one lane moves per row access: 16 B (fp32, bf16) or 4 B (fp8)."""
+    return 4 if dtype == FP8 else 16 // torch.tensor([], dtype=dtype).element_size()
 
 
 def padded_k(K: int, dtype: torch.dtype = torch.float32) -> int:
-    """Factor columns stored per row: K rounded up to a 16-byte multiple (and at least 8)."""
-    e = max(elems_per_lane(dtype), 8) if dtype == torch.bfloat16 else elems_per_lane(dtype)
+    """Factor columns stored per row: K rounded up to whole lanes (bf16: at least 8)."""
+    e = elems_per_lane(dtype)
     return ((K + e - 1) // e) * e
+
+
+def quantize_fp8_rows(vals: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """Per-row fp8 quantisation (the kernels' store_row): scale = max|v| / 448, q = rne(v / scale)."""
+    v = vals.float()
+    m = v.abs().amax(dim=1) if v.shape[1] else torch.zeros(v.shape[0], device=v.device)
+    s = torch.where(m > 0, m / FP8_MAX, torch.ones_like(m))
+    q = (v / s[:, None]).clamp(-FP8_MAX, FP8_MAX).to(FP8)
+    return q, s
 
 
 @dataclass

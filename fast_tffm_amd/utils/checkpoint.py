@@ -62,7 +62,10 @@ def latest_checkpoint(log_dir: str | None) -> str | None:
 
 def _table_tensors(table) -> dict[str, torch.Tensor]:
     K = table.K
-    t = {"w": table.w, "v": table.v[:, :K], "s0w": table.s0w, "s0v": table.s0v[:, :K]}
+    t = {"w": table.w, "v": table.dense_v()[:, :K], "s0w": table.s0w, "s0v": table.s0v[:, :K]}
+    if table.fp8:  # exact fp8 payload + scales next to the portable fp32 values
+        t["v_fp8"] = table.v.view(torch.uint8)
+        t["v_scale"] = table.scale
     if table.s1v is not None:
         t["s1w"] = table.s1w
         t["s1v"] = table.s1v[:, :K]
@@ -182,7 +185,13 @@ def _copy_rows(table, local_rows, t: dict, K: int, dev) -> None:
                 dst[local_rows] = src
 
     put(table.w, t.get("w"))
-    put(table.v, t.get("v"), cols=True)
+    if table.fp8 and "v_fp8" in t:
+        put(table.v.view(torch.uint8), t["v_fp8"])
+        put(table.scale, t["v_scale"])
+    elif table.fp8:
+        table.set_v(local_rows, t["v"].float())
+    else:
+        put(table.v, t.get("v"), cols=True)
     put(table.s0w, t.get("s0w"))
     put(table.s0v, t.get("s0v"), cols=True)
     put(table.s1w, t.get("s1w"))
