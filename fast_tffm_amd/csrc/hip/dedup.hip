@@ -38,13 +38,15 @@ struct RleArgs {
   int slice_shift;                // example slice = ex >> slice_shift; < 0: no slicing
   int nslices;                    // example slices (<= kMaxSlices)
   int hot;                        // a row is "hot" at j when skeys[j -/+ hot] has its key (multiple of 8)
+  int dense_min;                  // rows with >= dense_min occurrences are "dense" (0: none)
+  int* dense_list;                // [kMaxDense] segment ids of the first dense rows in key order
   const uint32_t* skeys;          // sorted keys
   const int* spay;                // sorted payload (occurrence or example index)
   const int* sex;                 // sorted example index (== spay when the payload is the example), or null
   int ex_shift;                   // > 0: payload / ex_of_occ hold packed codes (example << ex_shift | slot)
   const int* offsets;             // [B+1] CSR offsets (packed codes -> occurrence index)
-  unsigned* tile_cnt;             // [2][ntiles] heads, chunk starts per tile
-  unsigned* tile_off;             // [2][ntiles] exclusive offsets
+  unsigned* tile_cnt;             // [3][ntiles] heads, chunk starts, dense heads per tile
+  unsigned* tile_off;             // [3][ntiles] exclusive offsets
   unsigned* slice_cnt;            // [nslices][ntiles] chunks per (slice, tile)
   uint32_t* uniq;                 // [n] unique keys (first U valid)
   int* seg_start;                 // [n+1]
@@ -127,87 +129,117 @@ __device__ inline void rle_flags8(const RleArgs& a, int j0, Rle8& r) {
   }
 }
 
+// Head of a row with at least dense_min occurrences (the MFMA backward path, fm_bwd.hip).
+__device__ inline bool dense_head(const RleArgs& a, int j, uint32_t k) {
+  return a.dense_min > 0 && j + a.dense_min - 1 < a.n && a.skeys[j + a.dense_min - 1] == k;
+}
+
 __device__ inline int chunk_slice(const RleArgs& a, bool hot, int ex, int c) {
   return hot ? min(ex >> a.slice_shift, a.nslices - 1) : c % a.nslices;
 }
 
-// Block-wide exclusive scan of two per-thread counts (packed in one u32 pair).
-__device__ inline void block_excl_scan2(unsigned h, unsigned c, unsigned& h_ex, unsigned& c_ex, unsigned& h_tot,
-                                        unsigned& c_tot) {
-  __shared__ unsigned sh[2][kWavesPerBlock];
+// Block-wide exclusive scan of NC per-thread counts (segment heads, chunk
+// starts, dense-row heads).
+template <int NC>
+__device__ inline void block_excl_scan(const unsigned (&v)[NC], unsigned (&ex)[NC], unsigned (&tot)[NC]) {
+  __shared__ unsigned sh[NC][kWavesPerBlock];
   const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x >> 6;
-  unsigned hi = h, ci = c;  // inclusive wave scan
+  unsigned inc[NC];  // inclusive wave scan
+#pragma unroll
+  for (int i = 0; i < NC; ++i) inc[i] = v[i];
 #pragma unroll
   for (int o = 1; o < kWave; o <<= 1) {
-    const unsigned hs = __shfl_up(hi, o, kWave), cs = __shfl_up(ci, o, kWave);
-    if (lane >= o) { hi += hs; ci += cs; }
-  }
-  if (lane == kWave - 1) { sh[0][wv] = hi; sh[1][wv] = ci; }
-  __syncthreads();
-  unsigned hb = 0, cb = 0;
-  h_tot = c_tot = 0;
 #pragma unroll
-  for (int w = 0; w < kWavesPerBlock; ++w) {
-    if (w < wv) { hb += sh[0][w]; cb += sh[1][w]; }
-    h_tot += sh[0][w];
-    c_tot += sh[1][w];
+    for (int i = 0; i < NC; ++i) {
+      const unsigned up = __shfl_up(inc[i], o, kWave);
+      if (lane >= o) inc[i] += up;
+    }
   }
-  h_ex = hb + hi - h;
-  c_ex = cb + ci - c;
+  if (lane == kWave - 1) {
+#pragma unroll
+    for (int i = 0; i < NC; ++i) sh[i][wv] = inc[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    unsigned b = 0, t = 0;
+#pragma unroll
+    for (int w = 0; w < kWavesPerBlock; ++w) {
+      if (w < wv) b += sh[i][w];
+      t += sh[i][w];
+    }
+    ex[i] = b + inc[i] - v[i];
+    tot[i] = t;
+  }
   __syncthreads();
 }
 
 __global__ __launch_bounds__(kBlock) void rle_tile_count_kernel(RleArgs a) {
   const int tile = blockIdx.x;
   Rle8 r;
-  rle_flags8(a, tile * kRleTile + threadIdx.x * kRleItems, r);
-  unsigned h = 0, c = 0;
+  const int j0 = tile * kRleTile + threadIdx.x * kRleItems;
+  rle_flags8(a, j0, r);
+  unsigned v[3] = {0u, 0u, 0u}, ex[3], tot[3];
 #pragma unroll
-  for (int q = 0; q < kRleItems; ++q) { h += r.hd[q]; c += r.cs[q]; }
-  unsigned he, ce, ht, ct;
-  block_excl_scan2(h, c, he, ce, ht, ct);
+  for (int q = 0; q < kRleItems; ++q) {
+    v[0] += r.hd[q];
+    v[1] += r.cs[q];
+    v[2] += r.hd[q] && dense_head(a, j0 + q, r.k[q]);
+  }
+  block_excl_scan<3>(v, ex, tot);
   if (threadIdx.x == 0) {
-    a.tile_cnt[tile] = ht;
-    a.tile_cnt[a.ntiles + tile] = ct;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) a.tile_cnt[i * a.ntiles + tile] = tot[i];
   }
 }
 
 // One workgroup of 1024 threads: exclusive scan of the tile totals.
 __global__ __launch_bounds__(1024) void rle_tile_scan_kernel(RleArgs a) {
-  __shared__ unsigned carry[2];
-  __shared__ unsigned wsum[2][16];
-  if (threadIdx.x == 0) { carry[0] = 0; carry[1] = 0; }
+  __shared__ unsigned carry[3];
+  __shared__ unsigned wsum[3][16];
+  if (threadIdx.x < 3) carry[threadIdx.x] = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (int base = 0; base < a.ntiles; base += 1024) {
     const int t = base + threadIdx.x;
-    const unsigned h = t < a.ntiles ? a.tile_cnt[t] : 0u;
-    const unsigned c = t < a.ntiles ? a.tile_cnt[a.ntiles + t] : 0u;
-    unsigned hi = h, ci = c;
+    unsigned v[3], inc[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) inc[i] = v[i] = t < a.ntiles ? a.tile_cnt[i * a.ntiles + t] : 0u;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-      const unsigned hs = __shfl_up(hi, o, 64), cs = __shfl_up(ci, o, 64);
-      if (lane >= o) { hi += hs; ci += cs; }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const unsigned up = __shfl_up(inc[i], o, 64);
+        if (lane >= o) inc[i] += up;
+      }
     }
-    if (lane == 63) { wsum[0][wv] = hi; wsum[1][wv] = ci; }
-    __syncthreads();
-    unsigned hb = carry[0], cb = carry[1], ht = 0, ct = 0;
-    for (int w = 0; w < 16; ++w) {
-      if (w < wv) { hb += wsum[0][w]; cb += wsum[1][w]; }
-      ht += wsum[0][w];
-      ct += wsum[1][w];
-    }
-    if (t < a.ntiles) {
-      a.tile_off[t] = hb + hi - h;
-      a.tile_off[a.ntiles + t] = cb + ci - c;
+    if (lane == 63) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) wsum[i][wv] = inc[i];
     }
     __syncthreads();
-    if (threadIdx.x == 0) { carry[0] += ht; carry[1] += ct; }
+    unsigned b[3], tot[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      b[i] = carry[i];
+      tot[i] = 0;
+      for (int w = 0; w < 16; ++w) {
+        if (w < wv) b[i] += wsum[i][w];
+        tot[i] += wsum[i][w];
+      }
+      if (t < a.ntiles) a.tile_off[i * a.ntiles + t] = b[i] + inc[i] - v[i];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) carry[i] += tot[i];
+    }
     __syncthreads();
   }
   if (threadIdx.x == 0) {
     a.counts[0] = (int)carry[0];
     a.counts[1] = (int)carry[1];
+    a.counts[3] = (int)carry[2];  // dense rows (all of them; the first kMaxDense are listed)
     a.seg_start[carry[0]] = a.n;
     a.seg_chunk[carry[0]] = (int)carry[1];
     a.chunk_start[carry[1]] = a.n;
@@ -223,14 +255,20 @@ __global__ __launch_bounds__(kBlock) void rle_tile_emit_kernel(RleArgs a) {
     for (int sl = threadIdx.x; sl < kMaxSlices; sl += kBlock) sc[sl] = 0;
   Rle8 r;
   rle_flags8(a, j0, r);
-  unsigned h = 0, c = 0;
+  unsigned v[3] = {0u, 0u, 0u}, ex[3], tot[3];
+  bool dn[kRleItems];
 #pragma unroll
-  for (int q = 0; q < kRleItems; ++q) { h += r.hd[q]; c += r.cs[q]; }
-  unsigned he, ce, ht, ct;
-  block_excl_scan2(h, c, he, ce, ht, ct);  // (its barriers also order the sc[] reset)
-  // running (inclusive) segment / chunk ids of this thread's elements
-  int s = (int)(a.tile_off[tile] + he) - 1;
-  int ch = (int)(a.tile_off[a.ntiles + tile] + ce) - 1;
+  for (int q = 0; q < kRleItems; ++q) {
+    dn[q] = r.hd[q] && dense_head(a, j0 + q, r.k[q]);
+    v[0] += r.hd[q];
+    v[1] += r.cs[q];
+    v[2] += dn[q];
+  }
+  block_excl_scan<3>(v, ex, tot);  // (its barriers also order the sc[] reset)
+  // running (inclusive) segment / chunk / dense-row ids of this thread's elements
+  int s = (int)(a.tile_off[tile] + ex[0]) - 1;
+  int ch = (int)(a.tile_off[a.ntiles + tile] + ex[1]) - 1;
+  int dslot = (int)(a.tile_off[2 * a.ntiles + tile] + ex[2]);
   int sq[kRleItems];
 #pragma unroll
   for (int q = 0; q < kRleItems; ++q) {
@@ -243,6 +281,10 @@ __global__ __launch_bounds__(kBlock) void rle_tile_emit_kernel(RleArgs a) {
       a.uniq[s] = r.k[q];
       a.seg_start[s] = j;
       a.seg_chunk[s] = ch;
+      if (dn[q]) {  // dense rows in key order: the first kMaxDense take the MFMA path
+        if (dslot < kMaxDense) a.dense_list[dslot] = s;
+        ++dslot;
+      }
     }
     if (r.cs[q]) {
       // a head chunk is the row's only one iff the row ends before the next CH-aligned cut
@@ -284,6 +326,15 @@ __global__ __launch_bounds__(kBlock) void rle_tile_emit_kernel(RleArgs a) {
     __syncthreads();
     for (int sl = threadIdx.x; sl < a.nslices; sl += kBlock) a.slice_cnt[sl * a.ntiles + tile] = sc[sl];
   }
+}
+
+// Flag every chunk of a listed dense row: the chunk kernel skips them (their
+// gradient comes from the MFMA path).
+__global__ __launch_bounds__(kBlock) void mark_dense_chunks_kernel(RleArgs a) {
+  const int nd = min(a.counts[3], kMaxDense);
+  if ((int)blockIdx.x >= nd) return;
+  const int u = a.dense_list[blockIdx.x];
+  for (int c = a.seg_chunk[u] + threadIdx.x; c < a.seg_chunk[u + 1]; c += kBlock) a.chunk_seg[c] |= kChunkDense;
 }
 
 static size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
@@ -369,11 +420,11 @@ static size_t sort_temp_bytes(int n, hipStream_t st) {
   return align_up(best);
 }
 
-// Workspace layout: [rocprim sort temp | tile_cnt(2*ntiles) | tile_off(2*ntiles) | slice scan temp | cnt | off]
+// Workspace layout: [rocprim sort temp | tile_cnt(3*ntiles) | tile_off(3*ntiles) | slice scan temp | cnt | off]
 size_t dedup_workspace_bytes(int n) {
   if (n <= 0) return 256;
   const size_t ntiles = ((size_t)n + kRleTile - 1) / kRleTile;
-  return sort_temp_bytes(n, 0) + 2 * align_up(2 * ntiles * sizeof(unsigned)) + slice_scan_bytes(n) + 256;
+  return sort_temp_bytes(n, 0) + 2 * align_up(3 * ntiles * sizeof(unsigned)) + slice_scan_bytes(n) + 256;
 }
 
 struct DedupArgs {
@@ -400,6 +451,8 @@ struct DedupArgs {
   int ex_shift;            // > 0: the payload is the packed code (example << ex_shift | slot), see csr_rows
   const int* offsets;      // [B+1] (ex_shift > 0)
   int slice_shift;         // < 0: no slicing; else example slice = ex >> slice_shift
+  int dense_min;           // rows with >= dense_min occurrences go to the MFMA backward (0: off)
+  int* dense_list;         // [kMaxDense]
   int nslices;             // slices (<= kMaxSlices)
   int* slice_list;         // [n] chunk ids grouped by slice
   int* slice_start;        // [nslices + 1]
@@ -420,8 +473,8 @@ int launch_dedup(const DedupArgs& a, hipStream_t st) {
   const size_t tmp = sort_temp_bytes(a.n, st);
   char* base = static_cast<char*>(a.ws);
   unsigned* tile_cnt = reinterpret_cast<unsigned*>(base + tmp);
-  unsigned* tile_off = reinterpret_cast<unsigned*>(base + tmp + align_up(2 * (size_t)ntiles * sizeof(unsigned)));
-  if (tmp + 2 * align_up(2 * (size_t)ntiles * sizeof(unsigned)) + slice_scan_bytes(a.n) > a.ws_bytes) return -2;
+  unsigned* tile_off = reinterpret_cast<unsigned*>(base + tmp + align_up(3 * (size_t)ntiles * sizeof(unsigned)));
+  if (tmp + 2 * align_up(3 * (size_t)ntiles * sizeof(unsigned)) + slice_scan_bytes(a.n) > a.ws_bytes) return -2;
 
   size_t sort_bytes = tmp;
   hipError_t e = sort_pairs(a.ws, sort_bytes, a.keys, a.skeys, a.payload, a.spay, a.n, a.end_bit, st);
@@ -429,16 +482,18 @@ int launch_dedup(const DedupArgs& a, hipStream_t st) {
   const bool sliced = a.slice_shift >= 0 && a.nslices > 0 && a.nslices <= kMaxSlices && a.slice_list;
   // slice scan scratch: [rocprim temp | cnt | off], m = nslices * ntiles
   const size_t m = (size_t)kMaxSlices * (size_t)ntiles;
-  char* sbase = base + tmp + 2 * align_up(2 * (size_t)ntiles * sizeof(unsigned));
+  char* sbase = base + tmp + 2 * align_up(3 * (size_t)ntiles * sizeof(unsigned));
   const size_t scan_cap = slice_scan_bytes(a.n) - 2 * align_up(m * sizeof(unsigned));
   unsigned* cnt = reinterpret_cast<unsigned*>(sbase + scan_cap);
   unsigned* off = reinterpret_cast<unsigned*>(sbase + scan_cap + align_up(m * sizeof(unsigned)));
-  RleArgs r{a.n, a.CH, ntiles, sliced ? a.slice_shift : -1, sliced ? a.nslices : 0, 8 * a.CH, a.skeys, a.spay,
+  RleArgs r{a.n, a.CH, ntiles, sliced ? a.slice_shift : -1, sliced ? a.nslices : 0, 8 * a.CH,
+            a.dense_list ? a.dense_min : 0, a.dense_list, a.skeys, a.spay,
             a.payload_is_ex ? a.spay : nullptr, a.ex_shift, a.offsets, tile_cnt, tile_off, cnt, a.uniq, a.seg_start, a.seg_chunk,
             a.chunk_start, a.chunk_seg, a.chunk_key, a.counts, a.inv, a.ex_of_occ, a.sorted_ex, a.vals, a.sorted_x};
   hipLaunchKernelGGL(rle_tile_count_kernel, dim3(ntiles), dim3(kBlock), 0, st, r);
   hipLaunchKernelGGL(rle_tile_scan_kernel, dim3(1), dim3(1024), 0, st, r);
   hipLaunchKernelGGL(rle_tile_emit_kernel, dim3(ntiles), dim3(kBlock), 0, st, r);
+  if (r.dense_min > 0) hipLaunchKernelGGL(mark_dense_chunks_kernel, dim3(kMaxDense), dim3(kBlock), 0, st, r);
   if (!sliced) return (int)hipGetLastError();
 
   // per-slice chunk lists

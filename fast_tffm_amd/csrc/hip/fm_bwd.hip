@@ -66,6 +66,9 @@ struct BwdArgs {
   const int* slice_list;    // chunk ids grouped by example slice, or null
   const int* slice_start;   // [nslices + 1]
   int nslices;
+  const int* dense_list;    // [kMaxDense] dense rows (dedup), counts[3] of them; null: no dense path
+  float* dense_part;        // [gridDim(dense) * kMaxDense, Kp + 4] per-workgroup partial rows
+  int nex;                  // examples in the batch (dense path)
 };
 
 // Parameter row + optimizer slots of one segment, read before its gradient is
@@ -204,11 +207,13 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_chunk_kernel(BwdArgs a) {
     const int u = d_seg & kChunkSegMask;
     const bool single = (unsigned)d_seg & kChunkSingle;
     const bool first = d_seg & kChunkFirst;
+    const bool dense = d_seg & kChunkDense;
     if (ii + stride < i1) {
       c = cn;
       d_j0 = a.chunk_start[c]; d_j1 = a.chunk_start[c + 1]; d_seg = a.chunk_seg[c]; d_key = a.chunk_key[c];
       cn = ii + 2 * stride < i1 ? chunk_at(ii + 2 * stride) : 0;
     }
+    if (dense) continue;  // gradient from the MFMA path (fm_bwd_dense_kernel)
     const int len = j1 - j0;
     RowState<EPL> rs;
     if (single) bwd_load_row<TV, EPL>(a, a.mode == kBwdLocal ? (long long)key : (long long)u, tE, rs);
@@ -409,17 +414,238 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_big_kernel(BwdArgs a) {
   }
 }
 
-int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_unique, hipStream_t st) {
+// ---------------------------------------------------------------------------
+// Dense rows on the matrix cores.  The hottest rows (>= dense_min occurrences,
+// e.g. the values of Criteo's low-cardinality fields, each present in 5-60% of
+// the examples) make the occurrence-gather backward pay one r1 row per
+// occurrence.  For them the reduction is a dense GEMM instead:
+//     G[h, :] = sum_e A[e, h] * dpred_e * r1_e,   A[e, h] = sum of x over the
+// occurrences of dense row h in example e,
+// computed per 64-example tile with v_mfma_f32_16x16x4_f32 (exact fp32): each
+// workgroup owns a contiguous example range, builds A (64 x 128) in LDS from the
+// rows' sorted occurrence lists (one thread per dense row, a cursor per row),
+// stages D = dpred * r1 (64 x Kp, coalesced) in LDS and accumulates G in AGPR/VGPR
+// accumulators across its tiles.  r1 is read once, coalesced, instead of once
+// per occurrence.  Partial G rows are summed over workgroups in a fixed order
+// by fm_bwd_dense_apply_kernel, which then applies the optimizer.
+// ---------------------------------------------------------------------------
+constexpr int kDenseE = 64;                 // examples per tile (the MFMA reduction dim)
+constexpr int kDenseAS = kMaxDense + 16;     // A row stride in LDS (floats): rows 16 banks apart
+constexpr int kDenseWG = 256;               // workgroups of the dense kernel (one per CU)
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+template <int NB>  // 16-column blocks of Kp (Kp <= NB * 16)
+__global__ __launch_bounds__(kBlock) void fm_bwd_dense_kernel(BwdArgs a) {
+  constexpr int DS = NB * 16 + 16;   // D row stride in LDS (floats)
+  __shared__ float As[kDenseE * kDenseAS];
+  __shared__ float Ds[kDenseE * DS];
+  __shared__ float dps[kDenseE];
+  const int nd = min(a.counts[3], kMaxDense);
+  if (nd == 0) return;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid >> 6;
+  const int per = ((a.nex + (int)gridDim.x - 1) / (int)gridDim.x + kDenseE - 1) / kDenseE * kDenseE;
+  const int e_begin = blockIdx.x * per, e_end = min(a.nex, e_begin + per);
+  // thread h < nd walks dense row h's occurrences (sorted by example) from e_begin on
+  int cur = 0, cend = 0;
+  float sc = 0.f, scx = 0.f;
+  if (tid < nd) {
+    const int u = a.dense_list[tid];
+    int lo = a.seg_start[u], hi = a.seg_start[u + 1];
+    cend = hi;
+    // occurrences are spread ~uniformly over the examples: probe a window around the
+    // interpolated position first, then finish with a binary search inside it
+    const int len = hi - lo;
+    const int guess = lo + (int)((long long)len * e_begin / max(a.nex, 1));
+    const int win = 2 * (int)sqrtf((float)len) + 32;
+    const int wlo = max(lo, guess - win), whi = min(hi, guess + win);
+    if (wlo > lo && (a.sorted_ex[wlo] >> a.ex_shift) < e_begin) lo = wlo;
+    if (whi < hi && (a.sorted_ex[whi] >> a.ex_shift) >= e_begin) hi = whi;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if ((a.sorted_ex[mid] >> a.ex_shift) < e_begin) lo = mid + 1; else hi = mid;
+    }
+    cur = lo;
+  }
+  floatx4 acc[2][NB];
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int kq = a.Kp / 4;  // float4 columns of r1
+  for (int e0 = e_begin; e0 < e_end; e0 += kDenseE) {
+    for (int i = tid; i < kDenseE * kDenseAS; i += kBlock) As[i] = 0.f;
+    for (int i = tid; i < kDenseE * NB * 4; i += kBlock) {
+      const int e = i / (NB * 4), q = i % (NB * 4), ex = e0 + e;
+      float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ex < e_end && q < kq) {
+        const float d = a.dpred[ex];
+        f = *reinterpret_cast<const float4*>(a.r1 + (long long)ex * a.Kp + 4 * q);
+        f.x *= d; f.y *= d; f.z *= d; f.w *= d;
+      }
+      *reinterpret_cast<float4*>(Ds + e * DS + 4 * q) = f;
+    }
+    if (tid < kDenseE) dps[tid] = e0 + tid < e_end ? a.dpred[e0 + tid] : 0.f;
+    __syncthreads();
+    if (tid < nd) {
+      // 16 upcoming occurrences of the row per round trip (the densest rows have ~40
+      // per tile; a dependent load per occurrence would serialise on memory latency)
+      const int lim = min(e0 + kDenseE, e_end);
+      for (;;) {
+        int exs[16];
+        float xs[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int idx = cur + q;
+          const bool ok = idx < cend;
+          const int li = ok ? idx : cend - 1;  // loads stay inside the row (cend > seg start here)
+          exs[q] = ok ? (a.sorted_ex[li] >> a.ex_shift) : 0x7fffffff;
+          xs[q] = a.sorted_x ? a.sorted_x[li] : 1.f;
+        }
+        int taken = 0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          if (exs[q] < lim) {  // ascending: the taken ones are a prefix
+            As[(exs[q] - e0) * kDenseAS + tid] += xs[q];  // column tid: this thread only
+            const float c = dps[exs[q] - e0] * xs[q];
+            sc += c;
+            scx += c * xs[q];
+            ++taken;
+          }
+        }
+        cur += taken;
+        if (taken < 16) break;
+      }
+    }
+    __syncthreads();
+    // G[m, n] += sum_e A[e, m] D[e, n]; wave wv owns rows 32 wv .. 32 wv + 31
+#pragma unroll 4
+    for (int kk = 0; kk < kDenseE; kk += 4) {
+      const int e = kk + (lane >> 4);
+      const float a0 = As[e * kDenseAS + (2 * wv) * 16 + (lane & 15)];
+      const float a1 = As[e * kDenseAS + (2 * wv + 1) * 16 + (lane & 15)];
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const float b = Ds[e * DS + nb * 16 + (lane & 15)];
+        acc[0][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b, acc[0][nb], 0, 0, 0);
+        acc[1][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b, acc[1][nb], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  // partial rows: C/D map of 16x16 MFMA tiles: col = lane & 15, row = (lane >> 4) * 4 + i
+  const int PS = a.Kp + 4;
+  float* part = a.dense_part + (long long)blockIdx.x * kMaxDense * PS;
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = (2 * wv + mb) * 16 + (lane >> 4) * 4 + i, n = nb * 16 + (lane & 15);
+        if (m < nd && n < a.Kp) part[(long long)m * PS + n] = acc[mb][nb][i];
+      }
+  if (tid < nd) {
+    part[(long long)tid * PS + a.Kp] = scx;
+    part[(long long)tid * PS + a.Kp + 1] = sc;
+  }
+}
+
+// One workgroup per dense row: ordered sum of the per-workgroup partials
+// (4 stripes of workgroups, then the stripes in order), then the optimizer.
+template <int LPR, typename TV>
+__global__ __launch_bounds__(kBlock) void fm_bwd_dense_apply_kernel(BwdArgs a) {
+  constexpr int EPL = Frag<TV>::N;
+  __shared__ float4 red[kWavesPerBlock][kWave];
+  __shared__ float row[kWave * 4];
+  const int nd = min(a.counts[3], kMaxDense);
+  const int h = blockIdx.x;
+  if (h >= nd) return;
+  const int tid = threadIdx.x, q = tid & (kWave - 1), stripe = tid >> 6;
+  const int PS = a.Kp + 4, nq = PS / 4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (q < nq) {
+    for (int wg = stripe; wg < kDenseWG; wg += kWavesPerBlock) {
+      const float4 f = *reinterpret_cast<const float4*>(a.dense_part + ((long long)wg * kMaxDense + h) * PS + 4 * q);
+      s.x += f.x; s.y += f.y; s.z += f.z; s.w += f.w;
+    }
+  }
+  red[stripe][q] = s;
+  __syncthreads();
+  if (stripe == 0 && q < nq) {
+    float4 t = red[0][q];
+#pragma unroll
+    for (int k = 1; k < kWavesPerBlock; ++k) {
+      const float4 f = red[k][q];
+      t.x += f.x; t.y += f.y; t.z += f.z; t.w += f.w;
+    }
+    row[4 * q] = t.x; row[4 * q + 1] = t.y; row[4 * q + 2] = t.z; row[4 * q + 3] = t.w;
+  }
+  __syncthreads();
+  if (tid < LPR) {
+    const int t = tid;
+    const int nv = a.Kp / EPL;
+    const bool tact = t < nv;
+    const int tE = tact ? t : nv - 1;
+    float A[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) A[k] = row[tE * EPL + k];
+    const int u = a.dense_list[h];
+    bwd_finalize<LPR, TV, EPL>(a, u, t, tact, tE, A, row[a.Kp], row[a.Kp + 1], a.seg_start[u + 1] - a.seg_start[u]);
+  }
+}
+
+// The dense kernel runs on its own stream, concurrently with the chunk kernel
+// (disjoint outputs; both only read r1 / dpred / the dedup plan): its latency-bound
+// phases (cursor search, occurrence scan) hide under the chunk kernel's traffic.
+static hipEvent_t dense_fork_event() {
+  static hipEvent_t ev = nullptr;
+  if (!ev) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  return ev;
+}
+static hipEvent_t dense_join_event() {
+  static hipEvent_t ev = nullptr;
+  if (!ev) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  return ev;
+}
+
+int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_unique, hipStream_t st,
+               hipStream_t dense_st) {
   if (max_chunks <= 0) return 0;
   const int lpr = lanes_per_row(a.Kp, dtype);
   const int G = kWave / lpr;
   (void)hipMemsetAsync(a.big_count, 0, sizeof(int), st);
   (void)hipMemsetAsync(a.counts_rw + 2, 0, sizeof(int), st);  // #multi-chunk rows, appended by the chunk kernel
   const int g1 = (fill_grid(max_chunks, kWavesPerBlock * G) + 7) / 8 * 8;  // multiple of 8: XCD groups
+  const bool dense = a.dense_list && a.dense_part;
+  const bool fork = dense && dense_st && dense_st != st;
+  hipStream_t ds = fork ? dense_st : st;
+  if (dense) {
+    if (a.Kp > 128 || a.Kp % 4 != 0) return -5;
+    if (fork) {
+      (void)hipEventRecord(dense_fork_event(), st);
+      (void)hipStreamWaitEvent(ds, dense_fork_event(), 0);
+    }
+    switch ((a.Kp + 15) / 16) {
+      case 1: hipLaunchKernelGGL(fm_bwd_dense_kernel<1>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
+      case 2: hipLaunchKernelGGL(fm_bwd_dense_kernel<2>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
+      case 3: hipLaunchKernelGGL(fm_bwd_dense_kernel<3>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
+      case 4: hipLaunchKernelGGL(fm_bwd_dense_kernel<4>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
+      case 5: hipLaunchKernelGGL(fm_bwd_dense_kernel<5>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
+      case 6: hipLaunchKernelGGL(fm_bwd_dense_kernel<6>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
+      case 7: hipLaunchKernelGGL(fm_bwd_dense_kernel<7>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
+      default: hipLaunchKernelGGL(fm_bwd_dense_kernel<8>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
+    }
+    if (fork) (void)hipEventRecord(dense_join_event(), ds);
+  }
   FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, a);
   const int g2 = fill_grid(max_unique, kWavesPerBlock * G, 2048);
   FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, a);
   FM_DISPATCH(dtype, lpr, fm_bwd_big_kernel, 1024, st, a);
+  if (dense) {
+    if (fork) (void)hipStreamWaitEvent(st, dense_join_event(), 0);
+    FM_DISPATCH(dtype, lpr, fm_bwd_dense_apply_kernel, kMaxDense, st, a);
+  }
   return (int)hipGetLastError();
 }
 

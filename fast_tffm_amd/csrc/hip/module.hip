@@ -77,7 +77,8 @@ PYBIND11_MODULE(_fm_hip, m) {
          u64 sorted_ex, int ex_shift, u64 sorted_x, u64 dpred, u64 r1, int Kp, u64 v, long long v_stride, u64 w,
          long long w_stride, u64 s0v, u64 s1v, long long s_stride, u64 s0w, u64 s1w, float reg_v, float reg_w,
          int opt_type, float lr, float l1, float l2, float beta, u64 grad_out, long long g_stride, u64 partial,
-         u64 big_list, u64 big_count, u64 multi, u64 slice_list, u64 slice_start, int nslices, int dtype,
+         u64 big_list, u64 big_count, u64 multi, u64 slice_list, u64 slice_start, int nslices, u64 dense_list,
+         u64 dense_part, int nex, u64 dense_stream, int dtype,
          long long max_chunks, long long max_unique, u64 stream) {
         fm::BwdArgs a;
         a.mode = mode; a.counts = P<const int>(counts); a.chunk_start = P<const int>(chunk_start);
@@ -94,7 +95,8 @@ PYBIND11_MODULE(_fm_hip, m) {
         a.big_list = P<int>(big_list); a.big_count = P<int>(big_count); a.multi = P<int>(multi);
         a.counts_rw = P<int>(counts); a.slice_list = P<const int>(slice_list);
         a.slice_start = P<const int>(slice_start); a.nslices = nslices;
-        check(fm::launch_bwd(a, dtype, max_chunks, max_unique, S(stream)), "fm_bwd");
+        a.dense_list = P<const int>(dense_list); a.dense_part = P<float>(dense_part); a.nex = nex;
+        check(fm::launch_bwd(a, dtype, max_chunks, max_unique, S(stream), S(dense_stream)), "fm_bwd");
       },
       py::arg("mode"), py::arg("counts"), py::arg("chunk_start"), py::arg("chunk_seg"), py::arg("chunk_key"),
       py::arg("seg_start"),
@@ -103,7 +105,8 @@ PYBIND11_MODULE(_fm_hip, m) {
       py::arg("s0v"), py::arg("s1v"), py::arg("s_stride"), py::arg("s0w"), py::arg("s1w"), py::arg("reg_v"),
       py::arg("reg_w"), py::arg("opt_type"), py::arg("lr"), py::arg("l1"), py::arg("l2"), py::arg("beta"),
       py::arg("grad_out"), py::arg("g_stride"), py::arg("partial"), py::arg("big_list"), py::arg("big_count"),
-      py::arg("multi"), py::arg("slice_list"), py::arg("slice_start"), py::arg("nslices"), py::arg("dtype"),
+      py::arg("multi"), py::arg("slice_list"), py::arg("slice_start"), py::arg("nslices"), py::arg("dense_list"),
+      py::arg("dense_part"), py::arg("nex"), py::arg("dense_stream"), py::arg("dtype"),
       py::arg("max_chunks"), py::arg("max_unique"), py::arg("stream"));
 
   m.def("dedup_workspace_bytes", &fm::dedup_workspace_bytes, py::arg("n"));
@@ -112,7 +115,7 @@ PYBIND11_MODULE(_fm_hip, m) {
       "dedup",
       [](int n, int end_bit, int CH, u64 keys, u64 payload, u64 skeys, u64 spay, u64 uniq, u64 seg_start,
          u64 seg_chunk, u64 chunk_start, u64 chunk_seg, u64 chunk_key, u64 counts, u64 inv, u64 ex_of_occ,
-         u64 sorted_ex, u64 vals, u64 sorted_x, int payload_is_ex, int ex_shift, u64 offsets, int slice_shift, int nslices, u64 slice_list,
+         u64 sorted_ex, u64 vals, u64 sorted_x, int payload_is_ex, int ex_shift, u64 offsets, int dense_min, u64 dense_list, int slice_shift, int nslices, u64 slice_list,
          u64 slice_start, u64 ws, size_t ws_bytes, u64 stream) {
         if (CH < 1 || CH > fm::kMaxCH) throw std::invalid_argument("CH must be in [1, MAX_CH]");
         fm::DedupArgs a;
@@ -125,6 +128,7 @@ PYBIND11_MODULE(_fm_hip, m) {
         a.vals = P<const float>(vals); a.sorted_x = P<float>(sorted_x); a.ws = P<void>(ws);
         a.payload_is_ex = payload_is_ex; a.ex_shift = ex_shift; a.offsets = P<const int>(offsets);
         a.slice_shift = slice_shift; a.nslices = nslices;
+        a.dense_min = dense_min; a.dense_list = P<int>(dense_list);
         a.slice_list = P<int>(slice_list); a.slice_start = P<int>(slice_start);
         a.ws_bytes = ws_bytes;
         check(fm::launch_dedup(a, S(stream)), "dedup");
@@ -133,10 +137,12 @@ PYBIND11_MODULE(_fm_hip, m) {
       py::arg("spay"), py::arg("uniq"), py::arg("seg_start"), py::arg("seg_chunk"), py::arg("chunk_start"),
       py::arg("chunk_seg"), py::arg("chunk_key"), py::arg("counts"), py::arg("inv"), py::arg("ex_of_occ"),
       py::arg("sorted_ex"),
-      py::arg("vals"), py::arg("sorted_x"), py::arg("payload_is_ex"), py::arg("ex_shift"), py::arg("offsets"),
+      py::arg("vals"), py::arg("sorted_x"), py::arg("payload_is_ex"), py::arg("ex_shift"), py::arg("offsets"), py::arg("dense_min"), py::arg("dense_list"),
       py::arg("slice_shift"), py::arg("nslices"),
       py::arg("slice_list"), py::arg("slice_start"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"));
   m.attr("MAX_SLICES") = fm::kMaxSlices;
+  m.attr("MAX_DENSE") = fm::kMaxDense;
+  m.attr("DENSE_WG") = fm::kDenseWG;
 
   m.def(
       "gather_rows",

@@ -23,11 +23,16 @@ from __future__ import annotations
 
 from dataclasses import dataclass, field
 
+import os
+
 import torch
 
 from ..data.batch import Batch
 from ..ops import kernels as K
 from ..utils.trace import roctx_range
+
+# dedup on a side stream concurrently with the forward (1) or before it on the same stream (0)
+_SIDE_STREAM = os.environ.get("FM_SIDE_STREAM", "1") == "1"
 from .table import FMTable, bits_for, rows_per_shard
 
 
@@ -80,6 +85,9 @@ class _Workspace:
             self.bwd_partial = (torch.empty((K.partial_rows(cap, self.CH), Kp + 4), dtype=torch.float32, device=dev)
                                 if dev.type == "cuda" else None)
             self.cap_n = cap
+        if not hasattr(self, "dense_part"):
+            self.dense_part = (torch.empty((K.DENSE_WG * K.MAX_DENSE, Kp + 4), dtype=torch.float32, device=dev)
+                               if dev.type == "cuda" and Kp <= 128 else None)
         if not hasattr(self, "fwd_partial"):
             self.fwd_partial = torch.zeros(3 * 4096, dtype=torch.float32, device=dev)
 
@@ -243,13 +251,15 @@ class FactorizationMachine:
         gpu = self.device.type == "cuda"
         if gpu:
             main = torch.cuda.current_stream(self.device)
-            side = self._side_stream()
-            side.wait_stream(main)  # inputs ready; previous step's readers of ws.dd are enqueued before
+            side = self._side_stream() if _SIDE_STREAM else main
+            if side is not main:  # (a stream waiting on itself inside a hipGraph capture faults at replay)
+                side.wait_stream(main)  # inputs ready; previous step's readers of ws.dd are enqueued before
             with torch.cuda.stream(side), roctx_range("dedup"):
                 sb = self._slot_bits(b)
                 ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz, slot_bits=sb)
                 dd = K.dedup(rows, ws=ws.dd, key_bits=bits_for(self.table.rows), ex_of_occ=ex, vals=b.vals,
-                             num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets)
+                             num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets,
+                             dense_min=K.dense_min_for(b.B, self.Kp, cfg.dedup_chunk))
         else:
             ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz)
         with roctx_range("fwd"):
@@ -258,13 +268,15 @@ class FactorizationMachine:
                               pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
                               threads=cfg.threads)
         if gpu:
-            main.wait_stream(side)
+            if side is not main:
+                main.wait_stream(side)
         else:
             dd = K.dedup(rows, ws=ws.dd, key_bits=bits_for(self.table.rows), ex_of_occ=ex, vals=b.vals)
         rv, rw = self.reg_coeffs
         with roctx_range("bwd+update"):
             K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
-                          reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads)
+                          reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, dense_part=ws.dense_part,
+                          dense_stream=self._side_stream() if gpu and _SIDE_STREAM else None)
         return StepOut(fo.loss_sum, b.B)
 
     # ------------------------------------------------------------------

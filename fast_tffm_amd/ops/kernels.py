@@ -225,7 +225,7 @@ class DedupOut:
 
     __slots__ = ("n", "skeys", "perm", "uniq", "seg_start", "seg_chunk", "chunk_start", "chunk_seg", "chunk_key", "counts",
                  "num_unique", "inv", "sorted_ex", "sorted_x", "U_host", "CH", "big_list", "big_count", "multi",
-                 "slice_list", "slice_start", "nslices", "ex_shift")
+                 "slice_list", "slice_start", "nslices", "ex_shift", "dense_list")
 
     def __init__(self, **kw):
         for k in self.__slots__:
@@ -266,6 +266,7 @@ class DedupWorkspace:
         self.big_count = torch.zeros(1, **i32)
         self.slice_list = torch.empty(n1, **i32)
         self.slice_start = torch.empty(MAX_SLICES + 1, **i32)
+        self.dense_list = torch.empty(MAX_DENSE, **i32)
         if device.type == "cuda":
             nbytes = native.hip().dedup_workspace_bytes(n1)
             self.ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
@@ -303,6 +304,20 @@ def csr_rows(offsets: torch.Tensor, out: torch.Tensor | None = None, nnz: int | 
 
 
 MAX_SLICES = 64            # = fm::kMaxSlices (dedup.hip)
+MAX_DENSE = 128            # = fm::kMaxDense: rows on the MFMA backward path
+DENSE_WG = 256             # = fm::kDenseWG: workgroups (partial rows) of the dense kernel
+
+
+def dense_min_for(num_examples: int, Kp: int, CH: int = 32) -> int:
+    """Occurrence threshold of the MFMA backward rows (0 = off).
+
+    A row present in >= ~4% of the batch's examples (>= B/24 occurrences) is
+    reduced as a dense GEMM over example tiles: below that density the MFMA
+    tile is mostly zeros and the occurrence gather is cheaper.  Needs Kp <= 128
+    (the tile's N) and a batch large enough to fill the 256 tile workgroups."""
+    if os.environ.get("FM_DENSE_BWD", "0") != "1" or Kp > 128 or Kp % 4 or num_examples < 16384:
+        return 0
+    return max(8 * CH, num_examples // 24)
 SLICE_BYTES = 2 << 20      # r1 bytes per example slice of the XCD-sliced backward (XCD L2 = 4 MB)
 
 
@@ -330,7 +345,8 @@ def slice_plan(num_examples: int, Kp: int) -> tuple[int, int]:
 def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int = 32,
           ex_of_occ: torch.Tensor | None = None, vals: torch.Tensor | None = None, want_inv: bool = False,
           CH: int | None = None, want_perm: bool = False, num_examples: int | None = None,
-          Kp: int | None = None, ex_shift: int = 0, offsets: torch.Tensor | None = None) -> DedupOut:
+          Kp: int | None = None, ex_shift: int = 0, offsets: torch.Tensor | None = None,
+          dense_min: int = 0) -> DedupOut:
     """Sort-based unique over non-negative int32 keys (reference tf.unique, fm_model.py:72).
 
     Unique keys come out in ascending order (the reference's first-occurrence
@@ -367,7 +383,8 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
                    sorted_ex=(ws.perm if ex_payload else ws.sorted_ex) if ex_of_occ is not None else None,
                    sorted_x=ws.sorted_x if vals is not None else None, CH=CH, big_list=ws.big_list,
                    big_count=ws.big_count, multi=ws.multi, slice_list=ws.slice_list if nsl else None,
-                   slice_start=ws.slice_start, nslices=nsl, ex_shift=int(ex_shift))
+                   slice_start=ws.slice_start, nslices=nsl, ex_shift=int(ex_shift),
+                   dense_list=ws.dense_list if dense_min > 0 and ex_of_occ is not None and _is_gpu(keys) else None)
     if _is_gpu(keys):
         h = native.hip()
         _check(1 <= CH <= h.MAX_CH, f"CH must be in [1, {h.MAX_CH}]")
@@ -379,6 +396,7 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
                 ex_of_occ=0 if ex_payload else _p(ex_of_occ),
                 sorted_ex=0 if ex_payload else _p(out.sorted_ex), vals=_p(vals), sorted_x=_p(out.sorted_x),
                 payload_is_ex=int(ex_payload), ex_shift=int(ex_shift), offsets=_p(offsets),
+                dense_min=int(dense_min) if out.dense_list is not None else 0, dense_list=_p(out.dense_list),
                 slice_shift=shift, nslices=nsl,
                 slice_list=_p(out.slice_list), slice_start=_p(ws.slice_start), ws=_p(ws.ws),
                 ws_bytes=ws.ws.numel(), stream=_stream(keys))
@@ -415,7 +433,8 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
                 table: TableState | None = None, opt: OptConfig | None = None,
                 src_v: torch.Tensor | None = None, src_w: torch.Tensor | None = None,
                 grad_out: torch.Tensor | None = None, reg_v: float = 0.0, reg_w: float = 0.0,
-                partial: torch.Tensor | None = None, threads: int = 0) -> torch.Tensor | None:
+                partial: torch.Tensor | None = None, threads: int = 0,
+                dense_part: torch.Tensor | None = None, dense_stream=None) -> torch.Tensor | None:
     """Segmented FM backward over the dedup grouping (reference FmGrad, cc/fm_grad_op.h:59-163).
 
     Per unique row u with occurrences (i, x):
@@ -456,6 +475,11 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
         if partial is None:
             partial = torch.empty((partial_rows(dd.n, dd.CH), Kp + 4), dtype=torch.float32, device=dev)
         _check(partial.numel() >= partial_rows(dd.n, dd.CH) * (Kp + 4), "partial scratch too small")
+        dp = None
+        if dd.dense_list is not None:  # MFMA path for the dense rows
+            dp = dense_part if dense_part is not None else torch.empty(
+                (DENSE_WG * MAX_DENSE, Kp + 4), dtype=torch.float32, device=dev)
+            _check(dp.numel() >= DENSE_WG * MAX_DENSE * (Kp + 4), "dense_part scratch too small")
         h.bwd(mode=mode, counts=_p(dd.counts), chunk_start=_p(dd.chunk_start), chunk_seg=_p(dd.chunk_seg),
               chunk_key=_p(dd.chunk_key),
               seg_start=_p(dd.seg_start), seg_chunk=_p(dd.seg_chunk), uniq=_p(dd.uniq),
@@ -466,7 +490,9 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               opt_type=o.code, lr=float(o.lr), l1=float(o.l1), l2=float(o.l2), beta=float(o.beta),
               grad_out=gptr, g_stride=gstride, partial=_p(partial), big_list=_p(dd.big_list),
               big_count=_p(dd.big_count), multi=_p(dd.multi), slice_list=_p(dd.slice_list),
-              slice_start=_p(dd.slice_start), nslices=int(dd.nslices or 0), dtype=dt, max_chunks=dd.n, max_unique=dd.n,
+              slice_start=_p(dd.slice_start), nslices=int(dd.nslices or 0), dense_list=_p(dd.dense_list),
+              dense_part=_p(dp), nex=int(dpred.numel()),
+              dense_stream=dense_stream.cuda_stream if dense_stream is not None else 0, dtype=dt, max_chunks=dd.n, max_unique=dd.n,
               stream=_stream(dpred))
     else:
         U = dd.sync()

@@ -48,9 +48,39 @@ def cpu():
     return _load("_fm_cpu", "cpu")
 
 
+class _SyncChecked:
+    """FM_SYNC_LAUNCH=1: every kernel entry point synchronises the device after its
+    launches, so a fault is reported by the Python frame of the op that caused it
+    (debugging aid; never on for timing runs)."""
+
+    def __init__(self, mod):
+        self._mod = mod
+
+    def __getattr__(self, name):
+        f = getattr(self._mod, name)
+        if not callable(f):
+            return f
+
+        def wrapped(*args, **kw):
+            import torch
+
+            out = f(*args, **kw)
+            try:
+                torch.cuda.synchronize()
+            except Exception as e:  # noqa: BLE001
+                raise RuntimeError(f"_fm_hip.{name} faulted: {e}") from e
+            return out
+
+        return wrapped
+
+
+_SYNC = os.environ.get("FM_SYNC_LAUNCH", "0") == "1"
+
+
 def hip():
     """gfx950 module: GPU step kernels. Raises if unavailable."""
-    return _load("_fm_hip", "hip")
+    mod = _load("_fm_hip", "hip")
+    return _SyncChecked(mod) if _SYNC else mod
 
 
 def loaded_paths() -> dict[str, str]:

@@ -170,7 +170,8 @@ class ShardExchange(_Base):
                 ex = K.csr_rows(b.offsets, out=slot.dd.ex_of_occ[: b.nnz], nnz=b.nnz, slot_bits=sb)
             dd = K.dedup(keys, ws=slot.dd, key_bits=self.key_bits, ex_of_occ=ex,
                          vals=b.vals if ex is not None else None, want_inv=True, num_examples=b.B, Kp=self.m.Kp,
-                         ex_shift=sb, offsets=b.offsets if sb else None)
+                         ex_shift=sb, offsets=b.offsets if sb else None,
+                         dense_min=K.dense_min_for(b.B, self.m.Kp, m.cfg.dedup_chunk) if train else 0)
             # per-owner counts: one small D2H on this (side) stream -- the only host sync of the
             # step, it waits for this dedup only -- then the count exchange on the CPU group
             sc = K.owner_counts(dd, self.Rps, self.W).cpu()
@@ -253,7 +254,8 @@ class ShardExchange(_Base):
         rv, rw = m.reg_coeffs
         with roctx_range("bwd"):
             K.fm_backward(dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT, src_v=src_v, src_w=src_w, grad_out=grad,
-                          reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads)
+                          reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, dense_part=ws.dense_part,
+                          dense_stream=m._side_stream() if self.dev.type == "cuda" else None)
         grad_recv = torch.empty((pl.R, self.gs), dtype=torch.float32, device=self.dev)
         with roctx_range("a2a_grads"):
             _a2a(grad_recv, grad, pl.rc, pl.sc, self.group)

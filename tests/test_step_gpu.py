@@ -92,3 +92,43 @@ def test_xcd_sliced_schedule_matches_oracle(monkeypatch, k):
     assert torch.equal(lst, torch.arange(C, dtype=torch.int32))
     st = dd.slice_start[: dd.nslices + 1].cpu()
     assert int(st[0]) == 0 and int(st[-1]) == C and bool((st[1:] >= st[:-1]).all())
+
+
+@pytest.mark.parametrize("k,dtype,vals", [(16, torch.float32, False), (64, torch.float32, False),
+                                          (100, torch.float32, True), (64, torch.bfloat16, True)])
+def test_dense_mfma_backward_matches_oracle(monkeypatch, k, dtype, vals):
+    """Rows above the density threshold go through the MFMA (dense GEMM) backward; forced
+    here with a low threshold so a small batch has dense rows of every kind."""
+    monkeypatch.setattr(K, "dense_min_for", lambda B, Kp, CH=32: 48)
+    if vals:
+        b = random_batch(2048, 400, max_feats=30, seed=12, device="cuda")
+        V = 400
+    else:
+        V = 5000
+        b = CriteoSynth(V, device="cuda", seed=13).batch(2048)
+    m = _model(V=V, k=k, dtype=dtype)
+    p0 = m.table.reference_rows().double().cpu()
+    m.train_step(b)
+    dd = m.ws.dd
+    assert int(dd.counts[3]) > 0  # dense rows existed
+    p1, _, _ = reference_train_step(p0, torch.full_like(p0, 0.1), b.to("cpu"), "logistic", 0.05, 0.01, 0.01, 512)
+    got = m.table.reference_rows().double().cpu()
+    if dtype == torch.float32:
+        torch.testing.assert_close(got, p1, rtol=2e-4, atol=5e-6)
+    else:
+        torch.testing.assert_close(got, p1, rtol=2e-2, atol=2e-3)
+
+
+def test_dense_mfma_backward_is_deterministic(monkeypatch):
+    monkeypatch.setattr(K, "dense_min_for", lambda B, Kp, CH=32: 48)
+    gen = CriteoSynth(5000, device="cuda", seed=14)
+    batches = [gen.batch(4096) for _ in range(2)]
+    runs = []
+    for _ in range(2):
+        m = _model(V=5000)
+        for bt in batches:
+            m.train_step(bt)
+        torch.cuda.synchronize()
+        runs.append(_state(m))
+    for x, y in zip(*runs):
+        assert torch.equal(x, y)
