@@ -16,7 +16,9 @@ Decisions on reference quirks:
 * ``model_file`` is read and kept, unused, like the reference (:405-407).
 
 Extensions (new keys, all optional):
-  [General]     seed, dtype = fp32|bf16|fp8 (fp8: OCP e4m3 + per-row scale, GPU), device = auto|cpu|cuda
+  [General]     seed, device = auto|cpu|cuda,
+                global_bias = true|false (learned b0; its gradient is all-reduced over ranks),
+                dtype = fp32|bf16|fp8 (fp8: OCP e4m3 + per-row scale, GPU)
   [Train]       optimizer = adagrad|ftrl|sgd, ftrl.l1, ftrl.l2, ftrl.beta,
                 ftrl.initial_accumulator, parse_threads, shuffle = true|false,
                 max_steps, dedup_chunk, log_steps
@@ -88,6 +90,7 @@ class FMRunConfig:
     shuffle: bool = True
     max_steps: int | None = None
     dedup_chunk: int = 32
+    global_bias: bool = False
     log_steps: int = 1
     # [Predict]
     predict_files: list[str] = field(default_factory=list)
@@ -114,7 +117,7 @@ class FMRunConfig:
                         init_value_range=self.init_value_range, seed=self.seed,
                         dtype={"fp32": torch.float32, "bf16": torch.bfloat16,
                                "fp8": torch.float8_e4m3fn}[self.dtype], opt=opt, mode=self.mode,
-                        grad_reduce=self.grad_reduce, dedup_chunk=self.dedup_chunk)
+                        grad_reduce=self.grad_reduce, dedup_chunk=self.dedup_chunk, global_bias=self.global_bias)
 
 
 def load_config(config_file: str, *, echo: bool = True, printer=print) -> FMRunConfig:
@@ -158,6 +161,7 @@ def load_config(config_file: str, *, echo: bool = True, printer=print) -> FMRunC
     c.model_file = read(GENERAL, "model_file", required=False)
     c.save_summaries_steps = opt(GENERAL, "save_summaries_steps", int, c.save_summaries_steps)
     c.seed = opt(GENERAL, "seed", int, c.seed)
+    c.global_bias = opt(GENERAL, "global_bias", to_bool, c.global_bias)
     c.dtype = opt(GENERAL, "dtype", lambda s: s.strip().lower(), c.dtype)
     c.device = opt(GENERAL, "device", lambda s: s.strip().lower(), c.device)
 

@@ -89,7 +89,8 @@ void update_row(const OptParams& opt, long long row, const float* g, float gw, i
 
 FwdResult fwd(int B, const int* offsets, const int* rows, const float* vals, const void* v, long long v_stride,
               const float* w, long long w_stride, int Kp, int dtype, const float* labels, const float* weights,
-              int loss_type, float grad_scale, float* pred, float* r1, float* dpred, int threads) {
+              int loss_type, float grad_scale, float* pred, float* r1, float* dpred, int threads,
+              const float* bias) {
   set_threads(threads);
   double loss_sum = 0, regv_sum = 0, regw_sum = 0;
 #pragma omp parallel reduction(+ : loss_sum, regv_sum, regw_sum)
@@ -116,7 +117,7 @@ FwdResult fwd(int B, const int* offsets, const int* rows, const float* vals, con
       }
       float part = 0.f;
       for (int k = 0; k < Kp; ++k) part += s1[k] * s1[k] - s2[k];
-      const float p = lin + 0.5f * part;
+      const float p = lin + 0.5f * part + (bias ? bias[0] : 0.f);
       pred[i] = p;
       if (r1) std::memcpy(r1 + (long long)i * Kp, s1.data(), sizeof(float) * Kp);
       regv_sum += rv;

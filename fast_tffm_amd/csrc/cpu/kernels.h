@@ -21,7 +21,8 @@ struct FwdResult {
 
 FwdResult fwd(int B, const int* offsets, const int* rows, const float* vals, const void* v, long long v_stride,
               const float* w, long long w_stride, int Kp, int dtype, const float* labels, const float* weights,
-              int loss_type, float grad_scale, float* pred, float* r1, float* dpred, int threads);
+              int loss_type, float grad_scale, float* pred, float* r1, float* dpred, int threads,
+              const float* bias = nullptr);
 
 // Stable sort of (key, occurrence) + run-length encoding. Returns U.
 int dedup(int n, const uint32_t* keys, uint32_t* skeys, int* perm, uint32_t* uniq, int* seg_start, int* inv,

@@ -150,21 +150,21 @@ PYBIND11_MODULE(_fm_cpu, m) {
       "fwd",
       [](int B, u64 offsets, u64 rows, u64 vals, u64 v, long long v_stride, u64 w, long long w_stride, int Kp,
          int dtype, u64 labels, u64 weights, int loss_type, float grad_scale, u64 pred, u64 r1, u64 dpred,
-         int threads) {
+         int threads, u64 bias) {
         fm::cpu::FwdResult r;
         {
           py::gil_scoped_release nogil;
           r = fm::cpu::fwd(B, P<const int>(offsets), P<const int>(rows), P<const float>(vals), P<const void>(v),
                            v_stride, P<const float>(w), w_stride, Kp, dtype, P<const float>(labels),
                            P<const float>(weights), loss_type, grad_scale, P<float>(pred), P<float>(r1),
-                           P<float>(dpred), threads);
+                           P<float>(dpred), threads, P<const float>(bias));
         }
         return py::make_tuple(r.loss_sum, r.regv_sum, r.regw_sum);
       },
       py::arg("B"), py::arg("offsets"), py::arg("rows"), py::arg("vals"), py::arg("v"), py::arg("v_stride"),
       py::arg("w"), py::arg("w_stride"), py::arg("Kp"), py::arg("dtype"), py::arg("labels"), py::arg("weights"),
       py::arg("loss_type"), py::arg("grad_scale"), py::arg("pred"), py::arg("r1"), py::arg("dpred"),
-      py::arg("threads") = 0);
+      py::arg("threads"), py::arg("bias") = 0);
 
   m.def(
       "dedup",

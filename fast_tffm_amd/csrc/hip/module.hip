@@ -55,7 +55,7 @@ PYBIND11_MODULE(_fm_hip, m) {
       "fwd",
       [](int B, u64 offsets, u64 rows, u64 vals, u64 v, long long v_stride, u64 w, long long w_stride, int Kp,
          int dtype, u64 labels, u64 weights, int loss_type, float grad_scale, u64 pred, u64 r1, u64 dpred,
-         u64 loss_partial, u64 reg_partial, int grid, u64 stream) {
+         u64 loss_partial, u64 reg_partial, int grid, u64 stream, u64 bias) {
         fm::FwdArgs a;
         a.B = B; a.offsets = P<const int>(offsets); a.rows = P<const int>(rows);
         a.vals = P<const float>(vals); a.v = P<const void>(v); a.v_stride = v_stride;
@@ -63,13 +63,13 @@ PYBIND11_MODULE(_fm_hip, m) {
         a.labels = P<const float>(labels); a.weights = P<const float>(weights);
         a.loss_type = loss_type; a.grad_scale = grad_scale; a.pred = P<float>(pred);
         a.r1 = P<float>(r1); a.dpred = P<float>(dpred); a.loss_partial = P<float>(loss_partial);
-        a.reg_partial = P<float>(reg_partial);
+        a.reg_partial = P<float>(reg_partial); a.bias = P<const float>(bias);
         check(fm::launch_fwd(a, dtype, grid, S(stream)), "fm_fwd");
       },
       py::arg("B"), py::arg("offsets"), py::arg("rows"), py::arg("vals"), py::arg("v"), py::arg("v_stride"),
       py::arg("w"), py::arg("w_stride"), py::arg("Kp"), py::arg("dtype"), py::arg("labels"), py::arg("weights"),
       py::arg("loss_type"), py::arg("grad_scale"), py::arg("pred"), py::arg("r1"), py::arg("dpred"),
-      py::arg("loss_partial"), py::arg("reg_partial"), py::arg("grid"), py::arg("stream"));
+      py::arg("loss_partial"), py::arg("reg_partial"), py::arg("grid"), py::arg("stream"), py::arg("bias") = 0);
 
   m.def(
       "bwd",

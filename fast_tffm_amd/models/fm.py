@@ -52,6 +52,7 @@ class FMConfig:
     grad_reduce: str = "sum"          # sum | mean (multi-rank)
     dedup_chunk: int = 32             # CH of the segmented backward
     threads: int = 0                  # CPU kernels (0 = OpenMP default)
+    global_bias: bool = False         # learned global bias b0 (extension; the reference has none)
 
 
 @dataclass
@@ -172,6 +173,15 @@ class FactorizationMachine:
         self._graph = None
         self._graph_pool: list[_GraphedStep] = []
         self._exchange = None
+        # optional global bias b0 (+ optimizer state), replicated on every rank; its gradient
+        # sum(dpred) is all-reduced over the ranks each step (the model's one dense parameter)
+        if cfg.global_bias:
+            acc0 = float(cfg.opt.initial_accumulator) if cfg.opt.name in ("adagrad", "ftrl") else 0.0
+            self.gbias = torch.zeros(1, dtype=torch.float32, device=self.device)
+            self.gbias_s0 = torch.full((1,), acc0, dtype=torch.float32, device=self.device)
+            self.gbias_s1 = torch.zeros(1, dtype=torch.float32, device=self.device)
+        else:
+            self.gbias = self.gbias_s0 = self.gbias_s1 = None
         if mode in ("shard", "dp", "dp_dense") and self.world >= 1 and dist is not None:
             from ..parallel.exchange import make_exchange
 
@@ -193,6 +203,31 @@ class FactorizationMachine:
         if self.world > 1 and self.cfg.grad_reduce == "mean":
             s /= self.world
         return s
+
+    def bias_step(self, dpred: torch.Tensor) -> None:
+        """Update the global bias from this rank's dpred (dL/dpred, already scaled): the
+        gradient sum(dpred) is summed over ranks (all-reduce), then the optimizer step
+        (same rule as the table's) runs identically on every rank.  Graph-capturable."""
+        if self.gbias is None:
+            return
+        g = dpred.sum().reshape(1)
+        if self.dist is not None and self.world > 1:
+            import torch.distributed as tdist
+
+            tdist.all_reduce(g, group=self.dist.group)
+        o = self.cfg.opt
+        if o.name == "adagrad":
+            self.gbias_s0.add_(g * g)
+            self.gbias.sub_(o.lr * g * torch.rsqrt(self.gbias_s0))
+        elif o.name == "ftrl":
+            n_new = self.gbias_s0 + g * g
+            self.gbias_s1.add_(g - (n_new.sqrt() - self.gbias_s0.sqrt()) / o.lr * self.gbias)
+            self.gbias_s0.copy_(n_new)
+            quad = (o.beta + n_new.sqrt()) / o.lr + 2.0 * o.l2
+            z = self.gbias_s1
+            self.gbias.copy_(torch.where(z.abs() > o.l1, (torch.sign(z) * o.l1 - z) / quad, torch.zeros_like(z)))
+        else:
+            self.gbias.sub_(o.lr * g)
 
     @staticmethod
     def _slot_bits(b: Batch, always: bool = False) -> int:
@@ -266,7 +301,8 @@ class FactorizationMachine:
             fo = K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,
                               weights=b.weights, loss=cfg.loss_type, grad_scale=self.grad_scale(b.B), want_r1=True,
                               pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
-                              threads=cfg.threads)
+                              threads=cfg.threads, bias=self.gbias)
+            self.bias_step(fo.dpred)
         if gpu:
             if side is not main:
                 main.wait_stream(side)
@@ -317,7 +353,7 @@ class FactorizationMachine:
         rows = b.ids.to(torch.int32)
         return K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,
                             weights=b.weights, loss=loss, grad_scale=1.0, want_r1=False, want_reg=want_reg,
-                            threads=self.cfg.threads)
+                            threads=self.cfg.threads, bias=self.gbias)
 
     def predict(self, b: Batch) -> torch.Tensor:
         """Raw scores (logits for logistic loss), like the reference's pred_ops (run_tffm.py:10-17)."""

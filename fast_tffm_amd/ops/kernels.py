@@ -152,10 +152,12 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
                weights: torch.Tensor | None = None, loss: str = "none", grad_scale: float = 1.0,
                want_r1: bool = True, want_reg: bool = False, pred: torch.Tensor | None = None,
                r1: torch.Tensor | None = None, dpred: torch.Tensor | None = None,
-               partial: torch.Tensor | None = None, threads: int = 0) -> FwdOut:
+               partial: torch.Tensor | None = None, threads: int = 0,
+               bias: torch.Tensor | None = None) -> FwdOut:
     """FM score of a CSR batch (reference FmScorer, cc/fm_scorer_op.h:101-140), fused with the loss.
 
-    pred_i = sum_j x_j w_j + 1/2 sum_k [(sum_j x_j v_jk)^2 - sum_j x_j^2 v_jk^2]
+    pred_i = sum_j x_j w_j + 1/2 sum_k [(sum_j x_j v_jk)^2 - sum_j x_j^2 v_jk^2]  (+ bias[0], optional
+    global bias; the reference has none, fm_scorer_op.h:134-136)
     With ``loss`` in {mse, logistic} also returns the summed weighted loss and
     ``dpred = grad_scale * dL_i/dpred_i``.
     """
@@ -171,6 +173,8 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
     w_stride = w.stride(0)
     _check(w.shape[0] >= v.shape[0], "w: fewer rows than v")
     lt = LOSS_TYPES[loss]
+    if bias is not None:
+        _chk_vec(bias, torch.float32, 1, "bias", dev)
     if lt:
         _chk_vec(labels, torch.float32, B, "labels", dev)
         _chk_vec(weights, torch.float32, B, "weights", dev)
@@ -195,7 +199,7 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
               w_stride=w_stride, Kp=Kp, dtype=dt, labels=_p(labels), weights=_p(weights), loss_type=lt,
               grad_scale=float(grad_scale), pred=_p(pred), r1=_p(r1), dpred=_p(dpred) if lt else 0,
               loss_partial=_p(lp) if lt else 0, reg_partial=_p(rp) if want_reg else 0, grid=grid,
-              stream=_stream(rows))
+              stream=_stream(rows), bias=_p(bias))
         loss_sum = lp.sum(dtype=torch.float32) if lt else None
         regv = rp.view(grid, 2)[:, 0].sum() if want_reg else None
         regw = rp.view(grid, 2)[:, 1].sum() if want_reg else None
@@ -204,7 +208,7 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
         ls, rv, rw = c.fwd(B=B, offsets=_p(offsets), rows=_p(rows), vals=_p(vals), v=_p(v), v_stride=v_stride,
                            w=_p(w), w_stride=w_stride, Kp=Kp, dtype=dt, labels=_p(labels), weights=_p(weights),
                            loss_type=lt, grad_scale=float(grad_scale), pred=_p(pred), r1=_p(r1),
-                           dpred=_p(dpred) if lt else 0, threads=threads)
+                           dpred=_p(dpred) if lt else 0, threads=threads, bias=_p(bias))
         loss_sum = torch.tensor(ls, dtype=torch.float32) if lt else None
         regv = torch.tensor(rv, dtype=torch.float32) if want_reg else None
         regw = torch.tensor(rw, dtype=torch.float32) if want_reg else None

@@ -249,7 +249,8 @@ class ShardExchange(_Base):
             fo = K.fm_forward(b.offsets, dd.inv[: b.nnz], b.vals, src_v, src_w, Kp, labels=b.labels,
                               weights=b.weights, loss=cfg.loss_type, grad_scale=m.grad_scale(b.B), want_r1=True,
                               pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B],
-                              partial=ws.fwd_partial, threads=cfg.threads)
+                              partial=ws.fwd_partial, threads=cfg.threads, bias=m.gbias)
+            m.bias_step(fo.dpred)
         grad = torch.empty((pl.U, self.gs), dtype=torch.float32, device=self.dev)
         rv, rw = m.reg_coeffs
         with roctx_range("bwd"):
@@ -277,7 +278,7 @@ class ShardExchange(_Base):
         gathered = self._gather(pl)
         out = K.fm_forward(b.offsets, pl.dd.inv[: b.nnz], b.vals, gathered[:, : self.Kp], gathered[:, self.Kp],
                            self.Kp, labels=b.labels, weights=b.weights, loss=loss, grad_scale=1.0, want_r1=False,
-                           want_reg=want_reg, threads=self.m.cfg.threads)
+                           want_reg=want_reg, threads=self.m.cfg.threads, bias=self.m.gbias)
         if self.dev.type == "cuda":
             done = torch.cuda.Event()
             done.record(torch.cuda.current_stream(self.dev))
@@ -294,7 +295,9 @@ class DPExchange(_Base):
         ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz)
         fo = K.fm_forward(b.offsets, rows, b.vals, m.table.v, m.table.w, Kp, labels=b.labels, weights=b.weights,
                           loss=cfg.loss_type, grad_scale=m.grad_scale(b.B), want_r1=True, pred=ws.pred[: b.B],
-                          r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial, threads=cfg.threads)
+                          r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial, threads=cfg.threads,
+                          bias=m.gbias)
+        m.bias_step(fo.dpred)
         dd = K.dedup(rows, ws=ws.dd, key_bits=bits_for(m.table.rows), ex_of_occ=ex, vals=b.vals,
                      num_examples=b.B, Kp=Kp)
         U = dd.sync()
@@ -337,7 +340,7 @@ class DPExchange(_Base):
         t = self.m.table
         return K.fm_forward(b.offsets, b.ids.to(torch.int32), b.vals, t.v, t.w, self.Kp, labels=b.labels,
                             weights=b.weights, loss=loss, grad_scale=1.0, want_r1=False, want_reg=want_reg,
-                            threads=self.m.cfg.threads)
+                            threads=self.m.cfg.threads, bias=self.m.gbias)
 
 
 class DPDenseExchange(DPExchange):

@@ -58,7 +58,9 @@ def export_model(ckpt_dir: str, export_path: str, *, vocabulary_block_num: int, 
         "hash_feature_id": bool(hash_feature_id),
         "loss_type": loss_type,
         "global_step": meta["global_step"],
-        "score": "raw FM score (logit for logistic loss), no global bias",
+        "global_bias": meta.get("global_bias"),
+        "score": "raw FM score (logit for logistic loss)" + (" incl. the global bias" if meta.get("global_bias")
+                                                             is not None else ", no global bias"),
     })
     with open(os.path.join(tmp, "saved_model.json"), "w") as f:
         json.dump(doc, f, indent=1)
@@ -129,8 +131,10 @@ class ServingModel:
         flat = np.asarray(data_lines).reshape(-1).tolist()
         offsets, ids, vals = parse_serving_lines(flat, self.meta["vocabulary_size"], self.meta["hash_feature_id"])
         d = self.device
+        gb = self.meta.get("global_bias")
+        bias = torch.tensor([gb], dtype=torch.float32, device=d) if gb is not None else None
         fo = Kn.fm_forward(offsets.to(d), ids.to(torch.int32).to(d), vals.to(d), self.v, self.w, self.Kp,
-                           want_r1=False)
+                           want_r1=False, bias=bias)
         return fo.pred.cpu().numpy()
 
 

@@ -84,7 +84,11 @@ def save_checkpoint(model, log_dir: str, step: int, *, reader_state: dict | None
     if sharded or rank == 0:
         shard_rank, shard_world = (table.rank, table.world)
         tmp = os.path.join(path, _shard_name(shard_rank, shard_world) + ".tmp")
-        save_file(_table_tensors(table), tmp, metadata={"format": FORMAT, "rank": str(shard_rank),
+        tensors = _table_tensors(table)
+        if getattr(model, "gbias", None) is not None:  # replicated global bias + optimizer state
+            for k in ("gbias", "gbias_s0", "gbias_s1"):
+                tensors[k] = getattr(model, k).detach().to("cpu").contiguous()
+        save_file(tensors, tmp, metadata={"format": FORMAT, "rank": str(shard_rank),
                                                           "world": str(shard_world)})
         os.replace(tmp, os.path.join(path, _shard_name(shard_rank, shard_world)))
     if ctx is not None and world > 1:
@@ -101,6 +105,7 @@ def save_checkpoint(model, log_dir: str, step: int, *, reader_state: dict | None
             "mode": model.mode,
             "loss_type": model.cfg.loss_type,
             "reader_state": reader_state or {},
+            "global_bias": float(model.gbias.item()) if getattr(model, "gbias", None) is not None else None,
         }
         with open(os.path.join(path, "meta.json.tmp"), "w") as f:
             json.dump(meta, f, indent=1)
@@ -149,6 +154,12 @@ def restore_checkpoint(model, ckpt_dir: str) -> dict:
     K = table.K
     dev = table.device
     direct = os.path.join(ckpt_dir, _shard_name(table.rank, table.world))
+    if getattr(model, "gbias", None) is not None:
+        first = next(iter(_iter_shards(ckpt_dir)), None)
+        bt = load_file(first[2]) if first is not None else {}
+        for k in ("gbias", "gbias_s0", "gbias_s1"):
+            if k in bt:
+                getattr(model, k).copy_(bt[k].to(getattr(model, k).device))
     if os.path.exists(direct):
         t = load_file(direct)
         _copy_rows(table, None, t, K, dev)

@@ -41,7 +41,7 @@ def workdir(tmp_path, ref_data_dir):
 
 def _write_cfg(workdir, **over):
     vals = dict(loss_type="logistic", batch_size=1000, epoch_num=2, save_steps=3, extra_train="",
-                log_dir=str(workdir / "log"), factor_num=8)
+                log_dir=str(workdir / "log"), factor_num=8, extra_general="")
     vals.update(over)
     text = f"""[General]
 vocabulary_size = 200000
@@ -51,6 +51,7 @@ hash_feature_id = False
 log_dir = {vals['log_dir']}
 save_summaries_steps = 1
 device = cpu
+{vals['extra_general']}
 
 [Train]
 batch_size = {vals['batch_size']}
@@ -104,8 +105,9 @@ def test_reference_sample_cfg_loads():
     assert len(c.train_files) == 5 and len(c.weight_files) == 5  # resolved next to the cfg
 
 
-def test_train_predict_generate(workdir):
-    cfg_path = _write_cfg(workdir)
+@pytest.mark.parametrize("global_bias", [False, True])
+def test_train_predict_generate(workdir, global_bias):
+    cfg_path = _write_cfg(workdir, extra_general="global_bias = true" if global_bias else "")
     rc, out = _run(["train", cfg_path, "--max-steps", "5"])
     assert rc == 0
     assert "======== train ========" in out
