@@ -31,6 +31,11 @@ CPU_SOURCES = ["cpu/module.cpp", "cpu/parser.cpp", "cpu/kernels.cpp"]
 HIP_SOURCES = ["hip/module.hip"]
 HIP_DEPS = ["hip/fm_fwd.hip", "hip/fm_bwd.hip", "hip/dedup.hip", "hip/shard.hip", "hip/init.hip",
             "hip/fm_common.h", "hash64.h"]
+# A/B build variants of the gfx950 module: name -> preprocessor defines (module _fm_hip_<name>,
+# selected at run time with FM_HIP_VARIANT=<name>; tools/gpu_ab.sh).  Used for same-box kernel
+# comparisons, e.g. {"pipe": ["-DFM_VARIANT_PIPE"]} measured the software-pipelined fwd/chunk
+# kernels at -0.6% step time under the lookahead step (not kept: no clear win).
+HIP_VARIANTS: dict[str, list[str]] = {}
 
 
 _EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"  # resolved once (lazy init is not thread-safe)
@@ -84,16 +89,18 @@ def hipcc_path() -> str | None:
     return None
 
 
-def build_hip(force: bool = False) -> str:
+def build_hip(force: bool = False, variant: str | None = None) -> str:
     os.makedirs(OUT, exist_ok=True)
-    target = os.path.join(OUT, "_fm_hip" + _ext_suffix())
+    name = "_fm_hip" + (f"_{variant}" if variant else "")
+    defines = [f"-DFM_HIP_MODULE={name}", *(HIP_VARIANTS[variant] if variant else [])]
+    target = os.path.join(OUT, name + _ext_suffix())
     if force or _stale(target, HIP_SOURCES + HIP_DEPS):
         hipcc = hipcc_path()
         if hipcc is None:
             raise RuntimeError("hipcc not found; cannot build the gfx950 extension")
         tmp = target + ".tmp"
         cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
-               "-Wno-unused-result", *_py_includes(), f"-I{CSRC}",
+               "-Wno-unused-result", *defines, *_py_includes(), f"-I{CSRC}",
                *[os.path.join(CSRC, s) for s in HIP_SOURCES], "-o", tmp]
         _run(cmd)
         os.replace(tmp, target)
@@ -115,7 +122,11 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--cpu-only", action="store_true")
     ap.add_argument("--hip-only", action="store_true")
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--variant", choices=sorted(HIP_VARIANTS), help="build an A/B variant of the HIP module")
     a = ap.parse_args(argv)
+    if a.variant:
+        print("built", build_hip(a.force, a.variant))
+        return 0
     outs = build_all(force=a.force, cpu=not a.hip_only, hip=not a.cpu_only)
     for o in outs:
         print("built", o)

@@ -191,116 +191,98 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_chunk_kernel(BwdArgs a) {
   for (int s = nslc ? (int)(blockIdx.x % nx) : 0; s < (nslc ? nslc : 1); s += nx) {
   const int i0 = nslc ? a.slice_start[s] : 0;
   const int i1 = nslc ? a.slice_start[s + 1] : nchunks;
-  // Software pipeline over this lane group's chunks k = ii, ii+stride, ...: while
-  // chunk k is reduced, the descriptor of k+2 (chunk id of k+3), the occurrences
-  // (example, x) of k+1 and -- after the reduction -- dpred of k+1 are loaded, so
-  // the only memory round trip left on a chunk's critical path is its r1 gather
-  // (the row state loads of single-chunk rows are issued alongside).
-  struct Desc { int j0, j1, seg, key; };
-  auto valid = [&](int i) { return i < i1; };
-  auto cid_at = [&](int i) { return nslc ? a.slice_list[i] : i; };
-  auto load_desc = [&](int i, int cid) {
-    Desc d{0, 0, 0, 0};
-    if (valid(i)) { d.j0 = a.chunk_start[cid]; d.j1 = a.chunk_start[cid + 1]; d.seg = a.chunk_seg[cid]; d.key = a.chunk_key[cid]; }
-    return d;
-  };
-  auto load_occ = [&](const Desc& d, int (&ex)[PF], float (&x)[PF]) {
+  // Software pipeline over this lane group's chunks: the descriptor of the next
+  // chunk (and the list entry of the one after) load while the current one is
+  // reduced, so the dependent metadata chain is off the critical path.
+  int ii = i0 + wave_in_x * G + g;
+  auto chunk_at = [&](int i) { return nslc ? a.slice_list[i] : i; };
+  int c = ii < i1 ? chunk_at(ii) : 0;
+  int cn = ii + stride < i1 ? chunk_at(ii + stride) : 0;
+  int d_j0 = 0, d_j1 = 0, d_seg = 0, d_key = 0;
+  if (ii < i1) {
+    d_j0 = a.chunk_start[c]; d_j1 = a.chunk_start[c + 1]; d_seg = a.chunk_seg[c]; d_key = a.chunk_key[c];
+  }
+  for (; ii < i1; ii += stride) {
+    const int cc = c, j0 = d_j0, j1 = d_j1, key = d_key;
+    const int u = d_seg & kChunkSegMask;
+    const bool single = (unsigned)d_seg & kChunkSingle;
+    const bool first = d_seg & kChunkFirst;
+    const bool dense = d_seg & kChunkDense;
+    if (ii + stride < i1) {
+      c = cn;
+      d_j0 = a.chunk_start[c]; d_j1 = a.chunk_start[c + 1]; d_seg = a.chunk_seg[c]; d_key = a.chunk_key[c];
+      cn = ii + 2 * stride < i1 ? chunk_at(ii + 2 * stride) : 0;
+    }
+    if (dense) continue;  // gradient from the MFMA path (fm_bwd_dense_kernel)
+    const int len = j1 - j0;
+    RowState<EPL> rs;
+    if (single) bwd_load_row<TV, EPL>(a, a.mode == kBwdLocal ? (long long)key : (long long)u, tE, rs);
+    // lane-parallel prefetch of the chunk's (example, dpred*x, x)
+    int pex[PF];
+    float pc[PF], px[PF];
 #pragma unroll
     for (int q = 0; q < PF; ++q) {
-      const int jj = d.j0 + q * LPR + t;
-      const int jc = jj < d.j1 ? jj : d.j0;
-      ex[q] = a.sorted_ex[jc] >> a.ex_shift;
-      x[q] = a.sorted_x ? a.sorted_x[jc] : 1.f;
+      const int jj = j0 + q * LPR + t;
+      const bool ok = jj < j1;
+      const int jc = ok ? jj : j0;
+      const int ex = a.sorted_ex[jc] >> a.ex_shift;
+      const float x = a.sorted_x ? a.sorted_x[jc] : 1.f;
+      pex[q] = ex;
+      px[q] = x;
+      pc[q] = ok ? a.dpred[ex] * x : 0.f;
     }
-  };
-  auto load_c = [&](const Desc& d, const int (&ex)[PF], const float (&x)[PF], float (&c)[PF]) {
+    float A[EPL];
 #pragma unroll
-    for (int q = 0; q < PF; ++q) c[q] = d.j0 + q * LPR + t < d.j1 ? a.dpred[ex[q]] * x[q] : 0.f;
-  };
-  int ii = i0 + wave_in_x * G + g;
-  int c0 = valid(ii) ? cid_at(ii) : 0;
-  int c1 = valid(ii + stride) ? cid_at(ii + stride) : 0;
-  int c2 = valid(ii + 2 * stride) ? cid_at(ii + 2 * stride) : 0;
-  Desc d0 = load_desc(ii, c0), d1 = load_desc(ii + stride, c1);
-  int pex[PF];
-  float pc[PF], px[PF];
-  load_occ(d0, pex, px);
-  load_c(d0, pex, px, pc);
-  for (; ii < i1; ii += stride) {
-    const Desc d2 = load_desc(ii + 2 * stride, c2);
-    const int c3 = valid(ii + 3 * stride) ? cid_at(ii + 3 * stride) : 0;
-    int nex[PF];
-    float nxv[PF];
-    load_occ(d1, nex, nxv);
-    const int cid = c0, j0 = d0.j0, j1 = d0.j1, key = d0.key;
-    const int u = d0.seg & kChunkSegMask;
-    const bool single = (unsigned)d0.seg & kChunkSingle;
-    const bool first = d0.seg & kChunkFirst;
-    const bool dense = d0.seg & kChunkDense;  // gradient from the MFMA path (fm_bwd_dense_kernel)
-    if (!dense) {
-      const int len = j1 - j0;
-      RowState<EPL> rs;
-      if (single) bwd_load_row<TV, EPL>(a, a.mode == kBwdLocal ? (long long)key : (long long)u, tE, rs);
-      float A[EPL];
+    for (int k = 0; k < EPL; ++k) A[k] = 0.f;
+    float Scx = 0.f, Sc = 0.f;
 #pragma unroll
-      for (int k = 0; k < EPL; ++k) A[k] = 0.f;
-      float Scx = 0.f, Sc = 0.f;
+    for (int q = 0; q < PF; ++q) {
+      if (q * LPR < len) {
+        for (int l = 0; l < LPR && q * LPR + l < len; l += UNR) {
+          float rr[UNR][EPL], cc[UNR], xx[UNR];
 #pragma unroll
-      for (int q = 0; q < PF; ++q) {
-        if (q * LPR < len) {
-          for (int l = 0; l < LPR && q * LPR + l < len; l += UNR) {
-            float rr[UNR][EPL], cv[UNR], xx[UNR];
+          for (int uu = 0; uu < UNR; ++uu) {
+            const int li = l + uu;
+            const bool ok = li < LPR && q * LPR + li < len;
+            const int src = gbase + (ok ? li : 0);
+            // shuffles are unconditional (every lane of the group takes part); mask after
+            const int ex = __shfl(pex[q], src, kWave);
+            const float cs = __shfl(pc[q], src, kWave);
+            cc[uu] = ok ? cs : 0.f;
+            xx[uu] = __shfl(px[q], src, kWave);
+            const float* rp = a.r1 + (long long)ex * a.Kp + tE * EPL;
 #pragma unroll
-            for (int uu = 0; uu < UNR; ++uu) {
-              const int li = l + uu;
-              const bool ok = li < LPR && q * LPR + li < len;
-              const int src = gbase + (ok ? li : 0);
-              // shuffles are unconditional (every lane of the group takes part); mask after
-              const int ex = __shfl(pex[q], src, kWave);
-              const float cs = __shfl(pc[q], src, kWave);
-              cv[uu] = ok ? cs : 0.f;
-              xx[uu] = __shfl(px[q], src, kWave);
-              const float* rp = a.r1 + (long long)ex * a.Kp + tE * EPL;
-#pragma unroll
-              for (int k = 0; k < EPL; k += 4) {
-                const float4 f = *reinterpret_cast<const float4*>(rp + k);
-                rr[uu][k] = f.x; rr[uu][k + 1] = f.y; rr[uu][k + 2] = f.z; rr[uu][k + 3] = f.w;
-              }
+            for (int k = 0; k < EPL; k += 4) {
+              const float4 f = *reinterpret_cast<const float4*>(rp + k);
+              rr[uu][k] = f.x; rr[uu][k + 1] = f.y; rr[uu][k + 2] = f.z; rr[uu][k + 3] = f.w;
             }
+          }
 #pragma unroll
-            for (int uu = 0; uu < UNR; ++uu) {
+          for (int uu = 0; uu < UNR; ++uu) {
 #pragma unroll
-              for (int k = 0; k < EPL; ++k) A[k] += cv[uu] * rr[uu][k];
-              Scx += cv[uu] * xx[uu];
-              Sc += cv[uu];
-            }
+            for (int k = 0; k < EPL; ++k) A[k] += cc[uu] * rr[uu][k];
+            Scx += cc[uu] * xx[uu];
+            Sc += cc[uu];
           }
         }
       }
-      if (single) {
-        bwd_finish<LPR, TV, EPL>(a, u, t, tact, rs, A, Scx, Sc, len);
-      } else {
-        float* dst = a.partial + (long long)cid * (a.Kp + 4);
-        if (tact) {
+    }
+    if (single) {
+      bwd_finish<LPR, TV, EPL>(a, u, t, tact, rs, A, Scx, Sc, len);
+    } else {
+      float* dst = a.partial + (long long)cc * (a.Kp + 4);
+      if (tact) {
 #pragma unroll
-          for (int k = 0; k < EPL; k += 4)
-            *reinterpret_cast<float4*>(dst + t * EPL + k) = make_float4(A[k], A[k + 1], A[k + 2], A[k + 3]);
-        }
-        if (t == 0) {
-          dst[a.Kp] = Scx;
-          dst[a.Kp + 1] = Sc;
-          // the row's first chunk registers the row for the combine kernels
-          if (first) a.multi[atomicAdd(&a.counts_rw[2], 1)] = u;
-        }
+        for (int k = 0; k < EPL; k += 4)
+          *reinterpret_cast<float4*>(dst + t * EPL + k) = make_float4(A[k], A[k + 1], A[k + 2], A[k + 3]);
+      }
+      if (t == 0) {
+        dst[a.Kp] = Scx;
+        dst[a.Kp + 1] = Sc;
+        // the row's first chunk registers the row for the combine kernels
+        if (first) a.multi[atomicAdd(&a.counts_rw[2], 1)] = u;
       }
     }
-    // dpred of chunk k+1 (its examples arrived during this chunk's reduction), then rotate
-    float npc[PF];
-    load_c(d1, nex, nxv, npc);
-#pragma unroll
-    for (int q = 0; q < PF; ++q) { pex[q] = nex[q]; px[q] = nxv[q]; pc[q] = npc[q]; }
-    c0 = c1; c1 = c2; c2 = c3;
-    d0 = d1; d1 = d2;
   }
   }
 }

@@ -38,18 +38,17 @@ struct FwdArgs {
 // Rows of one example kept in flight per lane group: enough to cover a
 // Criteo-shaped example (39 features) in one round for K=64 (G=4 -> 10 row
 // loads per lane) while bounding VGPRs for large K.
-template <int G, int EPL>
+template <int G>
 struct FwdUnroll {
-  static constexpr int cap = 40 / EPL;  // <= 40 fp32 row values in flight per lane (fits 4 waves/SIMD)
-  static constexpr int v = (40 / G) < 1 ? 1 : ((40 / G) > cap ? cap : (40 / G));
+  static constexpr int v = (40 / G) < 1 ? 1 : ((40 / G) > 12 ? 12 : (40 / G));
 };
 
 template <int LPR, typename TV>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void fm_fwd_kernel(FwdArgs a) {
+__global__ __launch_bounds__(kBlock) void fm_fwd_kernel(FwdArgs a) {
   using F = Frag<TV>;
   constexpr int EPL = F::N;
   constexpr int G = kWave / LPR;
-  constexpr int UNR = FwdUnroll<G, EPL>::v;
+  constexpr int UNR = FwdUnroll<G>::v;
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR, t = lane % LPR;
   const int nv = a.Kp / EPL;
@@ -63,36 +62,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   const bool want_reg = a.reg_partial != nullptr;
 
   float loss_acc = 0.f, regv_acc = 0.f, regw_acc = 0.f;
-  // Software pipeline over this wave's examples i, i+nw, i+2nw: the CSR bounds are
-  // loaded two examples ahead and the first 64 (row, x) pairs one example ahead, so
-  // the only memory round trip left on an example's critical path is its row loads.
-  int cs = 0, ce = 0, ns = 0, ne = 0;
-  int pre_row = 0;
-  float pre_x = 0.f;
-  if (wave < a.B) {
-    cs = a.offsets[wave]; ce = a.offsets[wave + 1];
-    if (lane < ce - cs) {
-      pre_row = a.rows[cs + lane];
-      pre_x = a.vals ? a.vals[cs + lane] : 1.f;
-    }
-  }
-  if (wave + nwaves < a.B) { ns = a.offsets[wave + nwaves]; ne = a.offsets[wave + nwaves + 1]; }
   for (int i = wave; i < a.B; i += nwaves) {
-    const int s = cs, e = ce;
-    const int cur_row = pre_row;
-    const float cur_x = pre_x;
-    {  // issue the loads of the next two examples before this one's row loads
-      const int i1 = i + nwaves, i2 = i + 2 * nwaves;
-      int fs2 = 0, fe2 = 0;
-      if (i2 < a.B) { fs2 = a.offsets[i2]; fe2 = a.offsets[i2 + 1]; }
-      pre_row = 0;
-      pre_x = 0.f;
-      if (i1 < a.B && lane < ne - ns) {
-        pre_row = a.rows[ns + lane];
-        pre_x = a.vals ? a.vals[ns + lane] : 1.f;
-      }
-      cs = ns; ce = ne; ns = fs2; ne = fe2;
-    }
+    const int s = a.offsets[i], e = a.offsets[i + 1];
     float s1[EPL], s2[EPL];
 #pragma unroll
     for (int k = 0; k < EPL; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
@@ -101,10 +72,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       const int m = min(kWave, e - base);
       int my_row = 0;
       float my_x = 0.f;
-      if (base == s) {  // prefetched
-        my_row = cur_row;
-        my_x = cur_x;
-      } else if (lane < m) {
+      if (lane < m) {
         my_row = a.rows[base + lane];
         my_x = a.vals ? a.vals[base + lane] : 1.f;
       }

@@ -13,6 +13,10 @@
 #include "fm_common.h"
 
 namespace py = pybind11;
+
+#ifndef FM_HIP_MODULE
+#define FM_HIP_MODULE _fm_hip
+#endif
 using u64 = std::uintptr_t;
 
 // Unity build: all kernel sources are compiled in this translation unit.
@@ -43,7 +47,7 @@ fm::OptParams opt_params(int type, float lr, float l1, float l2, float beta) {
 
 }  // namespace
 
-PYBIND11_MODULE(_fm_hip, m) {
+PYBIND11_MODULE(FM_HIP_MODULE, m) {
   m.doc() = "gfx950 HIP kernels for fast_tffm_amd (FM forward/backward/optimizer, dedup, sharding)";
   m.attr("ARCH") = "gfx950";
   m.attr("MAX_CH") = fm::kMaxCH;

@@ -31,8 +31,6 @@ from ..data.batch import Batch
 from ..ops import kernels as K
 from ..utils.trace import roctx_range
 
-# dedup on a side stream concurrently with the forward (1) or before it on the same stream (0)
-_SIDE_STREAM = os.environ.get("FM_SIDE_STREAM", "1") == "1"
 from .table import FMTable, bits_for, rows_per_shard
 
 
@@ -91,6 +89,93 @@ class _Workspace:
                                if dev.type == "cuda" and Kp <= 128 else None)
         if not hasattr(self, "fwd_partial"):
             self.fwd_partial = torch.zeros(3 * 4096, dtype=torch.float32, device=dev)
+
+
+class _LocalSlot:
+    """Double-buffered dedup workspace of the local lookahead pipeline."""
+
+    def __init__(self):
+        self.dd: K.DedupWorkspace | None = None
+        self.rows32: torch.Tensor | None = None
+        self.done = None
+
+    def ensure(self, nnz: int, dev, CH: int) -> None:
+        if self.dd is None or self.dd.cap < nnz:
+            cap = max(nnz, 1, int(1.25 * (self.dd.cap if self.dd else 0)))
+            self.dd = K.DedupWorkspace(cap, dev, CH)
+            self.rows32 = torch.empty(cap, dtype=torch.int32, device=dev)
+
+
+@dataclass
+class _LocalPlan:
+    b: Batch
+    slot: int
+    rows: torch.Tensor
+    dd: object
+    ready: object
+
+
+class _LookaheadGraphRing:
+    """hipGraphs of the lookahead local step over a ring of n (even) static input buffers.
+
+    Graph k replays [side stream: csr_rows + dedup of buffer k+1 into slot (k+1)%2]
+    concurrently with [main: forward + loss + backward/update of buffer k reading
+    slot k%2], i.e. the eager lookahead step with one launch.  The plan of buffer 0
+    is built eagerly once; a launch of graph k completes before graph k+1 starts, so
+    slot k%2 is never written while it is read.
+    """
+
+    def __init__(self, model: "FactorizationMachine", example: Batch, n: int):
+        if n < 2 or n % 2:
+            raise ValueError("the lookahead ring needs an even number (>= 2) of buffers")
+        self.m = model
+        dev = model.device
+
+        def static(t):
+            return None if t is None else torch.empty_like(t, device=dev)
+
+        ids = example.ids if example.ids.dtype == torch.int32 else example.ids.to(torch.int32)
+        self.bufs = [Batch(static(example.labels), static(example.offsets), static(ids), static(example.vals),
+                           static(example.weights), example.nnz, max_feats=example.max_feats) for _ in range(n)]
+        self.graphs: list = [None] * n
+        self.outs: list = [None] * n
+        self.dds: list = [None, None]    # DedupOut views of slot 0 / 1 (fixed addresses)
+        self.rows: list = [None, None]
+        self.primed = False
+
+    def index(self, b: Batch, nb: Batch | None) -> int:
+        n = len(self.bufs)
+        for k, buf in enumerate(self.bufs):
+            if buf.ids.data_ptr() == b.ids.data_ptr():
+                return k if nb is not None and self.bufs[(k + 1) % n].ids.data_ptr() == nb.ids.data_ptr() else -1
+        return -1
+
+    def _body(self, k: int) -> StepOut:
+        m, n = self.m, len(self.bufs)
+        main = torch.cuda.current_stream(m.device)
+        side = m._side_stream()
+        side.wait_stream(main)
+        nxt = (k + 1) % n
+        with torch.cuda.stream(side):
+            self.rows[nxt % 2], self.dds[nxt % 2] = m._plan_into(m._lslots[nxt % 2], self.bufs[nxt])
+        out = m._fwd_bwd_local(self.bufs[k], self.rows[k % 2], self.dds[k % 2])
+        main.wait_stream(side)
+        return out
+
+    def replay(self, k: int) -> StepOut:
+        m = self.m
+        m.ws.ensure(self.bufs[k].B, self.bufs[k].nnz)
+        if not self.primed:  # plan of buffer 0, eagerly
+            self.rows[0], self.dds[0] = m._plan_into(m._lslots[0], self.bufs[0])
+            self.primed = True
+        if self.graphs[k] is None:
+            torch.cuda.synchronize(m.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.outs[k] = self._body(k)  # capture executes nothing; the replay below runs the step
+            self.graphs[k] = g
+        self.graphs[k].replay()
+        return StepOut(self.outs[k].loss_sum.clone(), self.bufs[k].B)
 
 
 class _GraphedStep:
@@ -170,6 +255,10 @@ class FactorizationMachine:
         self.ws = _Workspace(self.device, self.Kp, cfg.dedup_chunk)
         self.global_step = 0
         self._side = None
+        self._lslots = [_LocalSlot(), _LocalSlot()]   # lookahead dedup plans (eager local path)
+        self._lpending = None
+        self._llast = 1
+        self._ring = None
         self._graph = None
         self._graph_pool: list[_GraphedStep] = []
         self._exchange = None
@@ -251,7 +340,9 @@ class FactorizationMachine:
         ``next_batch`` (optional lookahead): the batch of the following call;
         multi-rank executors prepare its table-independent work (dedup, id
         exchange) concurrently with this step."""
-        if self._graph is not None and self._graph.matches(b):
+        if self._ring is not None and (k := self._ring.index(b, next_batch)) >= 0:
+            out = self._ring.replay(k)
+        elif self._graph is not None and self._graph.matches(b):
             g = self._graph
             # a batch that already lives in a captured graph's input buffers replays that graph, no copy
             for other in self._graph_pool:
@@ -265,6 +356,8 @@ class FactorizationMachine:
                 out = self._exchange.train_step(b, next_batch)
             elif self._exchange is not None:
                 out = self._exchange.train_step(b)
+            elif self.device.type == "cuda" and (next_batch is not None or self._lpending is not None):
+                out = self._local_lookahead_step(b, next_batch)
             else:
                 out = self._local_train_step(b)
         self.global_step += 1
@@ -286,9 +379,8 @@ class FactorizationMachine:
         gpu = self.device.type == "cuda"
         if gpu:
             main = torch.cuda.current_stream(self.device)
-            side = self._side_stream() if _SIDE_STREAM else main
-            if side is not main:  # (a stream waiting on itself inside a hipGraph capture faults at replay)
-                side.wait_stream(main)  # inputs ready; previous step's readers of ws.dd are enqueued before
+            side = self._side_stream()
+            side.wait_stream(main)  # inputs ready; previous step's readers of ws.dd are enqueued before
             with torch.cuda.stream(side), roctx_range("dedup"):
                 sb = self._slot_bits(b)
                 ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz, slot_bits=sb)
@@ -304,18 +396,103 @@ class FactorizationMachine:
                               threads=cfg.threads, bias=self.gbias)
             self.bias_step(fo.dpred)
         if gpu:
-            if side is not main:
-                main.wait_stream(side)
+            main.wait_stream(side)
         else:
             dd = K.dedup(rows, ws=ws.dd, key_bits=bits_for(self.table.rows), ex_of_occ=ex, vals=b.vals)
         rv, rw = self.reg_coeffs
         with roctx_range("bwd+update"):
             K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
                           reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, dense_part=ws.dense_part,
-                          dense_stream=self._side_stream() if gpu and _SIDE_STREAM else None)
+                          dense_stream=self._side_stream() if gpu else None)
         return StepOut(fo.loss_sum, b.B)
 
     # ------------------------------------------------------------------
+    def _local_plan(self, b: Batch, inputs_ready=None) -> "_LocalPlan":
+        """dedup (+ csr_rows) of ``b`` on the side stream into a double-buffered slot."""
+        idx = (self._lpending.slot ^ 1) if self._lpending is not None else (self._llast ^ 1)
+        self._llast = idx
+        slot = self._lslots[idx]
+        cfg = self.cfg
+        st = self._side_stream()
+        if slot.done is not None:
+            st.wait_event(slot.done)       # the step that last read this slot has finished
+        ready = getattr(b, "ready", None) or inputs_ready
+        if ready is not None:
+            st.wait_event(ready)
+        else:
+            st.wait_stream(torch.cuda.current_stream(self.device))
+        for t in (b.labels, b.offsets, b.ids, b.vals, b.weights):
+            if t is not None:
+                t.record_stream(st)
+        with torch.cuda.stream(st), roctx_range("dedup_next"):
+            rows, dd = self._plan_into(slot, b)
+            ev = torch.cuda.Event()
+            ev.record(st)
+        return _LocalPlan(b, idx, rows, dd, ev)
+
+    def _plan_into(self, slot: "_LocalSlot", b: Batch):
+        """csr_rows + dedup of ``b`` into ``slot`` on the current stream; returns (rows, DedupOut)."""
+        cfg = self.cfg
+        slot.ensure(b.nnz, self.device, cfg.dedup_chunk)
+        rows = b.ids if b.ids.dtype == torch.int32 else slot.rows32[: b.nnz].copy_(b.ids)
+        sb = self._slot_bits(b)
+        ex = K.csr_rows(b.offsets, out=slot.dd.ex_of_occ[: b.nnz], nnz=b.nnz, slot_bits=sb)
+        dd = K.dedup(rows, ws=slot.dd, key_bits=bits_for(self.table.rows), ex_of_occ=ex, vals=b.vals,
+                     num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets,
+                     dense_min=K.dense_min_for(b.B, self.Kp, cfg.dedup_chunk))
+        return rows, dd
+
+    def _fwd_bwd_local(self, b: Batch, rows: torch.Tensor, dd) -> StepOut:
+        """Forward + loss + backward/update of ``b`` on the current stream (dedup ``dd`` ready)."""
+        ws, cfg = self.ws, self.cfg
+        with roctx_range("fwd"):
+            fo = K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,
+                              weights=b.weights, loss=cfg.loss_type, grad_scale=self.grad_scale(b.B), want_r1=True,
+                              pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
+                              threads=cfg.threads, bias=self.gbias)
+            self.bias_step(fo.dpred)
+        rv, rw = self.reg_coeffs
+        with roctx_range("bwd+update"):
+            K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
+                          reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, dense_part=ws.dense_part,
+                          dense_stream=self._side_stream())
+        return StepOut(fo.loss_sum, b.B)
+
+    def _local_lookahead_step(self, b: Batch, next_batch: Batch | None) -> StepOut:
+        """Eager local step with lookahead: the dedup of ``next_batch`` runs on the side stream
+        concurrently with this step's forward + backward (the dedup of ``b`` was done the same
+        way during the previous step), taking the sort off the critical path."""
+        ws, cfg = self.ws, self.cfg
+        main = torch.cuda.current_stream(self.device)
+        nb_ready = None
+        if next_batch is not None and getattr(next_batch, "ready", None) is None:
+            nb_ready = torch.cuda.Event()   # next_batch's producers: everything enqueued so far
+            nb_ready.record(main)
+        pl = self._lpending
+        if pl is not None and pl.b is b:
+            self._lpending = None
+        else:
+            pl = self._local_plan(b)
+        main.wait_event(pl.ready)
+        out = self._fwd_bwd_local(b, pl.rows, pl.dd)
+        done = torch.cuda.Event()
+        done.record(main)
+        self._lslots[pl.slot].done = done
+        if next_batch is not None:
+            self._lpending = self._local_plan(next_batch, nb_ready)
+        return out
+
+    def lookahead_graph_buffers(self, example: Batch, n: int = 4) -> list[Batch]:
+        """Static input buffers of a lookahead hipGraph ring (local GPU step).
+
+        Calling ``train_step(bufs[k], bufs[(k + 1) % n])`` replays graph k: this
+        step's forward/backward and, concurrently, the dedup of the next buffer (the
+        producer writes batch k+1 into bufs[k+1] before that call)."""
+        if self.device.type != "cuda" or self._exchange is not None:
+            raise RuntimeError("graph capture is available for the local GPU step")
+        self._ring = _LookaheadGraphRing(self, example, n)
+        return self._ring.bufs
+
     def capture_graph(self, example: Batch, warmup: int = 1) -> None:
         """Arm hipGraph execution of the local training step for batches shaped like ``example``.
 

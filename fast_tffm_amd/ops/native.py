@@ -79,7 +79,8 @@ _SYNC = os.environ.get("FM_SYNC_LAUNCH", "0") == "1"
 
 def hip():
     """gfx950 module: GPU step kernels. Raises if unavailable."""
-    mod = _load("_fm_hip", "hip")
+    var = os.environ.get("FM_HIP_VARIANT")  # A/B builds (build_native --variant)
+    mod = _load(f"_fm_hip_{var}", "hip") if var else _load("_fm_hip", "hip")
     return _SyncChecked(mod) if _SYNC else mod
 
 

@@ -132,3 +132,35 @@ def test_dense_mfma_backward_is_deterministic(monkeypatch):
         runs.append(_state(m))
     for x, y in zip(*runs):
         assert torch.equal(x, y)
+
+
+def test_local_lookahead_matches_plain_steps_bitwise():
+    """Eager lookahead (next batch's dedup on the side stream during this step) == plain steps."""
+    gen = CriteoSynth(20000, device="cuda", seed=15)
+    batches = [gen.batch(1024) for _ in range(4)]
+    a, b = _model(), _model()
+    for bt in batches:
+        a.train_step(bt)
+    for i, bt in enumerate(batches):
+        b.train_step(bt, batches[i + 1] if i + 1 < len(batches) else None)
+    torch.cuda.synchronize()
+    for x, y in zip(_state(a), _state(b)):
+        assert torch.equal(x, y)
+
+
+def test_lookahead_graph_ring_matches_eager_bitwise():
+    gen = CriteoSynth(20000, device="cuda", seed=16)
+    batches = [gen.batch(1024) for _ in range(4)]
+    a, b = _model(), _model()
+    order = [0, 1, 2, 3, 0, 1, 2]
+    for i in order:
+        a.train_step(batches[i])
+    bufs = b.lookahead_graph_buffers(batches[0], 4)
+    for dst, src in zip(bufs, batches):
+        for d, s in ((dst.labels, src.labels), (dst.offsets, src.offsets), (dst.ids, src.ids)):
+            d.copy_(s)
+    losses = [b.train_step(bufs[i], bufs[(i + 1) % 4]).mean_loss() for i in order]
+    torch.cuda.synchronize()
+    for x, y in zip(_state(a), _state(b)):
+        assert torch.equal(x, y)
+    assert all(l == l for l in losses)

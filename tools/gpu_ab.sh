@@ -1,6 +1,7 @@
 #!/bin/bash
-# A/B of step variants selected by environment variables (1 GPU, default bench config).
-# usage: tools/gpu_ab.sh <tag> "ENV=.. ENV=.." "ENV=.." ...
+# A/B of step variants on one box (1 GPU, default bench config unless args given).
+# usage: tools/gpu_ab.sh <tag> "ENV=.. ENV=..|bench args" "ENV=..|bench args" ...
+# (the part before '|' is the environment, after it extra bench.py arguments)
 set -o pipefail
 TAG=${1:-ab}; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -11,6 +12,9 @@ cd $R
 i=0
 for V in "$@"; do
   i=$((i+1))
-  env $V timeout -k 10 200 python bench.py --steps 40 --warmup 5 > $OUT/v$i.json 2> $OUT/v$i.err || { echo "variant $V failed"; tail -20 $OUT/v$i.err; exit 1; }
+  ENVS=${V%%|*}
+  ARGS=""
+  [[ "$V" == *"|"* ]] && ARGS=${V#*|}
+  env FM_AB_RUN=$i $ENVS timeout -k 10 200 python bench.py --steps 40 --warmup 5 $ARGS > $OUT/v$i.json 2> $OUT/v$i.err || { echo "variant $V failed"; tail -20 $OUT/v$i.err; exit 1; }
   echo "[$V] $(grep ms/step $OUT/v$i.err)"
 done
