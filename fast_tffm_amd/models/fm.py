@@ -363,6 +363,12 @@ class FactorizationMachine:
         self.global_step += 1
         return out
 
+    def _dense_stream(self):
+        """Stream of the MFMA dense-row backward (forked from / joined into the compute stream)."""
+        if getattr(self, "_dense_st", None) is None:
+            self._dense_st = torch.cuda.Stream(self.device)
+        return self._dense_st
+
     def _side_stream(self):
         if self._side is None:
             self._side = torch.cuda.Stream(self.device)
@@ -403,7 +409,7 @@ class FactorizationMachine:
         with roctx_range("bwd+update"):
             K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
                           reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, dense_part=ws.dense_part,
-                          dense_stream=self._side_stream() if gpu else None)
+                          dense_stream=self._dense_stream() if gpu else None)
         return StepOut(fo.loss_sum, b.B)
 
     # ------------------------------------------------------------------
@@ -455,7 +461,7 @@ class FactorizationMachine:
         with roctx_range("bwd+update"):
             K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
                           reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, dense_part=ws.dense_part,
-                          dense_stream=self._side_stream())
+                          dense_stream=self._dense_stream())
         return StepOut(fo.loss_sum, b.B)
 
     def _local_lookahead_step(self, b: Batch, next_batch: Batch | None) -> StepOut:

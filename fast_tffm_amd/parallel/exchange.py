@@ -256,7 +256,7 @@ class ShardExchange(_Base):
         with roctx_range("bwd"):
             K.fm_backward(dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT, src_v=src_v, src_w=src_w, grad_out=grad,
                           reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, dense_part=ws.dense_part,
-                          dense_stream=m._side_stream() if self.dev.type == "cuda" else None)
+                          dense_stream=m._dense_stream() if self.dev.type == "cuda" else None)
         grad_recv = torch.empty((pl.R, self.gs), dtype=torch.float32, device=self.dev)
         with roctx_range("a2a_grads"):
             _a2a(grad_recv, grad, pl.rc, pl.sc, self.group)
