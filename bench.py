@@ -50,6 +50,10 @@ PRESETS = {
     "k128_fp8_ftrl": dict(k=128, dtype="fp8", opt="ftrl", mode="auto", slots_per_gpu=62_500_000),
     # same with a bf16 table (reference point for the fp8 one)
     "k128_ftrl": dict(k=128, dtype="bf16", opt="ftrl", mode="auto", slots_per_gpu=62_500_000),
+    # BASELINE config 1: 2nd-order FM k=4 on a tiny a1a-shaped libsvm set, CPU, world_size 1
+    # (plumbing: text -> C++ parser -> OpenMP CPU kernels); data goes through the real reader
+    "a1a_cpu": dict(k=4, dtype="fp32", opt="adagrad", mode="local", slots_per_gpu=None, vocab=124,
+                    device="cpu", data="a1a", batch=1605),
 }
 
 
@@ -58,7 +62,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=131072, help="examples per GPU per step")
+    ap.add_argument("--batch", type=int, default=None, help="examples per GPU per step (default 131072)")
     ap.add_argument("--preset", default="k64", choices=sorted(PRESETS))
     ap.add_argument("--slots-per-gpu", type=int, default=None, help="override hashed slots per GPU")
     ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled")
@@ -71,6 +75,7 @@ def main() -> int:
     a = ap.parse_args()
 
     p = dict(PRESETS[a.preset])
+    a.batch = a.batch or p.get("batch", 131072)
     mode = a.mode or p["mode"]
     if mode not in ("auto", "local") or int(os.environ.get("WORLD_SIZE", "1")) > 1:
         # HIP maps streams round-robin onto GPU_MAX_HW_QUEUES hardware queues (4 by default):
@@ -79,7 +84,7 @@ def main() -> int:
         # step is 3% faster with 4.  Must be set before HIP initialises (first device call).
         if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
             os.environ["GPU_MAX_HW_QUEUES"] = "8"
-    ctx = fmdist.init_distributed(force_pg=mode not in ("auto", "local"))
+    ctx = fmdist.init_distributed(force_pg=mode not in ("auto", "local"), device=p.get("device"))
     W, rank = ctx.world, ctx.rank
     if W != a.gpus and rank == 0:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={W}; using {W}", file=sys.stderr)
@@ -101,8 +106,21 @@ def main() -> int:
         print(f"[bench] {model.table.memory_report()} (init {time.time() - t0:.1f}s), mode={model.mode}, "
               f"vocab={vocab}, B/gpu={a.batch}", file=sys.stderr)
 
-    gen = CriteoSynth(vocab, alpha=a.alpha, seed=1000 + rank, device=dev)
-    pool = [gen.batch(a.batch) for _ in range(max(1, a.pool))]
+    if p.get("data") == "a1a":  # libsvm text through the C++ parser (tools/make_sample_data.py shape)
+        import tempfile
+
+        from fast_tffm_amd.data.reader import load_file_batch
+        from fast_tffm_amd.data.synthetic import write_libsvm
+
+        pool = []
+        with tempfile.TemporaryDirectory() as td:
+            for i in range(max(1, a.pool)):
+                path = os.path.join(td, f"a1a_{i}")
+                write_libsvm(path, a.batch, shape="a1a", seed=1000 * rank + i, weights_path=None)
+                pool.append(load_file_batch([path], None, vocab, False, 4).to(dev))
+    else:
+        gen = CriteoSynth(vocab, alpha=a.alpha, seed=1000 + rank, device=dev)
+        pool = [gen.batch(a.batch) for _ in range(max(1, a.pool))]
     if dev.type == "cuda":
         torch.cuda.synchronize()
     graphed = False
@@ -164,7 +182,8 @@ def main() -> int:
         par = ("rowshard%d" % W) if model.mode == "shard" else (model.mode + str(W) if W > 1 else "single")
         print(f"[bench] loss={loss:.5f} ms/step={ms:.3f} ex/s={value:.4g}", file=sys.stderr)
         print(json.dumps({
-            "metric": "examples/sec (whole node), Criteo-shaped FM k=%d" % p["k"],
+            "metric": ("examples/sec (whole node), Criteo-shaped FM k=%d" % p["k"]) if p.get("data") != "a1a"
+            else "examples/sec, a1a-shaped FM k=%d on CPU (plumbing config)" % p["k"],
             "value": value,
             "unit": "examples/s",
             "n_gpus": W,
@@ -176,7 +195,8 @@ def main() -> int:
             "vs_baseline": None,
             # compute dtype: fp32 arithmetic throughout; the table is stored as p["dtype"]
             "dtype": p["dtype"],
-            "data": "synthetic Criteo-shaped (39 fields, Zipf a=%.2f), random-init weights" % a.alpha,
+            "data": ("synthetic Criteo-shaped (39 fields, Zipf a=%.2f), random-init weights" % a.alpha)
+            if p.get("data") != "a1a" else "synthetic a1a-shaped libsvm text (123 features), parsed",
             "config": {
                 "model": "FM k=%d, %s table + %s, hashed vocab %d (%d/GPU)" % (
                     p["k"], p["dtype"], p["opt"], vocab, vocab // W if model.mode == "shard" else vocab),

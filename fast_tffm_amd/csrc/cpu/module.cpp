@@ -65,7 +65,60 @@ fm::cpu::OptParams opt_params(int type, float lr, float l1, float l2, float beta
 
 }  // namespace
 
+namespace {
+
+// CRC-32C (Castagnoli), hardware crc32 instructions (SSE4.2) with a portable
+// table fallback: checksums of TF tensor bundles and TensorBoard event records.
+uint32_t crc32c_table(uint32_t crc, const uint8_t* p, size_t n) {
+  static uint32_t table[256];
+  static bool init = false;
+  if (!init) {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0x82F63B78u : c >> 1;
+      table[i] = c;
+    }
+    init = true;
+  }
+  for (size_t i = 0; i < n; ++i) crc = table[(crc ^ p[i]) & 0xff] ^ (crc >> 8);
+  return crc;
+}
+
+#if defined(__x86_64__)
+__attribute__((target("sse4.2"))) uint32_t crc32c_hw(uint32_t crc, const uint8_t* p, size_t n) {
+  uint64_t c = crc;
+  while (n >= 8) {
+    uint64_t v;
+    std::memcpy(&v, p, 8);
+    c = __builtin_ia32_crc32di(c, v);
+    p += 8;
+    n -= 8;
+  }
+  uint32_t c32 = (uint32_t)c;
+  while (n--) c32 = __builtin_ia32_crc32qi(c32, *p++);
+  return c32;
+}
+#endif
+
+uint32_t crc32c(const uint8_t* p, size_t n) {
+#if defined(__x86_64__)
+  if (__builtin_cpu_supports("sse4.2")) return ~crc32c_hw(~0u, p, n);
+#endif
+  return ~crc32c_table(~0u, p, n);
+}
+
+}  // namespace
+
 PYBIND11_MODULE(_fm_cpu, m) {
+  m.def(
+      "crc32c",
+      [](py::buffer b) {
+        py::buffer_info info = b.request();
+        const size_t n = (size_t)info.size * (size_t)info.itemsize;
+        py::gil_scoped_release nogil;
+        return crc32c(static_cast<const uint8_t*>(info.ptr), n);
+      },
+      py::arg("data"), "CRC-32C of a contiguous buffer");
   m.doc() = "host native components of fast_tffm_amd (parser, hash64, CPU step kernels)";
   py::register_exception<fm::ParseError>(m, "ParseError", PyExc_ValueError);
 

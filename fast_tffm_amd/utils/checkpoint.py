@@ -270,3 +270,56 @@ def import_reference_blocks(model, in_dir: str, block_num: int) -> None:
         ref = torch.from_numpy(np.ascontiguousarray(arr[rows]))
         a = torch.from_numpy(np.ascontiguousarray(acc[rows])) if acc is not None else None
         table.load_reference_rows(local[m].to(table.device), ref, a)
+
+
+# ---------------------------------------------------------------------------
+# TensorFlow checkpoint (tensor bundle) in the reference's variable layout
+# ---------------------------------------------------------------------------
+def export_tf_checkpoint(ckpt_dir: str, out_dir: str, block_num: int, *, with_slots: bool = True) -> str:
+    """Write ``out_dir/model.ckpt-<step>.{index,data-00000-of-00001}`` + ``checkpoint`` with the
+    reference's variables: ``vocab_block_{i}`` [V//N+1, K+1] (col 0 = w), ``vocab_block_{i}/Adagrad``
+    and ``global_step`` (what tf.train.Saver wrote for the reference, fm_model.py:269-284, :365)."""
+    from .tf_bundle import write_bundle, write_checkpoint_state
+
+    meta = read_meta(ckpt_dir)
+    tmp = os.path.join(out_dir, ".blocks")
+    export_reference_blocks(ckpt_dir, tmp, block_num, with_slots=with_slots)
+    tensors = {"global_step": np.array(meta["global_step"], dtype=np.int64)}
+    for i in range(block_num):
+        tensors[f"vocab_block_{i}"] = np.load(os.path.join(tmp, f"vocab_block_{i}.npy"), mmap_mode="r")
+        if with_slots:
+            tensors[f"vocab_block_{i}/Adagrad"] = np.load(os.path.join(tmp, f"vocab_block_{i}_Adagrad.npy"),
+                                                          mmap_mode="r")
+    name = f"model.ckpt-{meta['global_step']}"
+    write_bundle(os.path.join(out_dir, name), tensors)
+    write_checkpoint_state(out_dir, name)
+    shutil.rmtree(tmp, ignore_errors=True)
+    return os.path.join(out_dir, name)
+
+
+def import_tf_checkpoint(model, prefix: str, block_num: int | None = None) -> int:
+    """Load a reference-layout TF checkpoint (``prefix`` = .../model.ckpt-N) into the model's
+    local table shard; returns its global_step."""
+    from .tf_bundle import read_bundle
+
+    t = read_bundle(prefix)
+    if block_num is None:
+        block_num = sum(1 for k in t if k.startswith("vocab_block_") and "/" not in k)
+    table = model.table
+    gids = table.global_ids().cpu()
+    ok = gids < table.vocab_size
+    gids = gids[ok]
+    local = torch.nonzero(ok).flatten()
+    b, r = gids % block_num, torch.div(gids, block_num, rounding_mode="floor")
+    for i in range(block_num):
+        m = b == i
+        if not bool(m.any()):
+            continue
+        rows = r[m].numpy()
+        ref = torch.from_numpy(np.ascontiguousarray(t[f"vocab_block_{i}"][rows]))
+        acc = t.get(f"vocab_block_{i}/Adagrad")
+        a = torch.from_numpy(np.ascontiguousarray(acc[rows])) if acc is not None else None
+        table.load_reference_rows(local[m].to(table.device), ref, a)
+    step = int(t.get("global_step", np.array(0)))
+    model.global_step = step
+    return step

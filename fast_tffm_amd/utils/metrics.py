@@ -30,16 +30,30 @@ for _i in range(256):
     _CRC_TABLE.append(_c)
 
 
-def crc32c(data: bytes) -> int:
+def _crc32c_py(data: bytes) -> int:
     crc = 0xFFFFFFFF
     for b in data:
         crc = _CRC_TABLE[(crc ^ b) & 0xFF] ^ (crc >> 8)
     return crc ^ 0xFFFFFFFF
 
 
-def _masked_crc(data: bytes) -> int:
+def crc32c(data) -> int:
+    """CRC-32C of bytes / a contiguous buffer (native SSE4.2 path, Python fallback)."""
+    try:
+        from ..ops import native
+
+        return int(native.cpu().crc32c(memoryview(data).cast("B")))
+    except Exception:  # noqa: BLE001  (extension unavailable)
+        return _crc32c_py(bytes(data))
+
+
+def masked_crc32c(data) -> int:
+    """TFRecord / LevelDB checksum masking: rotate right by 15, add 0xa282ead8."""
     c = crc32c(data)
     return (((c >> 15) | (c << 17)) + 0xA282EAD8) & 0xFFFFFFFF
+
+
+_masked_crc = masked_crc32c
 
 
 # ---------------------------------------------------------------------------
