@@ -68,6 +68,8 @@ def main() -> int:
     ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled")
     ap.add_argument("--alpha", type=float, default=1.1, help="Zipf exponent of field values")
     ap.add_argument("--mode", default=None, help="override step mode (local|shard|dp|dp_dense)")
+    ap.add_argument("--comm-dtype", default="auto", choices=["auto", "fp32", "bf16"],
+                    help="row-sharded wire rows (auto = table storage dtype; bf16 rounds fp32 rows for transport)")
     ap.add_argument("--profile-steps", type=int, default=0, help="also emit a torch.profiler trace")
     ap.add_argument("--graph", type=int, default=0,
                     help="local step: 0 = eager lookahead pipeline (next batch's dedup overlaps this step; "
@@ -97,7 +99,7 @@ def main() -> int:
     opt = K.OptConfig(p["opt"], lr=0.01 if p["opt"] == "adagrad" else 0.05, l1=0.001, l2=0.001, beta=1.0,
                       initial_accumulator=0.1)
     cfg = FMConfig(vocabulary_size=vocab, factor_num=p["k"], loss_type="logistic", batch_size=a.batch,
-                   init_value_range=0.01, seed=42, dtype=dtype, opt=opt, mode=mode)
+                   init_value_range=0.01, seed=42, dtype=dtype, opt=opt, mode=mode, comm_dtype=a.comm_dtype)
     t0 = time.time()
     model = FactorizationMachine(cfg, device=dev, dist=ctx if W > 1 or mode not in ("auto", "local") else None)
     if dev.type == "cuda":
@@ -203,6 +205,8 @@ def main() -> int:
                 "global_batch": a.batch * W,
                 "seq_len": 39,
                 "parallelism": par,
+                "wire": str(model._exchange.wire.dtype).replace("torch.", "")
+                if model.mode == "shard" else None,
             },
         }), flush=True)
     fmdist.shutdown()

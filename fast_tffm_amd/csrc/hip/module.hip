@@ -161,11 +161,25 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("Kp"), py::arg("dtype"), py::arg("out"), py::arg("o_stride"), py::arg("stream"));
 
   m.def(
+      "gather_wire",
+      [](int R, u64 req, u64 v, long long v_bytes_stride, u64 w, long long w_stride, int vbytes, int scaled,
+         int to_bf16, u64 out, long long rb, int vb, u64 stream) {
+        fm::GatherWireArgs a{};
+        a.R = R; a.req = P<const int>(req); a.v = P<const void>(v); a.v_bytes_stride = v_bytes_stride;
+        a.w = P<const float>(w); a.w_stride = w_stride; a.vbytes = vbytes; a.scaled = scaled; a.to_bf16 = to_bf16;
+        a.out = P<unsigned char>(out); a.rb = rb; a.vb = vb;
+        check(fm::launch_gather_wire(a, S(stream)), "gather_wire");
+      },
+      py::arg("R"), py::arg("req"), py::arg("v"), py::arg("v_bytes_stride"), py::arg("w"), py::arg("w_stride"),
+      py::arg("vbytes"), py::arg("scaled"), py::arg("to_bf16"), py::arg("out"), py::arg("rb"), py::arg("vb"),
+      py::arg("stream"));
+
+  m.def(
       "apply_rows",
       [](u64 num_unique, u64 seg_start, u64 uniq, u64 perm, u64 grad_in, long long g_stride, int Kp, u64 v,
          long long v_stride, u64 w, long long w_stride, u64 s0v, u64 s1v, long long s_stride, u64 s0w, u64 s1w,
          int opt_type, float lr, float l1, float l2, float beta, int dtype, long long max_unique, u64 stream) {
-        fm::ApplyArgs a;
+        fm::ApplyArgs a{};
         a.num_unique = P<const int>(num_unique); a.seg_start = P<const int>(seg_start);
         a.uniq = P<const int>(uniq); a.perm = P<const int>(perm); a.grad_in = P<const float>(grad_in);
         a.g_stride = g_stride; a.Kp = Kp; a.v = P<void>(v); a.v_stride = v_stride; a.w = P<float>(w);
@@ -178,6 +192,24 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("s0v"), py::arg("s1v"), py::arg("s_stride"), py::arg("s0w"), py::arg("s1w"), py::arg("opt_type"),
       py::arg("lr"), py::arg("l1"), py::arg("l2"), py::arg("beta"), py::arg("dtype"), py::arg("max_unique"),
       py::arg("stream"));
+
+  m.def(
+      "apply_runs",
+      [](int R, int W, u64 run_off, u64 req, u64 match, u64 grad_in, long long g_stride, int Kp, u64 v,
+         long long v_stride, u64 w, long long w_stride, u64 s0v, u64 s1v, long long s_stride, u64 s0w, u64 s1w,
+         int opt_type, float lr, float l1, float l2, float beta, int dtype, u64 stream) {
+        fm::ApplyArgs a{};
+        a.R = R; a.W = W; a.run_off = P<const int>(run_off); a.req = P<const int>(req);
+        a.match = P<const int>(match); a.grad_in = P<const float>(grad_in);
+        a.g_stride = g_stride; a.Kp = Kp; a.v = P<void>(v); a.v_stride = v_stride; a.w = P<float>(w);
+        a.w_stride = w_stride; a.s0v = P<float>(s0v); a.s1v = P<float>(s1v); a.s_stride = s_stride;
+        a.s0w = P<float>(s0w); a.s1w = P<float>(s1w); a.opt = opt_params(opt_type, lr, l1, l2, beta);
+        check(fm::launch_apply_runs(a, P<int>(match), dtype, S(stream)), "apply_runs");
+      },
+      py::arg("R"), py::arg("W"), py::arg("run_off"), py::arg("req"), py::arg("match"), py::arg("grad_in"),
+      py::arg("g_stride"), py::arg("Kp"), py::arg("v"), py::arg("v_stride"), py::arg("w"), py::arg("w_stride"),
+      py::arg("s0v"), py::arg("s1v"), py::arg("s_stride"), py::arg("s0w"), py::arg("s1w"), py::arg("opt_type"),
+      py::arg("lr"), py::arg("l1"), py::arg("l2"), py::arg("beta"), py::arg("dtype"), py::arg("stream"));
 
   m.def(
       "init_rows",

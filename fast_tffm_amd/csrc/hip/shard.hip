@@ -3,6 +3,7 @@
 // the gradient rows every peer returned for one table row before applying the
 // optimizer once (replaces the PS-side embedding gather and SparseApplyAdagrad
 // that the reference gets from TF's gRPC runtime, tffm/fm_model.py:291, :341-348).
+#include <algorithm>
 #include "fm_common.h"
 
 namespace fm {
@@ -52,6 +53,86 @@ __global__ __launch_bounds__(kBlock) void gather_rows_kernel(GatherArgs a) {
   }
 }
 
+// Wire-format gather (row-sharded exchange): the row leaves the owner in the
+// format the requester's forward/backward read directly, so bf16 / fp8 tables
+// cross xGMI at their storage size (exact: the stored bits are copied) and an
+// fp32 table can optionally be sent as bf16 (comm_dtype = bf16, RNE).
+// Wire row (RB bytes, RB % 16 == 0): [v: Kp elements of the wire dtype, padded
+// to vb bytes (vb % 16 == 0)] [w fp32] [scale fp32 (fp8) / 0] [0] [0].
+struct GatherWireArgs {
+  int R;
+  const int* req;           // [R] local table rows requested by peers
+  const void* v; long long v_bytes_stride;   // table rows (bytes between rows)
+  const float* w; long long w_stride;        // fp8 tables: scale at w[row * w_stride + 1]
+  int vbytes;               // bytes of a stored row's Kp elements
+  int scaled;               // 1: fp8 table (copy the per-row scale)
+  int to_bf16;              // 1: fp32 table -> bf16 wire (Kp % 8 == 0)
+  unsigned char* out; long long rb;          // [R, rb] wire rows
+  int vb;                   // byte offset of w inside a wire row
+};
+
+// One lane group per row; lane t moves 16 bytes of the wire row's v section
+// (UNIT = 16) or 4 bytes (UNIT = 4, rows whose v section is not 16-byte sized).
+template <int LPR, int UNIT>
+__global__ __launch_bounds__(kBlock) void gather_wire_kernel(GatherWireArgs a) {
+  constexpr int G = kWave / LPR;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPR, t = lane % LPR;
+  const int out_bytes = a.to_bf16 ? a.vbytes / 2 : a.vbytes;
+  const int nunits = out_bytes / UNIT;
+  const int ngroups = gridDim.x * kWavesPerBlock * G;
+  for (int p = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g; p < a.R; p += ngroups) {
+    const long long row = a.req[p];
+    const unsigned char* src = reinterpret_cast<const unsigned char*>(a.v) + row * a.v_bytes_stride;
+    unsigned char* dst = a.out + (long long)p * a.rb;
+    for (int u = t; u < nunits; u += LPR) {
+      if constexpr (UNIT == 16) {
+        if (a.to_bf16) {  // 8 fp32 -> 8 bf16
+          const float4 f0 = *reinterpret_cast<const float4*>(src + u * 32);
+          const float4 f1 = *reinterpret_cast<const float4*>(src + u * 32 + 16);
+          uint4 o;
+          o.x = f32_to_bf16_bits(f0.x) | (f32_to_bf16_bits(f0.y) << 16);
+          o.y = f32_to_bf16_bits(f0.z) | (f32_to_bf16_bits(f0.w) << 16);
+          o.z = f32_to_bf16_bits(f1.x) | (f32_to_bf16_bits(f1.y) << 16);
+          o.w = f32_to_bf16_bits(f1.z) | (f32_to_bf16_bits(f1.w) << 16);
+          *reinterpret_cast<uint4*>(dst + u * 16) = o;
+        } else {
+          *reinterpret_cast<uint4*>(dst + u * 16) = *reinterpret_cast<const uint4*>(src + u * 16);
+        }
+      } else {
+        *reinterpret_cast<uint32_t*>(dst + u * 4) = *reinterpret_cast<const uint32_t*>(src + u * 4);
+      }
+    }
+    if (t == 0) {
+      float* tail = reinterpret_cast<float*>(dst + a.vb);
+      tail[0] = a.w[row * a.w_stride];
+      tail[1] = a.scaled ? a.w[row * a.w_stride + 1] : 0.f;
+      tail[2] = 0.f;
+      tail[3] = 0.f;
+    }
+  }
+}
+
+int launch_gather_wire(const GatherWireArgs& a, hipStream_t st) {
+  if (a.R <= 0) return 0;
+  const int out_bytes = a.to_bf16 ? a.vbytes / 2 : a.vbytes;
+  const bool u16 = out_bytes % 16 == 0;
+  if (a.to_bf16 && !u16) return -7;
+  const int lpr = std::min(64, next_pow2(std::max(1, u16 ? out_bytes / 16 : out_bytes / 4)));
+  const int grid = fill_grid(a.R, kWavesPerBlock * (kWave / lpr));
+#define FM_GW(L)                                                                                        \
+  case L:                                                                                               \
+    if (u16) hipLaunchKernelGGL((gather_wire_kernel<L, 16>), dim3(grid), dim3(kBlock), 0, st, a);      \
+    else hipLaunchKernelGGL((gather_wire_kernel<L, 4>), dim3(grid), dim3(kBlock), 0, st, a);           \
+    break;
+  switch (lpr) {
+    FM_GW(1) FM_GW(2) FM_GW(4) FM_GW(8) FM_GW(16) FM_GW(32) FM_GW(64)
+    default: return -1;
+  }
+#undef FM_GW
+  return (int)hipGetLastError();
+}
+
 struct ApplyArgs {
   const int* num_unique;    // device scalar: number of distinct rows received
   const int* seg_start;     // [U+1] into perm
@@ -64,36 +145,35 @@ struct ApplyArgs {
   float* s0v; float* s1v; long long s_stride;
   float* s0w; float* s1w;
   OptParams opt;
+  // run-merge form (apply_runs): R received rows forming W ascending runs (one per
+  // source rank) and the [R, W] cross-run match matrix of owner_match_kernel
+  int R, W;
+  const int* run_off;       // [W+1]
+  const int* req;           // [R] local table row of each received gradient row
+  const int* match;         // [R, W]: index of the same row in run q, or -1 (null when W == 1)
 };
 
-// Owner-side: sum the gradient rows every peer sent for one table row (in
-// source-rank order: the sort is stable and the receive buffer is rank-major)
-// and apply the optimizer once.
+// One table row's parameters + optimizer state in registers (this lane's EPL
+// columns; lane t == 0 also holds w and its state).  load() is issued before the
+// gradient sum so that the row's loads overlap it.
 template <int LPR, typename TV>
-__global__ __launch_bounds__(kBlock) void apply_rows_kernel(ApplyArgs a) {
+struct RowUpdate {
   using F = Frag<TV>;
-  constexpr int EPL = F::N;
-  constexpr int G = kWave / LPR;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int g = lane / LPR, t = lane % LPR;
-  const int nv = a.Kp / EPL;
-  const bool tact = t < nv;
-  const int tE = tact ? t : nv - 1;
-  const int U = *a.num_unique;
-  const int ngroups = gridDim.x * kWavesPerBlock * G;
-  for (int u = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g; u < U; u += ngroups) {
-    // table row + optimizer state first: their loads overlap the gradient sum below
-    const long long row = a.uniq[u];
-    TV* vrow = reinterpret_cast<TV*>(a.v) + row * a.v_stride + tE * EPL;
-    float vv[EPL], st0[EPL], st1[EPL];
+  static constexpr int EPL = F::N;
+  float vv[EPL], st0[EPL], st1[EPL];
+  float pw, q0, q1;
+  TV* vrow; float* s0; float* s1;
+
+  __device__ inline void load(const ApplyArgs& a, long long row, int tE) {
+    vrow = reinterpret_cast<TV*>(a.v) + row * a.v_stride + tE * EPL;
     F::load(vrow, vv);
     if constexpr (F::kScaled) {
       const float s = row_scale<TV>(a.w, row, a.w_stride);
 #pragma unroll
       for (int k = 0; k < EPL; ++k) vv[k] *= s;
     }
-    float* s0 = a.s0v + row * a.s_stride + tE * EPL;
-    float* s1 = a.s1v ? a.s1v + row * a.s_stride + tE * EPL : nullptr;
+    s0 = a.s0v + row * a.s_stride + tE * EPL;
+    s1 = a.s1v ? a.s1v + row * a.s_stride + tE * EPL : nullptr;
 #pragma unroll
     for (int k = 0; k < EPL; k += 4) {
       const float4 q = *reinterpret_cast<const float4*>(s0 + k);
@@ -101,22 +181,13 @@ __global__ __launch_bounds__(kBlock) void apply_rows_kernel(ApplyArgs a) {
       const float4 z = s1 ? *reinterpret_cast<const float4*>(s1 + k) : make_float4(0.f, 0.f, 0.f, 0.f);
       st1[k] = z.x; st1[k + 1] = z.y; st1[k + 2] = z.z; st1[k + 3] = z.w;
     }
-    float* wp = a.w + row * a.w_stride;
-    float pw = *wp, q0 = a.s0w[row], q1 = a.s1w ? a.s1w[row] : 0.f;
-    float gr[EPL];
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) gr[k] = 0.f;
-    float gw = 0.f;
-    const int j1 = a.seg_start[u + 1];
-    for (int j = a.seg_start[u]; j < j1; ++j) {
-      const float* src = a.grad_in + (long long)a.perm[j] * a.g_stride;
-#pragma unroll
-      for (int k = 0; k < EPL; k += 4) {
-        const float4 f = *reinterpret_cast<const float4*>(src + tE * EPL + k);
-        gr[k] += f.x; gr[k + 1] += f.y; gr[k + 2] += f.z; gr[k + 3] += f.w;
-      }
-      gw += src[a.Kp];
-    }
+    pw = a.w[row * a.w_stride];
+    q0 = a.s0w[row];
+    q1 = a.s1w ? a.s1w[row] : 0.f;
+  }
+
+  __device__ inline void step_store(const ApplyArgs& a, const float (&gr)[EPL], float gw, long long row, int t,
+                                    bool tact) {
 #pragma unroll
     for (int k = 0; k < EPL; ++k) opt_step(a.opt, gr[k], vv[k], st0[k], st1[k]);
     store_row<LPR, TV>(vrow, vv, a.w, row, a.w_stride, t, tact);
@@ -129,10 +200,110 @@ __global__ __launch_bounds__(kBlock) void apply_rows_kernel(ApplyArgs a) {
     }
     if (t == 0) {
       opt_step(a.opt, gw, pw, q0, q1);
-      *wp = pw;
+      a.w[row * a.w_stride] = pw;
       a.s0w[row] = q0;
       if (a.s1w) a.s1w[row] = q1;
     }
+  }
+};
+
+template <int EPL>
+__device__ inline void add_grad_row(const float* src, int tE, int Kp, float (&gr)[EPL], float& gw) {
+#pragma unroll
+  for (int k = 0; k < EPL; k += 4) {
+    const float4 f = *reinterpret_cast<const float4*>(src + tE * EPL + k);
+    gr[k] += f.x; gr[k + 1] += f.y; gr[k + 2] += f.z; gr[k + 3] += f.w;
+  }
+  gw += src[Kp];
+}
+
+// Owner-side: sum the gradient rows every peer sent for one table row (in
+// source-rank order: the sort is stable and the receive buffer is rank-major)
+// and apply the optimizer once.
+template <int LPR, typename TV>
+__global__ __launch_bounds__(kBlock) void apply_rows_kernel(ApplyArgs a) {
+  constexpr int EPL = Frag<TV>::N;
+  constexpr int G = kWave / LPR;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPR, t = lane % LPR;
+  const int nv = a.Kp / EPL;
+  const bool tact = t < nv;
+  const int tE = tact ? t : nv - 1;
+  const int U = *a.num_unique;
+  const int ngroups = gridDim.x * kWavesPerBlock * G;
+  for (int u = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g; u < U; u += ngroups) {
+    const long long row = a.uniq[u];
+    RowUpdate<LPR, TV> ru;
+    ru.load(a, row, tE);
+    float gr[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) gr[k] = 0.f;
+    float gw = 0.f;
+    const int j1 = a.seg_start[u + 1];
+    for (int j = a.seg_start[u]; j < j1; ++j)
+      add_grad_row<EPL>(a.grad_in + (long long)a.perm[j] * a.g_stride, tE, a.Kp, gr, gw);
+    ru.step_store(a, gr, gw, row, t, tact);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Run-merge grouping (replaces a sort of the received requests).  The owner
+// receives W runs, one per source rank, each holding that rank's unique rows
+// in ascending order, so a row appears at most once per run.  One thread per
+// (received row i, run q) binary-searches row req[i] in run q; the apply
+// kernel then treats the first run holding a row as its leader and sums the
+// row's gradients over the runs in rank order (deterministic, no atomics).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void owner_match_kernel(int R, int W, const int* run_off, const int* req,
+                                                             int* match) {
+  const long long n = (long long)R * W;
+  for (long long p = blockIdx.x * (long long)kBlock + threadIdx.x; p < n; p += (long long)gridDim.x * kBlock) {
+    const int i = (int)(p / W), q = (int)(p % W);
+    const int key = req[i];
+    int lo = run_off[q];
+    const int end = run_off[q + 1];
+    int hi = end;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (req[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    match[p] = (lo < end && req[lo] == key) ? lo : -1;
+  }
+}
+
+template <int LPR, typename TV>
+__global__ __launch_bounds__(kBlock) void apply_runs_kernel(ApplyArgs a) {
+  constexpr int EPL = Frag<TV>::N;
+  constexpr int G = kWave / LPR;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPR, t = lane % LPR;
+  const int nv = a.Kp / EPL;
+  const bool tact = t < nv;
+  const int tE = tact ? t : nv - 1;
+  const int ngroups = gridDim.x * kWavesPerBlock * G;
+  for (int i = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g; i < a.R; i += ngroups) {
+    int r = 0;
+    const int* mrow = nullptr;
+    if (a.W > 1) {
+      while (a.run_off[r + 1] <= i) ++r;
+      mrow = a.match + (long long)i * a.W;
+      bool led = true;
+      for (int q = 0; q < r; ++q) led &= mrow[q] < 0;
+      if (!led) continue;  // an earlier run holds this row: its leader applies it
+    }
+    const long long row = a.req[i];
+    RowUpdate<LPR, TV> ru;
+    ru.load(a, row, tE);
+    float gr[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) gr[k] = 0.f;
+    float gw = 0.f;
+    add_grad_row<EPL>(a.grad_in + (long long)i * a.g_stride, tE, a.Kp, gr, gw);
+    for (int q = r + 1; q < a.W; ++q) {
+      const int j = mrow[q];
+      if (j >= 0) add_grad_row<EPL>(a.grad_in + (long long)j * a.g_stride, tE, a.Kp, gr, gw);
+    }
+    ru.step_store(a, gr, gw, row, t, tact);
   }
 }
 
@@ -141,6 +312,19 @@ int launch_gather_rows(const GatherArgs& a, int dtype, hipStream_t st) {
   const int lpr = lanes_per_row(a.Kp, dtype);
   const int grid = fill_grid(a.R, kWavesPerBlock * (kWave / lpr));
   FM_DISPATCH(dtype, lpr, gather_rows_kernel, grid, st, a);
+  return (int)hipGetLastError();
+}
+
+int launch_apply_runs(const ApplyArgs& a, int* match, int dtype, hipStream_t st) {
+  if (a.R <= 0) return 0;
+  if (a.W > 1) {
+    const long long n = (long long)a.R * a.W;
+    hipLaunchKernelGGL(owner_match_kernel, dim3(fill_grid(n, kBlock, 16384)), dim3(kBlock), 0, st, a.R, a.W,
+                       a.run_off, a.req, match);
+  }
+  const int lpr = lanes_per_row(a.Kp, dtype);
+  const int grid = fill_grid(a.R, kWavesPerBlock * (kWave / lpr));
+  FM_DISPATCH(dtype, lpr, apply_runs_kernel, grid, st, a);
   return (int)hipGetLastError();
 }
 

@@ -48,6 +48,7 @@ class FMConfig:
     opt: K.OptConfig = field(default_factory=K.OptConfig)
     mode: str = "auto"                # auto | local | shard | dp | dp_dense
     grad_reduce: str = "sum"          # sum | mean (multi-rank)
+    comm_dtype: str = "auto"          # row-sharded wire rows: auto (= storage dtype) | fp32 | bf16
     dedup_chunk: int = 32             # CH of the segmented backward
     threads: int = 0                  # CPU kernels (0 = OpenMP default)
     global_bias: bool = False         # learned global bias b0 (extension; the reference has none)

@@ -465,8 +465,7 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
     else:
         _check(src_v is not None and src_w is not None and grad_out is not None, "EMIT mode needs src + grad_out")
         v, w = src_v, src_w
-        dt = 0
-        _check(v.dtype == torch.float32, "EMIT source rows must be fp32")
+        dt = dtype_code(v.dtype)  # gathered wire rows: fp32, bf16 or fp8 (+ scale at w + 1)
         s0v = s1v = s0w = s1w = None
         s_stride = 0
         _check(grad_out.dtype == torch.float32 and grad_out.stride(1) == 1, "grad_out: fp32 rows")
@@ -582,3 +581,108 @@ def apply_rows(dd: DedupOut, grad_in: torch.Tensor, table: TableState, opt: OptC
                                 s1v=_p(table.s1v), s_stride=s_stride, s0w=_p(table.s0w), s1w=_p(table.s1w),
                                 opt_type=opt.code, lr=float(opt.lr), l1=float(opt.l1), l2=float(opt.l2),
                                 beta=float(opt.beta), dtype=dt, threads=threads)
+
+
+def apply_runs(req: torch.Tensor, run_off: torch.Tensor, splits: list[int], grad_in: torch.Tensor,
+               table: TableState, opt: OptConfig, Kp: int, match: torch.Tensor | None = None,
+               threads: int = 0, ws: DedupWorkspace | None = None) -> None:
+    """Owner side of a sharded update over the received requests as W ascending runs.
+
+    ``req`` [R] holds the local rows requested by each source rank, rank-major
+    (``splits[q]`` rows from rank q, ascending and distinct within a run);
+    ``grad_in`` [R, >= Kp+1] the matching gradient rows.  Every distinct row gets
+    the sum of its gradient rows in source-rank order and one optimizer step.
+    On the GPU the grouping is a cross-run binary-search match (``run_off`` =
+    device int32 [W+1] prefix of ``splits``, ``match`` int32 scratch of R*W when
+    W > 1) instead of a sort; on the CPU a stable sort of ``req`` (``ws``).
+    """
+    R, W = int(sum(splits)), len(splits)
+    _chk_vec(req, torch.int32, R, "req", req.device)
+    _check(grad_in.dtype == torch.float32 and grad_in.stride(1) == 1 and grad_in.shape[0] >= R, "grad_in: fp32 rows")
+    if R == 0:
+        return
+    if not _is_gpu(grad_in):
+        dd = dedup(req[:R], ws=ws, key_bits=32, want_perm=True)
+        apply_rows(dd, grad_in, table, opt, Kp, threads=threads)
+        return
+    v_stride = _chk_rows(table.v, Kp, "v")
+    _range_check(req[:R], table.v.shape[0], "req")
+    _chk_vec(run_off, torch.int32, W + 1, "run_off", req.device)
+    if W > 1:
+        _chk_vec(match, torch.int32, R * W, "match", req.device)
+    dt = dtype_code(table.v.dtype)
+    s_stride = table.s0v.stride(0) if table.s0v is not None else 0
+    native.hip().apply_runs(R=R, W=W, run_off=_p(run_off), req=_p(req), match=_p(match) if W > 1 else 0,
+                            grad_in=_p(grad_in), g_stride=grad_in.stride(0), Kp=Kp, v=_p(table.v), v_stride=v_stride,
+                            w=_p(table.w), w_stride=table.w.stride(0), s0v=_p(table.s0v), s1v=_p(table.s1v),
+                            s_stride=s_stride, s0w=_p(table.s0w), s1w=_p(table.s1w), opt_type=opt.code,
+                            lr=float(opt.lr), l1=float(opt.l1), l2=float(opt.l2), beta=float(opt.beta), dtype=dt,
+                            stream=_stream(grad_in))
+
+
+@dataclass
+class WireFormat:
+    """Row layout of the row-sharded exchange (owner gather -> all-to-all -> fwd/bwd).
+
+    A wire row is ``rb`` bytes: the Kp factor values in ``dtype`` (padded to
+    ``vb`` bytes), then ``[w, scale, 0, 0]`` fp32 (scale only for fp8).  bf16 /
+    fp8 tables travel at their storage size (the stored bits); an fp32 table
+    travels as fp32 (``[v | w | pad]``, the same bytes as a [Kp+4] fp32 row) or,
+    with ``comm_dtype = bf16``, as bf16 (rounded to nearest even).
+    """
+
+    dtype: torch.dtype
+    Kp: int
+    vb: int
+    rb: int
+    table_dtype: torch.dtype
+
+    @staticmethod
+    def make(table_dtype: torch.dtype, Kp: int, comm_dtype: str = "auto") -> "WireFormat":
+        dt = table_dtype
+        if comm_dtype == "bf16" and table_dtype == torch.float32 and Kp % 8 == 0:
+            dt = torch.bfloat16
+        elif comm_dtype not in ("auto", "bf16", "fp32", "storage"):
+            raise ValueError(f"comm_dtype must be auto|storage|fp32|bf16, got {comm_dtype}")
+        if comm_dtype == "fp32":
+            dt = torch.float32
+        esz = torch.tensor([], dtype=dt).element_size()
+        vb = (Kp * esz + 15) // 16 * 16
+        return WireFormat(dt, Kp, vb, vb + 16, table_dtype)
+
+    @property
+    def fp32(self) -> bool:
+        return self.dtype == torch.float32
+
+    def empty(self, n: int, device) -> torch.Tensor:
+        if self.fp32:
+            return torch.empty((n, self.rb // 4), dtype=torch.float32, device=device)
+        return torch.empty((n, self.rb), dtype=torch.uint8, device=device)
+
+    def views(self, buf: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+        """(v [n, Kp] in the wire dtype, w [n] fp32 strided view; fp8 scale at w + 1) of a wire buffer."""
+        if self.fp32:
+            return buf[:, : self.Kp], buf[:, self.Kp]
+        return buf.view(self.dtype)[:, : self.Kp], buf.view(torch.float32)[:, self.vb // 4]
+
+
+def gather_wire(req: torch.Tensor, table: TableState, fmt: WireFormat, out: torch.Tensor,
+                threads: int = 0) -> torch.Tensor:
+    """Owner side of a sharded lookup: wire rows of table rows ``req`` into ``out`` (``fmt.empty``)."""
+    if fmt.fp32 and table.v.dtype == torch.float32:
+        return gather_rows(req, table, fmt.Kp, out, threads=threads)
+    _check(_is_gpu(req), "non-fp32 wire formats are a GPU path")
+    R = req.numel()
+    _chk_vec(req, torch.int32, R, "req", req.device)
+    _check(out.dtype == torch.uint8 and out.is_contiguous() and out.shape[0] >= R and out.shape[1] == fmt.rb,
+           "out: [R, rb] uint8 wire buffer")
+    v = table.v
+    _chk_rows(v, fmt.Kp, "v")
+    _range_check(req, v.shape[0], "req")
+    to_bf16 = v.dtype == torch.float32 and fmt.dtype == torch.bfloat16
+    _check(to_bf16 or v.dtype == fmt.dtype, f"wire dtype {fmt.dtype} cannot carry a {v.dtype} table")
+    native.hip().gather_wire(R=R, req=_p(req), v=_p(v), v_bytes_stride=v.stride(0) * v.element_size(),
+                             w=_p(table.w), w_stride=table.w.stride(0), vbytes=fmt.Kp * v.element_size(),
+                             scaled=int(v.dtype == FP8), to_bf16=int(to_bf16), out=_p(out), rb=fmt.rb, vb=fmt.vb,
+                             stream=_stream(req))
+    return out

@@ -73,7 +73,7 @@ class _ShardPlan:
     """The table-independent half of one batch's sharded step: dedup, owner counts,
     id all-to-all and the owner-side grouping of the received requests."""
 
-    __slots__ = ("b", "slot", "dd", "sc", "rc", "U", "R", "req_recv", "dd2", "ready")
+    __slots__ = ("b", "slot", "dd", "sc", "rc", "U", "R", "req_recv", "run_off", "match", "ready")
 
 
 class _PlanSlot:
@@ -85,12 +85,38 @@ class _PlanSlot:
         self.dd2: K.DedupWorkspace | None = None
         self.keys: torch.Tensor | None = None
         self.done: torch.cuda.Event | None = None  # main-stream event: last step using this slot finished
+        self.run_off_h: torch.Tensor | None = None  # pinned [W+1] receive-run offsets (host staging)
+        self.run_off: torch.Tensor | None = None    # device copy
+        self.match: torch.Tensor | None = None      # [R, W] cross-run match scratch (apply_runs)
 
     def ensure(self, nnz: int, dev, CH: int) -> None:
         if self.dd is None or self.dd.cap < nnz:
             cap = max(nnz, 1, int(1.25 * (self.dd.cap if self.dd else 0)))
             self.dd = K.DedupWorkspace(cap, dev, CH)
             self.keys = torch.empty(cap, dtype=torch.int32, device=dev)
+
+    def runs(self, splits: list[int], dev) -> torch.Tensor:
+        """Device int32 prefix offsets of the receive runs, staged through pinned memory.
+
+        Called after this stream's host sync on the owner counts, so the previous
+        copy out of the pinned buffer (same stream, earlier) has completed."""
+        W = len(splits)
+        if self.run_off is None or self.run_off.numel() < W + 1:
+            self.run_off_h = torch.empty(W + 1, dtype=torch.int32, pin_memory=True)
+            self.run_off = torch.empty(W + 1, dtype=torch.int32, device=dev)
+        acc = 0
+        self.run_off_h[0] = 0
+        for q, c in enumerate(splits):
+            acc += c
+            self.run_off_h[q + 1] = acc
+        self.run_off[: W + 1].copy_(self.run_off_h[: W + 1], non_blocking=True)
+        return self.run_off
+
+    def match_buf(self, n: int, dev) -> torch.Tensor:
+        if self.match is None or self.match.numel() < n:
+            self.match = torch.empty(max(n, 1, int(1.25 * (self.match.numel() if self.match is not None else 0))),
+                                     dtype=torch.int32, device=dev)
+        return self.match
 
     def ensure2(self, n: int, dev) -> K.DedupWorkspace:
         if self.dd2 is None or self.dd2.cap < n:
@@ -115,6 +141,9 @@ class ShardExchange(_Base):
         self.slots = [_PlanSlot(), _PlanSlot()]
         # lookahead plans talk on their own communicator (own RCCL stream): the id
         # all-to-all of batch t+1 does not queue behind step t's row / grad all-to-alls
+        # wire format of the gathered rows: storage dtype (exact) or bf16 for fp32 tables on request
+        tdt = model.table.v.dtype
+        self.wire = K.WireFormat.make(tdt, self.Kp, model.cfg.comm_dtype if self.dev.type == "cuda" else "fp32")
         self.plan_group = (dist.new_group(ranks=list(range(self.W)), backend=dist.get_backend(self.group))
                            if self.W > 1 else self.group)
         self.cpu_group = self.ctx.cpu_group or self.group
@@ -183,11 +212,18 @@ class ShardExchange(_Base):
                 self._check_splits(pl, dd)
             dd.U_host = pl.U
             req_send = torch.remainder(dd.uniq[: pl.U], self.Rps)  # keys are owner * Rps + local row
-            pl.req_recv = torch.empty(pl.R, dtype=torch.int32, device=self.dev)
-            _a2a(pl.req_recv, req_send, pl.rc, pl.sc, self.plan_group)
+            if self.W == 1:
+                pl.req_recv = req_send      # a one-rank exchange is the identity: no copy
+            else:
+                pl.req_recv = torch.empty(pl.R, dtype=torch.int32, device=self.dev)
+                _a2a(pl.req_recv, req_send, pl.rc, pl.sc, self.plan_group)
             pl.dd = dd
-            pl.dd2 = (K.dedup(pl.req_recv, ws=slot.ensure2(pl.R, self.dev), key_bits=bits_for(self.Rps),
-                              want_perm=True) if train else None)
+            # owner-side grouping of the received requests (W ascending runs): device run
+            # offsets + match scratch for apply_runs; the CPU path sorts inside apply_runs
+            pl.run_off = pl.match = None
+            if train and gpu:
+                pl.run_off = slot.runs(pl.rc, self.dev)
+                pl.match = slot.match_buf(pl.R * self.W, self.dev) if self.W > 1 else None
             if gpu:
                 pl.ready = torch.cuda.Event()
                 pl.ready.record(st)
@@ -223,13 +259,15 @@ class ShardExchange(_Base):
             pl.req_recv.record_stream(main)  # allocated on the side stream, read on main
         return pl
 
-    def _gather(self, pl: _ShardPlan) -> torch.Tensor:
-        """Owner gather of the requested rows + a2a back: [U, Kp+4] rows in unique order."""
-        rows_send = torch.empty((pl.R, self.gs), dtype=torch.float32, device=self.dev)
-        K.gather_rows(pl.req_recv, self.m.table.state, self.Kp, rows_send, threads=self.m.cfg.threads)
-        gathered = torch.empty((pl.U, self.gs), dtype=torch.float32, device=self.dev)
+    def _gather(self, pl: _ShardPlan) -> tuple[torch.Tensor, torch.Tensor]:
+        """Owner gather of the requested rows + a2a back: (v, w) views of the U wire rows in unique order."""
+        rows_send = self.wire.empty(pl.R, self.dev)
+        K.gather_wire(pl.req_recv, self.m.table.state, self.wire, rows_send, threads=self.m.cfg.threads)
+        if self.W == 1:
+            return self.wire.views(rows_send)
+        gathered = self.wire.empty(pl.U, self.dev)
         _a2a(gathered, rows_send, pl.sc, pl.rc, self.group)
-        return gathered
+        return self.wire.views(gathered)
 
     def train_step(self, b: Batch, next_batch: Batch | None = None):
         from ..models.fm import StepOut
@@ -243,8 +281,7 @@ class ShardExchange(_Base):
             pl = self._take_plan(b, True)
         dd = pl.dd
         with roctx_range("gather+a2a_rows"):
-            gathered = self._gather(pl)
-        src_v, src_w = gathered[:, :Kp], gathered[:, Kp]
+            src_v, src_w = self._gather(pl)
         with roctx_range("fwd"):
             fo = K.fm_forward(b.offsets, dd.inv[: b.nnz], b.vals, src_v, src_w, Kp, labels=b.labels,
                               weights=b.weights, loss=cfg.loss_type, grad_scale=m.grad_scale(b.B), want_r1=True,
@@ -257,11 +294,16 @@ class ShardExchange(_Base):
             K.fm_backward(dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT, src_v=src_v, src_w=src_w, grad_out=grad,
                           reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, dense_part=ws.dense_part,
                           dense_stream=m._dense_stream() if self.dev.type == "cuda" else None)
-        grad_recv = torch.empty((pl.R, self.gs), dtype=torch.float32, device=self.dev)
-        with roctx_range("a2a_grads"):
-            _a2a(grad_recv, grad, pl.rc, pl.sc, self.group)
+        if self.W == 1:
+            grad_recv = grad
+        else:
+            grad_recv = torch.empty((pl.R, self.gs), dtype=torch.float32, device=self.dev)
+            with roctx_range("a2a_grads"):
+                _a2a(grad_recv, grad, pl.rc, pl.sc, self.group)
         with roctx_range("apply"):
-            K.apply_rows(pl.dd2, grad_recv, m.table.state, cfg.opt, Kp, threads=cfg.threads)
+            K.apply_runs(pl.req_recv, pl.run_off, pl.rc, grad_recv, m.table.state, cfg.opt, Kp, match=pl.match,
+                         threads=cfg.threads, ws=self.slots[pl.slot].ensure2(pl.R, self.dev)
+                         if self.dev.type != "cuda" else None)
         if self.dev.type == "cuda":
             done = torch.cuda.Event()
             done.record(torch.cuda.current_stream(self.dev))
@@ -275,9 +317,8 @@ class ShardExchange(_Base):
     def forward(self, b: Batch, *, loss: str = "none", want_reg: bool = False) -> K.FwdOut:
         self.m.ws.ensure(b.B, b.nnz)
         pl = self._take_plan(b, False)
-        gathered = self._gather(pl)
-        out = K.fm_forward(b.offsets, pl.dd.inv[: b.nnz], b.vals, gathered[:, : self.Kp], gathered[:, self.Kp],
-                           self.Kp, labels=b.labels, weights=b.weights, loss=loss, grad_scale=1.0, want_r1=False,
+        src_v, src_w = self._gather(pl)
+        out = K.fm_forward(b.offsets, pl.dd.inv[: b.nnz], b.vals, src_v, src_w, self.Kp, labels=b.labels, weights=b.weights, loss=loss, grad_scale=1.0, want_r1=False,
                            want_reg=want_reg, threads=self.m.cfg.threads, bias=self.m.gbias)
         if self.dev.type == "cuda":
             done = torch.cuda.Event()

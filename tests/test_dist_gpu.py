@@ -58,3 +58,77 @@ def test_rccl_world1_matches_local(rccl_ctx, mode, dense, monkeypatch):
     torch.testing.assert_close(dm.table.reference_rows(), loc.table.reference_rows(), rtol=1e-5, atol=1e-7)
     ev = gen.batch(512)
     torch.testing.assert_close(dm.predict(ev), loc.predict(ev), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, K.FP8])
+@pytest.mark.parametrize("W", [2, 5, 8])
+def test_apply_runs_matches_sorted_apply(dtype, W):
+    """Owner-side run-merge update (cross-run match + leader apply) == sort-based grouping.
+
+    W source ranks each send an ascending run of distinct local rows (overlapping
+    across runs, some empty); both paths must sum each row's gradients in rank
+    order and apply one Adagrad step."""
+    from fast_tffm_amd.models.table import FMTable
+
+    g = torch.Generator().manual_seed(W)
+    rows, k = 5000, 64
+    opt = K.OptConfig("adagrad", lr=0.05)
+    runs = []
+    for q in range(W):
+        n = 0 if q == 1 else int(torch.randint(200, 3000, (1,), generator=g))
+        runs.append(torch.randperm(rows, generator=g)[:n].sort().values)
+    req = torch.cat(runs).to(torch.int32).cuda()
+    splits = [int(r.numel()) for r in runs]
+    R = req.numel()
+    tabs = [FMTable(rows, k, dtype=dtype, opt=opt, init_range=0.05, seed=7, device="cuda") for _ in range(2)]
+    Kp = tabs[0].Kp
+    grad = torch.randn((R, Kp + 4), generator=g).cuda()
+    dd = K.dedup(req, key_bits=32, want_perm=True)
+    K.apply_rows(dd, grad, tabs[0].state, opt, Kp)
+    off = torch.tensor([0] + list(torch.tensor(splits).cumsum(0)), dtype=torch.int32, device="cuda")
+    match = torch.empty(R * W, dtype=torch.int32, device="cuda")
+    K.apply_runs(req, off, splits, grad, tabs[1].state, opt, Kp, match=match)
+    torch.cuda.synchronize()
+    for a, b in zip((tabs[0].v, tabs[0].w, tabs[0].s0v, tabs[0].s0w), (tabs[1].v, tabs[1].w, tabs[1].s0v, tabs[1].s0w)):
+        assert torch.equal(a.float(), b.float())
+
+
+@pytest.mark.parametrize("dtype,k", [(torch.bfloat16, 16), (K.FP8, 128), (torch.bfloat16, 64)])
+def test_rccl_world1_shard_storage_wire_matches_local(rccl_ctx, dtype, k):
+    """bf16 / fp8 tables cross the exchange as their stored bits: the sharded step equals the local one."""
+    V = 50000
+    gen = CriteoSynth(V, device="cuda", seed=22)
+    batches = [gen.batch(2048) for _ in range(3)]
+
+    def cfg(mode):
+        return FMConfig(vocabulary_size=V, factor_num=k, loss_type="logistic", init_value_range=0.05, seed=3,
+                        opt=K.OptConfig("ftrl", lr=0.05, l1=0.001, l2=0.001, beta=1.0), batch_size=2048,
+                        factor_lambda=0.01, bias_lambda=0.01, mode=mode, dtype=dtype)
+
+    loc = FactorizationMachine(cfg("local"), device="cuda")
+    dm = FactorizationMachine(cfg("shard"), device="cuda", dist=rccl_ctx)
+    assert dm._exchange.wire.dtype == dtype
+    for i, b in enumerate(batches):
+        l1 = loc.train_step(b).mean_loss()
+        l2 = dm.train_step(b, batches[i + 1] if i + 1 < len(batches) else None).mean_loss()
+        assert abs(l1 - l2) <= 1e-5 * max(1.0, abs(l1))
+    torch.cuda.synchronize()
+    torch.testing.assert_close(dm.table.reference_rows(), loc.table.reference_rows(), rtol=1e-5, atol=1e-6)
+
+
+def test_rccl_world1_shard_bf16_wire_close_to_fp32(rccl_ctx):
+    """comm_dtype=bf16 on an fp32 table: rows are rounded for transport only (master rows stay fp32)."""
+    V = 50000
+    gen = CriteoSynth(V, device="cuda", seed=23)
+    batches = [gen.batch(2048) for _ in range(3)]
+    loc = FactorizationMachine(_cfg("local", V), device="cuda")
+    c = _cfg("shard", V)
+    c.comm_dtype = "bf16"
+    dm = FactorizationMachine(c, device="cuda", dist=rccl_ctx)
+    assert dm._exchange.wire.dtype == torch.bfloat16 and dm.table.v.dtype == torch.float32
+    for i, b in enumerate(batches):
+        l1 = loc.train_step(b).mean_loss()
+        l2 = dm.train_step(b, batches[i + 1] if i + 1 < len(batches) else None).mean_loss()
+        assert abs(l1 - l2) <= 2e-3 * max(1.0, abs(l1))
+    torch.cuda.synchronize()
+    torch.testing.assert_close(dm.table.reference_rows(), loc.table.reference_rows(), rtol=2e-2, atol=2e-3)
