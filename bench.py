@@ -41,6 +41,8 @@ from fast_tffm_amd.parallel import dist as fmdist  # noqa: E402
 PRESETS = {
     # BASELINE.json headline: FM k=64 Criteo-shaped, row-sharded 1B slots at N=8
     "k64": dict(k=64, dtype="fp32", opt="adagrad", mode="auto", slots_per_gpu=125_000_000),
+    # the headline model with a bf16 factor table (fp32 compute, accumulation and optimizer state)
+    "k64_bf16": dict(k=64, dtype="bf16", opt="adagrad", mode="auto", slots_per_gpu=125_000_000),
     # BASELINE config 2: k=16 bf16 table
     "k16_bf16": dict(k=16, dtype="bf16", opt="adagrad", mode="auto", slots_per_gpu=125_000_000),
     # BASELINE config 3: k=64 data-parallel, dense all-reduce (small replicated vocabulary)
@@ -68,6 +70,8 @@ def main() -> int:
     ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled")
     ap.add_argument("--alpha", type=float, default=1.1, help="Zipf exponent of field values")
     ap.add_argument("--mode", default=None, help="override step mode (local|shard|dp|dp_dense)")
+    ap.add_argument("--microbatches", type=int, default=0,
+                    help="row-sharded step: parts per batch overlapping the exchange (0/1 = one part)")
     ap.add_argument("--comm-dtype", default="auto", choices=["auto", "fp32", "bf16"],
                     help="row-sharded wire rows (auto = table storage dtype; bf16 rounds fp32 rows for transport)")
     ap.add_argument("--profile-steps", type=int, default=0, help="also emit a torch.profiler trace")
@@ -99,7 +103,8 @@ def main() -> int:
     opt = K.OptConfig(p["opt"], lr=0.01 if p["opt"] == "adagrad" else 0.05, l1=0.001, l2=0.001, beta=1.0,
                       initial_accumulator=0.1)
     cfg = FMConfig(vocabulary_size=vocab, factor_num=p["k"], loss_type="logistic", batch_size=a.batch,
-                   init_value_range=0.01, seed=42, dtype=dtype, opt=opt, mode=mode, comm_dtype=a.comm_dtype)
+                   init_value_range=0.01, seed=42, dtype=dtype, opt=opt, mode=mode, comm_dtype=a.comm_dtype,
+                   microbatches=a.microbatches)
     t0 = time.time()
     model = FactorizationMachine(cfg, device=dev, dist=ctx if W > 1 or mode not in ("auto", "local") else None)
     if dev.type == "cuda":
@@ -207,6 +212,7 @@ def main() -> int:
                 "parallelism": par,
                 "wire": str(model._exchange.wire.dtype).replace("torch.", "")
                 if model.mode == "shard" else None,
+                "microbatches": model._exchange.nparts if model.mode == "shard" else None,
             },
         }), flush=True)
     fmdist.shutdown()

@@ -56,8 +56,10 @@ struct BwdArgs {
   float* s1w;
   float reg_v, reg_w;       // lambda_f * reg_grad, lambda_b * reg_grad
   OptParams opt;
-  float* grad_out;          // EMIT: [U, g_stride], w-grad at column Kp
+  float* grad_out;          // EMIT: [U, g_stride] 4-byte words; v-grad fp32 (or bf16), w-grad fp32 at word g_wcol
   long long g_stride;
+  int g_wcol;               // word index of the w-grad in a gradient row
+  int g_bf16;               // 1: v-grad stored as bf16 (the exchange's bf16 wire)
   float* partial;           // [#chunks, Kp + 4]
   int* big_list;            // [U] rows for the workgroup combine
   int* big_count;           // device scalar, zeroed by the launcher
@@ -127,11 +129,22 @@ __device__ inline void bwd_finish(const BwdArgs& a, int u, int t, bool tact, Row
   if (a.mode == kBwdEmit) {
     float* dst = a.grad_out + (long long)u * a.g_stride;
     if (tact) {
+      if (a.g_bf16) {  // EPL bf16 values per lane (EPL * 2 bytes, 8-byte aligned)
+        uint16_t* d16 = reinterpret_cast<uint16_t*>(dst) + t * EPL;
 #pragma unroll
-      for (int k = 0; k < EPL; k += 4)
-        *reinterpret_cast<float4*>(dst + t * EPL + k) = make_float4(gr[k], gr[k + 1], gr[k + 2], gr[k + 3]);
+        for (int k = 0; k < EPL; k += 4) {
+          uint2 o;
+          o.x = f32_to_bf16_bits(gr[k]) | (f32_to_bf16_bits(gr[k + 1]) << 16);
+          o.y = f32_to_bf16_bits(gr[k + 2]) | (f32_to_bf16_bits(gr[k + 3]) << 16);
+          *reinterpret_cast<uint2*>(d16 + k) = o;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < EPL; k += 4)
+          *reinterpret_cast<float4*>(dst + t * EPL + k) = make_float4(gr[k], gr[k + 1], gr[k + 2], gr[k + 3]);
+      }
     }
-    if (t == 0) dst[a.Kp] = gw;
+    if (t == 0) dst[a.g_wcol] = gw;
     return;
   }
 #pragma unroll

@@ -138,7 +138,8 @@ struct ApplyArgs {
   const int* seg_start;     // [U+1] into perm
   const int* uniq;          // [U] local table row
   const int* perm;          // [R] position in grad_in of each sorted entry
-  const float* grad_in; long long g_stride;  // [R, g_stride], w-grad at column Kp
+  const float* grad_in; long long g_stride;  // [R, g_stride] words: v-grad fp32 (or bf16), w-grad at word g_wcol
+  int g_wcol, g_bf16;
   int Kp;
   void* v; long long v_stride;
   float* w; long long w_stride;
@@ -208,13 +209,23 @@ struct RowUpdate {
 };
 
 template <int EPL>
-__device__ inline void add_grad_row(const float* src, int tE, int Kp, float (&gr)[EPL], float& gw) {
+__device__ inline void add_grad_row(const ApplyArgs& a, const float* src, int tE, float (&gr)[EPL], float& gw) {
+  if (a.g_bf16) {
+    const uint16_t* s16 = reinterpret_cast<const uint16_t*>(src) + tE * EPL;
 #pragma unroll
-  for (int k = 0; k < EPL; k += 4) {
-    const float4 f = *reinterpret_cast<const float4*>(src + tE * EPL + k);
-    gr[k] += f.x; gr[k + 1] += f.y; gr[k + 2] += f.z; gr[k + 3] += f.w;
+    for (int k = 0; k < EPL; k += 4) {
+      const uint2 f = *reinterpret_cast<const uint2*>(s16 + k);
+      gr[k] += bf16_bits_to_f32(f.x & 0xffffu); gr[k + 1] += bf16_bits_to_f32(f.x >> 16);
+      gr[k + 2] += bf16_bits_to_f32(f.y & 0xffffu); gr[k + 3] += bf16_bits_to_f32(f.y >> 16);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < EPL; k += 4) {
+      const float4 f = *reinterpret_cast<const float4*>(src + tE * EPL + k);
+      gr[k] += f.x; gr[k + 1] += f.y; gr[k + 2] += f.z; gr[k + 3] += f.w;
+    }
   }
-  gw += src[Kp];
+  gw += src[a.g_wcol];
 }
 
 // Owner-side: sum the gradient rows every peer sent for one table row (in
@@ -241,7 +252,7 @@ __global__ __launch_bounds__(kBlock) void apply_rows_kernel(ApplyArgs a) {
     float gw = 0.f;
     const int j1 = a.seg_start[u + 1];
     for (int j = a.seg_start[u]; j < j1; ++j)
-      add_grad_row<EPL>(a.grad_in + (long long)a.perm[j] * a.g_stride, tE, a.Kp, gr, gw);
+      add_grad_row<EPL>(a, a.grad_in + (long long)a.perm[j] * a.g_stride, tE, gr, gw);
     ru.step_store(a, gr, gw, row, t, tact);
   }
 }
@@ -298,10 +309,10 @@ __global__ __launch_bounds__(kBlock) void apply_runs_kernel(ApplyArgs a) {
 #pragma unroll
     for (int k = 0; k < EPL; ++k) gr[k] = 0.f;
     float gw = 0.f;
-    add_grad_row<EPL>(a.grad_in + (long long)i * a.g_stride, tE, a.Kp, gr, gw);
+    add_grad_row<EPL>(a, a.grad_in + (long long)i * a.g_stride, tE, gr, gw);
     for (int q = r + 1; q < a.W; ++q) {
       const int j = mrow[q];
-      if (j >= 0) add_grad_row<EPL>(a.grad_in + (long long)j * a.g_stride, tE, a.Kp, gr, gw);
+      if (j >= 0) add_grad_row<EPL>(a, a.grad_in + (long long)j * a.g_stride, tE, gr, gw);
     }
     ru.step_store(a, gr, gw, row, t, tact);
   }

@@ -25,6 +25,7 @@ class Batch:
     nnz: int = -1                   # host copy of offsets[-1] (avoids a device sync)
     reader_pos: tuple | None = None  # (epoch, batches consumed in epoch) after this batch
     max_feats: int = -1             # host-known max features per example (-1: unknown)
+    offsets_host: torch.Tensor | None = None  # CPU copy of offsets (lets the executor split without a sync)
 
     def __post_init__(self):
         if self.nnz < 0:
@@ -38,19 +39,28 @@ class Batch:
     def device(self) -> torch.device:
         return self.ids.device
 
+    def _host_offsets(self) -> torch.Tensor | None:
+        return self.offsets_host if self.offsets_host is not None else (
+            self.offsets if self.offsets.device.type == "cpu" else None)
+
+    def host_offset(self, i: int) -> int:
+        """offsets[i] as a host int (a device read only when no host copy is known)."""
+        h = self._host_offsets()
+        return int(h[i]) if h is not None else int(self.offsets[i].item())
+
     def to(self, device, non_blocking: bool = True) -> "Batch":
         def mv(t):
             return None if t is None else t.to(device, non_blocking=non_blocking)
 
         return Batch(mv(self.labels), mv(self.offsets), mv(self.ids), mv(self.vals), mv(self.weights), self.nnz,
-                     self.reader_pos, self.max_feats)
+                     self.reader_pos, self.max_feats, self._host_offsets())
 
     def pin_memory(self) -> "Batch":
         def pn(t):
             return None if t is None else t.pin_memory()
 
         return Batch(pn(self.labels), pn(self.offsets), pn(self.ids), pn(self.vals), pn(self.weights), self.nnz,
-                     self.reader_pos, self.max_feats)
+                     self.reader_pos, self.max_feats, self._host_offsets())
 
     @staticmethod
     def from_parsed(labels: np.ndarray, sizes: np.ndarray, ids: np.ndarray, vals: np.ndarray,

@@ -71,7 +71,7 @@ class CriteoSynth:
         offsets = torch.arange(0, (B + 1) * self.F, self.F, dtype=torch.int32, device=dev)
         labels = (torch.rand(B, generator=self.gen, device=dev) < self.ctr).to(torch.float32)
         return Batch(labels=labels, offsets=offsets, ids=ids, vals=None, weights=None, nnz=B * self.F,
-                     max_feats=self.F)
+                     max_feats=self.F, offsets_host=torch.arange(0, (B + 1) * self.F, self.F, dtype=torch.int32))
 
 
 def random_batch(B: int, vocab_size: int, max_feats: int = 8, *, seed: int = 0, device="cpu",

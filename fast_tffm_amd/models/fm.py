@@ -49,6 +49,7 @@ class FMConfig:
     mode: str = "auto"                # auto | local | shard | dp | dp_dense
     grad_reduce: str = "sum"          # sum | mean (multi-rank)
     comm_dtype: str = "auto"          # row-sharded wire rows: auto (= storage dtype) | fp32 | bf16
+    microbatches: int = 0             # row-sharded step: parts per batch overlapping the exchange (0/1 = one)
     dedup_chunk: int = 32             # CH of the segmented backward
     threads: int = 0                  # CPU kernels (0 = OpenMP default)
     global_bias: bool = False         # learned global bias b0 (extension; the reference has none)

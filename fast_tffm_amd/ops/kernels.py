@@ -438,7 +438,8 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
                 src_v: torch.Tensor | None = None, src_w: torch.Tensor | None = None,
                 grad_out: torch.Tensor | None = None, reg_v: float = 0.0, reg_w: float = 0.0,
                 partial: torch.Tensor | None = None, threads: int = 0,
-                dense_part: torch.Tensor | None = None, dense_stream=None) -> torch.Tensor | None:
+                dense_part: torch.Tensor | None = None, dense_stream=None,
+                grad_bf16: bool = False) -> torch.Tensor | None:
     """Segmented FM backward over the dedup grouping (reference FmGrad, cc/fm_grad_op.h:59-163).
 
     Per unique row u with occurrences (i, x):
@@ -470,7 +471,9 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
         s_stride = 0
         _check(grad_out.dtype == torch.float32 and grad_out.stride(1) == 1, "grad_out: fp32 rows")
         gstride, gptr = grad_out.stride(0), grad_out.data_ptr()
-        _check(gstride >= Kp + 1 and gstride % 4 == 0, "grad_out row stride must be >= Kp+1 and a multiple of 4")
+        g_wcol = (Kp * 2 + 15) // 16 * 4 if grad_bf16 else Kp
+        _check(gstride >= g_wcol + 1 and gstride % 4 == 0, "grad_out row stride must hold the w column and be a multiple of 4")
+        _check(not grad_bf16 or _is_gpu(dpred), "bf16 gradient rows are a GPU path")
     v_stride = _chk_rows(v, Kp, "v")
     o = opt or OptConfig()
     if _is_gpu(dpred):
@@ -496,7 +499,7 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               slice_start=_p(dd.slice_start), nslices=int(dd.nslices or 0), dense_list=_p(dd.dense_list),
               dense_part=_p(dp), nex=int(dpred.numel()),
               dense_stream=dense_stream.cuda_stream if dense_stream is not None else 0, dtype=dt, max_chunks=dd.n, max_unique=dd.n,
-              stream=_stream(dpred))
+              stream=_stream(dpred), g_wcol=g_wcol if mode == BWD_EMIT else -1, g_bf16=int(bool(grad_bf16)))
     else:
         U = dd.sync()
         native.cpu().bwd(mode=mode, U=U, seg_start=_p(dd.seg_start), uniq=_p(dd.uniq), sorted_ex=_p(dd.sorted_ex),
@@ -585,7 +588,7 @@ def apply_rows(dd: DedupOut, grad_in: torch.Tensor, table: TableState, opt: OptC
 
 def apply_runs(req: torch.Tensor, run_off: torch.Tensor, splits: list[int], grad_in: torch.Tensor,
                table: TableState, opt: OptConfig, Kp: int, match: torch.Tensor | None = None,
-               threads: int = 0, ws: DedupWorkspace | None = None) -> None:
+               threads: int = 0, ws: DedupWorkspace | None = None, grad_bf16: bool = False) -> None:
     """Owner side of a sharded update over the received requests as W ascending runs.
 
     ``req`` [R] holds the local rows requested by each source rank, rank-major
@@ -602,6 +605,7 @@ def apply_runs(req: torch.Tensor, run_off: torch.Tensor, splits: list[int], grad
     if R == 0:
         return
     if not _is_gpu(grad_in):
+        _check(not grad_bf16, "bf16 gradient rows are a GPU path")
         dd = dedup(req[:R], ws=ws, key_bits=32, want_perm=True)
         apply_rows(dd, grad_in, table, opt, Kp, threads=threads)
         return
@@ -617,7 +621,8 @@ def apply_runs(req: torch.Tensor, run_off: torch.Tensor, splits: list[int], grad
                             w=_p(table.w), w_stride=table.w.stride(0), s0v=_p(table.s0v), s1v=_p(table.s1v),
                             s_stride=s_stride, s0w=_p(table.s0w), s1w=_p(table.s1w), opt_type=opt.code,
                             lr=float(opt.lr), l1=float(opt.l1), l2=float(opt.l2), beta=float(opt.beta), dtype=dt,
-                            stream=_stream(grad_in))
+                            stream=_stream(grad_in), g_wcol=(Kp * 2 + 15) // 16 * 4 if grad_bf16 else Kp,
+                            g_bf16=int(bool(grad_bf16)))
 
 
 @dataclass
@@ -636,19 +641,29 @@ class WireFormat:
     vb: int
     rb: int
     table_dtype: torch.dtype
+    grad_bf16: bool = False   # gradient rows: [Kp bf16 | pad to gvb][gw fp32, 0, 0, 0] instead of [Kp fp32 | gw | pad]
+    g_words: int = 0          # 4-byte words per gradient row
+    g_wcol: int = 0           # word index of the w-gradient
 
     @staticmethod
     def make(table_dtype: torch.dtype, Kp: int, comm_dtype: str = "auto") -> "WireFormat":
+        if comm_dtype not in ("auto", "bf16", "fp32", "storage"):
+            raise ValueError(f"comm_dtype must be auto|storage|fp32|bf16, got {comm_dtype}")
         dt = table_dtype
         if comm_dtype == "bf16" and table_dtype == torch.float32 and Kp % 8 == 0:
             dt = torch.bfloat16
-        elif comm_dtype not in ("auto", "bf16", "fp32", "storage"):
-            raise ValueError(f"comm_dtype must be auto|storage|fp32|bf16, got {comm_dtype}")
         if comm_dtype == "fp32":
             dt = torch.float32
         esz = torch.tensor([], dtype=dt).element_size()
         vb = (Kp * esz + 15) // 16 * 16
-        return WireFormat(dt, Kp, vb, vb + 16, table_dtype)
+        gbf = comm_dtype == "bf16"
+        gvb = (Kp * 2 + 15) // 16 * 16
+        g_words, g_wcol = ((gvb + 16) // 4, gvb // 4) if gbf else (Kp + 4, Kp)
+        return WireFormat(dt, Kp, vb, vb + 16, table_dtype, gbf, g_words, g_wcol)
+
+    def empty_grads(self, n: int, device) -> torch.Tensor:
+        """Gradient rows in the wire's gradient layout (fp32 words; bf16 pairs packed when ``grad_bf16``)."""
+        return torch.empty((n, self.g_words), dtype=torch.float32, device=device)
 
     @property
     def fp32(self) -> bool:

@@ -69,11 +69,20 @@ class _Base:
         return self.dd2ws
 
 
-class _ShardPlan:
-    """The table-independent half of one batch's sharded step: dedup, owner counts,
-    id all-to-all and the owner-side grouping of the received requests."""
+class _Part:
+    """One micro-batch of a sharded step: its examples, dedup grouping, owner split
+    sizes and the rows it requests from every owner."""
 
-    __slots__ = ("b", "slot", "dd", "sc", "rc", "U", "R", "req_recv", "run_off", "match", "ready")
+    __slots__ = ("b", "e0", "dd", "sc", "rc", "U", "R", "u0", "r0", "req_send")
+
+
+class _ShardPlan:
+    """The table-independent half of one batch's sharded step: per micro-batch part
+    the dedup, owner counts and id all-to-all, plus the owner-side run offsets
+    over all parts' received requests (``req_recv`` holds part 0's runs, then
+    part 1's, ...; ``run_off`` the W * parts run boundaries)."""
+
+    __slots__ = ("b", "slot", "parts", "U", "R", "req_recv", "run_off", "splits", "match", "ready")
 
 
 class _PlanSlot:
@@ -81,35 +90,40 @@ class _PlanSlot:
     while step t still reads the buffers of plan t)."""
 
     def __init__(self):
-        self.dd: K.DedupWorkspace | None = None
-        self.dd2: K.DedupWorkspace | None = None
-        self.keys: torch.Tensor | None = None
+        self.dd: list[K.DedupWorkspace | None] = []
+        self.keys: list[torch.Tensor | None] = []
+        self.dd2: K.DedupWorkspace | None = None   # CPU owner grouping
         self.done: torch.cuda.Event | None = None  # main-stream event: last step using this slot finished
-        self.run_off_h: torch.Tensor | None = None  # pinned [W+1] receive-run offsets (host staging)
+        self.run_off_h: torch.Tensor | None = None  # pinned receive-run offsets (host staging)
         self.run_off: torch.Tensor | None = None    # device copy
-        self.match: torch.Tensor | None = None      # [R, W] cross-run match scratch (apply_runs)
+        self.match: torch.Tensor | None = None      # [R, runs] cross-run match scratch (apply_runs)
 
-    def ensure(self, nnz: int, dev, CH: int) -> None:
-        if self.dd is None or self.dd.cap < nnz:
-            cap = max(nnz, 1, int(1.25 * (self.dd.cap if self.dd else 0)))
-            self.dd = K.DedupWorkspace(cap, dev, CH)
-            self.keys = torch.empty(cap, dtype=torch.int32, device=dev)
+    def ensure(self, k: int, nnz: int, dev, CH: int) -> K.DedupWorkspace:
+        while len(self.dd) <= k:
+            self.dd.append(None)
+            self.keys.append(None)
+        d = self.dd[k]
+        if d is None or d.cap < nnz:
+            cap = max(nnz, 1, int(1.25 * (d.cap if d else 0)))
+            self.dd[k] = K.DedupWorkspace(cap, dev, CH)
+            self.keys[k] = torch.empty(cap, dtype=torch.int32, device=dev)
+        return self.dd[k]
 
     def runs(self, splits: list[int], dev) -> torch.Tensor:
         """Device int32 prefix offsets of the receive runs, staged through pinned memory.
 
         Called after this stream's host sync on the owner counts, so the previous
         copy out of the pinned buffer (same stream, earlier) has completed."""
-        W = len(splits)
-        if self.run_off is None or self.run_off.numel() < W + 1:
-            self.run_off_h = torch.empty(W + 1, dtype=torch.int32, pin_memory=True)
-            self.run_off = torch.empty(W + 1, dtype=torch.int32, device=dev)
+        n = len(splits)
+        if self.run_off is None or self.run_off.numel() < n + 1:
+            self.run_off_h = torch.empty(n + 1, dtype=torch.int32, pin_memory=True)
+            self.run_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
         acc = 0
         self.run_off_h[0] = 0
         for q, c in enumerate(splits):
             acc += c
             self.run_off_h[q + 1] = acc
-        self.run_off[: W + 1].copy_(self.run_off_h[: W + 1], non_blocking=True)
+        self.run_off[: n + 1].copy_(self.run_off_h[: n + 1], non_blocking=True)
         return self.run_off
 
     def match_buf(self, n: int, dev) -> torch.Tensor:
@@ -124,13 +138,33 @@ class _PlanSlot:
         return self.dd2
 
 
+def _sub_batch(b: Batch, e0: int, e1: int, n0: int, n1: int, offsets: torch.Tensor) -> Batch:
+    """Examples [e0, e1) of ``b`` (occurrences [n0, n1)) as views, with rebased ``offsets``."""
+    return Batch(b.labels[e0:e1], offsets, b.ids[n0:n1], None if b.vals is None else b.vals[n0:n1],
+                 None if b.weights is None else b.weights[e0:e1], n1 - n0, max_feats=b.max_feats)
+
+
 class ShardExchange(_Base):
-    """Row-sharded step.  ``train_step(b, next_batch)`` builds the plan of the next
-    batch (everything that does not read the table: dedup, counts + id a2a with its
-    one host sync, owner-side grouping) on a side stream while this step's
-    forward/backward run, so only gather -> a2a(rows) -> fwd -> bwd -> a2a(grads)
-    -> apply stay on the critical path.  Synchronous semantics are unchanged: the
-    rows of step t+1 are gathered after step t's update."""
+    """Row-sharded step.
+
+    ``train_step(b, next_batch)`` builds the plan of the next batch (everything that
+    does not read the table: dedup, counts + id a2a with its one host sync,
+    owner-side run offsets) on a side stream while this step's forward/backward
+    run, so only gather -> a2a(rows) -> fwd -> bwd -> a2a(grads) -> apply stay on
+    the critical path.  Synchronous semantics are unchanged: the rows of step t+1
+    are gathered after step t's update.
+
+    With ``microbatches = P > 1`` the batch is cut into P parts with their own
+    dedup: the row all-to-all of part k+1 runs on RCCL's stream while part k
+    computes, and part k's gradient all-to-all while part k+1 computes; the owner
+    sums all parts' gradient rows (P*W runs, fixed order) and applies the
+    optimizer once.  Cost: rows used by several parts cross the wire once per
+    part (~+20% rows for P=2 on Criteo-shaped batches), the backward runs on
+    smaller groups and the plan chain (P dedups) grows: measured at world 1
+    (profiles/shard_mb), P=2 adds ~160 us of compute and ~35% to the plan chain,
+    more than it can hide when the exchange is link-bound (every a2a shares one
+    RCCL stream), so the default is one part.
+    """
 
     supports_lookahead = True
 
@@ -139,11 +173,13 @@ class ShardExchange(_Base):
         self.Rps = model.rps
         self.key_bits = bits_for(self.W * self.Rps)
         self.slots = [_PlanSlot(), _PlanSlot()]
-        # lookahead plans talk on their own communicator (own RCCL stream): the id
-        # all-to-all of batch t+1 does not queue behind step t's row / grad all-to-alls
         # wire format of the gathered rows: storage dtype (exact) or bf16 for fp32 tables on request
         tdt = model.table.v.dtype
         self.wire = K.WireFormat.make(tdt, self.Kp, model.cfg.comm_dtype if self.dev.type == "cuda" else "fp32")
+        mb = int(getattr(model.cfg, "microbatches", 0) or 0)
+        self.nparts = max(1, mb)
+        # lookahead plans talk on their own communicator (own RCCL stream): the id
+        # all-to-all of batch t+1 does not queue behind step t's row / grad all-to-alls
         self.plan_group = (dist.new_group(ranks=list(range(self.W)), backend=dist.get_backend(self.group))
                            if self.W > 1 else self.group)
         self.cpu_group = self.ctx.cpu_group or self.group
@@ -151,13 +187,18 @@ class ShardExchange(_Base):
         self.pending: _ShardPlan | None = None
         self._prep = None
 
-    def _keys(self, b: Batch, out: torch.Tensor) -> torch.Tensor:
-        return K.shard_keys(b.ids, self.W, self.Rps, out)
-
     def _prep_stream(self):
         if self._prep is None:
             self._prep = torch.cuda.Stream(self.dev)
         return self._prep
+
+    def _split(self, b: Batch, nparts: int) -> list[tuple[int, int, int, int]]:
+        """(e0, e1, n0, n1) example / occurrence ranges of the micro-batches of ``b``."""
+        if nparts <= 1 or b.B < 2 * nparts:
+            return [(0, b.B, 0, b.nnz)]
+        cuts = [b.B * i // nparts for i in range(nparts + 1)]
+        nz = [0] + [b.host_offset(c) for c in cuts[1:-1]] + [b.nnz]
+        return [(cuts[i], cuts[i + 1], nz[i], nz[i + 1]) for i in range(nparts)]
 
     def _plan(self, b: Batch, train: bool, inputs_ready=None) -> _ShardPlan:
         """Build the plan of ``b`` (on the side stream when on the GPU).
@@ -190,40 +231,62 @@ class ShardExchange(_Base):
             import contextlib
 
             ctx = contextlib.nullcontext()
+        ranges = self._split(b, self.nparts if train else 1)
         with ctx:
-            slot.ensure(b.nnz, self.dev, m.cfg.dedup_chunk)
-            keys = self._keys(b, slot.keys)
-            ex, sb = None, 0
-            if train:
-                sb = m._slot_bits(b, always=True)
-                ex = K.csr_rows(b.offsets, out=slot.dd.ex_of_occ[: b.nnz], nnz=b.nnz, slot_bits=sb)
-            dd = K.dedup(keys, ws=slot.dd, key_bits=self.key_bits, ex_of_occ=ex,
-                         vals=b.vals if ex is not None else None, want_inv=True, num_examples=b.B, Kp=self.m.Kp,
-                         ex_shift=sb, offsets=b.offsets if sb else None,
-                         dense_min=K.dense_min_for(b.B, self.m.Kp, m.cfg.dedup_chunk) if train else 0)
-            # per-owner counts: one small D2H on this (side) stream -- the only host sync of the
-            # step, it waits for this dedup only -- then the count exchange on the CPU group
-            sc = K.owner_counts(dd, self.Rps, self.W).cpu()
+            pl.parts = []
+            counts = []
+            for k, (e0, e1, n0, n1) in enumerate(ranges):
+                part = _Part()
+                offs = b.offsets[e0:e1 + 1] if n0 == 0 else b.offsets[e0:e1 + 1] - n0
+                part.b = sb = b if len(ranges) == 1 else _sub_batch(b, e0, e1, n0, n1, offs)
+                part.e0 = e0
+                dws = slot.ensure(k, sb.nnz, self.dev, m.cfg.dedup_chunk)
+                keys = K.shard_keys(sb.ids, self.W, self.Rps, slot.keys[k])
+                ex, shift = None, 0
+                if train:
+                    shift = m._slot_bits(sb, always=True)
+                    ex = K.csr_rows(sb.offsets, out=dws.ex_of_occ[: sb.nnz], nnz=sb.nnz, slot_bits=shift)
+                part.dd = K.dedup(keys, ws=dws, key_bits=self.key_bits, ex_of_occ=ex,
+                                  vals=sb.vals if ex is not None else None, want_inv=True, num_examples=sb.B,
+                                  Kp=self.m.Kp, ex_shift=shift, offsets=sb.offsets if shift else None,
+                                  dense_min=K.dense_min_for(sb.B, self.m.Kp, m.cfg.dedup_chunk) if train else 0)
+                counts.append(K.owner_counts(part.dd, self.Rps, self.W))
+                pl.parts.append(part)
+            P = len(pl.parts)
+            # per-owner counts of all parts: one small D2H on this (side) stream -- the only
+            # host sync of the step, it waits for these dedups only -- and one count exchange
+            # on the CPU group: row q of the [W, P] matrix is what goes to / comes from rank q
+            sc = torch.stack(counts, dim=1).cpu()
             rc = torch.empty_like(sc)
             dist.all_to_all_single(rc, sc, group=self.cpu_group)
-            pl.sc, pl.rc = sc.tolist(), rc.tolist()
-            pl.U, pl.R = int(sum(pl.sc)), int(sum(pl.rc))
-            if K.debug_checks():
-                self._check_splits(pl, dd)
-            dd.U_host = pl.U
-            req_send = torch.remainder(dd.uniq[: pl.U], self.Rps)  # keys are owner * Rps + local row
-            if self.W == 1:
-                pl.req_recv = req_send      # a one-rank exchange is the identity: no copy
-            else:
-                pl.req_recv = torch.empty(pl.R, dtype=torch.int32, device=self.dev)
-                _a2a(pl.req_recv, req_send, pl.rc, pl.sc, self.plan_group)
-            pl.dd = dd
-            # owner-side grouping of the received requests (W ascending runs): device run
-            # offsets + match scratch for apply_runs; the CPU path sorts inside apply_runs
+            sc_l, rc_l = sc.t().tolist(), rc.t().tolist()
+            u_off = r_off = 0
+            for k, part in enumerate(pl.parts):
+                part.sc, part.rc = sc_l[k], rc_l[k]
+                part.U, part.R = int(sum(part.sc)), int(sum(part.rc))
+                part.u0, part.r0 = u_off, r_off
+                u_off += part.U
+                r_off += part.R
+                part.dd.U_host = part.U
+                if K.debug_checks():
+                    self._check_splits(part)
+            pl.U, pl.R = u_off, r_off
+            pl.req_recv = torch.empty(max(pl.R, 1), dtype=torch.int32, device=self.dev)
+            for part in pl.parts:
+                # keys are owner * Rps + local row: the local rows requested from each owner
+                dst = pl.req_recv[part.r0: part.r0 + part.R]
+                if self.W == 1:
+                    torch.remainder(part.dd.uniq[: part.U], self.Rps, out=dst)  # identity exchange
+                else:
+                    req_send = torch.remainder(part.dd.uniq[: part.U], self.Rps)
+                    _a2a(dst, req_send, part.rc, part.sc, self.plan_group)
+            # owner-side grouping of the received requests (W * P ascending runs): device
+            # run offsets + match scratch for apply_runs; the CPU path sorts inside apply_runs
+            pl.splits = [c for part in pl.parts for c in part.rc]
             pl.run_off = pl.match = None
             if train and gpu:
-                pl.run_off = slot.runs(pl.rc, self.dev)
-                pl.match = slot.match_buf(pl.R * self.W, self.dev) if self.W > 1 else None
+                pl.run_off = slot.runs(pl.splits, self.dev)
+                pl.match = slot.match_buf(pl.R * len(pl.splits), self.dev) if len(pl.splits) > 1 else None
             if gpu:
                 pl.ready = torch.cuda.Event()
                 pl.ready.record(st)
@@ -231,25 +294,26 @@ class ShardExchange(_Base):
                 pl.ready = None
         return pl
 
-    def _check_splits(self, pl: _ShardPlan, dd) -> None:
+    def _check_splits(self, part: _Part) -> None:
         """FM_DEBUG_CHECKS=1: the split lists of every rank must form a consistent W x W
         exchange (what rank s sends to r is what r expects from s) and cover all unique ids."""
         mats = [None] * self.W
-        dist.all_gather_object(mats, (pl.sc, pl.rc), group=self.cpu_group)
+        dist.all_gather_object(mats, (part.sc, part.rc), group=self.cpu_group)
         for r in range(self.W):
             for q in range(self.W):
                 if mats[q][0][r] != mats[r][1][q]:
                     raise RuntimeError(f"a2a split mismatch: rank {q} sends {mats[q][0][r]} ids to rank {r}, "
                                        f"which expects {mats[r][1][q]}")
+        dd = part.dd
         u = int(dd.num_unique.item())
-        if u != pl.U:
-            raise RuntimeError(f"owner counts cover {pl.U} ids, dedup found {u}")
-        if pl.U and int(dd.uniq[pl.U - 1].item()) >= self.W * self.Rps:
+        if u != part.U:
+            raise RuntimeError(f"owner counts cover {part.U} ids, dedup found {u}")
+        if part.U and int(dd.uniq[part.U - 1].item()) >= self.W * self.Rps:
             raise RuntimeError("sharded key out of range")
 
     def _take_plan(self, b: Batch, train: bool) -> _ShardPlan:
         pl = self.pending
-        if pl is not None and pl.b is b:
+        if pl is not None and pl.b is b and (len(pl.parts) > 1) == (train and self.nparts > 1 and b.B >= 2 * self.nparts):
             self.pending = None
         else:  # (a pending plan for another batch, e.g. the next training batch, stays pending)
             pl = self._plan(b, train)
@@ -257,69 +321,95 @@ class ShardExchange(_Base):
             main = torch.cuda.current_stream(self.dev)
             main.wait_event(pl.ready)
             pl.req_recv.record_stream(main)  # allocated on the side stream, read on main
+            for part in pl.parts:
+                if part.b is not b:
+                    part.b.offsets.record_stream(main)
         return pl
 
-    def _gather(self, pl: _ShardPlan) -> tuple[torch.Tensor, torch.Tensor]:
-        """Owner gather of the requested rows + a2a back: (v, w) views of the U wire rows in unique order."""
-        rows_send = self.wire.empty(pl.R, self.dev)
-        K.gather_wire(pl.req_recv, self.m.table.state, self.wire, rows_send, threads=self.m.cfg.threads)
+    def _gather_part(self, pl: _ShardPlan, part: _Part, async_op: bool):
+        """Owner gather of the rows part ``part`` requested + a2a back.
+
+        Returns (buffer, work): the U wire rows in unique order arrive in ``buffer``
+        once ``work`` (None: already there) is waited for."""
+        rows_send = self.wire.empty(part.R, self.dev)
+        K.gather_wire(pl.req_recv[part.r0: part.r0 + part.R], self.m.table.state, self.wire, rows_send,
+                      threads=self.m.cfg.threads)
         if self.W == 1:
-            return self.wire.views(rows_send)
-        gathered = self.wire.empty(pl.U, self.dev)
-        _a2a(gathered, rows_send, pl.sc, pl.rc, self.group)
-        return self.wire.views(gathered)
+            return rows_send, None
+        gathered = self.wire.empty(part.U, self.dev)
+        work = dist.all_to_all_single(gathered, rows_send, part.sc, part.rc, group=self.group, async_op=async_op)
+        return gathered, work
 
     def train_step(self, b: Batch, next_batch: Batch | None = None):
         from ..models.fm import StepOut
 
         m, ws, cfg, Kp = self.m, self.m.ws, self.m.cfg, self.Kp
+        gpu = self.dev.type == "cuda"
         nb_ready = None
-        if next_batch is not None and self.dev.type == "cuda" and getattr(next_batch, "ready", None) is None:
+        if next_batch is not None and gpu and getattr(next_batch, "ready", None) is None:
             nb_ready = torch.cuda.Event()  # next_batch's producers: all work enqueued before this step
             nb_ready.record(torch.cuda.current_stream(self.dev))
         with roctx_range("plan"):
             pl = self._take_plan(b, True)
-        dd = pl.dd
+        wf = self.wire
+        # every part's rows are gathered first and their all-to-alls queued on RCCL's stream
+        # (async): part k+1's rows travel while part k computes
         with roctx_range("gather+a2a_rows"):
-            src_v, src_w = self._gather(pl)
-        with roctx_range("fwd"):
-            fo = K.fm_forward(b.offsets, dd.inv[: b.nnz], b.vals, src_v, src_w, Kp, labels=b.labels,
-                              weights=b.weights, loss=cfg.loss_type, grad_scale=m.grad_scale(b.B), want_r1=True,
-                              pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B],
-                              partial=ws.fwd_partial, threads=cfg.threads, bias=m.gbias)
-            m.bias_step(fo.dpred)
-        grad = torch.empty((pl.U, self.gs), dtype=torch.float32, device=self.dev)
+            rows = [self._gather_part(pl, part, async_op=True) for part in pl.parts]
+        grad_send = wf.empty_grads(max(pl.U, 1), self.dev)
+        grad_recv = grad_send if self.W == 1 else wf.empty_grads(max(pl.R, 1), self.dev)
+        gworks = []
+        loss = None
         rv, rw = m.reg_coeffs
-        with roctx_range("bwd"):
-            K.fm_backward(dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT, src_v=src_v, src_w=src_w, grad_out=grad,
-                          reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, dense_part=ws.dense_part,
-                          dense_stream=m._dense_stream() if self.dev.type == "cuda" else None)
-        if self.W == 1:
-            grad_recv = grad
-        else:
-            grad_recv = torch.empty((pl.R, self.gs), dtype=torch.float32, device=self.dev)
-            with roctx_range("a2a_grads"):
-                _a2a(grad_recv, grad, pl.rc, pl.sc, self.group)
+        gscale = m.grad_scale(b.B)
+        for part, (buf, work) in zip(pl.parts, rows):
+            sb, dd, e0 = part.b, part.dd, part.e0
+            if work is not None:
+                work.wait()               # the compute stream waits for this part's rows
+            src_v, src_w = wf.views(buf)
+            with roctx_range("fwd"):
+                fo = K.fm_forward(sb.offsets, dd.inv[: sb.nnz], sb.vals, src_v, src_w, Kp, labels=sb.labels,
+                                  weights=sb.weights, loss=cfg.loss_type, grad_scale=gscale, want_r1=True,
+                                  pred=ws.pred[e0: e0 + sb.B], r1=ws.r1[e0: e0 + sb.B],
+                                  dpred=ws.dpred[e0: e0 + sb.B], partial=ws.fwd_partial, threads=cfg.threads,
+                                  bias=m.gbias)
+            loss = fo.loss_sum if loss is None else loss + fo.loss_sum
+            gs = grad_send[part.u0: part.u0 + part.U]
+            with roctx_range("bwd"):
+                K.fm_backward(dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT, src_v=src_v, src_w=src_w, grad_out=gs,
+                              reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads,
+                              dense_part=ws.dense_part, dense_stream=m._dense_stream() if gpu else None,
+                              grad_bf16=wf.grad_bf16)
+            if self.W > 1:
+                with roctx_range("a2a_grads"):
+                    gworks.append(dist.all_to_all_single(grad_recv[part.r0: part.r0 + part.R], gs, part.rc, part.sc,
+                                                         group=self.group, async_op=True))
+        m.bias_step(ws.dpred[: b.B])
+        for w in gworks:
+            w.wait()
         with roctx_range("apply"):
-            K.apply_runs(pl.req_recv, pl.run_off, pl.rc, grad_recv, m.table.state, cfg.opt, Kp, match=pl.match,
-                         threads=cfg.threads, ws=self.slots[pl.slot].ensure2(pl.R, self.dev)
-                         if self.dev.type != "cuda" else None)
-        if self.dev.type == "cuda":
+            K.apply_runs(pl.req_recv, pl.run_off, pl.splits, grad_recv, m.table.state, cfg.opt, Kp, match=pl.match,
+                         threads=cfg.threads, ws=self.slots[pl.slot].ensure2(pl.R, self.dev) if not gpu else None,
+                         grad_bf16=wf.grad_bf16)
+        if gpu:
             done = torch.cuda.Event()
             done.record(torch.cuda.current_stream(self.dev))
             self.slots[pl.slot].done = done
         if next_batch is not None:
             with roctx_range("plan_next"):
                 self.pending = self._plan(next_batch, True, nb_ready)
-        return StepOut(fo.loss_sum, b.B)
+        return StepOut(loss, b.B)
 
     @torch.no_grad()
     def forward(self, b: Batch, *, loss: str = "none", want_reg: bool = False) -> K.FwdOut:
         self.m.ws.ensure(b.B, b.nnz)
         pl = self._take_plan(b, False)
-        src_v, src_w = self._gather(pl)
-        out = K.fm_forward(b.offsets, pl.dd.inv[: b.nnz], b.vals, src_v, src_w, self.Kp, labels=b.labels, weights=b.weights, loss=loss, grad_scale=1.0, want_r1=False,
-                           want_reg=want_reg, threads=self.m.cfg.threads, bias=self.m.gbias)
+        part = pl.parts[0]
+        buf, work = self._gather_part(pl, part, async_op=False)
+        src_v, src_w = self.wire.views(buf)
+        out = K.fm_forward(b.offsets, part.dd.inv[: b.nnz], b.vals, src_v, src_w, self.Kp, labels=b.labels,
+                           weights=b.weights, loss=loss, grad_scale=1.0, want_r1=False, want_reg=want_reg,
+                           threads=self.m.cfg.threads, bias=self.m.gbias)
         if self.dev.type == "cuda":
             done = torch.cuda.Event()
             done.record(torch.cuda.current_stream(self.dev))

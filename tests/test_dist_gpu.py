@@ -132,3 +132,24 @@ def test_rccl_world1_shard_bf16_wire_close_to_fp32(rccl_ctx):
         assert abs(l1 - l2) <= 2e-3 * max(1.0, abs(l1))
     torch.cuda.synchronize()
     torch.testing.assert_close(dm.table.reference_rows(), loc.table.reference_rows(), rtol=2e-2, atol=2e-3)
+
+
+@pytest.mark.parametrize("mb", [2, 3])
+def test_rccl_world1_shard_microbatches_match_local(rccl_ctx, mb):
+    """The micro-batched sharded step (parts with their own dedup, 2W owner runs) == the local step."""
+    V = 50000
+    gen = CriteoSynth(V, device="cuda", seed=24)
+    batches = [gen.batch(2048) for _ in range(3)]
+    loc = FactorizationMachine(_cfg("local", V), device="cuda")
+    c = _cfg("shard", V)
+    c.microbatches = mb
+    dm = FactorizationMachine(c, device="cuda", dist=rccl_ctx)
+    assert dm._exchange.nparts == mb
+    for i, b in enumerate(batches):
+        l1 = loc.train_step(b).mean_loss()
+        l2 = dm.train_step(b, batches[i + 1] if i + 1 < len(batches) else None).mean_loss()
+        assert abs(l1 - l2) <= 1e-5 * max(1.0, abs(l1))
+    torch.cuda.synchronize()
+    torch.testing.assert_close(dm.table.reference_rows(), loc.table.reference_rows(), rtol=1e-5, atol=1e-6)
+    ev = gen.batch(512)
+    torch.testing.assert_close(dm.predict(ev), loc.predict(ev), rtol=1e-5, atol=1e-6)

@@ -33,23 +33,25 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _cfg(mode, grad_reduce, bcfg):
+def _cfg(mode, grad_reduce, bcfg, mb=0):
     return FMConfig(vocabulary_size=V, factor_num=KF, loss_type="logistic", factor_lambda=0.05, bias_lambda=0.02,
                     batch_size=bcfg, init_value_range=0.1, seed=11, mode=mode, grad_reduce=grad_reduce,
-                    opt=K.OptConfig("adagrad", lr=0.1, initial_accumulator=0.1), threads=1)
+                    opt=K.OptConfig("adagrad", lr=0.1, initial_accumulator=0.1), threads=1, microbatches=mb)
 
 
 def _batch(step, rank):
     return random_batch(B, V, max_feats=10, seed=1000 * step + rank)
 
 
-def _worker(rank, world, port, mode, grad_reduce, out_dir):
+def _worker(rank, world, port, mode, grad_reduce, out_dir, mb=0):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     from fast_tffm_amd.parallel import dist as fmdist
 
     ctx = fmdist.init_distributed(backend="gloo", rank=rank, world=world, device="cpu")
-    m = FactorizationMachine(_cfg(mode, grad_reduce, 16), device="cpu", dist=ctx)
+    m = FactorizationMachine(_cfg(mode, grad_reduce, 16, mb), device="cpu", dist=ctx)
+    if mode == "shard":
+        assert m._exchange.nparts == max(1, mb)
     bs = [_batch(s, rank) for s in range(STEPS)]
     # shard mode also exercises the lookahead plan (next batch's dedup + id exchange built early)
     losses = [m.train_step(bs[s], bs[s + 1] if s + 1 < STEPS and mode == "shard" else None).mean_loss()
@@ -61,9 +63,9 @@ def _worker(rank, world, port, mode, grad_reduce, out_dir):
     fmdist.shutdown()
 
 
-def _run_world(tmp_path, mode, grad_reduce):
+def _run_world(tmp_path, mode, grad_reduce, mb=0):
     port = _free_port()
-    mp.spawn(_worker, args=(WORLD, port, mode, grad_reduce, str(tmp_path)), nprocs=WORLD, join=True)
+    mp.spawn(_worker, args=(WORLD, port, mode, grad_reduce, str(tmp_path), mb), nprocs=WORLD, join=True)
     return [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(WORLD)]
 
 
@@ -97,10 +99,11 @@ def _assemble(res):
     return rows
 
 
-@pytest.mark.parametrize("mode,grad_reduce", [("shard", "mean"), ("shard", "sum"), ("dp", "mean"),
-                                              ("dp_dense", "mean")])
-def test_multi_rank_equals_single_process(tmp_path, mode, grad_reduce):
-    res = _run_world(tmp_path, mode, grad_reduce)
+@pytest.mark.parametrize("mode,grad_reduce,mb", [("shard", "mean", 0), ("shard", "sum", 0), ("shard", "mean", 2),
+                                                 ("shard", "sum", 3), ("dp", "mean", 0), ("dp_dense", "mean", 0)])
+def test_multi_rank_equals_single_process(tmp_path, mode, grad_reduce, mb):
+    """shard: one part (default), 2 and 3 micro-batch parts."""
+    res = _run_world(tmp_path, mode, grad_reduce, mb)
     ref = _single(grad_reduce)
     ref_rows = ref.table.reference_rows()
     if mode == "shard":
@@ -114,7 +117,7 @@ def test_multi_rank_equals_single_process(tmp_path, mode, grad_reduce):
     for rank, r in enumerate(res):
         torch.testing.assert_close(r["pred"], ref.predict(_batch(99, rank)), rtol=1e-5, atol=1e-6)
 
-    if mode == "shard" and grad_reduce == "mean":
+    if mode == "shard" and grad_reduce == "mean" and mb == 0:
         # re-shard: 2-shard checkpoint -> 1-process table
         m1 = FactorizationMachine(_cfg("local", "sum", 16), device="cpu")
         meta = ckpt.restore_checkpoint(m1, ckpt.latest_checkpoint(str(tmp_path / "log")))
