@@ -1,0 +1,91 @@
+// Native training-data loader: files -> shuffled lines -> parsed CSR batches.
+//
+// Replaces the reference's TF input pipeline (tffm/fm_model.py:34-126):
+// string_input_producer(train_files, num_epochs, shuffle=True) ->
+// TextLineReader.read_up_to -> shuffle_batch(capacity = 4.5 B,
+// min_after_dequeue = 3 B, allow_smaller_final_batch) -> FmParser, run by
+// `shuffle_threads` QueueRunner threads into a FIFOQueue(queue_size).
+//
+// Here one producer thread owns the whole host pipeline:
+//  * files are mmap'ed (no copy, no per-line objects); weight files are paired
+//    with data files by index and checked line-for-line;
+//  * per epoch the file order is shuffled with a (seed, epoch)-seeded RNG; with
+//    world > 1 rank r takes files r, r+W, ... (or every W-th line when there are
+//    fewer files than ranks);
+//  * lines enter a shuffle window of 4.5 B spans; once it is full a batch of B
+//    random spans is drawn (partial Fisher-Yates, O(B)); the epoch's tail is
+//    drained in batches of <= B (allow_smaller_final_batch);
+//  * each batch is parsed by the multi-threaded libsvm parser (parser.h) into
+//    CSR with int32 ids / offsets and queued (bounded by queue_size);
+//  * the consumer (Python, GIL released while waiting) takes batches in order.
+// A (start_epoch, skip_batches) position resumes exactly where a checkpoint
+// was taken: the RNGs are re-seeded per epoch, skipped batches are not parsed.
+#pragma once
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "parser.h"
+
+namespace fm {
+
+struct LoaderOptions {
+  std::vector<std::string> files;
+  std::vector<std::string> weight_files;  // empty, or one per data file
+  int64_t batch_size = 1;
+  int64_t vocab_size = 1;
+  bool hash_feature_id = false;
+  bool shuffle = true;
+  int num_epochs = 1;
+  uint64_t seed = 0;
+  int threads = 4;            // parser threads per batch
+  int rank = 0, world = 1;
+  int queue_size = 4;         // parsed batches buffered ahead of the consumer
+  int start_epoch = 0;
+  int64_t skip_batches = 0;   // batches of start_epoch already consumed
+  double capacity_factor = 4.5;
+};
+
+struct LoadedBatch {
+  std::vector<float> labels;
+  std::vector<int32_t> offsets;   // [B+1]
+  std::vector<int32_t> ids;       // [nnz]
+  std::vector<float> vals;        // [nnz], empty when every value is 1
+  std::vector<float> weights;     // [B], empty without weight files
+  int max_feats = 0;
+  int epoch = 0;
+  int64_t count = 0;              // batches of this epoch consumed after this one
+};
+
+class TextLoader {
+ public:
+  explicit TextLoader(LoaderOptions o);
+  ~TextLoader();
+  TextLoader(const TextLoader&) = delete;
+  TextLoader& operator=(const TextLoader&) = delete;
+
+  // Next batch in order; false once every epoch is exhausted.  Rethrows a
+  // producer failure (ParseError for malformed input, runtime_error for I/O).
+  bool next(LoadedBatch& out);
+  size_t queued();
+  void close();
+
+ private:
+  void run();
+  bool push(LoadedBatch&& b);
+
+  LoaderOptions o_;
+  std::thread th_;
+  std::mutex mu_;
+  std::condition_variable cv_put_, cv_get_;
+  std::deque<LoadedBatch> q_;
+  bool done_ = false, stop_ = false;
+  bool failed_ = false, parse_error_ = false;
+  std::string error_;
+};
+
+}  // namespace fm

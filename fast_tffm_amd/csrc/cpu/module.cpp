@@ -11,6 +11,7 @@
 
 #include "../hash64.h"
 #include "kernels.h"
+#include "loader.h"
 #include "parser.h"
 
 namespace py = pybind11;
@@ -185,6 +186,44 @@ PYBIND11_MODULE(_fm_cpu, m) {
         return csr_to_py(std::move(b));
       },
       py::arg("buffer"), py::arg("vocab_size"), py::arg("hash_feature_id") = false, py::arg("threads") = 1);
+
+  // Native training-data loader (loader.h): mmap'ed files -> shuffle window -> parsed CSR batches.
+  py::class_<fm::TextLoader>(m, "TextLoader")
+      .def(py::init([](std::vector<std::string> files, std::vector<std::string> weight_files, long long batch_size,
+                       long long vocab_size, bool hash_feature_id, bool shuffle, int num_epochs,
+                       unsigned long long seed, int threads, int rank, int world, int queue_size, int start_epoch,
+                       long long skip_batches) {
+             fm::LoaderOptions o;
+             o.files = std::move(files); o.weight_files = std::move(weight_files); o.batch_size = batch_size;
+             o.vocab_size = vocab_size; o.hash_feature_id = hash_feature_id; o.shuffle = shuffle;
+             o.num_epochs = num_epochs; o.seed = seed; o.threads = threads; o.rank = rank; o.world = world;
+             o.queue_size = queue_size; o.start_epoch = start_epoch; o.skip_batches = skip_batches;
+             return new fm::TextLoader(std::move(o));
+           }),
+           py::arg("files"), py::arg("weight_files"), py::arg("batch_size"), py::arg("vocab_size"),
+           py::arg("hash_feature_id") = false, py::arg("shuffle") = true, py::arg("num_epochs") = 1,
+           py::arg("seed") = 0, py::arg("threads") = 4, py::arg("rank") = 0, py::arg("world") = 1,
+           py::arg("queue_size") = 4, py::arg("start_epoch") = 0, py::arg("skip_batches") = 0)
+      // -> (labels, offsets, ids, vals | None, weights | None, max_feats, epoch, count) or None at the end
+      .def("next",
+           [](fm::TextLoader& L) -> py::object {
+             fm::LoadedBatch b;
+             bool ok;
+             {
+               py::gil_scoped_release nogil;
+               ok = L.next(b);
+             }
+             if (!ok) return py::none();
+             py::object vals = b.vals.empty() ? py::object(py::none()) : py::object(to_numpy(std::move(b.vals)));
+             py::object w = b.weights.empty() ? py::object(py::none()) : py::object(to_numpy(std::move(b.weights)));
+             return py::make_tuple(to_numpy(std::move(b.labels)), to_numpy(std::move(b.offsets)),
+                                   to_numpy(std::move(b.ids)), vals, w, b.max_feats, b.epoch, b.count);
+           })
+      .def("queued", &fm::TextLoader::queued)
+      .def("close", [](fm::TextLoader& L) {
+        py::gil_scoped_release nogil;
+        L.close();
+      });
 
   m.def(
       "parse_floats",

@@ -105,7 +105,7 @@ void parse_line(const char* s, size_t len, int64_t vocab_size, bool hash_feature
 }
 
 void parse_lines(const char* const* ptrs, const size_t* lens, size_t n, int64_t vocab_size,
-                 bool hash_feature_id, int threads, CsrBatch& out) {
+                 bool hash_feature_id, int threads, CsrBatch& out, ParseWorkspace* ws) {
   out.labels.clear(); out.sizes.clear(); out.ids.clear(); out.vals.clear();
   if (n == 0) return;
   if (threads < 1) threads = 1;
@@ -117,40 +117,62 @@ void parse_lines(const char* const* ptrs, const size_t* lens, size_t n, int64_t 
     for (size_t i = 0; i < n; ++i) parse_line(ptrs[i], lens[i], vocab_size, hash_feature_id, out, scratch);
     return;
   }
-  std::vector<CsrBatch> parts(nt);
+  ParseWorkspace local;
+  if (!ws) ws = &local;
+  if (ws->parts.size() < nt) ws->parts.resize(nt);
+  std::vector<CsrBatch>& parts = ws->parts;
   std::vector<std::string> errors(nt);
   std::vector<size_t> err_line(nt, SIZE_MAX);
-  std::vector<std::thread> pool;
   const size_t per = (n + nt - 1) / nt;
-  for (size_t t = 0; t < nt; ++t) {
-    pool.emplace_back([&, t]() {
-      const size_t b = t * per, e = std::min(n, b + per);
-      std::string scratch;
-      CsrBatch& o = parts[t];
-      o.labels.reserve(e - b); o.sizes.reserve(e - b);
-      for (size_t i = b; i < e; ++i) {
-        try {
-          parse_line(ptrs[i], lens[i], vocab_size, hash_feature_id, o, scratch);
-        } catch (const ParseError& ex) {
-          errors[t] = ex.what();
-          err_line[t] = i;
-          return;
+  // phase 1: every thread parses its contiguous line range into private vectors
+  {
+    std::vector<std::thread> pool;
+    for (size_t t = 0; t < nt; ++t) {
+      pool.emplace_back([&, t]() {
+        const size_t b = t * per, e = std::min(n, b + per);
+        std::string scratch;
+        CsrBatch& o = parts[t];
+        o.labels.clear(); o.sizes.clear(); o.ids.clear(); o.vals.clear();
+        o.labels.reserve(e - b); o.sizes.reserve(e - b);
+        size_t bytes = 0;
+        for (size_t i = b; i < e; ++i) bytes += lens[i];
+        o.ids.reserve(bytes / 6 + 16); o.vals.reserve(bytes / 6 + 16);  // ~one token per 6+ bytes
+        for (size_t i = b; i < e; ++i) {
+          try {
+            parse_line(ptrs[i], lens[i], vocab_size, hash_feature_id, o, scratch);
+          } catch (const ParseError& ex) {
+            errors[t] = ex.what();
+            err_line[t] = i;
+            return;
+          }
         }
-      }
-    });
+      });
+    }
+    for (auto& th : pool) th.join();
   }
-  for (auto& th : pool) th.join();
   // report the first failing line in input order (same as a sequential parse)
   for (size_t t = 0; t < nt; ++t)
     if (err_line[t] != SIZE_MAX) throw ParseError(errors[t]);
-  size_t nnz = 0;
-  for (auto& pt : parts) nnz += pt.ids.size();
-  out.labels.reserve(n); out.sizes.reserve(n); out.ids.reserve(nnz); out.vals.reserve(nnz);
-  for (auto& pt : parts) {
-    out.labels.insert(out.labels.end(), pt.labels.begin(), pt.labels.end());
-    out.sizes.insert(out.sizes.end(), pt.sizes.begin(), pt.sizes.end());
-    out.ids.insert(out.ids.end(), pt.ids.begin(), pt.ids.end());
-    out.vals.insert(out.vals.end(), pt.vals.begin(), pt.vals.end());
+  // phase 2: size the outputs once, every thread copies its piece into place
+  std::vector<size_t> nz_off(nt + 1, 0), ln_off(nt + 1, 0);
+  for (size_t t = 0; t < nt; ++t) {
+    nz_off[t + 1] = nz_off[t] + parts[t].ids.size();
+    ln_off[t + 1] = ln_off[t] + parts[t].labels.size();
+  }
+  out.labels.resize(ln_off[nt]); out.sizes.resize(ln_off[nt]);
+  out.ids.resize(nz_off[nt]); out.vals.resize(nz_off[nt]);
+  {
+    std::vector<std::thread> pool;
+    for (size_t t = 0; t < nt; ++t) {
+      pool.emplace_back([&, t]() {
+        CsrBatch& pt = parts[t];
+        std::copy(pt.labels.begin(), pt.labels.end(), out.labels.begin() + ln_off[t]);
+        std::copy(pt.sizes.begin(), pt.sizes.end(), out.sizes.begin() + ln_off[t]);
+        std::copy(pt.ids.begin(), pt.ids.end(), out.ids.begin() + nz_off[t]);
+        std::copy(pt.vals.begin(), pt.vals.end(), out.vals.begin() + nz_off[t]);
+      });
+    }
+    for (auto& th : pool) th.join();
   }
 }
 

@@ -39,9 +39,15 @@ struct CsrBatch {
 void parse_line(const char* s, size_t len, int64_t vocab_size, bool hash_feature_id, CsrBatch& out,
                 std::string& scratch);
 
+// Per-thread scratch of parse_lines, reusable across calls (a long-lived caller,
+// e.g. the loader, keeps it so the pieces' memory stays mapped: no page faults).
+struct ParseWorkspace {
+  std::vector<CsrBatch> parts;
+};
+
 // Parse `n` lines given as (pointer, length) spans with up to `threads` threads.
 void parse_lines(const char* const* ptrs, const size_t* lens, size_t n, int64_t vocab_size,
-                 bool hash_feature_id, int threads, CsrBatch& out);
+                 bool hash_feature_id, int threads, CsrBatch& out, ParseWorkspace* ws = nullptr);
 
 // Parse one float per line (weight files; tf.string_to_number semantics:
 // the whole line must be a number, surrounding whitespace allowed).

@@ -157,6 +157,57 @@ class TextBatchReader:
         self.state.epoch = self.num_epochs
 
 
+class NativeTextReader:
+    """The training-batch iterator backed by the native loader (csrc/cpu/loader.h).
+
+    Same contract as ``TextBatchReader`` (epochs, per-epoch file shuffle, 4.5 B
+    shuffle window, per-rank file / line sharding, weight-file pairing, exact
+    resume from ``ReaderState``), but the whole host pipeline -- mmap'ed file
+    reading, line splitting, the shuffle window, multi-threaded parsing and CSR
+    assembly (int32 offsets and ids) -- runs in a C++ producer thread that
+    keeps ``queue_size`` batches ready; Python only wraps the arrays.
+    The batch composition (RNG streams) differs from ``TextBatchReader``.
+    """
+
+    def __init__(self, files: list[str], weight_files: list[str] | None, batch_size: int, *, vocab_size: int,
+                 hash_feature_id: bool = False, num_epochs: int = 1, shuffle: bool = True, seed: int = 0,
+                 parse_threads: int = 4, rank: int = 0, world: int = 1, state: ReaderState | None = None,
+                 queue_size: int = 4):
+        if weight_files and len(weight_files) != len(files):
+            raise ValueError("The numbers of train files and weight files do not match.")
+        self.args = dict(files=list(files), weight_files=list(weight_files or []), batch_size=int(batch_size),
+                         vocab_size=int(vocab_size), hash_feature_id=bool(hash_feature_id), shuffle=bool(shuffle),
+                         num_epochs=int(num_epochs), seed=int(seed), threads=int(parse_threads), rank=int(rank),
+                         world=int(world), queue_size=max(1, int(queue_size)))
+        self.state = state or ReaderState()
+        self.num_epochs = num_epochs
+        self._loader = None
+
+    def queued(self) -> int:
+        return self._loader.queued() if self._loader is not None else 0
+
+    def __iter__(self):
+        L = native.cpu().TextLoader(start_epoch=self.state.epoch, skip_batches=self.state.batches_in_epoch,
+                                    **self.args)
+        self._loader = L
+        try:
+            while True:
+                item = L.next()
+                if item is None:
+                    break
+                labels, offsets, ids, vals, weights, max_feats, epoch, count = item
+                b = Batch(torch.from_numpy(labels), torch.from_numpy(offsets), torch.from_numpy(ids),
+                          None if vals is None else torch.from_numpy(vals),
+                          None if weights is None else torch.from_numpy(weights), int(offsets[-1]),
+                          max_feats=int(max_feats))
+                self.state.epoch, self.state.batches_in_epoch = int(epoch), int(count)
+                b.reader_pos = (int(epoch), int(count))
+                yield b
+            self.state.epoch, self.state.batches_in_epoch = self.num_epochs, 0
+        finally:
+            L.close()
+
+
 class Prefetcher:
     """Background producer threads + bounded queue + pinned H2D on a side stream.
 

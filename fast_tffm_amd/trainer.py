@@ -29,7 +29,7 @@ import torch.distributed as dist
 from .config import FMRunConfig
 from .utils.fault import maybe_inject
 from .utils.trace import roctx_range
-from .data.reader import Prefetcher, ReaderState, TextBatchReader, load_file_batch
+from .data.reader import NativeTextReader, Prefetcher, ReaderState, TextBatchReader, load_file_batch
 from .models.fm import FactorizationMachine
 from .parallel.dist import DistContext
 from .utils import checkpoint as ckpt
@@ -117,10 +117,11 @@ class Trainer:
         c = self.cfg
         self.restore()
         vb = self.load_validation()
-        reader = TextBatchReader(c.train_files, c.weight_files or None, c.batch_size, vocab_size=c.vocabulary_size,
-                                 hash_feature_id=c.hash_feature_id, num_epochs=c.num_epochs, shuffle=c.shuffle,
-                                 seed=c.seed, parse_threads=c.parse_threads, rank=self.rank, world=self.world,
-                                 state=ReaderState(self.reader_state.epoch, self.reader_state.batches_in_epoch))
+        Reader = NativeTextReader if c.loader == "native" else TextBatchReader
+        reader = Reader(c.train_files, c.weight_files or None, c.batch_size, vocab_size=c.vocabulary_size,
+                        hash_feature_id=c.hash_feature_id, num_epochs=c.num_epochs, shuffle=c.shuffle,
+                        seed=c.seed, parse_threads=c.parse_threads, rank=self.rank, world=self.world,
+                        state=ReaderState(self.reader_state.epoch, self.reader_state.batches_in_epoch))
         pf = Prefetcher(reader, self.device, queue_size=max(1, min(c.queue_size, 64)))
         metrics = MetricsLogger(c.log_dir if self.rank == 0 else None, every=c.save_summaries_steps)
         self.print("========", "train", "========")
