@@ -20,7 +20,7 @@ Extensions (new keys, all optional):
                 global_bias = true|false (learned b0; its gradient is all-reduced over ranks),
                 dtype = fp32|bf16|fp8 (fp8: OCP e4m3 + per-row scale, GPU)
   [Train]       optimizer = adagrad|ftrl|sgd, ftrl.l1, ftrl.l2, ftrl.beta,
-                ftrl.initial_accumulator, parse_threads, loader = native|python, shuffle = true|false,
+                ftrl.initial_accumulator, parse_threads, loader = native|python, gpu_parse = true|false, shuffle = true|false,
                 max_steps, dedup_chunk, log_steps
   [Distributed] mode = auto|local|shard|dp|dp_dense, grad_reduce = sum|mean,
                 comm_dtype = auto|fp32|bf16 (row-sharded wire rows; auto = table storage dtype),
@@ -90,6 +90,7 @@ class FMRunConfig:
     ftrl_initial_accumulator: float = 0.1
     parse_threads: int = 4
     loader: str = "native"      # native (C++ loader thread) | python
+    gpu_parse: bool = False     # native loader: tokenize on the GPU (hip/parse.hip)
     shuffle: bool = True
     max_steps: int | None = None
     dedup_chunk: int = 32
@@ -189,6 +190,7 @@ def load_config(config_file: str, *, echo: bool = True, printer=print) -> FMRunC
     c.ftrl_initial_accumulator = opt(TRAIN, "ftrl.initial_accumulator", float, c.ftrl_initial_accumulator)
     c.parse_threads = opt(TRAIN, "parse_threads", int, c.parse_threads)
     c.loader = opt(TRAIN, "loader", lambda s: s.strip().lower(), c.loader)
+    c.gpu_parse = opt(TRAIN, "gpu_parse", lambda s: s.strip().lower() == "true", c.gpu_parse)
     if c.loader not in ("native", "python"):
         raise ConfigError(f"[Train] loader must be native or python, got {c.loader}")
     c.shuffle = opt(TRAIN, "shuffle", to_bool, c.shuffle)

@@ -188,6 +188,27 @@ void TextLoader::run() {
         }
         if (count <= skip) return true;
         LoadedBatch b;
+        if (o_.raw) {
+          size_t total = 0;
+          for (size_t i = 0; i < n; ++i) total += lens[i] + 1;
+          b.bytes.resize(total);
+          b.line_start.resize(n + 1);
+          size_t off = 0;
+          for (size_t i = 0; i < n; ++i) {
+            b.line_start[i] = static_cast<int64_t>(off);
+            std::memcpy(b.bytes.data() + off, ptrs[i], lens[i]);
+            off += lens[i];
+            b.bytes[off++] = '\n';
+          }
+          b.line_start[n] = static_cast<int64_t>(off);
+          if (weighted) {
+            b.weights.resize(n);
+            parse_floats(wptrs.data(), wlens.data(), n, b.weights.data());
+          }
+          b.epoch = epoch;
+          b.count = count;
+          return push(std::move(b));
+        }
         parse_lines(ptrs.data(), lens.data(), ptrs.size(), o_.vocab_size, o_.hash_feature_id, o_.threads, csr,
                     &pws);
         const size_t nb = csr.labels.size(), nnz = csr.ids.size();

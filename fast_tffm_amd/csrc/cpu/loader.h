@@ -18,6 +18,9 @@
 //  * each batch is parsed by the multi-threaded libsvm parser (parser.h) into
 //    CSR with int32 ids / offsets and queued (bounded by queue_size);
 //  * the consumer (Python, GIL released while waiting) takes batches in order.
+//  * raw mode (GPU tokenizer, hip/parse.hip): instead of parsing, the chosen
+//    lines are gathered into one '\n'-separated buffer + line offsets that the
+//    consumer copies to the device and tokenizes there.
 // A (start_epoch, skip_batches) position resumes exactly where a checkpoint
 // was taken: the RNGs are re-seeded per epoch, skipped batches are not parsed.
 #pragma once
@@ -48,6 +51,7 @@ struct LoaderOptions {
   int start_epoch = 0;
   int64_t skip_batches = 0;   // batches of start_epoch already consumed
   double capacity_factor = 4.5;
+  bool raw = false;           // emit the batch's line bytes (GPU tokenizer) instead of parsed CSR
 };
 
 struct LoadedBatch {
@@ -56,6 +60,9 @@ struct LoadedBatch {
   std::vector<int32_t> ids;       // [nnz]
   std::vector<float> vals;        // [nnz], empty when every value is 1
   std::vector<float> weights;     // [B], empty without weight files
+  // raw mode: the batch's lines, each '\n'-terminated, and their start offsets [B+1]
+  std::vector<uint8_t> bytes;
+  std::vector<int64_t> line_start;
   int max_feats = 0;
   int epoch = 0;
   int64_t count = 0;              // batches of this epoch consumed after this one

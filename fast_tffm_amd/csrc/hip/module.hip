@@ -25,6 +25,7 @@ using u64 = std::uintptr_t;
 #include "dedup.hip"
 #include "shard.hip"
 #include "init.hip"
+#include "parse.hip"
 
 namespace {
 
@@ -246,6 +247,21 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
         check(fm::launch_shard_keys(n, P<const int>(ids), W, Rps, P<int>(keys), S(stream)), "shard_keys");
       },
       py::arg("n"), py::arg("ids"), py::arg("W"), py::arg("Rps"), py::arg("keys"), py::arg("stream"));
+
+  m.def("parse_workspace_bytes", &fm::parse_workspace_bytes, py::arg("n"));
+  m.def(
+      "parse",
+      [](u64 buf, u64 line_start, int n, long long vocab, int hash, u64 counts, u64 offsets, u64 labels, u64 ids,
+         u64 vals, u64 status, u64 ws, long long ws_bytes, u64 stream) {
+        fm::ParseArgs a{};
+        a.buf = P<const char>(buf); a.line_start = P<const long long>(line_start); a.n = n; a.vocab = vocab;
+        a.hash = hash; a.counts = P<int>(counts); a.labels = P<float>(labels); a.ids = P<int>(ids);
+        a.vals = P<float>(vals); a.status = P<int>(status);
+        check(fm::launch_parse(a, P<void>(ws), (size_t)ws_bytes, P<int>(offsets), S(stream)), "parse");
+      },
+      py::arg("buf"), py::arg("line_start"), py::arg("n"), py::arg("vocab"), py::arg("hash"), py::arg("counts"),
+      py::arg("offsets"), py::arg("labels"), py::arg("ids"), py::arg("vals"), py::arg("status"), py::arg("ws"),
+      py::arg("ws_bytes"), py::arg("stream"));
 
   m.def(
       "csr_rows",

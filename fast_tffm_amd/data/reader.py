@@ -172,7 +172,7 @@ class NativeTextReader:
     def __init__(self, files: list[str], weight_files: list[str] | None, batch_size: int, *, vocab_size: int,
                  hash_feature_id: bool = False, num_epochs: int = 1, shuffle: bool = True, seed: int = 0,
                  parse_threads: int = 4, rank: int = 0, world: int = 1, state: ReaderState | None = None,
-                 queue_size: int = 4):
+                 queue_size: int = 4, gpu_parse: torch.device | str | None = None):
         if weight_files and len(weight_files) != len(files):
             raise ValueError("The numbers of train files and weight files do not match.")
         self.args = dict(files=list(files), weight_files=list(weight_files or []), batch_size=int(batch_size),
@@ -182,19 +182,33 @@ class NativeTextReader:
         self.state = state or ReaderState()
         self.num_epochs = num_epochs
         self._loader = None
+        # gpu_parse: the loader ships raw line bytes and the GPU tokenizer (hip/parse.hip) builds
+        # the CSR on this device; yielded batches then live on the device, ready to use
+        self.gpu = torch.device(gpu_parse) if gpu_parse is not None else None
+        if self.gpu is not None and self.gpu.type != "cuda":
+            self.gpu = None
+        self.fallbacks = 0
 
     def queued(self) -> int:
         return self._loader.queued() if self._loader is not None else 0
 
     def __iter__(self):
         L = native.cpu().TextLoader(start_epoch=self.state.epoch, skip_batches=self.state.batches_in_epoch,
-                                    **self.args)
+                                    raw=self.gpu is not None, **self.args)
         self._loader = L
+        stream = torch.cuda.Stream(self.gpu) if self.gpu is not None else None
         try:
             while True:
                 item = L.next()
                 if item is None:
                     break
+                if self.gpu is not None:
+                    buf, line_start, weights, epoch, count = item
+                    b = self._gpu_batch(buf, line_start, weights, stream)
+                    self.state.epoch, self.state.batches_in_epoch = int(epoch), int(count)
+                    b.reader_pos = (int(epoch), int(count))
+                    yield b
+                    continue
                 labels, offsets, ids, vals, weights, max_feats, epoch, count = item
                 b = Batch(torch.from_numpy(labels), torch.from_numpy(offsets), torch.from_numpy(ids),
                           None if vals is None else torch.from_numpy(vals),
@@ -206,6 +220,31 @@ class NativeTextReader:
             self.state.epoch, self.state.batches_in_epoch = self.num_epochs, 0
         finally:
             L.close()
+
+    def _gpu_batch(self, buf: np.ndarray, line_start: np.ndarray, weights, stream) -> Batch:
+        """H2D of the raw lines + GPU tokenizer on ``stream`` (CPU parser when the batch has syntax
+        outside the GPU subset or errors); returns a device batch whose work has completed."""
+        from ..ops import kernels as K
+
+        dev = self.gpu
+        with torch.cuda.stream(stream):
+            hb = torch.from_numpy(buf).pin_memory()
+            hl = torch.from_numpy(line_start).pin_memory()
+            db = hb.to(dev, non_blocking=True)
+            dl = hl.to(dev, non_blocking=True)
+            pg = K.parse_gpu(db, dl, self.args["vocab_size"], self.args["hash_feature_id"], stream=stream)
+            w = None if weights is None else torch.from_numpy(weights).to(dev, non_blocking=True)
+            if pg.fallback:
+                self.fallbacks += 1
+                labels, sizes, ids, vals = native.cpu().parse_buffer(buf, self.args["vocab_size"],
+                                                                     self.args["hash_feature_id"],
+                                                                     self.args["threads"])
+                b = Batch.from_parsed(labels, sizes, ids, vals).to(dev)
+                b.weights = w
+            else:
+                b = Batch(pg.labels, pg.offsets, pg.ids, pg.vals, w, pg.nnz, max_feats=pg.max_feats)
+            stream.synchronize()
+        return b
 
 
 class Prefetcher:
@@ -233,7 +272,9 @@ class Prefetcher:
             for b in self.reader:
                 if self._stop.is_set():
                     return
-                if self._stream is not None:
+                if b.ids.device.type == "cuda":
+                    self.q.put((b, "device", None))   # tokenized on the GPU, already complete
+                elif self._stream is not None:
                     b = b.pin_memory()
                     with torch.cuda.stream(self._stream):
                         db = b.to(self.device, non_blocking=True)
@@ -257,7 +298,13 @@ class Prefetcher:
                 if self._err is not None:
                     raise self._err
                 return
-            if ev is not None:
+            if ev == "device":
+                # produced on the reader's stream (synchronised): the compute stream uses it from now on
+                cur = torch.cuda.current_stream(self.device)
+                for t in (item.labels, item.offsets, item.ids, item.vals, item.weights):
+                    if t is not None:
+                        t.record_stream(cur)
+            elif ev is not None:
                 cur = torch.cuda.current_stream(self.device)
                 cur.wait_event(ev)
                 # the batch was allocated on the side stream: tell the caching allocator

@@ -701,3 +701,50 @@ def gather_wire(req: torch.Tensor, table: TableState, fmt: WireFormat, out: torc
                              scaled=int(v.dtype == FP8), to_bf16=int(to_bf16), out=_p(out), rb=fmt.rb, vb=fmt.vb,
                              stream=_stream(req))
     return out
+
+
+# ---------------------------------------------------------------------------
+# GPU libsvm tokenizer (hip/parse.hip)
+# ---------------------------------------------------------------------------
+@dataclass
+class ParsedGpu:
+    labels: torch.Tensor     # [n] f32
+    offsets: torch.Tensor    # [n+1] i32
+    ids: torch.Tensor        # [nnz] i32
+    vals: torch.Tensor | None  # [nnz] f32, None when every value is 1
+    nnz: int
+    max_feats: int
+    fallback: bool           # syntax outside the GPU subset (or an error): re-parse on the CPU
+
+
+def parse_gpu(buf: torch.Tensor, line_start: torch.Tensor, vocab_size: int, hash_feature_id: bool = False,
+              stream: torch.cuda.Stream | None = None) -> ParsedGpu:
+    """Tokenize n '\\n'-terminated libsvm lines (``buf`` uint8 on the GPU, line ``i`` =
+    ``buf[line_start[i]:line_start[i+1]]``) into CSR on the device.
+
+    Synchronises ``stream`` (the caller's side stream) once to read nnz and the
+    fallback flag; when ``fallback`` is set the outputs are incomplete and the
+    caller must parse the lines with the CPU parser (exact reference semantics
+    and error messages)."""
+    _check(_is_gpu(buf) and buf.dtype == torch.uint8 and buf.is_contiguous(), "buf: uint8 GPU bytes")
+    _check(line_start.dtype == torch.int64 and line_start.device == buf.device, "line_start: int64 on buf's device")
+    n = line_start.numel() - 1
+    dev = buf.device
+    st = stream or torch.cuda.current_stream(dev)
+    h = native.hip()
+    cap = buf.numel() // 2 + n + 1          # a token takes >= 2 bytes (separator + 1 char)
+    i32 = dict(dtype=torch.int32, device=dev)
+    counts = torch.empty(n + 1, **i32)
+    offsets = torch.empty(n + 1, **i32)
+    labels = torch.empty(n, dtype=torch.float32, device=dev)
+    ids = torch.empty(cap, **i32)
+    vals = torch.empty(cap, dtype=torch.float32, device=dev)
+    status = torch.empty(4, **i32)
+    wsb = h.parse_workspace_bytes(max(n, 1))
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+    h.parse(buf=_p(buf), line_start=_p(line_start), n=n, vocab=int(vocab_size), hash=int(bool(hash_feature_id)),
+            counts=_p(counts), offsets=_p(offsets), labels=_p(labels), ids=_p(ids), vals=_p(vals),
+            status=_p(status), ws=_p(ws), ws_bytes=wsb, stream=st.cuda_stream)
+    info = torch.cat([status, offsets[n:]]).cpu()   # one D2H: (fallback, max_feats, non-unit, -, nnz)
+    fb, mf, nonunit, nnz = int(info[0]), int(info[1]), int(info[2]), int(info[4])
+    return ParsedGpu(labels, offsets, ids[:nnz], vals[:nnz] if nonunit else None, nnz, mf, bool(fb))

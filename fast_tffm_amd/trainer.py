@@ -117,11 +117,14 @@ class Trainer:
         c = self.cfg
         self.restore()
         vb = self.load_validation()
-        Reader = NativeTextReader if c.loader == "native" else TextBatchReader
-        reader = Reader(c.train_files, c.weight_files or None, c.batch_size, vocab_size=c.vocabulary_size,
-                        hash_feature_id=c.hash_feature_id, num_epochs=c.num_epochs, shuffle=c.shuffle,
-                        seed=c.seed, parse_threads=c.parse_threads, rank=self.rank, world=self.world,
-                        state=ReaderState(self.reader_state.epoch, self.reader_state.batches_in_epoch))
+        kw = dict(vocab_size=c.vocabulary_size, hash_feature_id=c.hash_feature_id, num_epochs=c.num_epochs,
+                  shuffle=c.shuffle, seed=c.seed, parse_threads=c.parse_threads, rank=self.rank, world=self.world,
+                  state=ReaderState(self.reader_state.epoch, self.reader_state.batches_in_epoch))
+        if c.loader == "native":
+            reader = NativeTextReader(c.train_files, c.weight_files or None, c.batch_size,
+                                      gpu_parse=self.device if c.gpu_parse else None, **kw)
+        else:
+            reader = TextBatchReader(c.train_files, c.weight_files or None, c.batch_size, **kw)
         pf = Prefetcher(reader, self.device, queue_size=max(1, min(c.queue_size, 64)))
         metrics = MetricsLogger(c.log_dir if self.rank == 0 else None, every=c.save_summaries_steps)
         self.print("========", "train", "========")
