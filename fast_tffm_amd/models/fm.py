@@ -34,6 +34,15 @@ from ..utils.trace import roctx_range
 from .table import FMTable, bits_for, rows_per_shard
 
 
+def side_stream_priority() -> int:
+    """HIP priority of the lookahead / plan streams (FM_SIDE_PRIORITY: 0 = normal, -1 = high).
+
+    The next batch's dedup (+ the sharded plan's owner counts) runs beside this
+    step's forward/backward; a high-priority queue lets its small, dependent
+    kernels through instead of queueing behind the compute stream's workgroups."""
+    return int(os.environ.get("FM_SIDE_PRIORITY", "0"))
+
+
 @dataclass
 class FMConfig:
     vocabulary_size: int
@@ -373,7 +382,7 @@ class FactorizationMachine:
 
     def _side_stream(self):
         if self._side is None:
-            self._side = torch.cuda.Stream(self.device)
+            self._side = torch.cuda.Stream(self.device, priority=side_stream_priority())
         return self._side
 
     def _local_train_step(self, b: Batch) -> StepOut:

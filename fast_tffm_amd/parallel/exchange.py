@@ -29,6 +29,7 @@ meant for small vocabularies (BASELINE config 3).
 
 from __future__ import annotations
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -118,11 +119,9 @@ class _PlanSlot:
         if self.run_off is None or self.run_off.numel() < n + 1:
             self.run_off_h = torch.empty(n + 1, dtype=torch.int32, pin_memory=True)
             self.run_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
-        acc = 0
-        self.run_off_h[0] = 0
-        for q, c in enumerate(splits):
-            acc += c
-            self.run_off_h[q + 1] = acc
+        h = self.run_off_h.numpy()
+        h[0] = 0
+        np.cumsum(splits, out=h[1: n + 1])
         self.run_off[: n + 1].copy_(self.run_off_h[: n + 1], non_blocking=True)
         return self.run_off
 
@@ -189,7 +188,9 @@ class ShardExchange(_Base):
 
     def _prep_stream(self):
         if self._prep is None:
-            self._prep = torch.cuda.Stream(self.dev)
+            from ..models.fm import side_stream_priority
+
+            self._prep = torch.cuda.Stream(self.dev, priority=side_stream_priority())
         return self._prep
 
     def _split(self, b: Batch, nparts: int) -> list[tuple[int, int, int, int]]:
@@ -257,8 +258,11 @@ class ShardExchange(_Base):
             # host sync of the step, it waits for these dedups only -- and one count exchange
             # on the CPU group: row q of the [W, P] matrix is what goes to / comes from rank q
             sc = torch.stack(counts, dim=1).cpu()
-            rc = torch.empty_like(sc)
-            dist.all_to_all_single(rc, sc, group=self.cpu_group)
+            if self.W == 1:
+                rc = sc
+            else:
+                rc = torch.empty_like(sc)
+                dist.all_to_all_single(rc, sc, group=self.cpu_group)
             sc_l, rc_l = sc.t().tolist(), rc.t().tolist()
             u_off = r_off = 0
             for k, part in enumerate(pl.parts):
