@@ -20,7 +20,8 @@ Extensions (new keys, all optional):
                 global_bias = true|false (learned b0; its gradient is all-reduced over ranks),
                 dtype = fp32|bf16|fp8 (fp8: OCP e4m3 + per-row scale, GPU)
   [Train]       optimizer = adagrad|ftrl|sgd, ftrl.l1, ftrl.l2, ftrl.beta,
-                ftrl.initial_accumulator, parse_threads, loader = native|python, gpu_parse = true|false, shuffle = true|false,
+                ftrl.initial_accumulator, parse_threads, loader = native|python, gpu_parse = true|false, stochastic_rounding = true|false,
+                shuffle = true|false,
                 max_steps, dedup_chunk, log_steps
   [Distributed] mode = auto|local|shard|dp|dp_dense, grad_reduce = sum|mean,
                 comm_dtype = auto|fp32|bf16 (row-sharded wire rows; auto = table storage dtype),
@@ -91,6 +92,7 @@ class FMRunConfig:
     parse_threads: int = 4
     loader: str = "native"      # native (C++ loader thread) | python
     gpu_parse: bool = False     # native loader: tokenize on the GPU (hip/parse.hip)
+    stochastic_rounding: bool = True  # bf16 / fp8 tables: stochastically rounded updates
     shuffle: bool = True
     max_steps: int | None = None
     dedup_chunk: int = 32
@@ -124,7 +126,7 @@ class FMRunConfig:
                         dtype={"fp32": torch.float32, "bf16": torch.bfloat16,
                                "fp8": torch.float8_e4m3fn}[self.dtype], opt=opt, mode=self.mode,
                         grad_reduce=self.grad_reduce, comm_dtype=self.comm_dtype, microbatches=self.microbatches,
-                        dedup_chunk=self.dedup_chunk, global_bias=self.global_bias)
+                        stochastic_rounding=self.stochastic_rounding, dedup_chunk=self.dedup_chunk, global_bias=self.global_bias)
 
 
 def load_config(config_file: str, *, echo: bool = True, printer=print) -> FMRunConfig:
@@ -191,6 +193,8 @@ def load_config(config_file: str, *, echo: bool = True, printer=print) -> FMRunC
     c.parse_threads = opt(TRAIN, "parse_threads", int, c.parse_threads)
     c.loader = opt(TRAIN, "loader", lambda s: s.strip().lower(), c.loader)
     c.gpu_parse = opt(TRAIN, "gpu_parse", lambda s: s.strip().lower() == "true", c.gpu_parse)
+    c.stochastic_rounding = opt(TRAIN, "stochastic_rounding", lambda s: s.strip().lower() == "true",
+                                c.stochastic_rounding)
     if c.loader not in ("native", "python"):
         raise ConfigError(f"[Train] loader must be native or python, got {c.loader}")
     c.shuffle = opt(TRAIN, "shuffle", to_bool, c.shuffle)

@@ -60,6 +60,7 @@ struct BwdArgs {
   long long g_stride;
   int g_wcol;               // word index of the w-grad in a gradient row
   int g_bf16;               // 1: v-grad stored as bf16 (the exchange's bf16 wire)
+  const int* sr_counter;    // stochastic rounding of bf16 / fp8 row stores (null: round to nearest)
   float* partial;           // [#chunks, Kp + 4]
   int* big_list;            // [U] rows for the workgroup combine
   int* big_count;           // device scalar, zeroed by the launcher
@@ -119,7 +120,7 @@ __device__ inline void bwd_load_row(const BwdArgs& a, long long row, int tE, Row
 
 template <int LPR, typename TV, int EPL>
 __device__ inline void bwd_finish(const BwdArgs& a, int u, int t, bool tact, RowState<EPL>& r,
-                                  const float (&A)[EPL], float Scx, float Sc, int n_u) {
+                                  const float (&A)[EPL], float Scx, float Sc, int n_u, uint32_t sr) {
   using F = Frag<TV>;
   const float nreg_v = a.reg_v * (float)n_u, nreg_w = a.reg_w * (float)n_u;
   float gr[EPL];
@@ -150,7 +151,7 @@ __device__ inline void bwd_finish(const BwdArgs& a, int u, int t, bool tact, Row
 #pragma unroll
   for (int k = 0; k < EPL; ++k) opt_step(a.opt, gr[k], r.vv[k], r.st0[k], r.st1[k]);
   store_row<LPR, TV>(reinterpret_cast<TV*>(a.v) + r.row * a.v_stride + t * EPL, r.vv, a.w, r.row, a.w_stride, t,
-                     tact);
+                     tact, sr);
   if (tact) {
     float* s0 = a.s0v + r.row * a.s_stride + t * EPL;
 #pragma unroll
@@ -173,15 +174,16 @@ __device__ inline void bwd_finish(const BwdArgs& a, int u, int t, bool tact, Row
 
 template <int LPR, typename TV, int EPL>
 __device__ inline void bwd_finalize(const BwdArgs& a, int u, int t, bool tact, int tE,
-                                    const float (&A)[EPL], float Scx, float Sc, int n_u) {
+                                    const float (&A)[EPL], float Scx, float Sc, int n_u, uint32_t sr) {
   RowState<EPL> r;
   bwd_load_row<TV, EPL>(a, a.mode == kBwdLocal ? (long long)a.uniq[u] : (long long)u, tE, r);
-  bwd_finish<LPR, TV, EPL>(a, u, t, tact, r, A, Scx, Sc, n_u);
+  bwd_finish<LPR, TV, EPL>(a, u, t, tact, r, A, Scx, Sc, n_u, sr);
 }
 
 // One lane group per chunk of <= CH (<= kMaxCH) sorted occurrences of one row.
 template <int LPR, typename TV>
 __global__ __launch_bounds__(kBlock) void fm_bwd_chunk_kernel(BwdArgs a) {
+  const uint32_t sr = sr_step_seed(a.sr_counter);  // stochastic rounding seed (0: nearest)
   constexpr int EPL = Frag<TV>::N;  // elements per lane of the table dtype
   constexpr int G = kWave / LPR;
   constexpr int PF = (kMaxCH + LPR - 1) / LPR;  // prefetched occurrences per lane
@@ -281,7 +283,7 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_chunk_kernel(BwdArgs a) {
       }
     }
     if (single) {
-      bwd_finish<LPR, TV, EPL>(a, u, t, tact, rs, A, Scx, Sc, len);
+      bwd_finish<LPR, TV, EPL>(a, u, t, tact, rs, A, Scx, Sc, len, sr);
     } else {
       float* dst = a.partial + (long long)cc * (a.Kp + 4);
       if (tact) {
@@ -304,6 +306,7 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_chunk_kernel(BwdArgs a) {
 // Hotter rows are appended to big_list for fm_bwd_big_kernel.
 template <int LPR, typename TV>
 __global__ __launch_bounds__(kBlock) void fm_bwd_combine_kernel(BwdArgs a) {
+  const uint32_t sr = sr_step_seed(a.sr_counter);  // stochastic rounding seed (0: nearest)
   constexpr int EPL = Frag<TV>::N;
   constexpr int G = kWave / LPR;
   const int lane = threadIdx.x & (kWave - 1);
@@ -351,7 +354,7 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_combine_kernel(BwdArgs a) {
         Sc += pt[q];
       }
     }
-    bwd_finalize<LPR, TV, EPL>(a, u, t, tact, tE, A, Scx, Sc, a.seg_start[u + 1] - a.seg_start[u]);
+    bwd_finalize<LPR, TV, EPL>(a, u, t, tact, tE, A, Scx, Sc, a.seg_start[u + 1] - a.seg_start[u], sr);
   }
 }
 
@@ -359,6 +362,7 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_combine_kernel(BwdArgs a) {
 // c0+q, c0+q+NG, ... ; the NG group sums are reduced in LDS in group order.
 template <int LPR, typename TV>
 __global__ __launch_bounds__(kBlock) void fm_bwd_big_kernel(BwdArgs a) {
+  const uint32_t sr = sr_step_seed(a.sr_counter);  // stochastic rounding seed (0: nearest)
   constexpr int EPL = Frag<TV>::N;
   constexpr int G = kWave / LPR;
   constexpr int NG = kWavesPerBlock * G;
@@ -421,7 +425,7 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_big_kernel(BwdArgs a) {
         Scx += o[LPR * EPL];
         Sc += o[LPR * EPL + 1];
       }
-      bwd_finalize<LPR, TV, EPL>(a, u, t, tact, tE, A, Scx, Sc, a.seg_start[u + 1] - a.seg_start[u]);
+      bwd_finalize<LPR, TV, EPL>(a, u, t, tact, tE, A, Scx, Sc, a.seg_start[u + 1] - a.seg_start[u], sr);
     }
     __syncthreads();
   }
@@ -568,6 +572,7 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_dense_kernel(BwdArgs a) {
 // (4 stripes of workgroups, then the stripes in order), then the optimizer.
 template <int LPR, typename TV>
 __global__ __launch_bounds__(kBlock) void fm_bwd_dense_apply_kernel(BwdArgs a) {
+  const uint32_t sr = sr_step_seed(a.sr_counter);  // stochastic rounding seed (0: nearest)
   constexpr int EPL = Frag<TV>::N;
   __shared__ float4 red[kWavesPerBlock][kWave];
   __shared__ float row[kWave * 4];
@@ -604,7 +609,7 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_dense_apply_kernel(BwdArgs a) {
 #pragma unroll
     for (int k = 0; k < EPL; ++k) A[k] = row[tE * EPL + k];
     const int u = a.dense_list[h];
-    bwd_finalize<LPR, TV, EPL>(a, u, t, tact, tE, A, row[a.Kp], row[a.Kp + 1], a.seg_start[u + 1] - a.seg_start[u]);
+    bwd_finalize<LPR, TV, EPL>(a, u, t, tact, tE, A, row[a.Kp], row[a.Kp + 1], a.seg_start[u + 1] - a.seg_start[u], sr);
   }
 }
 

@@ -38,6 +38,25 @@ enum DType : int { kF32 = 0, kBF16 = 1, kFP8 = 2 };
 struct fp8e4m3 { uint8_t bits; };
 constexpr float kFp8Max = 448.f;
 
+// ---- stochastic rounding -----------------------------------------------------
+// Low-precision tables (bf16 / fp8) store updated rows with stochastic rounding
+// when a step seed is given (0 = round to nearest even): small Adagrad / FTRL
+// steps then survive in expectation instead of being rounded away.  The random
+// bits are a hash of (step seed, table row, column): deterministic run to run.
+__device__ inline uint32_t sr_hash(uint32_t seed, uint32_t row, uint32_t col) {
+  uint32_t h = seed ^ (row * 0x9E3779B1u) ^ (col * 0x85EBCA77u);
+  h ^= h >> 16; h *= 0x7feb352du;
+  h ^= h >> 15; h *= 0x846ca68bu;
+  h ^= h >> 16;
+  return h;
+}
+
+// Next random word of a lane's stream (xorshift32: one hash per lane, not per element).
+__device__ inline uint32_t sr_next(uint32_t r) {
+  r ^= r << 13; r ^= r >> 17; r ^= r << 5;
+  return r;
+}
+
 // ---- 16-byte row fragments ------------------------------------------------
 template <typename T> struct Frag;
 
@@ -51,6 +70,7 @@ template <> struct Frag<float> {
   __device__ static inline void store(float* p, const float (&o)[4]) {
     *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
   }
+  __device__ static inline void store_sr(float* p, const float (&o)[4], uint32_t, uint32_t, uint32_t) { store(p, o); }
 };
 
 __device__ inline float bf16_bits_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
@@ -59,6 +79,14 @@ __device__ inline uint32_t f32_to_bf16_bits(float f) {
   uint32_t u = __float_as_uint(f);
   if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (u >> 16) | 0x40u;
   return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+
+// Stochastically rounded f32 -> bf16 bits: add 16 random bits below the kept
+// mantissa, truncate (Inf / NaN pass through).
+__device__ inline uint32_t f32_to_bf16_bits_sr(float f, uint32_t r) {
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (u >> 16) | ((u & 0x7fffffu) ? 0x40u : 0u);
+  return (u + (r & 0xffffu)) >> 16;
 }
 
 template <> struct Frag<__hip_bfloat16> {
@@ -81,6 +109,18 @@ template <> struct Frag<__hip_bfloat16> {
     v.w = f32_to_bf16_bits(o[6]) | (f32_to_bf16_bits(o[7]) << 16);
     *reinterpret_cast<uint4*>(p) = v;
   }
+  __device__ static inline void store_sr(__hip_bfloat16* p, const float (&o)[8], uint32_t seed, uint32_t row,
+                                         uint32_t col) {
+    uint32_t b[8];
+    uint32_t r = sr_hash(seed, row, col);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      b[k] = f32_to_bf16_bits_sr(o[k], r);
+      r = sr_next(r);
+    }
+    *reinterpret_cast<uint4*>(p) = make_uint4(b[0] | (b[1] << 16), b[2] | (b[3] << 16), b[4] | (b[5] << 16),
+                                              b[6] | (b[7] << 16));
+  }
 };
 
 // 4 fp8 per lane (a 4-byte load: a K=128 row is one 32-lane instruction, the
@@ -97,6 +137,16 @@ template <> struct Frag<fp8e4m3> {
   __device__ static inline void store(fp8e4m3* p, const float (&o)[4]) {
     int u = __builtin_amdgcn_cvt_pk_fp8_f32(o[0], o[1], 0, false);
     u = __builtin_amdgcn_cvt_pk_fp8_f32(o[2], o[3], u, true);
+    *reinterpret_cast<int*>(p) = u;
+  }
+  // gfx950 v_cvt_sr_fp8_f32: hardware stochastic rounding with the given random bits
+  __device__ static inline void store_sr(fp8e4m3* p, const float (&o)[4], uint32_t seed, uint32_t row,
+                                         uint32_t col) {
+    const uint32_t r0 = sr_hash(seed, row, col), r1 = sr_next(r0), r2 = sr_next(r1), r3 = sr_next(r2);
+    int u = __builtin_amdgcn_cvt_sr_fp8_f32(o[0], (int)r0, 0, 0);
+    u = __builtin_amdgcn_cvt_sr_fp8_f32(o[1], (int)r1, u, 1);
+    u = __builtin_amdgcn_cvt_sr_fp8_f32(o[2], (int)r2, u, 2);
+    u = __builtin_amdgcn_cvt_sr_fp8_f32(o[3], (int)r3, u, 3);
     *reinterpret_cast<int*>(p) = u;
   }
 };
@@ -127,8 +177,9 @@ __device__ inline float row_scale(const float* w, long long row, long long w_str
 // call: scaled dtypes reduce the row's max |v| over the group first).
 template <int LPR, typename TV>
 __device__ inline void store_row(TV* lane_ptr, const float (&o)[Frag<TV>::N], float* w, long long row,
-                                 long long w_stride, int t, bool tact) {
+                                 long long w_stride, int t, bool tact, uint32_t sr_seed = 0) {
   using F = Frag<TV>;
+  const uint32_t col = (uint32_t)(t * F::N);
   if constexpr (F::kScaled) {
     float m = 0.f;
 #pragma unroll
@@ -139,11 +190,23 @@ __device__ inline void store_row(TV* lane_ptr, const float (&o)[Frag<TV>::N], fl
     float q[F::N];
 #pragma unroll
     for (int k = 0; k < F::N; ++k) q[k] = fminf(fmaxf(o[k] * inv, -kFp8Max), kFp8Max);
-    if (tact) F::store(lane_ptr, q);
+    if (tact) {
+      if (sr_seed) F::store_sr(lane_ptr, q, sr_seed, (uint32_t)row, col);
+      else F::store(lane_ptr, q);
+    }
     if (t == 0) w[row * w_stride + 1] = s;
   } else {
-    if (tact) F::store(lane_ptr, o);
+    if (tact) {
+      if (sr_seed) F::store_sr(lane_ptr, o, sr_seed, (uint32_t)row, col);
+      else F::store(lane_ptr, o);
+    }
   }
+}
+
+// Per-step seed of the stochastic rounding (device counter ticked once per training
+// step, so hipGraph replays draw fresh bits); 0 = round to nearest even.
+__device__ inline uint32_t sr_step_seed(const int* counter) {
+  return counter ? (sr_hash((uint32_t)*counter, 0x5bd1e995u, 0x1b873593u) | 1u) : 0u;
 }
 
 // Sum over the row groups of a wave: lanes t, t+LPR, t+2*LPR, ...

@@ -84,8 +84,9 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
          int opt_type, float lr, float l1, float l2, float beta, u64 grad_out, long long g_stride, u64 partial,
          u64 big_list, u64 big_count, u64 multi, u64 slice_list, u64 slice_start, int nslices, u64 dense_list,
          u64 dense_part, int nex, u64 dense_stream, int dtype,
-         long long max_chunks, long long max_unique, u64 stream, int g_wcol, int g_bf16) {
+         long long max_chunks, long long max_unique, u64 stream, int g_wcol, int g_bf16, u64 sr_counter) {
         fm::BwdArgs a{};
+        a.sr_counter = P<const int>(sr_counter);
         a.mode = mode; a.counts = P<const int>(counts); a.chunk_start = P<const int>(chunk_start);
         a.chunk_seg = P<const int>(chunk_seg); a.chunk_key = P<const int>(chunk_key);
         a.seg_start = P<const int>(seg_start);
@@ -114,7 +115,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("multi"), py::arg("slice_list"), py::arg("slice_start"), py::arg("nslices"), py::arg("dense_list"),
       py::arg("dense_part"), py::arg("nex"), py::arg("dense_stream"), py::arg("dtype"),
       py::arg("max_chunks"), py::arg("max_unique"), py::arg("stream"), py::arg("g_wcol") = -1,
-      py::arg("g_bf16") = 0);
+      py::arg("g_bf16") = 0, py::arg("sr_counter") = 0);
 
   m.def("dedup_workspace_bytes", &fm::dedup_workspace_bytes, py::arg("n"));
 
@@ -182,8 +183,9 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       [](u64 num_unique, u64 seg_start, u64 uniq, u64 perm, u64 grad_in, long long g_stride, int Kp, u64 v,
          long long v_stride, u64 w, long long w_stride, u64 s0v, u64 s1v, long long s_stride, u64 s0w, u64 s1w,
          int opt_type, float lr, float l1, float l2, float beta, int dtype, long long max_unique, u64 stream,
-         int g_wcol, int g_bf16) {
+         int g_wcol, int g_bf16, u64 sr_counter) {
         fm::ApplyArgs a{};
+        a.sr_counter = P<const int>(sr_counter);
         a.g_wcol = g_wcol < 0 ? Kp : g_wcol; a.g_bf16 = g_bf16;
         a.num_unique = P<const int>(num_unique); a.seg_start = P<const int>(seg_start);
         a.uniq = P<const int>(uniq); a.perm = P<const int>(perm); a.grad_in = P<const float>(grad_in);
@@ -196,14 +198,16 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("g_stride"), py::arg("Kp"), py::arg("v"), py::arg("v_stride"), py::arg("w"), py::arg("w_stride"),
       py::arg("s0v"), py::arg("s1v"), py::arg("s_stride"), py::arg("s0w"), py::arg("s1w"), py::arg("opt_type"),
       py::arg("lr"), py::arg("l1"), py::arg("l2"), py::arg("beta"), py::arg("dtype"), py::arg("max_unique"),
-      py::arg("stream"), py::arg("g_wcol") = -1, py::arg("g_bf16") = 0);
+      py::arg("stream"), py::arg("g_wcol") = -1, py::arg("g_bf16") = 0, py::arg("sr_counter") = 0);
 
   m.def(
       "apply_runs",
       [](int R, int W, u64 run_off, u64 req, u64 match, u64 grad_in, long long g_stride, int Kp, u64 v,
          long long v_stride, u64 w, long long w_stride, u64 s0v, u64 s1v, long long s_stride, u64 s0w, u64 s1w,
-         int opt_type, float lr, float l1, float l2, float beta, int dtype, u64 stream, int g_wcol, int g_bf16) {
+         int opt_type, float lr, float l1, float l2, float beta, int dtype, u64 stream, int g_wcol, int g_bf16,
+         u64 sr_counter) {
         fm::ApplyArgs a{};
+        a.sr_counter = P<const int>(sr_counter);
         a.g_wcol = g_wcol < 0 ? Kp : g_wcol; a.g_bf16 = g_bf16;
         a.R = R; a.W = W; a.run_off = P<const int>(run_off); a.req = P<const int>(req);
         a.match = P<const int>(match); a.grad_in = P<const float>(grad_in);
@@ -216,7 +220,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("g_stride"), py::arg("Kp"), py::arg("v"), py::arg("v_stride"), py::arg("w"), py::arg("w_stride"),
       py::arg("s0v"), py::arg("s1v"), py::arg("s_stride"), py::arg("s0w"), py::arg("s1w"), py::arg("opt_type"),
       py::arg("lr"), py::arg("l1"), py::arg("l2"), py::arg("beta"), py::arg("dtype"), py::arg("stream"),
-      py::arg("g_wcol") = -1, py::arg("g_bf16") = 0);
+      py::arg("g_wcol") = -1, py::arg("g_bf16") = 0, py::arg("sr_counter") = 0);
 
   m.def(
       "init_rows",

@@ -152,6 +152,7 @@ struct ApplyArgs {
   const int* run_off;       // [W+1]
   const int* req;           // [R] local table row of each received gradient row
   const int* match;         // [R, W]: index of the same row in run q, or -1 (null when W == 1)
+  const int* sr_counter;    // stochastic rounding of bf16 / fp8 row stores (null: round to nearest)
 };
 
 // One table row's parameters + optimizer state in registers (this lane's EPL
@@ -188,10 +189,10 @@ struct RowUpdate {
   }
 
   __device__ inline void step_store(const ApplyArgs& a, const float (&gr)[EPL], float gw, long long row, int t,
-                                    bool tact) {
+                                    bool tact, uint32_t sr) {
 #pragma unroll
     for (int k = 0; k < EPL; ++k) opt_step(a.opt, gr[k], vv[k], st0[k], st1[k]);
-    store_row<LPR, TV>(vrow, vv, a.w, row, a.w_stride, t, tact);
+    store_row<LPR, TV>(vrow, vv, a.w, row, a.w_stride, t, tact, sr);
     if (tact) {
 #pragma unroll
       for (int k = 0; k < EPL; k += 4) {
@@ -233,6 +234,7 @@ __device__ inline void add_grad_row(const ApplyArgs& a, const float* src, int tE
 // and apply the optimizer once.
 template <int LPR, typename TV>
 __global__ __launch_bounds__(kBlock) void apply_rows_kernel(ApplyArgs a) {
+  const uint32_t sr = sr_step_seed(a.sr_counter);  // stochastic rounding seed (0: nearest)
   constexpr int EPL = Frag<TV>::N;
   constexpr int G = kWave / LPR;
   const int lane = threadIdx.x & (kWave - 1);
@@ -253,7 +255,7 @@ __global__ __launch_bounds__(kBlock) void apply_rows_kernel(ApplyArgs a) {
     const int j1 = a.seg_start[u + 1];
     for (int j = a.seg_start[u]; j < j1; ++j)
       add_grad_row<EPL>(a, a.grad_in + (long long)a.perm[j] * a.g_stride, tE, gr, gw);
-    ru.step_store(a, gr, gw, row, t, tact);
+    ru.step_store(a, gr, gw, row, t, tact, sr);
   }
 }
 
@@ -284,6 +286,7 @@ __global__ __launch_bounds__(kBlock) void owner_match_kernel(int R, int W, const
 
 template <int LPR, typename TV>
 __global__ __launch_bounds__(kBlock) void apply_runs_kernel(ApplyArgs a) {
+  const uint32_t sr = sr_step_seed(a.sr_counter);  // stochastic rounding seed (0: nearest)
   constexpr int EPL = Frag<TV>::N;
   constexpr int G = kWave / LPR;
   const int lane = threadIdx.x & (kWave - 1);
@@ -314,7 +317,7 @@ __global__ __launch_bounds__(kBlock) void apply_runs_kernel(ApplyArgs a) {
       const int j = mrow[q];
       if (j >= 0) add_grad_row<EPL>(a, a.grad_in + (long long)j * a.g_stride, tE, gr, gw);
     }
-    ru.step_store(a, gr, gw, row, t, tact);
+    ru.step_store(a, gr, gw, row, t, tact, sr);
   }
 }
 

@@ -62,6 +62,7 @@ class FMConfig:
     dedup_chunk: int = 32             # CH of the segmented backward
     threads: int = 0                  # CPU kernels (0 = OpenMP default)
     global_bias: bool = False         # learned global bias b0 (extension; the reference has none)
+    stochastic_rounding: bool = True  # bf16 / fp8 tables (GPU): stochastically rounded row stores
 
 
 @dataclass
@@ -273,6 +274,12 @@ class FactorizationMachine:
         self._graph = None
         self._graph_pool: list[_GraphedStep] = []
         self._exchange = None
+        # stochastic rounding of low-precision row stores: a device step counter ticked inside
+        # every (captured) step, so graph replays draw fresh random bits
+        self.sr_base = (cfg.seed * 7919) & 0x3FFFFFFF
+        self.sr_state = (torch.full((1,), self.sr_base, dtype=torch.int32, device=self.device)
+                         if cfg.stochastic_rounding and cfg.dtype != torch.float32 and self.device.type == "cuda"
+                         else None)
         # optional global bias b0 (+ optimizer state), replicated on every rank; its gradient
         # sum(dpred) is all-reduced over the ranks each step (the model's one dense parameter)
         if cfg.global_bias:
@@ -288,6 +295,18 @@ class FactorizationMachine:
             self._exchange = make_exchange(self)
         elif mode != "local":
             raise ValueError(f"mode={mode} needs a distributed context")
+
+    def sr_tick(self) -> torch.Tensor | None:
+        """Advance the stochastic-rounding step counter (on the current stream); its tensor or None."""
+        if self.sr_state is None:
+            return None
+        self.sr_state.add_(1)
+        return self.sr_state
+
+    def sr_reset(self) -> None:
+        """Re-derive the stochastic-rounding counter from global_step (after a restore)."""
+        if self.sr_state is not None:
+            self.sr_state.fill_((self.sr_base + self.global_step) & 0x3FFFFFFF)
 
     # ------------------------------------------------------------------
     @property
@@ -420,7 +439,7 @@ class FactorizationMachine:
         with roctx_range("bwd+update"):
             K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
                           reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, dense_part=ws.dense_part,
-                          dense_stream=self._dense_stream() if gpu else None)
+                          dense_stream=self._dense_stream() if gpu else None, sr_counter=self.sr_tick())
         return StepOut(fo.loss_sum, b.B)
 
     # ------------------------------------------------------------------
@@ -472,7 +491,7 @@ class FactorizationMachine:
         with roctx_range("bwd+update"):
             K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
                           reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, dense_part=ws.dense_part,
-                          dense_stream=self._dense_stream())
+                          dense_stream=self._dense_stream(), sr_counter=self.sr_tick())
         return StepOut(fo.loss_sum, b.B)
 
     def _local_lookahead_step(self, b: Batch, next_batch: Batch | None) -> StepOut:

@@ -439,7 +439,7 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
                 grad_out: torch.Tensor | None = None, reg_v: float = 0.0, reg_w: float = 0.0,
                 partial: torch.Tensor | None = None, threads: int = 0,
                 dense_part: torch.Tensor | None = None, dense_stream=None,
-                grad_bf16: bool = False) -> torch.Tensor | None:
+                grad_bf16: bool = False, sr_counter: torch.Tensor | None = None) -> torch.Tensor | None:
     """Segmented FM backward over the dedup grouping (reference FmGrad, cc/fm_grad_op.h:59-163).
 
     Per unique row u with occurrences (i, x):
@@ -499,7 +499,8 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               slice_start=_p(dd.slice_start), nslices=int(dd.nslices or 0), dense_list=_p(dd.dense_list),
               dense_part=_p(dp), nex=int(dpred.numel()),
               dense_stream=dense_stream.cuda_stream if dense_stream is not None else 0, dtype=dt, max_chunks=dd.n, max_unique=dd.n,
-              stream=_stream(dpred), g_wcol=g_wcol if mode == BWD_EMIT else -1, g_bf16=int(bool(grad_bf16)))
+              stream=_stream(dpred), g_wcol=g_wcol if mode == BWD_EMIT else -1, g_bf16=int(bool(grad_bf16)),
+              sr_counter=_p(sr_counter))
     else:
         U = dd.sync()
         native.cpu().bwd(mode=mode, U=U, seg_start=_p(dd.seg_start), uniq=_p(dd.uniq), sorted_ex=_p(dd.sorted_ex),
@@ -563,7 +564,7 @@ def owner_counts(dd: DedupOut, rows_per_shard: int, world: int) -> torch.Tensor:
 
 
 def apply_rows(dd: DedupOut, grad_in: torch.Tensor, table: TableState, opt: OptConfig, Kp: int,
-               threads: int = 0) -> None:
+               threads: int = 0, sr_counter: torch.Tensor | None = None) -> None:
     """Owner side of a sharded update: sum received grad rows per table row, then one optimizer step."""
     v_stride = _chk_rows(table.v, Kp, "v")
     _check(grad_in.dtype == torch.float32 and grad_in.stride(1) == 1, "grad_in: fp32 rows")
@@ -576,7 +577,7 @@ def apply_rows(dd: DedupOut, grad_in: torch.Tensor, table: TableState, opt: OptC
                                 s0v=_p(table.s0v), s1v=_p(table.s1v), s_stride=s_stride, s0w=_p(table.s0w),
                                 s1w=_p(table.s1w), opt_type=opt.code, lr=float(opt.lr), l1=float(opt.l1),
                                 l2=float(opt.l2), beta=float(opt.beta), dtype=dt, max_unique=max(dd.n, 1),
-                                stream=_stream(grad_in))
+                                stream=_stream(grad_in), sr_counter=_p(sr_counter))
     else:
         native.cpu().apply_rows(U=dd.sync(), seg_start=_p(dd.seg_start), uniq=_p(dd.uniq), perm=_p(dd.perm),
                                 grad_in=_p(grad_in), g_stride=grad_in.stride(0), Kp=Kp, v=_p(table.v),
@@ -588,7 +589,8 @@ def apply_rows(dd: DedupOut, grad_in: torch.Tensor, table: TableState, opt: OptC
 
 def apply_runs(req: torch.Tensor, run_off: torch.Tensor, splits: list[int], grad_in: torch.Tensor,
                table: TableState, opt: OptConfig, Kp: int, match: torch.Tensor | None = None,
-               threads: int = 0, ws: DedupWorkspace | None = None, grad_bf16: bool = False) -> None:
+               threads: int = 0, ws: DedupWorkspace | None = None, grad_bf16: bool = False,
+               sr_counter: torch.Tensor | None = None) -> None:
     """Owner side of a sharded update over the received requests as W ascending runs.
 
     ``req`` [R] holds the local rows requested by each source rank, rank-major
@@ -607,7 +609,7 @@ def apply_runs(req: torch.Tensor, run_off: torch.Tensor, splits: list[int], grad
     if not _is_gpu(grad_in):
         _check(not grad_bf16, "bf16 gradient rows are a GPU path")
         dd = dedup(req[:R], ws=ws, key_bits=32, want_perm=True)
-        apply_rows(dd, grad_in, table, opt, Kp, threads=threads)
+        apply_rows(dd, grad_in, table, opt, Kp, threads=threads)  # (CPU tables: fp32 / bf16, nearest)
         return
     v_stride = _chk_rows(table.v, Kp, "v")
     _range_check(req[:R], table.v.shape[0], "req")
@@ -622,7 +624,7 @@ def apply_runs(req: torch.Tensor, run_off: torch.Tensor, splits: list[int], grad
                             s_stride=s_stride, s0w=_p(table.s0w), s1w=_p(table.s1w), opt_type=opt.code,
                             lr=float(opt.lr), l1=float(opt.l1), l2=float(opt.l2), beta=float(opt.beta), dtype=dt,
                             stream=_stream(grad_in), g_wcol=(Kp * 2 + 15) // 16 * 4 if grad_bf16 else Kp,
-                            g_bf16=int(bool(grad_bf16)))
+                            g_bf16=int(bool(grad_bf16)), sr_counter=_p(sr_counter))
 
 
 @dataclass

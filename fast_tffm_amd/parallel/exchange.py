@@ -394,7 +394,7 @@ class ShardExchange(_Base):
         with roctx_range("apply"):
             K.apply_runs(pl.req_recv, pl.run_off, pl.splits, grad_recv, m.table.state, cfg.opt, Kp, match=pl.match,
                          threads=cfg.threads, ws=self.slots[pl.slot].ensure2(pl.R, self.dev) if not gpu else None,
-                         grad_bf16=wf.grad_bf16)
+                         grad_bf16=wf.grad_bf16, sr_counter=m.sr_tick())
         if gpu:
             done = torch.cuda.Event()
             done.record(torch.cuda.current_stream(self.dev))
@@ -467,7 +467,8 @@ class DPExchange(_Base):
         g_cat = torch.cat([g_all[r][: sizes[r]] for r in range(self.W)])
         n = ids_cat.numel()
         dd2 = K.dedup(ids_cat, ws=self._dd2(n), key_bits=bits_for(self.m.table.rows), want_perm=True)
-        K.apply_rows(dd2, g_cat, self.m.table.state, self.m.cfg.opt, self.Kp, threads=self.m.cfg.threads)
+        K.apply_rows(dd2, g_cat, self.m.table.state, self.m.cfg.opt, self.Kp, threads=self.m.cfg.threads,
+                     sr_counter=self.m.sr_tick())
         return StepOut(fo.loss_sum, b.B)
 
     @torch.no_grad()
@@ -501,5 +502,6 @@ class DPDenseExchange(DPExchange):
         T = touched.numel()
         dd = K.DedupOut(n=T, uniq=touched, perm=touched, seg_start=self.arange[: T + 1],
                         num_unique=torch.tensor([T], dtype=torch.int32, device=self.dev), U_host=T)
-        K.apply_rows(dd, dense, self.m.table.state, self.m.cfg.opt, self.Kp, threads=self.m.cfg.threads)
+        K.apply_rows(dd, dense, self.m.table.state, self.m.cfg.opt, self.Kp, threads=self.m.cfg.threads,
+                     sr_counter=self.m.sr_tick())
         return StepOut(fo.loss_sum, b.B)

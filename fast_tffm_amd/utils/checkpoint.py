@@ -175,6 +175,8 @@ def restore_checkpoint(model, ckpt_dir: str) -> dict:
             local = torch.div(gid[sel], table.world, rounding_mode="floor")
             _copy_rows(table, local.to(dev), {k: v[sel] for k, v in t.items()}, K, dev)
     model.global_step = int(meta["global_step"])
+    if hasattr(model, "sr_reset"):
+        model.sr_reset()
     return meta
 
 
@@ -322,4 +324,6 @@ def import_tf_checkpoint(model, prefix: str, block_num: int | None = None) -> in
         table.load_reference_rows(local[m].to(table.device), ref, a)
     step = int(t.get("global_step", np.array(0)))
     model.global_step = step
+    if hasattr(model, "sr_reset"):
+        model.sr_reset()
     return step

@@ -52,7 +52,7 @@ def test_fp8_adagrad_step_within_requantisation_error():
     V = 5000
     gen = CriteoSynth(V, device="cuda", seed=9)
     b = gen.batch(2048)
-    m = _model(V, 64, FP8)
+    m = _model(V, 64, FP8, stochastic_rounding=False)  # the bound below is round-to-nearest's
     p0 = m.table.reference_rows().double().cpu()
     m.train_step(b)
     p1, _, _ = reference_train_step(p0, torch.full_like(p0, 0.1), b.to("cpu"), "logistic", 0.05, 0.01, 0.01, 512)

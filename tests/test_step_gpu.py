@@ -164,3 +164,39 @@ def test_lookahead_graph_ring_matches_eager_bitwise():
     for x, y in zip(_state(a), _state(b)):
         assert torch.equal(x, y)
     assert all(l == l for l in losses)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, K.FP8])
+def test_stochastic_rounding_keeps_small_updates(dtype):
+    """SGD steps far below half an ulp of the stored values: stochastic rounding (per-step
+    device seed) follows the fp32 trajectory in expectation, round-to-nearest does not."""
+    from fast_tffm_amd.models.table import FMTable
+
+    rows, k, steps, lr = 4096, 64, 200, 1e-4
+    opt = K.OptConfig("sgd", lr=lr)
+    fp8 = dtype == K.FP8
+    ends = {}
+    for sr in (False, True):
+        t = FMTable(rows, k, dtype=dtype, opt=opt, init=False, device="cuda")
+        init = torch.full((rows, t.Kp), 0.75, device="cuda")
+        if fp8:  # column 0 (= the row max) pins the per-row scale; the others sit at q = 224
+            init.fill_(0.5)
+            init[:, 0] = 1.0
+            q, sc = K.quantize_fp8_rows(init)
+            t.v.copy_(q)
+            t.scale.copy_(sc)
+        else:
+            t.v.copy_(init.to(dtype))
+        ctr = torch.zeros(1, dtype=torch.int32, device="cuda") if sr else None
+        dd = K.dedup(torch.arange(rows, dtype=torch.int32, device="cuda"), key_bits=32, want_perm=True)
+        grad = torch.ones((rows, t.Kp + 4), device="cuda")  # each step: v -= lr
+        for _ in range(steps):
+            if ctr is not None:
+                ctr.add_(1)
+            K.apply_rows(dd, grad, t.state, opt, t.Kp, sr_counter=ctr)
+        cols = t.reference_rows()[:, 2:].double()  # factor columns (col 0 of reference rows is w)
+        ends[sr] = cols.mean().item()
+    start = 0.5 if fp8 else 0.75
+    expect = start - steps * lr
+    assert abs(ends[True] - expect) < 0.15 * steps * lr           # unbiased within noise
+    assert abs(ends[False] - expect) > 0.4 * steps * lr           # nearest rounding drifts away
