@@ -54,7 +54,7 @@ struct RleArgs {
   int* chunk_start;               // [n+1]
   int* chunk_seg;                 // [n] segment id | kChunkFirst | kChunkSingle
   int* chunk_key;                 // [n] key of the chunk's segment
-  int* counts;                    // device [4]: U, #chunks, #multi-chunk rows, (spare)
+  int* counts;                    // device [8]: U, #chunks, #multi-chunk rows, #dense rows, bwd hot rows, -
   int* inv;                       // [n] occurrence -> segment (payload = occurrence)
   const int* ex_of_occ;           // [n] (payload = occurrence)
   int* sorted_ex;                 // [n] (payload = occurrence)
@@ -461,7 +461,10 @@ struct DedupArgs {
 };
 
 int launch_dedup(const DedupArgs& a, hipStream_t st) {
-  (void)hipMemsetAsync(a.counts, 0, 4 * sizeof(int), st);
+  // counts[0..3] = U, #chunks, #multi-chunk rows, #dense rows; counts[4] = the backward's
+  // hot-row count: both backward counters start at 0 here, on the dedup's stream (off the
+  // compute stream's critical path)
+  (void)hipMemsetAsync(a.counts, 0, 8 * sizeof(int), st);
   if (a.n <= 0) {
     (void)hipMemsetAsync(a.seg_start, 0, sizeof(int), st);
     (void)hipMemsetAsync(a.seg_chunk, 0, sizeof(int), st);

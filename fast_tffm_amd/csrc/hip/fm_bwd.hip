@@ -61,6 +61,7 @@ struct BwdArgs {
   int g_wcol;               // word index of the w-grad in a gradient row
   int g_bf16;               // 1: v-grad stored as bf16 (the exchange's bf16 wire)
   const int* sr_counter;    // stochastic rounding of bf16 / fp8 row stores (null: round to nearest)
+  int counters_ready;       // 1: counts[2] and *big_count are already 0 (fresh dedup)
   float* partial;           // [#chunks, Kp + 4]
   int* big_list;            // [U] rows for the workgroup combine
   int* big_count;           // device scalar, zeroed by the launcher
@@ -632,8 +633,10 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   if (max_chunks <= 0) return 0;
   const int lpr = lanes_per_row(a.Kp, dtype);
   const int G = kWave / lpr;
-  (void)hipMemsetAsync(a.big_count, 0, sizeof(int), st);
-  (void)hipMemsetAsync(a.counts_rw + 2, 0, sizeof(int), st);  // #multi-chunk rows, appended by the chunk kernel
+  if (!a.counters_ready) {  // (a fresh dedup zeroed both on its own stream)
+    (void)hipMemsetAsync(a.big_count, 0, sizeof(int), st);
+    (void)hipMemsetAsync(a.counts_rw + 2, 0, sizeof(int), st);  // #multi-chunk rows, appended by the chunk kernel
+  }
   const int g1 = (fill_grid(max_chunks, kWavesPerBlock * G) + 7) / 8 * 8;  // multiple of 8: XCD groups
   const bool dense = a.dense_list && a.dense_part;
   const bool fork = dense && dense_st && dense_st != st;

@@ -61,7 +61,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       [](int B, u64 offsets, u64 rows, u64 vals, u64 v, long long v_stride, u64 w, long long w_stride, int Kp,
          int dtype, u64 labels, u64 weights, int loss_type, float grad_scale, u64 pred, u64 r1, u64 dpred,
          u64 loss_partial, u64 reg_partial, int grid, u64 stream, u64 bias) {
-        fm::FwdArgs a;
+        fm::FwdArgs a{};
         a.B = B; a.offsets = P<const int>(offsets); a.rows = P<const int>(rows);
         a.vals = P<const float>(vals); a.v = P<const void>(v); a.v_stride = v_stride;
         a.w = P<const float>(w); a.w_stride = w_stride; a.Kp = Kp;
@@ -84,8 +84,10 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
          int opt_type, float lr, float l1, float l2, float beta, u64 grad_out, long long g_stride, u64 partial,
          u64 big_list, u64 big_count, u64 multi, u64 slice_list, u64 slice_start, int nslices, u64 dense_list,
          u64 dense_part, int nex, u64 dense_stream, int dtype,
-         long long max_chunks, long long max_unique, u64 stream, int g_wcol, int g_bf16, u64 sr_counter) {
+         long long max_chunks, long long max_unique, u64 stream, int g_wcol, int g_bf16, u64 sr_counter,
+         int counters_ready) {
         fm::BwdArgs a{};
+        a.counters_ready = counters_ready;
         a.sr_counter = P<const int>(sr_counter);
         a.mode = mode; a.counts = P<const int>(counts); a.chunk_start = P<const int>(chunk_start);
         a.chunk_seg = P<const int>(chunk_seg); a.chunk_key = P<const int>(chunk_key);
@@ -115,7 +117,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("multi"), py::arg("slice_list"), py::arg("slice_start"), py::arg("nslices"), py::arg("dense_list"),
       py::arg("dense_part"), py::arg("nex"), py::arg("dense_stream"), py::arg("dtype"),
       py::arg("max_chunks"), py::arg("max_unique"), py::arg("stream"), py::arg("g_wcol") = -1,
-      py::arg("g_bf16") = 0, py::arg("sr_counter") = 0);
+      py::arg("g_bf16") = 0, py::arg("sr_counter") = 0, py::arg("counters_ready") = 0);
 
   m.def("dedup_workspace_bytes", &fm::dedup_workspace_bytes, py::arg("n"));
 

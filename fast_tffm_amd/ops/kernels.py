@@ -200,6 +200,8 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
               grad_scale=float(grad_scale), pred=_p(pred), r1=_p(r1), dpred=_p(dpred) if lt else 0,
               loss_partial=_p(lp) if lt else 0, reg_partial=_p(rp) if want_reg else 0, grid=grid,
               stream=_stream(rows), bias=_p(bias))
+        # (an in-kernel last-block reduction was measured slower: the per-block agent-scope
+        # release fence writes back L2 -- fwd 211 -> 412 us; a separate reduce is ~10 us)
         loss_sum = lp.sum(dtype=torch.float32) if lt else None
         regv = rp.view(grid, 2)[:, 0].sum() if want_reg else None
         regw = rp.view(grid, 2)[:, 1].sum() if want_reg else None
@@ -229,7 +231,7 @@ class DedupOut:
 
     __slots__ = ("n", "skeys", "perm", "uniq", "seg_start", "seg_chunk", "chunk_start", "chunk_seg", "chunk_key", "counts",
                  "num_unique", "inv", "sorted_ex", "sorted_x", "U_host", "CH", "big_list", "big_count", "multi",
-                 "slice_list", "slice_start", "nslices", "ex_shift", "dense_list")
+                 "slice_list", "slice_start", "nslices", "ex_shift", "dense_list", "bwd_fresh")
 
     def __init__(self, **kw):
         for k in self.__slots__:
@@ -260,14 +262,14 @@ class DedupWorkspace:
         self.chunk_start = torch.empty(n1 + 1, **i32)
         self.chunk_seg = torch.empty(n1, **i32)   # segment id | first (bit 30) | single (bit 31)
         self.chunk_key = torch.empty(n1, **i32)
-        self.counts = torch.zeros(4, **i32)   # U, #chunks, #multi-chunk rows, spare
+        self.counts = torch.zeros(8, **i32)   # U, #chunks, #multi-chunk rows, #dense rows, bwd hot rows, -
         self.multi = torch.empty(n1, **i32)
         self.inv = torch.empty(n1, **i32)
         self.sorted_ex = torch.empty(n1, **i32)
         self.sorted_x = torch.empty(n1, dtype=torch.float32, device=device)
         self.ex_of_occ = torch.empty(n1, **i32)
         self.big_list = torch.empty(n1, **i32)
-        self.big_count = torch.zeros(1, **i32)
+        self.big_count = self.counts[4:5]     # zeroed with the counts by every GPU dedup
         self.slice_list = torch.empty(n1, **i32)
         self.slice_start = torch.empty(MAX_SLICES + 1, **i32)
         self.dense_list = torch.empty(MAX_DENSE, **i32)
@@ -404,6 +406,7 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
                 slice_shift=shift, nslices=nsl,
                 slice_list=_p(out.slice_list), slice_start=_p(ws.slice_start), ws=_p(ws.ws),
                 ws_bytes=ws.ws.numel(), stream=_stream(keys))
+        out.bwd_fresh = True  # the backward counters were zeroed on this stream
     else:
         U = native.cpu().dedup(n=n, keys=_p(keys), skeys=_p(ws.skeys), perm=_p(ws.perm), uniq=_p(ws.uniq),
                                seg_start=_p(ws.seg_start), inv=_p(out.inv), ex_of_occ=_p(ex_of_occ),
@@ -500,7 +503,8 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               dense_part=_p(dp), nex=int(dpred.numel()),
               dense_stream=dense_stream.cuda_stream if dense_stream is not None else 0, dtype=dt, max_chunks=dd.n, max_unique=dd.n,
               stream=_stream(dpred), g_wcol=g_wcol if mode == BWD_EMIT else -1, g_bf16=int(bool(grad_bf16)),
-              sr_counter=_p(sr_counter))
+              sr_counter=_p(sr_counter), counters_ready=int(bool(dd.bwd_fresh)))
+        dd.bwd_fresh = False  # a second backward over this grouping zeroes its counters itself
     else:
         U = dd.sync()
         native.cpu().bwd(mode=mode, U=U, seg_start=_p(dd.seg_start), uniq=_p(dd.uniq), sorted_ex=_p(dd.sorted_ex),
