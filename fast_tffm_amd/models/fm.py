@@ -103,7 +103,6 @@ class _Workspace:
             self.fwd_partial = torch.zeros(3 * 4096, dtype=torch.float32, device=dev)
 
 
-
 class _LocalSlot:
     """Double-buffered dedup workspace of the local lookahead pipeline."""
 
