@@ -258,8 +258,9 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
   m.def(
       "parse",
       [](u64 buf, u64 line_start, int n, long long vocab, int hash, u64 counts, u64 offsets, u64 labels, u64 ids,
-         u64 vals, u64 status, u64 ws, long long ws_bytes, u64 stream) {
+         u64 vals, u64 status, u64 ws, long long ws_bytes, u64 stream, int require_vals) {
         fm::ParseArgs a{};
+        a.require_vals = require_vals;
         a.buf = P<const char>(buf); a.line_start = P<const long long>(line_start); a.n = n; a.vocab = vocab;
         a.hash = hash; a.counts = P<int>(counts); a.labels = P<float>(labels); a.ids = P<int>(ids);
         a.vals = P<float>(vals); a.status = P<int>(status);
@@ -267,7 +268,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       },
       py::arg("buf"), py::arg("line_start"), py::arg("n"), py::arg("vocab"), py::arg("hash"), py::arg("counts"),
       py::arg("offsets"), py::arg("labels"), py::arg("ids"), py::arg("vals"), py::arg("status"), py::arg("ws"),
-      py::arg("ws_bytes"), py::arg("stream"));
+      py::arg("ws_bytes"), py::arg("stream"), py::arg("require_vals") = 0);
 
   m.def(
       "csr_rows",

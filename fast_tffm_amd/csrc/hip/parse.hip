@@ -35,6 +35,7 @@ struct ParseArgs {
   int n;
   long long vocab;
   int hash;
+  int require_vals;              // 1: every token must carry ':value' (serving lines), else fallback
   int* counts;                   // [n] tokens per line (pass 1)
   const int* offsets;            // [n + 1] exclusive scan of counts (pass 2)
   float* labels;                 // [n]
@@ -177,6 +178,7 @@ __global__ __launch_bounds__(kWave * kParseWaves) void parse_tokens_kernel(Parse
             if (nd == 0 || nd >= 18 || id >= a.vocab || (q < len && L[q] != ' ' && L[q] != ':')) bad = true;
           }
           float v = 1.f;
+          if (a.require_vals && !(q < len && L[q] == ':')) bad = true;
           if (!bad && q < len && L[q] == ':') {
             int r = q + 1;
             while (r < len && L[r] != ' ') ++r;

@@ -724,7 +724,7 @@ class ParsedGpu:
 
 
 def parse_gpu(buf: torch.Tensor, line_start: torch.Tensor, vocab_size: int, hash_feature_id: bool = False,
-              stream: torch.cuda.Stream | None = None) -> ParsedGpu:
+              stream: torch.cuda.Stream | None = None, require_vals: bool = False) -> ParsedGpu:
     """Tokenize n '\\n'-terminated libsvm lines (``buf`` uint8 on the GPU, line ``i`` =
     ``buf[line_start[i]:line_start[i+1]]``) into CSR on the device.
 
@@ -750,7 +750,7 @@ def parse_gpu(buf: torch.Tensor, line_start: torch.Tensor, vocab_size: int, hash
     ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
     h.parse(buf=_p(buf), line_start=_p(line_start), n=n, vocab=int(vocab_size), hash=int(bool(hash_feature_id)),
             counts=_p(counts), offsets=_p(offsets), labels=_p(labels), ids=_p(ids), vals=_p(vals),
-            status=_p(status), ws=_p(ws), ws_bytes=wsb, stream=st.cuda_stream)
+            status=_p(status), ws=_p(ws), ws_bytes=wsb, stream=st.cuda_stream, require_vals=int(bool(require_vals)))
     info = torch.cat([status, offsets[n:]]).cpu()   # one D2H: (fallback, max_feats, non-unit, -, nnz)
     fb, mf, nonunit, nnz = int(info[0]), int(info[1]), int(info[2]), int(info[4])
     return ParsedGpu(labels, offsets, ids[:nnz], vals[:nnz] if nonunit else None, nnz, mf, bool(fb))

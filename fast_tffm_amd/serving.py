@@ -68,32 +68,28 @@ def export_model(ckpt_dir: str, export_path: str, *, vocabulary_block_num: int, 
     return export_path
 
 
-def parse_serving_lines(lines, vocab_size: int, hash_feature_id: bool = False):
-    """Feature-only lines ``id:val id:val ...`` -> (offsets, ids, vals) (reference serving_parser)."""
-    offsets = [0]
-    ids: list[int] = []
-    vals: list[float] = []
+def parse_serving_lines(lines, vocab_size: int, hash_feature_id: bool = False, threads: int = 4):
+    """Feature-only lines ``id:val id:val ...`` -> (offsets, ids, vals) (reference serving_parser,
+    tffm/fm_model.py:195-220: whitespace-split tokens, ``:val`` mandatory, no label column).
+
+    Tokens are normalised to single spaces and parsed by the native multi-threaded parser
+    behind a dummy label; a line whose ':' count differs from its token count has a token
+    without a value (or with two) and is rejected like the reference's reshape([-1, 2])."""
     from .ops import native
 
+    norm = []
     for ln in lines:
-        if isinstance(ln, bytes):
-            ln = ln.decode()
+        if isinstance(ln, str):
+            ln = ln.encode()
         toks = ln.split()
-        for tok in toks:
-            fid, sep, fv = tok.rpartition(":")
-            if not sep:
-                raise ValueError(f"serving input needs id:val tokens, got {tok!r}")
-            if hash_feature_id:
-                ids.append(int(native.cpu().hash_bucket([fid], vocab_size)[0]))
-            else:
-                i = int(fid)
-                if not 0 <= i < vocab_size:
-                    raise ValueError(f"feature id {i} outside [0, {vocab_size})")
-                ids.append(i)
-            vals.append(float(fv))
-        offsets.append(len(ids))
-    return (torch.tensor(offsets, dtype=torch.int32), torch.tensor(ids, dtype=torch.int64),
-            torch.tensor(vals, dtype=torch.float32))
+        if ln.count(b":") != len(toks):
+            bad = next((t for t in toks if t.count(b":") != 1), b"")
+            raise ValueError(f"serving input needs id:val tokens, got {bad.decode(errors='replace')!r}")
+        norm.append(b"0 " + b" ".join(toks))
+    _, sizes, ids, vals = native.cpu().parse_lines(norm, int(vocab_size), bool(hash_feature_id), int(threads))
+    offsets = np.zeros(len(sizes) + 1, dtype=np.int32)
+    np.cumsum(sizes, out=offsets[1:])
+    return torch.from_numpy(offsets), torch.from_numpy(ids), torch.from_numpy(vals)
 
 
 class ServingModel:
@@ -125,12 +121,35 @@ class ServingModel:
             v[sel, :K] = rows[:, 1:]
         return cls(meta, v.to(dev), w.to(dev), dev)
 
+    def _parse_gpu(self, flat: list):
+        """GPU tokenizer (hip/parse.hip) over the lines behind a dummy label, ':value' required;
+        None when a line is outside its syntax subset (then the CPU path decides / raises)."""
+        from .ops import kernels as Kn
+
+        enc = [ln.encode() if isinstance(ln, str) else bytes(ln) for ln in flat]
+        data = b"".join(b"0 " + ln + b"\n" for ln in enc)
+        starts = np.zeros(len(enc) + 1, dtype=np.int64)
+        np.cumsum([len(ln) + 3 for ln in enc], out=starts[1:])
+        d = self.device
+        buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(d, non_blocking=False)
+        pg = Kn.parse_gpu(buf, torch.from_numpy(starts).to(d), self.meta["vocabulary_size"],
+                          self.meta["hash_feature_id"], require_vals=True)
+        if pg.fallback:
+            return None
+        vals = pg.vals if pg.vals is not None else torch.ones(pg.nnz, dtype=torch.float32, device=d)
+        return pg.offsets, pg.ids, vals
+
     def predict(self, data_lines) -> np.ndarray:
         from .ops import kernels as Kn
 
         flat = np.asarray(data_lines).reshape(-1).tolist()
-        offsets, ids, vals = parse_serving_lines(flat, self.meta["vocabulary_size"], self.meta["hash_feature_id"])
         d = self.device
+        parsed = self._parse_gpu(flat) if d.type == "cuda" and flat else None
+        if parsed is None:
+            offsets, ids, vals = parse_serving_lines(flat, self.meta["vocabulary_size"],
+                                                     self.meta["hash_feature_id"])
+        else:
+            offsets, ids, vals = parsed
         gb = self.meta.get("global_bias")
         bias = torch.tensor([gb], dtype=torch.float32, device=d) if gb is not None else None
         fo = Kn.fm_forward(offsets.to(d), ids.to(torch.int32).to(d), vals.to(d), self.v, self.w, self.Kp,
