@@ -144,35 +144,46 @@ class Trainer:
                     nb = None
             return nb, self._all_have_batch(nb is not None)
 
+        def report(p):
+            """Print / log a finished step.  Called once the NEXT step is enqueued, so reading
+            this step's loss (a host sync) overlaps the device work of the next one."""
+            sn, o, t0 = p
+            loss = o.mean_loss()  # the reference fetches the loss every step
+            tend = time.time()
+            if self.monitor:
+                q = pf.size()
+                self.print("speed:", c.batch_size * self.world / max(tend - t0, 1e-9),
+                           "shuffle_queue: %.2f%%" % 100.0,
+                           "example_queue: %.2f%%" % (q * 100.0 / pf.queue_size))
+            if c.log_steps <= 1 or sn % c.log_steps == 0:
+                self.print("-- Global Step: %d; Avg loss: %.5f;" % (sn, loss))
+            metrics.log(sn, loss=loss, exq_size=pf.size())
+            return loss, tend
+
         batch, have = fetch()
+        pending = None
+        tprev = time.time()
         while have:
             # lookahead: the next batch (when every rank has one) lets the sharded executor
             # build its dedup / id exchange while this step computes
             nxt, nhave = fetch()
             if self.trace and prof is None and step_num == start_step + 1:
                 prof = _start_profiler()
-            cur = time.time()
             with roctx_range("train_step"):
                 out = self.model.train_step(batch, nxt if nhave else None)
             step_num = self.model.global_step
             if batch.reader_pos is not None:  # position of the last CONSUMED batch (the reader runs ahead)
                 self.reader_state.epoch, self.reader_state.batches_in_epoch = batch.reader_pos
-            loss = out.mean_loss()  # host sync: the reference fetches the loss every step
-            last_loss = loss
-            tend = time.time()
+            if pending is not None:
+                last_loss, tprev = report(pending)
+            pending = (step_num, out, tprev)
             if prof is not None and step_num >= start_step + 1 + self.trace_steps:
                 _stop_profiler(prof, self.trace)
                 prof = None
                 self.trace = None
-            if self.monitor:
-                q = pf.size()
-                self.print("speed:", c.batch_size * self.world / max(tend - cur, 1e-9),
-                           "shuffle_queue: %.2f%%" % 100.0,
-                           "example_queue: %.2f%%" % (q * 100.0 / pf.queue_size))
-            if c.log_steps <= 1 or step_num % c.log_steps == 0:
-                self.print("-- Global Step: %d; Avg loss: %.5f;" % (step_num, loss))
-            metrics.log(step_num, loss=loss, exq_size=pf.size())
             if step_num % max(c.save_steps, 1) == 0:
+                last_loss, tprev = report(pending)
+                pending = None
                 if vb is not None:
                     v_loss = self.validation_loss(vb)
                     self.print("validation loss at step %d: %.8f" % (step_num, v_loss))
@@ -186,6 +197,8 @@ class Trainer:
             if ended_early or (c.max_steps is not None and step_num - start_step >= c.max_steps):
                 break
             batch, have = nxt, nhave
+        if pending is not None:
+            last_loss, _ = report(pending)
         if prof is not None:
             _stop_profiler(prof, self.trace)
         pf.close()
