@@ -8,6 +8,7 @@
 // lets the same kernels be called from torch streams, hipGraph captures and
 // the C++ step executor alike.
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 #include <stdexcept>
 #include <string>
 #include "fm_common.h"

@@ -43,6 +43,15 @@ def side_stream_priority() -> int:
     return int(os.environ.get("FM_SIDE_PRIORITY", "0"))
 
 
+def side_stream(device):
+    """Stream of the lookahead / plan work (normal queue; FM_SIDE_PRIORITY for its priority).
+
+    Measured alternatives (profiles/README.md): a high-priority queue (no gain) and a
+    CU-masked queue restricted to 32-128 CUs (hipExtStreamCreateWithCUMask: 0.67 -> 1.01
+    ms/step, the masked queue does not overlap with the compute stream's work)."""
+    return torch.cuda.Stream(device, priority=side_stream_priority())
+
+
 @dataclass
 class FMConfig:
     vocabulary_size: int
@@ -401,7 +410,7 @@ class FactorizationMachine:
 
     def _side_stream(self):
         if self._side is None:
-            self._side = torch.cuda.Stream(self.device, priority=side_stream_priority())
+            self._side = side_stream(self.device)
         return self._side
 
     def _local_train_step(self, b: Batch) -> StepOut:

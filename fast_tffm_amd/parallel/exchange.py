@@ -188,9 +188,9 @@ class ShardExchange(_Base):
 
     def _prep_stream(self):
         if self._prep is None:
-            from ..models.fm import side_stream_priority
+            from ..models.fm import side_stream
 
-            self._prep = torch.cuda.Stream(self.dev, priority=side_stream_priority())
+            self._prep = side_stream(self.dev)
         return self._prep
 
     def _split(self, b: Batch, nparts: int) -> list[tuple[int, int, int, int]]:
