@@ -72,6 +72,8 @@ def main() -> int:
     ap.add_argument("--mode", default=None, help="override step mode (local|shard|dp|dp_dense)")
     ap.add_argument("--microbatches", type=int, default=0,
                     help="row-sharded step: parts per batch overlapping the exchange (0/1 = one part)")
+    ap.add_argument("--prefetch-rows", default="auto", choices=["auto", "on", "off"],
+                    help="row-sharded step: exchange next step's rows early, patch the updated ones (auto: N > 1)")
     ap.add_argument("--comm-dtype", default="auto", choices=["auto", "fp32", "bf16"],
                     help="row-sharded wire rows (auto = table storage dtype; bf16 rounds fp32 rows for transport)")
     ap.add_argument("--profile-steps", type=int, default=0, help="also emit a torch.profiler trace")
@@ -104,7 +106,7 @@ def main() -> int:
                       initial_accumulator=0.1)
     cfg = FMConfig(vocabulary_size=vocab, factor_num=p["k"], loss_type="logistic", batch_size=a.batch,
                    init_value_range=0.01, seed=42, dtype=dtype, opt=opt, mode=mode, comm_dtype=a.comm_dtype,
-                   microbatches=a.microbatches)
+                   microbatches=a.microbatches, prefetch_rows=a.prefetch_rows)
     t0 = time.time()
     model = FactorizationMachine(cfg, device=dev, dist=ctx if W > 1 or mode not in ("auto", "local") else None)
     if dev.type == "cuda":
@@ -155,8 +157,11 @@ def main() -> int:
     def nxt(i):
         return pool[(i + 1) % len(pool)]
 
+    def nxt2(i):  # two batches of lookahead (the sharded executor's depth-2 pipeline)
+        return pool[(i + 2) % len(pool)] if len(pool) > 2 else None
+
     for i in range(a.warmup):
-        model.train_step(pool[i % len(pool)], nxt(i))
+        model.train_step(pool[i % len(pool)], nxt(i), nxt2(i))
     if dev.type == "cuda":
         torch.cuda.synchronize()
     ctx.barrier()
@@ -166,7 +171,7 @@ def main() -> int:
     t_start = time.perf_counter()
     last = None
     for i in range(a.steps):
-        last = model.train_step(pool[(a.warmup + i) % len(pool)], nxt(a.warmup + i))
+        last = model.train_step(pool[(a.warmup + i) % len(pool)], nxt(a.warmup + i), nxt2(a.warmup + i))
     if dev.type == "cuda":
         torch.cuda.synchronize()
     ctx.barrier()
@@ -213,6 +218,7 @@ def main() -> int:
                 "wire": str(model._exchange.wire.dtype).replace("torch.", "")
                 if model.mode == "shard" else None,
                 "microbatches": model._exchange.nparts if model.mode == "shard" else None,
+                "early_rows": bool(model._exchange.prefetch) if model.mode == "shard" else None,
             },
         }), flush=True)
     fmdist.shutdown()

@@ -170,8 +170,9 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
   m.def(
       "gather_wire",
       [](int R, u64 req, u64 v, long long v_bytes_stride, u64 w, long long w_stride, int vbytes, int scaled,
-         int to_bf16, u64 out, long long rb, int vb, u64 stream) {
+         int to_bf16, u64 out, long long rb, int vb, u64 stream, u64 idx, u64 run_off, int W) {
         fm::GatherWireArgs a{};
+        a.idx = P<const int>(idx); a.run_off = P<const int>(run_off); a.W = W;
         a.R = R; a.req = P<const int>(req); a.v = P<const void>(v); a.v_bytes_stride = v_bytes_stride;
         a.w = P<const float>(w); a.w_stride = w_stride; a.vbytes = vbytes; a.scaled = scaled; a.to_bf16 = to_bf16;
         a.out = P<unsigned char>(out); a.rb = rb; a.vb = vb;
@@ -179,7 +180,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       },
       py::arg("R"), py::arg("req"), py::arg("v"), py::arg("v_bytes_stride"), py::arg("w"), py::arg("w_stride"),
       py::arg("vbytes"), py::arg("scaled"), py::arg("to_bf16"), py::arg("out"), py::arg("rb"), py::arg("vb"),
-      py::arg("stream"));
+      py::arg("stream"), py::arg("idx") = 0, py::arg("run_off") = 0, py::arg("W") = 1);
 
   m.def(
       "apply_rows",
@@ -255,6 +256,43 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       },
       py::arg("n"), py::arg("ids"), py::arg("W"), py::arg("Rps"), py::arg("keys"), py::arg("stream"));
 
+  m.def(
+      "run_member",
+      [](int R, u64 req, int W, u64 run_off, u64 prev, u64 flag, u64 stream) {
+        check(fm::launch_run_member(R, P<const int>(req), W, P<const int>(run_off), P<const int>(prev), P<int>(flag),
+                                    S(stream)),
+              "run_member");
+      },
+      py::arg("R"), py::arg("req"), py::arg("W"), py::arg("run_off"), py::arg("prev"), py::arg("flag"),
+      py::arg("stream"));
+  m.def(
+      "dirty_scan",
+      [](int R, u64 req, int W, u64 run_off, int Wp, u64 prev_off, u64 prev, u64 flag, u64 dcount, u64 stream) {
+        check(fm::launch_dirty_scan(R, P<const int>(req), W, P<const int>(run_off), Wp, P<const int>(prev_off),
+                                    P<const int>(prev), P<int>(flag), P<int>(dcount), S(stream)),
+              "dirty_scan");
+      },
+      py::arg("R"), py::arg("req"), py::arg("W"), py::arg("run_off"), py::arg("Wp"), py::arg("prev_off"),
+      py::arg("prev"), py::arg("flag"), py::arg("dcount"), py::arg("stream"));
+  m.def("select_workspace_bytes", &fm::select_workspace_bytes, py::arg("n"));
+  m.def(
+      "select_flagged",
+      [](int n, u64 flag, u64 out, u64 count, u64 ws, long long ws_bytes, u64 stream) {
+        check(fm::launch_select_flagged(n, P<const int>(flag), P<int>(out), P<int>(count), P<void>(ws),
+                                        (size_t)ws_bytes, S(stream)),
+              "select_flagged");
+      },
+      py::arg("n"), py::arg("flag"), py::arg("out"), py::arg("count"), py::arg("ws"), py::arg("ws_bytes"),
+      py::arg("stream"));
+  m.def(
+      "patch_scatter",
+      [](int D, u64 recv, long long rb, int W, u64 recv_off, u64 sc_start, u64 gathered, u64 stream) {
+        check(fm::launch_patch_scatter(D, P<const unsigned char>(recv), rb, W, P<const int>(recv_off),
+                                       P<const int>(sc_start), P<unsigned char>(gathered), S(stream)),
+              "patch_scatter");
+      },
+      py::arg("D"), py::arg("recv"), py::arg("rb"), py::arg("W"), py::arg("recv_off"), py::arg("sc_start"),
+      py::arg("gathered"), py::arg("stream"));
   m.def("parse_workspace_bytes", &fm::parse_workspace_bytes, py::arg("n"));
   m.def(
       "parse",

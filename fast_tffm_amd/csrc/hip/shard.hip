@@ -4,9 +4,12 @@
 // optimizer once (replaces the PS-side embedding gather and SparseApplyAdagrad
 // that the reference gets from TF's gRPC runtime, tffm/fm_model.py:291, :341-348).
 #include <algorithm>
+#include <rocprim/rocprim.hpp>
 #include "fm_common.h"
 
 namespace fm {
+
+constexpr int kMaxRuns = 64;  // source ranks handled by the early-exchange kernels
 
 // ---------------------------------------------------------------------------
 // Row-sharded helpers
@@ -69,6 +72,11 @@ struct GatherWireArgs {
   int to_bf16;              // 1: fp32 table -> bf16 wire (Kp % 8 == 0)
   unsigned char* out; long long rb;          // [R, rb] wire rows
   int vb;                   // byte offset of w inside a wire row
+  // patch gathers (early row exchange): row p is req[idx[p]], and the tail's last word
+  // carries its tag idx[p] - run_off[run of idx[p]] (its position in its source's run)
+  const int* idx;           // [R] or null
+  const int* run_off;       // [W+1] (with idx)
+  int W;
 };
 
 // One lane group per row; lane t moves 16 bytes of the wire row's v section
@@ -82,7 +90,8 @@ __global__ __launch_bounds__(kBlock) void gather_wire_kernel(GatherWireArgs a) {
   const int nunits = out_bytes / UNIT;
   const int ngroups = gridDim.x * kWavesPerBlock * G;
   for (int p = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g; p < a.R; p += ngroups) {
-    const long long row = a.req[p];
+    const int ip = a.idx ? a.idx[p] : p;
+    const long long row = a.req[ip];
     const unsigned char* src = reinterpret_cast<const unsigned char*>(a.v) + row * a.v_bytes_stride;
     unsigned char* dst = a.out + (long long)p * a.rb;
     for (int u = t; u < nunits; u += LPR) {
@@ -108,7 +117,13 @@ __global__ __launch_bounds__(kBlock) void gather_wire_kernel(GatherWireArgs a) {
       tail[0] = a.w[row * a.w_stride];
       tail[1] = a.scaled ? a.w[row * a.w_stride + 1] : 0.f;
       tail[2] = 0.f;
-      tail[3] = 0.f;
+      int tag = 0;
+      if (a.idx) {
+        int q = 0;
+        while (q + 1 < a.W && a.run_off[q + 1] <= ip) ++q;
+        tag = ip - a.run_off[q];
+      }
+      reinterpret_cast<int*>(tail)[3] = tag;
     }
   }
 }
@@ -282,6 +297,130 @@ __global__ __launch_bounds__(kBlock) void owner_match_kernel(int R, int W, const
     }
     match[p] = (lo < end && req[lo] == key) ? lo : -1;
   }
+}
+
+// Membership of every row of a (next step's) request list in a previous request
+// list given as W ascending runs: flag[i] = 1 when some run holds req[i] (the row is
+// updated by that step's apply, so its early-gathered copy must be patched).
+__global__ __launch_bounds__(kBlock) void run_member_kernel(int R, const int* req, int W, const int* run_off,
+                                                            const int* prev, int* flag) {
+  for (int i = blockIdx.x * kBlock + threadIdx.x; i < R; i += gridDim.x * kBlock) {
+    const int key = req[i];
+    int hit = 0;
+    for (int q = 0; q < W && !hit; ++q) {
+      int lo = run_off[q];
+      const int end = run_off[q + 1];
+      int hi = end;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (prev[mid] < key) lo = mid + 1; else hi = mid;
+      }
+      hit = lo < end && prev[lo] == key;
+    }
+    flag[i] = hit;
+  }
+}
+
+// Early row exchange, owner side: flag[i] = 1 when request i (a row of the next step)
+// is in the previous step's request runs (the previous step's apply updates it), and
+// dcount[q] = number of flagged requests in run q of the next step (per source rank).
+__global__ __launch_bounds__(kBlock) void dirty_scan_kernel(int R, const int* req, int W, const int* run_off,
+                                                            int Wp, const int* prev_off, const int* prev, int* flag,
+                                                            int* dcount) {
+  __shared__ int cnt[kMaxRuns];
+  __shared__ int off[kMaxRuns + 1];
+  for (int q = threadIdx.x; q <= W; q += kBlock) {
+    if (q < W) cnt[q] = 0;
+    off[q] = run_off[q];
+  }
+  __syncthreads();
+  for (int i = blockIdx.x * kBlock + threadIdx.x; i < R; i += gridDim.x * kBlock) {
+    const int key = req[i];
+    int hit = 0;
+    for (int q = 0; q < Wp && !hit; ++q) {
+      int lo = prev_off[q];
+      const int end = prev_off[q + 1];
+      int hi = end;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (prev[mid] < key) lo = mid + 1; else hi = mid;
+      }
+      hit = lo < end && prev[lo] == key;
+    }
+    flag[i] = hit;
+    if (hit) {
+      int q = 0;
+      while (q + 1 < W && off[q + 1] <= i) ++q;
+      atomicAdd(&cnt[q], 1);
+    }
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < W; q += kBlock)
+    if (cnt[q]) atomicAdd(&dcount[q], cnt[q]);
+}
+
+// Early row exchange, requester side: patch row p (rank-major by owner, recv_off) goes to
+// gathered row sc_start[owner] + tag (the tag = its index among this rank's requests to
+// that owner, written by the owner's patch gather).  One lane group moves one row.
+__global__ __launch_bounds__(kBlock) void patch_scatter_kernel(int D, const unsigned char* recv, long long rb,
+                                                               int W, const int* recv_off, const int* sc_start,
+                                                               unsigned char* gathered) {
+  constexpr int LPR = 16;
+  constexpr int G = kWave / LPR;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPR, t = lane % LPR;
+  const int nunits = (int)(rb / 16);
+  const int ngroups = gridDim.x * kWavesPerBlock * G;
+  for (int p = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g; p < D; p += ngroups) {
+    const unsigned char* src = recv + (long long)p * rb;
+    int q = 0;
+    while (q + 1 < W && recv_off[q + 1] <= p) ++q;
+    const int tag = reinterpret_cast<const int*>(src + rb - 4)[0];
+    unsigned char* dst = gathered + (long long)(sc_start[q] + tag) * rb;
+    for (int u = t; u < nunits; u += LPR)
+      reinterpret_cast<uint4*>(dst)[u] = reinterpret_cast<const uint4*>(src)[u];
+  }
+}
+
+int launch_dirty_scan(int R, const int* req, int W, const int* run_off, int Wp, const int* prev_off, const int* prev,
+                      int* flag, int* dcount, hipStream_t st) {
+  if (W > kMaxRuns) return -8;
+  (void)hipMemsetAsync(dcount, 0, sizeof(int) * W, st);
+  if (R <= 0) return 0;
+  hipLaunchKernelGGL(dirty_scan_kernel, dim3(fill_grid(R, kBlock, 2048)), dim3(kBlock), 0, st, R, req, W, run_off,
+                     Wp, prev_off, prev, flag, dcount);
+  return (int)hipGetLastError();
+}
+
+size_t select_workspace_bytes(int n) {
+  size_t b = 0;
+  (void)rocprim::select((void*)nullptr, b, rocprim::counting_iterator<int>(0), (const int*)nullptr, (int*)nullptr,
+                        (int*)nullptr, (size_t)n, (hipStream_t)0);
+  return b;
+}
+
+// Stream compaction of the flagged positions (ascending): out[0..count) = i with flag[i] != 0.
+int launch_select_flagged(int n, const int* flag, int* out, int* count, void* ws, size_t ws_bytes, hipStream_t st) {
+  if (n <= 0) return (int)hipMemsetAsync(count, 0, sizeof(int), st);
+  size_t b = ws_bytes;
+  return (int)rocprim::select(ws, b, rocprim::counting_iterator<int>(0), flag, out, count, (size_t)n, st);
+}
+
+int launch_patch_scatter(int D, const unsigned char* recv, long long rb, int W, const int* recv_off,
+                         const int* sc_start, unsigned char* gathered, hipStream_t st) {
+  if (D <= 0) return 0;
+  if (rb % 16) return -9;
+  hipLaunchKernelGGL(patch_scatter_kernel, dim3(fill_grid(D, kWavesPerBlock * 4)), dim3(kBlock), 0, st, D, recv, rb,
+                     W, recv_off, sc_start, gathered);
+  return (int)hipGetLastError();
+}
+
+int launch_run_member(int R, const int* req, int W, const int* run_off, const int* prev, int* flag,
+                      hipStream_t st) {
+  if (R <= 0) return 0;
+  hipLaunchKernelGGL(run_member_kernel, dim3(fill_grid(R, kBlock, 8192)), dim3(kBlock), 0, st, R, req, W, run_off,
+                     prev, flag);
+  return (int)hipGetLastError();
 }
 
 template <int LPR, typename TV>

@@ -68,6 +68,7 @@ class FMConfig:
     grad_reduce: str = "sum"          # sum | mean (multi-rank)
     comm_dtype: str = "auto"          # row-sharded wire rows: auto (= storage dtype) | fp32 | bf16
     microbatches: int = 0             # row-sharded step: parts per batch overlapping the exchange (0/1 = one)
+    prefetch_rows: str = "auto"       # row-sharded step: early row exchange + patch (auto = on when world > 1)
     dedup_chunk: int = 32             # CH of the segmented backward
     threads: int = 0                  # CPU kernels (0 = OpenMP default)
     global_bias: bool = False         # learned global bias b0 (extension; the reference has none)
@@ -373,12 +374,12 @@ class FactorizationMachine:
         return out
 
     # ------------------------------------------------------------------
-    def train_step(self, b: Batch, next_batch: Batch | None = None) -> StepOut:
+    def train_step(self, b: Batch, next_batch: Batch | None = None, next2: Batch | None = None) -> StepOut:
         """One synchronous training step on ``b``.
 
-        ``next_batch`` (optional lookahead): the batch of the following call;
-        multi-rank executors prepare its table-independent work (dedup, id
-        exchange) concurrently with this step."""
+        ``next_batch`` / ``next2`` (optional lookahead): the batches of the following
+        calls; the executors prepare their table-independent work (dedup, id exchange,
+        early row exchange) concurrently with this step."""
         if self._ring is not None and (k := self._ring.index(b, next_batch)) >= 0:
             out = self._ring.replay(k)
         elif self._graph is not None and self._graph.matches(b):
@@ -392,7 +393,7 @@ class FactorizationMachine:
         else:
             self.ws.ensure(b.B, b.nnz)
             if getattr(self._exchange, "supports_lookahead", False):
-                out = self._exchange.train_step(b, next_batch)
+                out = self._exchange.train_step(b, next_batch, next2)
             elif self._exchange is not None:
                 out = self._exchange.train_step(b)
             elif self.device.type == "cuda" and (next_batch is not None or self._lpending is not None):

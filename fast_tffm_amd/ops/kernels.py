@@ -688,15 +688,22 @@ class WireFormat:
 
 
 def gather_wire(req: torch.Tensor, table: TableState, fmt: WireFormat, out: torch.Tensor,
-                threads: int = 0) -> torch.Tensor:
-    """Owner side of a sharded lookup: wire rows of table rows ``req`` into ``out`` (``fmt.empty``)."""
-    if fmt.fp32 and table.v.dtype == torch.float32:
+                threads: int = 0, idx: torch.Tensor | None = None, run_off: torch.Tensor | None = None,
+                W: int = 1) -> torch.Tensor:
+    """Owner side of a sharded lookup: wire rows of table rows ``req`` into ``out`` (``fmt.empty``).
+
+    With ``idx`` (GPU; patch gathers of the early row exchange) row p is ``req[idx[p]]``
+    and its last tail word gets the tag ``idx[p] - run_off[run]`` (W ascending runs)."""
+    if fmt.fp32 and table.v.dtype == torch.float32 and idx is None:
         return gather_rows(req, table, fmt.Kp, out, threads=threads)
-    _check(_is_gpu(req), "non-fp32 wire formats are a GPU path")
-    R = req.numel()
-    _chk_vec(req, torch.int32, R, "req", req.device)
-    _check(out.dtype == torch.uint8 and out.is_contiguous() and out.shape[0] >= R and out.shape[1] == fmt.rb,
-           "out: [R, rb] uint8 wire buffer")
+    _check(_is_gpu(req), "non-fp32 wire formats and tagged gathers are a GPU path")
+    R = req.numel() if idx is None else idx.numel()
+    _chk_vec(req, torch.int32, None, "req", req.device)
+    if idx is not None:
+        _chk_vec(idx, torch.int32, R, "idx", req.device)
+        _chk_vec(run_off, torch.int32, W + 1, "run_off", req.device)
+    ok = out.is_contiguous() and out.shape[0] >= R and out.shape[1] * out.element_size() == fmt.rb
+    _check(ok and out.dtype in (torch.uint8, torch.float32), "out: [R, rb bytes] wire buffer")
     v = table.v
     _chk_rows(v, fmt.Kp, "v")
     _range_check(req, v.shape[0], "req")
@@ -705,8 +712,35 @@ def gather_wire(req: torch.Tensor, table: TableState, fmt: WireFormat, out: torc
     native.hip().gather_wire(R=R, req=_p(req), v=_p(v), v_bytes_stride=v.stride(0) * v.element_size(),
                              w=_p(table.w), w_stride=table.w.stride(0), vbytes=fmt.Kp * v.element_size(),
                              scaled=int(v.dtype == FP8), to_bf16=int(to_bf16), out=_p(out), rb=fmt.rb, vb=fmt.vb,
-                             stream=_stream(req))
+                             stream=_stream(req), idx=_p(idx), run_off=_p(run_off), W=int(W))
     return out
+
+
+def dirty_scan(req: torch.Tensor, run_off: torch.Tensor, W: int, prev: torch.Tensor, prev_off: torch.Tensor,
+               Wp: int, flag: torch.Tensor, dcount: torch.Tensor) -> None:
+    """GPU: flag[i] = req[i] in any of the Wp runs of ``prev``; dcount[q] = flagged per run q of ``req``."""
+    R = req.numel()
+    native.hip().dirty_scan(R=R, req=_p(req), W=int(W), run_off=_p(run_off), Wp=int(Wp), prev_off=_p(prev_off),
+                            prev=_p(prev), flag=_p(flag), dcount=_p(dcount), stream=_stream(req))
+
+
+def select_flagged(flag: torch.Tensor, out: torch.Tensor, count: torch.Tensor, ws: torch.Tensor) -> None:
+    """GPU stream compaction: out[0..count) = ascending i with flag[i] != 0 (no host sync)."""
+    n = flag.numel()
+    native.hip().select_flagged(n=n, flag=_p(flag), out=_p(out), count=_p(count), ws=_p(ws), ws_bytes=ws.numel(),
+                                stream=_stream(flag))
+
+
+def select_workspace(n: int, device) -> torch.Tensor:
+    return torch.empty(max(native.hip().select_workspace_bytes(max(n, 1)), 1), dtype=torch.uint8, device=device)
+
+
+def patch_scatter(recv: torch.Tensor, n: int, W: int, recv_off: torch.Tensor, sc_start: torch.Tensor,
+                  gathered: torch.Tensor) -> None:
+    """GPU: wire row p of ``recv`` (rank-major by owner, ``recv_off``) -> ``gathered[sc_start[owner] + tag]``."""
+    rb = recv.shape[1] * recv.element_size()
+    native.hip().patch_scatter(D=int(n), recv=_p(recv), rb=rb, W=int(W), recv_off=_p(recv_off),
+                               sc_start=_p(sc_start), gathered=_p(gathered), stream=_stream(recv))
 
 
 # ---------------------------------------------------------------------------
@@ -754,3 +788,22 @@ def parse_gpu(buf: torch.Tensor, line_start: torch.Tensor, vocab_size: int, hash
     info = torch.cat([status, offsets[n:]]).cpu()   # one D2H: (fallback, max_feats, non-unit, -, nnz)
     fb, mf, nonunit, nnz = int(info[0]), int(info[1]), int(info[2]), int(info[4])
     return ParsedGpu(labels, offsets, ids[:nnz], vals[:nnz] if nonunit else None, nnz, mf, bool(fb))
+
+
+def run_member(req: torch.Tensor, prev: torch.Tensor, prev_run_off: torch.Tensor | None,
+               prev_splits: list[int]) -> torch.Tensor:
+    """int32 flag per element of ``req``: 1 when the row is in ``prev`` (W ascending runs of
+    ``prev_splits`` rows, device offsets ``prev_run_off`` on the GPU), else 0."""
+    R = req.numel()
+    flag = torch.empty(R, dtype=torch.int32, device=req.device)
+    if R == 0:
+        return flag
+    P = int(sum(prev_splits))
+    if not _is_gpu(req):
+        return torch.isin(req, prev[:P]).to(torch.int32)
+    _chk_vec(req, torch.int32, R, "req", req.device)
+    _chk_vec(prev, torch.int32, P, "prev", req.device)
+    _chk_vec(prev_run_off, torch.int32, len(prev_splits) + 1, "prev_run_off", req.device)
+    native.hip().run_member(R=R, req=_p(req), W=len(prev_splits), run_off=_p(prev_run_off), prev=_p(prev),
+                            flag=_p(flag), stream=_stream(req))
+    return flag

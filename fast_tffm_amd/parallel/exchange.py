@@ -83,7 +83,19 @@ class _ShardPlan:
     over all parts' received requests (``req_recv`` holds part 0's runs, then
     part 1's, ...; ``run_off`` the W * parts run boundaries)."""
 
-    __slots__ = ("b", "slot", "parts", "U", "R", "req_recv", "run_off", "splits", "match", "ready")
+    __slots__ = ("b", "slot", "parts", "U", "R", "req_recv", "run_off", "splits", "match", "ready", "early",
+                 "train", "counts", "counts_ev")
+
+
+class _Early:
+    """Rows of a plan gathered and exchanged ahead of time (during the previous step),
+    plus what must be re-sent once the previous step's update has landed: the requests
+    (rows) that the previous step also updated -- "dirty" -- with their index in their
+    source's run (the tag), per-source counts both ways, and the requester-side base
+    position of every patch row it will receive."""
+
+    __slots__ = ("gathered", "dirty_rows", "dtags", "dsend", "drecv", "dpos", "didx", "sc_start", "ev", "work",
+                 "rows_send")
 
 
 class _PlanSlot:
@@ -131,6 +143,20 @@ class _PlanSlot:
                                      dtype=torch.int32, device=dev)
         return self.match
 
+    def early_ws(self, R: int, W: int, dev) -> dict:
+        """Buffers of the early row exchange (device scratch, pinned staging), grown on demand."""
+        ew = getattr(self, "_early", None)
+        if ew is None or ew["R"] < R or ew["W"] != W:
+            cap = max(R, 1, int(1.25 * (ew["R"] if ew else 0)))
+            i32 = dict(dtype=torch.int32, device=dev)
+            ew = dict(R=cap, W=W, flag=torch.empty(cap, **i32), didx=torch.empty(cap, **i32),
+                      dcount=torch.empty(W + 1, **i32), sel=K.select_workspace(cap, dev),
+                      drecv=torch.empty(W, **i32),
+                      dsend_h=torch.empty((2, W), dtype=torch.int32, pin_memory=True),
+                      sc_h=torch.empty(W, dtype=torch.int32, pin_memory=True), sc=torch.empty(W, **i32))
+            self._early = ew
+        return ew
+
     def ensure2(self, n: int, dev) -> K.DedupWorkspace:
         if self.dd2 is None or self.dd2.cap < n:
             self.dd2 = K.DedupWorkspace(max(n, 1, int(1.25 * (self.dd2.cap if self.dd2 else 0))), dev)
@@ -171,19 +197,30 @@ class ShardExchange(_Base):
         super().__init__(model)
         self.Rps = model.rps
         self.key_bits = bits_for(self.W * self.Rps)
-        self.slots = [_PlanSlot(), _PlanSlot()]
+        self.slots = [_PlanSlot(), _PlanSlot(), _PlanSlot()]  # current, next, next-but-one plans
         # wire format of the gathered rows: storage dtype (exact) or bf16 for fp32 tables on request
         tdt = model.table.v.dtype
         self.wire = K.WireFormat.make(tdt, self.Kp, model.cfg.comm_dtype if self.dev.type == "cuda" else "fp32")
         mb = int(getattr(model.cfg, "microbatches", 0) or 0)
         self.nparts = max(1, mb)
+        # early row exchange (exact): rows of step t+1 are gathered and exchanged while step t
+        # computes; after step t's update only the rows it touched are re-sent (patch)
+        pr = str(getattr(model.cfg, "prefetch_rows", "auto")).lower()
+        forced = pr in ("on", "true", "1")
+        self.prefetch = self.nparts == 1 and (forced or (pr == "auto" and self.W > 1))
+        # with only one batch of lookahead the early exchange sits at the end of the plan chain
+        # (which can then become the critical path): "auto" uses it with two batches of lookahead
+        self.prefetch_depth1 = self.prefetch and forced
+        self.cur_plan: _ShardPlan | None = None
+        self.step_start = None
+        self.early_steps = 0          # steps that took the early-exchange + patch path
         # lookahead plans talk on their own communicator (own RCCL stream): the id
         # all-to-all of batch t+1 does not queue behind step t's row / grad all-to-alls
         self.plan_group = (dist.new_group(ranks=list(range(self.W)), backend=dist.get_backend(self.group))
                            if self.W > 1 else self.group)
         self.cpu_group = self.ctx.cpu_group or self.group
-        self.last_slot = 1
-        self.pending: _ShardPlan | None = None
+        self.last_slot = len(self.slots) - 1
+        self.pending: list[_ShardPlan] = []   # built plans of upcoming batches, in order
         self._prep = None
 
     def _prep_stream(self):
@@ -201,19 +238,42 @@ class ShardExchange(_Base):
         nz = [0] + [b.host_offset(c) for c in cuts[1:-1]] + [b.nnz]
         return [(cuts[i], cuts[i + 1], nz[i], nz[i + 1]) for i in range(nparts)]
 
-    def _plan(self, b: Batch, train: bool, inputs_ready=None) -> _ShardPlan:
-        """Build the plan of ``b`` (on the side stream when on the GPU).
+    def _plan(self, b: Batch, train: bool, inputs_ready=None, early: bool = True) -> _ShardPlan:
+        """Build the whole plan of ``b`` now (start + finish)."""
+        pl = self._plan_start(b, train, inputs_ready)
+        self._plan_finish(pl, early)
+        return pl
+
+    def _side_ctx(self):
+        if self.dev.type == "cuda":
+            return torch.cuda.stream(self._prep_stream())
+        import contextlib
+
+        return contextlib.nullcontext()
+
+    def _plan_start(self, b: Batch, train: bool, inputs_ready=None) -> _ShardPlan:
+        """First half of a plan, host-asynchronous (side stream on the GPU): dedup of every part
+        and the per-owner counts, copied to pinned host memory behind an event.  The host does
+        not wait for this dedup; ``_plan_finish`` reads the counts one call later.
 
         ``inputs_ready``: main-stream event after which ``b``'s tensors are valid
         (default: everything enqueued on the current stream so far)."""
         m = self.m
-        # never the slot of a pending (not yet consumed) plan; the other slot's last user
-        # step is waited for through its done event
-        idx = (self.pending.slot ^ 1) if self.pending is not None else (self.last_slot ^ 1)
+        # round robin over the slots: never the slot of a pending (not yet consumed) plan or of
+        # the current step's plan; the last step that used the slot is waited for (done event)
+        busy = {p.slot for p in self.pending}
+        if self.cur_plan is not None:
+            busy.add(self.cur_plan.slot)
+        idx = self.last_slot
+        for _ in range(len(self.slots)):
+            idx = (idx + 1) % len(self.slots)
+            if idx not in busy:
+                break
         self.last_slot = idx
         slot = self.slots[idx]
         pl = _ShardPlan()
-        pl.b, pl.slot = b, idx
+        pl.b, pl.slot, pl.train = b, idx, train
+        pl.early = pl.splits = pl.run_off = pl.match = pl.ready = None
         gpu = self.dev.type == "cuda"
         if gpu:
             st = self._prep_stream()
@@ -227,13 +287,8 @@ class ShardExchange(_Base):
             for t in (b.labels, b.offsets, b.ids, b.vals, b.weights):
                 if t is not None:
                     t.record_stream(st)
-            ctx = torch.cuda.stream(st)
-        else:
-            import contextlib
-
-            ctx = contextlib.nullcontext()
         ranges = self._split(b, self.nparts if train else 1)
-        with ctx:
+        with self._side_ctx():
             pl.parts = []
             counts = []
             for k, (e0, e1, n0, n1) in enumerate(ranges):
@@ -253,16 +308,43 @@ class ShardExchange(_Base):
                                   dense_min=K.dense_min_for(sb.B, self.m.Kp, m.cfg.dedup_chunk) if train else 0)
                 counts.append(K.owner_counts(part.dd, self.Rps, self.W))
                 pl.parts.append(part)
-            P = len(pl.parts)
-            # per-owner counts of all parts: one small D2H on this (side) stream -- the only
-            # host sync of the step, it waits for these dedups only -- and one count exchange
-            # on the CPU group: row q of the [W, P] matrix is what goes to / comes from rank q
-            sc = torch.stack(counts, dim=1).cpu()
-            if self.W == 1:
-                rc = sc
+            c = torch.stack(counts, dim=1)     # [W, P]: row q = what goes to rank q
+            if gpu:
+                # the count exchange runs on the device (RCCL, plan communicator) right behind the
+                # dedup: [0] = sent counts, [1] = received counts, both copied to pinned memory
+                both = torch.empty((2,) + tuple(c.shape), dtype=c.dtype, device=self.dev)
+                both[0].copy_(c)
+                if self.W == 1:
+                    both[1].copy_(c)
+                else:
+                    dist.all_to_all_single(both[1], both[0], group=self.plan_group)
+                pl.counts = torch.empty(both.shape, dtype=c.dtype, pin_memory=True)
+                pl.counts.copy_(both, non_blocking=True)
+                pl.counts_ev = torch.cuda.Event()
+                pl.counts_ev.record(torch.cuda.current_stream(self.dev))
             else:
-                rc = torch.empty_like(sc)
-                dist.all_to_all_single(rc, sc, group=self.cpu_group)
+                pl.counts, pl.counts_ev = c, None
+        return pl
+
+    def _plan_finish(self, pl: _ShardPlan, early: bool = False) -> None:
+        """Second half of a plan: per-owner counts to the host (its dedup finished long ago when
+        the plan was started a call earlier), count exchange on the CPU group, id all-to-all,
+        owner-side run offsets and -- optionally -- the early row exchange; records ``ready``."""
+        if pl.splits is not None:
+            return
+        gpu = self.dev.type == "cuda"
+        slot = self.slots[pl.slot]
+        with self._side_ctx():
+            if pl.counts_ev is not None:  # GPU: both count matrices exchanged on the device
+                pl.counts_ev.synchronize()
+                sc, rc = pl.counts[0].clone(), pl.counts[1].clone()
+            else:
+                sc = pl.counts.clone()
+                if self.W == 1:
+                    rc = sc
+                else:
+                    rc = torch.empty_like(sc)
+                    dist.all_to_all_single(rc, sc, group=self.cpu_group)
             sc_l, rc_l = sc.t().tolist(), rc.t().tolist()
             u_off = r_off = 0
             for k, part in enumerate(pl.parts):
@@ -287,16 +369,193 @@ class ShardExchange(_Base):
             # owner-side grouping of the received requests (W * P ascending runs): device
             # run offsets + match scratch for apply_runs; the CPU path sorts inside apply_runs
             pl.splits = [c for part in pl.parts for c in part.rc]
-            pl.run_off = pl.match = None
-            if train and gpu:
+            if pl.train and gpu:
                 pl.run_off = slot.runs(pl.splits, self.dev)
                 pl.match = slot.match_buf(pl.R * len(pl.splits), self.dev) if len(pl.splits) > 1 else None
+            if early and pl.train and self._early_ok(pl, self.cur_plan):
+                pl.early = self._early(pl, self.cur_plan)
             if gpu:
                 pl.ready = torch.cuda.Event()
-                pl.ready.record(st)
-            else:
-                pl.ready = None
-        return pl
+                pl.ready.record(torch.cuda.current_stream(self.dev))
+
+    def _early_ok(self, pl: _ShardPlan, cur: _ShardPlan | None) -> bool:
+        gpu = self.dev.type == "cuda"
+        return (self.prefetch and len(pl.parts) == 1 and pl.splits is not None and cur is not None
+                and cur.splits is not None and (cur.run_off is not None or not gpu) and len(cur.parts) == 1
+                and (pl.run_off is not None or not gpu))
+
+    def _early(self, pl: _ShardPlan, cur: _ShardPlan) -> _Early:
+        return self._early_gpu(pl, cur) if self.dev.type == "cuda" else self._early_cpu(pl, cur)
+
+    def _early_ahead(self, pl: _ShardPlan, cur: _ShardPlan) -> None:
+        """Depth-2 pipeline: at the start of step t, the early row exchange of the (already
+        built) plan of step t+1 against step t's plan, on the plan stream; its ready event
+        moves past the early work."""
+        gpu = self.dev.type == "cuda"
+        with self._side_ctx():
+            pl.early = self._early(pl, cur)
+            if gpu:
+                pl.ready = torch.cuda.Event()
+                pl.ready.record(torch.cuda.current_stream(self.dev))
+
+    def _patch(self, pl: _ShardPlan) -> tuple[torch.Tensor, torch.Tensor]:
+        return self._patch_gpu(pl) if self.dev.type == "cuda" else self._patch_cpu(pl)
+
+    def _early_gpu(self, pl: _ShardPlan, cur: _ShardPlan) -> _Early:
+        """GPU version of ``_early_cpu``: one scan kernel (membership + per-source dirty counts),
+        a rocPRIM compaction of the dirty positions, an async D2H of the counts, then the early
+        gather + row all-to-all -- no host sync and no per-element torch ops."""
+        dev, W = self.dev, self.W
+        part = pl.parts[0]
+        R, U = pl.R, pl.U
+        req = pl.req_recv[:R]
+        slot = self.slots[pl.slot]
+        e = _Early()
+        ew = slot.early_ws(R, W, dev)             # this slot's buffers (free again two plans later)
+        flag, e.didx, dcount = ew["flag"], ew["didx"], ew["dcount"]  # dcount: [W] per source, [W] total
+        K.dirty_scan(req, pl.run_off, W, cur.req_recv, cur.run_off, len(cur.splits), flag, dcount)
+        K.select_flagged(flag[:R], e.didx, dcount[W:], ew["sel"])
+        # dirty counts: sent (per source rank) and received (per owner), exchanged on the device
+        drecv = ew["drecv"]
+        if W == 1:
+            drecv.copy_(dcount[:W])
+        else:
+            dist.all_to_all_single(drecv, dcount[:W], group=self.plan_group)
+        e.dsend = ew["dsend_h"]
+        e.dsend[0].copy_(dcount[:W], non_blocking=True)
+        e.dsend[1].copy_(drecv, non_blocking=True)
+        e.ev = torch.cuda.Event()
+        e.ev.record(torch.cuda.current_stream(dev))
+        h = ew["sc_h"].numpy()
+        h[0] = 0
+        np.cumsum(part.sc[:-1], out=h[1:W])
+        e.sc_start = ew["sc"]
+        e.sc_start.copy_(ew["sc_h"], non_blocking=True)
+        if self.step_start is not None:
+            torch.cuda.current_stream(dev).wait_event(self.step_start)
+        rows_send = self.wire.empty(R, dev)
+        K.gather_wire(req, self.m.table.state, self.wire, rows_send, threads=self.m.cfg.threads)
+        e.work = None
+        if W == 1:
+            e.gathered = rows_send
+        else:
+            # asynchronous: the plan stream goes on (next dedup) while the rows travel; the
+            # compute stream waits for this work before it patches / reads the rows
+            e.gathered = self.wire.empty(U, dev)
+            e.rows_send = rows_send
+            e.work = dist.all_to_all_single(e.gathered, rows_send, part.sc, part.rc, group=self.plan_group,
+                                            async_op=True)
+        return e
+
+    def _patch_gpu(self, pl: _ShardPlan) -> tuple[torch.Tensor, torch.Tensor]:
+        """GPU version of ``_patch_cpu``: one tagged gather of the dirty rows, the patch
+        all-to-all, one scatter kernel into the early copies."""
+        e, dev, W = pl.early, self.dev, self.W
+        e.ev.synchronize()  # dirty counts (sent, received) on the host -- long done by now
+        ds, dr = e.dsend[0].tolist(), e.dsend[1].tolist()
+        D, Dr = int(sum(ds)), int(sum(dr))
+        patch = self.wire.empty(D, dev)
+        if D:
+            K.gather_wire(pl.req_recv, self.m.table.state, self.wire, patch, threads=self.m.cfg.threads,
+                          idx=e.didx[:D], run_off=pl.run_off, W=W)
+        if W == 1:
+            recv = patch
+        else:
+            recv = self.wire.empty(Dr, dev)
+            _a2a(recv, patch, dr, ds, self.group)
+        if e.work is not None:
+            e.work.wait()   # the early rows have arrived (compute stream waits on the RCCL stream)
+            e.work = e.rows_send = None
+        if Dr:
+            off = np.zeros(W + 1, dtype=np.int32)
+            off[1:] = np.cumsum(dr)
+            recv_off = torch.from_numpy(off).pin_memory().to(dev, non_blocking=True)
+            K.patch_scatter(recv, Dr, W, recv_off, e.sc_start, e.gathered)
+        return self.wire.views(e.gathered)
+
+    def _early_cpu(self, pl: _ShardPlan, cur: _ShardPlan) -> _Early:
+        """(side stream) Gather + exchange all rows of ``pl`` now, and work out which of them
+        the step being computed (plan ``cur``) will update: those are re-gathered and sent
+        again after that update (``_patch``).  The clean rows' values are final already: only
+        ``cur``'s apply writes the table until then, and this gather is ordered after the
+        previous step's apply (``step_start``).  No host sync here: the dirty counts travel
+        to the host asynchronously and are read by the next step."""
+        dev, W = self.dev, self.W
+        gpu = dev.type == "cuda"
+        part = pl.parts[0]
+        R, U = pl.R, pl.U
+        req = pl.req_recv[:R]
+        i64 = dict(dtype=torch.int64, device=dev)
+
+        def h2d(vals):  # small host list -> device without a blocking copy
+            t = torch.tensor(vals, dtype=torch.int64)
+            return t.pin_memory().to(dev, non_blocking=True) if gpu else t
+
+        flags = K.run_member(req, cur.req_recv, cur.run_off, cur.splits)
+        run_of = torch.repeat_interleave(torch.arange(W, **i64), h2d(part.rc), output_size=R)
+        e = _Early()
+        dsend = torch.zeros(W, **i64).index_add_(0, run_of, flags.to(torch.int64))
+        # compaction of the dirty positions without knowing their number on the host:
+        # slot R collects the clean ones, [0, D) the dirty ones in order
+        pos = torch.where(flags.bool(), torch.cumsum(flags, 0) - 1, torch.full_like(run_of, R))
+        didx = torch.empty(R + 1, **i64)
+        didx[pos] = torch.arange(R, **i64)
+        didx = didx[:R].clamp_(0, max(R - 1, 0))
+        e.dirty_rows = req[didx]
+        starts = h2d(np.concatenate([[0], np.cumsum(part.rc)[:-1]]).astype(np.int64).tolist())
+        e.dtags = (didx - starts[run_of[didx]]).to(torch.int32)
+        if gpu:
+            e.dsend = torch.empty(W, dtype=torch.int64, pin_memory=True)
+            e.dsend.copy_(dsend, non_blocking=True)
+            e.drecv = torch.cuda.Event()
+            e.drecv.record(torch.cuda.current_stream(dev))  # (the event doubles as "dsend arrived")
+        else:
+            e.dsend, e.drecv = dsend, None
+        e.dpos = h2d(np.concatenate([[0], np.cumsum(part.sc)[:-1]]).astype(np.int64).tolist())  # sc starts
+        if self.step_start is not None:
+            torch.cuda.current_stream(dev).wait_event(self.step_start)
+        rows_send = self.wire.empty(R, dev)
+        K.gather_wire(req, self.m.table.state, self.wire, rows_send, threads=self.m.cfg.threads)
+        if W == 1:
+            e.gathered = rows_send
+        else:
+            e.gathered = self.wire.empty(U, dev)
+            _a2a(e.gathered, rows_send, part.sc, part.rc, self.plan_group)
+        return e
+
+    def _tag_view(self, buf: torch.Tensor) -> torch.Tensor:
+        """int32 view of the last pad word of every wire row (carries a patch row's tag)."""
+        w = buf.view(torch.int32) if buf.dtype != torch.int32 else buf
+        col = (self.Kp + 3) if self.wire.fp32 else (self.wire.vb // 4 + 3)
+        return w[:, col]
+
+    def _patch_cpu(self, pl: _ShardPlan) -> tuple[torch.Tensor, torch.Tensor]:
+        """(compute stream, after the previous step's update) re-gather the dirty rows, send
+        them to their requesters and overwrite the early copies; returns the (v, w) views."""
+        e, dev, W = pl.early, self.dev, self.W
+        if e.drecv is not None:
+            e.drecv.synchronize()  # dirty counts copied to the host (long done by now)
+        dsend = e.dsend.clone()
+        if W == 1:
+            drecv = dsend
+        else:
+            drecv = torch.empty_like(dsend)
+            dist.all_to_all_single(drecv, dsend, group=self.cpu_group)
+        ds, dr = dsend.tolist(), drecv.tolist()
+        D, Dr = int(sum(ds)), int(sum(dr))
+        patch = self.wire.empty(D, dev)
+        K.gather_wire(e.dirty_rows[:D], self.m.table.state, self.wire, patch, threads=self.m.cfg.threads)
+        self._tag_view(patch).copy_(e.dtags[:D])
+        if W == 1:
+            recv = patch
+        else:
+            recv = self.wire.empty(Dr, dev)
+            _a2a(recv, patch, dr, ds, self.group)
+        if Dr:
+            cnt = drecv.pin_memory().to(dev, non_blocking=True) if dev.type == "cuda" else drecv
+            base = torch.repeat_interleave(e.dpos, cnt, output_size=Dr)
+            e.gathered.index_copy_(0, base + self._tag_view(recv).to(torch.int64), recv)
+        return self.wire.views(e.gathered)
 
     def _check_splits(self, part: _Part) -> None:
         """FM_DEBUG_CHECKS=1: the split lists of every rank must form a consistent W x W
@@ -316,11 +575,12 @@ class ShardExchange(_Base):
             raise RuntimeError("sharded key out of range")
 
     def _take_plan(self, b: Batch, train: bool) -> _ShardPlan:
-        pl = self.pending
+        pl = self.pending[0] if self.pending else None
         if pl is not None and pl.b is b and (len(pl.parts) > 1) == (train and self.nparts > 1 and b.B >= 2 * self.nparts):
-            self.pending = None
-        else:  # (a pending plan for another batch, e.g. the next training batch, stays pending)
-            pl = self._plan(b, train)
+            self.pending.pop(0)
+            self._plan_finish(pl)
+        else:  # (pending plans for other batches, e.g. the next training batches, stay pending)
+            pl = self._plan(b, train, early=False)
         if pl.ready is not None:
             main = torch.cuda.current_stream(self.dev)
             main.wait_event(pl.ready)
@@ -328,6 +588,11 @@ class ShardExchange(_Base):
             for part in pl.parts:
                 if part.b is not b:
                     part.b.offsets.record_stream(main)
+            if pl.early is not None:
+                e = pl.early
+                for t in (e.gathered, e.didx, e.sc_start):
+                    if t is not None:
+                        t.record_stream(main)
         return pl
 
     def _gather_part(self, pl: _ShardPlan, part: _Part, async_op: bool):
@@ -344,22 +609,46 @@ class ShardExchange(_Base):
         work = dist.all_to_all_single(gathered, rows_send, part.sc, part.rc, group=self.group, async_op=async_op)
         return gathered, work
 
-    def train_step(self, b: Batch, next_batch: Batch | None = None):
+    def train_step(self, b: Batch, next_batch: Batch | None = None, next2: Batch | None = None):
+        """One step on ``b``.  ``next_batch`` / ``next2``: the batches of the next two calls.
+
+        Depth-1 (``next_batch`` only): the plan of the next batch is built at the end of this
+        step (and, with early rows, its early exchange right after).  Depth-2 (both): the plan
+        of ``next2`` is built at the end of this step, and at the start of this step the early
+        row exchange of the next batch (planned during the previous step) is launched, so the
+        whole table-independent half of a step and its row exchange have a full step of slack."""
         from ..models.fm import StepOut
 
         m, ws, cfg, Kp = self.m, self.m.ws, self.m.cfg, self.Kp
         gpu = self.dev.type == "cuda"
+        build = next2 if next2 is not None else next_batch
         nb_ready = None
-        if next_batch is not None and gpu and getattr(next_batch, "ready", None) is None:
-            nb_ready = torch.cuda.Event()  # next_batch's producers: all work enqueued before this step
+        if build is not None and gpu and getattr(build, "ready", None) is None:
+            nb_ready = torch.cuda.Event()  # the batch's producers: all work enqueued before this step
             nb_ready.record(torch.cuda.current_stream(self.dev))
+        if gpu:
+            self.step_start = torch.cuda.Event()  # after the previous step's apply (early gathers wait on it)
+            self.step_start.record(torch.cuda.current_stream(self.dev))
         with roctx_range("plan"):
             pl = self._take_plan(b, True)
+        self.cur_plan = pl
+        if self.pending and next_batch is not None and self.pending[0].b is next_batch:
+            nxt_pl = self.pending[0]
+            with roctx_range("plan_finish_next"):
+                self._plan_finish(nxt_pl)   # counts ready since the last step: no wait
+            if nxt_pl.early is None and self._early_ok(nxt_pl, pl):
+                with roctx_range("early_rows_next"):
+                    self._early_ahead(nxt_pl, pl)
         wf = self.wire
         # every part's rows are gathered first and their all-to-alls queued on RCCL's stream
         # (async): part k+1's rows travel while part k computes
         with roctx_range("gather+a2a_rows"):
-            rows = [self._gather_part(pl, part, async_op=True) for part in pl.parts]
+            if pl.early is not None:
+                rows = [(None, None)]
+                early_views = self._patch(pl)
+                self.early_steps += 1
+            else:
+                rows = [self._gather_part(pl, part, async_op=True) for part in pl.parts]
         grad_send = wf.empty_grads(max(pl.U, 1), self.dev)
         grad_recv = grad_send if self.W == 1 else wf.empty_grads(max(pl.R, 1), self.dev)
         gworks = []
@@ -370,7 +659,7 @@ class ShardExchange(_Base):
             sb, dd, e0 = part.b, part.dd, part.e0
             if work is not None:
                 work.wait()               # the compute stream waits for this part's rows
-            src_v, src_w = wf.views(buf)
+            src_v, src_w = wf.views(buf) if buf is not None else early_views
             with roctx_range("fwd"):
                 fo = K.fm_forward(sb.offsets, dd.inv[: sb.nnz], sb.vals, src_v, src_w, Kp, labels=sb.labels,
                                   weights=sb.weights, loss=cfg.loss_type, grad_scale=gscale, want_r1=True,
@@ -399,9 +688,18 @@ class ShardExchange(_Base):
             done = torch.cuda.Event()
             done.record(torch.cuda.current_stream(self.dev))
             self.slots[pl.slot].done = done
-        if next_batch is not None:
+        if next2 is not None and not any(p.b is next2 for p in self.pending):
+            if not any(p.b is next_batch for p in self.pending) and next_batch is not None:
+                with roctx_range("plan_next"):  # (first depth-2 step: the next batch has no plan yet)
+                    self.pending.append(self._plan(next_batch, True, nb_ready, early=True))
+            with roctx_range("plan_next2"):  # started now, finished at the start of the next step
+                self.pending.append(self._plan_start(next2, True, nb_ready))
+        elif next2 is None and next_batch is not None and not any(p.b is next_batch for p in self.pending):
             with roctx_range("plan_next"):
-                self.pending = self._plan(next_batch, True, nb_ready)
+                if self.prefetch_depth1:  # built in full now, with its early row exchange
+                    self.pending.append(self._plan(next_batch, True, nb_ready, early=True))
+                else:  # started now, finished when the next step takes it
+                    self.pending.append(self._plan_start(next_batch, True, nb_ready))
         return StepOut(loss, b.B)
 
     @torch.no_grad()

@@ -161,16 +161,17 @@ class Trainer:
             return loss, tend
 
         batch, have = fetch()
+        nxt, nhave = fetch() if have else (None, False)
         pending = None
         tprev = time.time()
         while have:
-            # lookahead: the next batch (when every rank has one) lets the sharded executor
-            # build its dedup / id exchange while this step computes
-            nxt, nhave = fetch()
+            # lookahead: the next two batches (when every rank has them) let the executors build
+            # their dedup / id exchange / early row exchange while this step computes
+            nxt2, nhave2 = fetch() if nhave else (None, False)
             if self.trace and prof is None and step_num == start_step + 1:
                 prof = _start_profiler()
             with roctx_range("train_step"):
-                out = self.model.train_step(batch, nxt if nhave else None)
+                out = self.model.train_step(batch, nxt if nhave else None, nxt2 if nhave2 else None)
             step_num = self.model.global_step
             if batch.reader_pos is not None:  # position of the last CONSUMED batch (the reader runs ahead)
                 self.reader_state.epoch, self.reader_state.batches_in_epoch = batch.reader_pos
@@ -197,6 +198,7 @@ class Trainer:
             if ended_early or (c.max_steps is not None and step_num - start_step >= c.max_steps):
                 break
             batch, have = nxt, nhave
+            nxt, nhave = nxt2, nhave2
         if pending is not None:
             last_loss, _ = report(pending)
         if prof is not None:
