@@ -94,8 +94,9 @@ class _Early:
     source's run (the tag), per-source counts both ways, and the requester-side base
     position of every patch row it will receive."""
 
-    __slots__ = ("gathered", "dirty_rows", "dtags", "dsend", "drecv", "dpos", "didx", "sc_start", "ev", "work",
-                 "rows_send")
+    # GPU: gathered, didx, sc_start, dsend (pinned [2, W]: sent / received dirty counts), ev, work,
+    # rows_send; CPU reference: gathered, dirty_rows, dtags, dsend, dpos
+    __slots__ = ("gathered", "dirty_rows", "dtags", "dsend", "dpos", "didx", "sc_start", "ev", "work", "rows_send")
 
 
 class _PlanSlot:
@@ -474,52 +475,30 @@ class ShardExchange(_Base):
         return self.wire.views(e.gathered)
 
     def _early_cpu(self, pl: _ShardPlan, cur: _ShardPlan) -> _Early:
-        """(side stream) Gather + exchange all rows of ``pl`` now, and work out which of them
-        the step being computed (plan ``cur``) will update: those are re-gathered and sent
-        again after that update (``_patch``).  The clean rows' values are final already: only
-        ``cur``'s apply writes the table until then, and this gather is ordered after the
-        previous step's apply (``step_start``).  No host sync here: the dirty counts travel
-        to the host asynchronously and are read by the next step."""
-        dev, W = self.dev, self.W
-        gpu = dev.type == "cuda"
+        """CPU (gloo) reference of the early row exchange with plain torch ops: gather and
+        exchange all rows of ``pl`` now, flag the ones the step being computed (plan ``cur``)
+        will update -- they are re-gathered and re-sent after that update (``_patch_cpu``).
+        The clean rows' values are final already: only ``cur``'s apply writes the table
+        until then.  ``_early_gpu`` is the same with dedicated kernels."""
+        W = self.W
         part = pl.parts[0]
         R, U = pl.R, pl.U
         req = pl.req_recv[:R]
-        i64 = dict(dtype=torch.int64, device=dev)
-
-        def h2d(vals):  # small host list -> device without a blocking copy
-            t = torch.tensor(vals, dtype=torch.int64)
-            return t.pin_memory().to(dev, non_blocking=True) if gpu else t
-
-        flags = K.run_member(req, cur.req_recv, cur.run_off, cur.splits)
-        run_of = torch.repeat_interleave(torch.arange(W, **i64), h2d(part.rc), output_size=R)
+        flags = K.run_member(req, cur.req_recv, cur.run_off, cur.splits).bool()
+        run_of = torch.repeat_interleave(torch.arange(W), torch.tensor(part.rc), output_size=R)
+        didx = torch.nonzero(flags).flatten()
+        starts = torch.tensor(np.concatenate([[0], np.cumsum(part.rc)[:-1]]).astype(np.int64))
         e = _Early()
-        dsend = torch.zeros(W, **i64).index_add_(0, run_of, flags.to(torch.int64))
-        # compaction of the dirty positions without knowing their number on the host:
-        # slot R collects the clean ones, [0, D) the dirty ones in order
-        pos = torch.where(flags.bool(), torch.cumsum(flags, 0) - 1, torch.full_like(run_of, R))
-        didx = torch.empty(R + 1, **i64)
-        didx[pos] = torch.arange(R, **i64)
-        didx = didx[:R].clamp_(0, max(R - 1, 0))
         e.dirty_rows = req[didx]
-        starts = h2d(np.concatenate([[0], np.cumsum(part.rc)[:-1]]).astype(np.int64).tolist())
         e.dtags = (didx - starts[run_of[didx]]).to(torch.int32)
-        if gpu:
-            e.dsend = torch.empty(W, dtype=torch.int64, pin_memory=True)
-            e.dsend.copy_(dsend, non_blocking=True)
-            e.drecv = torch.cuda.Event()
-            e.drecv.record(torch.cuda.current_stream(dev))  # (the event doubles as "dsend arrived")
-        else:
-            e.dsend, e.drecv = dsend, None
-        e.dpos = h2d(np.concatenate([[0], np.cumsum(part.sc)[:-1]]).astype(np.int64).tolist())  # sc starts
-        if self.step_start is not None:
-            torch.cuda.current_stream(dev).wait_event(self.step_start)
-        rows_send = self.wire.empty(R, dev)
+        e.dsend = torch.bincount(run_of[didx], minlength=W)      # dirty rows per source rank
+        e.dpos = torch.tensor(np.concatenate([[0], np.cumsum(part.sc)[:-1]]).astype(np.int64))  # sc starts
+        rows_send = self.wire.empty(R, self.dev)
         K.gather_wire(req, self.m.table.state, self.wire, rows_send, threads=self.m.cfg.threads)
         if W == 1:
             e.gathered = rows_send
         else:
-            e.gathered = self.wire.empty(U, dev)
+            e.gathered = self.wire.empty(U, self.dev)
             _a2a(e.gathered, rows_send, part.sc, part.rc, self.plan_group)
         return e
 
@@ -530,30 +509,27 @@ class ShardExchange(_Base):
         return w[:, col]
 
     def _patch_cpu(self, pl: _ShardPlan) -> tuple[torch.Tensor, torch.Tensor]:
-        """(compute stream, after the previous step's update) re-gather the dirty rows, send
-        them to their requesters and overwrite the early copies; returns the (v, w) views."""
-        e, dev, W = pl.early, self.dev, self.W
-        if e.drecv is not None:
-            e.drecv.synchronize()  # dirty counts copied to the host (long done by now)
-        dsend = e.dsend.clone()
+        """CPU reference of ``_patch_gpu``: after the previous step's update, re-gather the
+        dirty rows (tagged with their index in their source's run), send them to their
+        requesters and overwrite the early copies; returns the (v, w) views."""
+        e, W = pl.early, self.W
+        dsend = e.dsend
         if W == 1:
             drecv = dsend
         else:
             drecv = torch.empty_like(dsend)
             dist.all_to_all_single(drecv, dsend, group=self.cpu_group)
         ds, dr = dsend.tolist(), drecv.tolist()
-        D, Dr = int(sum(ds)), int(sum(dr))
-        patch = self.wire.empty(D, dev)
-        K.gather_wire(e.dirty_rows[:D], self.m.table.state, self.wire, patch, threads=self.m.cfg.threads)
-        self._tag_view(patch).copy_(e.dtags[:D])
+        patch = self.wire.empty(len(e.dirty_rows), self.dev)
+        K.gather_wire(e.dirty_rows, self.m.table.state, self.wire, patch, threads=self.m.cfg.threads)
+        self._tag_view(patch).copy_(e.dtags)
         if W == 1:
             recv = patch
         else:
-            recv = self.wire.empty(Dr, dev)
+            recv = self.wire.empty(int(sum(dr)), self.dev)
             _a2a(recv, patch, dr, ds, self.group)
-        if Dr:
-            cnt = drecv.pin_memory().to(dev, non_blocking=True) if dev.type == "cuda" else drecv
-            base = torch.repeat_interleave(e.dpos, cnt, output_size=Dr)
+        if recv.shape[0]:
+            base = torch.repeat_interleave(e.dpos, drecv)
             e.gathered.index_copy_(0, base + self._tag_view(recv).to(torch.int64), recv)
         return self.wire.views(e.gathered)
 

@@ -1,0 +1,33 @@
+"""bench.py output contract (one JSON line with the driver's keys), exercised on CPU with a
+tiny configuration; the real measurement runs on the GPU (see profiles/)."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def _run(args):
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("args", [["--steps", "2", "--warmup", "1", "--batch", "256", "--slots-per-gpu", "20000"],
+                                  ["--preset", "a1a_cpu", "--steps", "2", "--warmup", "1"]])
+def test_bench_prints_one_json_line(args):
+    d = _run(args)
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["higher_is_better"] is True
+    assert d["value"] > 0 and d["ms_per_step"] > 0 and d["scaling"] == "weak"
+    assert {"model", "global_batch", "seq_len", "parallelism"} <= set(d["config"])
