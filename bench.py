@@ -74,6 +74,8 @@ def main() -> int:
                     help="row-sharded step: parts per batch overlapping the exchange (0/1 = one part)")
     ap.add_argument("--prefetch-rows", default="auto", choices=["auto", "on", "off"],
                     help="row-sharded step: exchange next step's rows early, patch the updated ones (auto: N > 1)")
+    ap.add_argument("--overlap-grads", default="auto", choices=["auto", "on", "off"],
+                    help="row-sharded step: split backward, first half's gradient rows sent early (auto: N > 1)")
     ap.add_argument("--comm-dtype", default="auto", choices=["auto", "fp32", "bf16"],
                     help="row-sharded wire rows (auto = table storage dtype; bf16 rounds fp32 rows for transport)")
     ap.add_argument("--profile-steps", type=int, default=0, help="also emit a torch.profiler trace")
@@ -106,7 +108,8 @@ def main() -> int:
                       initial_accumulator=0.1)
     cfg = FMConfig(vocabulary_size=vocab, factor_num=p["k"], loss_type="logistic", batch_size=a.batch,
                    init_value_range=0.01, seed=42, dtype=dtype, opt=opt, mode=mode, comm_dtype=a.comm_dtype,
-                   microbatches=a.microbatches, prefetch_rows=a.prefetch_rows)
+                   microbatches=a.microbatches, prefetch_rows=a.prefetch_rows,
+                   overlap_grads=a.overlap_grads)
     t0 = time.time()
     model = FactorizationMachine(cfg, device=dev, dist=ctx if W > 1 or mode not in ("auto", "local") else None)
     if dev.type == "cuda":
@@ -219,6 +222,7 @@ def main() -> int:
                 if model.mode == "shard" else None,
                 "microbatches": model._exchange.nparts if model.mode == "shard" else None,
                 "early_rows": bool(model._exchange.prefetch) if model.mode == "shard" else None,
+                "split_grads": bool(model._exchange.overlap_grads) if model.mode == "shard" else None,
             },
         }), flush=True)
     fmdist.shutdown()

@@ -26,7 +26,8 @@ Extensions (new keys, all optional):
   [Distributed] mode = auto|local|shard|dp|dp_dense, grad_reduce = sum|mean,
                 comm_dtype = auto|fp32|bf16 (row-sharded wire rows; auto = table storage dtype),
                 microbatches = 1|2|... (row-sharded step parts overlapping the exchange; default 1),
-                prefetch_rows = auto|on|off (exchange the next step's rows early, re-send updated ones)
+                prefetch_rows = auto|on|off (exchange the next step's rows early, re-send updated ones),
+                overlap_grads = auto|on|off (split backward; first half's gradients sent while the rest runs)
 """
 
 from __future__ import annotations
@@ -107,6 +108,7 @@ class FMRunConfig:
     comm_dtype: str = "auto"
     microbatches: int = 0
     prefetch_rows: str = "auto"
+    overlap_grads: str = "auto"
     config_file: str | None = None
 
     # ------------------------------------------------------------------
@@ -128,6 +130,7 @@ class FMRunConfig:
                         dtype={"fp32": torch.float32, "bf16": torch.bfloat16,
                                "fp8": torch.float8_e4m3fn}[self.dtype], opt=opt, mode=self.mode,
                         grad_reduce=self.grad_reduce, comm_dtype=self.comm_dtype, microbatches=self.microbatches, prefetch_rows=self.prefetch_rows,
+                        overlap_grads=self.overlap_grads,
                         stochastic_rounding=self.stochastic_rounding, dedup_chunk=self.dedup_chunk, global_bias=self.global_bias)
 
 
@@ -237,6 +240,7 @@ def load_config(config_file: str, *, echo: bool = True, printer=print) -> FMRunC
     c.comm_dtype = opt(DISTRIBUTED, "comm_dtype", lambda s: s.strip().lower(), c.comm_dtype)
     c.microbatches = opt(DISTRIBUTED, "microbatches", int, c.microbatches)
     c.prefetch_rows = opt(DISTRIBUTED, "prefetch_rows", lambda s: s.strip().lower(), c.prefetch_rows)
+    c.overlap_grads = opt(DISTRIBUTED, "overlap_grads", lambda s: s.strip().lower(), c.overlap_grads)
     if c.comm_dtype not in ("auto", "storage", "fp32", "bf16"):
         raise ConfigError(f"[Distributed] comm_dtype must be auto, fp32 or bf16, got {c.comm_dtype}")
     return c

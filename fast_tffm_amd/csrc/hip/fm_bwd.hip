@@ -29,6 +29,7 @@ namespace fm {
 enum BwdMode : int { kBwdLocal = 0, kBwdEmit = 1 };
 constexpr int kMaxCH = 32;        // chunk length cap (prefetch registers)
 constexpr int kSmallChunks = 16;  // rows with more chunks go to the workgroup combine
+constexpr int kMaxPieceOwners = 64;  // owners of a split backward piece
 
 struct BwdArgs {
   int mode;                 // BwdMode
@@ -62,6 +63,11 @@ struct BwdArgs {
   int g_bf16;               // 1: v-grad stored as bf16 (the exchange's bf16 wire)
   const int* sr_counter;    // stochastic rounding of bf16 / fp8 row stores (null: round to nearest)
   int counters_ready;       // 1: counts[2] and *big_count are already 0 (fresh dedup)
+  // split backward (row-sharded exchange): piece p >= 0 reduces only the segments in
+  // [seg_bounds[2q + p], seg_bounds[2q + p + 1]) for every owner q < n_owners, so the
+  // gradient rows of piece 0 can travel while piece 1 is computed; -1 = all segments
+  const int* seg_bounds;    // [2 * n_owners + 1]
+  int piece, n_owners;
   float* partial;           // [#chunks, Kp + 4]
   int* big_list;            // [U] rows for the workgroup combine
   int* big_count;           // device scalar, zeroed by the launcher
@@ -196,6 +202,23 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_chunk_kernel(BwdArgs a) {
   const bool tact = t < nv;
   const int tE = tact ? t : nv - 1;
   const int nchunks = a.counts[1];
+  // split-backward piece: this piece's chunk ranges (one per owner) and their prefix sums
+  __shared__ int pr_start[kMaxPieceOwners], pr_pre[kMaxPieceOwners + 1];
+  const bool pieced = a.piece >= 0;
+  if (pieced) {
+    if (threadIdx.x == 0) {
+      int acc = 0;
+      for (int q = 0; q < a.n_owners; ++q) {
+        const int c0 = a.seg_chunk[a.seg_bounds[2 * q + a.piece]];
+        const int c1 = a.seg_chunk[a.seg_bounds[2 * q + a.piece + 1]];
+        pr_start[q] = c0;
+        pr_pre[q] = acc;
+        acc += c1 - c0;
+      }
+      pr_pre[a.n_owners] = acc;
+    }
+    __syncthreads();
+  }
   // XCD-sliced schedule: workgroups b = x (mod 8) share an XCD under the observed
   // round-robin dispatch (speed only, never correctness) and walk the chunk lists
   // of example slices x, x+8, ... in order, so the r1 rows they gather stay in
@@ -206,12 +229,20 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_chunk_kernel(BwdArgs a) {
   const int stride = (gridDim.x / nx) * kWavesPerBlock * G;
   for (int s = nslc ? (int)(blockIdx.x % nx) : 0; s < (nslc ? nslc : 1); s += nx) {
   const int i0 = nslc ? a.slice_start[s] : 0;
-  const int i1 = nslc ? a.slice_start[s + 1] : nchunks;
+  const int i1 = nslc ? a.slice_start[s + 1] : (pieced ? pr_pre[a.n_owners] : nchunks);
   // Software pipeline over this lane group's chunks: the descriptor of the next
   // chunk (and the list entry of the one after) load while the current one is
   // reduced, so the dependent metadata chain is off the critical path.
   int ii = i0 + wave_in_x * G + g;
-  auto chunk_at = [&](int i) { return nslc ? a.slice_list[i] : i; };
+  auto chunk_at = [&](int i) {
+    if (nslc) return a.slice_list[i];
+    if (pieced) {
+      int q = 0;
+      while (q + 1 < a.n_owners && pr_pre[q + 1] <= i) ++q;
+      return pr_start[q] + (i - pr_pre[q]);
+    }
+    return i;
+  };
   int c = ii < i1 ? chunk_at(ii) : 0;
   int cn = ii + stride < i1 ? chunk_at(ii + stride) : 0;
   int d_j0 = 0, d_j1 = 0, d_seg = 0, d_key = 0;
@@ -638,7 +669,8 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
     (void)hipMemsetAsync(a.counts_rw + 2, 0, sizeof(int), st);  // #multi-chunk rows, appended by the chunk kernel
   }
   const int g1 = (fill_grid(max_chunks, kWavesPerBlock * G) + 7) / 8 * 8;  // multiple of 8: XCD groups
-  const bool dense = a.dense_list && a.dense_part;
+  const bool dense = a.dense_list && a.dense_part && a.piece < 0;
+  if (a.piece >= 0 && (a.n_owners > kMaxPieceOwners || a.slice_list)) return -6;
   const bool fork = dense && dense_st && dense_st != st;
   hipStream_t ds = fork ? dense_st : st;
   if (dense) {

@@ -86,9 +86,10 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
          u64 big_list, u64 big_count, u64 multi, u64 slice_list, u64 slice_start, int nslices, u64 dense_list,
          u64 dense_part, int nex, u64 dense_stream, int dtype,
          long long max_chunks, long long max_unique, u64 stream, int g_wcol, int g_bf16, u64 sr_counter,
-         int counters_ready) {
+         int counters_ready, u64 seg_bounds, int piece, int n_owners) {
         fm::BwdArgs a{};
         a.counters_ready = counters_ready;
+        a.seg_bounds = P<const int>(seg_bounds); a.piece = piece; a.n_owners = n_owners;
         a.sr_counter = P<const int>(sr_counter);
         a.mode = mode; a.counts = P<const int>(counts); a.chunk_start = P<const int>(chunk_start);
         a.chunk_seg = P<const int>(chunk_seg); a.chunk_key = P<const int>(chunk_key);
@@ -118,7 +119,8 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("multi"), py::arg("slice_list"), py::arg("slice_start"), py::arg("nslices"), py::arg("dense_list"),
       py::arg("dense_part"), py::arg("nex"), py::arg("dense_stream"), py::arg("dtype"),
       py::arg("max_chunks"), py::arg("max_unique"), py::arg("stream"), py::arg("g_wcol") = -1,
-      py::arg("g_bf16") = 0, py::arg("sr_counter") = 0, py::arg("counters_ready") = 0);
+      py::arg("g_bf16") = 0, py::arg("sr_counter") = 0, py::arg("counters_ready") = 0, py::arg("seg_bounds") = 0,
+      py::arg("piece") = -1, py::arg("n_owners") = 0);
 
   m.def("dedup_workspace_bytes", &fm::dedup_workspace_bytes, py::arg("n"));
 

@@ -442,7 +442,8 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
                 grad_out: torch.Tensor | None = None, reg_v: float = 0.0, reg_w: float = 0.0,
                 partial: torch.Tensor | None = None, threads: int = 0,
                 dense_part: torch.Tensor | None = None, dense_stream=None,
-                grad_bf16: bool = False, sr_counter: torch.Tensor | None = None) -> torch.Tensor | None:
+                grad_bf16: bool = False, sr_counter: torch.Tensor | None = None,
+                seg_bounds: torch.Tensor | None = None, piece: int = -1) -> torch.Tensor | None:
     """Segmented FM backward over the dedup grouping (reference FmGrad, cc/fm_grad_op.h:59-163).
 
     Per unique row u with occurrences (i, x):
@@ -450,7 +451,9 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
       g_w = sum x*dpred_i            + reg_w * n_u * w
     mode=BWD_LOCAL applies ``opt`` in place on ``table`` rows ``uniq[u]``;
     mode=BWD_EMIT writes [g_v, g_w] rows into ``grad_out[u]`` (``src_v``/``src_w``
-    hold the gathered parameter rows in unique order).
+    hold the gathered parameter rows in unique order).  ``piece`` 0 / 1 with
+    ``seg_bounds`` (GPU, int32 [2W+1]) reduces only the segments of every owner's first /
+    second part (split backward of the row-sharded exchange); piece 1 must follow piece 0.
     """
     dev = dpred.device
     _check(dd.sorted_ex is not None, "dedup must be run with ex_of_occ")
@@ -479,6 +482,10 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
         _check(not grad_bf16 or _is_gpu(dpred), "bf16 gradient rows are a GPU path")
     v_stride = _chk_rows(v, Kp, "v")
     o = opt or OptConfig()
+    if piece >= 0:
+        _check(_is_gpu(dpred) and seg_bounds is not None and mode == BWD_EMIT and dd.slice_list is None
+               and dd.dense_list is None, "split backward pieces: GPU, EMIT mode, seg_bounds, no sliced / dense path")
+        _chk_vec(seg_bounds, torch.int32, 3, "seg_bounds", dev)
     if _is_gpu(dpred):
         h = native.hip()
         if partial is None:
@@ -503,7 +510,9 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               dense_part=_p(dp), nex=int(dpred.numel()),
               dense_stream=dense_stream.cuda_stream if dense_stream is not None else 0, dtype=dt, max_chunks=dd.n, max_unique=dd.n,
               stream=_stream(dpred), g_wcol=g_wcol if mode == BWD_EMIT else -1, g_bf16=int(bool(grad_bf16)),
-              sr_counter=_p(sr_counter), counters_ready=int(bool(dd.bwd_fresh)))
+              sr_counter=_p(sr_counter), counters_ready=int(bool(dd.bwd_fresh)),
+              seg_bounds=_p(seg_bounds), piece=int(piece),
+              n_owners=(seg_bounds.numel() - 1) // 2 if seg_bounds is not None else 0)
         dd.bwd_fresh = False  # a second backward over this grouping zeroes its counters itself
     else:
         U = dd.sync()

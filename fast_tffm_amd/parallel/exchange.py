@@ -212,6 +212,10 @@ class ShardExchange(_Base):
         # with only one batch of lookahead the early exchange sits at the end of the plan chain
         # (which can then become the critical path): "auto" uses it with two batches of lookahead
         self.prefetch_depth1 = self.prefetch and forced
+        # split backward: the gradient rows of every owner's first half travel (P2P on RCCL)
+        # while the second half is reduced
+        og = str(getattr(model.cfg, "overlap_grads", "auto")).lower()
+        self.overlap_grads = self.nparts == 1 and (og in ("on", "true", "1") or (og == "auto" and self.W > 1))
         self.cur_plan: _ShardPlan | None = None
         self.step_start = None
         self.early_steps = 0          # steps that took the early-exchange + patch path
@@ -533,6 +537,72 @@ class ShardExchange(_Base):
             e.gathered.index_copy_(0, base + self._tag_view(recv).to(torch.int64), recv)
         return self.wire.views(e.gathered)
 
+    def _split_ok(self, pl: _ShardPlan, dd) -> bool:
+        return (self.overlap_grads and len(pl.parts) == 1 and dd.slice_list is None
+                and (dd.dense_list is None or self.dev.type != "cuda"))
+
+    def _half_bounds(self, part: _Part) -> tuple[list[int], list[int], list[int], list[int]]:
+        """Per owner q: start of my requests to q in unique order, and the size of their first half;
+        per source s: start of s's run in my received requests, and the size of its first half
+        (the sender's first half of a run of n rows is (n + 1) // 2 on both sides)."""
+        sc, rc = part.sc, part.rc
+        s_start = np.concatenate([[0], np.cumsum(sc)[:-1]]).astype(np.int64).tolist()
+        r_start = np.concatenate([[0], np.cumsum(rc)[:-1]]).astype(np.int64).tolist()
+        return s_start, [(n + 1) // 2 for n in sc], r_start, [(n + 1) // 2 for n in rc]
+
+    def _p2p_piece(self, piece: int, part: _Part, bounds, grad_send: torch.Tensor, grad_recv: torch.Tensor):
+        """Send every owner its rows of ``piece`` (0: first halves, 1: second halves) and receive
+        the matching rows of every source into their place in ``grad_recv`` (rank-major runs);
+        the own rank's rows are a local copy.  Returns the pending works."""
+        if self.W == 1:
+            return []  # (grad_recv is grad_send)
+        s_start, s_half, r_start, r_half = bounds
+        ops, me = [], self.ctx.rank
+        for q in range(self.W):
+            a0 = s_start[q] + (0 if piece == 0 else s_half[q])
+            a1 = s_start[q] + (s_half[q] if piece == 0 else part.sc[q])
+            b0 = r_start[q] + (0 if piece == 0 else r_half[q])
+            b1 = r_start[q] + (r_half[q] if piece == 0 else part.rc[q])
+            if q == me:
+                if b1 > b0:
+                    grad_recv[b0:b1].copy_(grad_send[a0:a1])
+                continue
+            if a1 > a0:
+                ops.append(dist.P2POp(dist.isend, grad_send[a0:a1], q, group=self.group))
+            if b1 > b0:
+                ops.append(dist.P2POp(dist.irecv, grad_recv[b0:b1], q, group=self.group))
+        if not ops:
+            return []
+        if self.dev.type == "cuda":
+            return list(dist.batch_isend_irecv(ops))
+        return [op.op(op.tensor, op.peer, group=op.group) for op in ops]
+
+    def _bwd_split_exchange(self, pl, part, dd, fo, src_v, src_w, gs, grad_recv, rv, rw) -> list:
+        """Backward in two pieces (every owner's first half of rows, then the second half) with
+        the first piece's gradient rows sent while the second is reduced."""
+        m, ws, cfg, Kp, wf = self.m, self.m.ws, self.m.cfg, self.Kp, self.wire
+        bounds = self._half_bounds(part)
+        kw = dict(mode=K.BWD_EMIT, src_v=src_v, src_w=src_w, grad_out=gs, reg_v=rv, reg_w=rw,
+                  partial=ws.bwd_partial, threads=cfg.threads, grad_bf16=wf.grad_bf16)
+        if self.dev.type != "cuda":  # CPU reference: one backward, the exchange still in two pieces
+            K.fm_backward(dd, fo.dpred, fo.r1, Kp, **kw)
+            return self._p2p_piece(0, part, bounds, gs, grad_recv) + self._p2p_piece(1, part, bounds, gs, grad_recv)
+        s_start, s_half = bounds[0], bounds[1]
+        sb = []
+        for q in range(self.W):
+            sb += [s_start[q], s_start[q] + s_half[q]]
+        sb.append(part.U)
+        slot = self.slots[pl.slot]
+        if getattr(slot, "sb_h", None) is None or slot.sb_h.numel() != len(sb):
+            slot.sb_h = torch.empty(len(sb), dtype=torch.int32, pin_memory=True)
+            slot.sb = torch.empty(len(sb), dtype=torch.int32, device=self.dev)
+        slot.sb_h.numpy()[:] = sb
+        slot.sb.copy_(slot.sb_h, non_blocking=True)
+        K.fm_backward(dd, fo.dpred, fo.r1, Kp, seg_bounds=slot.sb, piece=0, **kw)
+        works = self._p2p_piece(0, part, bounds, gs, grad_recv)
+        K.fm_backward(dd, fo.dpred, fo.r1, Kp, seg_bounds=slot.sb, piece=1, **kw)
+        return works + self._p2p_piece(1, part, bounds, gs, grad_recv)
+
     def _check_splits(self, part: _Part) -> None:
         """FM_DEBUG_CHECKS=1: the split lists of every rank must form a consistent W x W
         exchange (what rank s sends to r is what r expects from s) and cover all unique ids."""
@@ -644,6 +714,10 @@ class ShardExchange(_Base):
                                   bias=m.gbias)
             loss = fo.loss_sum if loss is None else loss + fo.loss_sum
             gs = grad_send[part.u0: part.u0 + part.U]
+            if self._split_ok(pl, dd):
+                with roctx_range("bwd_split+grads"):
+                    gworks += self._bwd_split_exchange(pl, part, dd, fo, src_v, src_w, gs, grad_recv, rv, rw)
+                continue
             with roctx_range("bwd"):
                 K.fm_backward(dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT, src_v=src_v, src_w=src_w, grad_out=gs,
                               reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads,

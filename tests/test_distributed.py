@@ -58,8 +58,9 @@ def _worker(rank, world, port, mode, grad_reduce, out_dir, mb=0):
     losses = [m.train_step(bs[s], bs[s + 1] if s + 1 < STEPS and mode == "shard" else None,
                            bs[s + 2] if s + 2 < STEPS and mode == "shard" else None).mean_loss()
               for s in range(STEPS)]
-    if mode == "shard":  # the early row exchange + patch path ran (lookahead steps 1..)
-        assert m._exchange.early_steps == (STEPS - 1 if max(1, mb) == 1 else 0)
+    if mode == "shard":  # the early row exchange + patch path ran (lookahead steps 1..); split-gradient
+        assert m._exchange.early_steps == (STEPS - 1 if max(1, mb) == 1 else 0)  # exchange with one part
+        assert m._exchange.overlap_grads == (max(1, mb) == 1)
     pred = m.predict(_batch(99, rank))
     torch.save({"gids": m.table.global_ids(), "rows": m.table.reference_rows(), "acc": m.table.s0v[:, :KF].clone(),
                 "losses": losses, "pred": pred}, os.path.join(out_dir, f"rank{rank}.pt"))
