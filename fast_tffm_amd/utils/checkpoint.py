@@ -31,7 +31,8 @@ import shutil
 
 import numpy as np
 import torch
-from safetensors.torch import load_file, save_file
+from safetensors import safe_open
+from safetensors.torch import load_file, save_file  # noqa: F401  (small files / tools)
 
 FORMAT = "fast_tffm_amd/ckpt-v1"
 INDEX = "checkpoint"
@@ -60,16 +61,67 @@ def latest_checkpoint(log_dir: str | None) -> str | None:
     return os.path.dirname(cands[-1]) if cands else None
 
 
-def _table_tensors(table) -> dict[str, torch.Tensor]:
-    K = table.K
-    t = {"w": table.w, "v": table.dense_v()[:, :K], "s0w": table.s0w, "s0v": table.s0v[:, :K]}
+# safetensors dtype names
+_ST_DTYPE = {torch.float32: "F32", torch.bfloat16: "BF16", torch.uint8: "U8", torch.int64: "I64",
+             torch.int32: "I32", torch.float16: "F16"}
+CHUNK_BYTES = 256 << 20   # rows move device -> file (and back) in chunks of about this size
+
+
+def _table_sources(table) -> dict:
+    """name -> (dtype, shape, chunk(r0, r1) -> tensor of rows [r0, r1)) of a table shard.
+
+    Chunked so that a checkpoint of a 125M-row shard never holds more than one chunk of
+    any table tensor in host memory (nor a full-size dequantised copy on the device)."""
+    K, n = table.K, table.rows
+
+    def rows(t, cols=None):
+        return lambda r0, r1: (t[r0:r1] if cols is None else t[r0:r1, :cols])
+
+    src = {"w": (torch.float32, (n,), rows(table.w)),
+           "v": (table.dtype if not table.fp8 else torch.float32, (n, K),
+                 (lambda r0, r1: table.dense_v(slice(r0, r1))[:, :K])
+                 if table.fp8 else rows(table.v, K)),
+           "s0w": (torch.float32, (n,), rows(table.s0w)),
+           "s0v": (torch.float32, (n, K), rows(table.s0v, K))}
     if table.fp8:  # exact fp8 payload + scales next to the portable fp32 values
-        t["v_fp8"] = table.v.view(torch.uint8)
-        t["v_scale"] = table.scale
+        src["v_fp8"] = (torch.uint8, (n, table.Kp), rows(table.v.view(torch.uint8)))
+        src["v_scale"] = (torch.float32, (n,), rows(table.scale))
     if table.s1v is not None:
-        t["s1w"] = table.s1w
-        t["s1v"] = table.s1v[:, :K]
-    return {k: v.detach().to("cpu").contiguous() for k, v in t.items()}
+        src["s1w"] = (torch.float32, (n,), rows(table.s1w))
+        src["s1v"] = (torch.float32, (n, K), rows(table.s1v, K))
+    return src
+
+
+def write_safetensors_streamed(path: str, sources: dict, metadata: dict | None = None) -> None:
+    """Write a safetensors file from row-chunk producers (see ``_table_sources``): the header
+    first (8-byte length + JSON, data aligned to 8 bytes), then each tensor chunk by chunk."""
+    header, off, plan = {}, 0, []
+    for name, (dtype, shape, chunk) in sources.items():
+        esz = torch.tensor([], dtype=dtype).element_size()
+        nbytes = int(np.prod(shape)) * esz if len(shape) else esz
+        header[name] = {"dtype": _ST_DTYPE[dtype], "shape": list(shape), "data_offsets": [off, off + nbytes]}
+        plan.append((name, dtype, shape, chunk, nbytes))
+        off += nbytes
+    if metadata:
+        header["__metadata__"] = {k: str(v) for k, v in metadata.items()}
+    hb = json.dumps(header, separators=(",", ":")).encode()
+    hb += b" " * ((8 - (len(hb) + 8) % 8) % 8)
+    with open(path, "wb") as f:
+        f.write(len(hb).to_bytes(8, "little"))
+        f.write(hb)
+        for name, dtype, shape, chunk, nbytes in plan:
+            n = shape[0] if shape else 1
+            row_bytes = max(1, nbytes // max(n, 1))
+            step = max(1, CHUNK_BYTES // row_bytes)
+            for r0 in range(0, n, step):
+                c = chunk(r0, min(n, r0 + step)).detach()
+                c = c.to(dtype).contiguous().cpu() if c.dtype != dtype else c.contiguous().cpu()
+                f.write(c.view(torch.uint8).numpy().tobytes())
+
+
+def _table_tensors(table) -> dict[str, torch.Tensor]:
+    """Whole shard tensors on the host (small tables / tests; checkpoints stream instead)."""
+    return {k: c(0, shape[0]).detach().to(dt).cpu().contiguous() for k, (dt, shape, c) in _table_sources(table).items()}
 
 
 def save_checkpoint(model, log_dir: str, step: int, *, reader_state: dict | None = None, ctx=None,
@@ -84,12 +136,12 @@ def save_checkpoint(model, log_dir: str, step: int, *, reader_state: dict | None
     if sharded or rank == 0:
         shard_rank, shard_world = (table.rank, table.world)
         tmp = os.path.join(path, _shard_name(shard_rank, shard_world) + ".tmp")
-        tensors = _table_tensors(table)
+        sources = _table_sources(table)
         if getattr(model, "gbias", None) is not None:  # replicated global bias + optimizer state
             for k in ("gbias", "gbias_s0", "gbias_s1"):
-                tensors[k] = getattr(model, k).detach().to("cpu").contiguous()
-        save_file(tensors, tmp, metadata={"format": FORMAT, "rank": str(shard_rank),
-                                                          "world": str(shard_world)})
+                t = getattr(model, k)
+                sources[k] = (torch.float32, tuple(t.shape), (lambda t_: lambda r0, r1: t_[r0:r1])(t))
+        write_safetensors_streamed(tmp, sources, {"format": FORMAT, "rank": shard_rank, "world": shard_world})
         os.replace(tmp, os.path.join(path, _shard_name(shard_rank, shard_world)))
     if ctx is not None and world > 1:
         ctx.barrier()
@@ -156,28 +208,45 @@ def restore_checkpoint(model, ckpt_dir: str) -> dict:
     direct = os.path.join(ckpt_dir, _shard_name(table.rank, table.world))
     if getattr(model, "gbias", None) is not None:
         first = next(iter(_iter_shards(ckpt_dir)), None)
-        bt = load_file(first[2]) if first is not None else {}
-        for k in ("gbias", "gbias_s0", "gbias_s1"):
-            if k in bt:
-                getattr(model, k).copy_(bt[k].to(getattr(model, k).device))
+        if first is not None:
+            with safe_open(first[2], framework="pt") as f:
+                for k in ("gbias", "gbias_s0", "gbias_s1"):
+                    if k in f.keys():
+                        getattr(model, k).copy_(f.get_tensor(k).to(getattr(model, k).device))
     if os.path.exists(direct):
-        t = load_file(direct)
-        _copy_rows(table, None, t, K, dev)
+        for r0, t in _iter_row_chunks(direct):
+            n = t["w"].shape[0]
+            _copy_rows(table, slice(r0, r0 + n), t, K, dev)
     else:
         for s_rank, s_world, path in _iter_shards(ckpt_dir):
-            t = load_file(path)
-            n = t["w"].shape[0]
-            gid = torch.arange(n, dtype=torch.int64) * s_world + s_rank
-            mine = (gid % table.world == table.rank) & (gid < table.vocab_size)
-            if not bool(mine.any()):
-                continue
-            sel = torch.nonzero(mine).flatten()
-            local = torch.div(gid[sel], table.world, rounding_mode="floor")
-            _copy_rows(table, local.to(dev), {k: v[sel] for k, v in t.items()}, K, dev)
+            for r0, t in _iter_row_chunks(path):
+                n = t["w"].shape[0]
+                gid = torch.arange(r0, r0 + n, dtype=torch.int64) * s_world + s_rank
+                mine = (gid % table.world == table.rank) & (gid < table.vocab_size)
+                if not bool(mine.any()):
+                    continue
+                sel = torch.nonzero(mine).flatten()
+                local = torch.div(gid[sel], table.world, rounding_mode="floor")
+                _copy_rows(table, local.to(dev), {k: v[sel] for k, v in t.items()}, K, dev)
     model.global_step = int(meta["global_step"])
     if hasattr(model, "sr_reset"):
         model.sr_reset()
     return meta
+
+
+_ROW_KEYS = ("w", "v", "s0w", "s0v", "s1w", "s1v", "v_fp8", "v_scale")
+
+
+def _iter_row_chunks(path: str):
+    """(first row, {name: rows}) chunks of a shard file's per-row tensors, read lazily."""
+    with safe_open(path, framework="pt") as f:
+        keys = [k for k in f.keys() if k in _ROW_KEYS]
+        n = f.get_slice("w").get_shape()[0]
+        row_bytes = sum(4 * int(np.prod(f.get_slice(k).get_shape()[1:] or [1])) for k in keys)
+        step = max(1, CHUNK_BYTES // max(row_bytes, 1))
+        for r0 in range(0, n, step):
+            r1 = min(n, r0 + step)
+            yield r0, {k: f.get_slice(k)[r0:r1] for k in keys}
 
 
 def _copy_rows(table, local_rows, t: dict, K: int, dev) -> None:
@@ -202,6 +271,8 @@ def _copy_rows(table, local_rows, t: dict, K: int, dev) -> None:
         put(table.v.view(torch.uint8), t["v_fp8"])
         put(table.scale, t["v_scale"])
     elif table.fp8:
+        if isinstance(local_rows, slice):
+            local_rows = torch.arange(local_rows.start, local_rows.stop, device=dev)
         table.set_v(local_rows, t["v"].float())
     else:
         put(table.v, t.get("v"), cols=True)
@@ -228,19 +299,19 @@ def export_reference_blocks(ckpt_dir: str, out_dir: str, block_num: int, *, with
             slots.append(np.lib.format.open_memmap(os.path.join(out_dir, f"vocab_block_{i}_Adagrad.npy"),
                                                    mode="w+", dtype=np.float32, shape=(rows_per_block, K + 1)))
     for s_rank, s_world, path in _iter_shards(ckpt_dir):
-        t = load_file(path)
-        n = t["w"].shape[0]
-        gid = np.arange(n, dtype=np.int64) * s_world + s_rank
-        ok = gid < V
-        gid = gid[ok]
-        ref = np.concatenate([t["w"].float().numpy()[ok, None], t["v"].float().numpy()[ok]], axis=1)
-        acc = np.concatenate([t["s0w"].numpy()[ok, None], t["s0v"].numpy()[ok]], axis=1)
-        b, r = gid % block_num, gid // block_num
-        for i in range(block_num):
-            m = b == i
-            blocks[i][r[m]] = ref[m]
-            if with_slots:
-                slots[i][r[m]] = acc[m]
+        for r0, t in _iter_row_chunks(path):
+            n = t["w"].shape[0]
+            gid = np.arange(r0, r0 + n, dtype=np.int64) * s_world + s_rank
+            ok = gid < V
+            gid = gid[ok]
+            ref = np.concatenate([t["w"].float().numpy()[ok, None], t["v"].float().numpy()[ok]], axis=1)
+            acc = np.concatenate([t["s0w"].numpy()[ok, None], t["s0v"].numpy()[ok]], axis=1)
+            b, r = gid % block_num, gid // block_num
+            for i in range(block_num):
+                m = b == i
+                blocks[i][r[m]] = ref[m]
+                if with_slots:
+                    slots[i][r[m]] = acc[m]
     files = []
     for i, arr in enumerate(blocks):
         arr.flush()
