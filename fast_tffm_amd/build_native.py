@@ -27,7 +27,7 @@ CSRC = os.path.join(PKG, "csrc")
 OUT = os.path.join(PKG, "_native")
 ARCH = os.environ.get("FM_OFFLOAD_ARCH", "gfx950")
 
-CPU_SOURCES = ["cpu/module.cpp", "cpu/parser.cpp", "cpu/kernels.cpp", "cpu/loader.cpp"]
+CPU_SOURCES = ["cpu/module.cpp", "cpu/parser.cpp", "cpu/kernels.cpp", "cpu/loader.cpp", "cpu/bincsr.cpp"]
 HIP_SOURCES = ["hip/module.hip"]
 HIP_DEPS = ["hip/fm_fwd.hip", "hip/fm_bwd.hip", "hip/dedup.hip", "hip/shard.hip", "hip/init.hip", "hip/parse.hip",
             "hip/fm_common.h", "hash64.h"]
@@ -71,7 +71,7 @@ def _run(cmd: list[str]) -> None:
 def build_cpu(force: bool = False) -> str:
     os.makedirs(OUT, exist_ok=True)
     target = os.path.join(OUT, "_fm_cpu" + _ext_suffix())
-    deps = CPU_SOURCES + ["cpu/parser.h", "cpu/kernels.h", "cpu/loader.h", "hash64.h"]
+    deps = CPU_SOURCES + ["cpu/parser.h", "cpu/kernels.h", "cpu/loader.h", "cpu/bincsr.h", "cpu/mapped_file.h", "hash64.h"]
     if force or _stale(target, deps):
         cxx = os.environ.get("CXX", "g++")
         tmp = target + ".tmp"

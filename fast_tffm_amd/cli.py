@@ -1,11 +1,14 @@
-"""Command line: ``python run.py {train,predict,generate} CONFIG [options]``.
+"""Command line: ``python run.py {train,predict,generate,convert} CONFIG [options]``.
 
 Same arguments as the reference's run_tffm.py (run_tffm.py:124-162):
   task {train,predict,generate}, config_file,
   --dist JOB_NAME TASK_INDEX PS_HOSTS WORKER_HOSTS, --protocol, --wait-for-workers N,
   -t/--trace FILE, -m/--monitor, --export_path DIR.
 Extensions: --device {auto,cpu,cuda}, --mode {auto,local,shard,dp,dp_dense},
---max-steps N, --log-dir DIR (overrides [General] log_dir).
+--max-steps N, --log-dir DIR (overrides [General] log_dir), and the task
+``convert CONFIG --out DIR``: parse the config's train files (+ weight files) once
+into binary CSR caches (``DIR/<name>.fmb``, data/bincache.py) that ``train``
+reads at memory speed when ``train_files`` points at them.
 
 Distributed runs: launch one process per GPU with torchrun (RANK/WORLD_SIZE/
 MASTER_ADDR from the environment), or keep the reference's ``--dist worker i
@@ -23,7 +26,7 @@ import sys
 
 def build_parser() -> argparse.ArgumentParser:
     p = argparse.ArgumentParser(prog="run.py", description="MI355X-native distributed factorization machine")
-    p.add_argument("task", choices=["train", "predict", "generate"])
+    p.add_argument("task", choices=["train", "predict", "generate", "convert"])
     p.add_argument("config_file", type=str)
     p.add_argument("--dist", nargs=4, metavar=("JOB_NAME", "TASK_INDEX", "PS_HOSTS", "WORKER_HOSTS"), default=None,
                    help="For distributed training or prediction")
@@ -39,6 +42,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--mode", default=None, choices=["auto", "local", "shard", "dp", "dp_dense"])
     p.add_argument("--max-steps", type=int, default=None)
     p.add_argument("--log-dir", default=None)
+    p.add_argument("--out", default=None, help="convert: output directory of the .fmb caches")
     return p
 
 
@@ -86,6 +90,20 @@ def main(argv: list[str] | None = None) -> int:
         export_model(path, args.export_path, vocabulary_block_num=cfg.vocabulary_block_num,
                      hash_feature_id=cfg.hash_feature_id, loss_type=cfg.loss_type)
         print("Done exporting!")
+        return 0
+
+    if args.task == "convert":
+        if args.out is None:
+            print("Output directory is not specified. Use --out.")
+            return 2
+        from .data.bincache import convert_files
+
+        for path, st in convert_files(cfg.train_files, cfg.weight_files or None, args.out, cfg.vocabulary_size,
+                                      cfg.hash_feature_id, cfg.parse_threads):
+            print(f"{path}: {st['examples']} examples, {st['nnz']} features"
+                  f"{' (+ weights)' if cfg.weight_files else ''}", flush=True)
+        print(f"Done converting. Set train_files = {os.path.join(args.out, '*.fmb')} and no weight_files to train "
+              "from the caches.")
         return 0
 
     ctx = None

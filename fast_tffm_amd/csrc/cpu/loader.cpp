@@ -1,10 +1,5 @@
 #include "loader.h"
 
-#include <fcntl.h>
-#include <sys/mman.h>
-#include <sys/stat.h>
-#include <unistd.h>
-
 #include <algorithm>
 #include <cerrno>
 #include <cstring>
@@ -12,40 +7,12 @@
 #include <random>
 #include <stdexcept>
 
+#include "bincsr.h"
+#include "mapped_file.h"
+
 namespace fm {
 
 namespace {
-
-// Read-only mapping of a whole file (empty files map to nothing).
-struct MappedFile {
-  const char* data = nullptr;
-  size_t size = 0;
-  explicit MappedFile(const std::string& path) {
-    const int fd = ::open(path.c_str(), O_RDONLY);
-    if (fd < 0) throw std::runtime_error("cannot open " + path + ": " + std::strerror(errno));
-    struct stat st {};
-    if (::fstat(fd, &st) != 0) {
-      ::close(fd);
-      throw std::runtime_error("cannot stat " + path);
-    }
-    size = static_cast<size_t>(st.st_size);
-    if (size > 0) {
-      void* p = ::mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
-      if (p == MAP_FAILED) {
-        ::close(fd);
-        throw std::runtime_error("cannot map " + path);
-      }
-      ::madvise(p, size, MADV_SEQUENTIAL);
-      data = static_cast<const char*>(p);
-    }
-    ::close(fd);
-  }
-  ~MappedFile() {
-    if (data) ::munmap(const_cast<char*>(data), size);
-  }
-  MappedFile(const MappedFile&) = delete;
-  MappedFile& operator=(const MappedFile&) = delete;
-};
 
 struct Span {
   const char* p;
@@ -67,9 +34,73 @@ void split_lines(const MappedFile& f, std::vector<Span>& out) {
   }
 }
 
+// A window entry: a text line (+ its weight line), or in binary mode one example of a
+// mapped .fmb file (line = its ids as (int32*, n), weight.p = its values or null).
 struct Item {
   Span line, weight;
+  float label = 0.f, wt = 1.f;
 };
+
+// Copy n chosen binary examples into a CSR batch (offsets, ids, values, labels, weights)
+// with up to `threads` threads; ids are range-checked on the way (a corrupt cache must
+// not reach the device kernels as an out-of-bounds row).
+void assemble_binary(const std::vector<Item>& its, bool weighted, int64_t vocab, int threads, LoadedBatch& b) {
+  const size_t n = its.size();
+  b.labels.resize(n);
+  b.offsets.resize(n + 1);
+  b.offsets[0] = 0;
+  bool any_vals = false;
+  int mf = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const int c = static_cast<int>(its[i].line.len);
+    b.offsets[i + 1] = b.offsets[i] + c;
+    mf = std::max(mf, c);
+    b.labels[i] = its[i].label;
+    any_vals |= its[i].weight.p != nullptr;
+  }
+  if (weighted) {
+    b.weights.resize(n);
+    for (size_t i = 0; i < n; ++i) b.weights[i] = its[i].wt;
+  }
+  b.max_feats = mf;
+  const size_t nnz = static_cast<size_t>(b.offsets[n]);
+  b.ids.resize(nnz);
+  if (any_vals) b.vals.resize(nnz);
+  const int T = std::max(1, std::min<int>(threads, static_cast<int>(nnz >> 16)));
+  std::vector<char> bad(static_cast<size_t>(T), 0);
+  auto work = [&](int t) {
+    const size_t i0 = n * t / T, i1 = n * (t + 1) / T;
+    for (size_t i = i0; i < i1; ++i) {
+      const Item& it = its[i];
+      const int32_t* src = reinterpret_cast<const int32_t*>(it.line.p);
+      int32_t* dst = b.ids.data() + b.offsets[i];
+      uint32_t any = 0;
+      for (uint32_t j = 0; j < it.line.len; ++j) {
+        dst[j] = src[j];
+        any |= static_cast<uint32_t>(static_cast<uint64_t>(static_cast<uint32_t>(src[j])) >=
+                                     static_cast<uint64_t>(vocab));
+      }
+      bad[t] |= any != 0;
+      if (any_vals) {
+        float* v = b.vals.data() + b.offsets[i];
+        if (it.weight.p)
+          std::memcpy(v, it.weight.p, 4 * it.line.len);
+        else
+          std::fill(v, v + it.line.len, 1.f);
+      }
+    }
+  };
+  if (T == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> ths;
+    for (int t = 1; t < T; ++t) ths.emplace_back(work, t);
+    work(0);
+    for (auto& th : ths) th.join();
+  }
+  for (char x : bad)
+    if (x) throw std::runtime_error("binary CSR cache holds a feature id outside [0, vocabulary_size)");
+}
 
 }  // namespace
 
@@ -77,6 +108,9 @@ TextLoader::TextLoader(LoaderOptions o) : o_(std::move(o)) {
   if (o_.batch_size < 1) throw std::invalid_argument("batch_size must be >= 1");
   if (!o_.weight_files.empty() && o_.weight_files.size() != o_.files.size())
     throw std::invalid_argument("The numbers of train files and weight files do not match.");
+  if (o_.binary && !o_.weight_files.empty())
+    throw std::invalid_argument("binary CSR caches carry their weights; pass no weight files");
+  if (o_.binary && o_.raw) throw std::invalid_argument("raw (GPU tokenizer) mode needs text files");
   if (o_.queue_size < 1) o_.queue_size = 1;
   th_ = std::thread([this] { run(); });
 }
@@ -128,8 +162,21 @@ void TextLoader::run() {
     const int64_t B = o_.batch_size;
     const size_t cap = std::max<size_t>(static_cast<size_t>(o_.capacity_factor * static_cast<double>(B)), B);
     const size_t nf = o_.files.size();
-    const bool weighted = !o_.weight_files.empty();
-    std::vector<Item> window;
+    bool weighted = !o_.weight_files.empty();
+    if (o_.binary && nf > 0) {  // every cache must match the model's id space and agree on weights
+      for (size_t i = 0; i < nf; ++i) {
+        BinFile f(o_.files[i]);
+        if (f.h.vocab_size != o_.vocab_size || ((f.h.flags & kBinFlagHashed) != 0) != o_.hash_feature_id)
+          throw std::runtime_error(o_.files[i] + ": converted with vocabulary_size " + std::to_string(f.h.vocab_size) +
+                                   ", hash_feature_id " + ((f.h.flags & kBinFlagHashed) ? "True" : "False") +
+                                   "; the model uses " + std::to_string(o_.vocab_size) + ", " +
+                                   (o_.hash_feature_id ? "True" : "False"));
+        const bool w = (f.h.flags & kBinFlagWeights) != 0;
+        if (i == 0) weighted = w;
+        if (w != weighted) throw std::runtime_error("binary CSR caches disagree on weights: " + o_.files[i]);
+      }
+    }
+    std::vector<Item> window, chosen;
     std::vector<const char*> ptrs, wptrs;
     std::vector<size_t> lens, wlens;
     std::vector<Span> lines, wlines;
@@ -156,30 +203,38 @@ void TextLoader::run() {
       window.clear();
       size_t head = 0;  // FIFO start (no-shuffle mode)
       std::vector<std::unique_ptr<MappedFile>> maps;  // alive until the epoch's batches are parsed
+      std::vector<std::unique_ptr<BinFile>> bins;
 
       // Draw n items from the window into ptrs/lens (random when shuffling, FIFO otherwise)
       // and parse them unless the batch is skipped (resume).
       auto emit = [&](size_t n) -> bool {
         ++count;
-        ptrs.clear(); lens.clear(); wptrs.clear(); wlens.clear();
+        ptrs.clear(); lens.clear(); wptrs.clear(); wlens.clear(); chosen.clear();
         if (o_.shuffle) {
           const size_t w = window.size();
           for (size_t i = 0; i < n; ++i) {  // partial Fisher-Yates: a uniform sample moved to the back
             const size_t j = i + static_cast<size_t>(rng() % (w - i));
             std::swap(window[w - 1 - i], window[w - 1 - j]);
           }
-          for (size_t i = 0; i < n; ++i) {
-            const Item& it = window[w - n + i];
-            ptrs.push_back(it.line.p); lens.push_back(it.line.len);
-            wptrs.push_back(it.weight.p); wlens.push_back(it.weight.len);
-          }
+          if (o_.binary)
+            chosen.assign(window.end() - static_cast<std::ptrdiff_t>(n), window.end());
+          else
+            for (size_t i = 0; i < n; ++i) {
+              const Item& it = window[w - n + i];
+              ptrs.push_back(it.line.p); lens.push_back(it.line.len);
+              wptrs.push_back(it.weight.p); wlens.push_back(it.weight.len);
+            }
           window.resize(w - n);
         } else {
-          for (size_t i = 0; i < n; ++i) {
-            const Item& it = window[head + i];
-            ptrs.push_back(it.line.p); lens.push_back(it.line.len);
-            wptrs.push_back(it.weight.p); wlens.push_back(it.weight.len);
-          }
+          if (o_.binary)
+            chosen.assign(window.begin() + static_cast<std::ptrdiff_t>(head),
+                          window.begin() + static_cast<std::ptrdiff_t>(head + n));
+          else
+            for (size_t i = 0; i < n; ++i) {
+              const Item& it = window[head + i];
+              ptrs.push_back(it.line.p); lens.push_back(it.line.len);
+              wptrs.push_back(it.weight.p); wlens.push_back(it.weight.len);
+            }
           head += n;
           if (head > (1u << 20) && head * 2 > window.size()) {
             window.erase(window.begin(), window.begin() + static_cast<std::ptrdiff_t>(head));
@@ -188,6 +243,12 @@ void TextLoader::run() {
         }
         if (count <= skip) return true;
         LoadedBatch b;
+        if (o_.binary) {
+          assemble_binary(chosen, weighted, o_.vocab_size, o_.threads, b);
+          b.epoch = epoch;
+          b.count = count;
+          return push(std::move(b));
+        }
         if (o_.raw) {
           size_t total = 0;
           for (size_t i = 0; i < n; ++i) total += lens[i] + 1;
@@ -237,6 +298,26 @@ void TextLoader::run() {
       };
 
       for (size_t fi : order) {
+        if (o_.binary) {
+          bins.push_back(std::make_unique<BinFile>(o_.files[fi]));
+          const BinFile& f = *bins.back();
+          const size_t step = line_shard ? static_cast<size_t>(o_.world) : 1;
+          for (size_t i = line_shard ? static_cast<size_t>(o_.rank) : 0; i < static_cast<size_t>(f.h.n); i += step) {
+            const int64_t o = f.offsets[i];
+            Item it;
+            it.line = {reinterpret_cast<const char*>(f.ids + o), static_cast<uint32_t>(f.offsets[i + 1] - o)};
+            it.weight = {f.vals ? reinterpret_cast<const char*>(f.vals + o) : nullptr, 0};
+            it.label = f.labels[i];
+            it.wt = f.weights ? f.weights[i] : 1.f;
+            window.push_back(it);
+            if (window.size() - head >= cap) {
+              if (!emit(static_cast<size_t>(B))) return;
+            }
+          }
+          std::lock_guard<std::mutex> lk(mu_);
+          if (stop_) return;
+          continue;
+        }
         maps.push_back(std::make_unique<MappedFile>(o_.files[fi]));
         split_lines(*maps.back(), lines);
         if (weighted) {

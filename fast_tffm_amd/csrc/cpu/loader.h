@@ -21,6 +21,9 @@
 //  * raw mode (GPU tokenizer, hip/parse.hip): instead of parsing, the chosen
 //    lines are gathered into one '\n'-separated buffer + line offsets that the
 //    consumer copies to the device and tokenizes there.
+//  * binary mode (bincsr.h): the files are pre-parsed .fmb caches; the window
+//    holds examples instead of lines (same RNG draws) and a batch is assembled
+//    by copying the chosen examples' ids / values with `threads` threads.
 // A (start_epoch, skip_batches) position resumes exactly where a checkpoint
 // was taken: the RNGs are re-seeded per epoch, skipped batches are not parsed.
 #pragma once
@@ -52,6 +55,7 @@ struct LoaderOptions {
   int64_t skip_batches = 0;   // batches of start_epoch already consumed
   double capacity_factor = 4.5;
   bool raw = false;           // emit the batch's line bytes (GPU tokenizer) instead of parsed CSR
+  bool binary = false;        // files are .fmb binary CSR caches (weights inside; weight_files empty)
 };
 
 struct LoadedBatch {

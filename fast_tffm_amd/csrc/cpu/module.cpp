@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../hash64.h"
+#include "bincsr.h"
 #include "kernels.h"
 #include "loader.h"
 #include "parser.h"
@@ -192,19 +193,20 @@ PYBIND11_MODULE(_fm_cpu, m) {
       .def(py::init([](std::vector<std::string> files, std::vector<std::string> weight_files, long long batch_size,
                        long long vocab_size, bool hash_feature_id, bool shuffle, int num_epochs,
                        unsigned long long seed, int threads, int rank, int world, int queue_size, int start_epoch,
-                       long long skip_batches, bool raw) {
+                       long long skip_batches, bool raw, bool binary) {
              fm::LoaderOptions o;
              o.files = std::move(files); o.weight_files = std::move(weight_files); o.batch_size = batch_size;
              o.vocab_size = vocab_size; o.hash_feature_id = hash_feature_id; o.shuffle = shuffle;
              o.num_epochs = num_epochs; o.seed = seed; o.threads = threads; o.rank = rank; o.world = world;
              o.queue_size = queue_size; o.start_epoch = start_epoch; o.skip_batches = skip_batches; o.raw = raw;
+             o.binary = binary;
              return new fm::TextLoader(std::move(o));
            }),
            py::arg("files"), py::arg("weight_files"), py::arg("batch_size"), py::arg("vocab_size"),
            py::arg("hash_feature_id") = false, py::arg("shuffle") = true, py::arg("num_epochs") = 1,
            py::arg("seed") = 0, py::arg("threads") = 4, py::arg("rank") = 0, py::arg("world") = 1,
            py::arg("queue_size") = 4, py::arg("start_epoch") = 0, py::arg("skip_batches") = 0,
-           py::arg("raw") = false)
+           py::arg("raw") = false, py::arg("binary") = false)
       // -> (labels, offsets, ids, vals | None, weights | None, max_feats, epoch, count) or None at the end
       .def("next",
            [](fm::TextLoader& L) -> py::object {
@@ -230,6 +232,27 @@ PYBIND11_MODULE(_fm_cpu, m) {
         py::gil_scoped_release nogil;
         L.close();
       });
+
+  // Binary CSR cache (bincsr.h): text (+ weight) file -> .fmb, and a magic check.
+  m.def(
+      "convert_to_bin",
+      [](const std::string& text, const std::string& weights, const std::string& out, long long vocab_size,
+         bool hash_feature_id, int threads, long long chunk_lines) {
+        fm::ConvertStats st;
+        {
+          py::gil_scoped_release nogil;
+          st = fm::convert_text_to_bin(text, weights, out, vocab_size, hash_feature_id, threads, chunk_lines);
+        }
+        py::dict d;
+        d["examples"] = st.n;
+        d["nnz"] = st.nnz;
+        d["max_feats"] = st.max_feats;
+        d["has_vals"] = st.has_vals;
+        return d;
+      },
+      py::arg("text"), py::arg("weights"), py::arg("out"), py::arg("vocab_size"), py::arg("hash_feature_id") = false,
+      py::arg("threads") = 4, py::arg("chunk_lines") = 1 << 20);
+  m.def("is_bin_file", &fm::is_bin_file, py::arg("path"));
 
   m.def(
       "parse_floats",

@@ -78,6 +78,8 @@ class TextBatchReader:
                  parse_threads: int = 4, rank: int = 0, world: int = 1, state: ReaderState | None = None):
         if weight_files and len(weight_files) != len(files):
             raise ValueError("The numbers of train files and weight files do not match.")
+        if any(native.cpu().is_bin_file(f) for f in files):
+            raise ValueError("binary CSR caches (.fmb) need the native loader ([Train] loader = native)")
         self.files = list(files)
         self.weight_files = list(weight_files) if weight_files else None
         self.B = int(batch_size)
@@ -167,6 +169,10 @@ class NativeTextReader:
     assembly (int32 offsets and ids) -- runs in a C++ producer thread that
     keeps ``queue_size`` batches ready; Python only wraps the arrays.
     The batch composition (RNG streams) differs from ``TextBatchReader``.
+
+    Binary CSR caches (``.fmb``, data/bincache.py) are detected by their magic: when every
+    file is one, the loader copies pre-parsed examples instead of parsing text (same
+    batches for the same seed; the weights come from the caches, so no weight files).
     """
 
     def __init__(self, files: list[str], weight_files: list[str] | None, batch_size: int, *, vocab_size: int,
@@ -175,6 +181,15 @@ class NativeTextReader:
                  queue_size: int = 4, gpu_parse: torch.device | str | None = None):
         if weight_files and len(weight_files) != len(files):
             raise ValueError("The numbers of train files and weight files do not match.")
+        kinds = {bool(native.cpu().is_bin_file(f)) for f in files}
+        if len(kinds) > 1:
+            raise ValueError("train files mix binary CSR caches (.fmb) and text files")
+        self.binary = kinds == {True}
+        if self.binary and weight_files:
+            raise ValueError("binary CSR caches (.fmb) already hold the weights of their conversion; "
+                             "remove weight_files")
+        if self.binary:
+            gpu_parse = None  # nothing to tokenize
         self.args = dict(files=list(files), weight_files=list(weight_files or []), batch_size=int(batch_size),
                          vocab_size=int(vocab_size), hash_feature_id=bool(hash_feature_id), shuffle=bool(shuffle),
                          num_epochs=int(num_epochs), seed=int(seed), threads=int(parse_threads), rank=int(rank),
@@ -194,7 +209,7 @@ class NativeTextReader:
 
     def __iter__(self):
         L = native.cpu().TextLoader(start_epoch=self.state.epoch, skip_batches=self.state.batches_in_epoch,
-                                    raw=self.gpu is not None, **self.args)
+                                    raw=self.gpu is not None, binary=self.binary, **self.args)
         self._loader = L
         stream = torch.cuda.Stream(self.gpu) if self.gpu is not None else None
         try:

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Input-pipeline throughput: text lines/s of the Python reader, the native C++
-loader (CPU parser) and the native loader + GPU tokenizer, on Criteo-shaped
-libsvm files written to a scratch directory.
+loader (CPU parser), the native loader + GPU tokenizer, and the native loader
+over binary CSR caches (.fmb, converted once), on Criteo-shaped libsvm files
+written to a scratch directory.
 
 usage: python tools/bench_input.py [--lines N] [--files F] [--batch B] [--threads T] [--dir D]
 """
@@ -16,6 +17,7 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
+from fast_tffm_amd.data import bincache  # noqa: E402
 from fast_tffm_amd.data.reader import NativeTextReader, TextBatchReader  # noqa: E402
 from fast_tffm_amd.data.synthetic import write_libsvm  # noqa: E402
 
@@ -60,6 +62,11 @@ def main():
         run(NativeTextReader(files[:1], wfiles[:1], a.batch, gpu_parse="cuda", **dict(kw, num_epochs=1)))  # warm-up
         results["native loader + GPU tokenizer"] = run(NativeTextReader(files, wfiles, a.batch, gpu_parse="cuda",
                                                                         **kw))
+    t = time.time()
+    caches = [p for p, _ in bincache.convert_files(files, wfiles, os.path.join(a.dir, "fmb"), 1_000_000,
+                                                   threads=a.threads)]
+    print(f"converted to .fmb in {time.time() - t:.1f}s", flush=True)
+    results["native loader (.fmb cache)"] = run(NativeTextReader(caches, None, a.batch, **kw))
     for k, (n, nnz, dt) in results.items():
         print(f"{k:32s} {n / dt / 1e6:7.2f} M lines/s  {nnz / dt / 1e6:8.1f} M features/s  ({n} lines, {dt:.2f}s)",
               flush=True)

@@ -37,8 +37,8 @@ learning_rate = 0.01
 adagrad.initial_accumulator = 0.1
 save_steps = 1000000
 loss_type = mse
-train_files = {data}/train_*
-weight_files = {data}/weight_*
+train_files = {train}
+{weights}
 parse_threads = {threads}
 gpu_parse = {gpu}
 log_steps = 1000000
@@ -67,10 +67,22 @@ def main():
         for s, d in ((src, f"train_{i}"), (wsrc, f"weight_{i}")):
             if not os.path.exists(os.path.join(data, d)):
                 shutil.copy(s, os.path.join(data, d))
-    for gpu in ("false", "true"):
+    text = dict(train=f"{data}/train_*", weights=f"weight_files = {data}/weight_*")
+    for gpu in ("false", "true", "fmb"):
         cfg = os.path.join(a.dir, f"e2e_{gpu}.cfg")
+        src = text if gpu != "fmb" else dict(train=f"{a.dir}/fmb/*.fmb", weights="")
         with open(cfg, "w") as f:
-            f.write(CFG.format(batch=a.batch, epochs=a.epochs, data=data, threads=a.threads, gpu=gpu))
+            f.write(CFG.format(batch=a.batch, epochs=a.epochs, threads=a.threads,
+                               gpu="false" if gpu == "fmb" else gpu, **src))
+        if gpu == "fmb":
+            t = time.time()
+            r = subprocess.run([sys.executable, os.path.join(ROOT, "run.py"), "convert",
+                                os.path.join(a.dir, "e2e_false.cfg"), "--out", os.path.join(a.dir, "fmb")],
+                               capture_output=True, text=True)
+            if r.returncode != 0:
+                print(r.stdout[-2000:], r.stderr[-3000:])
+                sys.exit(r.returncode)
+            print(f"run.py convert: {time.time() - t:.1f}s (incl. start-up)", flush=True)
         t = time.time()
         r = subprocess.run([sys.executable, os.path.join(ROOT, "run.py"), "train", cfg,
                             "--log-dir", os.path.join(a.dir, f"log_{gpu}")], capture_output=True, text=True)
@@ -79,7 +91,8 @@ def main():
             sys.exit(r.returncode)
         m = re.search(r"Average speed:\s+([0-9.eE+]+)", r.stdout)
         steps = len(re.findall(r"Global Step", r.stdout))
-        print(f"gpu_parse={gpu}: Average speed {float(m.group(1)):.4g} ex/s "
+        name = "binary .fmb caches" if gpu == "fmb" else f"gpu_parse={gpu}"
+        print(f"{name}: Average speed {float(m.group(1)):.4g} ex/s "
               f"({a.files * a.lines * a.epochs} examples, wall {time.time() - t:.1f}s incl. start-up)", flush=True)
 
 
