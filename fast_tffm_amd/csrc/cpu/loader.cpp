@@ -66,29 +66,31 @@ void assemble_binary(const std::vector<Item>& its, bool weighted, int64_t vocab,
   const size_t nnz = static_cast<size_t>(b.offsets[n]);
   b.ids.resize(nnz);
   if (any_vals) b.vals.resize(nnz);
-  const int T = std::max(1, std::min<int>(threads, static_cast<int>(nnz >> 16)));
+  // >= 256k ids per thread; pointers hoisted so the copies are plain memcpy (no aliasing
+  // through `b`), the range check runs over the thread's contiguous output afterwards
+  const int T = std::max(1, std::min<int>(threads, static_cast<int>(nnz >> 18)));
   std::vector<char> bad(static_cast<size_t>(T), 0);
-  auto work = [&](int t) {
+  int32_t* const ids_out = b.ids.data();
+  float* const vals_out = any_vals ? b.vals.data() : nullptr;
+  const int32_t* const offs = b.offsets.data();
+  const Item* const items = its.data();
+  const uint32_t V = static_cast<uint32_t>(vocab);
+  auto work = [=, &bad](int t) {
     const size_t i0 = n * t / T, i1 = n * (t + 1) / T;
     for (size_t i = i0; i < i1; ++i) {
-      const Item& it = its[i];
-      const int32_t* src = reinterpret_cast<const int32_t*>(it.line.p);
-      int32_t* dst = b.ids.data() + b.offsets[i];
-      uint32_t any = 0;
-      for (uint32_t j = 0; j < it.line.len; ++j) {
-        dst[j] = src[j];
-        any |= static_cast<uint32_t>(static_cast<uint64_t>(static_cast<uint32_t>(src[j])) >=
-                                     static_cast<uint64_t>(vocab));
-      }
-      bad[t] |= any != 0;
-      if (any_vals) {
-        float* v = b.vals.data() + b.offsets[i];
+      const Item& it = items[i];
+      std::memcpy(ids_out + offs[i], it.line.p, 4 * static_cast<size_t>(it.line.len));
+      if (vals_out) {
+        float* v = vals_out + offs[i];
         if (it.weight.p)
-          std::memcpy(v, it.weight.p, 4 * it.line.len);
+          std::memcpy(v, it.weight.p, 4 * static_cast<size_t>(it.line.len));
         else
           std::fill(v, v + it.line.len, 1.f);
       }
     }
+    uint32_t any = 0;
+    for (int32_t j = offs[i0]; j < offs[i1]; ++j) any |= static_cast<uint32_t>(ids_out[j]) >= V;
+    bad[t] = any != 0;
   };
   if (T == 1) {
     work(0);
