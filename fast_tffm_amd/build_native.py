@@ -30,6 +30,7 @@ ARCH = os.environ.get("FM_OFFLOAD_ARCH", "gfx950")
 CPU_SOURCES = ["cpu/module.cpp", "cpu/parser.cpp", "cpu/kernels.cpp", "cpu/loader.cpp", "cpu/bincsr.cpp"]
 HIP_SOURCES = ["hip/module.hip"]
 HIP_DEPS = ["hip/fm_fwd.hip", "hip/fm_bwd.hip", "hip/dedup.hip", "hip/shard.hip", "hip/init.hip", "hip/parse.hip",
+            "hip/batch_gather.hip",
             "hip/fm_common.h", "hash64.h"]
 # A/B build variants of the gfx950 module: name -> preprocessor defines (module _fm_hip_<name>,
 # selected at run time with FM_HIP_VARIANT=<name>; tools/gpu_ab.sh).  Used for same-box kernel

@@ -20,7 +20,7 @@ Extensions (new keys, all optional):
                 global_bias = true|false (learned b0; its gradient is all-reduced over ranks),
                 dtype = fp32|bf16|fp8 (fp8: OCP e4m3 + per-row scale, GPU)
   [Train]       optimizer = adagrad|ftrl|sgd, ftrl.l1, ftrl.l2, ftrl.beta,
-                ftrl.initial_accumulator, parse_threads, loader = native|python, gpu_parse = true|false, stochastic_rounding = true|false,
+                ftrl.initial_accumulator, parse_threads, loader = native|python, gpu_parse = true|false, device_cache = auto|true|false, stochastic_rounding = true|false,
                 shuffle = true|false,
                 max_steps, dedup_chunk, log_steps
   [Distributed] mode = auto|local|shard|dp|dp_dense, grad_reduce = sum|mean,
@@ -94,6 +94,8 @@ class FMRunConfig:
     parse_threads: int = 4
     loader: str = "native"      # native (C++ loader thread) | python
     gpu_parse: bool = False     # native loader: tokenize on the GPU (hip/parse.hip)
+    device_cache: str = "auto"  # .fmb train files: keep them in HBM, gather batches on the device
+                                # (auto: when they take <= 40% of the free device memory)
     stochastic_rounding: bool = True  # bf16 / fp8 tables: stochastically rounded updates
     shuffle: bool = True
     max_steps: int | None = None
@@ -198,6 +200,9 @@ def load_config(config_file: str, *, echo: bool = True, printer=print) -> FMRunC
     c.parse_threads = opt(TRAIN, "parse_threads", int, c.parse_threads)
     c.loader = opt(TRAIN, "loader", lambda s: s.strip().lower(), c.loader)
     c.gpu_parse = opt(TRAIN, "gpu_parse", lambda s: s.strip().lower() == "true", c.gpu_parse)
+    c.device_cache = opt(TRAIN, "device_cache", lambda s: s.strip().lower(), c.device_cache)
+    if c.device_cache not in ("auto", "true", "false"):
+        raise ConfigError(f"[Train] device_cache must be auto, true or false, got {c.device_cache}")
     c.stochastic_rounding = opt(TRAIN, "stochastic_rounding", lambda s: s.strip().lower() == "true",
                                 c.stochastic_rounding)
     if c.loader not in ("native", "python"):

@@ -39,7 +39,27 @@ void split_lines(const MappedFile& f, std::vector<Span>& out) {
 struct Item {
   Span line, weight;
   float label = 0.f, wt = 1.f;
+  int64_t row = -1;  // binary: global row (file rows concatenated in option order)
 };
+
+// rows mode: the batch's CSR offsets + global rows, the data stays where it is
+void emit_rows(const std::vector<Item>& its, LoadedBatch& b) {
+  const size_t n = its.size();
+  b.offsets.resize(n + 1);
+  b.rows.resize(n);
+  b.offsets[0] = 0;
+  int mf = 0;
+  bool vals = false;
+  for (size_t i = 0; i < n; ++i) {
+    const int c = static_cast<int>(its[i].line.len);
+    b.offsets[i + 1] = b.offsets[i] + c;
+    mf = std::max(mf, c);
+    b.rows[i] = its[i].row;
+    vals |= its[i].weight.p != nullptr;
+  }
+  b.max_feats = mf;
+  b.has_vals = vals;
+}
 
 // Copy n chosen binary examples into a CSR batch (offsets, ids, values, labels, weights)
 // with up to `threads` threads; ids are range-checked on the way (a corrupt cache must
@@ -113,6 +133,7 @@ TextLoader::TextLoader(LoaderOptions o) : o_(std::move(o)) {
   if (o_.binary && !o_.weight_files.empty())
     throw std::invalid_argument("binary CSR caches carry their weights; pass no weight files");
   if (o_.binary && o_.raw) throw std::invalid_argument("raw (GPU tokenizer) mode needs text files");
+  if (o_.rows && !o_.binary) throw std::invalid_argument("rows mode needs binary CSR caches");
   if (o_.queue_size < 1) o_.queue_size = 1;
   th_ = std::thread([this] { run(); });
 }
@@ -165,9 +186,11 @@ void TextLoader::run() {
     const size_t cap = std::max<size_t>(static_cast<size_t>(o_.capacity_factor * static_cast<double>(B)), B);
     const size_t nf = o_.files.size();
     bool weighted = !o_.weight_files.empty();
+    std::vector<int64_t> row_base(nf + 1, 0);  // binary: first global row of each file
     if (o_.binary && nf > 0) {  // every cache must match the model's id space and agree on weights
       for (size_t i = 0; i < nf; ++i) {
         BinFile f(o_.files[i]);
+        row_base[i + 1] = row_base[i] + f.h.n;
         if (f.h.vocab_size != o_.vocab_size || ((f.h.flags & kBinFlagHashed) != 0) != o_.hash_feature_id)
           throw std::runtime_error(o_.files[i] + ": converted with vocabulary_size " + std::to_string(f.h.vocab_size) +
                                    ", hash_feature_id " + ((f.h.flags & kBinFlagHashed) ? "True" : "False") +
@@ -246,7 +269,10 @@ void TextLoader::run() {
         if (count <= skip) return true;
         LoadedBatch b;
         if (o_.binary) {
-          assemble_binary(chosen, weighted, o_.vocab_size, o_.threads, b);
+          if (o_.rows)
+            emit_rows(chosen, b);
+          else
+            assemble_binary(chosen, weighted, o_.vocab_size, o_.threads, b);
           b.epoch = epoch;
           b.count = count;
           return push(std::move(b));
@@ -311,6 +337,7 @@ void TextLoader::run() {
             it.weight = {f.vals ? reinterpret_cast<const char*>(f.vals + o) : nullptr, 0};
             it.label = f.labels[i];
             it.wt = f.weights ? f.weights[i] : 1.f;
+            it.row = row_base[fi] + static_cast<int64_t>(i);
             window.push_back(it);
             if (window.size() - head >= cap) {
               if (!emit(static_cast<size_t>(B))) return;

@@ -23,7 +23,10 @@
 //    consumer copies to the device and tokenizes there.
 //  * binary mode (bincsr.h): the files are pre-parsed .fmb caches; the window
 //    holds examples instead of lines (same RNG draws) and a batch is assembled
-//    by copying the chosen examples' ids / values with `threads` threads.
+//    by copying the chosen examples' ids / values with `threads` threads; with
+//    `rows` set only the chosen examples' global row numbers (file rows
+//    concatenated in `files` order) and the batch's CSR offsets are emitted, and
+//    the device gathers the data from an HBM-resident copy (hip/batch_gather.hip).
 // A (start_epoch, skip_batches) position resumes exactly where a checkpoint
 // was taken: the RNGs are re-seeded per epoch, skipped batches are not parsed.
 #pragma once
@@ -56,6 +59,7 @@ struct LoaderOptions {
   double capacity_factor = 4.5;
   bool raw = false;           // emit the batch's line bytes (GPU tokenizer) instead of parsed CSR
   bool binary = false;        // files are .fmb binary CSR caches (weights inside; weight_files empty)
+  bool rows = false;          // binary: emit row numbers + offsets instead of the data
 };
 
 struct LoadedBatch {
@@ -67,6 +71,9 @@ struct LoadedBatch {
   // raw mode: the batch's lines, each '\n'-terminated, and their start offsets [B+1]
   std::vector<uint8_t> bytes;
   std::vector<int64_t> line_start;
+  // rows mode: global example rows [B] (offsets, max_feats filled; has_vals = some row has values)
+  std::vector<int64_t> rows;
+  bool has_vals = false;
   int max_feats = 0;
   int epoch = 0;
   int64_t count = 0;              // batches of this epoch consumed after this one

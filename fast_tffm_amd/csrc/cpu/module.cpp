@@ -193,20 +193,20 @@ PYBIND11_MODULE(_fm_cpu, m) {
       .def(py::init([](std::vector<std::string> files, std::vector<std::string> weight_files, long long batch_size,
                        long long vocab_size, bool hash_feature_id, bool shuffle, int num_epochs,
                        unsigned long long seed, int threads, int rank, int world, int queue_size, int start_epoch,
-                       long long skip_batches, bool raw, bool binary) {
+                       long long skip_batches, bool raw, bool binary, bool rows) {
              fm::LoaderOptions o;
              o.files = std::move(files); o.weight_files = std::move(weight_files); o.batch_size = batch_size;
              o.vocab_size = vocab_size; o.hash_feature_id = hash_feature_id; o.shuffle = shuffle;
              o.num_epochs = num_epochs; o.seed = seed; o.threads = threads; o.rank = rank; o.world = world;
              o.queue_size = queue_size; o.start_epoch = start_epoch; o.skip_batches = skip_batches; o.raw = raw;
-             o.binary = binary;
+             o.binary = binary; o.rows = rows;
              return new fm::TextLoader(std::move(o));
            }),
            py::arg("files"), py::arg("weight_files"), py::arg("batch_size"), py::arg("vocab_size"),
            py::arg("hash_feature_id") = false, py::arg("shuffle") = true, py::arg("num_epochs") = 1,
            py::arg("seed") = 0, py::arg("threads") = 4, py::arg("rank") = 0, py::arg("world") = 1,
            py::arg("queue_size") = 4, py::arg("start_epoch") = 0, py::arg("skip_batches") = 0,
-           py::arg("raw") = false, py::arg("binary") = false)
+           py::arg("raw") = false, py::arg("binary") = false, py::arg("rows") = false)
       // -> (labels, offsets, ids, vals | None, weights | None, max_feats, epoch, count) or None at the end
       .def("next",
            [](fm::TextLoader& L) -> py::object {
@@ -217,6 +217,10 @@ PYBIND11_MODULE(_fm_cpu, m) {
                ok = L.next(b);
              }
              if (!ok) return py::none();
+             if (!b.rows.empty()) {  // rows mode: (rows, offsets, has_vals, max_feats, epoch, count)
+               return py::make_tuple(to_numpy(std::move(b.rows)), to_numpy(std::move(b.offsets)), b.has_vals,
+                                     b.max_feats, b.epoch, b.count);
+             }
              if (!b.line_start.empty()) {  // raw mode: (bytes, line_start, weights | None, epoch, count)
                py::object w = b.weights.empty() ? py::object(py::none()) : py::object(to_numpy(std::move(b.weights)));
                return py::make_tuple(to_numpy(std::move(b.bytes)), to_numpy(std::move(b.line_start)), w, b.epoch,

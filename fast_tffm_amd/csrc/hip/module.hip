@@ -27,6 +27,7 @@ using u64 = std::uintptr_t;
 #include "shard.hip"
 #include "init.hip"
 #include "parse.hip"
+#include "batch_gather.hip"
 
 namespace {
 
@@ -310,6 +311,22 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("buf"), py::arg("line_start"), py::arg("n"), py::arg("vocab"), py::arg("hash"), py::arg("counts"),
       py::arg("offsets"), py::arg("labels"), py::arg("ids"), py::arg("vals"), py::arg("status"), py::arg("ws"),
       py::arg("ws_bytes"), py::arg("stream"), py::arg("require_vals") = 0);
+
+  m.def(
+      "batch_gather",
+      [](u64 rows, u64 boff, int B, long long N, u64 src_off, u64 src_ids, u64 src_vals, u64 src_labels,
+         u64 src_weights, u64 ids, u64 vals, u64 labels, u64 weights, u64 stream) {
+        fm::BatchGatherArgs a{};
+        a.rows = P<const long long>(rows); a.boff = P<const int>(boff); a.B = B; a.N = N;
+        a.src_off = P<const long long>(src_off); a.src_ids = P<const int>(src_ids);
+        a.src_vals = P<const float>(src_vals); a.src_labels = P<const float>(src_labels);
+        a.src_weights = P<const float>(src_weights); a.ids = P<int>(ids); a.vals = P<float>(vals);
+        a.labels = P<float>(labels); a.weights = P<float>(weights);
+        check(fm::launch_batch_gather(a, S(stream)), "batch_gather");
+      },
+      py::arg("rows"), py::arg("boff"), py::arg("B"), py::arg("N"), py::arg("src_off"), py::arg("src_ids"),
+      py::arg("src_vals"), py::arg("src_labels"), py::arg("src_weights"), py::arg("ids"), py::arg("vals"),
+      py::arg("labels"), py::arg("weights"), py::arg("stream"));
 
   m.def(
       "csr_rows",

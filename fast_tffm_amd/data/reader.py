@@ -173,12 +173,15 @@ class NativeTextReader:
     Binary CSR caches (``.fmb``, data/bincache.py) are detected by their magic: when every
     file is one, the loader copies pre-parsed examples instead of parsing text (same
     batches for the same seed; the weights come from the caches, so no weight files).
+    ``device_cache`` (a GPU) uploads the caches to HBM once (data/device_cache.py) and
+    the loader then ships only row numbers: batches are gathered on the device.
     """
 
     def __init__(self, files: list[str], weight_files: list[str] | None, batch_size: int, *, vocab_size: int,
                  hash_feature_id: bool = False, num_epochs: int = 1, shuffle: bool = True, seed: int = 0,
                  parse_threads: int = 4, rank: int = 0, world: int = 1, state: ReaderState | None = None,
-                 queue_size: int = 4, gpu_parse: torch.device | str | None = None):
+                 queue_size: int = 4, gpu_parse: torch.device | str | None = None,
+                 device_cache: torch.device | str | None = None):
         if weight_files and len(weight_files) != len(files):
             raise ValueError("The numbers of train files and weight files do not match.")
         kinds = {bool(native.cpu().is_bin_file(f)) for f in files}
@@ -203,20 +206,34 @@ class NativeTextReader:
         if self.gpu is not None and self.gpu.type != "cuda":
             self.gpu = None
         self.fallbacks = 0
+        self.dds = None
+        if device_cache is not None and self.binary and torch.device(device_cache).type == "cuda":
+            from .device_cache import DeviceDataset
+
+            self.dds = DeviceDataset(self.args["files"], device_cache, int(vocab_size), bool(hash_feature_id))
 
     def queued(self) -> int:
         return self._loader.queued() if self._loader is not None else 0
 
     def __iter__(self):
         L = native.cpu().TextLoader(start_epoch=self.state.epoch, skip_batches=self.state.batches_in_epoch,
-                                    raw=self.gpu is not None, binary=self.binary, **self.args)
+                                    raw=self.gpu is not None, binary=self.binary, rows=self.dds is not None,
+                                    **self.args)
         self._loader = L
-        stream = torch.cuda.Stream(self.gpu) if self.gpu is not None else None
+        dev = self.gpu if self.gpu is not None else (self.dds.device if self.dds is not None else None)
+        stream = torch.cuda.Stream(dev) if dev is not None else None
         try:
             while True:
                 item = L.next()
                 if item is None:
                     break
+                if self.dds is not None:
+                    rows, offsets, has_vals, max_feats, epoch, count = item
+                    b = self._gather_batch(rows, offsets, has_vals, int(max_feats), stream)
+                    self.state.epoch, self.state.batches_in_epoch = int(epoch), int(count)
+                    b.reader_pos = (int(epoch), int(count))
+                    yield b
+                    continue
                 if self.gpu is not None:
                     buf, line_start, weights, epoch, count = item
                     b = self._gpu_batch(buf, line_start, weights, stream)
@@ -235,6 +252,20 @@ class NativeTextReader:
             self.state.epoch, self.state.batches_in_epoch = self.num_epochs, 0
         finally:
             L.close()
+
+    def _gather_batch(self, rows: np.ndarray, offsets: np.ndarray, has_vals: bool, max_feats: int, stream) -> Batch:
+        """H2D of the batch's row numbers + offsets and the device gather (hip/batch_gather.hip)
+        on ``stream``; returns a device batch whose work has completed."""
+        dev = self.dds.device
+        with torch.cuda.stream(stream):
+            hr = torch.from_numpy(rows).pin_memory()
+            ho = torch.from_numpy(offsets)
+            d_rows = hr.to(dev, non_blocking=True)
+            d_off = ho.pin_memory().to(dev, non_blocking=True)
+            nnz = int(offsets[-1])
+            labels, ids, vals, weights = self.dds.gather(d_rows, d_off, nnz, bool(has_vals), stream)
+            stream.synchronize()
+        return Batch(labels, d_off, ids, vals, weights, nnz, max_feats=max_feats, offsets_host=ho)
 
     def _gpu_batch(self, buf: np.ndarray, line_start: np.ndarray, weights, stream) -> Batch:
         """H2D of the raw lines + GPU tokenizer on ``stream`` (CPU parser when the batch has syntax

@@ -108,6 +108,21 @@ class Trainer:
             b = _take(b, idx)
         return b.to(self.device)
 
+    def _device_cache(self):
+        """The device to keep .fmb training files on, or None ([Train] device_cache)."""
+        c = self.cfg
+        if c.device_cache == "false" or self.device.type != "cuda" or not c.train_files:
+            return None
+        from .data import bincache, device_cache
+
+        if not all(bincache.is_bin_file(f) for f in c.train_files):
+            return None
+        if c.device_cache == "auto":
+            free, _ = torch.cuda.mem_get_info(self.device)
+            if device_cache.dataset_bytes(c.train_files) > 0.4 * free:
+                return None
+        return self.device
+
     def validation_loss(self, vb) -> float:
         fo = self.model.forward(vb, loss=self.cfg.loss_type)
         return self._global_loss(float(fo.loss_sum), vb.B)
@@ -122,7 +137,11 @@ class Trainer:
                   state=ReaderState(self.reader_state.epoch, self.reader_state.batches_in_epoch))
         if c.loader == "native":
             reader = NativeTextReader(c.train_files, c.weight_files or None, c.batch_size,
-                                      gpu_parse=self.device if c.gpu_parse else None, **kw)
+                                      gpu_parse=self.device if c.gpu_parse else None,
+                                      device_cache=self._device_cache(), **kw)
+            if reader.dds is not None:
+                self.print(f"Training data resident on {self.device}: {reader.dds.N} examples, "
+                           f"{reader.dds.nbytes / 2**30:.2f} GiB")
         else:
             reader = TextBatchReader(c.train_files, c.weight_files or None, c.batch_size, **kw)
         pf = Prefetcher(reader, self.device, queue_size=max(1, min(c.queue_size, 64)))

@@ -189,3 +189,56 @@ predict_files =
             assert cli.main(["train", str(c)]) == 0
         outs.append(re.findall(r"-- Global Step: \d+; Avg loss: ([0-9.]+);", buf.getvalue()))
     assert len(outs[0]) == 6 and outs[0] == outs[1]  # same batches -> same losses
+
+
+def _host_gather(caches, rows):
+    """Reference gather of global rows from the cache files (numpy, via the header layout)."""
+    from fast_tffm_amd.data.device_cache import read_header
+
+    parts = []
+    for c in caches:
+        h = read_header(c)
+        mm = np.memmap(c, dtype=np.uint8, mode="r")
+        off = np.frombuffer(mm, np.int64, h["n"] + 1, h["offsets"])
+        parts.append((h, mm, off))
+    labels, ids, vals, weights = [], [], [], []
+    base = np.cumsum([0] + [p[0]["n"] for p in parts])
+    for r in rows:
+        fi = int(np.searchsorted(base, r, side="right") - 1)
+        h, mm, off = parts[fi]
+        i = int(r - base[fi])
+        labels.append(np.frombuffer(mm, np.float32, 1, h["labels"] + 4 * i)[0])
+        weights.append(np.frombuffer(mm, np.float32, 1, h["weights"] + 4 * i)[0] if h["weights"] >= 0 else 1.0)
+        k = int(off[i + 1] - off[i])
+        ids.append(np.frombuffer(mm, np.int32, k, h["ids"] + 4 * int(off[i])))
+        vals.append(np.frombuffer(mm, np.float32, k, h["vals"] + 4 * int(off[i])) if h["vals"] >= 0
+                    else np.ones(k, np.float32))
+    return (np.array(labels, np.float32), np.concatenate(ids), np.concatenate(vals), np.array(weights, np.float32))
+
+
+def test_rows_mode_names_the_binary_batches(data):
+    """Rows mode (the device cache's host half) emits the rows whose data the binary mode copies."""
+    from fast_tffm_amd.ops import native
+
+    _, _, caches = data
+    kw = dict(batch_size=97, vocab_size=V, shuffle=True, num_epochs=2, seed=5, threads=2, rank=0, world=1)
+    La = native.cpu().TextLoader(caches, [], binary=True, **kw)
+    Lr = native.cpu().TextLoader(caches, [], binary=True, rows=True, **kw)
+    nb = 0
+    while True:
+        a, r = La.next(), Lr.next()
+        if a is None:
+            assert r is None
+            break
+        labels, offsets, ids, vals, weights, mf, ep, cnt = a
+        rows, roffs, has_vals, rmf, rep, rcnt = r
+        assert (ep, cnt, mf) == (rep, rcnt, rmf) and np.array_equal(offsets, roffs)
+        assert has_vals == (vals is not None)
+        hl, hi, hv, hw = _host_gather(caches, rows)
+        np.testing.assert_array_equal(labels, hl)
+        np.testing.assert_array_equal(ids, hi)
+        np.testing.assert_array_equal(weights, hw)
+        if vals is not None:
+            np.testing.assert_array_equal(vals, hv)
+        nb += 1
+    assert nb > 10

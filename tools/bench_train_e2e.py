@@ -41,6 +41,7 @@ train_files = {train}
 {weights}
 parse_threads = {threads}
 gpu_parse = {gpu}
+device_cache = {dcache}
 log_steps = 1000000
 [Predict]
 predict_files =
@@ -68,12 +69,13 @@ def main():
             if not os.path.exists(os.path.join(data, d)):
                 shutil.copy(s, os.path.join(data, d))
     text = dict(train=f"{data}/train_*", weights=f"weight_files = {data}/weight_*")
-    for gpu in ("false", "true", "fmb"):
+    for gpu in ("false", "true", "fmb", "fmb_hbm"):
         cfg = os.path.join(a.dir, f"e2e_{gpu}.cfg")
-        src = text if gpu != "fmb" else dict(train=f"{a.dir}/fmb/*.fmb", weights="")
+        fmb = gpu.startswith("fmb")
+        src = text if not fmb else dict(train=f"{a.dir}/fmb/*.fmb", weights="")
         with open(cfg, "w") as f:
-            f.write(CFG.format(batch=a.batch, epochs=a.epochs, threads=a.threads,
-                               gpu="false" if gpu == "fmb" else gpu, **src))
+            f.write(CFG.format(batch=a.batch, epochs=a.epochs, threads=a.threads, gpu="false" if fmb else gpu,
+                               dcache="true" if gpu == "fmb_hbm" else "false", **src))
         if gpu == "fmb":
             t = time.time()
             r = subprocess.run([sys.executable, os.path.join(ROOT, "run.py"), "convert",
@@ -83,6 +85,7 @@ def main():
                 print(r.stdout[-2000:], r.stderr[-3000:])
                 sys.exit(r.returncode)
             print(f"run.py convert: {time.time() - t:.1f}s (incl. start-up)", flush=True)
+        shutil.rmtree(os.path.join(a.dir, f"log_{gpu}"), ignore_errors=True)  # no auto-resume of an old run
         t = time.time()
         r = subprocess.run([sys.executable, os.path.join(ROOT, "run.py"), "train", cfg,
                             "--log-dir", os.path.join(a.dir, f"log_{gpu}")], capture_output=True, text=True)
@@ -91,7 +94,8 @@ def main():
             sys.exit(r.returncode)
         m = re.search(r"Average speed:\s+([0-9.eE+]+)", r.stdout)
         steps = len(re.findall(r"Global Step", r.stdout))
-        name = "binary .fmb caches" if gpu == "fmb" else f"gpu_parse={gpu}"
+        name = {"fmb": "binary .fmb caches (host assembly)",
+                "fmb_hbm": "binary .fmb caches resident in HBM"}.get(gpu, f"gpu_parse={gpu}")
         print(f"{name}: Average speed {float(m.group(1)):.4g} ex/s "
               f"({a.files * a.lines * a.epochs} examples, wall {time.time() - t:.1f}s incl. start-up)", flush=True)
 
