@@ -112,5 +112,5 @@ predict_files =
         outs.append(buf.getvalue())
     assert "Training data resident on cuda" in outs[1]
     la, lb = (re.findall(r"-- Global Step: \d+; Avg loss: ([0-9.]+);", o) for o in outs)
-    assert len(la) == 8 and la == lb
+    assert len(la) == 16 and la == lb
     torch.cuda.synchronize()
