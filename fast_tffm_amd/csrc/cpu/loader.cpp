@@ -34,16 +34,49 @@ void split_lines(const MappedFile& f, std::vector<Span>& out) {
   }
 }
 
-// A window entry: a text line (+ its weight line), or in binary mode one example of a
-// mapped .fmb file (line = its ids as (int32*, n), weight.p = its values or null).
+// A window entry of the text path: a line (+ its weight line).
 struct Item {
   Span line, weight;
-  float label = 0.f, wt = 1.f;
-  int64_t row = -1;  // binary: global row (file rows concatenated in option order)
+};
+
+// A window entry of the binary path (16 bytes: the window is shuffled in place, so it
+// pays to keep it small): global row (file rows concatenated in option order), its
+// feature count and file index; the data is looked up only for the chosen rows.
+struct BinItem {
+  int64_t row;
+  uint32_t len;
+  uint32_t file;
+};
+
+// Take n entries from the window into `out`: a uniform sample moved to the back by a
+// partial Fisher-Yates when shuffling, else the FIFO head.
+template <class T, class R>
+void draw(std::vector<T>& win, size_t& head, size_t n, bool shuffle, R& rng, std::vector<T>& out) {
+  if (shuffle) {
+    const size_t w = win.size();
+    for (size_t i = 0; i < n; ++i) {
+      const size_t j = i + static_cast<size_t>(rng() % (w - i));
+      std::swap(win[w - 1 - i], win[w - 1 - j]);
+    }
+    out.assign(win.end() - static_cast<std::ptrdiff_t>(n), win.end());
+    win.resize(w - n);
+  } else {
+    out.assign(win.begin() + static_cast<std::ptrdiff_t>(head), win.begin() + static_cast<std::ptrdiff_t>(head + n));
+    head += n;
+    if (head > (1u << 20) && head * 2 > win.size()) {
+      win.erase(win.begin(), win.begin() + static_cast<std::ptrdiff_t>(head));
+      head = 0;
+    }
+  }
+}
+
+struct BinSet {
+  std::vector<std::unique_ptr<BinFile>> files;
+  std::vector<int64_t> base;  // first global row of each file
 };
 
 // rows mode: the batch's CSR offsets + global rows, the data stays where it is
-void emit_rows(const std::vector<Item>& its, LoadedBatch& b) {
+void emit_rows(const std::vector<BinItem>& its, const BinSet& bs, LoadedBatch& b) {
   const size_t n = its.size();
   b.offsets.resize(n + 1);
   b.rows.resize(n);
@@ -51,11 +84,11 @@ void emit_rows(const std::vector<Item>& its, LoadedBatch& b) {
   int mf = 0;
   bool vals = false;
   for (size_t i = 0; i < n; ++i) {
-    const int c = static_cast<int>(its[i].line.len);
+    const int c = static_cast<int>(its[i].len);
     b.offsets[i + 1] = b.offsets[i] + c;
     mf = std::max(mf, c);
     b.rows[i] = its[i].row;
-    vals |= its[i].weight.p != nullptr;
+    vals |= bs.files[its[i].file]->vals != nullptr;
   }
   b.max_feats = mf;
   b.has_vals = vals;
@@ -64,7 +97,8 @@ void emit_rows(const std::vector<Item>& its, LoadedBatch& b) {
 // Copy n chosen binary examples into a CSR batch (offsets, ids, values, labels, weights)
 // with up to `threads` threads; ids are range-checked on the way (a corrupt cache must
 // not reach the device kernels as an out-of-bounds row).
-void assemble_binary(const std::vector<Item>& its, bool weighted, int64_t vocab, int threads, LoadedBatch& b) {
+void assemble_binary(const std::vector<BinItem>& its, const BinSet& bs, bool weighted, int64_t vocab, int threads,
+                     LoadedBatch& b) {
   const size_t n = its.size();
   b.labels.resize(n);
   b.offsets.resize(n + 1);
@@ -72,16 +106,12 @@ void assemble_binary(const std::vector<Item>& its, bool weighted, int64_t vocab,
   bool any_vals = false;
   int mf = 0;
   for (size_t i = 0; i < n; ++i) {
-    const int c = static_cast<int>(its[i].line.len);
+    const int c = static_cast<int>(its[i].len);
     b.offsets[i + 1] = b.offsets[i] + c;
     mf = std::max(mf, c);
-    b.labels[i] = its[i].label;
-    any_vals |= its[i].weight.p != nullptr;
+    any_vals |= bs.files[its[i].file]->vals != nullptr;
   }
-  if (weighted) {
-    b.weights.resize(n);
-    for (size_t i = 0; i < n; ++i) b.weights[i] = its[i].wt;
-  }
+  if (weighted) b.weights.resize(n);
   b.max_feats = mf;
   const size_t nnz = static_cast<size_t>(b.offsets[n]);
   b.ids.resize(nnz);
@@ -92,20 +122,29 @@ void assemble_binary(const std::vector<Item>& its, bool weighted, int64_t vocab,
   std::vector<char> bad(static_cast<size_t>(T), 0);
   int32_t* const ids_out = b.ids.data();
   float* const vals_out = any_vals ? b.vals.data() : nullptr;
+  float* const lab_out = b.labels.data();
+  float* const w_out = weighted ? b.weights.data() : nullptr;
   const int32_t* const offs = b.offsets.data();
-  const Item* const items = its.data();
+  const BinItem* const items = its.data();
+  const BinFile* const* const files = reinterpret_cast<const BinFile* const*>(bs.files.data());
+  const int64_t* const base = bs.base.data();
   const uint32_t V = static_cast<uint32_t>(vocab);
   auto work = [=, &bad](int t) {
     const size_t i0 = n * t / T, i1 = n * (t + 1) / T;
     for (size_t i = i0; i < i1; ++i) {
-      const Item& it = items[i];
-      std::memcpy(ids_out + offs[i], it.line.p, 4 * static_cast<size_t>(it.line.len));
+      const BinItem& it = items[i];
+      const BinFile& f = *files[it.file];
+      const int64_t r = it.row - base[it.file];
+      const int64_t o = f.offsets[r];
+      std::memcpy(ids_out + offs[i], f.ids + o, 4 * static_cast<size_t>(it.len));
+      lab_out[i] = f.labels[r];
+      if (w_out) w_out[i] = f.weights ? f.weights[r] : 1.f;
       if (vals_out) {
         float* v = vals_out + offs[i];
-        if (it.weight.p)
-          std::memcpy(v, it.weight.p, 4 * static_cast<size_t>(it.line.len));
+        if (f.vals)
+          std::memcpy(v, f.vals + o, 4 * static_cast<size_t>(it.len));
         else
-          std::fill(v, v + it.line.len, 1.f);
+          std::fill(v, v + it.len, 1.f);
       }
     }
     uint32_t any = 0;
@@ -186,11 +225,13 @@ void TextLoader::run() {
     const size_t cap = std::max<size_t>(static_cast<size_t>(o_.capacity_factor * static_cast<double>(B)), B);
     const size_t nf = o_.files.size();
     bool weighted = !o_.weight_files.empty();
-    std::vector<int64_t> row_base(nf + 1, 0);  // binary: first global row of each file
+    BinSet bs;  // binary: every cache mapped and validated once, for all epochs
     if (o_.binary && nf > 0) {  // every cache must match the model's id space and agree on weights
+      bs.base.assign(nf + 1, 0);
       for (size_t i = 0; i < nf; ++i) {
-        BinFile f(o_.files[i]);
-        row_base[i + 1] = row_base[i] + f.h.n;
+        bs.files.push_back(std::make_unique<BinFile>(o_.files[i]));
+        const BinFile& f = *bs.files.back();
+        bs.base[i + 1] = bs.base[i] + f.h.n;
         if (f.h.vocab_size != o_.vocab_size || ((f.h.flags & kBinFlagHashed) != 0) != o_.hash_feature_id)
           throw std::runtime_error(o_.files[i] + ": converted with vocabulary_size " + std::to_string(f.h.vocab_size) +
                                    ", hash_feature_id " + ((f.h.flags & kBinFlagHashed) ? "True" : "False") +
@@ -202,6 +243,7 @@ void TextLoader::run() {
       }
     }
     std::vector<Item> window, chosen;
+    std::vector<BinItem> bwindow, bchosen;
     std::vector<const char*> ptrs, wptrs;
     std::vector<size_t> lens, wlens;
     std::vector<Span> lines, wlines;
@@ -226,57 +268,34 @@ void TextLoader::run() {
                           0x9E3779B97F4A7C15ull * static_cast<uint64_t>(epoch + 1));
       int64_t count = 0;
       window.clear();
+      bwindow.clear();
       size_t head = 0;  // FIFO start (no-shuffle mode)
       std::vector<std::unique_ptr<MappedFile>> maps;  // alive until the epoch's batches are parsed
-      std::vector<std::unique_ptr<BinFile>> bins;
 
-      // Draw n items from the window into ptrs/lens (random when shuffling, FIFO otherwise)
-      // and parse them unless the batch is skipped (resume).
+      // Draw n items from the window (random when shuffling, FIFO otherwise) and build the
+      // batch unless it is skipped (resume).
       auto emit = [&](size_t n) -> bool {
         ++count;
-        ptrs.clear(); lens.clear(); wptrs.clear(); wlens.clear(); chosen.clear();
-        if (o_.shuffle) {
-          const size_t w = window.size();
-          for (size_t i = 0; i < n; ++i) {  // partial Fisher-Yates: a uniform sample moved to the back
-            const size_t j = i + static_cast<size_t>(rng() % (w - i));
-            std::swap(window[w - 1 - i], window[w - 1 - j]);
-          }
-          if (o_.binary)
-            chosen.assign(window.end() - static_cast<std::ptrdiff_t>(n), window.end());
-          else
-            for (size_t i = 0; i < n; ++i) {
-              const Item& it = window[w - n + i];
-              ptrs.push_back(it.line.p); lens.push_back(it.line.len);
-              wptrs.push_back(it.weight.p); wlens.push_back(it.weight.len);
-            }
-          window.resize(w - n);
-        } else {
-          if (o_.binary)
-            chosen.assign(window.begin() + static_cast<std::ptrdiff_t>(head),
-                          window.begin() + static_cast<std::ptrdiff_t>(head + n));
-          else
-            for (size_t i = 0; i < n; ++i) {
-              const Item& it = window[head + i];
-              ptrs.push_back(it.line.p); lens.push_back(it.line.len);
-              wptrs.push_back(it.weight.p); wlens.push_back(it.weight.len);
-            }
-          head += n;
-          if (head > (1u << 20) && head * 2 > window.size()) {
-            window.erase(window.begin(), window.begin() + static_cast<std::ptrdiff_t>(head));
-            head = 0;
-          }
-        }
-        if (count <= skip) return true;
-        LoadedBatch b;
         if (o_.binary) {
+          draw(bwindow, head, n, o_.shuffle, rng, bchosen);
+          if (count <= skip) return true;
+          LoadedBatch b;
           if (o_.rows)
-            emit_rows(chosen, b);
+            emit_rows(bchosen, bs, b);
           else
-            assemble_binary(chosen, weighted, o_.vocab_size, o_.threads, b);
+            assemble_binary(bchosen, bs, weighted, o_.vocab_size, o_.threads, b);
           b.epoch = epoch;
           b.count = count;
           return push(std::move(b));
         }
+        draw(window, head, n, o_.shuffle, rng, chosen);
+        if (count <= skip) return true;
+        ptrs.clear(); lens.clear(); wptrs.clear(); wlens.clear();
+        for (const Item& it : chosen) {
+          ptrs.push_back(it.line.p); lens.push_back(it.line.len);
+          wptrs.push_back(it.weight.p); wlens.push_back(it.weight.len);
+        }
+        LoadedBatch b;
         if (o_.raw) {
           size_t total = 0;
           for (size_t i = 0; i < n; ++i) total += lens[i] + 1;
@@ -327,19 +346,12 @@ void TextLoader::run() {
 
       for (size_t fi : order) {
         if (o_.binary) {
-          bins.push_back(std::make_unique<BinFile>(o_.files[fi]));
-          const BinFile& f = *bins.back();
+          const BinFile& f = *bs.files[fi];
           const size_t step = line_shard ? static_cast<size_t>(o_.world) : 1;
           for (size_t i = line_shard ? static_cast<size_t>(o_.rank) : 0; i < static_cast<size_t>(f.h.n); i += step) {
-            const int64_t o = f.offsets[i];
-            Item it;
-            it.line = {reinterpret_cast<const char*>(f.ids + o), static_cast<uint32_t>(f.offsets[i + 1] - o)};
-            it.weight = {f.vals ? reinterpret_cast<const char*>(f.vals + o) : nullptr, 0};
-            it.label = f.labels[i];
-            it.wt = f.weights ? f.weights[i] : 1.f;
-            it.row = row_base[fi] + static_cast<int64_t>(i);
-            window.push_back(it);
-            if (window.size() - head >= cap) {
+            bwindow.push_back({bs.base[fi] + static_cast<int64_t>(i), static_cast<uint32_t>(f.offsets[i + 1] - f.offsets[i]),
+                               static_cast<uint32_t>(fi)});
+            if (bwindow.size() - head >= cap) {
               if (!emit(static_cast<size_t>(B))) return;
             }
           }
@@ -369,8 +381,9 @@ void TextLoader::run() {
           if (stop_) return;
         }
       }
-      while (window.size() > head) {
-        if (!emit(std::min<size_t>(static_cast<size_t>(B), window.size() - head))) return;
+      const auto left = [&] { return (o_.binary ? bwindow.size() : window.size()) - head; };
+      while (left() > 0) {
+        if (!emit(std::min<size_t>(static_cast<size_t>(B), left()))) return;
       }
     }
   } catch (const ParseError& e) {
