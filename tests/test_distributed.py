@@ -1,4 +1,4 @@
-"""Multi-rank correctness on CPU (gloo, world_size 2): every exchange mode is a
+"""Multi-rank correctness on CPU (gloo, world_size 2; shard / dp_dense also at 4 and 8): every exchange mode is a
 drop-in replacement for the single-process step.
 
 * ``shard`` (row-sharded table, all-to-all lookups/grads), ``dp`` (replicated,
@@ -68,10 +68,10 @@ def _worker(rank, world, port, mode, grad_reduce, out_dir, mb=0):
     fmdist.shutdown()
 
 
-def _run_world(tmp_path, mode, grad_reduce, mb=0):
+def _run_world(tmp_path, mode, grad_reduce, mb=0, world=WORLD):
     port = _free_port()
-    mp.spawn(_worker, args=(WORLD, port, mode, grad_reduce, str(tmp_path), mb), nprocs=WORLD, join=True)
-    return [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(WORLD)]
+    mp.spawn(_worker, args=(world, port, mode, grad_reduce, str(tmp_path), mb), nprocs=world, join=True)
+    return [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(world)]
 
 
 def _concat(batches, weight_mult=1.0):
@@ -86,12 +86,12 @@ def _concat(batches, weight_mult=1.0):
     return Batch(torch.cat(labels), torch.cat(offs), torch.cat(ids), torch.cat(vals), torch.cat(weights), base)
 
 
-def _single(grad_reduce):
-    bcfg = 16 * WORLD if grad_reduce == "mean" else 16
+def _single(grad_reduce, world=WORLD):
+    bcfg = 16 * world if grad_reduce == "mean" else 16
     m = FactorizationMachine(_cfg("local", "sum", bcfg), device="cpu")
-    wm = 1.0 if grad_reduce == "mean" else float(WORLD)
+    wm = 1.0 if grad_reduce == "mean" else float(world)
     for s in range(STEPS):
-        m.train_step(_concat([_batch(s, r) for r in range(WORLD)], wm))
+        m.train_step(_concat([_batch(s, r) for r in range(world)], wm))
     return m
 
 
@@ -134,3 +134,25 @@ def test_multi_rank_equals_single_process(tmp_path, mode, grad_reduce, mb):
         m2 = FactorizationMachine(_cfg("local", "sum", 16), device="cpu")
         ckpt.import_reference_blocks(m2, str(tmp_path / "ref"), 4)
         assert torch.equal(m2.table.reference_rows(), _assemble(res))  # bit-exact round trip of the shards
+
+
+@pytest.mark.parametrize("world,mode", [(4, "shard"), (8, "shard"), (4, "dp_dense")])
+def test_larger_worlds_equal_single_process(tmp_path, world, mode):
+    """World 4 / 8 (the node sizes of the scaling runs): the sharded step with its N>1
+    pipelining (depth-2 plan, early row exchange with dirty-row patches, split backward
+    with per-owner halves) and the dense all-reduce mode equal one process on the
+    concatenated batches; the W-shard checkpoint re-shards into one table."""
+    res = _run_world(tmp_path, mode, "mean", 0, world)
+    ref = _single("mean", world)
+    ref_rows = ref.table.reference_rows()
+    if mode == "shard":
+        torch.testing.assert_close(_assemble(res), ref_rows, rtol=1e-5, atol=1e-7)
+        m1 = FactorizationMachine(_cfg("local", "sum", 16), device="cpu")
+        meta = ckpt.restore_checkpoint(m1, ckpt.latest_checkpoint(str(tmp_path / "log")))
+        assert meta["shard_world"] == world
+        torch.testing.assert_close(m1.table.reference_rows(), ref_rows, rtol=1e-5, atol=1e-7)
+    else:
+        for r in res:
+            torch.testing.assert_close(r["rows"], ref_rows, rtol=1e-5, atol=1e-7)
+    for rank, r in enumerate(res):
+        torch.testing.assert_close(r["pred"], ref.predict(_batch(99, rank)), rtol=1e-5, atol=1e-6)
