@@ -53,9 +53,46 @@ def parse_lines_to_batch(lines: list[bytes], vocab_size: int, hash_feature_id: b
     return Batch.from_parsed(labels, sizes, ids, vals, weights)
 
 
+def _load_bin_batch(files: list[str], vocab_size: int, hash_feature_id: bool) -> Batch:
+    """All examples of binary CSR caches (in order) as one host batch."""
+    from .device_cache import F_HASHED, read_header
+
+    labels, weights, sizes, ids, vals = [], [], [], [], []
+    hs = [read_header(f) for f in files]
+    any_w = any(h["weights"] >= 0 for h in hs)
+    for f, h in zip(files, hs):
+        if h["vocab_size"] != vocab_size or bool(h["flags"] & F_HASHED) != bool(hash_feature_id):
+            raise ValueError(f"{f}: converted with vocabulary_size {h['vocab_size']}, hash_feature_id "
+                             f"{bool(h['flags'] & F_HASHED)}; the model uses {vocab_size}, {bool(hash_feature_id)}")
+        mm = np.memmap(f, dtype=np.uint8, mode="r")
+        n, z = h["n"], h["nnz"]
+        labels.append(np.frombuffer(mm, np.float32, n, h["labels"]).copy())
+        weights.append(np.frombuffer(mm, np.float32, n, h["weights"]).copy() if h["weights"] >= 0
+                       else np.ones(n, np.float32))
+        sizes.append(np.diff(np.frombuffer(mm, np.int64, n + 1, h["offsets"])).astype(np.int32))
+        fid = np.frombuffer(mm, np.int32, z, h["ids"]).copy()
+        if z and (int(fid.min()) < 0 or int(fid.max()) >= vocab_size):
+            raise ValueError(f"{f}: feature ids outside [0, {vocab_size})")
+        ids.append(fid)
+        vals.append(np.frombuffer(mm, np.float32, z, h["vals"]).copy() if h["vals"] >= 0 else np.ones(z, np.float32))
+        del mm
+    cat = (lambda xs, dt: np.concatenate(xs) if xs else np.zeros(0, dt))
+    return Batch.from_parsed(cat(labels, np.float32), cat(sizes, np.int32), cat(ids, np.int32),
+                             cat(vals, np.float32), cat(weights, np.float32) if any_w else None)
+
+
 def load_file_batch(files: list[str], weight_files: list[str] | None, vocab_size: int, hash_feature_id: bool,
                     threads: int = 4) -> Batch:
-    """All lines of ``files`` (in order) as one batch (validation / predict)."""
+    """All lines of ``files`` (in order) as one batch (validation / predict); binary CSR
+    caches (.fmb) are read directly (their weights are inside: no weight files)."""
+    kinds = {bool(native.cpu().is_bin_file(f)) for f in files}
+    if kinds == {True}:
+        if weight_files:
+            raise ValueError("binary CSR caches (.fmb) already hold the weights of their conversion; "
+                             "remove the weight files")
+        return _load_bin_batch(files, vocab_size, hash_feature_id)
+    if len(kinds) > 1:
+        raise ValueError("files mix binary CSR caches (.fmb) and text files")
     lines: list[bytes] = []
     for f in files:
         lines.extend(_read_lines(f))

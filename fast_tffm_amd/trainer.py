@@ -273,8 +273,12 @@ def _take(b, idx: torch.Tensor):
     o = b.offsets.long()
     sizes = (o[1:] - o[:-1])[idx]
     starts = o[:-1][idx]
-    gather = torch.cat([torch.arange(int(s), int(s) + int(n)) for s, n in zip(starts, sizes)]) if idx.numel() else \
-        torch.zeros(0, dtype=torch.long)
+    # feature positions of the chosen examples, vectorised: start of each example repeated
+    # over its features + the position inside the example
+    ends = torch.cumsum(sizes, 0)
+    total = int(ends[-1]) if idx.numel() else 0
+    within = torch.arange(total, dtype=torch.long) - torch.repeat_interleave(ends - sizes, sizes)
+    gather = torch.repeat_interleave(starts, sizes) + within
     offs = torch.zeros(idx.numel() + 1, dtype=torch.int32)
     offs[1:] = torch.cumsum(sizes, 0)
     return Batch(b.labels[idx], offs, b.ids[gather], None if b.vals is None else b.vals[gather],

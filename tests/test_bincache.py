@@ -242,3 +242,39 @@ def test_rows_mode_names_the_binary_batches(data):
             np.testing.assert_array_equal(vals, hv)
         nb += 1
     assert nb > 10
+
+
+def test_file_batch_from_caches_equals_text(data):
+    """Validation / predict inputs: a cache loads as the same one-batch CSR as its text file."""
+    from fast_tffm_amd.data.reader import load_file_batch
+
+    files, wfiles, caches = data
+    a = load_file_batch(files, wfiles, V, False, 2)
+    b = load_file_batch(caches, None, V, False, 2)
+    for x, y in ((a.labels, b.labels), (a.offsets, b.offsets), (a.ids, b.ids), (a.vals, b.vals),
+                 (a.weights, b.weights)):
+        assert x is not None and y is not None and np.array_equal(x.numpy(), y.numpy())
+    assert (a.nnz, a.max_feats) == (b.nnz, b.max_feats)
+    c = load_file_batch(caches[:1], None, V, False, 2)  # file 0: all values 1 -> no value array
+    assert c.vals is None
+    with pytest.raises(ValueError, match="already hold the weights"):
+        load_file_batch(caches, wfiles, V, False)
+
+
+def test_take_rank_slice():
+    """trainer._take (rank-strided sub-batch for distributed predict / validation)."""
+    import torch
+
+    from fast_tffm_amd.data.synthetic import random_batch
+    from fast_tffm_amd.trainer import _take
+
+    b = random_batch(57, 1000, max_feats=9, seed=4)
+    for idx in (torch.arange(1, 57, 3), torch.arange(0), torch.tensor([5])):
+        t = _take(b, idx)
+        o = b.offsets.long()
+        want = [b.ids[int(o[i]): int(o[i + 1])] for i in idx]
+        assert torch.equal(t.ids, torch.cat(want) if want else b.ids[:0])
+        assert torch.equal(t.labels, b.labels[idx]) and t.B == idx.numel()
+        if b.vals is not None:
+            assert torch.equal(t.vals, torch.cat([b.vals[int(o[i]): int(o[i + 1])] for i in idx]) if want
+                               else b.vals[:0])
