@@ -196,7 +196,7 @@ def main() -> int:
     if rank == 0:
         par = ("rowshard%d" % W) if model.mode == "shard" else (model.mode + str(W) if W > 1 else "single")
         print(f"[bench] loss={loss:.5f} ms/step={ms:.3f} ex/s={value:.4g}", file=sys.stderr)
-        print(json.dumps({
+        line = json.dumps({
             "metric": ("examples/sec (whole node), Criteo-shaped FM k=%d" % p["k"]) if p.get("data") != "a1a"
             else "examples/sec, a1a-shaped FM k=%d on CPU (plumbing config)" % p["k"],
             "value": value,
@@ -224,10 +224,19 @@ def main() -> int:
                 "early_rows": bool(model._exchange.prefetch) if model.mode == "shard" else None,
                 "split_grads": bool(model._exchange.overlap_grads) if model.mode == "shard" else None,
             },
-        }), flush=True)
+        })
+        sys.stdout.flush()
+        os.write(_RESULT_FD, (line + "\n").encode())
     fmdist.shutdown()
     return 0
 
 
+# stdout carries exactly one line, the JSON result of rank 0: everything else the process
+# writes to fd 1 -- including the C++ libraries' own messages (gloo prints its connection
+# lines there when the CPU side-group is created) -- goes to stderr
+_RESULT_FD = 1
+
 if __name__ == "__main__":
+    _RESULT_FD = os.dup(1)
+    os.dup2(2, 1)
     sys.exit(main())

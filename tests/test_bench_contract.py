@@ -31,3 +31,26 @@ def test_bench_prints_one_json_line(args):
     assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["higher_is_better"] is True
     assert d["value"] > 0 and d["ms_per_step"] > 0 and d["scaling"] == "weak"
     assert {"model", "global_batch", "seq_len", "parallelism"} <= set(d["config"])
+
+
+def test_bench_two_ranks_one_json_line():
+    """The driver's N>1 launch (torch.distributed.run, one process per device, 127.0.0.1):
+    stdout holds exactly rank 0's JSON line (the gloo side-group's connection messages and
+    every other rank's output go to stderr), n_gpus / global_batch / parallelism follow the
+    world size.  CPU + gloo here; the same path runs RCCL on MI355X."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "256", "--slots-per-gpu", "20000"],
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert KEYS <= set(d) and d["n_gpus"] == 2 and d["config"]["global_batch"] == 512
+    assert d["config"]["parallelism"] == "rowshard2" and d["config"]["early_rows"] and d["config"]["split_grads"]
