@@ -23,21 +23,31 @@ ap.add_argument("--mode", default="shard")
 ap.add_argument("--steps", type=int, default=30)
 ap.add_argument("--batch", type=int, default=131072)
 ap.add_argument("--vocab", type=int, default=125_000_000)
+ap.add_argument("--prefetch-rows", default="auto", choices=["auto", "on", "off"])
+ap.add_argument("--overlap-grads", default="auto", choices=["auto", "on", "off"])
+ap.add_argument("--depth", type=int, default=2, help="batches of lookahead passed to train_step (1 or 2)")
 a = ap.parse_args()
 ctx = fmdist.init_distributed(force_pg=a.mode != "local")
 cfg = FMConfig(vocabulary_size=a.vocab, factor_num=64, loss_type="logistic", batch_size=a.batch, seed=1,
-               opt=K.OptConfig("adagrad", lr=0.01), mode=a.mode)
+               opt=K.OptConfig("adagrad", lr=0.01), mode=a.mode, prefetch_rows=a.prefetch_rows,
+               overlap_grads=a.overlap_grads)
 m = FactorizationMachine(cfg, device=ctx.device, dist=ctx if a.mode != "local" else None)
 gen = CriteoSynth(a.vocab, seed=3, device=ctx.device)
 pool = [gen.batch(a.batch) for _ in range(4)]
+
+
+def step(i):
+    return m.train_step(pool[i % 4], pool[(i + 1) % 4], pool[(i + 2) % 4] if a.depth > 1 else None)
+
+
 for i in range(5):
-    m.train_step(pool[i % 4], pool[(i + 1) % 4])
+    step(i)
 torch.cuda.synchronize()
 host = []
 t0 = time.perf_counter()
 for i in range(a.steps):
     h0 = time.perf_counter()
-    m.train_step(pool[i % 4], pool[(i + 1) % 4])
+    step(i)
     host.append(time.perf_counter() - h0)
 torch.cuda.synchronize()
 wall = (time.perf_counter() - t0) / a.steps
@@ -49,7 +59,7 @@ from torch.profiler import ProfilerActivity, profile  # noqa: E402
 
 with profile(activities=[ProfilerActivity.CPU]) as prof:
     for i in range(5):
-        m.train_step(pool[i % 4], pool[(i + 1) % 4])
+        step(i)
     torch.cuda.synchronize()
 print(prof.key_averages().table(sort_by="self_cpu_time_total", row_limit=25))
 fmdist.shutdown()
