@@ -1,4 +1,4 @@
-"""Command line: ``python run.py {train,predict,generate,convert} CONFIG [options]``.
+"""Command line: ``python run.py {train,predict,generate,convert,import_tf,export_tf} CONFIG [options]``.
 
 Same arguments as the reference's run_tffm.py (run_tffm.py:124-162):
   task {train,predict,generate}, config_file,
@@ -8,7 +8,12 @@ Extensions: --device {auto,cpu,cuda}, --mode {auto,local,shard,dp,dp_dense},
 --max-steps N, --log-dir DIR (overrides [General] log_dir), and the task
 ``convert CONFIG --out DIR``: parse the config's train files (+ weight files) once
 into binary CSR caches (``DIR/<name>.fmb``, data/bincache.py) that ``train``
-reads at memory speed when ``train_files`` points at them.
+reads at memory speed when ``train_files`` points at them.  Checkpoint migration:
+``import_tf CONFIG --tf_checkpoint DIR|PREFIX`` loads a TensorFlow checkpoint in the
+reference's variable layout (``vocab_block_{i}`` + ``/Adagrad`` slots + ``global_step``)
+and writes it as this package's checkpoint into ``log_dir`` (``train`` resumes from it,
+``predict`` / ``generate`` use it); ``export_tf CONFIG --export_path DIR`` writes the
+latest checkpoint of ``log_dir`` back as such a TF checkpoint.
 
 Distributed runs: launch one process per GPU with torchrun (RANK/WORLD_SIZE/
 MASTER_ADDR from the environment), or keep the reference's ``--dist worker i
@@ -26,7 +31,7 @@ import sys
 
 def build_parser() -> argparse.ArgumentParser:
     p = argparse.ArgumentParser(prog="run.py", description="MI355X-native distributed factorization machine")
-    p.add_argument("task", choices=["train", "predict", "generate", "convert"])
+    p.add_argument("task", choices=["train", "predict", "generate", "convert", "import_tf", "export_tf"])
     p.add_argument("config_file", type=str)
     p.add_argument("--dist", nargs=4, metavar=("JOB_NAME", "TASK_INDEX", "PS_HOSTS", "WORKER_HOSTS"), default=None,
                    help="For distributed training or prediction")
@@ -43,6 +48,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--max-steps", type=int, default=None)
     p.add_argument("--log-dir", default=None)
     p.add_argument("--out", default=None, help="convert: output directory of the .fmb caches")
+    p.add_argument("--tf_checkpoint", default=None,
+                   help="import_tf: TF checkpoint directory (its 'checkpoint' file names the newest) or prefix")
     return p
 
 
@@ -106,6 +113,9 @@ def main(argv: list[str] | None = None) -> int:
               "from the caches.")
         return 0
 
+    if args.task in ("import_tf", "export_tf"):
+        return _migrate(args, cfg)
+
     ctx = None
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if dist_info.get("role") == "worker" or world_env > 1:
@@ -126,6 +136,53 @@ def main(argv: list[str] | None = None) -> int:
     finally:
         if ctx is not None:
             fmdist.shutdown()
+    return 0
+
+
+def _tf_prefix(path: str) -> str:
+    """A TF checkpoint prefix from a directory (via its ``checkpoint`` state file) or a prefix."""
+    import re
+
+    if os.path.isdir(path):
+        state = os.path.join(path, "checkpoint")
+        if not os.path.exists(state):
+            raise FileNotFoundError(f"no 'checkpoint' state file in {path}")
+        with open(state) as f:
+            m = re.search(r'^model_checkpoint_path:\s*"(.*)"', f.read(), re.M)
+        if m is None:
+            raise ValueError(f"{state} names no model_checkpoint_path")
+        p = m.group(1)
+        return p if os.path.isabs(p) else os.path.join(path, p)
+    return path
+
+
+def _migrate(args, cfg) -> int:
+    from .utils import checkpoint as ckpt
+
+    if cfg.log_dir is None:
+        print("Missing log directory.")
+        return 1
+    if args.task == "export_tf":
+        if args.export_path is None:
+            print("Export path is not specified. Use --export_path.")
+            return 2
+        path = ckpt.latest_checkpoint(cfg.log_dir)
+        if path is None:
+            print(f"No checkpoint found in {cfg.log_dir}.")
+            return 1
+        prefix = ckpt.export_tf_checkpoint(path, args.export_path, cfg.vocabulary_block_num)
+        print(f"TensorFlow checkpoint written to {prefix}")
+        return 0
+    if args.tf_checkpoint is None:
+        print("TF checkpoint is not specified. Use --tf_checkpoint.")
+        return 2
+    from .trainer import Trainer
+
+    prefix = _tf_prefix(args.tf_checkpoint)
+    tr = Trainer(cfg, None)
+    step = ckpt.import_tf_checkpoint(tr.model, prefix, cfg.vocabulary_block_num)
+    path = ckpt.save_checkpoint(tr.model, cfg.log_dir, step)
+    print(f"Imported {prefix} (global_step {step}) into {path}")
     return 0
 
 

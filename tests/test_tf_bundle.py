@@ -48,3 +48,60 @@ def test_checkpoint_to_tf_and_back(tmp_path):
     assert ckpt.import_tf_checkpoint(m2, prefix) == 3
     assert torch.equal(m2.table.reference_rows(), m.table.reference_rows())
     torch.testing.assert_close(m2.table.s0v[:, :6], m.table.s0v[:, :6])
+
+
+def test_cli_import_then_export_tf(tmp_path):
+    """run.py import_tf / export_tf: a reference-layout TF checkpoint (vocab_block_i [V//N+1, K+1]
+    + /Adagrad slots + global_step) becomes this package's checkpoint in log_dir and comes
+    back out bit-exactly."""
+    import contextlib
+    import io
+
+    from fast_tffm_amd import cli
+    from fast_tffm_amd.utils.tf_bundle import write_checkpoint_state
+
+    V, N, KF = 1000, 4, 6
+    rng = np.random.default_rng(1)
+    src = tmp_path / "tf"
+    src.mkdir()
+    tensors = {"global_step": np.array(77, dtype=np.int64)}
+    for i in range(N):
+        tensors[f"vocab_block_{i}"] = rng.uniform(-0.1, 0.1, (V // N + 1, KF + 1)).astype(np.float32)
+        tensors[f"vocab_block_{i}/Adagrad"] = rng.uniform(0.1, 2.0, (V // N + 1, KF + 1)).astype(np.float32)
+    write_bundle(str(src / "model.ckpt-77"), tensors)
+    write_checkpoint_state(str(src), "model.ckpt-77")
+    cfg = tmp_path / "m.cfg"
+    cfg.write_text(f"""[General]
+vocabulary_size = {V}
+vocabulary_block_num = {N}
+factor_num = {KF}
+hash_feature_id = False
+log_dir = {tmp_path / 'log'}
+device = cpu
+[Train]
+batch_size = 10
+init_value_range = 0.01
+factor_lambda = 0
+bias_lambda = 0
+epoch_num = 1
+learning_rate = 0.01
+adagrad.initial_accumulator = 0.1
+save_steps = 100
+loss_type = logistic
+train_files = {tmp_path}/none_*
+[Predict]
+predict_files =
+""")
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        assert cli.main(["import_tf", str(cfg), "--tf_checkpoint", str(src)]) == 0
+        assert ckpt.latest_checkpoint(str(tmp_path / "log")).endswith("model.ckpt-77")
+        assert cli.main(["export_tf", str(cfg), "--export_path", str(tmp_path / "out")]) == 0
+    back = read_bundle(str(tmp_path / "out" / "model.ckpt-77"))
+    assert int(back["global_step"]) == 77
+    for i in range(N):
+        # ids >= V in the last rows of some blocks do not exist in the table: compare the real ones
+        ids = np.arange(V // N + 1) * N + i
+        ok = ids < V
+        assert np.array_equal(back[f"vocab_block_{i}"][ok], tensors[f"vocab_block_{i}"][ok])
+        assert np.array_equal(back[f"vocab_block_{i}/Adagrad"][ok], tensors[f"vocab_block_{i}/Adagrad"][ok])
