@@ -206,3 +206,29 @@ def test_rccl_world1_split_backward_matches_local(rccl_ctx, dtype, k):
         assert abs(l1 - l2) <= 1e-5 * max(1.0, abs(l1)), (i, l1, l2)
     torch.cuda.synchronize()
     torch.testing.assert_close(dm.table.reference_rows(), loc.table.reference_rows(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_rccl_world1_pipelined_shard_step_is_bitwise_deterministic(rccl_ctx, dtype):
+    """Race detection for the sharded pipeline: with the side-stream plan two
+    batches ahead, the early row exchange + patches and the split backward all on, two runs
+    of the same batches leave bit-identical tables (bf16 with stochastic rounding too)."""
+    V = 20000
+    gen = CriteoSynth(V, device="cuda", seed=27)
+    batches = [gen.batch(4096) for _ in range(6)]
+
+    def run():
+        cfg = FMConfig(vocabulary_size=V, factor_num=64, loss_type="logistic", init_value_range=0.05, seed=3,
+                       opt=K.OptConfig("adagrad", lr=0.05), batch_size=4096, factor_lambda=0.01, bias_lambda=0.01,
+                       mode="shard", dtype=dtype, prefetch_rows="on", overlap_grads="on")
+        m = FactorizationMachine(cfg, device="cuda", dist=rccl_ctx)
+        losses = []
+        for i, b in enumerate(batches):
+            nb = batches[i + 1] if i + 1 < len(batches) else None
+            nb2 = batches[i + 2] if i + 2 < len(batches) else None
+            losses.append(m.train_step(b, nb, nb2).mean_loss())
+        torch.cuda.synchronize()
+        return m.table.reference_rows().cpu(), m.table.s0v.cpu().clone(), losses
+
+    a, b = run(), run()
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and a[2] == b[2]
