@@ -200,3 +200,23 @@ def test_stochastic_rounding_keeps_small_updates(dtype):
     expect = start - steps * lr
     assert abs(ends[True] - expect) < 0.15 * steps * lr           # unbiased within noise
     assert abs(ends[False] - expect) > 0.4 * steps * lr           # nearest rounding drifts away
+
+
+@pytest.mark.parametrize("B,maxf", [(131072, 39), (1000, 0), (777, 200), (64, 5), (1, 70), (3000, 1)])
+def test_csr_rows_matches_torch(B, maxf):
+    """csr_rows_kernel (a wave per 64 examples, shuffle search) vs repeat_interleave: example
+    index and packed (example << bits | slot) code, with empty examples, examples longer than
+    a wave and B not a multiple of 64."""
+    g = torch.Generator().manual_seed(B + maxf)
+    sizes = torch.randint(0, maxf + 1, (B,), generator=g, dtype=torch.int32)
+    if maxf:
+        sizes[:: 7] = 0
+    offs = torch.zeros(B + 1, dtype=torch.int32)
+    offs[1:] = torch.cumsum(sizes, 0)
+    nnz = int(offs[-1])
+    ex = torch.repeat_interleave(torch.arange(B, dtype=torch.int32), sizes)
+    slot = torch.arange(nnz, dtype=torch.int32) - torch.repeat_interleave(offs[:-1], sizes)
+    d = offs.cuda()
+    torch.testing.assert_close(K.csr_rows(d, nnz=nnz).cpu(), ex, rtol=0, atol=0)
+    bits = max(1, int(max(int(sizes.max()), 1) - 1).bit_length())
+    torch.testing.assert_close(K.csr_rows(d, nnz=nnz, slot_bits=bits).cpu(), (ex << bits) | slot, rtol=0, atol=0)
