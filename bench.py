@@ -78,6 +78,8 @@ def main() -> int:
                     help="row-sharded step: split backward, first half's gradient rows sent early (auto: N > 1)")
     ap.add_argument("--comm-dtype", default="auto", choices=["auto", "fp32", "bf16"],
                     help="row-sharded wire rows (auto = table storage dtype; bf16 rounds fp32 rows for transport)")
+    ap.add_argument("--stochastic-rounding", default="on", choices=["on", "off"],
+                    help="bf16 / fp8 tables: stochastically rounded row stores (the training default)")
     ap.add_argument("--profile-steps", type=int, default=0, help="also emit a torch.profiler trace")
     ap.add_argument("--graph", type=int, default=0,
                     help="local step: 0 = eager lookahead pipeline (next batch's dedup overlaps this step; "
@@ -109,7 +111,7 @@ def main() -> int:
     cfg = FMConfig(vocabulary_size=vocab, factor_num=p["k"], loss_type="logistic", batch_size=a.batch,
                    init_value_range=0.01, seed=42, dtype=dtype, opt=opt, mode=mode, comm_dtype=a.comm_dtype,
                    microbatches=a.microbatches, prefetch_rows=a.prefetch_rows,
-                   overlap_grads=a.overlap_grads)
+                   overlap_grads=a.overlap_grads, stochastic_rounding=a.stochastic_rounding == "on")
     t0 = time.time()
     model = FactorizationMachine(cfg, device=dev, dist=ctx if W > 1 or mode not in ("auto", "local") else None)
     if dev.type == "cuda":

@@ -187,9 +187,25 @@ __device__ inline void bwd_finalize(const BwdArgs& a, int u, int t, bool tact, i
   bwd_finish<LPR, TV, EPL>(a, u, t, tact, r, A, Scx, Sc, n_u, sr);
 }
 
+// Minimum waves per SIMD the chunk kernel must keep (amdgpu_waves_per_eu): the fp8
+// instantiations with 32 / 64 lanes per row sit a few VGPRs above the 128-VGPR step
+// (129 -> 3 waves/SIMD instead of 4: +5% on the k128 fp8 FTRL step); capping them at
+// 128 costs no spills.  1 = no constraint (the compiler's own choice).
+template <int LPR, typename TV>
+constexpr int chunk_min_waves() {
+#if defined(FM_CHUNK_NOCAP)
+  return 1;
+#elif defined(FM_CHUNK_CAP_F32)  // A/B: also the fp32 k=64 kernel (135 VGPRs -> 128 + 44 B/lane of spills)
+  return ((sizeof(TV) == 1 && LPR == 32) || (sizeof(TV) == 4 && LPR == 16)) ? 4 : 1;
+#else
+  return (sizeof(TV) == 1 && LPR == 32) ? 4 : 1;
+#endif
+}
+
 // One lane group per chunk of <= CH (<= kMaxCH) sorted occurrences of one row.
 template <int LPR, typename TV>
-__global__ __launch_bounds__(kBlock) void fm_bwd_chunk_kernel(BwdArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(chunk_min_waves<LPR, TV>())))
+void fm_bwd_chunk_kernel(BwdArgs a) {
   const uint32_t sr = sr_step_seed(a.sr_counter);  // stochastic rounding seed (0: nearest)
   constexpr int EPL = Frag<TV>::N;  // elements per lane of the table dtype
   constexpr int G = kWave / LPR;
