@@ -89,37 +89,36 @@ __device__ inline uint32_t f32_to_bf16_bits_sr(float f, uint32_t r) {
   return (u + (r & 0xffffu)) >> 16;
 }
 
+// 4 bf16 per lane (an 8-byte load): the same lane mapping and fp32 register
+// footprint as an fp32 row (a K=64 row is one 16-lane instruction).  With 16-byte
+// fragments (8 values per lane) the backward chunk kernel needed 185 VGPRs (2
+// waves/SIMD) and the k=64 bf16 step was slower than the fp32 one.
 template <> struct Frag<__hip_bfloat16> {
-  static constexpr int N = 8;
+  static constexpr int N = 4;
   static constexpr bool kScaled = false;
-  __device__ static inline void load(const __hip_bfloat16* p, float (&o)[8]) {
-    const uint4 v = *reinterpret_cast<const uint4*>(p);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      o[2 * i] = bf16_bits_to_f32(w[i] & 0xffffu);
-      o[2 * i + 1] = bf16_bits_to_f32(w[i] >> 16);
-    }
+  __device__ static inline void load(const __hip_bfloat16* p, float (&o)[4]) {
+    const uint2 v = *reinterpret_cast<const uint2*>(p);
+    o[0] = bf16_bits_to_f32(v.x & 0xffffu);
+    o[1] = bf16_bits_to_f32(v.x >> 16);
+    o[2] = bf16_bits_to_f32(v.y & 0xffffu);
+    o[3] = bf16_bits_to_f32(v.y >> 16);
   }
-  __device__ static inline void store(__hip_bfloat16* p, const float (&o)[8]) {
-    uint4 v;
+  __device__ static inline void store(__hip_bfloat16* p, const float (&o)[4]) {
+    uint2 v;
     v.x = f32_to_bf16_bits(o[0]) | (f32_to_bf16_bits(o[1]) << 16);
     v.y = f32_to_bf16_bits(o[2]) | (f32_to_bf16_bits(o[3]) << 16);
-    v.z = f32_to_bf16_bits(o[4]) | (f32_to_bf16_bits(o[5]) << 16);
-    v.w = f32_to_bf16_bits(o[6]) | (f32_to_bf16_bits(o[7]) << 16);
-    *reinterpret_cast<uint4*>(p) = v;
+    *reinterpret_cast<uint2*>(p) = v;
   }
-  __device__ static inline void store_sr(__hip_bfloat16* p, const float (&o)[8], uint32_t seed, uint32_t row,
+  __device__ static inline void store_sr(__hip_bfloat16* p, const float (&o)[4], uint32_t seed, uint32_t row,
                                          uint32_t col) {
-    uint32_t b[8];
+    uint32_t b[4];
     uint32_t r = sr_hash(seed, row, col);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < 4; ++k) {
       b[k] = f32_to_bf16_bits_sr(o[k], r);
       r = sr_next(r);
     }
-    *reinterpret_cast<uint4*>(p) = make_uint4(b[0] | (b[1] << 16), b[2] | (b[3] << 16), b[4] | (b[5] << 16),
-                                              b[6] | (b[7] << 16));
+    *reinterpret_cast<uint2*>(p) = make_uint2(b[0] | (b[1] << 16), b[2] | (b[3] << 16));
   }
 };
 
@@ -255,7 +254,7 @@ __device__ inline void opt_step(const OptParams& o, float g, float& p, float& s0
 inline int next_pow2(int x) { int p = 1; while (p < x) p <<= 1; return p; }
 
 inline int lanes_per_row(int Kp, int dtype) {
-  const int epl = dtype == kBF16 ? 8 : 4;  // fp32: 16 B, bf16: 16 B, fp8: 4 B per lane
+  const int epl = 4;  // fp32: 16 B, bf16: 8 B, fp8: 4 B per lane
   return next_pow2((Kp + epl - 1) / epl);
 }
 

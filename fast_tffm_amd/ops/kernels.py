@@ -52,12 +52,12 @@ def dtype_code(t: torch.dtype) -> int:
 
 
 def elems_per_lane(dtype: torch.dtype) -> int:
-    """Table elements one lane moves per row access: 16 B (fp32, bf16) or 4 B (fp8)."""
-    return 4 if dtype == FP8 else 16 // torch.tensor([], dtype=dtype).element_size()
+    """Table elements one lane moves per row access: 4 (16 B fp32, 8 B bf16, 4 B fp8)."""
+    return 4
 
 
 def padded_k(K: int, dtype: torch.dtype = torch.float32) -> int:
-    """Factor columns stored per row: K rounded up to whole lanes (bf16: at least 8)."""
+    """Factor columns stored per row: K rounded up to whole lanes (multiples of 4)."""
     e = elems_per_lane(dtype)
     return ((K + e - 1) // e) * e
 
