@@ -210,7 +210,10 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
   constexpr int EPL = Frag<TV>::N;  // elements per lane of the table dtype
   constexpr int G = kWave / LPR;
   constexpr int PF = (kMaxCH + LPR - 1) / LPR;  // prefetched occurrences per lane
-  constexpr int UNR = LPR < 8 ? LPR : 8;         // r1 rows in flight per lane
+#ifndef FM_CHUNK_UNR
+#define FM_CHUNK_UNR 8
+#endif
+  constexpr int UNR = LPR < FM_CHUNK_UNR ? LPR : FM_CHUNK_UNR;  // r1 rows in flight per lane
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR, t = lane % LPR;
   const int gbase = g * LPR;
