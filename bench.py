@@ -8,10 +8,12 @@ Workload per step and rank (weak scaling: per-GPU work is fixed as N grows):
   * B examples x 39 features (13 bucketized integer + 26 categorical Criteo
     fields, Zipf value popularity), synthetic, generated on the device before
     timing (a pool of distinct batches is cycled);
-  * FM k=64, fp32 table + fp32 Adagrad slots, hashed vocabulary of
-    125M slots per GPU (1B slots at N=8), row-sharded over the GPUs with RCCL
-    all-to-all for lookups and gradients (mode "shard"); N=1 runs the local
-    single-GPU path;
+  * FM k=64 (default preset k64_bf16): bf16 factor table -- stochastically
+    rounded row stores -- with fp32 arithmetic, fp32 linear weights and fp32
+    Adagrad slots; hashed vocabulary of 125M slots per GPU (1B slots at N=8),
+    row-sharded over the GPUs with RCCL all-to-all for lookups and gradients
+    (mode "shard"; bf16 rows travel at their storage size); N=1 runs the local
+    single-GPU path.  `--preset k64` is the same model with an fp32 table;
   * the timed step is the full training step: id -> key, dedup, (a2a), fused
     forward + loss, fused backward + Adagrad update, (a2a + owner update).
 
@@ -65,7 +67,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=None, help="examples per GPU per step (default 131072)")
-    ap.add_argument("--preset", default="k64", choices=sorted(PRESETS))
+    ap.add_argument("--preset", default="k64_bf16", choices=sorted(PRESETS))
     ap.add_argument("--slots-per-gpu", type=int, default=None, help="override hashed slots per GPU")
     ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled")
     ap.add_argument("--alpha", type=float, default=1.1, help="Zipf exponent of field values")
@@ -210,7 +212,8 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            # compute dtype: fp32 arithmetic throughout; the table is stored as p["dtype"]
+            # the table's storage dtype (bf16 / fp8 tables: fp32 arithmetic, accumulators and
+            # optimizer state; fp32: everything fp32)
             "dtype": p["dtype"],
             "data": ("synthetic Criteo-shaped (39 fields, Zipf a=%.2f), random-init weights" % a.alpha)
             if p.get("data") != "a1a" else "synthetic a1a-shaped libsvm text (123 features), parsed",

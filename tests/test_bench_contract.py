@@ -46,7 +46,8 @@ def test_bench_two_ranks_one_json_line():
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-                        "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "256", "--slots-per-gpu", "20000"],
+                        "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "256", "--slots-per-gpu", "20000",
+                        "--preset", "k64"],  # (bf16 storage wires of the default preset are a GPU path)
                        capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]

@@ -8,7 +8,7 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 export FM_NO_AUTOBUILD=1
 cd $R
-for P in k64 k16_bf16 k128_ftrl k128_fp8_ftrl k64_dp_dense; do
+for P in k64_bf16 k64 k16_bf16 k128_ftrl k128_fp8_ftrl k64_dp_dense; do
   timeout -k 10 300 python bench.py --preset $P --steps 30 --warmup 5 > $OUT/bench_$P.json 2> $OUT/bench_$P.err || { echo "bench $P failed"; tail -20 $OUT/bench_$P.err; exit 1; }
   echo "$P: $(tail -1 $OUT/bench_$P.err)"
 done
