@@ -38,7 +38,9 @@ HIP_DEPS = ["hip/fm_fwd.hip", "hip/fm_bwd.hip", "hip/dedup.hip", "hip/shard.hip"
 # kernels at -0.6% step time under the lookahead step (not kept: no clear win).
 HIP_VARIANTS: dict[str, list[str]] = {"nocap": ["-DFM_CHUNK_NOCAP"], "capf32": ["-DFM_CHUNK_CAP_F32"],
                                       "unr4": ["-DFM_CHUNK_UNR=4"], "unr6": ["-DFM_CHUNK_UNR=6"],
-                                      "unr16": ["-DFM_CHUNK_UNR=16"], "unr12": ["-DFM_CHUNK_UNR=12"]}
+                                      "unr16": ["-DFM_CHUNK_UNR=16"], "unr12": ["-DFM_CHUNK_UNR=12"],
+                                      "fwdw5": ["-DFM_FWD_WAVES_LPR16=5"],
+                                      "fwdw6": ["-DFM_FWD_WAVES_LPR16=6"]}
 
 
 _EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"  # resolved once (lazy init is not thread-safe)

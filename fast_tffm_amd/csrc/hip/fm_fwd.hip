@@ -43,8 +43,22 @@ struct FwdUnroll {
   static constexpr int v = (40 / G) < 1 ? 1 : ((40 / G) > 12 ? 12 : (40 / G));
 };
 
+// Minimum waves per SIMD of the forward (amdgpu_waves_per_eu; 1 = compiler's choice): the
+// 32/64-lane instantiations (k>=128) need 132-136 VGPRs -> 3 waves/SIMD uncapped; capped at
+// 4 the k=128 FTRL step runs 1.038 -> 0.992 ms (fp32) and 1.033 -> 0.987 ms (fp8)
+// (profiles/r1s3/fwd_cap_ab.txt).  FM_FWD_WAVES_LPR16=N forces a floor on the k=64 (16-lane)
+// instantiations (A/B build knob: 5 or 6 waves spill, 0.65 -> 0.73 / 0.86 ms).
 template <int LPR, typename TV>
-__global__ __launch_bounds__(kBlock) void fm_fwd_kernel(FwdArgs a) {
+constexpr int fwd_min_waves() {
+#if defined(FM_FWD_WAVES_LPR16)
+  if (LPR == 16) return FM_FWD_WAVES_LPR16;
+#endif
+  return LPR >= 32 ? 4 : 1;
+}
+
+template <int LPR, typename TV>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(fwd_min_waves<LPR, TV>())))
+void fm_fwd_kernel(FwdArgs a) {
   using F = Frag<TV>;
   constexpr int EPL = F::N;
   constexpr int G = kWave / LPR;
