@@ -15,6 +15,7 @@ The backend is "nccl" (= RCCL on ROCm) for GPU tensors and "gloo" on CPU.
 from __future__ import annotations
 
 import datetime
+import gc
 import os
 from dataclasses import dataclass
 
@@ -127,8 +128,14 @@ def local_context(device: str | torch.device = "cpu") -> DistContext:
 
 
 def shutdown() -> None:
+    """Destroy the process groups.  Unreachable models / exchanges that still hold
+    communicators are collected first, while their groups are alive: a communicator
+    finalised later by the garbage collector, after the destroy, can abort the process."""
     global _CTX
     if dist.is_available() and dist.is_initialized():
+        gc.collect()
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.synchronize()
         dist.destroy_process_group()
     _CTX = None
 
