@@ -39,7 +39,7 @@ HIP_DEPS = ["hip/fm_fwd.hip", "hip/fm_bwd.hip", "hip/dedup.hip", "hip/shard.hip"
 HIP_VARIANTS: dict[str, list[str]] = {"nocap": ["-DFM_CHUNK_NOCAP"], "capf32": ["-DFM_CHUNK_CAP_F32"],
                                       "unr4": ["-DFM_CHUNK_UNR=4"], "unr6": ["-DFM_CHUNK_UNR=6"],
                                       "unr16": ["-DFM_CHUNK_UNR=16"], "unr12": ["-DFM_CHUNK_UNR=12"],
-                                      "fwdw5": ["-DFM_FWD_WAVES_LPR16=5"], "fwdceil": ["-DFM_FWD_UNR_CEIL"],
+                                      "fwdw5": ["-DFM_FWD_WAVES_LPR16=5"],
                                       "fwdw6": ["-DFM_FWD_WAVES_LPR16=6"]}
 
 

@@ -301,34 +301,72 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
 #pragma unroll
     for (int k = 0; k < EPL; ++k) A[k] = 0.f;
     float Scx = 0.f, Sc = 0.f;
+    if constexpr (LPR < FM_CHUNK_UNR) {
+      // narrow rows (k=16 bf16: LPR 2): flat walk over the chunk's occurrences with
+      // FM_CHUNK_UNR r1 rows in flight per lane (the q-major walk below keeps only LPR in
+      // flight); same summation order.  k16 bf16 step 0.525 -> 0.497 ms; for LPR >= 8 the
+      // flat walk measured slower (k64 0.652 -> 0.665, k128 fp8 0.989 -> 1.039 ms):
+      // profiles/r1s4/chunk_flat_ab.txt
+      constexpr int UNRF = FM_CHUNK_UNR;
 #pragma unroll
-    for (int q = 0; q < PF; ++q) {
-      if (q * LPR < len) {
-        for (int l = 0; l < LPR && q * LPR + l < len; l += UNR) {
-          float rr[UNR][EPL], cc[UNR], xx[UNR];
+      for (int o0 = 0; o0 < PF * LPR; o0 += UNRF) {
+        if (o0 >= len) break;
+        float rr[UNRF][EPL], cc[UNRF], xx[UNRF];
 #pragma unroll
-          for (int uu = 0; uu < UNR; ++uu) {
-            const int li = l + uu;
-            const bool ok = li < LPR && q * LPR + li < len;
-            const int src = gbase + (ok ? li : 0);
-            // shuffles are unconditional (every lane of the group takes part); mask after
-            const int ex = __shfl(pex[q], src, kWave);
-            const float cs = __shfl(pc[q], src, kWave);
-            cc[uu] = ok ? cs : 0.f;
-            xx[uu] = __shfl(px[q], src, kWave);
-            const float* rp = a.r1 + (long long)ex * a.Kp + tE * EPL;
+        for (int uu = 0; uu < UNRF; ++uu) {
+          const int oi = o0 + uu;
+          const int q = oi / LPR < PF ? oi / LPR : PF - 1, li = oi % LPR;
+          const bool ok = oi < PF * LPR && oi < len;
+          const int src = gbase + (ok ? li : 0);
+          const int ex = __shfl(pex[q], src, kWave);
+          const float cs = __shfl(pc[q], src, kWave);
+          cc[uu] = ok ? cs : 0.f;
+          xx[uu] = __shfl(px[q], src, kWave);
+          const float* rp = a.r1 + (long long)ex * a.Kp + tE * EPL;
 #pragma unroll
-            for (int k = 0; k < EPL; k += 4) {
-              const float4 f = *reinterpret_cast<const float4*>(rp + k);
-              rr[uu][k] = f.x; rr[uu][k + 1] = f.y; rr[uu][k + 2] = f.z; rr[uu][k + 3] = f.w;
-            }
+          for (int k = 0; k < EPL; k += 4) {
+            const float4 f = *reinterpret_cast<const float4*>(rp + k);
+            rr[uu][k] = f.x; rr[uu][k + 1] = f.y; rr[uu][k + 2] = f.z; rr[uu][k + 3] = f.w;
           }
+        }
 #pragma unroll
-          for (int uu = 0; uu < UNR; ++uu) {
+        for (int uu = 0; uu < UNRF; ++uu) {
 #pragma unroll
-            for (int k = 0; k < EPL; ++k) A[k] += cc[uu] * rr[uu][k];
-            Scx += cc[uu] * xx[uu];
-            Sc += cc[uu];
+          for (int k = 0; k < EPL; ++k) A[k] += cc[uu] * rr[uu][k];
+          Scx += cc[uu] * xx[uu];
+          Sc += cc[uu];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        if (q * LPR < len) {
+          for (int l = 0; l < LPR && q * LPR + l < len; l += UNR) {
+            float rr[UNR][EPL], cc[UNR], xx[UNR];
+#pragma unroll
+            for (int uu = 0; uu < UNR; ++uu) {
+              const int li = l + uu;
+              const bool ok = li < LPR && q * LPR + li < len;
+              const int src = gbase + (ok ? li : 0);
+              // shuffles are unconditional (every lane of the group takes part); mask after
+              const int ex = __shfl(pex[q], src, kWave);
+              const float cs = __shfl(pc[q], src, kWave);
+              cc[uu] = ok ? cs : 0.f;
+              xx[uu] = __shfl(px[q], src, kWave);
+              const float* rp = a.r1 + (long long)ex * a.Kp + tE * EPL;
+#pragma unroll
+              for (int k = 0; k < EPL; k += 4) {
+                const float4 f = *reinterpret_cast<const float4*>(rp + k);
+                rr[uu][k] = f.x; rr[uu][k + 1] = f.y; rr[uu][k + 2] = f.z; rr[uu][k + 3] = f.w;
+              }
+            }
+#pragma unroll
+            for (int uu = 0; uu < UNR; ++uu) {
+#pragma unroll
+              for (int k = 0; k < EPL; ++k) A[k] += cc[uu] * rr[uu][k];
+              Scx += cc[uu] * xx[uu];
+              Sc += cc[uu];
+            }
           }
         }
       }

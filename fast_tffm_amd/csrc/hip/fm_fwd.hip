@@ -38,17 +38,12 @@ struct FwdArgs {
 // Rows of one example kept in flight per lane group: enough to cover a
 // Criteo-shaped example (39 features) in one round for K=64 (G=4 -> 10 row
 // loads per lane) while bounding VGPRs for large K.
-#if defined(FM_FWD_UNR_CEIL)
+// ceil(40 / G): G = 32 (k=16 bf16) keeps both of an example's row groups in flight
+// (floor gave 1: k16 bf16 step 0.532 -> 0.522 ms, profiles/r1s4/fwd_unroll_ceil_ab.txt).
 template <int G>
 struct FwdUnroll {
   static constexpr int v = ((40 + G - 1) / G) > 12 ? 12 : ((40 + G - 1) / G);
 };
-#else
-template <int G>
-struct FwdUnroll {
-  static constexpr int v = (40 / G) < 1 ? 1 : ((40 / G) > 12 ? 12 : (40 / G));
-};
-#endif
 
 // Minimum waves per SIMD of the forward (amdgpu_waves_per_eu; 1 = compiler's choice): the
 // 32/64-lane instantiations (k>=128) need 132-136 VGPRs -> 3 waves/SIMD uncapped; capped at
