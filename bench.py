@@ -8,12 +8,12 @@ Workload per step and rank (weak scaling: per-GPU work is fixed as N grows):
   * B examples x 39 features (13 bucketized integer + 26 categorical Criteo
     fields, Zipf value popularity), synthetic, generated on the device before
     timing (a pool of distinct batches is cycled);
-  * FM k=64 (default preset k64_bf16): bf16 factor table -- stochastically
-    rounded row stores -- with fp32 arithmetic, fp32 linear weights and fp32
-    Adagrad slots; hashed vocabulary of 125M slots per GPU (1B slots at N=8),
-    row-sharded over the GPUs with RCCL all-to-all for lookups and gradients
-    (mode "shard"; bf16 rows travel at their storage size); N=1 runs the local
-    single-GPU path.  `--preset k64` is the same model with an fp32 table;
+  * FM k=64 (default preset k64): fp32 factor table, fp32 arithmetic and fp32
+    Adagrad slots -- the reference's precision (tffm/fm_model.py:269-284);
+    hashed vocabulary of 125M slots per GPU (1B slots at N=8), row-sharded over
+    the GPUs with RCCL all-to-all for lookups and gradients (mode "shard", fp32
+    rows on the wire); N=1 runs the local single-GPU path.  `--preset k64_bf16`
+    is the same model with a bf16 table (secondary number, profiles/);
   * the timed step is the full training step: id -> key, dedup, (a2a), fused
     forward + loss, fused backward + Adagrad update, (a2a + owner update).
 
@@ -39,6 +39,12 @@ from fast_tffm_amd.data.synthetic import CriteoSynth  # noqa: E402
 from fast_tffm_amd.models.fm import FactorizationMachine, FMConfig  # noqa: E402
 from fast_tffm_amd.ops import kernels as K  # noqa: E402
 from fast_tffm_amd.parallel import dist as fmdist  # noqa: E402
+
+
+def native_hashes() -> dict:
+    from fast_tffm_amd.ops import native
+
+    return native.build_hashes()
 
 PRESETS = {
     # BASELINE.json headline: FM k=64 Criteo-shaped, row-sharded 1B slots at N=8
@@ -67,9 +73,9 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=None, help="examples per GPU per step (default 131072)")
-    ap.add_argument("--preset", default="k64_bf16", choices=sorted(PRESETS))
+    ap.add_argument("--preset", default="k64", choices=sorted(PRESETS))
     ap.add_argument("--slots-per-gpu", type=int, default=None, help="override hashed slots per GPU")
-    ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled")
+    ap.add_argument("--pool", type=int, default=16, help="distinct synthetic batches cycled")
     ap.add_argument("--alpha", type=float, default=1.1, help="Zipf exponent of field values")
     ap.add_argument("--mode", default=None, help="override step mode (local|shard|dp|dp_dense)")
     ap.add_argument("--microbatches", type=int, default=0,
@@ -98,7 +104,10 @@ def main() -> int:
         # step is 3% faster with 4.  Must be set before HIP initialises (first device call).
         if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
             os.environ["GPU_MAX_HW_QUEUES"] = "8"
-    ctx = fmdist.init_distributed(force_pg=mode not in ("auto", "local"), device=p.get("device"))
+    # bounded collective timeout: a hang in the multi-GPU bench exits non-zero after
+    # FM_PG_TIMEOUT seconds (RCCL watchdog) instead of holding the node for 30 minutes
+    ctx = fmdist.init_distributed(force_pg=mode not in ("auto", "local"), device=p.get("device"),
+                                  timeout_s=float(os.environ.get("FM_PG_TIMEOUT", "300")))
     W, rank = ctx.world, ctx.rank
     if W != a.gpus and rank == 0:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={W}; using {W}", file=sys.stderr)
@@ -228,6 +237,9 @@ def main() -> int:
                 "microbatches": model._exchange.nparts if model.mode == "shard" else None,
                 "early_rows": bool(model._exchange.prefetch) if model.mode == "shard" else None,
                 "split_grads": bool(model._exchange.overlap_grads) if model.mode == "shard" else None,
+                "comm": getattr(model._exchange, "comm_mode", None),
+                "pool": len(pool),
+                "native_build": native_hashes(),
             },
         })
         sys.stdout.flush()

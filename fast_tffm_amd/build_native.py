@@ -15,6 +15,8 @@ Usage:  python -m fast_tffm_amd.build_native [--cpu-only|--hip-only] [--force]
 from __future__ import annotations
 
 import argparse
+import glob
+import hashlib
 import os
 import shutil
 import subprocess
@@ -29,9 +31,6 @@ ARCH = os.environ.get("FM_OFFLOAD_ARCH", "gfx950")
 
 CPU_SOURCES = ["cpu/module.cpp", "cpu/parser.cpp", "cpu/kernels.cpp", "cpu/loader.cpp", "cpu/bincsr.cpp"]
 HIP_SOURCES = ["hip/module.hip"]
-HIP_DEPS = ["hip/fm_fwd.hip", "hip/fm_bwd.hip", "hip/dedup.hip", "hip/shard.hip", "hip/init.hip", "hip/parse.hip",
-            "hip/batch_gather.hip",
-            "hip/fm_common.h", "hash64.h"]
 # A/B build variants of the gfx950 module: name -> preprocessor defines (module _fm_hip_<name>,
 # selected at run time with FM_HIP_VARIANT=<name>; tools/gpu_ab.sh).  Used for same-box kernel
 # comparisons, e.g. {"pipe": ["-DFM_VARIANT_PIPE"]} measured the software-pipelined fwd/chunk
@@ -57,15 +56,51 @@ def _py_includes() -> list[str]:
     return [f"-I{p}" for p in sorted(incs)]
 
 
-def _stale(target: str, sources: list[str]) -> bool:
-    if not os.path.exists(target):
-        return True
-    t = os.path.getmtime(target)
-    for s in sources:
-        p = os.path.join(CSRC, s)
-        if os.path.exists(p) and os.path.getmtime(p) > t:
-            return True
-    return False
+# Rebuild decisions use a content hash, never mtimes: the hash covers every source and
+# header the module is compiled from, the compiler command line (flags, defines, arch) and
+# this file.  The hash is compiled into the module (``BUILD_HASH`` attribute and a
+# ``FMBUILDHASH:<hex>`` marker in the binary), so a loader can check -- without importing
+# it -- that a shipped .so was built from the sources next to it (ops/native.py).
+HASH_MARKER = b"FMBUILDHASH:"
+
+
+def _dep_files(kind: str) -> list[str]:
+    if kind == "cpu":
+        pats = ["cpu/*.cpp", "cpu/*.h", "*.h"]
+    else:
+        pats = ["hip/*.hip", "hip/*.h", "*.h"]
+    out = []
+    for p in pats:
+        out += glob.glob(os.path.join(CSRC, p))
+    return sorted(set(out))
+
+
+def source_hash(kind: str, flags: list[str]) -> str:
+    """sha256 (hex, 32 chars) of the sources, headers, flags and this builder."""
+    h = hashlib.sha256()
+    h.update(("\0".join(flags)).encode())
+    for f in _dep_files(kind) + [os.path.abspath(__file__)]:
+        h.update(os.path.relpath(f, PKG).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:32]
+
+
+def embedded_hash(target: str) -> str | None:
+    """The FMBUILDHASH marker of a built module (scanned from the file, not imported)."""
+    try:
+        with open(target, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    i = data.find(HASH_MARKER)
+    if i < 0:
+        return None
+    return data[i + len(HASH_MARKER): i + len(HASH_MARKER) + 32].decode("ascii", "replace")
+
+
+def _stale(target: str, want: str) -> bool:
+    return embedded_hash(target) != want
 
 
 def _run(cmd: list[str]) -> None:
@@ -73,15 +108,27 @@ def _run(cmd: list[str]) -> None:
     subprocess.run(cmd, check=True)
 
 
+def _cpu_flags() -> list[str]:
+    return ["-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-fvisibility=hidden"]
+
+
+def cpu_target() -> str:
+    return os.path.join(OUT, "_fm_cpu" + _ext_suffix())
+
+
+def cpu_hash() -> str:
+    return source_hash("cpu", _cpu_flags() + CPU_SOURCES)
+
+
 def build_cpu(force: bool = False) -> str:
     os.makedirs(OUT, exist_ok=True)
-    target = os.path.join(OUT, "_fm_cpu" + _ext_suffix())
-    deps = CPU_SOURCES + ["cpu/parser.h", "cpu/kernels.h", "cpu/loader.h", "cpu/bincsr.h", "cpu/mapped_file.h", "hash64.h"]
-    if force or _stale(target, deps):
+    target = cpu_target()
+    want = cpu_hash()
+    if force or _stale(target, want):
         cxx = os.environ.get("CXX", "g++")
         tmp = target + ".tmp"
-        cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-fvisibility=hidden",
-               *_py_includes(), *[os.path.join(CSRC, s) for s in CPU_SOURCES], "-o", tmp]
+        cmd = [cxx, *_cpu_flags(), f'-DFM_BUILD_HASH="{want}"', *_py_includes(),
+               *[os.path.join(CSRC, s) for s in CPU_SOURCES], "-o", tmp]
         _run(cmd)
         os.replace(tmp, target)
     return target
@@ -94,18 +141,34 @@ def hipcc_path() -> str | None:
     return None
 
 
+def _hip_flags(variant: str | None) -> list[str]:
+    name = hip_module_name(variant)
+    return [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
+            "-Wno-unused-result", f"-DFM_HIP_MODULE={name}", *(HIP_VARIANTS[variant] if variant else [])]
+
+
+def hip_module_name(variant: str | None = None) -> str:
+    return "_fm_hip" + (f"_{variant}" if variant else "")
+
+
+def hip_target(variant: str | None = None) -> str:
+    return os.path.join(OUT, hip_module_name(variant) + _ext_suffix())
+
+
+def hip_hash(variant: str | None = None) -> str:
+    return source_hash("hip", _hip_flags(variant) + HIP_SOURCES)
+
+
 def build_hip(force: bool = False, variant: str | None = None) -> str:
     os.makedirs(OUT, exist_ok=True)
-    name = "_fm_hip" + (f"_{variant}" if variant else "")
-    defines = [f"-DFM_HIP_MODULE={name}", *(HIP_VARIANTS[variant] if variant else [])]
-    target = os.path.join(OUT, name + _ext_suffix())
-    if force or _stale(target, HIP_SOURCES + HIP_DEPS):
+    target = hip_target(variant)
+    want = hip_hash(variant)
+    if force or _stale(target, want):
         hipcc = hipcc_path()
         if hipcc is None:
             raise RuntimeError("hipcc not found; cannot build the gfx950 extension")
         tmp = target + ".tmp"
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
-               "-Wno-unused-result", *defines, *_py_includes(), f"-I{CSRC}",
+        cmd = [hipcc, *_hip_flags(variant), f'-DFM_BUILD_HASH="{want}"', *_py_includes(), f"-I{CSRC}",
                *[os.path.join(CSRC, s) for s in HIP_SOURCES], "-o", tmp]
         _run(cmd)
         os.replace(tmp, target)

@@ -20,7 +20,8 @@ Extensions (new keys, all optional):
                 global_bias = true|false (learned b0; its gradient is all-reduced over ranks),
                 dtype = fp32|bf16|fp8 (fp8: OCP e4m3 + per-row scale, GPU)
   [Train]       optimizer = adagrad|ftrl|sgd, ftrl.l1, ftrl.l2, ftrl.beta,
-                ftrl.initial_accumulator, parse_threads, loader = native|python, gpu_parse = true|false, device_cache = auto|true|false, stochastic_rounding = true|false,
+                ftrl.initial_accumulator, parse_threads, loader = native|python, gpu_parse = true|false,
+                device_cache = auto|true|false, stochastic_rounding = true|false,
                 shuffle = true|false,
                 max_steps, dedup_chunk, log_steps
   [Distributed] mode = auto|local|shard|dp|dp_dense, grad_reduce = sum|mean,
@@ -131,9 +132,11 @@ class FMRunConfig:
                         init_value_range=self.init_value_range, seed=self.seed,
                         dtype={"fp32": torch.float32, "bf16": torch.bfloat16,
                                "fp8": torch.float8_e4m3fn}[self.dtype], opt=opt, mode=self.mode,
-                        grad_reduce=self.grad_reduce, comm_dtype=self.comm_dtype, microbatches=self.microbatches, prefetch_rows=self.prefetch_rows,
+                        grad_reduce=self.grad_reduce, comm_dtype=self.comm_dtype, microbatches=self.microbatches,
+                        prefetch_rows=self.prefetch_rows,
                         overlap_grads=self.overlap_grads,
-                        stochastic_rounding=self.stochastic_rounding, dedup_chunk=self.dedup_chunk, global_bias=self.global_bias)
+                        stochastic_rounding=self.stochastic_rounding, dedup_chunk=self.dedup_chunk,
+                        global_bias=self.global_bias)
 
 
 def load_config(config_file: str, *, echo: bool = True, printer=print) -> FMRunConfig:

@@ -276,6 +276,8 @@ void TextLoader::run() {
       // batch unless it is skipped (resume).
       auto emit = [&](size_t n) -> bool {
         ++count;
+        const size_t in_win = (o_.binary ? bwindow.size() : window.size()) - (o_.shuffle ? 0 : head);
+        fill_.store(std::min(1.f, static_cast<float>(in_win) / static_cast<float>(cap)), std::memory_order_relaxed);
         if (o_.binary) {
           draw(bwindow, head, n, o_.shuffle, rng, bchosen);
           if (count <= skip) return true;

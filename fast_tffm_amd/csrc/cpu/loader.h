@@ -30,6 +30,7 @@
 // A (start_epoch, skip_batches) position resumes exactly where a checkpoint
 // was taken: the RNGs are re-seeded per epoch, skipped batches are not parsed.
 #pragma once
+#include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
@@ -90,6 +91,9 @@ class TextLoader {
   // producer failure (ParseError for malformed input, runtime_error for I/O).
   bool next(LoadedBatch& out);
   size_t queued();
+  // Shuffle-window fill (items in the window / window capacity) at the latest draw: the
+  // reference's -m "shuffle_queue" figure (run_tffm.py:52-63, shuffle_batch queue size).
+  float window_fill() const { return fill_.load(std::memory_order_relaxed); }
   void close();
 
  private:
@@ -104,6 +108,7 @@ class TextLoader {
   bool done_ = false, stop_ = false;
   bool failed_ = false, parse_error_ = false;
   std::string error_;
+  std::atomic<float> fill_{0.f};
 };
 
 }  // namespace fm

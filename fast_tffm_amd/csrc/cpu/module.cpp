@@ -111,7 +111,15 @@ uint32_t crc32c(const uint8_t* p, size_t n) {
 
 }  // namespace
 
+// Content hash of the sources / flags this module was built from (build_native.py); the
+// marker string lets the loader check a shipped binary without importing it.
+#ifndef FM_BUILD_HASH
+#define FM_BUILD_HASH "unhashed"
+#endif
+extern "C" __attribute__((used, visibility("default"))) const char fm_build_hash_marker[] = "FMBUILDHASH:" FM_BUILD_HASH;
+
 PYBIND11_MODULE(_fm_cpu, m) {
+  m.attr("BUILD_HASH") = FM_BUILD_HASH;
   m.def(
       "crc32c",
       [](py::buffer b) {
@@ -232,6 +240,7 @@ PYBIND11_MODULE(_fm_cpu, m) {
                                    to_numpy(std::move(b.ids)), vals, w, b.max_feats, b.epoch, b.count);
            })
       .def("queued", &fm::TextLoader::queued)
+      .def("window_fill", &fm::TextLoader::window_fill)
       .def("close", [](fm::TextLoader& L) {
         py::gil_scoped_release nogil;
         L.close();

@@ -50,9 +50,17 @@ fm::OptParams opt_params(int type, float lr, float l1, float l2, float beta) {
 
 }  // namespace
 
+// Content hash of the sources / flags this module was built from (build_native.py); the
+// marker string lets the loader check a shipped binary without importing it.
+#ifndef FM_BUILD_HASH
+#define FM_BUILD_HASH "unhashed"
+#endif
+extern "C" __attribute__((used, visibility("default"))) const char fm_build_hash_marker[] = "FMBUILDHASH:" FM_BUILD_HASH;
+
 PYBIND11_MODULE(FM_HIP_MODULE, m) {
   m.doc() = "gfx950 HIP kernels for fast_tffm_amd (FM forward/backward/optimizer, dedup, sharding)";
   m.attr("ARCH") = "gfx950";
+  m.attr("BUILD_HASH") = FM_BUILD_HASH;
   m.attr("MAX_CH") = fm::kMaxCH;
 
   m.def("fwd_grid", &fm::fwd_grid, py::arg("B"));

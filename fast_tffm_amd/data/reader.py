@@ -130,6 +130,10 @@ class TextBatchReader:
         self.state = state or ReaderState()
         self.capacity = int(3 * self.B + 1.5 * self.B)
         self.min_after = 3 * self.B
+        self.fill = 0.0  # shuffle-window fill at the latest draw (-m "shuffle_queue")
+
+    def window_fill(self) -> float:
+        return self.fill
 
     def _my_files(self, epoch: int) -> list[tuple[str, str | None]]:
         pairs = list(zip(self.files, self.weight_files or [None] * len(self.files)))
@@ -176,6 +180,7 @@ class TextBatchReader:
             for item in self._lines(epoch):
                 buf.append(item)
                 if len(buf) >= self.capacity:
+                    self.fill = len(buf) / self.capacity
                     if self.shuffle:
                         rng.shuffle(buf)
                     out, buf = buf[: self.B], buf[self.B:]
@@ -186,6 +191,7 @@ class TextBatchReader:
             if self.shuffle:
                 rng.shuffle(buf)
             while buf:
+                self.fill = len(buf) / self.capacity
                 out, buf = buf[: self.B], buf[self.B:]
                 count += 1
                 if count > skip:
@@ -251,6 +257,10 @@ class NativeTextReader:
 
     def queued(self) -> int:
         return self._loader.queued() if self._loader is not None else 0
+
+    def window_fill(self) -> float:
+        """Shuffle-window fill (0..1) at the loader's latest draw (-m "shuffle_queue")."""
+        return float(self._loader.window_fill()) if self._loader is not None else 0.0
 
     def __iter__(self):
         L = native.cpu().TextLoader(start_epoch=self.state.epoch, skip_batches=self.state.batches_in_epoch,
@@ -373,6 +383,11 @@ class Prefetcher:
 
     def size(self) -> int:
         return self.q.qsize()
+
+    def shuffle_fill(self) -> float:
+        """The reader's shuffle-window fill (0..1), the reference's shuffle_queue metric."""
+        f = getattr(self.reader, "window_fill", None)
+        return float(f()) if f is not None else 0.0
 
     def __iter__(self):
         while True:

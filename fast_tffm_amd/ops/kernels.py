@@ -229,8 +229,9 @@ class DedupOut:
     the dedup ran with the example index as payload (then ``sorted_ex is perm``).
     """
 
-    __slots__ = ("n", "skeys", "perm", "uniq", "seg_start", "seg_chunk", "chunk_start", "chunk_seg", "chunk_key", "counts",
-                 "num_unique", "inv", "sorted_ex", "sorted_x", "U_host", "CH", "big_list", "big_count", "multi",
+    __slots__ = ("n", "skeys", "perm", "uniq", "seg_start", "seg_chunk", "chunk_start", "chunk_seg", "chunk_key",
+                 "counts", "num_unique", "inv", "sorted_ex", "sorted_x", "U_host", "CH", "big_list", "big_count",
+                 "multi",
                  "slice_list", "slice_start", "nslices", "ex_shift", "dense_list", "bwd_fresh")
 
     def __init__(self, **kw):
@@ -478,7 +479,8 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
         _check(grad_out.dtype == torch.float32 and grad_out.stride(1) == 1, "grad_out: fp32 rows")
         gstride, gptr = grad_out.stride(0), grad_out.data_ptr()
         g_wcol = (Kp * 2 + 15) // 16 * 4 if grad_bf16 else Kp
-        _check(gstride >= g_wcol + 1 and gstride % 4 == 0, "grad_out row stride must hold the w column and be a multiple of 4")
+        _check(gstride >= g_wcol + 1 and gstride % 4 == 0,
+               "grad_out row stride must hold the w column and be a multiple of 4")
         _check(not grad_bf16 or _is_gpu(dpred), "bf16 gradient rows are a GPU path")
     v_stride = _chk_rows(v, Kp, "v")
     o = opt or OptConfig()
@@ -508,7 +510,8 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               big_count=_p(dd.big_count), multi=_p(dd.multi), slice_list=_p(dd.slice_list),
               slice_start=_p(dd.slice_start), nslices=int(dd.nslices or 0), dense_list=_p(dd.dense_list),
               dense_part=_p(dp), nex=int(dpred.numel()),
-              dense_stream=dense_stream.cuda_stream if dense_stream is not None else 0, dtype=dt, max_chunks=dd.n, max_unique=dd.n,
+              dense_stream=dense_stream.cuda_stream if dense_stream is not None else 0, dtype=dt, max_chunks=dd.n,
+              max_unique=dd.n,
               stream=_stream(dpred), g_wcol=g_wcol if mode == BWD_EMIT else -1, g_bf16=int(bool(grad_bf16)),
               sr_counter=_p(sr_counter), counters_ready=int(bool(dd.bwd_fresh)),
               seg_bounds=_p(seg_bounds), piece=int(piece),

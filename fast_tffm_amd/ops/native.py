@@ -19,26 +19,37 @@ class NativeExtensionError(RuntimeError):
     pass
 
 
-def _load(name: str, build_kind: str):
+def _load(name: str, build_kind: str, variant: str | None = None):
+    """Import an in-tree module, (re)building it first when it is missing or was not built
+    from the current sources (content hash embedded in the binary, see build_native)."""
     with _lock:
         if name in _mods:
             return _mods[name]
-        try:
-            mod = importlib.import_module(f"fast_tffm_amd._native.{name}")
-        except ImportError as first:
-            if os.environ.get("FM_NO_AUTOBUILD") == "1":
-                raise NativeExtensionError(
-                    f"native extension {name} is not built; run `python -m fast_tffm_amd.build_native`") from first
-            from fast_tffm_amd import build_native
+        from fast_tffm_amd import build_native as bn
 
+        if build_kind == "cpu":
+            target, want = bn.cpu_target(), bn.cpu_hash()
+        else:
+            target, want = bn.hip_target(variant), bn.hip_hash(variant)
+        have = bn.embedded_hash(target)
+        if have != want:
+            why = "is not built" if have is None else f"is stale (built from {have}, sources are {want})"
+            if os.environ.get("FM_NO_AUTOBUILD") == "1":
+                raise NativeExtensionError(f"native extension {name} {why}; run `python -m fast_tffm_amd.build_native`")
+            print(f"[fast_tffm_amd] native extension {name} {why}: building", flush=True)
             try:
                 if build_kind == "cpu":
-                    build_native.build_cpu()
+                    bn.build_cpu()
                 else:
-                    build_native.build_hip()
-                mod = importlib.import_module(f"fast_tffm_amd._native.{name}")
+                    bn.build_hip(variant=variant)
             except Exception as e:  # noqa: BLE001
-                raise NativeExtensionError(f"could not build/load native extension {name}: {e}") from e
+                raise NativeExtensionError(f"could not build native extension {name}: {e}") from e
+        try:
+            mod = importlib.import_module(f"fast_tffm_amd._native.{name}")
+        except ImportError as e:
+            raise NativeExtensionError(f"could not load native extension {name}: {e}") from e
+        if getattr(mod, "BUILD_HASH", None) != want:
+            raise NativeExtensionError(f"{name}: loaded module hash {getattr(mod, 'BUILD_HASH', None)} != {want}")
         _mods[name] = mod
         return mod
 
@@ -80,9 +91,14 @@ _SYNC = os.environ.get("FM_SYNC_LAUNCH", "0") == "1"
 def hip():
     """gfx950 module: GPU step kernels. Raises if unavailable."""
     var = os.environ.get("FM_HIP_VARIANT")  # A/B builds (build_native --variant)
-    mod = _load(f"_fm_hip_{var}", "hip") if var else _load("_fm_hip", "hip")
+    mod = _load(f"_fm_hip_{var}", "hip", var) if var else _load("_fm_hip", "hip")
     return _SyncChecked(mod) if _SYNC else mod
 
 
 def loaded_paths() -> dict[str, str]:
     return {k: getattr(v, "__file__", "?") for k, v in _mods.items()}
+
+
+def build_hashes() -> dict[str, str]:
+    """Content hashes of the loaded native modules (reported by bench.py)."""
+    return {k: getattr(v, "BUILD_HASH", "?") for k, v in _mods.items()}

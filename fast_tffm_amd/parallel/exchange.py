@@ -29,6 +29,8 @@ meant for small vocabularies (BASELINE config 3).
 
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -171,6 +173,9 @@ def _sub_batch(b: Batch, e0: int, e1: int, n0: int, n1: int, offsets: torch.Tens
 
 
 class ShardExchange(_Base):
+    N_TRAIN_SLOTS = 3
+    EVAL_SLOT = 3
+
     """Row-sharded step.
 
     ``train_step(b, next_batch)`` builds the plan of the next batch (everything that
@@ -198,7 +203,9 @@ class ShardExchange(_Base):
         super().__init__(model)
         self.Rps = model.rps
         self.key_bits = bits_for(self.W * self.Rps)
-        self.slots = [_PlanSlot(), _PlanSlot(), _PlanSlot()]  # current, next, next-but-one plans
+        # training plans rotate over slots 0..2 (current, next, next-but-one); slot 3 belongs to
+        # evaluation / prediction plans (forward()), which never reuse a training slot
+        self.slots = [_PlanSlot(), _PlanSlot(), _PlanSlot(), _PlanSlot()]
         # wire format of the gathered rows: storage dtype (exact) or bf16 for fp32 tables on request
         tdt = model.table.v.dtype
         self.wire = K.WireFormat.make(tdt, self.Kp, model.cfg.comm_dtype if self.dev.type == "cuda" else "fp32")
@@ -219,12 +226,24 @@ class ShardExchange(_Base):
         self.cur_plan: _ShardPlan | None = None
         self.step_start = None
         self.early_steps = 0          # steps that took the early-exchange + patch path
-        # lookahead plans talk on their own communicator (own RCCL stream): the id
-        # all-to-all of batch t+1 does not queue behind step t's row / grad all-to-alls
+        # Communicators.  "dual" (default): lookahead plans talk on their own communicator (own
+        # RCCL stream), so the id all-to-all of batch t+1 does not queue behind step t's row /
+        # grad all-to-alls.  Ordering invariant that keeps this deadlock-free: every rank issues
+        # the collectives of EACH communicator in the same host program order (the executor's
+        # control flow depends only on values that are identical on all ranks: the lookahead
+        # depth and the exchanged count matrices), and the two communicators never wait on each
+        # other inside a collective -- a main-communicator collective may depend on a plan
+        # collective only through stream events recorded after it on the same rank.  RCCL
+        # kernels of the two communicators then make progress independently (each occupies a
+        # few CUs).  FM_SINGLE_COMM=1 ("single") routes every collective through the main
+        # communicator in program order (no cross-communicator progress assumption; the plan's
+        # exchanges then serialise with the step's row / grad all-to-alls).
+        single = os.environ.get("FM_SINGLE_COMM", "0") == "1"
+        self.comm_mode = "single" if (single or self.W == 1) else "dual"
         self.plan_group = (dist.new_group(ranks=list(range(self.W)), backend=dist.get_backend(self.group))
-                           if self.W > 1 else self.group)
+                           if self.comm_mode == "dual" else self.group)
         self.cpu_group = self.ctx.cpu_group or self.group
-        self.last_slot = len(self.slots) - 1
+        self.last_slot = self.N_TRAIN_SLOTS - 1
         self.pending: list[_ShardPlan] = []   # built plans of upcoming batches, in order
         self._prep = None
 
@@ -264,17 +283,23 @@ class ShardExchange(_Base):
         ``inputs_ready``: main-stream event after which ``b``'s tensors are valid
         (default: everything enqueued on the current stream so far)."""
         m = self.m
-        # round robin over the slots: never the slot of a pending (not yet consumed) plan or of
-        # the current step's plan; the last step that used the slot is waited for (done event)
-        busy = {p.slot for p in self.pending}
-        if self.cur_plan is not None:
-            busy.add(self.cur_plan.slot)
-        idx = self.last_slot
-        for _ in range(len(self.slots)):
-            idx = (idx + 1) % len(self.slots)
-            if idx not in busy:
-                break
-        self.last_slot = idx
+        if train:
+            # round robin over the training slots: never the slot of a pending (not yet consumed)
+            # plan or of the current step's plan; the last step that used the slot is waited for
+            # (done event)
+            busy = {p.slot for p in self.pending}
+            if self.cur_plan is not None:
+                busy.add(self.cur_plan.slot)
+            idx = self.last_slot
+            for _ in range(self.N_TRAIN_SLOTS):
+                idx = (idx + 1) % self.N_TRAIN_SLOTS
+                if idx not in busy:
+                    break
+            else:
+                raise RuntimeError("ShardExchange: every training plan slot is in use")
+            self.last_slot = idx
+        else:
+            idx = self.EVAL_SLOT  # (its done event orders it after the previous forward)
         slot = self.slots[idx]
         pl = _ShardPlan()
         pl.b, pl.slot, pl.train = b, idx, train
@@ -621,8 +646,8 @@ class ShardExchange(_Base):
             raise RuntimeError("sharded key out of range")
 
     def _take_plan(self, b: Batch, train: bool) -> _ShardPlan:
-        pl = self.pending[0] if self.pending else None
-        if pl is not None and pl.b is b and (len(pl.parts) > 1) == (train and self.nparts > 1 and b.B >= 2 * self.nparts):
+        pl = self.pending[0] if (self.pending and train) else None
+        if pl is not None and pl.b is b and (len(pl.parts) > 1) == (self.nparts > 1 and b.B >= 2 * self.nparts):
             self.pending.pop(0)
             self._plan_finish(pl)
         else:  # (pending plans for other batches, e.g. the next training batches, stay pending)

@@ -67,7 +67,16 @@ class Trainer:
         if path is None:
             return False
         meta = ckpt.restore_checkpoint(self.model, path)
-        rs = meta.get("reader_state") or {}
+        # this rank's own reader position (each rank reads its own file subset); a checkpoint
+        # from another world size (or without per-rank entries) falls back to rank 0's
+        per_rank = meta.get("reader_states") or {}
+        if int(meta.get("reader_world", 1)) == self.world and str(self.rank) in per_rank:
+            rs = per_rank[str(self.rank)] or {}
+        else:
+            rs = meta.get("reader_state") or {}
+            if self.world > 1:
+                self.print(f"Checkpoint reader positions are for world {meta.get('reader_world', 1)}; "
+                           f"every rank resumes at rank 0's position")
         self.reader_state = ReaderState(epoch=int(rs.get("epoch", 0)),
                                         batches_in_epoch=int(rs.get("batches_in_epoch", 0)))
         self.restored_from = path
@@ -172,11 +181,11 @@ class Trainer:
             if self.monitor:
                 q = pf.size()
                 self.print("speed:", c.batch_size * self.world / max(tend - t0, 1e-9),
-                           "shuffle_queue: %.2f%%" % 100.0,
+                           "shuffle_queue: %.2f%%" % (100.0 * pf.shuffle_fill()),
                            "example_queue: %.2f%%" % (q * 100.0 / pf.queue_size))
             if c.log_steps <= 1 or sn % c.log_steps == 0:
                 self.print("-- Global Step: %d; Avg loss: %.5f;" % (sn, loss))
-            metrics.log(sn, loss=loss, exq_size=pf.size())
+            metrics.log(sn, loss=loss, exq_size=pf.size(), shuffle_fill=pf.shuffle_fill())
             return loss, tend
 
         batch, have = fetch()

@@ -143,7 +143,15 @@ def save_checkpoint(model, log_dir: str, step: int, *, reader_state: dict | None
                 sources[k] = (torch.float32, tuple(t.shape), (lambda t_: lambda r0, r1: t_[r0:r1])(t))
         write_safetensors_streamed(tmp, sources, {"format": FORMAT, "rank": shard_rank, "world": shard_world})
         os.replace(tmp, os.path.join(path, _shard_name(shard_rank, shard_world)))
+    # every rank reads its own file subset (reader.py / loader.cpp shard the files by rank),
+    # so each rank's reader position is saved and restored separately
+    reader_states = {"0": reader_state or {}}
     if ctx is not None and world > 1:
+        import torch.distributed as dist
+
+        allrs = [None] * world
+        dist.all_gather_object(allrs, reader_state or {}, group=ctx.cpu_group or ctx.group)
+        reader_states = {str(r): s for r, s in enumerate(allrs)}
         ctx.barrier()
     if rank == 0:
         meta = {
@@ -156,7 +164,9 @@ def save_checkpoint(model, log_dir: str, step: int, *, reader_state: dict | None
             "shard_world": table.world,
             "mode": model.mode,
             "loss_type": model.cfg.loss_type,
-            "reader_state": reader_state or {},
+            "reader_state": reader_state or {},          # rank 0's (single-process readers)
+            "reader_states": reader_states,              # per rank
+            "reader_world": world,
             "global_bias": float(model.gbias.item()) if getattr(model, "gbias", None) is not None else None,
         }
         with open(os.path.join(path, "meta.json.tmp"), "w") as f:

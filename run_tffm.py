@@ -1,5 +1,8 @@
 #!/usr/bin/env python3
-"""Reference-compatible entry point name (run_tffm.py). Entry point: python run.py {train,predict,generate} CONFIG [--dist ...] [-t FILE] [-m] [--export_path DIR]."""
+"""Reference-compatible entry point name (run_tffm.py).
+
+Usage: python run_tffm.py {train,predict,generate} CONFIG [--dist ...] [-t FILE] [-m] [--export_path DIR]
+"""
 import os
 import sys
 

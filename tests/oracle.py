@@ -31,7 +31,8 @@ def fm_scores(params: torch.Tensor, offsets: torch.Tensor, ids: torch.Tensor, va
 
 def fm_objective(params, batch, loss_type: str, factor_lambda=0.0, bias_lambda=0.0, batch_size_cfg=None,
                  grad_scale_mult: float = 1.0):
-    pred, rv, rw = fm_scores(params, batch.offsets.cpu(), batch.ids.cpu(), None if batch.vals is None else batch.vals.cpu())
+    vals = None if batch.vals is None else batch.vals.cpu()
+    pred, rv, rw = fm_scores(params, batch.offsets.cpu(), batch.ids.cpu(), vals)
     y = batch.labels.cpu().to(params.dtype)
     wt = batch.weights.cpu().to(params.dtype) if batch.weights is not None else torch.ones_like(y)
     if loss_type == "mse":

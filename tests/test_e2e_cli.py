@@ -12,7 +12,6 @@ import re
 
 import numpy as np
 import pytest
-import torch
 
 from fast_tffm_amd import cli
 from fast_tffm_amd.config import load_config
@@ -176,3 +175,9 @@ def test_trace_file_written(workdir):
     rc, out = _run(["train", cfg_path, "-t", trace, "-m"])
     assert os.path.exists(trace + ".json")
     assert "speed:" in out and "example_queue:" in out
+    # shuffle_queue is the loader's real window fill (reference run_tffm.py:52-63), not a constant:
+    # the window holds between min_after_dequeue + B and capacity (4.5 B) lines while full, less
+    # while the epoch's tail drains
+    fills = [float(x) for x in re.findall(r"shuffle_queue: ([0-9.]+)%", out)]
+    assert fills and all(0.0 <= f <= 100.0 for f in fills)
+    assert len(set(fills)) > 1 or fills[0] < 100.0

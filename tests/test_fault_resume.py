@@ -72,18 +72,23 @@ def _final_state(log_dir):
 
 
 @pytest.mark.timeout(600)
-def test_killed_rank_restarts_and_resumes_exactly(tmp_path):
+@pytest.mark.parametrize("sizes,fault_step", [((600, 600), 3), ((700, 300, 500), 7)], ids=["equal", "unequal"])
+def test_killed_rank_restarts_and_resumes_exactly(tmp_path, sizes, fault_step):
+    """equal: one 600-line file per rank.  unequal: 3 files of different sizes over 2 ranks,
+    2 epochs -- the ranks cross their epoch boundaries at different steps, so the
+    checkpoint must carry each rank's own reader position (a restore of rank 0's position
+    on every rank skips / replays data and changes the final model)."""
     tmp = str(tmp_path)
     os.makedirs(os.path.join(tmp, "data"))
-    for i in range(2):
-        write_libsvm(os.path.join(tmp, "data", f"train_{i}"), 600, vocab_size=50000, seed=i,
+    for i, n in enumerate(sizes):
+        write_libsvm(os.path.join(tmp, "data", f"train_{i}"), n, vocab_size=50000, seed=i,
                      weights_path=os.path.join(tmp, "data", f"weight_{i}"))
     marker = os.path.join(tmp, "fault.marker")
     faulty = _torchrun(_cfg(tmp, os.path.join(tmp, "log_fault")),
-                       {"FM_FAULT_STEP": "3", "FM_FAULT_RANK": "1", "FM_FAULT_MARKER": marker})
+                       {"FM_FAULT_STEP": str(fault_step), "FM_FAULT_RANK": "1", "FM_FAULT_MARKER": marker})
     assert faulty.returncode == 0, faulty.stdout[-3000:] + faulty.stderr[-3000:]
     assert os.path.exists(marker), "the fault was never injected"
-    assert "injected failure after step 3 on rank 1" in faulty.stderr
+    assert f"injected failure after step {fault_step} on rank 1" in faulty.stderr
     clean = _torchrun(_cfg(tmp, os.path.join(tmp, "log_clean")), {})
     assert clean.returncode == 0, clean.stdout[-3000:] + clean.stderr[-3000:]
 
