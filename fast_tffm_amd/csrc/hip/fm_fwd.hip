@@ -71,7 +71,6 @@ void fm_fwd_kernel(FwdArgs a) {
   const bool tact = t < nv;
   const int tE = tact ? t : nv - 1;        // clamped: loads never leave the row
   const float tmask = tact ? 1.f : 0.f;
-  const float wmask = (t == 0) ? 1.f : 0.f;
   const TV* vbase = reinterpret_cast<const TV*>(a.v) + tE * EPL;
   const int wave = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   const int nwaves = gridDim.x * kWavesPerBlock;
@@ -87,13 +86,21 @@ void fm_fwd_kernel(FwdArgs a) {
     for (int base = s; base < e; base += kWave) {
       const int m = min(kWave, e - base);
       int my_row = 0;
-      float my_x = 0.f;
+      float my_x = 0.f, my_w = 0.f, my_s = 1.f;
       if (lane < m) {
         my_row = a.rows[base + lane];
         my_x = a.vals ? a.vals[base + lane] : 1.f;
+        // the linear weight (and fp8 scale, same cache line) of occurrence `lane`, one
+        // lane-parallel load per 64 occurrences instead of one per row group: the w loads
+        // were ~45% of the kernel's VMEM instructions with the TA 72% busy
+        // (profiles/r2/pmc_k64_fp32_before.txt)
+        my_w = a.w[(long long)my_row * a.w_stride];
+        my_s = row_scale<TV>(a.w, my_row, a.w_stride);
       }
+      lin += my_x * my_w;
+      if (want_reg) rw += my_w * my_w;
       for (int q = 0; q < m; q += G * UNR) {
-        float fr[UNR][EPL], fw[UNR], fx[UNR], fs[UNR];
+        float fr[UNR][EPL], fx[UNR], fs[UNR];
         // Issue every row load of the round before the first use.  Loads are
         // unconditional (slots past the example re-read a valid row of it and are
         // masked to zero afterwards), so hipcc keeps all UNR loads in flight.
@@ -105,8 +112,7 @@ void fm_fwd_kernel(FwdArgs a) {
           const float x = __shfl(my_x, src, kWave);
           fx[u] = f < m ? x : 0.f;
           F::load(vbase + (long long)row * a.v_stride, fr[u]);
-          fw[u] = a.w[(long long)row * a.w_stride];
-          fs[u] = row_scale<TV>(a.w, row, a.w_stride);  // (fp8: same cache line as w)
+          if constexpr (F::kScaled) fs[u] = __shfl(my_s, src, kWave);
         }
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
@@ -121,12 +127,10 @@ void fm_fwd_kernel(FwdArgs a) {
             s1[k] += xv;
             s2[k] += xv * xv;
           }
-          lin += wmask * fx[u] * fw[u];
           if (want_reg) {
             const float ok = (q + u * G + g) < m ? 1.f : 0.f;
 #pragma unroll
             for (int k = 0; k < EPL; ++k) rv += ok * tmask * fr[u][k] * fr[u][k];
-            rw += ok * wmask * fw[u] * fw[u];
           }
         }
       }

@@ -703,13 +703,6 @@ class ShardExchange(_Base):
         with roctx_range("plan"):
             pl = self._take_plan(b, True)
         self.cur_plan = pl
-        if self.pending and next_batch is not None and self.pending[0].b is next_batch:
-            nxt_pl = self.pending[0]
-            with roctx_range("plan_finish_next"):
-                self._plan_finish(nxt_pl)   # counts ready since the last step: no wait
-            if nxt_pl.early is None and self._early_ok(nxt_pl, pl):
-                with roctx_range("early_rows_next"):
-                    self._early_ahead(nxt_pl, pl)
         wf = self.wire
         # every part's rows are gathered first and their all-to-alls queued on RCCL's stream
         # (async): part k+1's rows travel while part k computes
@@ -763,6 +756,20 @@ class ShardExchange(_Base):
             done = torch.cuda.Event()
             done.record(torch.cuda.current_stream(self.dev))
             self.slots[pl.slot].done = done
+        if self.pending and next_batch is not None and self.pending[0].b is next_batch:
+            # Finish the next batch's plan only now, with this whole step already enqueued: the
+            # host's wait for its owner counts (dedup on the plan stream, started one step ago)
+            # then overlaps this step's GPU work instead of holding back the step's launches
+            # (at the start of the step it left the compute stream idle ~270 us per step at
+            # world 1: profiles/shard_w1_r1s3/timeline_early_split_off.txt).  Its early row
+            # exchange gathers against the table as of this step's start (step_start) and is
+            # patched after this step's update.
+            nxt_pl = self.pending[0]
+            with roctx_range("plan_finish_next"):
+                self._plan_finish(nxt_pl)
+            if nxt_pl.early is None and self._early_ok(nxt_pl, pl):
+                with roctx_range("early_rows_next"):
+                    self._early_ahead(nxt_pl, pl)
         if next2 is not None and not any(p.b is next2 for p in self.pending):
             if not any(p.b is next_batch for p in self.pending) and next_batch is not None:
                 with roctx_range("plan_next"):  # (first depth-2 step: the next batch has no plan yet)

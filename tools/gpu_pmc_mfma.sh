@@ -1,16 +1,17 @@
 #!/bin/bash
-# MFMA / LDS counters of the dense-row MFMA backward (FM_DENSE_BWD=1), kernel trace only.
-# usage: tools/gpu_pmc_mfma.sh <tag>
+# MFMA / VALU / LDS counters (kernel trace only), summarised by tools/pmc_summary.py
+# (MFMA% = sum SQ_VALU_MFMA_BUSY_CYCLES / (per-instance GRBM_GUI_ACTIVE x 1024 SIMDs), as rocprof's MfmaUtil).
+# usage: tools/gpu_pmc_mfma.sh <tag> [bench args...]
 set -o pipefail
-TAG=${1:-pmc_mfma}
+TAG=${1:-pmc_mfma}; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
-export FM_NO_AUTOBUILD=1 FM_DENSE_BWD=1
+export FM_NO_AUTOBUILD=1
 cd /tmp && export TMPDIR=/tmp
 i=0
-for CTRS in "SQ_INSTS_VALU_MFMA_F32 SQ_INSTS_MFMA GRBM_GUI_ACTIVE" "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" "TCC_HIT_sum TCC_MISS_sum" "FETCH_SIZE"; do
+for CTRS in "SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE" "TCC_HIT_sum TCC_MISS_sum" "FETCH_SIZE"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $CTRS --kernel-trace --output-format csv -d $OUT/p$i -o run -- python3 $R/bench.py --steps 5 --warmup 2 > $OUT/p$i.log 2>&1 || { echo "pmc pass $i failed"; tail -20 $OUT/p$i.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $CTRS --kernel-trace --output-format csv -d $OUT/p$i -o run -- python3 $R/bench.py --steps 5 --warmup 2 "$@" > $OUT/p$i.log 2>&1 || { echo "pmc pass $i failed"; tail -20 $OUT/p$i.log; exit 1; }
 done
-python3 $R/tools/pmc_mfma_summary.py $OUT | tee $OUT/pmc_mfma_summary.txt
+python3 $R/tools/pmc_summary.py $OUT | tee $OUT/pmc_summary.txt

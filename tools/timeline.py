@@ -13,7 +13,10 @@ if len(idx) < 3:
     sys.exit("not enough steps in trace")
 a, b = idx[-3], idx[-2]
 t0 = int(rows[a]["Start_Timestamp"])
-print(f"{'start_us':>9} {'dur_us':>8}  kernel   (step = {(int(rows[b]['Start_Timestamp']) - t0) / 1000:.1f} us)")
+qcol = next((c for c in ("Stream_Id", "Queue_Id") if c in rows[0]), None)
+step_us = (int(rows[b]["Start_Timestamp"]) - t0) / 1000
+print(f"{'start_us':>9} {'dur_us':>8} {'q':>3}  kernel   (step = {step_us:.1f} us)")
 for r in rows[a:b]:
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-    print(f"{(s - t0) / 1000:9.1f} {(e - s) / 1000:8.1f}  {r['Kernel_Name'][:100]}")
+    q = r[qcol] if qcol else "-"
+    print(f"{(s - t0) / 1000:9.1f} {(e - s) / 1000:8.1f} {q:>3}  {r['Kernel_Name'][:100]}")
