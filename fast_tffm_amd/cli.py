@@ -134,6 +134,7 @@ def main(argv: list[str] | None = None) -> int:
         else:
             tr.predict()
     finally:
+        tr.close()
         if ctx is not None:
             fmdist.shutdown()
     return 0

@@ -24,6 +24,7 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 
 import os
+import weakref
 
 import torch
 
@@ -151,7 +152,7 @@ class _LookaheadGraphRing:
     def __init__(self, model: "FactorizationMachine", example: Batch, n: int):
         if n < 2 or n % 2:
             raise ValueError("the lookahead ring needs an even number (>= 2) of buffers")
-        self.m = model
+        self.m = weakref.proxy(model)  # no cycle: a dropped model is closed by refcount at once
         dev = model.device
 
         def static(t):
@@ -205,7 +206,7 @@ class _GraphedStep:
     """A hipGraph of the local training step over static input buffers."""
 
     def __init__(self, model: "FactorizationMachine", ex: Batch, warmup: int = 1):
-        self.m = model
+        self.m = weakref.proxy(model)
         dev = model.device
         self.sig = self._sig(ex)
 
@@ -306,6 +307,60 @@ class FactorizationMachine:
             self._exchange = make_exchange(self)
         elif mode != "local":
             raise ValueError(f"mode={mode} needs a distributed context")
+        self.closed = False
+        if self._exchange is not None:  # holds communicators: closed by dist.shutdown() first
+            from ..parallel.dist import register_closeable
+
+            register_closeable(self)
+
+    # ------------------------------------------------------------------
+    def close(self) -> None:
+        """Release the step executor's device resources in a safe order: wait for the
+        device, drop captured hipGraphs (their kernel nodes reference workspace and stream
+        state), close the exchange (pending RCCL works, its plan communicator), then the
+        side / dense streams.  Idempotent; the table stays readable (checkpointing after
+        close works), further ``train_step`` calls raise.  ``Trainer`` and
+        ``parallel.dist.shutdown()`` call it, so no teardown is left to the garbage
+        collector (a communicator finalised by it after the process group was destroyed
+        aborted the process: round-1 GPU suite, commit 62c2bac)."""
+        if getattr(self, "closed", True):
+            return
+        self.closed = True
+        if self.device.type == "cuda" and torch.cuda.is_initialized():
+            torch.cuda.synchronize(self.device)
+        for g in ([self._graph] if self._graph is not None else []) + list(self._graph_pool):
+            if g.graph is not None:
+                g.graph.reset()
+            g.graph = None
+        if self._ring is not None:
+            for g in self._ring.graphs:
+                if g is not None:
+                    g.reset()
+            self._ring.graphs = [None] * len(self._ring.graphs)
+        self._graph, self._graph_pool, self._ring = None, [], None
+        if self._exchange is not None:
+            self._exchange.close()
+            self._exchange = None
+        self._lpending = None
+        self._lslots = [_LocalSlot(), _LocalSlot()]
+        self._side = None
+        self._dense_st = None
+        if self.device.type == "cuda" and torch.cuda.is_initialized():
+            torch.cuda.synchronize(self.device)
+
+    def __del__(self):
+        # refcount drop (helpers and exchanges hold the model through weak proxies, so there
+        # is no cycle): the teardown runs right where the last reference goes, in program order
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 -- interpreter shutdown: HIP / dist may be gone already
+            pass
+
+    def __enter__(self) -> "FactorizationMachine":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
 
     def sr_tick(self) -> torch.Tensor | None:
         """Advance the stochastic-rounding step counter (on the current stream); its tensor or None."""
@@ -381,6 +436,8 @@ class FactorizationMachine:
         ``next_batch`` / ``next2`` (optional lookahead): the batches of the following
         calls; the executors prepare their table-independent work (dedup, id exchange,
         early row exchange) concurrently with this step."""
+        if self.closed:
+            raise RuntimeError("train_step on a closed FactorizationMachine")
         if self._ring is not None and (k := self._ring.index(b, next_batch)) >= 0:
             out = self._ring.replay(k)
         elif self._graph is not None and self._graph.matches(b):
@@ -572,6 +629,8 @@ class FactorizationMachine:
     @torch.no_grad()
     def forward(self, b: Batch, *, loss: str = "none", want_reg: bool = False) -> K.FwdOut:
         """Scores (and optionally the summed loss) without touching parameters."""
+        if self.closed and self.mode != "local":
+            raise RuntimeError("forward on a closed multi-rank FactorizationMachine")
         if self._exchange is not None:
             return self._exchange.forward(b, loss=loss, want_reg=want_reg)
         rows = b.ids.to(torch.int32)

@@ -15,8 +15,8 @@ The backend is "nccl" (= RCCL on ROCm) for GPU tensors and "gloo" on CPU.
 from __future__ import annotations
 
 import datetime
-import gc
 import os
+import weakref
 from dataclasses import dataclass
 
 import torch
@@ -53,6 +53,17 @@ class DistContext:
 
 
 _CTX: DistContext | None = None
+# objects holding communicators, streams or captured graphs (models / exchanges): closed, in
+# creation order, before the process groups are destroyed
+_LIVE: "weakref.WeakValueDictionary[int, object]" = weakref.WeakValueDictionary()
+_LIVE_SEQ = 0
+
+
+def register_closeable(obj) -> None:
+    """Track ``obj`` (with a ``close()`` method) so that ``shutdown()`` releases it first."""
+    global _LIVE_SEQ
+    _LIVE_SEQ += 1
+    _LIVE[_LIVE_SEQ] = obj
 
 
 def parse_dist_args(dist_args: list[str] | None) -> dict:
@@ -128,12 +139,16 @@ def local_context(device: str | torch.device = "cpu") -> DistContext:
 
 
 def shutdown() -> None:
-    """Destroy the process groups.  Unreachable models / exchanges that still hold
-    communicators are collected first, while their groups are alive: a communicator
-    finalised later by the garbage collector, after the destroy, can abort the process."""
+    """Close every live model / exchange (their communicators, streams and hipGraphs are
+    released in a fixed order while the process groups still exist), then destroy the
+    groups.  Nothing is left for the garbage collector to finalise after the destroy."""
     global _CTX
+    for key in sorted(list(_LIVE.keys())):
+        obj = _LIVE.get(key)
+        if obj is not None:
+            obj.close()
+    _LIVE.clear()
     if dist.is_available() and dist.is_initialized():
-        gc.collect()
         if torch.cuda.is_available() and torch.cuda.is_initialized():
             torch.cuda.synchronize()
         dist.destroy_process_group()

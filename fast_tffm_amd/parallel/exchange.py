@@ -30,6 +30,7 @@ meant for small vocabularies (BASELINE config 3).
 from __future__ import annotations
 
 import os
+import weakref
 
 import numpy as np
 import torch
@@ -57,7 +58,7 @@ def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits: list[int], in_splits:
 
 class _Base:
     def __init__(self, model):
-        self.m = model
+        self.m = weakref.proxy(model)   # the model owns the exchange (no reference cycle)
         self.ctx = model.dist
         self.group = self.ctx.group
         self.W = model.world
@@ -65,6 +66,10 @@ class _Base:
         self.gs = model.Kp + 4          # exchange row: [v(Kp) | w | pad 3]
         self.dev = model.device
         self.dd2ws: K.DedupWorkspace | None = None
+
+    def close(self) -> None:
+        """Release device resources (model.close() calls this after a device sync)."""
+        self.dd2ws = None
 
     def _dd2(self, n: int) -> K.DedupWorkspace:
         if self.dd2ws is None or self.dd2ws.cap < n:
@@ -239,13 +244,35 @@ class ShardExchange(_Base):
         # communicator in program order (no cross-communicator progress assumption; the plan's
         # exchanges then serialise with the step's row / grad all-to-alls).
         single = os.environ.get("FM_SINGLE_COMM", "0") == "1"
-        self.comm_mode = "single" if (single or self.W == 1) else "dual"
+        # (FM_COMM_MODE=dual forces the plan communicator at world 1: teardown tests)
+        forced = os.environ.get("FM_COMM_MODE", "")
+        self.comm_mode = forced if forced in ("single", "dual") else (
+            "single" if (single or self.W == 1) else "dual")
         self.plan_group = (dist.new_group(ranks=list(range(self.W)), backend=dist.get_backend(self.group))
                            if self.comm_mode == "dual" else self.group)
         self.cpu_group = self.ctx.cpu_group or self.group
         self.last_slot = self.N_TRAIN_SLOTS - 1
         self.pending: list[_ShardPlan] = []   # built plans of upcoming batches, in order
         self._prep = None
+
+    def close(self) -> None:
+        """Wait for in-flight exchange works, drop every plan (device buffers, pinned
+        staging, events) and destroy the plan communicator (dual mode) while the main
+        process group is still alive."""
+        for pl in [self.cur_plan] + list(self.pending):
+            e = getattr(pl, "early", None) if pl is not None else None
+            if e is not None and getattr(e, "work", None) is not None:
+                e.work.wait()
+                e.work = None
+        if self.dev.type == "cuda" and torch.cuda.is_initialized():
+            torch.cuda.synchronize(self.dev)
+        self.pending, self.cur_plan, self.step_start = [], None, None
+        self.slots = [_PlanSlot() for _ in self.slots]
+        if self.comm_mode == "dual" and self.plan_group is not None and dist.is_initialized():
+            dist.destroy_process_group(self.plan_group)
+        self.plan_group = None
+        self._prep = None
+        super().close()
 
     def _prep_stream(self):
         if self._prep is None:

@@ -61,6 +61,16 @@ class Trainer:
         self.reader_state = ReaderState()
         self.restored_from = None
 
+    def close(self) -> None:
+        """Release the model's executor resources (graphs, exchange, streams)."""
+        self.model.close()
+
+    def __enter__(self) -> "Trainer":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
+
     # ------------------------------------------------------------------
     def restore(self) -> bool:
         path = ckpt.latest_checkpoint(self.cfg.log_dir)

@@ -41,18 +41,3 @@ def ref_data_dir():
     if not os.path.isdir(REF_DATA):
         pytest.skip("reference data directory not available")
     return REF_DATA
-
-
-@pytest.fixture(autouse=True)
-def _collect_gpu_garbage(request):
-    """GPU tests: objects a test leaves in reference cycles (models holding hipGraphs,
-    streams, communicators) are collected right after it, so their teardown runs under
-    that test's name instead of inside a later, unrelated test."""
-    yield
-    if "gpu" in request.keywords and _gpu_available():
-        import gc
-
-        import torch
-
-        gc.collect()
-        torch.cuda.synchronize()
