@@ -26,7 +26,12 @@
 
 namespace fm {
 
-enum BwdMode : int { kBwdLocal = 0, kBwdEmit = 1 };
+// LOCAL: parameters read from and the optimizer applied to table rows uniq[u];
+// EMIT: parameters read from gathered rows u, gradient row written to grad_out[u];
+// EMIT_TABLE (replicated-table data parallelism): parameters read from table rows
+// uniq[u], gradient row scattered to grad_out[uniq[u]] of a persistent dense buffer
+// with a touch marker (1.0) in the word after the w-gradient.
+enum BwdMode : int { kBwdLocal = 0, kBwdEmit = 1, kBwdEmitTable = 2 };
 constexpr int kMaxCH = 32;        // chunk length cap (prefetch registers)
 constexpr int kSmallChunks = 16;  // rows with more chunks go to the workgroup combine
 constexpr int kMaxPieceOwners = 64;  // owners of a split backward piece
@@ -102,7 +107,7 @@ __device__ inline void bwd_load_row(const BwdArgs& a, long long row, int tE, Row
 #pragma unroll
     for (int k = 0; k < EPL; ++k) r.vv[k] *= s;
   }
-  if (a.mode == kBwdEmit) return;
+  if (a.mode != kBwdLocal) return;
   const float* s0 = a.s0v + r.row * a.s_stride + tE * EPL;
 #pragma unroll
   for (int k = 0; k < EPL; k += 4) {
@@ -134,8 +139,8 @@ __device__ inline void bwd_finish(const BwdArgs& a, int u, int t, bool tact, Row
 #pragma unroll
   for (int k = 0; k < EPL; ++k) gr[k] = A[k] - Scx * r.vv[k] + nreg_v * r.vv[k];
   const float gw = Sc + nreg_w * r.wv;
-  if (a.mode == kBwdEmit) {
-    float* dst = a.grad_out + (long long)u * a.g_stride;
+  if (a.mode != kBwdLocal) {
+    float* dst = a.grad_out + (a.mode == kBwdEmitTable ? r.row : (long long)u) * a.g_stride;
     if (tact) {
       if (a.g_bf16) {  // EPL bf16 values per lane (EPL * 2 bytes, 8-byte aligned)
         uint16_t* d16 = reinterpret_cast<uint16_t*>(dst) + t * EPL;
@@ -152,7 +157,10 @@ __device__ inline void bwd_finish(const BwdArgs& a, int u, int t, bool tact, Row
           *reinterpret_cast<float4*>(dst + t * EPL + k) = make_float4(gr[k], gr[k + 1], gr[k + 2], gr[k + 3]);
       }
     }
-    if (t == 0) dst[a.g_wcol] = gw;
+    if (t == 0) {
+      dst[a.g_wcol] = gw;
+      if (a.mode == kBwdEmitTable) dst[a.g_wcol + 1] = 1.f;  // touched (the dense apply scans for it)
+    }
     return;
   }
 #pragma unroll
@@ -183,7 +191,7 @@ template <int LPR, typename TV, int EPL>
 __device__ inline void bwd_finalize(const BwdArgs& a, int u, int t, bool tact, int tE,
                                     const float (&A)[EPL], float Scx, float Sc, int n_u, uint32_t sr) {
   RowState<EPL> r;
-  bwd_load_row<TV, EPL>(a, a.mode == kBwdLocal ? (long long)a.uniq[u] : (long long)u, tE, r);
+  bwd_load_row<TV, EPL>(a, a.mode == kBwdEmit ? (long long)u : (long long)a.uniq[u], tE, r);
   bwd_finish<LPR, TV, EPL>(a, u, t, tact, r, A, Scx, Sc, n_u, sr);
 }
 
@@ -282,7 +290,7 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
     if (dense) continue;  // gradient from the MFMA path (fm_bwd_dense_kernel)
     const int len = j1 - j0;
     RowState<EPL> rs;
-    if (single) bwd_load_row<TV, EPL>(a, a.mode == kBwdLocal ? (long long)key : (long long)u, tE, rs);
+    if (single) bwd_load_row<TV, EPL>(a, a.mode == kBwdEmit ? (long long)u : (long long)key, tE, rs);
     // lane-parallel prefetch of the chunk's (example, dpred*x, x)
     int pex[PF];
     float pc[PF], px[PF];

@@ -238,6 +238,26 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("g_wcol") = -1, py::arg("g_bf16") = 0, py::arg("sr_counter") = 0);
 
   m.def(
+      "dense_apply",
+      [](long long R, long long row0, u64 grad, long long g_stride, int touch_col, int zero, int Kp, u64 v,
+         long long v_stride, u64 w, long long w_stride, u64 s0v, u64 s1v, long long s_stride, u64 s0w, u64 s1w,
+         int opt_type, float lr, float l1, float l2, float beta, int dtype, u64 stream, u64 sr_counter) {
+        fm::ApplyArgs a{};
+        a.sr_counter = P<const int>(sr_counter);
+        a.g_wcol = Kp; a.g_bf16 = 0;
+        a.R = (int)R; a.row0 = row0; a.touch_col = touch_col;
+        a.grad_in = P<const float>(grad); a.grad_zero = zero ? P<float>(grad) : nullptr;
+        a.g_stride = g_stride; a.Kp = Kp; a.v = P<void>(v); a.v_stride = v_stride; a.w = P<float>(w);
+        a.w_stride = w_stride; a.s0v = P<float>(s0v); a.s1v = P<float>(s1v); a.s_stride = s_stride;
+        a.s0w = P<float>(s0w); a.s1w = P<float>(s1w); a.opt = opt_params(opt_type, lr, l1, l2, beta);
+        check(fm::launch_dense_apply(a, dtype, S(stream)), "dense_apply");
+      },
+      py::arg("R"), py::arg("row0"), py::arg("grad"), py::arg("g_stride"), py::arg("touch_col"), py::arg("zero"),
+      py::arg("Kp"), py::arg("v"), py::arg("v_stride"), py::arg("w"), py::arg("w_stride"), py::arg("s0v"),
+      py::arg("s1v"), py::arg("s_stride"), py::arg("s0w"), py::arg("s1w"), py::arg("opt_type"), py::arg("lr"),
+      py::arg("l1"), py::arg("l2"), py::arg("beta"), py::arg("dtype"), py::arg("stream"), py::arg("sr_counter") = 0);
+
+  m.def(
       "init_rows",
       [](u64 v, long long v_stride, u64 w, long long w_stride, long long rows, int K, int Kp, int dtype,
          long long gid_mul, long long gid_add, unsigned long long seed, float range, u64 stream) {

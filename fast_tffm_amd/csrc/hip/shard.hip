@@ -168,6 +168,11 @@ struct ApplyArgs {
   const int* req;           // [R] local table row of each received gradient row
   const int* match;         // [R, W]: index of the same row in run q, or -1 (null when W == 1)
   const int* sr_counter;    // stochastic rounding of bf16 / fp8 row stores (null: round to nearest)
+  // dense form (dense_apply): rows row0 .. row0 + R of a dense gradient buffer, touched ones
+  // marked at word touch_col; grad_zero (== grad_in, writable) gets every applied row zeroed
+  long long row0;
+  int touch_col;
+  float* grad_zero;
 };
 
 // One table row's parameters + optimizer state in registers (this lane's EPL
@@ -458,6 +463,50 @@ __global__ __launch_bounds__(kBlock) void apply_runs_kernel(ApplyArgs a) {
     }
     ru.step_store(a, gr, gw, row, t, tact, sr);
   }
+}
+
+// Replicated-table (data-parallel) update from a dense, all-reduced gradient buffer:
+// one lane group per buffer row; rows without the touch marker are all zero and
+// skipped; a touched row gets one optimizer step and is zeroed for the next step, so
+// the buffer is never cleared wholesale (reads: one word per untouched row).
+template <int LPR, typename TV>
+__global__ __launch_bounds__(kBlock) void dense_apply_kernel(ApplyArgs a) {
+  const uint32_t sr = sr_step_seed(a.sr_counter);
+  constexpr int EPL = Frag<TV>::N;
+  constexpr int G = kWave / LPR;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPR, t = lane % LPR;
+  const int nv = a.Kp / EPL;
+  const bool tact = t < nv;
+  const int tE = tact ? t : nv - 1;
+  const int ngroups = gridDim.x * kWavesPerBlock * G;
+  for (int i = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g; i < a.R; i += ngroups) {
+    const float* grow = a.grad_in + (long long)i * a.g_stride;
+    if (grow[a.touch_col] == 0.f) continue;  // (group-uniform)
+    const long long row = a.row0 + i;
+    RowUpdate<LPR, TV> ru;
+    ru.load(a, row, tE);
+    float gr[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) gr[k] = 0.f;
+    float gw = 0.f;
+    add_grad_row<EPL>(a, grow, tE, gr, gw);
+    ru.step_store(a, gr, gw, row, t, tact, sr);
+    if (a.grad_zero) {
+      float4* z = reinterpret_cast<float4*>(a.grad_zero + (long long)i * a.g_stride);
+      const int nq = (int)(a.g_stride / 4);
+      for (int q = t; q < nq; q += LPR) z[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+}
+
+int launch_dense_apply(const ApplyArgs& a, int dtype, hipStream_t st) {
+  if (a.R <= 0) return 0;
+  if (a.g_stride % 4 != 0 || a.touch_col >= a.g_stride) return -7;
+  const int lpr = lanes_per_row(a.Kp, dtype);
+  const int grid = fill_grid(a.R, kWavesPerBlock * (kWave / lpr), 16384);
+  FM_DISPATCH(dtype, lpr, dense_apply_kernel, grid, st, a);
+  return (int)hipGetLastError();
 }
 
 int launch_gather_rows(const GatherArgs& a, int dtype, hipStream_t st) {

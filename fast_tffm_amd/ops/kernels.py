@@ -23,6 +23,7 @@ from . import native
 LOSS_TYPES = {"none": 0, "mse": 1, "logistic": 2}
 OPT_TYPES = {"adagrad": 0, "ftrl": 1, "sgd": 2}
 BWD_LOCAL, BWD_EMIT = 0, 1
+BWD_EMIT_TABLE = 2   # params from table rows uniq[u]; gradient scattered to grad_out[uniq[u]] + touch mark
 
 _DEBUG = os.environ.get("FM_DEBUG_CHECKS", "0") == "1"
 
@@ -460,7 +461,19 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
     _check(dd.sorted_ex is not None, "dedup must be run with ex_of_occ")
     _chk_vec(dpred, torch.float32, None, "dpred", dev)
     _check(r1.dtype == torch.float32 and r1.is_contiguous() and r1.shape[1] == Kp, "r1: [B, Kp] fp32 contiguous")
-    if mode == BWD_LOCAL:
+    if mode == BWD_EMIT_TABLE:
+        _check(_is_gpu(dpred) and table is not None and grad_out is not None,
+               "EMIT_TABLE mode: GPU, table (parameter rows) + dense grad_out")
+        v, w = table.v, table.w
+        dt = dtype_code(v.dtype)
+        s0v = s1v = s0w = s1w = None
+        s_stride = 0
+        _check(grad_out.dtype == torch.float32 and grad_out.stride(1) == 1 and grad_out.shape[0] >= v.shape[0],
+               "grad_out: dense fp32 rows covering the table")
+        gstride, gptr = grad_out.stride(0), grad_out.data_ptr()
+        g_wcol = Kp
+        _check(gstride >= Kp + 2 and gstride % 4 == 0, "grad_out rows: [g_v | g_w | touch | ...], stride % 4 == 0")
+    elif mode == BWD_LOCAL:
         _check(table is not None and opt is not None, "LOCAL mode needs table + opt")
         v, w = table.v, table.w
         dt = dtype_code(v.dtype)
@@ -512,7 +525,7 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               dense_part=_p(dp), nex=int(dpred.numel()),
               dense_stream=dense_stream.cuda_stream if dense_stream is not None else 0, dtype=dt, max_chunks=dd.n,
               max_unique=dd.n,
-              stream=_stream(dpred), g_wcol=g_wcol if mode == BWD_EMIT else -1, g_bf16=int(bool(grad_bf16)),
+              stream=_stream(dpred), g_wcol=g_wcol if mode != BWD_LOCAL else -1, g_bf16=int(bool(grad_bf16)),
               sr_counter=_p(sr_counter), counters_ready=int(bool(dd.bwd_fresh)),
               seg_bounds=_p(seg_bounds), piece=int(piece),
               n_owners=(seg_bounds.numel() - 1) // 2 if seg_bounds is not None else 0)
@@ -601,6 +614,27 @@ def apply_rows(dd: DedupOut, grad_in: torch.Tensor, table: TableState, opt: OptC
                                 s1v=_p(table.s1v), s_stride=s_stride, s0w=_p(table.s0w), s1w=_p(table.s1w),
                                 opt_type=opt.code, lr=float(opt.lr), l1=float(opt.l1), l2=float(opt.l2),
                                 beta=float(opt.beta), dtype=dt, threads=threads)
+
+
+def dense_apply(grad: torch.Tensor, table: TableState, opt: OptConfig, Kp: int, row0: int = 0,
+                rows: int | None = None, zero: bool = True, sr_counter: torch.Tensor | None = None) -> None:
+    """Replicated-table update from a dense gradient buffer ``grad`` [n, Kp+4] (rows
+    [g_v | g_w | touch | pad], e.g. all-reduced over the data-parallel ranks): every row whose
+    touch word is non-zero gets one optimizer step on table row ``row0 + i`` and (``zero``) is
+    cleared for the next step; untouched rows cost one word read.  GPU only; no host sync."""
+    _check(_is_gpu(grad), "dense_apply is a GPU path")
+    n = grad.shape[0] if rows is None else int(rows)
+    v_stride = _chk_rows(table.v, Kp, "v")
+    _check(grad.dtype == torch.float32 and grad.is_contiguous() and grad.shape[1] >= Kp + 2
+           and grad.shape[1] % 4 == 0, "grad: contiguous fp32 [n, Kp+4]")
+    _check(row0 >= 0 and row0 + n <= table.v.shape[0], "dense_apply rows outside the table")
+    s_stride = table.s0v.stride(0) if table.s0v is not None else 0
+    native.hip().dense_apply(R=n, row0=row0, grad=_p(grad), g_stride=grad.stride(0), touch_col=Kp + 1,
+                             zero=int(zero), Kp=Kp, v=_p(table.v), v_stride=v_stride, w=_p(table.w),
+                             w_stride=table.w.stride(0), s0v=_p(table.s0v), s1v=_p(table.s1v), s_stride=s_stride,
+                             s0w=_p(table.s0w), s1w=_p(table.s1w), opt_type=opt.code, lr=float(opt.lr),
+                             l1=float(opt.l1), l2=float(opt.l2), beta=float(opt.beta),
+                             dtype=dtype_code(table.v.dtype), stream=_stream(grad), sr_counter=_p(sr_counter))
 
 
 def apply_runs(req: torch.Tensor, run_off: torch.Tensor, splits: list[int], grad_in: torch.Tensor,

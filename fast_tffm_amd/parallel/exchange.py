@@ -887,15 +887,78 @@ class DPExchange(_Base):
 
 
 class DPDenseExchange(DPExchange):
-    """Replicated table; dense all-reduce of a [vocab, Kp+4] gradient buffer (small vocabularies)."""
+    """Replicated table; dense all-reduce of a [vocab, Kp+4] gradient buffer (small vocabularies,
+    BASELINE config 3).
+
+    GPU step (no host synchronisation, lookahead dedup as in the local step):
+      dedup of this batch (side stream, done during the previous step) -> forward on the
+      replica -> backward in EMIT_TABLE mode: each unique row's [g_v | g_w | 1] is scattered
+      straight into the persistent dense buffer ``G`` (the touch word marks it) -> all-reduce of
+      ``G`` over the ranks (RCCL ring / tree over xGMI; ``comm_dtype = bf16`` halves the bytes)
+      -> ``dense_apply``: every touched row gets one optimizer step on every replica (identical
+      inputs -> identical replicas) and is zeroed in ``G``, so ``G`` is never cleared wholesale.
+    The CPU (gloo) path keeps the plain-torch reference (gather, index_copy, nonzero)."""
+
+    supports_lookahead = True
 
     def __init__(self, model):
         super().__init__(model)
         V = model.table.rows
         self.dense = torch.zeros((V, self.gs), dtype=torch.float32, device=self.dev)
         self.arange = torch.arange(V + 1, dtype=torch.int32, device=self.dev)
+        self.wire16 = (torch.empty((V, self.gs), dtype=torch.bfloat16, device=self.dev)
+                       if self.dev.type == "cuda" and model.cfg.comm_dtype == "bf16" else None)
 
-    def train_step(self, b: Batch):
+    def close(self) -> None:
+        self.dense = self.wire16 = None
+        super().close()
+
+    def train_step(self, b: Batch, next_batch: Batch | None = None, next2: Batch | None = None):
+        from ..models.fm import StepOut
+
+        if self.dev.type != "cuda":
+            return self._train_step_reference(b)
+        m, ws, cfg, Kp = self.m, self.m.ws, self.m.cfg, self.Kp
+        main = torch.cuda.current_stream(self.dev)
+        nb_ready = None
+        if next_batch is not None and getattr(next_batch, "ready", None) is None:
+            nb_ready = torch.cuda.Event()
+            nb_ready.record(main)
+        pl = m._lpending
+        if pl is not None and pl.b is b:
+            m._lpending = None
+        else:
+            pl = m._local_plan(b)
+        main.wait_event(pl.ready)
+        with roctx_range("fwd"):
+            fo = K.fm_forward(b.offsets, pl.rows, b.vals, m.table.v, m.table.w, Kp, labels=b.labels,
+                              weights=b.weights, loss=cfg.loss_type, grad_scale=m.grad_scale(b.B), want_r1=True,
+                              pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
+                              bias=m.gbias)
+            m.bias_step(fo.dpred)
+        rv, rw = m.reg_coeffs
+        with roctx_range("bwd_scatter"):
+            K.fm_backward(pl.dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT_TABLE, table=m.table.state,
+                          grad_out=self.dense, reg_v=rv, reg_w=rw, partial=ws.bwd_partial,
+                          dense_part=ws.dense_part, dense_stream=m._dense_stream())
+        done = torch.cuda.Event()
+        done.record(main)
+        m._lslots[pl.slot].done = done
+        if next_batch is not None:
+            m._lpending = m._local_plan(next_batch, nb_ready)
+        if self.W > 1:
+            with roctx_range("allreduce_grads"):
+                if self.wire16 is not None:
+                    self.wire16.copy_(self.dense)
+                    dist.all_reduce(self.wire16, group=self.group)
+                    self.dense.copy_(self.wire16)
+                else:
+                    dist.all_reduce(self.dense, group=self.group)
+        with roctx_range("dense_apply"):
+            K.dense_apply(self.dense, m.table.state, cfg.opt, Kp, sr_counter=m.sr_tick())
+        return StepOut(fo.loss_sum, b.B)
+
+    def _train_step_reference(self, b: Batch):
         from ..models.fm import StepOut
 
         fo, uniq, grad = self._local_grads(b)
@@ -904,7 +967,8 @@ class DPDenseExchange(DPExchange):
         idx = uniq.to(torch.int64)
         dense.index_copy_(0, idx, grad)
         dense[idx, self.Kp + 1] = 1.0  # touch counter travels in a pad column
-        dist.all_reduce(dense, group=self.group)
+        if self.W > 1:
+            dist.all_reduce(dense, group=self.group)
         touched = torch.nonzero(dense[:, self.Kp + 1] > 0).flatten().to(torch.int32)
         T = touched.numel()
         dd = K.DedupOut(n=T, uniq=touched, perm=touched, seg_start=self.arange[: T + 1],
