@@ -84,7 +84,11 @@ struct BwdArgs {
   const int* dense_list;    // [kMaxDense] dense rows (dedup), counts[3] of them; null: no dense path
   float* dense_part;        // [gridDim(dense) * kMaxDense, Kp + 4] per-workgroup partial rows
   int nex;                  // examples in the batch (dense path)
+  const uint8_t* dense_A;   // [nex, kMaxDense] occurrence counts of the dense rows (written by the forward)
+  int cold_split;           // 1: chunks of <= kColdMax occurrences go to fm_bwd_cold_kernel, the chunk kernel skips them
 };
+
+constexpr int kColdMax = 4;  // occurrences of a "cold" chunk
 
 // Parameter row + optimizer slots of one segment, read before its gradient is
 // known so that the loads overlap the occurrence reduction.
@@ -289,6 +293,7 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
     }
     if (dense) continue;  // gradient from the MFMA path (fm_bwd_dense_kernel)
     const int len = j1 - j0;
+    if (a.cold_split && len <= kColdMax) continue;  // fm_bwd_cold_kernel's
     RowState<EPL> rs;
     if (single) bwd_load_row<TV, EPL>(a, a.mode == kBwdEmit ? (long long)u : (long long)key, tE, rs);
     // lane-parallel prefetch of the chunk's (example, dpred*x, x)
@@ -427,6 +432,94 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
   }
 }
 
+// Cold chunks (<= kColdMax occurrences: 341k of the 510k chunks of a Criteo-shaped batch,
+// mostly rows that occur once) in a kernel of their own.  Such a chunk is a chain of
+// dependent loads (descriptor -> occurrence -> dpred / r1 row) plus one table-row
+// read-modify-write, with almost nothing to compute: the chunk kernel's 8-deep r1
+// unroll and its 133 VGPRs (3 waves / SIMD) leave too few of them in flight to cover
+// the latency.  This kernel keeps 4 r1 rows and one row state per lane group, runs at
+// twice the occupancy and pipelines the next chunk's descriptor.  Same summation order
+// as the chunk kernel's short-chunk path (bitwise identical results).
+template <int LPR, typename TV>
+__global__ __launch_bounds__(kBlock) void fm_bwd_cold_kernel(BwdArgs a) {
+  const uint32_t sr = sr_step_seed(a.sr_counter);
+  constexpr int EPL = Frag<TV>::N;
+  constexpr int G = kWave / LPR;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPR, t = lane % LPR;
+  const int gbase = g * LPR;
+  const int nv = a.Kp / EPL;
+  const bool tact = t < nv;
+  const int tE = tact ? t : nv - 1;
+  const int nchunks = a.counts[1];
+  const int stride = gridDim.x * kWavesPerBlock * G;
+  int ii = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g;
+  int d_j0 = 0, d_j1 = 0;
+  if (ii < nchunks) { d_j0 = a.chunk_start[ii]; d_j1 = a.chunk_start[ii + 1]; }
+  for (; ii < nchunks; ii += stride) {
+    const int c = ii, j0 = d_j0, j1 = d_j1;
+    if (ii + stride < nchunks) { d_j0 = a.chunk_start[ii + stride]; d_j1 = a.chunk_start[ii + stride + 1]; }
+    const int len = j1 - j0;
+    if (len > kColdMax) continue;
+    const int seg = a.chunk_seg[c];
+    if (seg & kChunkDense) continue;
+    const int u = seg & kChunkSegMask;
+    const bool single = (unsigned)seg & kChunkSingle;
+    RowState<EPL> rs;
+    if (single) bwd_load_row<TV, EPL>(a, a.mode == kBwdEmit ? (long long)u : (long long)a.chunk_key[c], tE, rs);
+    int pex = 0;
+    float pc = 0.f, px = 0.f;
+    if (t < len) {
+      const int jj = j0 + t;
+      pex = a.sorted_ex[jj] >> a.ex_shift;
+      px = a.sorted_x ? a.sorted_x[jj] : 1.f;
+      pc = a.dpred[pex] * px;
+    }
+    float rr[kColdMax][EPL], cc[kColdMax], xx[kColdMax];
+#pragma unroll
+    for (int uu = 0; uu < kColdMax; ++uu) {
+      const bool ok = uu < len;
+      const int src = gbase + (ok ? uu : 0);
+      const int ex = __shfl(pex, src, kWave);
+      const float cs = __shfl(pc, src, kWave);
+      cc[uu] = ok ? cs : 0.f;
+      xx[uu] = __shfl(px, src, kWave);
+      const float* rp = a.r1 + (long long)ex * a.Kp + tE * EPL;
+#pragma unroll
+      for (int k = 0; k < EPL; k += 4) {
+        const float4 f = *reinterpret_cast<const float4*>(rp + k);
+        rr[uu][k] = f.x; rr[uu][k + 1] = f.y; rr[uu][k + 2] = f.z; rr[uu][k + 3] = f.w;
+      }
+    }
+    float A[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) A[k] = 0.f;
+    float Scx = 0.f, Sc = 0.f;
+#pragma unroll
+    for (int uu = 0; uu < kColdMax; ++uu) {
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) A[k] += cc[uu] * rr[uu][k];
+      Scx += cc[uu] * xx[uu];
+      Sc += cc[uu];
+    }
+    if (single) {
+      bwd_finish<LPR, TV, EPL>(a, u, t, tact, rs, A, Scx, Sc, len, sr);
+    } else {
+      float* dst = a.partial + (long long)c * (a.Kp + 4);
+      if (tact) {
+#pragma unroll
+        for (int k = 0; k < EPL; k += 4)
+          *reinterpret_cast<float4*>(dst + t * EPL + k) = make_float4(A[k], A[k + 1], A[k + 2], A[k + 3]);
+      }
+      if (t == 0) {
+        dst[a.Kp] = Scx;
+        dst[a.Kp + 1] = Sc;
+        if (seg & kChunkFirst) a.multi[atomicAdd(&a.counts_rw[2], 1)] = u;
+      }
+    }
+  }
+}
+
 // Rows split over 2..kSmallChunks chunks: one lane group, ordered sum of the partials.
 // Hotter rows are appended to big_list for fm_bwd_big_kernel.
 template <int LPR, typename TV>
@@ -557,138 +650,157 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_big_kernel(BwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Dense rows on the matrix cores.  The hottest rows (>= dense_min occurrences,
-// e.g. the values of Criteo's low-cardinality fields, each present in 5-60% of
-// the examples) make the occurrence-gather backward pay one r1 row per
-// occurrence.  For them the reduction is a dense GEMM instead:
-//     G[h, :] = sum_e A[e, h] * dpred_e * r1_e,   A[e, h] = sum of x over the
-// occurrences of dense row h in example e,
-// computed per 64-example tile with v_mfma_f32_16x16x4_f32 (exact fp32): each
-// workgroup owns a contiguous example range, builds A (64 x 128) in LDS from the
-// rows' sorted occurrence lists (one thread per dense row, a cursor per row),
-// stages D = dpred * r1 (64 x Kp, coalesced) in LDS and accumulates G in AGPR/VGPR
-// accumulators across its tiles.  r1 is read once, coalesced, instead of once
-// per occurrence.  Partial G rows are summed over workgroups in a fixed order
-// by fm_bwd_dense_apply_kernel, which then applies the optimizer.
+// Dense rows on the matrix cores.  The hottest rows of a batch (the values of
+// Criteo's low-cardinality fields: the 256 densest cover ~47% of a Criteo-shaped
+// batch's occurrences, each present in >= 2.5% of the examples) make the
+// occurrence-gather backward fetch one random r1 row per occurrence.  For them the
+// reduction is a GEMM over example tiles instead:
+//     G[h, :] = sum_e A[e, h] * D[e, :],   D[e, :] = dpred_e * r1_e,
+// with A[e, h] = occurrences of dense row h in example e (binary features, so
+// x = 1; counted by the forward kernel into a coalesced [B, 256] byte matrix).
+// Each workgroup owns a contiguous example range and streams it in 64-example
+// tiles: A^T and D are staged in LDS as bf16 images transposed so that every MFMA
+// operand fragment is one 16-byte read, and the product runs on
+// v_mfma_f32_16x16x32_bf16 with D split into three bf16 parts (hi + mid + lo carry
+// D's 24-bit mantissa; A's small integer counts are exact in bf16), accumulated in
+// fp32: the result matches an fp32 GEMM to fp32 accumulation error at 3/16 of the
+// fp32-MFMA cost.  r1 is read once, coalesced, instead of once per occurrence.
+// Per-workgroup partial rows are summed in a fixed order by
+// fm_bwd_dense_apply_kernel, which applies the optimizer (deterministic).
 // ---------------------------------------------------------------------------
-constexpr int kDenseE = 64;                 // examples per tile (the MFMA reduction dim)
-constexpr int kDenseAS = kMaxDense + 16;     // A row stride in LDS (floats): rows 16 banks apart
-constexpr int kDenseWG = 256;               // workgroups of the dense kernel (one per CU)
+constexpr int kDenseE = 64;                 // examples per staged tile (2 MFMA k-steps of 32)
+constexpr int kDenseEP = kDenseE + 8;       // LDS row pitch in bf16 (144 B: conflict-free 16-B fragment reads)
+constexpr int kDenseWG = 256;               // workgroups of the dense kernel (partial rows)
+static_assert(kMaxDense == 4 * kWave, "dense rows: 4 per lane in the forward's count rows, 64 per wave here");
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
 
 template <int NB>  // 16-column blocks of Kp (Kp <= NB * 16)
 __global__ __launch_bounds__(kBlock) void fm_bwd_dense_kernel(BwdArgs a) {
-  constexpr int DS = NB * 16 + 16;   // D row stride in LDS (floats)
-  __shared__ float As[kDenseE * kDenseAS];
-  __shared__ float Ds[kDenseE * DS];
+  __shared__ __align__(16) uint16_t At[kMaxDense * kDenseEP];      // A^T tile: [dense row][example]
+  __shared__ __align__(16) uint16_t Dt[3 * NB * 16 * kDenseEP];    // D^T tile, 3 bf16 parts: [part][col][example]
   __shared__ float dps[kDenseE];
   const int nd = min(a.counts[3], kMaxDense);
   if (nd == 0) return;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid >> 6;
   const int per = ((a.nex + (int)gridDim.x - 1) / (int)gridDim.x + kDenseE - 1) / kDenseE * kDenseE;
   const int e_begin = blockIdx.x * per, e_end = min(a.nex, e_begin + per);
-  // thread h < nd walks dense row h's occurrences (sorted by example) from e_begin on
-  int cur = 0, cend = 0;
-  float sc = 0.f, scx = 0.f;
-  if (tid < nd) {
-    const int u = a.dense_list[tid];
-    int lo = a.seg_start[u], hi = a.seg_start[u + 1];
-    cend = hi;
-    // occurrences are spread ~uniformly over the examples: probe a window around the
-    // interpolated position first, then finish with a binary search inside it
-    const int len = hi - lo;
-    const int guess = lo + (int)((long long)len * e_begin / max(a.nex, 1));
-    const int win = 2 * (int)sqrtf((float)len) + 32;
-    const int wlo = max(lo, guess - win), whi = min(hi, guess + win);
-    if (wlo > lo && (a.sorted_ex[wlo] >> a.ex_shift) < e_begin) lo = wlo;
-    if (whi < hi && (a.sorted_ex[whi] >> a.ex_shift) >= e_begin) hi = whi;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if ((a.sorted_ex[mid] >> a.ex_shift) < e_begin) lo = mid + 1; else hi = mid;
-    }
-    cur = lo;
-  }
-  floatx4 acc[2][NB];
+  floatx4 acc[4][NB];
 #pragma unroll
-  for (int mb = 0; mb < 2; ++mb)
+  for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const int kq = a.Kp / 4;  // float4 columns of r1
+    for (int nb = 0; nb < NB; ++nb) acc[rb][nb] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float sc = 0.f;  // thread tid = dense row h: sum_e A[e, h] * dpred_e (= Sc = Scx for x = 1)
+  const int kq = a.Kp / 4;
   for (int e0 = e_begin; e0 < e_end; e0 += kDenseE) {
-    for (int i = tid; i < kDenseE * kDenseAS; i += kBlock) As[i] = 0.f;
-    for (int i = tid; i < kDenseE * NB * 4; i += kBlock) {
-      const int e = i / (NB * 4), q = i % (NB * 4), ex = e0 + e;
-      float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ex < e_end && q < kq) {
-        const float d = a.dpred[ex];
-        f = *reinterpret_cast<const float4*>(a.r1 + (long long)ex * a.Kp + 4 * q);
-        f.x *= d; f.y *= d; f.z *= d; f.w *= d;
+    // Staging writes pack two examples into one dword (lanes 0-31: consecutive example
+    // pairs -> consecutive dwords; lanes 32-63: rows 8 apart = 288 dwords = +32 banks), so
+    // every ds_write_b32 wave instruction is bank-conflict free.  (The first version wrote
+    // one bf16 per ds_write_b16 with 16 rows of one wave on one bank: 215 us for this kernel,
+    // profiles/r2/timeline_dense_v1.txt.)
+    const int ep = lane & 31, half = lane >> 5;
+    const int ea = e0 + 2 * ep, eb = ea + 1;
+    // A^T: wave wv, pass it: dense rows 16 q .. 16 q + 15 with q = 4 it + wv; 8 of them per lane
+    for (int it = 0; it < kMaxDense / 64; ++it) {
+      const int q = 4 * it + wv;
+      const int hb = 16 * q + 8 * half;
+      uint2 ca = make_uint2(0u, 0u), cb = make_uint2(0u, 0u);
+      if (ea < e_end) ca = *reinterpret_cast<const uint2*>(a.dense_A + (long long)ea * kMaxDense + hb);
+      if (eb < e_end) cb = *reinterpret_cast<const uint2*>(a.dense_A + (long long)eb * kMaxDense + hb);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t xa = ((j < 4 ? ca.x : ca.y) >> (8 * (j & 3))) & 0xffu;
+        const uint32_t xb = ((j < 4 ? cb.x : cb.y) >> (8 * (j & 3))) & 0xffu;
+        const uint32_t pk = f32_to_bf16_bits((float)xa) | (f32_to_bf16_bits((float)xb) << 16);  // exact
+        *reinterpret_cast<uint32_t*>(At + (hb + j) * kDenseEP + 2 * ep) = pk;
       }
-      *reinterpret_cast<float4*>(Ds + e * DS + 4 * q) = f;
+    }
+    // D^T = (dpred * r1)^T as hi / mid / lo bf16 parts: lane = (example pair, column quad);
+    // the two lane halves take column quads 2 apart (rows 8 apart)
+    for (int cq = wv; cq < 2 * NB; cq += kWavesPerBlock) {  // pairs of column quads {4c+0|4c+2, ...}
+      const int qd = (cq / 2) * 4 + (cq & 1) + 2 * half;     // column quad: columns 4 qd .. 4 qd + 3
+      float fa[4] = {0.f, 0.f, 0.f, 0.f}, fb[4] = {0.f, 0.f, 0.f, 0.f};
+      if (qd < kq) {
+        if (ea < e_end) {
+          const float d = a.dpred[ea];
+          const float4 r = *reinterpret_cast<const float4*>(a.r1 + (long long)ea * a.Kp + 4 * qd);
+          fa[0] = d * r.x; fa[1] = d * r.y; fa[2] = d * r.z; fa[3] = d * r.w;
+        }
+        if (eb < e_end) {
+          const float d = a.dpred[eb];
+          const float4 r = *reinterpret_cast<const float4*>(a.r1 + (long long)eb * a.Kp + 4 * qd);
+          fb[0] = d * r.x; fb[1] = d * r.y; fb[2] = d * r.z; fb[3] = d * r.w;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = 4 * qd + j;
+        if (n >= NB * 16) continue;
+        uint32_t pa[3], pb[3];
+        {
+          pa[0] = f32_to_bf16_bits(fa[j]);
+          const float r = fa[j] - bf16_bits_to_f32(pa[0]);
+          pa[1] = f32_to_bf16_bits(r);
+          pa[2] = f32_to_bf16_bits(r - bf16_bits_to_f32(pa[1]));
+        }
+        {
+          pb[0] = f32_to_bf16_bits(fb[j]);
+          const float r = fb[j] - bf16_bits_to_f32(pb[0]);
+          pb[1] = f32_to_bf16_bits(r);
+          pb[2] = f32_to_bf16_bits(r - bf16_bits_to_f32(pb[1]));
+        }
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          *reinterpret_cast<uint32_t*>(Dt + ((p * NB * 16) + n) * kDenseEP + 2 * ep) = pa[p] | (pb[p] << 16);
+      }
     }
     if (tid < kDenseE) dps[tid] = e0 + tid < e_end ? a.dpred[e0 + tid] : 0.f;
     __syncthreads();
-    if (tid < nd) {
-      // 16 upcoming occurrences of the row per round trip (the densest rows have ~40
-      // per tile; a dependent load per occurrence would serialise on memory latency)
-      const int lim = min(e0 + kDenseE, e_end);
-      for (;;) {
-        int exs[16];
-        float xs[16];
+    if (tid < nd) {  // 16-byte reads of the row (16 rows per lane group: conflict free)
+      const bf16x8* row = reinterpret_cast<const bf16x8*>(At + tid * kDenseEP);
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int idx = cur + q;
-          const bool ok = idx < cend;
-          const int li = ok ? idx : cend - 1;  // loads stay inside the row (cend > seg start here)
-          exs[q] = ok ? (a.sorted_ex[li] >> a.ex_shift) : 0x7fffffff;
-          xs[q] = a.sorted_x ? a.sorted_x[li] : 1.f;
-        }
-        int taken = 0;
+      for (int c8 = 0; c8 < kDenseE / 8; ++c8) {
+        const bf16x8 v8 = row[c8];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          if (exs[q] < lim) {  // ascending: the taken ones are a prefix
-            As[(exs[q] - e0) * kDenseAS + tid] += xs[q];  // column tid: this thread only
-            const float c = dps[exs[q] - e0] * xs[q];
-            sc += c;
-            scx += c * xs[q];
-            ++taken;
-          }
-        }
-        cur += taken;
-        if (taken < 16) break;
+        for (int j = 0; j < 8; ++j) sc += bf16_bits_to_f32((uint16_t)v8[j]) * dps[8 * c8 + j];
       }
     }
-    __syncthreads();
-    // G[m, n] += sum_e A[e, m] D[e, n]; wave wv owns rows 32 wv .. 32 wv + 31
-#pragma unroll 4
-    for (int kk = 0; kk < kDenseE; kk += 4) {
-      const int e = kk + (lane >> 4);
-      const float a0 = As[e * kDenseAS + (2 * wv) * 16 + (lane & 15)];
-      const float a1 = As[e * kDenseAS + (2 * wv + 1) * 16 + (lane & 15)];
+    // G[h, n] += sum_e A^T[h, e] D^T[n, e]; wave wv owns dense rows 64 wv .. 64 wv + 63
+#pragma unroll
+    for (int ks = 0; ks < kDenseE / 32; ++ks) {
+      const int kofs = 32 * ks + 8 * (lane >> 4);
+      bf16x8 af[4];
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+        af[rb] = *reinterpret_cast<const bf16x8*>(At + (64 * wv + 16 * rb + (lane & 15)) * kDenseEP + kofs);
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) {
-        const float b = Ds[e * DS + nb * 16 + (lane & 15)];
-        acc[0][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b, acc[0][nb], 0, 0, 0);
-        acc[1][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b, acc[1][nb], 0, 0, 0);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(Dt + ((p * NB + nb) * 16 + (lane & 15)) * kDenseEP + kofs);
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb)
+            acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[rb], bfr, acc[rb][nb], 0, 0, 0);
+        }
       }
     }
     __syncthreads();
   }
-  // partial rows: C/D map of 16x16 MFMA tiles: col = lane & 15, row = (lane >> 4) * 4 + i
+  // partial rows: C/D map of the 16x16 tiles: col = lane & 15, row = (lane >> 4) * 4 + i
   const int PS = a.Kp + 4;
   float* part = a.dense_part + (long long)blockIdx.x * kMaxDense * PS;
 #pragma unroll
-  for (int mb = 0; mb < 2; ++mb)
+  for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int m = (2 * wv + mb) * 16 + (lane >> 4) * 4 + i, n = nb * 16 + (lane & 15);
-        if (m < nd && n < a.Kp) part[(long long)m * PS + n] = acc[mb][nb][i];
+        const int m = 64 * wv + 16 * rb + (lane >> 4) * 4 + i, n = nb * 16 + (lane & 15);
+        if (m < nd && n < a.Kp) part[(long long)m * PS + n] = acc[rb][nb][i];
       }
   if (tid < nd) {
-    part[(long long)tid * PS + a.Kp] = scx;
+    part[(long long)tid * PS + a.Kp] = sc;
     part[(long long)tid * PS + a.Kp + 1] = sc;
   }
 }
@@ -762,7 +874,7 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
     (void)hipMemsetAsync(a.counts_rw + 2, 0, sizeof(int), st);  // #multi-chunk rows, appended by the chunk kernel
   }
   const int g1 = (fill_grid(max_chunks, kWavesPerBlock * G) + 7) / 8 * 8;  // multiple of 8: XCD groups
-  const bool dense = a.dense_list && a.dense_part && a.piece < 0;
+  const bool dense = a.dense_list && a.dense_part && a.dense_A && a.piece < 0;
   if (a.piece >= 0 && (a.n_owners > kMaxPieceOwners || a.slice_list)) return -6;
   const bool fork = dense && dense_st && dense_st != st;
   hipStream_t ds = fork ? dense_st : st;
@@ -784,7 +896,16 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
     }
     if (fork) (void)hipEventRecord(dense_join_event(), ds);
   }
-  FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, a);
+  // cold chunks in their own kernel (full-batch walks only: not with the sliced schedule or
+  // split-backward pieces); opt-in (a.cold_split, FM_COLD_SPLIT=1): measured slower (k64 fp32
+  // 0.667 -> 0.705 ms, k128 fp8 FTRL 0.973 -> 1.081 ms; profiles/r2/cold_split_ab.txt)
+  BwdArgs ac = a;
+  ac.cold_split = a.cold_split && a.piece < 0 && !a.slice_list && lpr >= kColdMax ? 1 : 0;
+  if (ac.cold_split) {
+    const int gc = fill_grid(max_chunks, kWavesPerBlock * G, 16384);
+    FM_DISPATCH(dtype, lpr, fm_bwd_cold_kernel, gc, st, ac);
+  }
+  FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, ac);
   const int g2 = fill_grid(max_unique, kWavesPerBlock * G, 2048);
   FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, a);
   FM_DISPATCH(dtype, lpr, fm_bwd_big_kernel, 1024, st, a);

@@ -33,7 +33,30 @@ struct FwdArgs {
   float* loss_partial;  // [gridDim.x] or nullptr
   float* reg_partial;   // [2*gridDim.x] (sum |v|^2, sum w^2) or nullptr
   const float* bias;    // [1] global bias (optional model extension) or nullptr
+  // Dense-row occurrence matrix for the MFMA backward (fm_bwd.hip): the forward already
+  // walks every example's rows, so it counts, per example, the occurrences of each of the
+  // batch's dense rows (listed by the dedup, which ran before this forward) and writes them
+  // as one coalesced kMaxDense-byte row.  Null dense_A: off.
+  const int* dense_list;   // [kMaxDense] segment ids of the dense rows
+  const int* dense_uniq;   // segment -> row key (local step: uniq = table rows) or null (rows ARE segment ids)
+  const int* dense_count;  // device scalar: number of dense rows (capped at kMaxDense here)
+  uint8_t* dense_A;        // [B, kMaxDense] occurrence counts (saturated at 255)
 };
+
+constexpr int kDenseHash = 4 * kMaxDense;  // open-addressing table of the dense keys (LDS, load <= 1/4)
+
+__device__ inline int dense_hash(int key) { return (int)(((uint32_t)key * 0x9E3779B1u) >> 22) & (kDenseHash - 1); }
+
+__device__ inline int dense_probe(const int* hkey, const int* hval, int key) {
+  int slot = dense_hash(key);
+  for (int p = 0; p < kDenseHash; ++p) {
+    const int k = hkey[slot];
+    if (k == key) return hval[slot];
+    if (k == -1) return -1;
+    slot = (slot + 1) & (kDenseHash - 1);
+  }
+  return -1;
+}
 
 // Rows of one example kept in flight per lane group: enough to cover a
 // Criteo-shaped example (39 features) in one round for K=64 (G=4 -> 10 row
@@ -76,6 +99,26 @@ void fm_fwd_kernel(FwdArgs a) {
   const int nwaves = gridDim.x * kWavesPerBlock;
   const bool want_reg = a.reg_partial != nullptr;
 
+  // dense rows: key -> dense index hash (built once per workgroup) and per-wave counters
+  __shared__ int hkey[kDenseHash], hval[kDenseHash];
+  __shared__ unsigned dcnt[kWavesPerBlock][kMaxDense];
+  const bool dense = a.dense_A != nullptr;
+  const int wv = threadIdx.x >> 6;
+  if (dense) {
+    const int nd = min(*a.dense_count, kMaxDense);
+    for (int k = threadIdx.x; k < kDenseHash; k += kBlock) hkey[k] = -1;
+    for (int k = threadIdx.x; k < kWavesPerBlock * kMaxDense; k += kBlock) (&dcnt[0][0])[k] = 0u;
+    __syncthreads();
+    for (int h = threadIdx.x; h < nd; h += kBlock) {
+      const int sg = a.dense_list[h];
+      const int key = a.dense_uniq ? a.dense_uniq[sg] : sg;
+      int slot = dense_hash(key);
+      while (atomicCAS(&hkey[slot], -1, key) != -1) slot = (slot + 1) & (kDenseHash - 1);
+      hval[slot] = h;  // (keys are distinct; read only after the barrier)
+    }
+    __syncthreads();
+  }
+
   float loss_acc = 0.f, regv_acc = 0.f, regw_acc = 0.f;
   for (int i = wave; i < a.B; i += nwaves) {
     const int s = a.offsets[i], e = a.offsets[i + 1];
@@ -99,6 +142,10 @@ void fm_fwd_kernel(FwdArgs a) {
       }
       lin += my_x * my_w;
       if (want_reg) rw += my_w * my_w;
+      if (dense && lane < m) {
+        const int h = dense_probe(hkey, hval, my_row);
+        if (h >= 0) atomicAdd(&dcnt[wv][h], 1u);  // integer: order-independent
+      }
       for (int q = 0; q < m; q += G * UNR) {
         float fr[UNR][EPL], fx[UNR], fs[UNR];
         // Issue every row load of the round before the first use.  Loads are
@@ -134,6 +181,18 @@ void fm_fwd_kernel(FwdArgs a) {
           }
         }
       }
+    }
+    if (dense) {  // flush this example's dense-row counts: 4 per lane, one coalesced row
+      // (LDS instructions of one wave complete in issue order, and the compiler keeps these
+      // reads after the possibly-aliasing atomics above)
+      uint32_t packed = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        unsigned c = dcnt[wv][4 * lane + j];
+        dcnt[wv][4 * lane + j] = 0u;
+        packed |= (c > 255u ? 255u : c) << (8 * j);
+      }
+      reinterpret_cast<uint32_t*>(a.dense_A + (long long)i * kMaxDense)[lane] = packed;
     }
     float part = 0.f;
 #pragma unroll
@@ -179,7 +238,6 @@ void fm_fwd_kernel(FwdArgs a) {
   }
   if (a.loss_partial == nullptr && a.reg_partial == nullptr) return;
   __shared__ float red[3][kWavesPerBlock];
-  const int wv = threadIdx.x >> 6;
   if (lane == 0) {
     red[0][wv] = loss_acc;
     red[1][wv] = regv_acc;

@@ -70,8 +70,12 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       "fwd",
       [](int B, u64 offsets, u64 rows, u64 vals, u64 v, long long v_stride, u64 w, long long w_stride, int Kp,
          int dtype, u64 labels, u64 weights, int loss_type, float grad_scale, u64 pred, u64 r1, u64 dpred,
-         u64 loss_partial, u64 reg_partial, int grid, u64 stream, u64 bias) {
+         u64 loss_partial, u64 reg_partial, int grid, u64 stream, u64 bias, u64 dense_list, u64 dense_uniq,
+         u64 dense_count, u64 dense_A) {
         fm::FwdArgs a{};
+        a.dense_list = P<const int>(dense_list); a.dense_uniq = P<const int>(dense_uniq);
+        a.dense_count = P<const int>(dense_count); a.dense_A = P<uint8_t>(dense_A);
+        if (a.dense_A && (!a.dense_list || !a.dense_count)) throw std::runtime_error("fm_fwd: dense_A needs the dense list");
         a.B = B; a.offsets = P<const int>(offsets); a.rows = P<const int>(rows);
         a.vals = P<const float>(vals); a.v = P<const void>(v); a.v_stride = v_stride;
         a.w = P<const float>(w); a.w_stride = w_stride; a.Kp = Kp;
@@ -84,7 +88,8 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("B"), py::arg("offsets"), py::arg("rows"), py::arg("vals"), py::arg("v"), py::arg("v_stride"),
       py::arg("w"), py::arg("w_stride"), py::arg("Kp"), py::arg("dtype"), py::arg("labels"), py::arg("weights"),
       py::arg("loss_type"), py::arg("grad_scale"), py::arg("pred"), py::arg("r1"), py::arg("dpred"),
-      py::arg("loss_partial"), py::arg("reg_partial"), py::arg("grid"), py::arg("stream"), py::arg("bias") = 0);
+      py::arg("loss_partial"), py::arg("reg_partial"), py::arg("grid"), py::arg("stream"), py::arg("bias") = 0,
+      py::arg("dense_list") = 0, py::arg("dense_uniq") = 0, py::arg("dense_count") = 0, py::arg("dense_A") = 0);
 
   m.def(
       "bwd",
@@ -95,8 +100,10 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
          u64 big_list, u64 big_count, u64 multi, u64 slice_list, u64 slice_start, int nslices, u64 dense_list,
          u64 dense_part, int nex, u64 dense_stream, int dtype,
          long long max_chunks, long long max_unique, u64 stream, int g_wcol, int g_bf16, u64 sr_counter,
-         int counters_ready, u64 seg_bounds, int piece, int n_owners) {
+         int counters_ready, u64 seg_bounds, int piece, int n_owners, u64 dense_A, int cold_split) {
         fm::BwdArgs a{};
+        a.dense_A = P<const uint8_t>(dense_A);
+        a.cold_split = cold_split;
         a.counters_ready = counters_ready;
         a.seg_bounds = P<const int>(seg_bounds); a.piece = piece; a.n_owners = n_owners;
         a.sr_counter = P<const int>(sr_counter);
@@ -129,7 +136,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("dense_part"), py::arg("nex"), py::arg("dense_stream"), py::arg("dtype"),
       py::arg("max_chunks"), py::arg("max_unique"), py::arg("stream"), py::arg("g_wcol") = -1,
       py::arg("g_bf16") = 0, py::arg("sr_counter") = 0, py::arg("counters_ready") = 0, py::arg("seg_bounds") = 0,
-      py::arg("piece") = -1, py::arg("n_owners") = 0);
+      py::arg("piece") = -1, py::arg("n_owners") = 0, py::arg("dense_A") = 0, py::arg("cold_split") = 0);
 
   m.def("dedup_workspace_bytes", &fm::dedup_workspace_bytes, py::arg("n"));
 

@@ -100,6 +100,9 @@ class _Workspace:
             self.pred = torch.empty(cap, dtype=torch.float32, device=dev)
             self.dpred = torch.empty(cap, dtype=torch.float32, device=dev)
             self.r1 = torch.empty((cap, Kp), dtype=torch.float32, device=dev)
+            # dense-row occurrence counts (forward -> MFMA backward), GPU only
+            self._dense_A = (torch.empty((cap, K.MAX_DENSE), dtype=torch.uint8, device=dev)
+                             if dev.type == "cuda" else None)
             self.cap_b = cap
         if nnz > self.cap_n:
             cap = max(nnz, int(self.cap_n * 1.25), 1)
@@ -113,6 +116,13 @@ class _Workspace:
                                if dev.type == "cuda" and Kp <= 128 else None)
         if not hasattr(self, "fwd_partial"):
             self.fwd_partial = torch.zeros(3 * 4096, dtype=torch.float32, device=dev)
+
+    def dense_counts(self, B: int) -> torch.Tensor:
+        """[B, MAX_DENSE] uint8 dense-row occurrence counts (written by the forward, read by the
+        MFMA backward), grown on demand."""
+        if B > self.cap_b:
+            self.ensure(B, 0)
+        return self._dense_A[:B]
 
 
 class _LocalSlot:
@@ -490,7 +500,7 @@ class FactorizationMachine:
                 ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz, slot_bits=sb)
                 dd = K.dedup(rows, ws=ws.dd, key_bits=bits_for(self.table.rows), ex_of_occ=ex, vals=b.vals,
                              num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets,
-                             dense_min=K.dense_min_for(b.B, self.Kp, cfg.dedup_chunk))
+                             dense_min=0)  # (runs beside the forward, which counts dense rows: off here)
         else:
             ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz)
         with roctx_range("fwd"):
@@ -543,23 +553,25 @@ class FactorizationMachine:
         ex = K.csr_rows(b.offsets, out=slot.dd.ex_of_occ[: b.nnz], nnz=b.nnz, slot_bits=sb)
         dd = K.dedup(rows, ws=slot.dd, key_bits=bits_for(self.table.rows), ex_of_occ=ex, vals=b.vals,
                      num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets,
-                     dense_min=K.dense_min_for(b.B, self.Kp, cfg.dedup_chunk))
+                     dense_min=K.dense_min_for(b.B, self.Kp, cfg.dedup_chunk, has_vals=b.vals is not None,
+                                               max_feats=b.max_feats))
         return rows, dd
 
     def _fwd_bwd_local(self, b: Batch, rows: torch.Tensor, dd) -> StepOut:
         """Forward + loss + backward/update of ``b`` on the current stream (dedup ``dd`` ready)."""
         ws, cfg = self.ws, self.cfg
+        dA = ws.dense_counts(b.B) if dd.dense_list is not None else None
         with roctx_range("fwd"):
             fo = K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,
                               weights=b.weights, loss=cfg.loss_type, grad_scale=self.grad_scale(b.B), want_r1=True,
                               pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
-                              threads=cfg.threads, bias=self.gbias)
+                              threads=cfg.threads, bias=self.gbias, dense=dd, dense_A=dA)
             self.bias_step(fo.dpred)
         rv, rw = self.reg_coeffs
         with roctx_range("bwd+update"):
             K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
                           reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, dense_part=ws.dense_part,
-                          dense_stream=self._dense_stream(), sr_counter=self.sr_tick())
+                          dense_stream=self._dense_stream(), sr_counter=self.sr_tick(), dense_A=dA)
         return StepOut(fo.loss_sum, b.B)
 
     def _local_lookahead_step(self, b: Batch, next_batch: Batch | None) -> StepOut:

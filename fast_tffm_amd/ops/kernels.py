@@ -154,13 +154,19 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
                want_r1: bool = True, want_reg: bool = False, pred: torch.Tensor | None = None,
                r1: torch.Tensor | None = None, dpred: torch.Tensor | None = None,
                partial: torch.Tensor | None = None, threads: int = 0,
-               bias: torch.Tensor | None = None) -> FwdOut:
+               bias: torch.Tensor | None = None, dense: "DedupOut | None" = None,
+               dense_A: torch.Tensor | None = None, dense_by_segment: bool = False) -> FwdOut:
     """FM score of a CSR batch (reference FmScorer, cc/fm_scorer_op.h:101-140), fused with the loss.
 
     pred_i = sum_j x_j w_j + 1/2 sum_k [(sum_j x_j v_jk)^2 - sum_j x_j^2 v_jk^2]  (+ bias[0], optional
     global bias; the reference has none, fm_scorer_op.h:134-136)
     With ``loss`` in {mse, logistic} also returns the summed weighted loss and
     ``dpred = grad_scale * dL_i/dpred_i``.
+
+    ``dense`` (GPU, the batch's dedup with a dense-row list) and ``dense_A`` ([B, MAX_DENSE]
+    uint8): also count every example's occurrences of the dense rows into ``dense_A`` for the
+    MFMA backward; ``rows`` are table rows (``dense.uniq`` maps segments to them) or, with
+    ``dense_by_segment``, the segment ids themselves (the sharded step's inverse map).
     """
     dev = rows.device
     B = offsets.numel() - 1
@@ -196,11 +202,18 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
             partial = torch.zeros(3 * grid, dtype=torch.float32, device=dev)
         lp = partial[:grid]
         rp = partial[grid:3 * grid]
+        dkw = {}
+        if dense is not None and dense.dense_list is not None and dense_A is not None:
+            _check(vals is None, "dense-row counts are for binary-feature batches (vals is None)")
+            _check(dense_A.dtype == torch.uint8 and dense_A.is_contiguous() and dense_A.shape[1] == MAX_DENSE
+                   and dense_A.shape[0] >= B, "dense_A: contiguous uint8 [>= B, MAX_DENSE]")
+            dkw = dict(dense_list=_p(dense.dense_list), dense_uniq=0 if dense_by_segment else _p(dense.uniq),
+                       dense_count=_p(dense.counts) + 12, dense_A=_p(dense_A))
         h.fwd(B=B, offsets=_p(offsets), rows=_p(rows), vals=_p(vals), v=_p(v), v_stride=v_stride, w=_p(w),
               w_stride=w_stride, Kp=Kp, dtype=dt, labels=_p(labels), weights=_p(weights), loss_type=lt,
               grad_scale=float(grad_scale), pred=_p(pred), r1=_p(r1), dpred=_p(dpred) if lt else 0,
               loss_partial=_p(lp) if lt else 0, reg_partial=_p(rp) if want_reg else 0, grid=grid,
-              stream=_stream(rows), bias=_p(bias))
+              stream=_stream(rows), bias=_p(bias), **dkw)
         # (an in-kernel last-block reduction was measured slower: the per-block agent-scope
         # release fence writes back L2 -- fwd 211 -> 412 us; a separate reduce is ~10 us)
         loss_sum = lp.sum(dtype=torch.float32) if lt else None
@@ -312,20 +325,25 @@ def csr_rows(offsets: torch.Tensor, out: torch.Tensor | None = None, nnz: int | 
 
 
 MAX_SLICES = 64            # = fm::kMaxSlices (dedup.hip)
-MAX_DENSE = 128            # = fm::kMaxDense: rows on the MFMA backward path
+MAX_DENSE = 256            # = fm::kMaxDense: rows on the MFMA backward path
 DENSE_WG = 256             # = fm::kDenseWG: workgroups (partial rows) of the dense kernel
 
 
-def dense_min_for(num_examples: int, Kp: int, CH: int = 32) -> int:
+def dense_min_for(num_examples: int, Kp: int, CH: int = 32, *, has_vals: bool = False,
+                  max_feats: int = 0) -> int:
     """Occurrence threshold of the MFMA backward rows (0 = off).
 
-    A row present in >= ~4% of the batch's examples (>= B/24 occurrences) is
-    reduced as a dense GEMM over example tiles: below that density the MFMA
-    tile is mostly zeros and the occurrence gather is cheaper.  Needs Kp <= 128
-    (the tile's N) and a batch large enough to fill the 256 tile workgroups."""
-    if os.environ.get("FM_DENSE_BWD", "0") != "1" or Kp > 128 or Kp % 4 or num_examples < 16384:
+    A row present in >= 2.5% of the batch's examples (>= B/40 occurrences; the first
+    MAX_DENSE = 256 such rows in key order) is reduced as a GEMM over example tiles on the
+    matrix cores (fm_bwd.hip, fm_bwd_dense_kernel): on a Criteo-shaped batch those rows hold
+    ~47% of the occurrences, whose r1 rows the occurrence-gather backward would fetch one by
+    one.  Needs binary features (the forward counts occurrences: x = 1), fewer than 256
+    features per example (byte counts, exact in bf16), Kp <= 128 (the tile's N) and a batch
+    that fills the 256 tile workgroups.  Opt-in: FM_DENSE_BWD=1."""
+    if (os.environ.get("FM_DENSE_BWD", "0") != "1" or has_vals or Kp > 128 or Kp % 4 or num_examples < 16384
+            or max_feats > 255):
         return 0
-    return max(8 * CH, num_examples // 24)
+    return max(8 * CH, num_examples // 40)
 SLICE_BYTES = 2 << 20      # r1 bytes per example slice of the XCD-sliced backward (XCD L2 = 4 MB)
 
 
@@ -445,7 +463,8 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
                 partial: torch.Tensor | None = None, threads: int = 0,
                 dense_part: torch.Tensor | None = None, dense_stream=None,
                 grad_bf16: bool = False, sr_counter: torch.Tensor | None = None,
-                seg_bounds: torch.Tensor | None = None, piece: int = -1) -> torch.Tensor | None:
+                seg_bounds: torch.Tensor | None = None, piece: int = -1,
+                dense_A: torch.Tensor | None = None) -> torch.Tensor | None:
     """Segmented FM backward over the dedup grouping (reference FmGrad, cc/fm_grad_op.h:59-163).
 
     Per unique row u with occurrences (i, x):
@@ -507,7 +526,9 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
             partial = torch.empty((partial_rows(dd.n, dd.CH), Kp + 4), dtype=torch.float32, device=dev)
         _check(partial.numel() >= partial_rows(dd.n, dd.CH) * (Kp + 4), "partial scratch too small")
         dp = None
-        if dd.dense_list is not None:  # MFMA path for the dense rows
+        if dd.dense_list is not None:  # MFMA path for the dense rows (counts written by the forward)
+            _check(dense_A is not None and dense_A.dtype == torch.uint8 and dense_A.shape[1] == MAX_DENSE
+                   and dense_A.shape[0] >= dpred.numel(), "dense rows need the forward's dense_A counts")
             dp = dense_part if dense_part is not None else torch.empty(
                 (DENSE_WG * MAX_DENSE, Kp + 4), dtype=torch.float32, device=dev)
             _check(dp.numel() >= DENSE_WG * MAX_DENSE * (Kp + 4), "dense_part scratch too small")
@@ -528,7 +549,9 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               stream=_stream(dpred), g_wcol=g_wcol if mode != BWD_LOCAL else -1, g_bf16=int(bool(grad_bf16)),
               sr_counter=_p(sr_counter), counters_ready=int(bool(dd.bwd_fresh)),
               seg_bounds=_p(seg_bounds), piece=int(piece),
-              n_owners=(seg_bounds.numel() - 1) // 2 if seg_bounds is not None else 0)
+              n_owners=(seg_bounds.numel() - 1) // 2 if seg_bounds is not None else 0,
+              dense_A=_p(dense_A) if dd.dense_list is not None else 0,
+              cold_split=int(os.environ.get("FM_COLD_SPLIT", "0") == "1"))
         dd.bwd_fresh = False  # a second backward over this grouping zeroes its counters itself
     else:
         U = dd.sync()

@@ -362,7 +362,9 @@ class ShardExchange(_Base):
                 part.dd = K.dedup(keys, ws=dws, key_bits=self.key_bits, ex_of_occ=ex,
                                   vals=sb.vals if ex is not None else None, want_inv=True, num_examples=sb.B,
                                   Kp=self.m.Kp, ex_shift=shift, offsets=sb.offsets if shift else None,
-                                  dense_min=K.dense_min_for(sb.B, self.m.Kp, m.cfg.dedup_chunk) if train else 0)
+                                  dense_min=K.dense_min_for(sb.B, self.m.Kp, m.cfg.dedup_chunk,
+                                                            has_vals=sb.vals is not None,
+                                                            max_feats=sb.max_feats) if train else 0)
                 counts.append(K.owner_counts(part.dd, self.Rps, self.W))
                 pl.parts.append(part)
             c = torch.stack(counts, dim=1)     # [W, P]: row q = what goes to rank q
@@ -751,12 +753,13 @@ class ShardExchange(_Base):
             if work is not None:
                 work.wait()               # the compute stream waits for this part's rows
             src_v, src_w = wf.views(buf) if buf is not None else early_views
+            dA = ws.dense_counts(ws.cap_b)[e0: e0 + sb.B] if dd.dense_list is not None else None
             with roctx_range("fwd"):
                 fo = K.fm_forward(sb.offsets, dd.inv[: sb.nnz], sb.vals, src_v, src_w, Kp, labels=sb.labels,
                                   weights=sb.weights, loss=cfg.loss_type, grad_scale=gscale, want_r1=True,
                                   pred=ws.pred[e0: e0 + sb.B], r1=ws.r1[e0: e0 + sb.B],
                                   dpred=ws.dpred[e0: e0 + sb.B], partial=ws.fwd_partial, threads=cfg.threads,
-                                  bias=m.gbias)
+                                  bias=m.gbias, dense=dd, dense_A=dA, dense_by_segment=True)
             loss = fo.loss_sum if loss is None else loss + fo.loss_sum
             gs = grad_send[part.u0: part.u0 + part.U]
             if self._split_ok(pl, dd):
@@ -767,7 +770,7 @@ class ShardExchange(_Base):
                 K.fm_backward(dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT, src_v=src_v, src_w=src_w, grad_out=gs,
                               reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads,
                               dense_part=ws.dense_part, dense_stream=m._dense_stream() if gpu else None,
-                              grad_bf16=wf.grad_bf16)
+                              grad_bf16=wf.grad_bf16, dense_A=dA)
             if self.W > 1:
                 with roctx_range("a2a_grads"):
                     gworks.append(dist.all_to_all_single(grad_recv[part.r0: part.r0 + part.R], gs, part.rc, part.sc,
@@ -930,17 +933,18 @@ class DPDenseExchange(DPExchange):
         else:
             pl = m._local_plan(b)
         main.wait_event(pl.ready)
+        dA = ws.dense_counts(b.B) if pl.dd.dense_list is not None else None
         with roctx_range("fwd"):
             fo = K.fm_forward(b.offsets, pl.rows, b.vals, m.table.v, m.table.w, Kp, labels=b.labels,
                               weights=b.weights, loss=cfg.loss_type, grad_scale=m.grad_scale(b.B), want_r1=True,
                               pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
-                              bias=m.gbias)
+                              bias=m.gbias, dense=pl.dd, dense_A=dA)
             m.bias_step(fo.dpred)
         rv, rw = m.reg_coeffs
         with roctx_range("bwd_scatter"):
             K.fm_backward(pl.dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT_TABLE, table=m.table.state,
                           grad_out=self.dense, reg_v=rv, reg_w=rw, partial=ws.bwd_partial,
-                          dense_part=ws.dense_part, dense_stream=m._dense_stream())
+                          dense_part=ws.dense_part, dense_stream=m._dense_stream(), dense_A=dA)
         done = torch.cuda.Event()
         done.record(main)
         m._lslots[pl.slot].done = done

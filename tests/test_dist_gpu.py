@@ -44,7 +44,7 @@ def _cfg(mode, V):
 @pytest.mark.parametrize("dense", [False, True])
 def test_rccl_world1_matches_local(rccl_ctx, mode, dense, monkeypatch):
     if dense:  # MFMA backward rows (EMIT mode on the sharded path), forced on a small batch
-        monkeypatch.setattr(K, "dense_min_for", lambda B, Kp, CH=32: 48)
+        monkeypatch.setattr(K, "dense_min_for", lambda B, Kp, CH=32, **kw: 48)
     V = 50000
     gen = CriteoSynth(V, device="cuda", seed=21)
     batches = [gen.batch(2048) for _ in range(3)]

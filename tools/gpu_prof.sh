@@ -1,0 +1,16 @@
+#!/bin/bash
+# Kernel profile + one-step timeline of the default bench (no tests).
+# usage: tools/gpu_prof.sh <tag> [bench args...]   (env vars pass through)
+set -o pipefail
+TAG=${1:-prof}; shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/$TAG
+mkdir -p $OUT
+export FM_NO_AUTOBUILD=1
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $R/bench.py --steps 20 --warmup 5 "$@" > $OUT/prof.log 2>&1 || { echo "rocprof failed"; tail -30 $OUT/prof.log; exit 1; }
+grep ms/step $OUT/prof.log
+python3 $R/tools/kstats.py $OUT/prof/run_kernel_stats.csv 25 > $OUT/kernel_summary.txt
+python3 $R/tools/timeline.py $OUT/prof/run_kernel_trace.csv fm_fwd_kernel > $OUT/timeline.txt
+rm -f $OUT/prof/run_kernel_trace.csv
+head -25 $OUT/kernel_summary.txt; cat $OUT/timeline.txt
