@@ -269,6 +269,7 @@ class NativeTextReader:
         self._loader = L
         dev = self.gpu if self.gpu is not None else (self.dds.device if self.dds is not None else None)
         stream = torch.cuda.Stream(dev) if dev is not None else None
+        pending = None  # GPU tokenizer: batch k is launched, then k-1 finished and yielded
         try:
             while True:
                 item = L.next()
@@ -282,11 +283,10 @@ class NativeTextReader:
                     yield b
                     continue
                 if self.gpu is not None:
-                    buf, line_start, weights, epoch, count = item
-                    b = self._gpu_batch(buf, line_start, weights, stream)
-                    self.state.epoch, self.state.batches_in_epoch = int(epoch), int(count)
-                    b.reader_pos = (int(epoch), int(count))
-                    yield b
+                    launched = self._gpu_launch(item, stream)
+                    if pending is not None:
+                        yield self._gpu_finish(pending)
+                    pending = launched
                     continue
                 labels, offsets, ids, vals, weights, max_feats, epoch, count = item
                 b = Batch(torch.from_numpy(labels), torch.from_numpy(offsets), torch.from_numpy(ids),
@@ -296,6 +296,9 @@ class NativeTextReader:
                 self.state.epoch, self.state.batches_in_epoch = int(epoch), int(count)
                 b.reader_pos = (int(epoch), int(count))
                 yield b
+            if pending is not None:
+                yield self._gpu_finish(pending)
+                pending = None
             self.state.epoch, self.state.batches_in_epoch = self.num_epochs, 0
         finally:
             L.close()
@@ -314,29 +317,61 @@ class NativeTextReader:
             stream.synchronize()
         return Batch(labels, d_off, ids, vals, weights, nnz, max_feats=max_feats, offsets_host=ho)
 
-    def _gpu_batch(self, buf: np.ndarray, line_start: np.ndarray, weights, stream) -> Batch:
-        """H2D of the raw lines + GPU tokenizer on ``stream`` (CPU parser when the batch has syntax
-        outside the GPU subset or errors); returns a device batch whose work has completed."""
+    def _stage(self, buf: np.ndarray, line_start: np.ndarray) -> tuple[torch.Tensor, torch.Tensor]:
+        """Copy the raw batch into a reusable pinned staging slot (ring of 2, grown on demand).
+
+        ``pin_memory()`` per batch allocated and filled a fresh page-locked buffer every time;
+        the slots are allocated once and filled by torch's (multi-threaded) host copy.  A slot
+        is reused two batches later, after ``_gpu_finish`` has waited for that batch's parse
+        (which follows its host-to-device copy on the same stream)."""
+        ring = getattr(self, "_ring", None)
+        if ring is None:
+            ring = self._ring = {"k": 0, "bytes": [None, None], "ls": [None, None]}
+        k = ring["k"] = ring["k"] ^ 1
+        n, m = buf.shape[0], line_start.shape[0]
+        if ring["bytes"][k] is None or ring["bytes"][k].numel() < n:
+            ring["bytes"][k] = torch.empty(max(n, int(1.25 * n)), dtype=torch.uint8, pin_memory=True)
+        if ring["ls"][k] is None or ring["ls"][k].numel() < m:
+            ring["ls"][k] = torch.empty(max(m, int(1.25 * m)), dtype=torch.int64, pin_memory=True)
+        hb, hl = ring["bytes"][k][:n], ring["ls"][k][:m]
+        hb.copy_(torch.from_numpy(buf))
+        hl.copy_(torch.from_numpy(line_start))
+        return hb, hl
+
+    def _gpu_launch(self, item, stream):
+        """Stage the raw lines of a loader item in pinned memory, copy them to the device and
+        launch the GPU tokenizer on ``stream`` -- without waiting: the host stages the next
+        batch while this one is copied and parsed (``_gpu_finish`` collects it)."""
         from ..ops import kernels as K
 
+        buf, line_start, weights, epoch, count = item
         dev = self.gpu
         with torch.cuda.stream(stream):
-            hb = torch.from_numpy(buf).pin_memory()
-            hl = torch.from_numpy(line_start).pin_memory()
+            hb, hl = self._stage(buf, line_start)
             db = hb.to(dev, non_blocking=True)
             dl = hl.to(dev, non_blocking=True)
-            pg = K.parse_gpu(db, dl, self.args["vocab_size"], self.args["hash_feature_id"], stream=stream)
+            pp = K.parse_gpu_start(db, dl, self.args["vocab_size"], self.args["hash_feature_id"], stream=stream)
             w = None if weights is None else torch.from_numpy(weights).to(dev, non_blocking=True)
-            if pg.fallback:
-                self.fallbacks += 1
-                labels, sizes, ids, vals = native.cpu().parse_buffer(buf, self.args["vocab_size"],
-                                                                     self.args["hash_feature_id"],
-                                                                     self.args["threads"])
-                b = Batch.from_parsed(labels, sizes, ids, vals).to(dev)
-                b.weights = w
-            else:
-                b = Batch(pg.labels, pg.offsets, pg.ids, pg.vals, w, pg.nnz, max_feats=pg.max_feats)
-            stream.synchronize()
+        return pp, buf, w, int(epoch), int(count)
+
+    def _gpu_finish(self, launched) -> Batch:
+        """Wait for a launched tokenizer pass and wrap its outputs (CPU parser when the batch has
+        syntax outside the GPU subset or errors); the returned device batch is complete."""
+        pp, buf, w, epoch, count = launched
+        pg = pp.finish()
+        dev = self.gpu
+        if pg.fallback:
+            self.fallbacks += 1
+            labels, sizes, ids, vals = native.cpu().parse_buffer(buf, self.args["vocab_size"],
+                                                                 self.args["hash_feature_id"],
+                                                                 self.args["threads"])
+            b = Batch.from_parsed(labels, sizes, ids, vals).to(dev)
+            b.weights = w
+            torch.cuda.current_stream(dev).synchronize()
+        else:
+            b = Batch(pg.labels, pg.offsets, pg.ids, pg.vals, w, pg.nnz, max_feats=pg.max_feats)
+        self.state.epoch, self.state.batches_in_epoch = epoch, count
+        b.reader_pos = (epoch, count)
         return b
 
 

@@ -826,15 +826,28 @@ class ParsedGpu:
     fallback: bool           # syntax outside the GPU subset (or an error): re-parse on the CPU
 
 
-def parse_gpu(buf: torch.Tensor, line_start: torch.Tensor, vocab_size: int, hash_feature_id: bool = False,
-              stream: torch.cuda.Stream | None = None, require_vals: bool = False) -> ParsedGpu:
-    """Tokenize n '\\n'-terminated libsvm lines (``buf`` uint8 on the GPU, line ``i`` =
-    ``buf[line_start[i]:line_start[i+1]]``) into CSR on the device.
+class ParsePending:
+    """A launched GPU tokenizer pass whose (fallback, max_feats, non-unit, nnz) summary is on its
+    way to pinned host memory; ``finish()`` waits for it (an event, not a stream sync), so the
+    caller can stage and launch the next batch in between."""
 
-    Synchronises ``stream`` (the caller's side stream) once to read nnz and the
-    fallback flag; when ``fallback`` is set the outputs are incomplete and the
-    caller must parse the lines with the CPU parser (exact reference semantics
-    and error messages)."""
+    def __init__(self, labels, offsets, ids, vals, info_h, ev):
+        self.labels, self.offsets, self.ids, self.vals = labels, offsets, ids, vals
+        self.info_h, self.ev = info_h, ev
+
+    def finish(self) -> ParsedGpu:
+        self.ev.synchronize()
+        info = self.info_h
+        fb, mf, nonunit, nnz = int(info[0]), int(info[1]), int(info[2]), int(info[4])
+        return ParsedGpu(self.labels, self.offsets, self.ids[:nnz], self.vals[:nnz] if nonunit else None, nnz, mf,
+                         bool(fb))
+
+
+def parse_gpu_start(buf: torch.Tensor, line_start: torch.Tensor, vocab_size: int, hash_feature_id: bool = False,
+                    stream: torch.cuda.Stream | None = None, require_vals: bool = False) -> ParsePending:
+    """Launch the tokenizer of n '\n'-terminated libsvm lines (``buf`` uint8 on the GPU, line ``i``
+    = ``buf[line_start[i]:line_start[i+1]]``) into CSR on the device, asynchronously on
+    ``stream``; see ``parse_gpu``."""
     _check(_is_gpu(buf) and buf.dtype == torch.uint8 and buf.is_contiguous(), "buf: uint8 GPU bytes")
     _check(line_start.dtype == torch.int64 and line_start.device == buf.device, "line_start: int64 on buf's device")
     n = line_start.numel() - 1
@@ -843,20 +856,33 @@ def parse_gpu(buf: torch.Tensor, line_start: torch.Tensor, vocab_size: int, hash
     h = native.hip()
     cap = buf.numel() // 2 + n + 1          # a token takes >= 2 bytes (separator + 1 char)
     i32 = dict(dtype=torch.int32, device=dev)
-    counts = torch.empty(n + 1, **i32)
-    offsets = torch.empty(n + 1, **i32)
-    labels = torch.empty(n, dtype=torch.float32, device=dev)
-    ids = torch.empty(cap, **i32)
-    vals = torch.empty(cap, dtype=torch.float32, device=dev)
-    status = torch.empty(4, **i32)
-    wsb = h.parse_workspace_bytes(max(n, 1))
-    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
-    h.parse(buf=_p(buf), line_start=_p(line_start), n=n, vocab=int(vocab_size), hash=int(bool(hash_feature_id)),
-            counts=_p(counts), offsets=_p(offsets), labels=_p(labels), ids=_p(ids), vals=_p(vals),
-            status=_p(status), ws=_p(ws), ws_bytes=wsb, stream=st.cuda_stream, require_vals=int(bool(require_vals)))
-    info = torch.cat([status, offsets[n:]]).cpu()   # one D2H: (fallback, max_feats, non-unit, -, nnz)
-    fb, mf, nonunit, nnz = int(info[0]), int(info[1]), int(info[2]), int(info[4])
-    return ParsedGpu(labels, offsets, ids[:nnz], vals[:nnz] if nonunit else None, nnz, mf, bool(fb))
+    with torch.cuda.stream(st):
+        offsets = torch.empty(n + 1, **i32)
+        counts = torch.empty(n + 1, **i32)
+        labels = torch.empty(n, dtype=torch.float32, device=dev)
+        ids = torch.empty(cap, **i32)
+        vals = torch.empty(cap, dtype=torch.float32, device=dev)
+        status = torch.empty(5, **i32)
+        wsb = h.parse_workspace_bytes(max(n, 1))
+        ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+        h.parse(buf=_p(buf), line_start=_p(line_start), n=n, vocab=int(vocab_size), hash=int(bool(hash_feature_id)),
+                counts=_p(counts), offsets=_p(offsets), labels=_p(labels), ids=_p(ids), vals=_p(vals),
+                status=_p(status), ws=_p(ws), ws_bytes=wsb, stream=st.cuda_stream,
+                require_vals=int(bool(require_vals)))
+        status[4:5].copy_(offsets[n:])   # (fallback, max_feats, non-unit, -, nnz)
+        info_h = torch.empty(5, dtype=torch.int32, pin_memory=True)
+        info_h.copy_(status, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(st)
+    return ParsePending(labels, offsets, ids, vals, info_h, ev)
+
+
+def parse_gpu(buf: torch.Tensor, line_start: torch.Tensor, vocab_size: int, hash_feature_id: bool = False,
+              stream: torch.cuda.Stream | None = None, require_vals: bool = False) -> ParsedGpu:
+    """Tokenize n '\n'-terminated libsvm lines on the GPU (launch + wait, see
+    ``parse_gpu_start``).  When ``fallback`` is set the outputs are incomplete and the caller
+    must parse the lines with the CPU parser (exact reference semantics and error messages)."""
+    return parse_gpu_start(buf, line_start, vocab_size, hash_feature_id, stream, require_vals).finish()
 
 
 def run_member(req: torch.Tensor, prev: torch.Tensor, prev_run_off: torch.Tensor | None,

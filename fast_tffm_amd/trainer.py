@@ -202,6 +202,9 @@ class Trainer:
         nxt, nhave = fetch() if have else (None, False)
         pending = None
         tprev = time.time()
+        # steady state: from the end of the first epoch (input caches, page cache, lazy
+        # kernel loads and allocator growth are warm by then) to the end of the run
+        steady_t0, steady_step = None, None
         while have:
             # lookahead: the next two batches (when every rank has them) let the executors build
             # their dedup / id exchange / early row exchange while this step computes
@@ -213,6 +216,10 @@ class Trainer:
             step_num = self.model.global_step
             if batch.reader_pos is not None:  # position of the last CONSUMED batch (the reader runs ahead)
                 self.reader_state.epoch, self.reader_state.batches_in_epoch = batch.reader_pos
+                if steady_t0 is None and batch.reader_pos[0] >= 1:
+                    if self.device.type == "cuda":
+                        torch.cuda.synchronize(self.device)
+                    steady_t0, steady_step = time.time(), step_num - 1
             if pending is not None:
                 last_loss, tprev = report(pending)
             pending = (step_num, out, tprev)
@@ -247,11 +254,15 @@ class Trainer:
         total = time.time() - st
         speed = (step_num - start_step) * c.batch_size * self.world / max(total, 1e-9)
         self.print("Average speed: ", speed, " ex/s")
+        steady = None
+        if steady_t0 is not None and step_num - steady_step > 0:
+            steady = (step_num - steady_step) * c.batch_size * self.world / max(time.time() - steady_t0, 1e-9)
+            self.print("Steady-state speed (epochs 2+): ", steady, " ex/s")
         if c.log_dir:
             self.save()
         self.print("Model saved to ", c.log_dir)
         metrics.close()
-        return {"steps": step_num - start_step, "global_step": step_num, "avg_speed": speed,
+        return {"steps": step_num - start_step, "global_step": step_num, "avg_speed": speed, "steady_speed": steady,
                 "last_loss": last_loss, "early_stop": ended_early}
 
     # ------------------------------------------------------------------

@@ -3,9 +3,11 @@
 (sample.cfg: vocabulary 800k, factor_num 100, batch 50000, Adagrad, weighted mse,
 text files + weight files), reporting the reference's own metric line
 ``Average speed: ... ex/s`` (run_tffm.py:79-81) for each input path:
-native C++ loader with the CPU parser, and with the GPU tokenizer.
+native C++ loader with the CPU parser, with the GPU tokenizer, binary .fmb caches and
+HBM-resident .fmb caches -- plus the trainer's steady-state speed (epochs 2+: excludes
+process start-up, reader warm-up and the first pass over the files).
 
-usage: python tools/bench_train_e2e.py [--lines 200000] [--files 4] [--epochs 2]
+usage: python tools/bench_train_e2e.py [--lines 500000] [--files 4] [--epochs 6]
 """
 
 import argparse
@@ -50,9 +52,9 @@ predict_files =
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--lines", type=int, default=200_000)
+    ap.add_argument("--lines", type=int, default=500_000)
     ap.add_argument("--files", type=int, default=4)
-    ap.add_argument("--epochs", type=int, default=2)
+    ap.add_argument("--epochs", type=int, default=6)
     ap.add_argument("--batch", type=int, default=50_000)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--dir", default="/tmp/fm_e2e")
@@ -93,10 +95,12 @@ def main():
             print(r.stdout[-2000:], r.stderr[-3000:])
             sys.exit(r.returncode)
         m = re.search(r"Average speed:\s+([0-9.eE+]+)", r.stdout)
+        ms = re.search(r"Steady-state speed \(epochs 2\+\):\s+([0-9.eE+]+)", r.stdout)
         steps = len(re.findall(r"Global Step", r.stdout))
         name = {"fmb": "binary .fmb caches (host assembly)",
                 "fmb_hbm": "binary .fmb caches resident in HBM"}.get(gpu, f"gpu_parse={gpu}")
-        print(f"{name}: Average speed {float(m.group(1)):.4g} ex/s "
+        steady = f"{float(ms.group(1)):.4g}" if ms else "n/a"
+        print(f"{name}: Average speed {float(m.group(1)):.4g} ex/s, steady state (epochs 2+) {steady} ex/s "
               f"({a.files * a.lines * a.epochs} examples, wall {time.time() - t:.1f}s incl. start-up)", flush=True)
 
 
