@@ -98,12 +98,9 @@ def main() -> int:
     a.batch = a.batch or p.get("batch", 131072)
     mode = a.mode or p["mode"]
     if mode not in ("auto", "local") or int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        # HIP maps streams round-robin onto GPU_MAX_HW_QUEUES hardware queues (4 by default):
-        # the multi-rank step's compute, lookahead and RCCL streams then share queues and
-        # serialize (measured: sharded step 1.43 -> 1.18 ms with 8).  The single-GPU graphed
-        # step is 3% faster with 4.  Must be set before HIP initialises (first device call).
-        if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
-            os.environ["GPU_MAX_HW_QUEUES"] = "8"
+        # 8 HIP hardware queues for the multi-rank step (parallel/dist.py ensure_hw_queues; the
+        # single-GPU step keeps HIP's default 4).  Must be set before HIP initialises.
+        fmdist.ensure_hw_queues()
     # bounded collective timeout: a hang in the multi-GPU bench exits non-zero after
     # FM_PG_TIMEOUT seconds (RCCL watchdog) instead of holding the node for 30 minutes
     ctx = fmdist.init_distributed(force_pg=mode not in ("auto", "local"), device=p.get("device"),

@@ -81,6 +81,24 @@ def parse_dist_args(dist_args: list[str] | None) -> dict:
             "master_port": int(port) if port else 29500}
 
 
+MIN_HW_QUEUES = 8
+
+
+def ensure_hw_queues(n: int = MIN_HW_QUEUES) -> int:
+    """Give this process >= ``n`` HIP hardware queues (GPU_MAX_HW_QUEUES, default 4): HIP maps
+    streams round-robin onto them, and streams that share a queue execute in submission order.
+    The multi-rank step keeps the compute, plan / lookahead and dense streams plus one RCCL
+    stream per communicator busy at once; on shared queues they serialise (sharded step 1.43 ->
+    1.18 ms measured with 8), and two communicators' collective kernels queued in opposite
+    orders on two ranks could wait on each other.  Only effective before HIP initialises (the
+    first device call); returns the value in force."""
+    cur = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+    if cur < n:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(n)
+        cur = n
+    return cur
+
+
 def init_distributed(*, backend: str | None = None, rank: int | None = None, world: int | None = None,
                      master_addr: str | None = None, master_port: int | None = None,
                      device: str | None = None, timeout_s: float = 1800.0,
@@ -95,6 +113,8 @@ def init_distributed(*, backend: str | None = None, rank: int | None = None, wor
         return _CTX
     env_world = int(os.environ.get("WORLD_SIZE", "1"))
     world = int(world if world is not None else env_world)
+    if world > 1 or force_pg:
+        ensure_hw_queues()  # (before torch.cuda.is_available() below initialises HIP)
     rank = int(rank if rank is not None else os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", rank if world > 1 else 0))
     use_gpu = torch.cuda.is_available() if device is None else device.startswith("cuda")

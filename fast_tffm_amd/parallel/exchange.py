@@ -246,8 +246,12 @@ class ShardExchange(_Base):
         single = os.environ.get("FM_SINGLE_COMM", "0") == "1"
         # (FM_COMM_MODE=dual forces the plan communicator at world 1: teardown tests)
         forced = os.environ.get("FM_COMM_MODE", "")
+        # dual needs the RCCL streams of both communicators on hardware queues of their own
+        # (dist.ensure_hw_queues); with fewer queues (GPU_MAX_HW_QUEUES forced low by the user)
+        # every collective goes through the main communicator in program order
+        few_queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8
         self.comm_mode = forced if forced in ("single", "dual") else (
-            "single" if (single or self.W == 1) else "dual")
+            "single" if (single or self.W == 1 or few_queues) else "dual")
         self.plan_group = (dist.new_group(ranks=list(range(self.W)), backend=dist.get_backend(self.group))
                            if self.comm_mode == "dual" else self.group)
         self.cpu_group = self.ctx.cpu_group or self.group
