@@ -210,7 +210,8 @@ constexpr int chunk_min_waves() {
 #elif defined(FM_CHUNK_CAP_F32)  // A/B: also the fp32 k=64 kernel (135 VGPRs -> 128 + 44 B/lane of spills)
   return ((sizeof(TV) == 1 && LPR == 32) || (sizeof(TV) == 4 && LPR == 16)) ? 4 : 1;
 #else
-  return (sizeof(TV) == 1 && LPR == 32) ? 4 : 1;
+  // (bf16 LPR 32 -- k=128 bf16 -- crossed to 129 VGPRs with the short-chunk path: capped too)
+  return LPR == 32 ? 4 : 1;
 #endif
 }
 
@@ -226,6 +227,7 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
 #define FM_CHUNK_UNR 8
 #endif
   constexpr int UNR = LPR < FM_CHUNK_UNR ? LPR : FM_CHUNK_UNR;  // r1 rows in flight per lane
+  constexpr bool kShortPath = LPR >= 32;                          // short-chunk block (below)
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR, t = lane % LPR;
   const int gbase = g * LPR;
@@ -350,10 +352,13 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
           Sc += cc[uu];
         }
       }
-    } else if (len <= 4) {
+#ifndef FM_NO_SHORT_CHUNK
+    } else if (kShortPath && len <= 4) {
       // short chunks (275k of the 378k rows of a Criteo-shaped batch occur once, 341k of
       // the 510k chunks have <= 4 occurrences): one block of 4 r1 rows instead of UNR,
-      // so the group issues no redundant loads for the occurrences it does not have
+      // so the group issues no redundant loads for the occurrences it does not have.
+      // Same-box A/B (profiles/r2/short_chunk_ab.txt): k128 bf16 FTRL 1.044 -> 0.976 ms;
+      // k64 bf16 0.655 -> 0.695 ms (slower), k64 fp32 +-0: on for the 32-lane rows only
       constexpr int U4 = 4;
       float rr[U4][EPL], cc[U4], xx[U4];
 #pragma unroll
@@ -378,6 +383,7 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
         Scx += cc[uu] * xx[uu];
         Sc += cc[uu];
       }
+#endif
     } else {
 #pragma unroll
       for (int q = 0; q < PF; ++q) {

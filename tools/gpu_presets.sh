@@ -8,12 +8,16 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 export FM_NO_AUTOBUILD=1
 cd $R
-for P in k64_bf16 k64 k16_bf16 k128_ftrl k128_fp8_ftrl k64_dp_dense; do
+for P in k64 k64_bf16 k16_bf16 k128_ftrl k128_fp8_ftrl k64_dp_dense; do
   timeout -k 10 300 python bench.py --preset $P --steps 30 --warmup 5 > $OUT/bench_$P.json 2> $OUT/bench_$P.err || { echo "bench $P failed"; tail -20 $OUT/bench_$P.err; exit 1; }
   echo "$P: $(tail -1 $OUT/bench_$P.err)"
 done
-timeout -k 10 300 torchrun --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --mode shard --steps 30 --warmup 5 > $OUT/bench_shard.json 2> $OUT/bench_shard.err || { echo "shard bench failed"; tail -20 $OUT/bench_shard.err; exit 1; }
-echo "shard: $(grep ms/step $OUT/bench_shard.err)"
+for V in "off off" "on off" "on on"; do
+  set -- $V
+  timeout -k 10 300 torchrun --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --mode shard --prefetch-rows $1 --overlap-grads $2 --steps 30 --warmup 5 > $OUT/bench_shard_$1_$2.json 2> $OUT/bench_shard_$1_$2.err || { echo "shard bench failed"; tail -20 $OUT/bench_shard_$1_$2.err; exit 1; }
+  echo "shard (early rows $1, split grads $2): $(grep ms/step $OUT/bench_shard_$1_$2.err)"
+done
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_shard -o run -- python3 $R/bench.py --mode shard --steps 20 --warmup 5 > $OUT/prof_shard.log 2>&1 || { echo "rocprof failed"; tail -30 $OUT/prof_shard.log; exit 1; }
-python3 $R/tools/kstats.py $OUT/prof_shard/run_kernel_stats.csv 30 | tee $OUT/kernel_summary_shard.txt
+python3 $R/tools/kstats.py $OUT/prof_shard/run_kernel_stats.csv 30 > $OUT/kernel_summary_shard.txt
+rm -f $OUT/prof_shard/run_kernel_trace.csv
