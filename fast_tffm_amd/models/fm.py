@@ -472,7 +472,10 @@ class FactorizationMachine:
         return out
 
     def _dense_stream(self):
-        """Stream of the MFMA dense-row backward (forked from / joined into the compute stream)."""
+        """Stream of the MFMA dense-row backward (forked from / joined into the compute stream);
+        None (FM_DENSE_FORK=0): it runs on the compute stream before the chunk kernel."""
+        if os.environ.get("FM_DENSE_FORK", "1") == "0":
+            return None
         if getattr(self, "_dense_st", None) is None:
             self._dense_st = torch.cuda.Stream(self.device)
         return self._dense_st
