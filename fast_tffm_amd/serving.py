@@ -8,10 +8,15 @@ pure TF: ``serving_parser`` splits feature-only lines ``id:val id:val ...``
 ``vocab_block_i`` with the "mod" partition and evaluates the FM densely
 (tffm/fm_model.py:195-265).  The export path must not exist yet.
 
-Here the export is a self-contained directory::
+Here the export directory holds both forms::
 
-    export_path/saved_model.json        signature + model metadata
-    export_path/variables/vocab_block_{i}.npy   reference layout [V // N + 1, K + 1]
+    export_path/saved_model.pb                      TF SavedModel of the reference's serving graph
+    export_path/variables/variables.{index,data-*}  its variables (TF V2 tensor bundle)
+    export_path/saved_model.json                    signature + model metadata (native predictor)
+    export_path/variables/vocab_block_{i}.npy       reference layout [V // N + 1, K + 1]
+
+(utils/saved_model.py writes the SavedModel without TensorFlow; its parity with TF's loader
+is unpinned, checked by an independent numpy interpreter of the graph in the tests.)
 
 ``ServingModel.load(export_path).predict(data_lines)`` reproduces the
 signature (lines -> scores) with the native scorer (CPU or gfx950), and
@@ -64,6 +69,12 @@ def export_model(ckpt_dir: str, export_path: str, *, vocabulary_block_num: int, 
     })
     with open(os.path.join(tmp, "saved_model.json"), "w") as f:
         json.dump(doc, f, indent=1)
+    from .utils.saved_model import write_saved_model
+
+    blocks = [np.load(os.path.join(tmp, "variables", f"vocab_block_{i}.npy"), mmap_mode="r", allow_pickle=False)
+              for i in range(vocabulary_block_num)]
+    write_saved_model(tmp, blocks, meta["vocabulary_size"], meta["factor_num"], global_bias=meta.get("global_bias"))
+    del blocks
     os.replace(tmp, export_path)
     return export_path
 

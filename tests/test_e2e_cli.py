@@ -138,6 +138,16 @@ def test_train_predict_generate(workdir, global_bias):
     lines = open(workdir / "data" / "test_0").read().splitlines()[:50]
     feats = [" ".join(t if ":" in t else t + ":1" for t in ln.split()[1:]) for ln in lines]
     np.testing.assert_allclose(sm.predict(np.array(feats)), scores[:50], rtol=1e-5, atol=1e-6)
+    # the TF SavedModel of the reference's serving graph (saved_model.pb + variables bundle),
+    # evaluated by the independent numpy graph interpreter, gives the same scores
+    from fast_tffm_amd.utils import saved_model as tfsm
+
+    info = tfsm.read_saved_model(str(export))
+    assert info["tags"] == ["serve"] and info["saver"]["restore_op_name"] == "save/restore_all"
+    sig = info["signatures"]["serving_default"]
+    assert sig["method_name"] == "tensorflow/serving/predict"
+    assert set(sig["inputs"]) == {"data_lines"} and set(sig["outputs"]) == {"scores"}
+    np.testing.assert_allclose(tfsm.run_graph(str(export), feats), scores[:50], rtol=1e-5, atol=1e-5)
     # export path must be new
     with pytest.raises(FileExistsError):
         _run(["generate", cfg_path, "--export_path", str(export)])
