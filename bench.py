@@ -83,7 +83,7 @@ def main() -> int:
     ap.add_argument("--prefetch-rows", default="auto", choices=["auto", "on", "off"],
                     help="row-sharded step: exchange next step's rows early, patch the updated ones (auto: N > 1)")
     ap.add_argument("--overlap-grads", default="auto", choices=["auto", "on", "off"],
-                    help="row-sharded step: split backward, first half's gradient rows sent early (auto: N > 1)")
+                    help="row-sharded step: split backward, first half's gradient rows sent early (auto: off)")
     ap.add_argument("--comm-dtype", default="auto", choices=["auto", "fp32", "bf16"],
                     help="row-sharded wire rows (auto = table storage dtype; bf16 rounds fp32 rows for transport)")
     ap.add_argument("--stochastic-rounding", default="on", choices=["on", "off"],

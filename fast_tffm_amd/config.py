@@ -28,7 +28,8 @@ Extensions (new keys, all optional):
                 comm_dtype = auto|fp32|bf16 (row-sharded wire rows; auto = table storage dtype),
                 microbatches = 1|2|... (row-sharded step parts overlapping the exchange; default 1),
                 prefetch_rows = auto|on|off (exchange the next step's rows early, re-send updated ones),
-                overlap_grads = auto|on|off (split backward; first half's gradients sent while the rest runs)
+                overlap_grads = auto|on|off (split backward; first half's gradients sent while the rest runs;
+                                auto = off)
 """
 
 from __future__ import annotations

@@ -86,6 +86,7 @@ struct BwdArgs {
   int nex;                  // examples in the batch (dense path)
   const uint8_t* dense_A;   // [nex, kMaxDense] occurrence counts of the dense rows (written by the forward)
   int cold_split;           // 1: chunks of <= kColdMax occurrences go to fm_bwd_cold_kernel, the chunk kernel skips them
+  SelfRows self;            // EMIT (row-sharded step): segments that are this rank's own table rows
 };
 
 constexpr int kColdMax = 4;  // occurrences of a "cold" chunk
@@ -95,23 +96,36 @@ constexpr int kColdMax = 4;  // occurrences of a "cold" chunk
 template <int EPL>
 struct RowState {
   long long row;
+  bool apply;               // optimizer step in place on table row `row` (else: gradient row out)
   float vv[EPL], st0[EPL], st1[EPL];
   float wv, q0, q1;
 };
 
-// row: the table row (LOCAL) or the gathered row u (EMIT).
+// Parameters (and, when the row is updated here, optimizer state) of segment u with key
+// `key`: LOCAL reads table row key; EMIT reads gathered row u, or -- a self row of the
+// row-sharded step -- table row key - self.base, applied in place when exclusive;
+// EMIT_TABLE reads table row key and scatters its gradient there.
 template <typename TV, int EPL>
-__device__ inline void bwd_load_row(const BwdArgs& a, long long row, int tE, RowState<EPL>& r) {
+__device__ inline void bwd_load(const BwdArgs& a, int u, long long key, int tE, RowState<EPL>& r) {
   using F = Frag<TV>;
-  r.row = row;
-  F::load(reinterpret_cast<const TV*>(a.v) + r.row * a.v_stride + tE * EPL, r.vv);
-  r.wv = a.w[r.row * a.w_stride];
+  const void* vsrc = a.v;
+  const float* wsrc = a.w;
+  long long vst = a.v_stride, wst = a.w_stride;
+  r.apply = a.mode == kBwdLocal;
+  r.row = a.mode == kBwdEmit ? (long long)u : key;
+  if (a.mode == kBwdEmit && a.self.has(u)) {
+    r.row = key - a.self.base;
+    r.apply = a.self.exclusive(u);
+    vsrc = a.self.v; wsrc = a.self.w; vst = a.self.v_stride; wst = a.self.w_stride;
+  }
+  F::load(reinterpret_cast<const TV*>(vsrc) + r.row * vst + tE * EPL, r.vv);
+  r.wv = wsrc[r.row * wst];
   if constexpr (F::kScaled) {
-    const float s = row_scale<TV>(a.w, r.row, a.w_stride);
+    const float s = row_scale<TV>(wsrc, r.row, wst);
 #pragma unroll
     for (int k = 0; k < EPL; ++k) r.vv[k] *= s;
   }
-  if (a.mode != kBwdLocal) return;
+  if (!r.apply) return;
   const float* s0 = a.s0v + r.row * a.s_stride + tE * EPL;
 #pragma unroll
   for (int k = 0; k < EPL; k += 4) {
@@ -143,7 +157,7 @@ __device__ inline void bwd_finish(const BwdArgs& a, int u, int t, bool tact, Row
 #pragma unroll
   for (int k = 0; k < EPL; ++k) gr[k] = A[k] - Scx * r.vv[k] + nreg_v * r.vv[k];
   const float gw = Sc + nreg_w * r.wv;
-  if (a.mode != kBwdLocal) {
+  if (!r.apply) {
     float* dst = a.grad_out + (a.mode == kBwdEmitTable ? r.row : (long long)u) * a.g_stride;
     if (tact) {
       if (a.g_bf16) {  // EPL bf16 values per lane (EPL * 2 bytes, 8-byte aligned)
@@ -167,10 +181,14 @@ __device__ inline void bwd_finish(const BwdArgs& a, int u, int t, bool tact, Row
     }
     return;
   }
+  // in place: the table (LOCAL) or this rank's own table (EMIT self row)
+  const bool own = a.mode != kBwdLocal;
+  TV* tv = reinterpret_cast<TV*>(own ? const_cast<void*>(a.self.v) : a.v);
+  float* tw = own ? a.self.w : a.w;
+  const long long tvs = own ? a.self.v_stride : a.v_stride, tws = own ? a.self.w_stride : a.w_stride;
 #pragma unroll
   for (int k = 0; k < EPL; ++k) opt_step(a.opt, gr[k], r.vv[k], r.st0[k], r.st1[k]);
-  store_row<LPR, TV>(reinterpret_cast<TV*>(a.v) + r.row * a.v_stride + t * EPL, r.vv, a.w, r.row, a.w_stride, t,
-                     tact, sr);
+  store_row<LPR, TV>(tv + r.row * tvs + t * EPL, r.vv, tw, r.row, tws, t, tact, sr);
   if (tact) {
     float* s0 = a.s0v + r.row * a.s_stride + t * EPL;
 #pragma unroll
@@ -185,7 +203,7 @@ __device__ inline void bwd_finish(const BwdArgs& a, int u, int t, bool tact, Row
   }
   if (t == 0) {
     opt_step(a.opt, gw, r.wv, r.q0, r.q1);
-    a.w[r.row * a.w_stride] = r.wv;
+    tw[r.row * tws] = r.wv;
     a.s0w[r.row] = r.q0;
     if (a.s1w) a.s1w[r.row] = r.q1;
   }
@@ -195,7 +213,7 @@ template <int LPR, typename TV, int EPL>
 __device__ inline void bwd_finalize(const BwdArgs& a, int u, int t, bool tact, int tE,
                                     const float (&A)[EPL], float Scx, float Sc, int n_u, uint32_t sr) {
   RowState<EPL> r;
-  bwd_load_row<TV, EPL>(a, a.mode == kBwdEmit ? (long long)u : (long long)a.uniq[u], tE, r);
+  bwd_load<TV, EPL>(a, u, (long long)a.uniq[u], tE, r);
   bwd_finish<LPR, TV, EPL>(a, u, t, tact, r, A, Scx, Sc, n_u, sr);
 }
 
@@ -297,7 +315,7 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
     const int len = j1 - j0;
     if (a.cold_split && len <= kColdMax) continue;  // fm_bwd_cold_kernel's
     RowState<EPL> rs;
-    if (single) bwd_load_row<TV, EPL>(a, a.mode == kBwdEmit ? (long long)u : (long long)key, tE, rs);
+    if (single) bwd_load<TV, EPL>(a, u, (long long)key, tE, rs);
     // lane-parallel prefetch of the chunk's (example, dpred*x, x)
     int pex[PF];
     float pc[PF], px[PF];
@@ -472,7 +490,7 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_cold_kernel(BwdArgs a) {
     const int u = seg & kChunkSegMask;
     const bool single = (unsigned)seg & kChunkSingle;
     RowState<EPL> rs;
-    if (single) bwd_load_row<TV, EPL>(a, a.mode == kBwdEmit ? (long long)u : (long long)a.chunk_key[c], tE, rs);
+    if (single) bwd_load<TV, EPL>(a, u, (long long)a.chunk_key[c], tE, rs);
     int pex = 0;
     float pc = 0.f, px = 0.f;
     if (t < len) {

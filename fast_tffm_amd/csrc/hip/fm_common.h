@@ -230,6 +230,25 @@ struct OptParams {
   float beta;        // ftrl beta
 };
 
+// Row-sharded step, the rows this rank owns ("self rows", parallel/exchange.py): segments
+// [u0, u1) of the batch's sorted unique keys are this rank's own table rows (row = key -
+// base).  The forward and the backward read them straight from the table instead of the
+// gathered wire buffer (no owner gather, no early copy to patch), and the backward applies
+// the optimizer in place to the exclusive ones -- rows no other rank requested this step,
+// whose whole gradient is this rank's -- instead of emitting a gradient row for the owner's
+// apply.  Empty range: off.
+struct SelfRows {
+  int u0, u1;
+  long long base;           // key of local row 0 (rank * rows per shard)
+  const int* keys;          // [U] segment keys
+  const int* excl;          // [u1 - u0] 1 = exclusive (applied in place); null = all exclusive
+  const void* v; long long v_stride;   // table rows (elements of the table dtype)
+  float* w; long long w_stride;        // table linear weights (fp8: scale at w + 1)
+  __device__ inline bool has(int u) const { return u >= u0 && u < u1; }
+  __device__ inline bool exclusive(int u) const { return excl == nullptr || excl[u - u0] != 0; }
+  __device__ inline long long row(int u) const { return (long long)keys[u] - base; }
+};
+
 // In-place per-element optimizer step on fp32 registers. `s0`/`s1` are the
 // optimizer state values (adagrad: s0 = accumulator; ftrl: s0 = n, s1 = z).
 __device__ inline void opt_step(const OptParams& o, float g, float& p, float& s0, float& s1) {

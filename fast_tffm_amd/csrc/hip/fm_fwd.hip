@@ -41,8 +41,10 @@ struct FwdArgs {
   const int* dense_uniq;   // segment -> row key (local step: uniq = table rows) or null (rows ARE segment ids)
   const int* dense_count;  // device scalar: number of dense rows (capped at kMaxDense here)
   uint8_t* dense_A;        // [B, kMaxDense] occurrence counts (saturated at 255)
+  SelfRows self;           // row-sharded step: segments read from this rank's own table rows
 };
 
+constexpr int kSelfBit = (int)0x80000000u;   // row index tag: this rank's own table row (SelfRows)
 constexpr int kDenseHash = 4 * kMaxDense;  // open-addressing table of the dense keys (LDS, load <= 1/4)
 
 __device__ inline int dense_hash(int key) { return (int)(((uint32_t)key * 0x9E3779B1u) >> 22) & (kDenseHash - 1); }
@@ -95,6 +97,8 @@ void fm_fwd_kernel(FwdArgs a) {
   const int tE = tact ? t : nv - 1;        // clamped: loads never leave the row
   const float tmask = tact ? 1.f : 0.f;
   const TV* vbase = reinterpret_cast<const TV*>(a.v) + tE * EPL;
+  const bool self_on = a.self.u1 > a.self.u0;  // (uniform)
+  const TV* tbase = self_on ? reinterpret_cast<const TV*>(a.self.v) + tE * EPL : vbase;
   const int wave = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   const int nwaves = gridDim.x * kWavesPerBlock;
   const bool want_reg = a.reg_partial != nullptr;
@@ -128,22 +132,30 @@ void fm_fwd_kernel(FwdArgs a) {
     float lin = 0.f, rv = 0.f, rw = 0.f;
     for (int base = s; base < e; base += kWave) {
       const int m = min(kWave, e - base);
-      int my_row = 0;
+      int my_row = 0, my_seg = 0;
       float my_x = 0.f, my_w = 0.f, my_s = 1.f;
       if (lane < m) {
-        my_row = a.rows[base + lane];
+        my_seg = my_row = a.rows[base + lane];
         my_x = a.vals ? a.vals[base + lane] : 1.f;
         // the linear weight (and fp8 scale, same cache line) of occurrence `lane`, one
         // lane-parallel load per 64 occurrences instead of one per row group: the w loads
         // were ~45% of the kernel's VMEM instructions with the TA 72% busy
         // (profiles/r2/pmc_k64_fp32_before.txt)
-        my_w = a.w[(long long)my_row * a.w_stride];
-        my_s = row_scale<TV>(a.w, my_row, a.w_stride);
+        if (self_on && a.self.has(my_row)) {
+          // own table row: its index with the top bit set selects the table in the row loads
+          const long long trow = a.self.row(my_row);
+          my_w = a.self.w[trow * a.self.w_stride];
+          my_s = row_scale<TV>(a.self.w, trow, a.self.w_stride);
+          my_row = (int)trow | kSelfBit;
+        } else {
+          my_w = a.w[(long long)my_row * a.w_stride];
+          my_s = row_scale<TV>(a.w, my_row, a.w_stride);
+        }
       }
       lin += my_x * my_w;
       if (want_reg) rw += my_w * my_w;
       if (dense && lane < m) {
-        const int h = dense_probe(hkey, hval, my_row);
+        const int h = dense_probe(hkey, hval, my_seg);
         if (h >= 0) atomicAdd(&dcnt[wv][h], 1u);  // integer: order-independent
       }
       for (int q = 0; q < m; q += G * UNR) {
@@ -158,7 +170,9 @@ void fm_fwd_kernel(FwdArgs a) {
           const int row = __shfl(my_row, src, kWave);
           const float x = __shfl(my_x, src, kWave);
           fx[u] = f < m ? x : 0.f;
-          F::load(vbase + (long long)row * a.v_stride, fr[u]);
+          // (one load either way: the tagged index selects the base, not the instruction)
+          F::load(row < 0 ? tbase + (long long)(row & ~kSelfBit) * a.self.v_stride
+                          : vbase + (long long)row * a.v_stride, fr[u]);
           if constexpr (F::kScaled) fs[u] = __shfl(my_s, src, kWave);
         }
 #pragma unroll

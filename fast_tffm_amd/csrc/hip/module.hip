@@ -42,6 +42,20 @@ void check(int code, const char* what) {
   }
 }
 
+// Self rows (fm::SelfRows) arrive packed in one int64 list -- [u0, u1, base, keys, excl, v,
+// v_stride, w, w_stride] -- or empty (off); the kernel entry points already take ~60
+// arguments, past what pybind11's keyword dispatch handles comfortably.
+fm::SelfRows self_rows(const std::vector<long long>& f) {
+  fm::SelfRows r{};
+  if (f.empty()) return r;
+  if (f.size() != 9) throw std::invalid_argument("self_rows: [u0, u1, base, keys, excl, v, v_stride, w, w_stride]");
+  if (f[1] > f[0] && (!f[3] || !f[5] || !f[7])) throw std::runtime_error("self rows need keys and the table");
+  r.u0 = (int)f[0]; r.u1 = (int)(f[1] > f[0] ? f[1] : f[0]); r.base = f[2];
+  r.keys = P<const int>((u64)f[3]); r.excl = P<const int>((u64)f[4]);
+  r.v = P<const void>((u64)f[5]); r.v_stride = f[6]; r.w = P<float>((u64)f[7]); r.w_stride = f[8];
+  return r;
+}
+
 fm::OptParams opt_params(int type, float lr, float l1, float l2, float beta) {
   fm::OptParams o;
   o.type = type; o.lr = lr; o.l1 = l1; o.l2 = l2; o.beta = beta;
@@ -71,8 +85,9 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       [](int B, u64 offsets, u64 rows, u64 vals, u64 v, long long v_stride, u64 w, long long w_stride, int Kp,
          int dtype, u64 labels, u64 weights, int loss_type, float grad_scale, u64 pred, u64 r1, u64 dpred,
          u64 loss_partial, u64 reg_partial, int grid, u64 stream, u64 bias, u64 dense_list, u64 dense_uniq,
-         u64 dense_count, u64 dense_A) {
+         u64 dense_count, u64 dense_A, const std::vector<long long>& self) {
         fm::FwdArgs a{};
+        a.self = self_rows(self);
         a.dense_list = P<const int>(dense_list); a.dense_uniq = P<const int>(dense_uniq);
         a.dense_count = P<const int>(dense_count); a.dense_A = P<uint8_t>(dense_A);
         if (a.dense_A && (!a.dense_list || !a.dense_count)) throw std::runtime_error("fm_fwd: dense_A needs the dense list");
@@ -89,7 +104,8 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("w"), py::arg("w_stride"), py::arg("Kp"), py::arg("dtype"), py::arg("labels"), py::arg("weights"),
       py::arg("loss_type"), py::arg("grad_scale"), py::arg("pred"), py::arg("r1"), py::arg("dpred"),
       py::arg("loss_partial"), py::arg("reg_partial"), py::arg("grid"), py::arg("stream"), py::arg("bias") = 0,
-      py::arg("dense_list") = 0, py::arg("dense_uniq") = 0, py::arg("dense_count") = 0, py::arg("dense_A") = 0);
+      py::arg("dense_list") = 0, py::arg("dense_uniq") = 0, py::arg("dense_count") = 0, py::arg("dense_A") = 0,
+      py::arg("self_rows") = std::vector<long long>{});
 
   m.def(
       "bwd",
@@ -100,8 +116,14 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
          u64 big_list, u64 big_count, u64 multi, u64 slice_list, u64 slice_start, int nslices, u64 dense_list,
          u64 dense_part, int nex, u64 dense_stream, int dtype,
          long long max_chunks, long long max_unique, u64 stream, int g_wcol, int g_bf16, u64 sr_counter,
-         int counters_ready, u64 seg_bounds, int piece, int n_owners, u64 dense_A, int cold_split) {
+         int counters_ready, u64 seg_bounds, int piece, int n_owners, u64 dense_A, int cold_split,
+         const std::vector<long long>& self) {
         fm::BwdArgs a{};
+        a.self = self_rows(self);
+        if (a.self.u1 > a.self.u0 && a.self.keys != P<const int>(uniq))
+          throw std::runtime_error("fm_bwd: self-row keys must be the dedup's unique keys");
+        if (a.self.u1 > a.self.u0 && (mode != 1 || !s0v || !s0w))
+          throw std::runtime_error("fm_bwd: self rows are an EMIT-mode path and need the table's optimizer state");
         a.dense_A = P<const uint8_t>(dense_A);
         a.cold_split = cold_split;
         a.counters_ready = counters_ready;
@@ -136,7 +158,8 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("dense_part"), py::arg("nex"), py::arg("dense_stream"), py::arg("dtype"),
       py::arg("max_chunks"), py::arg("max_unique"), py::arg("stream"), py::arg("g_wcol") = -1,
       py::arg("g_bf16") = 0, py::arg("sr_counter") = 0, py::arg("counters_ready") = 0, py::arg("seg_bounds") = 0,
-      py::arg("piece") = -1, py::arg("n_owners") = 0, py::arg("dense_A") = 0, py::arg("cold_split") = 0);
+      py::arg("piece") = -1, py::arg("n_owners") = 0, py::arg("dense_A") = 0, py::arg("cold_split") = 0,
+      py::arg("self_rows") = std::vector<long long>{});
 
   m.def("dedup_workspace_bytes", &fm::dedup_workspace_bytes, py::arg("n"));
 
@@ -176,20 +199,23 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
   m.def(
       "gather_rows",
       [](int R, u64 req, u64 v, long long v_stride, u64 w, long long w_stride, int Kp, int dtype, u64 out,
-         long long o_stride, u64 stream) {
+         long long o_stride, u64 stream, int skip0, int skip1) {
         fm::GatherArgs a;
+        a.skip0 = skip0; a.skip1 = skip1;
         a.R = R; a.req = P<const int>(req); a.v = P<const void>(v); a.v_stride = v_stride;
         a.w = P<const float>(w); a.w_stride = w_stride; a.Kp = Kp; a.out = P<float>(out); a.o_stride = o_stride;
         check(fm::launch_gather_rows(a, dtype, S(stream)), "gather_rows");
       },
       py::arg("R"), py::arg("req"), py::arg("v"), py::arg("v_stride"), py::arg("w"), py::arg("w_stride"),
-      py::arg("Kp"), py::arg("dtype"), py::arg("out"), py::arg("o_stride"), py::arg("stream"));
+      py::arg("Kp"), py::arg("dtype"), py::arg("out"), py::arg("o_stride"), py::arg("stream"), py::arg("skip0") = 0,
+      py::arg("skip1") = 0);
 
   m.def(
       "gather_wire",
       [](int R, u64 req, u64 v, long long v_bytes_stride, u64 w, long long w_stride, int vbytes, int scaled,
-         int to_bf16, u64 out, long long rb, int vb, u64 stream, u64 idx, u64 run_off, int W) {
+         int to_bf16, u64 out, long long rb, int vb, u64 stream, u64 idx, u64 run_off, int W, int skip0, int skip1) {
         fm::GatherWireArgs a{};
+        a.skip0 = skip0; a.skip1 = skip1;
         a.idx = P<const int>(idx); a.run_off = P<const int>(run_off); a.W = W;
         a.R = R; a.req = P<const int>(req); a.v = P<const void>(v); a.v_bytes_stride = v_bytes_stride;
         a.w = P<const float>(w); a.w_stride = w_stride; a.vbytes = vbytes; a.scaled = scaled; a.to_bf16 = to_bf16;
@@ -198,7 +224,8 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       },
       py::arg("R"), py::arg("req"), py::arg("v"), py::arg("v_bytes_stride"), py::arg("w"), py::arg("w_stride"),
       py::arg("vbytes"), py::arg("scaled"), py::arg("to_bf16"), py::arg("out"), py::arg("rb"), py::arg("vb"),
-      py::arg("stream"), py::arg("idx") = 0, py::arg("run_off") = 0, py::arg("W") = 1);
+      py::arg("stream"), py::arg("idx") = 0, py::arg("run_off") = 0, py::arg("W") = 1, py::arg("skip0") = 0,
+      py::arg("skip1") = 0);
 
   m.def(
       "apply_rows",
@@ -227,8 +254,9 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       [](int R, int W, u64 run_off, u64 req, u64 match, u64 grad_in, long long g_stride, int Kp, u64 v,
          long long v_stride, u64 w, long long w_stride, u64 s0v, u64 s1v, long long s_stride, u64 s0w, u64 s1w,
          int opt_type, float lr, float l1, float l2, float beta, int dtype, u64 stream, int g_wcol, int g_bf16,
-         u64 sr_counter) {
+         u64 sr_counter, int self_run, u64 self_excl) {
         fm::ApplyArgs a{};
+        a.self_run = self_run; a.self_excl = P<const int>(self_excl);
         a.sr_counter = P<const int>(sr_counter);
         a.g_wcol = g_wcol < 0 ? Kp : g_wcol; a.g_bf16 = g_bf16;
         a.R = R; a.W = W; a.run_off = P<const int>(run_off); a.req = P<const int>(req);
@@ -242,7 +270,8 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("g_stride"), py::arg("Kp"), py::arg("v"), py::arg("v_stride"), py::arg("w"), py::arg("w_stride"),
       py::arg("s0v"), py::arg("s1v"), py::arg("s_stride"), py::arg("s0w"), py::arg("s1w"), py::arg("opt_type"),
       py::arg("lr"), py::arg("l1"), py::arg("l2"), py::arg("beta"), py::arg("dtype"), py::arg("stream"),
-      py::arg("g_wcol") = -1, py::arg("g_bf16") = 0, py::arg("sr_counter") = 0);
+      py::arg("g_wcol") = -1, py::arg("g_bf16") = 0, py::arg("sr_counter") = 0, py::arg("self_run") = -1,
+      py::arg("self_excl") = 0);
 
   m.def(
       "dense_apply",
@@ -305,13 +334,23 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("stream"));
   m.def(
       "dirty_scan",
-      [](int R, u64 req, int W, u64 run_off, int Wp, u64 prev_off, u64 prev, u64 flag, u64 dcount, u64 stream) {
+      [](int R, u64 req, int W, u64 run_off, int Wp, u64 prev_off, u64 prev, u64 flag, u64 dcount, u64 stream,
+         int skip0, int skip1) {
         check(fm::launch_dirty_scan(R, P<const int>(req), W, P<const int>(run_off), Wp, P<const int>(prev_off),
-                                    P<const int>(prev), P<int>(flag), P<int>(dcount), S(stream)),
+                                    P<const int>(prev), P<int>(flag), P<int>(dcount), skip0, skip1, S(stream)),
               "dirty_scan");
       },
       py::arg("R"), py::arg("req"), py::arg("W"), py::arg("run_off"), py::arg("Wp"), py::arg("prev_off"),
-      py::arg("prev"), py::arg("flag"), py::arg("dcount"), py::arg("stream"));
+      py::arg("prev"), py::arg("flag"), py::arg("dcount"), py::arg("stream"), py::arg("skip0") = 0,
+      py::arg("skip1") = 0);
+  m.def(
+      "self_excl",
+      [](u64 req, int W, u64 run_off, int me, int n, u64 excl, u64 stream) {
+        check(fm::launch_self_excl(P<const int>(req), W, P<const int>(run_off), me, n, P<int>(excl), S(stream)),
+              "self_excl");
+      },
+      py::arg("req"), py::arg("W"), py::arg("run_off"), py::arg("me"), py::arg("n"), py::arg("excl"),
+      py::arg("stream"));
   m.def("select_workspace_bytes", &fm::select_workspace_bytes, py::arg("n"));
   m.def(
       "select_flagged",

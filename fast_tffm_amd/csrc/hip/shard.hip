@@ -21,6 +21,7 @@ struct GatherArgs {
   const float* w; long long w_stride;
   int Kp;
   float* out; long long o_stride;   // [R, o_stride]: v at [0,Kp), w at Kp
+  int skip0, skip1;         // requests [skip0, skip1) are not gathered (this rank's own: self rows)
 };
 
 template <int LPR, typename TV>
@@ -34,7 +35,9 @@ __global__ __launch_bounds__(kBlock) void gather_rows_kernel(GatherArgs a) {
   const bool tact = t < nv;
   const int tE = tact ? t : nv - 1;
   const int ngroups = gridDim.x * kWavesPerBlock * G;
-  for (int p = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g; p < a.R; p += ngroups) {
+  const int nskip = a.skip1 - a.skip0;
+  for (int q = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g; q < a.R - nskip; q += ngroups) {
+    const int p = q < a.skip0 ? q : q + nskip;
     const long long row = a.req[p];
     float vv[EPL];
     F::load(reinterpret_cast<const TV*>(a.v) + row * a.v_stride + tE * EPL, vv);
@@ -77,6 +80,7 @@ struct GatherWireArgs {
   const int* idx;           // [R] or null
   const int* run_off;       // [W+1] (with idx)
   int W;
+  int skip0, skip1;         // (without idx) requests [skip0, skip1) are not gathered (self rows)
 };
 
 // One lane group per row; lane t moves 16 bytes of the wire row's v section
@@ -89,7 +93,9 @@ __global__ __launch_bounds__(kBlock) void gather_wire_kernel(GatherWireArgs a) {
   const int out_bytes = a.to_bf16 ? a.vbytes / 2 : a.vbytes;
   const int nunits = out_bytes / UNIT;
   const int ngroups = gridDim.x * kWavesPerBlock * G;
-  for (int p = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g; p < a.R; p += ngroups) {
+  const int nskip = a.skip1 - a.skip0;
+  for (int q = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g; q < a.R - nskip; q += ngroups) {
+    const int p = q < a.skip0 ? q : q + nskip;
     const int ip = a.idx ? a.idx[p] : p;
     const long long row = a.req[ip];
     const unsigned char* src = reinterpret_cast<const unsigned char*>(a.v) + row * a.v_bytes_stride;
@@ -133,8 +139,9 @@ int launch_gather_wire(const GatherWireArgs& a, hipStream_t st) {
   const int out_bytes = a.to_bf16 ? a.vbytes / 2 : a.vbytes;
   const bool u16 = out_bytes % 16 == 0;
   if (a.to_bf16 && !u16) return -7;
+  if (a.skip1 < a.skip0 || a.skip0 < 0 || a.skip1 > a.R || (a.idx && a.skip1 > a.skip0)) return -10;
   const int lpr = std::min(64, next_pow2(std::max(1, u16 ? out_bytes / 16 : out_bytes / 4)));
-  const int grid = fill_grid(a.R, kWavesPerBlock * (kWave / lpr));
+  const int grid = fill_grid(std::max(1, a.R - (a.skip1 - a.skip0)), kWavesPerBlock * (kWave / lpr));
 #define FM_GW(L)                                                                                        \
   case L:                                                                                               \
     if (u16) hipLaunchKernelGGL((gather_wire_kernel<L, 16>), dim3(grid), dim3(kBlock), 0, st, a);      \
@@ -173,6 +180,10 @@ struct ApplyArgs {
   long long row0;
   int touch_col;
   float* grad_zero;
+  // row-sharded step: run self_run holds this rank's own requests; the flagged (exclusive)
+  // ones were applied in place by the backward (SelfRows) and are skipped here
+  int self_run;             // -1: none
+  const int* self_excl;     // [run length] 1 = exclusive; null = the whole run
 };
 
 // One table row's parameters + optimizer state in registers (this lane's EPL
@@ -331,7 +342,7 @@ __global__ __launch_bounds__(kBlock) void run_member_kernel(int R, const int* re
 // dcount[q] = number of flagged requests in run q of the next step (per source rank).
 __global__ __launch_bounds__(kBlock) void dirty_scan_kernel(int R, const int* req, int W, const int* run_off,
                                                             int Wp, const int* prev_off, const int* prev, int* flag,
-                                                            int* dcount) {
+                                                            int* dcount, int skip0, int skip1) {
   __shared__ int cnt[kMaxRuns];
   __shared__ int off[kMaxRuns + 1];
   for (int q = threadIdx.x; q <= W; q += kBlock) {
@@ -342,7 +353,8 @@ __global__ __launch_bounds__(kBlock) void dirty_scan_kernel(int R, const int* re
   for (int i = blockIdx.x * kBlock + threadIdx.x; i < R; i += gridDim.x * kBlock) {
     const int key = req[i];
     int hit = 0;
-    for (int q = 0; q < Wp && !hit; ++q) {
+    // (requests [skip0, skip1): this rank's own rows, read from the table -- never patched)
+    for (int q = 0; q < Wp && !hit && (i < skip0 || i >= skip1); ++q) {
       int lo = prev_off[q];
       const int end = prev_off[q + 1];
       int hi = end;
@@ -388,12 +400,43 @@ __global__ __launch_bounds__(kBlock) void patch_scatter_kernel(int D, const unsi
 }
 
 int launch_dirty_scan(int R, const int* req, int W, const int* run_off, int Wp, const int* prev_off, const int* prev,
-                      int* flag, int* dcount, hipStream_t st) {
+                      int* flag, int* dcount, int skip0, int skip1, hipStream_t st) {
   if (W > kMaxRuns) return -8;
   (void)hipMemsetAsync(dcount, 0, sizeof(int) * W, st);
   if (R <= 0) return 0;
   hipLaunchKernelGGL(dirty_scan_kernel, dim3(fill_grid(R, kBlock, 2048)), dim3(kBlock), 0, st, R, req, W, run_off,
-                     Wp, prev_off, prev, flag, dcount);
+                     Wp, prev_off, prev, flag, dcount, skip0, skip1);
+  return (int)hipGetLastError();
+}
+
+// Self rows of the row-sharded step: run `me` of the received requests is this rank's own
+// requests; excl[i] = 1 when no other run (source rank) requested the same row this step,
+// so the whole gradient of the row is this rank's and its backward can apply it in place.
+__global__ __launch_bounds__(kBlock) void self_excl_kernel(const int* req, int W, const int* run_off, int me,
+                                                           int* excl) {
+  const int i0 = run_off[me], n = run_off[me + 1] - i0;
+  for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+    const int key = req[i0 + i];
+    int hit = 0;
+    for (int q = 0; q < W && !hit; ++q) {
+      if (q == me) continue;
+      int lo = run_off[q];
+      const int end = run_off[q + 1];
+      int hi = end;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (req[mid] < key) lo = mid + 1; else hi = mid;
+      }
+      hit = lo < end && req[lo] == key;
+    }
+    excl[i] = !hit;
+  }
+}
+
+int launch_self_excl(const int* req, int W, const int* run_off, int me, int n, int* excl, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(self_excl_kernel, dim3(fill_grid(n, kBlock, 4096)), dim3(kBlock), 0, st, req, W, run_off, me,
+                     excl);
   return (int)hipGetLastError();
 }
 
@@ -442,8 +485,9 @@ __global__ __launch_bounds__(kBlock) void apply_runs_kernel(ApplyArgs a) {
   for (int i = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g; i < a.R; i += ngroups) {
     int r = 0;
     const int* mrow = nullptr;
+    if (a.W > 1) while (a.run_off[r + 1] <= i) ++r;
+    if (r == a.self_run && (a.self_excl == nullptr || a.self_excl[i - a.run_off[r]])) continue;  // done in place
     if (a.W > 1) {
-      while (a.run_off[r + 1] <= i) ++r;
       mrow = a.match + (long long)i * a.W;
       bool led = true;
       for (int q = 0; q < r; ++q) led &= mrow[q] < 0;
@@ -511,8 +555,9 @@ int launch_dense_apply(const ApplyArgs& a, int dtype, hipStream_t st) {
 
 int launch_gather_rows(const GatherArgs& a, int dtype, hipStream_t st) {
   if (a.R <= 0) return 0;
+  if (a.skip1 < a.skip0 || a.skip0 < 0 || a.skip1 > a.R) return -10;
   const int lpr = lanes_per_row(a.Kp, dtype);
-  const int grid = fill_grid(a.R, kWavesPerBlock * (kWave / lpr));
+  const int grid = fill_grid(std::max(1, a.R - (a.skip1 - a.skip0)), kWavesPerBlock * (kWave / lpr));
   FM_DISPATCH(dtype, lpr, gather_rows_kernel, grid, st, a);
   return (int)hipGetLastError();
 }

@@ -155,7 +155,8 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
                r1: torch.Tensor | None = None, dpred: torch.Tensor | None = None,
                partial: torch.Tensor | None = None, threads: int = 0,
                bias: torch.Tensor | None = None, dense: "DedupOut | None" = None,
-               dense_A: torch.Tensor | None = None, dense_by_segment: bool = False) -> FwdOut:
+               dense_A: torch.Tensor | None = None, dense_by_segment: bool = False,
+               self_rows: SelfRows | None = None) -> FwdOut:
     """FM score of a CSR batch (reference FmScorer, cc/fm_scorer_op.h:101-140), fused with the loss.
 
     pred_i = sum_j x_j w_j + 1/2 sum_k [(sum_j x_j v_jk)^2 - sum_j x_j^2 v_jk^2]  (+ bias[0], optional
@@ -167,6 +168,7 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
     uint8): also count every example's occurrences of the dense rows into ``dense_A`` for the
     MFMA backward; ``rows`` are table rows (``dense.uniq`` maps segments to them) or, with
     ``dense_by_segment``, the segment ids themselves (the sharded step's inverse map).
+    ``self_rows`` (GPU, ``rows`` = segment ids): segments in its range read this rank's table.
     """
     dev = rows.device
     B = offsets.numel() - 1
@@ -209,6 +211,9 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
                    and dense_A.shape[0] >= B, "dense_A: contiguous uint8 [>= B, MAX_DENSE]")
             dkw = dict(dense_list=_p(dense.dense_list), dense_uniq=0 if dense_by_segment else _p(dense.uniq),
                        dense_count=_p(dense.counts) + 12, dense_A=_p(dense_A))
+        if self_rows is not None and self_rows.u1 > self_rows.u0:
+            _self_check(self_rows, v, None)
+            dkw["self_rows"] = self_rows.packed()
         h.fwd(B=B, offsets=_p(offsets), rows=_p(rows), vals=_p(vals), v=_p(v), v_stride=v_stride, w=_p(w),
               w_stride=w_stride, Kp=Kp, dtype=dt, labels=_p(labels), weights=_p(weights), loss_type=lt,
               grad_scale=float(grad_scale), pred=_p(pred), r1=_p(r1), dpred=_p(dpred) if lt else 0,
@@ -220,6 +225,7 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
         regv = rp.view(grid, 2)[:, 0].sum() if want_reg else None
         regw = rp.view(grid, 2)[:, 1].sum() if want_reg else None
     else:
+        _check(self_rows is None, "self rows are a GPU path")
         c = native.cpu()
         ls, rv, rw = c.fwd(B=B, offsets=_p(offsets), rows=_p(rows), vals=_p(vals), v=_p(v), v_stride=v_stride,
                            w=_p(w), w_stride=w_stride, Kp=Kp, dtype=dt, labels=_p(labels), weights=_p(weights),
@@ -451,6 +457,37 @@ class TableState:
     s1w: torch.Tensor | None = None  # [rows]
 
 
+@dataclass
+class SelfRows:
+    """Row-sharded step (GPU): segments ``[u0, u1)`` of a batch's sorted unique keys ``keys``
+    are this rank's own table rows (row = key - ``base``).  ``fm_forward`` / ``fm_backward``
+    read them from ``table`` instead of the gathered wire rows, and the backward applies the
+    optimizer in place to the exclusive ones (``excl`` int32 [u1 - u0], 1 = no other rank
+    requested the row this step; None = all, world 1) -- hip/fm_common.h SelfRows."""
+
+    u0: int
+    u1: int
+    base: int
+    keys: torch.Tensor
+    table: TableState
+    excl: torch.Tensor | None = None
+
+    def packed(self) -> list[int]:
+        """The binding's form: [u0, u1, base, keys, excl, v, v_stride, w, w_stride]."""
+        t = self.table
+        return [self.u0, self.u1, self.base, _p(self.keys), _p(self.excl), _p(t.v), t.v.stride(0), _p(t.w),
+                t.w.stride(0)]
+
+
+def _self_check(sr: SelfRows, v: torch.Tensor, keys: torch.Tensor | None) -> None:
+    _check(sr.table.v.dtype == v.dtype, "self rows: the table and the wire rows must share the dtype")
+    _check(keys is None or sr.keys.data_ptr() == keys.data_ptr(), "self rows: keys must be the dedup's uniq")
+    _check(0 <= sr.u0 <= sr.u1, "self rows: bad segment range")
+    if sr.excl is not None:
+        _chk_vec(sr.excl, torch.int32, None, "self excl", v.device)
+        _check(sr.excl.numel() >= sr.u1 - sr.u0, "self excl too short")
+
+
 def partial_rows(n: int, CH: int) -> int:
     """Upper bound on backward chunks (= partial rows) for n occurrences: U + n / CH."""
     return max(n, 1) + max(n, 1) // max(CH, 1) + 1
@@ -464,7 +501,7 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
                 dense_part: torch.Tensor | None = None, dense_stream=None,
                 grad_bf16: bool = False, sr_counter: torch.Tensor | None = None,
                 seg_bounds: torch.Tensor | None = None, piece: int = -1,
-                dense_A: torch.Tensor | None = None) -> torch.Tensor | None:
+                dense_A: torch.Tensor | None = None, self_rows: SelfRows | None = None) -> torch.Tensor | None:
     """Segmented FM backward over the dedup grouping (reference FmGrad, cc/fm_grad_op.h:59-163).
 
     Per unique row u with occurrences (i, x):
@@ -475,6 +512,8 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
     hold the gathered parameter rows in unique order).  ``piece`` 0 / 1 with
     ``seg_bounds`` (GPU, int32 [2W+1]) reduces only the segments of every owner's first /
     second part (split backward of the row-sharded exchange); piece 1 must follow piece 0.
+    ``self_rows`` (GPU, EMIT): segments in its range are read from its table; the exclusive ones
+    get ``opt`` applied in place (with ``sr_counter``) and no gradient row.
     """
     dev = dpred.device
     _check(dd.sorted_ex is not None, "dedup must be run with ex_of_occ")
@@ -514,6 +553,13 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
         _check(gstride >= g_wcol + 1 and gstride % 4 == 0,
                "grad_out row stride must hold the w column and be a multiple of 4")
         _check(not grad_bf16 or _is_gpu(dpred), "bf16 gradient rows are a GPU path")
+        if self_rows is not None and self_rows.u1 > self_rows.u0:
+            _check(_is_gpu(dpred) and opt is not None, "self rows: GPU path with the optimizer")
+            _self_check(self_rows, v, dd.uniq)
+            t = self_rows.table
+            s0v, s1v, s0w, s1w = t.s0v, t.s1v, t.s0w, t.s1w
+            _check(s0v is not None and s0w is not None, "self rows: the table's optimizer state")
+            s_stride = s0v.stride(0)
     v_stride = _chk_rows(v, Kp, "v")
     o = opt or OptConfig()
     if piece >= 0:
@@ -532,6 +578,9 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
             dp = dense_part if dense_part is not None else torch.empty(
                 (DENSE_WG * MAX_DENSE, Kp + 4), dtype=torch.float32, device=dev)
             _check(dp.numel() >= DENSE_WG * MAX_DENSE * (Kp + 4), "dense_part scratch too small")
+        skw = {}
+        if mode == BWD_EMIT and self_rows is not None and self_rows.u1 > self_rows.u0:
+            skw = dict(self_rows=self_rows.packed())
         h.bwd(mode=mode, counts=_p(dd.counts), chunk_start=_p(dd.chunk_start), chunk_seg=_p(dd.chunk_seg),
               chunk_key=_p(dd.chunk_key),
               seg_start=_p(dd.seg_start), seg_chunk=_p(dd.seg_chunk), uniq=_p(dd.uniq),
@@ -551,9 +600,10 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               seg_bounds=_p(seg_bounds), piece=int(piece),
               n_owners=(seg_bounds.numel() - 1) // 2 if seg_bounds is not None else 0,
               dense_A=_p(dense_A) if dd.dense_list is not None else 0,
-              cold_split=int(os.environ.get("FM_COLD_SPLIT", "0") == "1"))
+              cold_split=int(os.environ.get("FM_COLD_SPLIT", "0") == "1"), **skw)
         dd.bwd_fresh = False  # a second backward over this grouping zeroes its counters itself
     else:
+        _check(self_rows is None, "self rows are a GPU path")
         U = dd.sync()
         native.cpu().bwd(mode=mode, U=U, seg_start=_p(dd.seg_start), uniq=_p(dd.uniq), sorted_ex=_p(dd.sorted_ex),
                          sorted_x=_p(dd.sorted_x), dpred=_p(dpred), r1=_p(r1), Kp=Kp, v=_p(v), v_stride=v_stride,
@@ -567,8 +617,10 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
 # ---------------------------------------------------------------------------
 # row-sharded helpers
 # ---------------------------------------------------------------------------
-def gather_rows(req: torch.Tensor, table: TableState, Kp: int, out: torch.Tensor, threads: int = 0) -> torch.Tensor:
-    """out[p] = [v[req[p]], w[req[p]], 0...] (fp32), the owner side of a sharded lookup."""
+def gather_rows(req: torch.Tensor, table: TableState, Kp: int, out: torch.Tensor, threads: int = 0,
+                skip: tuple[int, int] | None = None) -> torch.Tensor:
+    """out[p] = [v[req[p]], w[req[p]], 0...] (fp32), the owner side of a sharded lookup.
+    ``skip`` (GPU): requests [s0, s1) are left out (their ``out`` rows are not written)."""
     dev = req.device
     R = req.numel()
     _chk_vec(req, torch.int32, R, "req", dev)
@@ -578,10 +630,13 @@ def gather_rows(req: torch.Tensor, table: TableState, Kp: int, out: torch.Tensor
     _range_check(req, table.v.shape[0], "req")
     dt = dtype_code(table.v.dtype)
     if _is_gpu(req):
+        s0, s1 = skip or (0, 0)
+        _check(0 <= s0 <= s1 <= R, "gather skip range")
         native.hip().gather_rows(R=R, req=_p(req), v=_p(table.v), v_stride=v_stride, w=_p(table.w),
                                  w_stride=table.w.stride(0), Kp=Kp, dtype=dt, out=_p(out), o_stride=out.stride(0),
-                                 stream=_stream(req))
+                                 stream=_stream(req), skip0=s0, skip1=s1)
     else:
+        _check(skip is None, "gather skip ranges are a GPU path")
         native.cpu().gather_rows(R=R, req=_p(req), v=_p(table.v), v_stride=v_stride, w=_p(table.w),
                                  w_stride=table.w.stride(0), Kp=Kp, dtype=dt, out=_p(out), o_stride=out.stride(0),
                                  threads=threads)
@@ -663,7 +718,8 @@ def dense_apply(grad: torch.Tensor, table: TableState, opt: OptConfig, Kp: int, 
 def apply_runs(req: torch.Tensor, run_off: torch.Tensor, splits: list[int], grad_in: torch.Tensor,
                table: TableState, opt: OptConfig, Kp: int, match: torch.Tensor | None = None,
                threads: int = 0, ws: DedupWorkspace | None = None, grad_bf16: bool = False,
-               sr_counter: torch.Tensor | None = None) -> None:
+               sr_counter: torch.Tensor | None = None, self_run: int = -1,
+               self_excl: torch.Tensor | None = None) -> None:
     """Owner side of a sharded update over the received requests as W ascending runs.
 
     ``req`` [R] holds the local rows requested by each source rank, rank-major
@@ -673,6 +729,8 @@ def apply_runs(req: torch.Tensor, run_off: torch.Tensor, splits: list[int], grad
     On the GPU the grouping is a cross-run binary-search match (``run_off`` =
     device int32 [W+1] prefix of ``splits``, ``match`` int32 scratch of R*W when
     W > 1) instead of a sort; on the CPU a stable sort of ``req`` (``ws``).
+    ``self_run`` >= 0 (GPU): the rows of that run flagged in ``self_excl`` (None: all of them)
+    were updated in place by the backward (``SelfRows``) and are skipped.
     """
     R, W = int(sum(splits)), len(splits)
     _chk_vec(req, torch.int32, R, "req", req.device)
@@ -680,7 +738,7 @@ def apply_runs(req: torch.Tensor, run_off: torch.Tensor, splits: list[int], grad
     if R == 0:
         return
     if not _is_gpu(grad_in):
-        _check(not grad_bf16, "bf16 gradient rows are a GPU path")
+        _check(not grad_bf16 and self_run < 0, "bf16 gradient rows and self runs are a GPU path")
         dd = dedup(req[:R], ws=ws, key_bits=32, want_perm=True)
         apply_rows(dd, grad_in, table, opt, Kp, threads=threads)  # (CPU tables: fp32 / bf16, nearest)
         return
@@ -697,7 +755,17 @@ def apply_runs(req: torch.Tensor, run_off: torch.Tensor, splits: list[int], grad
                             s_stride=s_stride, s0w=_p(table.s0w), s1w=_p(table.s1w), opt_type=opt.code,
                             lr=float(opt.lr), l1=float(opt.l1), l2=float(opt.l2), beta=float(opt.beta), dtype=dt,
                             stream=_stream(grad_in), g_wcol=(Kp * 2 + 15) // 16 * 4 if grad_bf16 else Kp,
-                            g_bf16=int(bool(grad_bf16)), sr_counter=_p(sr_counter))
+                            g_bf16=int(bool(grad_bf16)), sr_counter=_p(sr_counter), self_run=int(self_run),
+                            self_excl=_p(self_excl))
+
+
+def self_excl(req: torch.Tensor, W: int, run_off: torch.Tensor, me: int, n: int, out: torch.Tensor) -> torch.Tensor:
+    """GPU: out[i] = 1 when request ``run_off[me] + i`` (this rank's own run) is in no other run."""
+    _chk_vec(out, torch.int32, None, "excl", req.device)
+    _check(out.numel() >= n, "excl too short")
+    native.hip().self_excl(req=_p(req), W=int(W), run_off=_p(run_off), me=int(me), n=int(n), excl=_p(out),
+                           stream=_stream(req))
+    return out
 
 
 @dataclass
@@ -758,13 +826,15 @@ class WireFormat:
 
 def gather_wire(req: torch.Tensor, table: TableState, fmt: WireFormat, out: torch.Tensor,
                 threads: int = 0, idx: torch.Tensor | None = None, run_off: torch.Tensor | None = None,
-                W: int = 1) -> torch.Tensor:
+                W: int = 1, skip: tuple[int, int] | None = None) -> torch.Tensor:
     """Owner side of a sharded lookup: wire rows of table rows ``req`` into ``out`` (``fmt.empty``).
 
     With ``idx`` (GPU; patch gathers of the early row exchange) row p is ``req[idx[p]]``
-    and its last tail word gets the tag ``idx[p] - run_off[run]`` (W ascending runs)."""
+    and its last tail word gets the tag ``idx[p] - run_off[run]`` (W ascending runs).
+    ``skip`` (GPU, without ``idx``): requests [s0, s1) are left out (self rows)."""
     if fmt.fp32 and table.v.dtype == torch.float32 and idx is None:
-        return gather_rows(req, table, fmt.Kp, out, threads=threads)
+        return gather_rows(req, table, fmt.Kp, out, threads=threads, skip=skip)
+    _check(skip is None or idx is None, "skip ranges are for plain gathers")
     _check(_is_gpu(req), "non-fp32 wire formats and tagged gathers are a GPU path")
     R = req.numel() if idx is None else idx.numel()
     _chk_vec(req, torch.int32, None, "req", req.device)
@@ -781,16 +851,20 @@ def gather_wire(req: torch.Tensor, table: TableState, fmt: WireFormat, out: torc
     native.hip().gather_wire(R=R, req=_p(req), v=_p(v), v_bytes_stride=v.stride(0) * v.element_size(),
                              w=_p(table.w), w_stride=table.w.stride(0), vbytes=fmt.Kp * v.element_size(),
                              scaled=int(v.dtype == FP8), to_bf16=int(to_bf16), out=_p(out), rb=fmt.rb, vb=fmt.vb,
-                             stream=_stream(req), idx=_p(idx), run_off=_p(run_off), W=int(W))
+                             stream=_stream(req), idx=_p(idx), run_off=_p(run_off), W=int(W),
+                             skip0=(skip or (0, 0))[0], skip1=(skip or (0, 0))[1])
     return out
 
 
 def dirty_scan(req: torch.Tensor, run_off: torch.Tensor, W: int, prev: torch.Tensor, prev_off: torch.Tensor,
-               Wp: int, flag: torch.Tensor, dcount: torch.Tensor) -> None:
-    """GPU: flag[i] = req[i] in any of the Wp runs of ``prev``; dcount[q] = flagged per run q of ``req``."""
+               Wp: int, flag: torch.Tensor, dcount: torch.Tensor, skip: tuple[int, int] | None = None) -> None:
+    """GPU: flag[i] = req[i] in any of the Wp runs of ``prev``; dcount[q] = flagged per run q of ``req``.
+    Requests in ``skip`` = [s0, s1) (self rows, read from the table) are never flagged."""
     R = req.numel()
+    s0, s1 = skip or (0, 0)
     native.hip().dirty_scan(R=R, req=_p(req), W=int(W), run_off=_p(run_off), Wp=int(Wp), prev_off=_p(prev_off),
-                            prev=_p(prev), flag=_p(flag), dcount=_p(dcount), stream=_stream(req))
+                            prev=_p(prev), flag=_p(flag), dcount=_p(dcount), stream=_stream(req), skip0=s0,
+                            skip1=s1)
 
 
 def select_flagged(flag: torch.Tensor, out: torch.Tensor, count: torch.Tensor, ws: torch.Tensor) -> None:

@@ -91,7 +91,7 @@ class _ShardPlan:
     part 1's, ...; ``run_off`` the W * parts run boundaries)."""
 
     __slots__ = ("b", "slot", "parts", "U", "R", "req_recv", "run_off", "splits", "match", "ready", "early",
-                 "train", "counts", "counts_ev")
+                 "train", "counts", "counts_ev", "self_u", "self_r", "self_excl")
 
 
 class _Early:
@@ -118,6 +118,7 @@ class _PlanSlot:
         self.run_off_h: torch.Tensor | None = None  # pinned receive-run offsets (host staging)
         self.run_off: torch.Tensor | None = None    # device copy
         self.match: torch.Tensor | None = None      # [R, runs] cross-run match scratch (apply_runs)
+        self.excl: torch.Tensor | None = None       # [own requests] exclusive flags (self rows)
 
     def ensure(self, k: int, nnz: int, dev, CH: int) -> K.DedupWorkspace:
         while len(self.dd) <= k:
@@ -144,6 +145,12 @@ class _PlanSlot:
         np.cumsum(splits, out=h[1: n + 1])
         self.run_off[: n + 1].copy_(self.run_off_h[: n + 1], non_blocking=True)
         return self.run_off
+
+    def excl_buf(self, n: int, dev) -> torch.Tensor:
+        if self.excl is None or self.excl.numel() < n:
+            self.excl = torch.empty(max(n, 1, int(1.25 * (self.excl.numel() if self.excl is not None else 0))),
+                                    dtype=torch.int32, device=dev)
+        return self.excl
 
     def match_buf(self, n: int, dev) -> torch.Tensor:
         if self.match is None or self.match.numel() < n:
@@ -225,9 +232,18 @@ class ShardExchange(_Base):
         # (which can then become the critical path): "auto" uses it with two batches of lookahead
         self.prefetch_depth1 = self.prefetch and forced
         # split backward: the gradient rows of every owner's first half travel (P2P on RCCL)
-        # while the second half is reduced
+        # while the second half is reduced.  Opt-in ("auto" = off): the two backward passes cost
+        # ~0.1-0.19 ms more compute than one (measured at world 1, profiles/r2/self_rows_ab.txt),
+        # more than the half of the gradient all-to-all they can hide on the 8-GPU mesh (~95 MB
+        # per rank over 7 xGMI links, ~0.1 ms)
         og = str(getattr(model.cfg, "overlap_grads", "auto")).lower()
-        self.overlap_grads = self.nparts == 1 and (og in ("on", "true", "1") or (og == "auto" and self.W > 1))
+        self.overlap_grads = self.nparts == 1 and og in ("on", "true", "1")
+        # self rows (hip/fm_common.h SelfRows): this rank's own rows are read from the table by the
+        # forward / backward -- no owner gather, no row exchange or early copy to patch for them --
+        # and the exclusive ones (requested by no other rank this step) are updated in place by
+        # the backward instead of the owner's apply.  GPU, wire dtype = table dtype, one part.
+        self.self_rows = (self.dev.type == "cuda" and self.wire.dtype == tdt and self.nparts == 1
+                          and os.environ.get("FM_SELF_ROWS", "1") != "0")
         self.cur_plan: _ShardPlan | None = None
         self.step_start = None
         self.early_steps = 0          # steps that took the early-exchange + patch path
@@ -335,6 +351,7 @@ class ShardExchange(_Base):
         pl = _ShardPlan()
         pl.b, pl.slot, pl.train = b, idx, train
         pl.early = pl.splits = pl.run_off = pl.match = pl.ready = None
+        pl.self_u = pl.self_r = pl.self_excl = None
         gpu = self.dev.type == "cuda"
         if gpu:
             st = self._prep_stream()
@@ -435,6 +452,14 @@ class ShardExchange(_Base):
             if pl.train and gpu:
                 pl.run_off = slot.runs(pl.splits, self.dev)
                 pl.match = slot.match_buf(pl.R * len(pl.splits), self.dev) if len(pl.splits) > 1 else None
+                part = pl.parts[0]
+                if self.self_rows and len(pl.parts) == 1 and part.dd.dense_list is None:
+                    me = self.ctx.rank
+                    s0, r0 = int(sum(part.sc[:me])), int(sum(part.rc[:me]))
+                    pl.self_u, pl.self_r = (s0, s0 + part.sc[me]), (r0, r0 + part.rc[me])
+                    if self.W > 1 and part.rc[me]:
+                        pl.self_excl = K.self_excl(pl.req_recv, self.W, pl.run_off, me, part.rc[me],
+                                                   slot.excl_buf(part.rc[me], self.dev))
             if early and pl.train and self._early_ok(pl, self.cur_plan):
                 pl.early = self._early(pl, self.cur_plan)
             if gpu:
@@ -443,6 +468,8 @@ class ShardExchange(_Base):
 
     def _early_ok(self, pl: _ShardPlan, cur: _ShardPlan | None) -> bool:
         gpu = self.dev.type == "cuda"
+        if pl.self_r is not None and pl.self_r[1] - pl.self_r[0] == pl.R:
+            return False  # every request is this rank's own row (world 1): nothing to exchange early
         return (self.prefetch and len(pl.parts) == 1 and pl.splits is not None and cur is not None
                 and cur.splits is not None and (cur.run_off is not None or not gpu) and len(cur.parts) == 1
                 and (pl.run_off is not None or not gpu))
@@ -476,7 +503,7 @@ class ShardExchange(_Base):
         e = _Early()
         ew = slot.early_ws(R, W, dev)             # this slot's buffers (free again two plans later)
         flag, e.didx, dcount = ew["flag"], ew["didx"], ew["dcount"]  # dcount: [W] per source, [W] total
-        K.dirty_scan(req, pl.run_off, W, cur.req_recv, cur.run_off, len(cur.splits), flag, dcount)
+        K.dirty_scan(req, pl.run_off, W, cur.req_recv, cur.run_off, len(cur.splits), flag, dcount, skip=pl.self_r)
         K.select_flagged(flag[:R], e.didx, dcount[W:], ew["sel"])
         # dirty counts: sent (per source rank) and received (per owner), exchanged on the device
         drecv = ew["drecv"]
@@ -497,7 +524,7 @@ class ShardExchange(_Base):
         if self.step_start is not None:
             torch.cuda.current_stream(dev).wait_event(self.step_start)
         rows_send = self.wire.empty(R, dev)
-        K.gather_wire(req, self.m.table.state, self.wire, rows_send, threads=self.m.cfg.threads)
+        K.gather_wire(req, self.m.table.state, self.wire, rows_send, threads=self.m.cfg.threads, skip=pl.self_r)
         e.work = None
         if W == 1:
             e.gathered = rows_send
@@ -635,13 +662,13 @@ class ShardExchange(_Base):
             return list(dist.batch_isend_irecv(ops))
         return [op.op(op.tensor, op.peer, group=op.group) for op in ops]
 
-    def _bwd_split_exchange(self, pl, part, dd, fo, src_v, src_w, gs, grad_recv, rv, rw) -> list:
+    def _bwd_split_exchange(self, pl, part, dd, fo, src_v, src_w, gs, grad_recv, rv, rw, skw) -> list:
         """Backward in two pieces (every owner's first half of rows, then the second half) with
         the first piece's gradient rows sent while the second is reduced."""
         m, ws, cfg, Kp, wf = self.m, self.m.ws, self.m.cfg, self.Kp, self.wire
         bounds = self._half_bounds(part)
         kw = dict(mode=K.BWD_EMIT, src_v=src_v, src_w=src_w, grad_out=gs, reg_v=rv, reg_w=rw,
-                  partial=ws.bwd_partial, threads=cfg.threads, grad_bf16=wf.grad_bf16)
+                  partial=ws.bwd_partial, threads=cfg.threads, grad_bf16=wf.grad_bf16, **skw)
         if self.dev.type != "cuda":  # CPU reference: one backward, the exchange still in two pieces
             K.fm_backward(dd, fo.dpred, fo.r1, Kp, **kw)
             return self._p2p_piece(0, part, bounds, gs, grad_recv) + self._p2p_piece(1, part, bounds, gs, grad_recv)
@@ -706,7 +733,7 @@ class ShardExchange(_Base):
         once ``work`` (None: already there) is waited for."""
         rows_send = self.wire.empty(part.R, self.dev)
         K.gather_wire(pl.req_recv[part.r0: part.r0 + part.R], self.m.table.state, self.wire, rows_send,
-                      threads=self.m.cfg.threads)
+                      threads=self.m.cfg.threads, skip=pl.self_r)
         if self.W == 1:
             return rows_send, None
         gathered = self.wire.empty(part.U, self.dev)
@@ -752,6 +779,14 @@ class ShardExchange(_Base):
         loss = None
         rv, rw = m.reg_coeffs
         gscale = m.grad_scale(b.B)
+        # (one stochastic-rounding tick per step, shared by the in-place self-row updates of the
+        # backward and the owner's apply: the same row gets the same bits either way)
+        sr = m.sr_tick()
+        srows, skw = None, {}
+        if pl.self_u is not None:
+            srows = K.SelfRows(pl.self_u[0], pl.self_u[1], self.ctx.rank * self.Rps, pl.parts[0].dd.uniq,
+                               m.table.state, pl.self_excl)
+            skw = dict(self_rows=srows, opt=cfg.opt, sr_counter=sr)
         for part, (buf, work) in zip(pl.parts, rows):
             sb, dd, e0 = part.b, part.dd, part.e0
             if work is not None:
@@ -763,18 +798,18 @@ class ShardExchange(_Base):
                                   weights=sb.weights, loss=cfg.loss_type, grad_scale=gscale, want_r1=True,
                                   pred=ws.pred[e0: e0 + sb.B], r1=ws.r1[e0: e0 + sb.B],
                                   dpred=ws.dpred[e0: e0 + sb.B], partial=ws.fwd_partial, threads=cfg.threads,
-                                  bias=m.gbias, dense=dd, dense_A=dA, dense_by_segment=True)
+                                  bias=m.gbias, dense=dd, dense_A=dA, dense_by_segment=True, self_rows=srows)
             loss = fo.loss_sum if loss is None else loss + fo.loss_sum
             gs = grad_send[part.u0: part.u0 + part.U]
             if self._split_ok(pl, dd):
                 with roctx_range("bwd_split+grads"):
-                    gworks += self._bwd_split_exchange(pl, part, dd, fo, src_v, src_w, gs, grad_recv, rv, rw)
+                    gworks += self._bwd_split_exchange(pl, part, dd, fo, src_v, src_w, gs, grad_recv, rv, rw, skw)
                 continue
             with roctx_range("bwd"):
                 K.fm_backward(dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT, src_v=src_v, src_w=src_w, grad_out=gs,
                               reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads,
                               dense_part=ws.dense_part, dense_stream=m._dense_stream() if gpu else None,
-                              grad_bf16=wf.grad_bf16, dense_A=dA)
+                              grad_bf16=wf.grad_bf16, dense_A=dA, **skw)
             if self.W > 1:
                 with roctx_range("a2a_grads"):
                     gworks.append(dist.all_to_all_single(grad_recv[part.r0: part.r0 + part.R], gs, part.rc, part.sc,
@@ -783,9 +818,12 @@ class ShardExchange(_Base):
         for w in gworks:
             w.wait()
         with roctx_range("apply"):
-            K.apply_runs(pl.req_recv, pl.run_off, pl.splits, grad_recv, m.table.state, cfg.opt, Kp, match=pl.match,
-                         threads=cfg.threads, ws=self.slots[pl.slot].ensure2(pl.R, self.dev) if not gpu else None,
-                         grad_bf16=wf.grad_bf16, sr_counter=m.sr_tick())
+            if not (srows is not None and self.W == 1):  # (world 1: every row was updated in place)
+                K.apply_runs(pl.req_recv, pl.run_off, pl.splits, grad_recv, m.table.state, cfg.opt, Kp,
+                             match=pl.match, threads=cfg.threads,
+                             ws=self.slots[pl.slot].ensure2(pl.R, self.dev) if not gpu else None,
+                             grad_bf16=wf.grad_bf16, sr_counter=sr, self_run=self.ctx.rank if srows else -1,
+                             self_excl=pl.self_excl)
         if gpu:
             done = torch.cuda.Event()
             done.record(torch.cuda.current_stream(self.dev))

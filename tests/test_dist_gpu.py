@@ -155,11 +155,15 @@ def test_rccl_world1_shard_microbatches_match_local(rccl_ctx, mb):
     torch.testing.assert_close(dm.predict(ev), loc.predict(ev), rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("self_rows", ["0", "1"])
 @pytest.mark.parametrize("depth", [1, 2])
 @pytest.mark.parametrize("dtype,k", [(torch.float32, 64), (torch.bfloat16, 16), (K.FP8, 128)])
-def test_rccl_world1_early_exchange_matches_local(rccl_ctx, dtype, k, depth):
+def test_rccl_world1_early_exchange_matches_local(rccl_ctx, dtype, k, depth, self_rows, monkeypatch):
     """Early row exchange + dirty-row patch (prefetch_rows=on) is exact: every step equals the
-    local step, though rows shared by consecutive batches are read before the update lands."""
+    local step, though rows shared by consecutive batches are read before the update lands.
+    FM_SELF_ROWS=0 sends the rank's own rows through the exchange (the early machinery then
+    runs at world 1); with self rows every request is the rank's own and nothing is exchanged."""
+    monkeypatch.setenv("FM_SELF_ROWS", self_rows)
     V = 20000
     gen = CriteoSynth(V, device="cuda", seed=25)
     batches = [gen.batch(2048) for _ in range(6)]
@@ -178,14 +182,17 @@ def test_rccl_world1_early_exchange_matches_local(rccl_ctx, dtype, k, depth):
         l2 = dm.train_step(b, nb, nb2).mean_loss()
         assert abs(l1 - l2) <= 1e-5 * max(1.0, abs(l1)), (i, l1, l2)
     torch.cuda.synchronize()
-    assert dm._exchange.early_steps == len(batches) - 1
+    assert dm._exchange.early_steps == (len(batches) - 1 if self_rows == "0" else 0)
     torch.testing.assert_close(dm.table.reference_rows(), loc.table.reference_rows(), rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("self_rows", ["0", "1"])
 @pytest.mark.parametrize("dtype,k", [(torch.float32, 64), (torch.bfloat16, 16), (K.FP8, 128)])
-def test_rccl_world1_split_backward_matches_local(rccl_ctx, dtype, k):
+def test_rccl_world1_split_backward_matches_local(rccl_ctx, dtype, k, self_rows, monkeypatch):
     """Backward split into every owner's first / second half of rows (overlap_grads=on, with
-    the early row exchange) reduces exactly what the one-piece backward does."""
+    the early row exchange) reduces exactly what the one-piece backward does (self rows: both
+    pieces update their rows in place)."""
+    monkeypatch.setenv("FM_SELF_ROWS", self_rows)
     V = 20000
     gen = CriteoSynth(V, device="cuda", seed=26)
     batches = [gen.batch(2048) for _ in range(5)]
@@ -208,11 +215,13 @@ def test_rccl_world1_split_backward_matches_local(rccl_ctx, dtype, k):
     torch.testing.assert_close(dm.table.reference_rows(), loc.table.reference_rows(), rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("self_rows", ["0", "1"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_rccl_world1_pipelined_shard_step_is_bitwise_deterministic(rccl_ctx, dtype):
+def test_rccl_world1_pipelined_shard_step_is_bitwise_deterministic(rccl_ctx, dtype, self_rows, monkeypatch):
     """Race detection for the sharded pipeline: with the side-stream plan two
     batches ahead, the early row exchange + patches and the split backward all on, two runs
     of the same batches leave bit-identical tables (bf16 with stochastic rounding too)."""
+    monkeypatch.setenv("FM_SELF_ROWS", self_rows)
     V = 20000
     gen = CriteoSynth(V, device="cuda", seed=27)
     batches = [gen.batch(4096) for _ in range(6)]

@@ -90,6 +90,8 @@ def _worker(rank, world, port, out_dir, variant):
     from fast_tffm_amd.models.fm import FactorizationMachine
     from fast_tffm_amd.parallel import dist as fmdist
 
+    variant = dict(variant)
+    os.environ.update(variant.pop("env", {}))
     ctx = fmdist.init_distributed(backend="gloo", rank=rank, world=world, device="cuda:0")
     m = FactorizationMachine(_cfg("shard", B, **variant), device="cuda:0", dist=ctx)
     bs = [_batch(s, rank) for s in range(STEPS)]
@@ -105,16 +107,21 @@ def _worker(rank, world, port, out_dir, variant):
     fmdist.shutdown()
 
 
-@pytest.mark.parametrize("world,variant", [(2, dict()), (2, dict(prefetch_rows="off", overlap_grads="off")),
-                                           (4, dict()), (3, dict(dtype="bf16")), (2, dict(dtype="fp8"))])
+@pytest.mark.parametrize("world,variant", [
+    (2, dict()), (2, dict(prefetch_rows="off")), (4, dict()), (3, dict(dtype="bf16")), (2, dict(dtype="fp8")),
+    (3, dict(overlap_grads="on")), (2, dict(overlap_grads="on", env={"FM_SELF_ROWS": "0"})),
+    (3, dict(dtype="bf16", env={"FM_SELF_ROWS": "0"}))])
 def test_ranks_on_one_gpu_equal_one_process(tmp_path, world, variant):
+    """Self rows (the default) at world 2-4: each rank reads its own rows from its table and
+    updates the ones no other rank requested in place; FM_SELF_ROWS=0 exchanges them too."""
     from fast_tffm_amd.data.batch import Batch
     from fast_tffm_amd.models.fm import FactorizationMachine
 
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), variant), nprocs=world, join=True)
     res = [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(world)]
-    if "prefetch_rows" not in variant:  # defaults at world > 1: early row exchange + split backward both on
-        assert all(r["early"] == STEPS - 1 and r["split"] for r in res)
+    if "prefetch_rows" not in variant:  # default at world > 1: early row exchange on
+        assert all(r["early"] == STEPS - 1 for r in res)
+    assert all(r["split"] == (variant.get("overlap_grads") == "on") for r in res)  # (split backward: opt-in)
     ref = FactorizationMachine(_cfg("local", B * world, dtype=variant.get("dtype", "fp32")), device="cuda")
     for s in range(STEPS):
         parts = [_batch(s, r) for r in range(world)]
