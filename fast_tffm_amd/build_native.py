@@ -39,7 +39,8 @@ HIP_VARIANTS: dict[str, list[str]] = {"nocap": ["-DFM_CHUNK_NOCAP"], "capf32": [
                                       "unr4": ["-DFM_CHUNK_UNR=4"], "unr6": ["-DFM_CHUNK_UNR=6"],
                                       "unr16": ["-DFM_CHUNK_UNR=16"], "unr12": ["-DFM_CHUNK_UNR=12"],
                                       "fwdw5": ["-DFM_FWD_WAVES_LPR16=5"],
-                                      "fwdw6": ["-DFM_FWD_WAVES_LPR16=6"], "noshort": ["-DFM_NO_SHORT_CHUNK"]}
+                                      "fwdw6": ["-DFM_FWD_WAVES_LPR16=6"], "noshort": ["-DFM_NO_SHORT_CHUNK"],
+                                      "fp8packed": ["-DFM_FWD_FP8_PACKED=1"]}
 
 
 _EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"  # resolved once (lazy init is not thread-safe)

@@ -49,7 +49,7 @@ struct BwdArgs {
   int ex_shift;             // > 0: sorted_ex holds packed codes (example << ex_shift | slot)
   const float* sorted_x;    // [nnz] value of each sorted occurrence or nullptr (=1)
   const float* dpred;       // [B]
-  const float* r1;          // [B, Kp]
+  const void* r1;           // [B, Kp] fp32 (bf16 for fp8 tables: R1Bf16)
   int Kp;
   void* v;                  // LOCAL: table (read/write); EMIT: gathered rows (read)
   long long v_stride;
@@ -355,12 +355,7 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
           const float cs = __shfl(pc[q], src, kWave);
           cc[uu] = ok ? cs : 0.f;
           xx[uu] = __shfl(px[q], src, kWave);
-          const float* rp = a.r1 + (long long)ex * a.Kp + tE * EPL;
-#pragma unroll
-          for (int k = 0; k < EPL; k += 4) {
-            const float4 f = *reinterpret_cast<const float4*>(rp + k);
-            rr[uu][k] = f.x; rr[uu][k + 1] = f.y; rr[uu][k + 2] = f.z; rr[uu][k + 3] = f.w;
-          }
+          load_r1<TV, EPL>(a.r1, (long long)ex * a.Kp + tE * EPL, rr[uu]);
         }
 #pragma unroll
         for (int uu = 0; uu < UNRF; ++uu) {
@@ -387,12 +382,7 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
         const float cs = __shfl(pc[0], src, kWave);
         cc[uu] = ok ? cs : 0.f;
         xx[uu] = __shfl(px[0], src, kWave);
-        const float* rp = a.r1 + (long long)ex * a.Kp + tE * EPL;
-#pragma unroll
-        for (int k = 0; k < EPL; k += 4) {
-          const float4 f = *reinterpret_cast<const float4*>(rp + k);
-          rr[uu][k] = f.x; rr[uu][k + 1] = f.y; rr[uu][k + 2] = f.z; rr[uu][k + 3] = f.w;
-        }
+        load_r1<TV, EPL>(a.r1, (long long)ex * a.Kp + tE * EPL, rr[uu]);
       }
 #pragma unroll
       for (int uu = 0; uu < U4; ++uu) {
@@ -418,12 +408,7 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
               const float cs = __shfl(pc[q], src, kWave);
               cc[uu] = ok ? cs : 0.f;
               xx[uu] = __shfl(px[q], src, kWave);
-              const float* rp = a.r1 + (long long)ex * a.Kp + tE * EPL;
-#pragma unroll
-              for (int k = 0; k < EPL; k += 4) {
-                const float4 f = *reinterpret_cast<const float4*>(rp + k);
-                rr[uu][k] = f.x; rr[uu][k + 1] = f.y; rr[uu][k + 2] = f.z; rr[uu][k + 3] = f.w;
-              }
+              load_r1<TV, EPL>(a.r1, (long long)ex * a.Kp + tE * EPL, rr[uu]);
             }
 #pragma unroll
             for (int uu = 0; uu < UNR; ++uu) {
@@ -508,12 +493,7 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_cold_kernel(BwdArgs a) {
       const float cs = __shfl(pc, src, kWave);
       cc[uu] = ok ? cs : 0.f;
       xx[uu] = __shfl(px, src, kWave);
-      const float* rp = a.r1 + (long long)ex * a.Kp + tE * EPL;
-#pragma unroll
-      for (int k = 0; k < EPL; k += 4) {
-        const float4 f = *reinterpret_cast<const float4*>(rp + k);
-        rr[uu][k] = f.x; rr[uu][k + 1] = f.y; rr[uu][k + 2] = f.z; rr[uu][k + 3] = f.w;
-      }
+      load_r1<TV, EPL>(a.r1, (long long)ex * a.Kp + tE * EPL, rr[uu]);
     }
     float A[EPL];
 #pragma unroll
@@ -748,12 +728,12 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_dense_kernel(BwdArgs a) {
       if (qd < kq) {
         if (ea < e_end) {
           const float d = a.dpred[ea];
-          const float4 r = *reinterpret_cast<const float4*>(a.r1 + (long long)ea * a.Kp + 4 * qd);
+          const float4 r = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.r1) + (long long)ea * a.Kp + 4 * qd);
           fa[0] = d * r.x; fa[1] = d * r.y; fa[2] = d * r.z; fa[3] = d * r.w;
         }
         if (eb < e_end) {
           const float d = a.dpred[eb];
-          const float4 r = *reinterpret_cast<const float4*>(a.r1 + (long long)eb * a.Kp + 4 * qd);
+          const float4 r = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.r1) + (long long)eb * a.Kp + 4 * qd);
           fb[0] = d * r.x; fb[1] = d * r.y; fb[2] = d * r.z; fb[3] = d * r.w;
         }
       }
@@ -903,7 +883,7 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   const bool fork = dense && dense_st && dense_st != st;
   hipStream_t ds = fork ? dense_st : st;
   if (dense) {
-    if (a.Kp > 128 || a.Kp % 4 != 0) return -5;
+    if (a.Kp > 128 || a.Kp % 4 != 0 || dtype == kFP8) return -5;  // (fp32 r1 only: not with fp8 tables)
     if (fork) {
       (void)hipEventRecord(dense_fork_event(), st);
       (void)hipStreamWaitEvent(ds, dense_fork_event(), 0);

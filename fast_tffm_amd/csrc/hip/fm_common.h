@@ -127,12 +127,12 @@ template <> struct Frag<__hip_bfloat16> {
 template <> struct Frag<fp8e4m3> {
   static constexpr int N = 4;
   static constexpr bool kScaled = true;
-  __device__ static inline void load(const fp8e4m3* p, float (&o)[4]) {
-    const int u = *reinterpret_cast<const int*>(p);
+  __device__ static inline void cvt(int u, float (&o)[4]) {
     const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8(u, false);
     const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8(u, true);
     o[0] = lo[0]; o[1] = lo[1]; o[2] = hi[0]; o[3] = hi[1];
   }
+  __device__ static inline void load(const fp8e4m3* p, float (&o)[4]) { cvt(*reinterpret_cast<const int*>(p), o); }
   __device__ static inline void store(fp8e4m3* p, const float (&o)[4]) {
     int u = __builtin_amdgcn_cvt_pk_fp8_f32(o[0], o[1], 0, false);
     u = __builtin_amdgcn_cvt_pk_fp8_f32(o[2], o[3], u, true);
@@ -163,6 +163,52 @@ __device__ inline float group_max(float v) {
 #pragma unroll
   for (int o = WIDTH / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
   return v;
+}
+
+// r1 = sum_j x_j v_j of every example, written by the forward and gathered once per
+// occurrence by the backward (its largest stream: 5.1M rows of a Criteo-shaped batch).
+// fp32 for fp32 / bf16 tables; bf16 for fp8 tables, whose factors carry 3 mantissa bits:
+// r1's rounding (2^-9 relative) stays far below the table's own quantisation step (2^-4)
+// and the gather halves (k=128: 512 -> 256 B per occurrence).
+template <typename TV> struct R1Bf16 { static constexpr bool v = false; };
+template <> struct R1Bf16<fp8e4m3> { static constexpr bool v = true; };
+
+template <typename TV, int EPL>
+__device__ inline void load_r1(const void* r1, long long off, float (&o)[EPL]) {
+  if constexpr (R1Bf16<TV>::v) {
+    const uint16_t* p = reinterpret_cast<const uint16_t*>(r1) + off;
+#pragma unroll
+    for (int k = 0; k < EPL; k += 4) {
+      const uint2 h = *reinterpret_cast<const uint2*>(p + k);
+      o[k] = bf16_bits_to_f32(h.x & 0xffffu); o[k + 1] = bf16_bits_to_f32(h.x >> 16);
+      o[k + 2] = bf16_bits_to_f32(h.y & 0xffffu); o[k + 3] = bf16_bits_to_f32(h.y >> 16);
+    }
+  } else {
+    const float* p = reinterpret_cast<const float*>(r1) + off;
+#pragma unroll
+    for (int k = 0; k < EPL; k += 4) {
+      const float4 f = *reinterpret_cast<const float4*>(p + k);
+      o[k] = f.x; o[k + 1] = f.y; o[k + 2] = f.z; o[k + 3] = f.w;
+    }
+  }
+}
+
+template <typename TV, int EPL>
+__device__ inline void store_r1(void* r1, long long off, const float (&s)[EPL]) {
+  if constexpr (R1Bf16<TV>::v) {
+    uint16_t* p = reinterpret_cast<uint16_t*>(r1) + off;
+#pragma unroll
+    for (int k = 0; k < EPL; k += 4) {
+      uint2 h;
+      h.x = f32_to_bf16_bits(s[k]) | (f32_to_bf16_bits(s[k + 1]) << 16);
+      h.y = f32_to_bf16_bits(s[k + 2]) | (f32_to_bf16_bits(s[k + 3]) << 16);
+      *reinterpret_cast<uint2*>(p + k) = h;
+    }
+  } else {
+    float* p = reinterpret_cast<float*>(r1) + off;
+#pragma unroll
+    for (int k = 0; k < EPL; k += 4) *reinterpret_cast<float4*>(p + k) = make_float4(s[k], s[k + 1], s[k + 2], s[k + 3]);
+  }
 }
 
 // Dequantisation factor of a table row (1 for unscaled dtypes).

@@ -28,7 +28,7 @@ struct FwdArgs {
   int loss_type;        // LossType
   float grad_scale;     // dL/dpred scale (1/B for a batch mean)
   float* pred;          // [B]
-  float* r1;            // [B, Kp] fp32 or nullptr
+  void* r1;             // [B, Kp] fp32 (bf16 for fp8 tables: R1Bf16) or nullptr
   float* dpred;         // [B] or nullptr
   float* loss_partial;  // [gridDim.x] or nullptr
   float* reg_partial;   // [2*gridDim.x] (sum |v|^2, sum w^2) or nullptr
@@ -44,6 +44,11 @@ struct FwdArgs {
   SelfRows self;           // row-sharded step: segments read from this rank's own table rows
 };
 
+// A/B build knob (variant "fp8packed"): fp8 rows kept packed in flight, a whole example per
+// round.  Measured slower: k128 fp8 FTRL step 0.93 -> 1.04 ms (profiles/r2/fp8_forward_ab.txt)
+#ifndef FM_FWD_FP8_PACKED
+#define FM_FWD_FP8_PACKED 0
+#endif
 constexpr int kSelfBit = (int)0x80000000u;   // row index tag: this rank's own table row (SelfRows)
 constexpr int kDenseHash = 4 * kMaxDense;  // open-addressing table of the dense keys (LDS, load <= 1/4)
 
@@ -83,13 +88,22 @@ constexpr int fwd_min_waves() {
   return LPR >= 32 ? 4 : 1;
 }
 
+// FM_FWD_FP8_PACKED: fp8 rows stay packed while in flight (one VGPR per row per lane instead
+// of four, converted at use), so a whole Criteo-shaped example is issued in one round:
+// ceil(40 / G) rows per lane group, up to 24 (k=128: 20 instead of 12).
+template <int G>
+struct FwdUnrollPacked {
+  static constexpr int v = ((40 + G - 1) / G) > 24 ? 24 : ((40 + G - 1) / G);
+};
+
 template <int LPR, typename TV>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(fwd_min_waves<LPR, TV>())))
 void fm_fwd_kernel(FwdArgs a) {
   using F = Frag<TV>;
   constexpr int EPL = F::N;
   constexpr int G = kWave / LPR;
-  constexpr int UNR = FwdUnroll<G>::v;
+  constexpr bool kPacked = F::kScaled && FM_FWD_FP8_PACKED;
+  constexpr int UNR = kPacked ? FwdUnrollPacked<G>::v : FwdUnroll<G>::v;
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR, t = lane % LPR;
   const int nv = a.Kp / EPL;
@@ -159,7 +173,8 @@ void fm_fwd_kernel(FwdArgs a) {
         if (h >= 0) atomicAdd(&dcnt[wv][h], 1u);  // integer: order-independent
       }
       for (int q = 0; q < m; q += G * UNR) {
-        float fr[UNR][EPL], fx[UNR], fs[UNR];
+        float fr[kPacked ? 1 : UNR][EPL], fx[UNR], fs[UNR];
+        int raw[kPacked ? UNR : 1];
         // Issue every row load of the round before the first use.  Loads are
         // unconditional (slots past the example re-read a valid row of it and are
         // masked to zero afterwards), so hipcc keeps all UNR loads in flight.
@@ -171,27 +186,31 @@ void fm_fwd_kernel(FwdArgs a) {
           const float x = __shfl(my_x, src, kWave);
           fx[u] = f < m ? x : 0.f;
           // (one load either way: the tagged index selects the base, not the instruction)
-          F::load(row < 0 ? tbase + (long long)(row & ~kSelfBit) * a.self.v_stride
-                          : vbase + (long long)row * a.v_stride, fr[u]);
+          const TV* rp = row < 0 ? tbase + (long long)(row & ~kSelfBit) * a.self.v_stride
+                                 : vbase + (long long)row * a.v_stride;
+          if constexpr (kPacked) raw[u] = *reinterpret_cast<const int*>(rp);
+          else F::load(rp, fr[u]);
           if constexpr (F::kScaled) fs[u] = __shfl(my_s, src, kWave);
         }
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
+          float (&fv)[EPL] = fr[kPacked ? 0 : u];
+          if constexpr (kPacked) F::cvt(raw[u], fv);
           if constexpr (F::kScaled) {
 #pragma unroll
-            for (int k = 0; k < EPL; ++k) fr[u][k] *= fs[u];
+            for (int k = 0; k < EPL; ++k) fv[k] *= fs[u];
           }
           const float xm = fx[u] * tmask;
 #pragma unroll
           for (int k = 0; k < EPL; ++k) {
-            const float xv = xm * fr[u][k];
+            const float xv = xm * fv[k];
             s1[k] += xv;
             s2[k] += xv * xv;
           }
           if (want_reg) {
             const float ok = (q + u * G + g) < m ? 1.f : 0.f;
 #pragma unroll
-            for (int k = 0; k < EPL; ++k) rv += ok * tmask * fr[u][k] * fr[u][k];
+            for (int k = 0; k < EPL; ++k) rv += ok * tmask * fv[k] * fv[k];
           }
         }
       }
@@ -218,12 +237,7 @@ void fm_fwd_kernel(FwdArgs a) {
     part = group_sum<LPR>(part);
     lin = group_sum<kWave>(lin);
     const float pred = lin + 0.5f * part + (a.bias ? a.bias[0] : 0.f);
-    if (a.r1 != nullptr && g == 0 && tact) {
-      float* dst = a.r1 + (long long)i * a.Kp + t * EPL;
-#pragma unroll
-      for (int k = 0; k < EPL; k += 4)
-        *reinterpret_cast<float4*>(dst + k) = make_float4(s1[k], s1[k + 1], s1[k + 2], s1[k + 3]);
-    }
+    if (a.r1 != nullptr && g == 0 && tact) store_r1<TV, EPL>(a.r1, (long long)i * a.Kp + t * EPL, s1);
     if (want_reg) {
       rv = group_sum<kWave>(rv);
       rw = group_sum<kWave>(rw);

@@ -96,7 +96,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
         a.w = P<const float>(w); a.w_stride = w_stride; a.Kp = Kp;
         a.labels = P<const float>(labels); a.weights = P<const float>(weights);
         a.loss_type = loss_type; a.grad_scale = grad_scale; a.pred = P<float>(pred);
-        a.r1 = P<float>(r1); a.dpred = P<float>(dpred); a.loss_partial = P<float>(loss_partial);
+        a.r1 = P<void>(r1); a.dpred = P<float>(dpred); a.loss_partial = P<float>(loss_partial);
         a.reg_partial = P<float>(reg_partial); a.bias = P<const float>(bias);
         check(fm::launch_fwd(a, dtype, grid, S(stream)), "fm_fwd");
       },
@@ -134,7 +134,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
         a.seg_start = P<const int>(seg_start);
         a.seg_chunk = P<const int>(seg_chunk); a.uniq = P<const int>(uniq);
         a.sorted_ex = P<const int>(sorted_ex); a.ex_shift = ex_shift; a.sorted_x = P<const float>(sorted_x);
-        a.dpred = P<const float>(dpred); a.r1 = P<const float>(r1); a.Kp = Kp;
+        a.dpred = P<const float>(dpred); a.r1 = P<const void>(r1); a.Kp = Kp;
         a.v = P<void>(v); a.v_stride = v_stride; a.w = P<float>(w); a.w_stride = w_stride;
         a.s0v = P<float>(s0v); a.s1v = P<float>(s1v); a.s_stride = s_stride; a.s0w = P<float>(s0w);
         a.s1w = P<float>(s1w); a.reg_v = reg_v; a.reg_w = reg_w;

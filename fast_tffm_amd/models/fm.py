@@ -89,8 +89,8 @@ class StepOut:
 class _Workspace:
     """Per-step buffers, grown on demand and then reused (no per-step allocation)."""
 
-    def __init__(self, device: torch.device, Kp: int, CH: int):
-        self.device, self.Kp, self.CH = device, Kp, CH
+    def __init__(self, device: torch.device, Kp: int, CH: int, r1_dtype: torch.dtype = torch.float32):
+        self.device, self.Kp, self.CH, self.r1_dtype = device, Kp, CH, r1_dtype
         self.cap_b = self.cap_n = 0
 
     def ensure(self, B: int, nnz: int) -> None:
@@ -99,7 +99,7 @@ class _Workspace:
             cap = max(B, int(self.cap_b * 1.25))
             self.pred = torch.empty(cap, dtype=torch.float32, device=dev)
             self.dpred = torch.empty(cap, dtype=torch.float32, device=dev)
-            self.r1 = torch.empty((cap, Kp), dtype=torch.float32, device=dev)
+            self.r1 = torch.empty((cap, Kp), dtype=self.r1_dtype, device=dev)
             # dense-row occurrence counts (forward -> MFMA backward), GPU only
             self._dense_A = (torch.empty((cap, K.MAX_DENSE), dtype=torch.uint8, device=dev)
                              if dev.type == "cuda" else None)
@@ -286,7 +286,7 @@ class FactorizationMachine:
                              init_range=cfg.init_value_range, seed=cfg.seed, device=self.device)
         self.K, self.Kp = self.table.K, self.table.Kp
         self.rps = rows_per_shard(cfg.vocabulary_size, self.world) if sharded else cfg.vocabulary_size
-        self.ws = _Workspace(self.device, self.Kp, cfg.dedup_chunk)
+        self.ws = _Workspace(self.device, self.Kp, cfg.dedup_chunk, K.r1_dtype(cfg.dtype))
         self.global_step = 0
         self._side = None
         self._lslots = [_LocalSlot(), _LocalSlot()]   # lookahead dedup plans (eager local path)
@@ -556,7 +556,8 @@ class FactorizationMachine:
         ex = K.csr_rows(b.offsets, out=slot.dd.ex_of_occ[: b.nnz], nnz=b.nnz, slot_bits=sb)
         dd = K.dedup(rows, ws=slot.dd, key_bits=bits_for(self.table.rows), ex_of_occ=ex, vals=b.vals,
                      num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets,
-                     dense_min=K.dense_min_for(b.B, self.Kp, cfg.dedup_chunk, has_vals=b.vals is not None,
+                     dense_min=K.dense_min_for(b.B, self.Kp, cfg.dedup_chunk, table_dtype=self.table.v.dtype,
+                                               has_vals=b.vals is not None,
                                                max_feats=b.max_feats))
         return rows, dd
 

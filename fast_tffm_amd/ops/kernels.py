@@ -63,6 +63,13 @@ def padded_k(K: int, dtype: torch.dtype = torch.float32) -> int:
     return ((K + e - 1) // e) * e
 
 
+def r1_dtype(table_dtype: torch.dtype) -> torch.dtype:
+    """Storage dtype of the forward's r1 cache [B, Kp] for a table dtype: fp32, or bf16 for fp8
+    tables (3-bit factor mantissas; bf16 r1 halves the backward's per-occurrence gather --
+    hip/fm_common.h R1Bf16)."""
+    return torch.bfloat16 if table_dtype == FP8 else torch.float32
+
+
 def quantize_fp8_rows(vals: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
     """Per-row fp8 quantisation (the kernels' store_row): scale = max|v| / 448, q = rne(v / scale)."""
     v = vals.float()
@@ -191,7 +198,10 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
     if pred is None:
         pred = torch.empty(B, dtype=torch.float32, device=dev)
     if want_r1 and r1 is None:
-        r1 = torch.empty((B, Kp), dtype=torch.float32, device=dev)
+        r1 = torch.empty((B, Kp), dtype=r1_dtype(v.dtype), device=dev)
+    if want_r1:
+        _check(r1.dtype == r1_dtype(v.dtype) and r1.is_contiguous() and r1.shape[1] == Kp and r1.shape[0] >= B,
+               f"r1: contiguous [B, Kp] {r1_dtype(v.dtype)} for a {v.dtype} table")
     if not want_r1:
         r1 = None
     if lt and dpred is None:
@@ -336,7 +346,7 @@ DENSE_WG = 256             # = fm::kDenseWG: workgroups (partial rows) of the de
 
 
 def dense_min_for(num_examples: int, Kp: int, CH: int = 32, *, has_vals: bool = False,
-                  max_feats: int = 0) -> int:
+                  max_feats: int = 0, table_dtype: torch.dtype = torch.float32) -> int:
     """Occurrence threshold of the MFMA backward rows (0 = off).
 
     A row present in >= 2.5% of the batch's examples (>= B/40 occurrences; the first
@@ -345,9 +355,9 @@ def dense_min_for(num_examples: int, Kp: int, CH: int = 32, *, has_vals: bool = 
     ~47% of the occurrences, whose r1 rows the occurrence-gather backward would fetch one by
     one.  Needs binary features (the forward counts occurrences: x = 1), fewer than 256
     features per example (byte counts, exact in bf16), Kp <= 128 (the tile's N) and a batch
-    that fills the 256 tile workgroups.  Opt-in: FM_DENSE_BWD=1."""
+    that fills the 256 tile workgroups, and an fp32 r1 (not fp8 tables).  Opt-in: FM_DENSE_BWD=1."""
     if (os.environ.get("FM_DENSE_BWD", "0") != "1" or has_vals or Kp > 128 or Kp % 4 or num_examples < 16384
-            or max_feats > 255):
+            or max_feats > 255 or r1_dtype(table_dtype) != torch.float32):
         return 0
     return max(8 * CH, num_examples // 40)
 SLICE_BYTES = 2 << 20      # r1 bytes per example slice of the XCD-sliced backward (XCD L2 = 4 MB)
@@ -518,7 +528,7 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
     dev = dpred.device
     _check(dd.sorted_ex is not None, "dedup must be run with ex_of_occ")
     _chk_vec(dpred, torch.float32, None, "dpred", dev)
-    _check(r1.dtype == torch.float32 and r1.is_contiguous() and r1.shape[1] == Kp, "r1: [B, Kp] fp32 contiguous")
+    _check(r1.is_contiguous() and r1.shape[1] == Kp, "r1: [B, Kp] contiguous")
     if mode == BWD_EMIT_TABLE:
         _check(_is_gpu(dpred) and table is not None and grad_out is not None,
                "EMIT_TABLE mode: GPU, table (parameter rows) + dense grad_out")
@@ -561,6 +571,8 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
             _check(s0v is not None and s0w is not None, "self rows: the table's optimizer state")
             s_stride = s0v.stride(0)
     v_stride = _chk_rows(v, Kp, "v")
+    _check(r1.dtype == r1_dtype(v.dtype), f"r1: {r1_dtype(v.dtype)} for {v.dtype} rows (the forward's r1)")
+    _check(r1.dtype == torch.float32 or dd.dense_list is None, "the dense-row MFMA backward reads an fp32 r1")
     o = opt or OptConfig()
     if piece >= 0:
         _check(_is_gpu(dpred) and seg_bounds is not None and mode == BWD_EMIT and dd.slice_list is None

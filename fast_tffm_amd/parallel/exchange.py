@@ -384,6 +384,7 @@ class ShardExchange(_Base):
                                   vals=sb.vals if ex is not None else None, want_inv=True, num_examples=sb.B,
                                   Kp=self.m.Kp, ex_shift=shift, offsets=sb.offsets if shift else None,
                                   dense_min=K.dense_min_for(sb.B, self.m.Kp, m.cfg.dedup_chunk,
+                                                            table_dtype=m.table.v.dtype,
                                                             has_vals=sb.vals is not None,
                                                             max_feats=sb.max_feats) if train else 0)
                 counts.append(K.owner_counts(part.dd, self.Rps, self.W))
