@@ -174,7 +174,29 @@ TextLoader::TextLoader(LoaderOptions o) : o_(std::move(o)) {
   if (o_.binary && o_.raw) throw std::invalid_argument("raw (GPU tokenizer) mode needs text files");
   if (o_.rows && !o_.binary) throw std::invalid_argument("rows mode needs binary CSR caches");
   if (o_.queue_size < 1) o_.queue_size = 1;
+  if (!o_.raw_slots.empty() && !o_.raw) throw std::invalid_argument("raw slots need raw mode");
+  for (size_t s = 0; s < o_.raw_slots.size(); ++s) free_slots_.push_back(static_cast<int>(s));
   th_ = std::thread([this] { run(); });
+}
+
+int TextLoader::acquire_slot() {
+  std::unique_lock<std::mutex> lk(mu_);
+  cv_slot_.wait(lk, [&] { return stop_ || !free_slots_.empty(); });
+  if (stop_) return -1;
+  const int s = free_slots_.front();
+  free_slots_.pop_front();
+  return s;
+}
+
+void TextLoader::release(int slot) {
+  if (slot < 0 || slot >= static_cast<int>(o_.raw_slots.size())) throw std::out_of_range("raw slot");
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int s : free_slots_)
+      if (s == slot) throw std::logic_error("raw slot released twice");
+    free_slots_.push_back(slot);
+  }
+  cv_slot_.notify_one();
 }
 
 TextLoader::~TextLoader() { close(); }
@@ -186,6 +208,7 @@ void TextLoader::close() {
   }
   cv_put_.notify_all();
   cv_get_.notify_all();
+  cv_slot_.notify_all();
   if (th_.joinable()) th_.join();
 }
 
@@ -323,17 +346,38 @@ void TextLoader::run() {
         LoadedBatch b;
         if (o_.raw) {
           // offsets first, then the line copies in parallel (one thread copying ~15 MB of
-          // 300-byte lines per 50k-line batch capped the GPU-tokenizer path near 1e7 ex/s)
-          b.line_start.resize(n + 1);
+          // 300-byte lines per 50k-line batch capped the GPU-tokenizer path near 1e7 ex/s);
+          // into a caller's (pinned) slot when one is configured and the batch fits
+          size_t total = 0;
+          for (size_t i = 0; i < n; ++i) total += lens[i] + 1;
+          int64_t* ls = nullptr;
+          uint8_t* dst = nullptr;
+          if (!o_.raw_slots.empty()) {
+            const int s = acquire_slot();
+            if (s < 0) return false;  // stopped
+            const RawSlot& rs = o_.raw_slots[static_cast<size_t>(s)];
+            if (total <= rs.bytes_cap && n + 1 <= rs.ls_cap) {
+              b.slot = s;
+              ls = rs.line_start;
+              dst = rs.bytes;
+            } else {
+              release(s);
+            }
+          }
+          if (b.slot < 0) {
+            b.line_start.resize(n + 1);
+            b.bytes.resize(total);
+            ls = b.line_start.data();
+            dst = b.bytes.data();
+          }
           size_t off = 0;
           for (size_t i = 0; i < n; ++i) {
-            b.line_start[i] = static_cast<int64_t>(off);
+            ls[i] = static_cast<int64_t>(off);
             off += lens[i] + 1;
           }
-          b.line_start[n] = static_cast<int64_t>(off);
-          b.bytes.resize(off);
-          uint8_t* dst = b.bytes.data();
-          const int64_t* ls = b.line_start.data();
+          ls[n] = static_cast<int64_t>(off);
+          b.nbytes = off;
+          b.nlines = n;
 #pragma omp parallel for num_threads(std::max(1, o_.threads)) schedule(static, 1024) if (n >= 4096)
           for (long long i = 0; i < (long long)n; ++i) {
             std::memcpy(dst + ls[i], ptrs[i], lens[i]);

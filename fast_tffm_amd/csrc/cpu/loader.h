@@ -43,6 +43,16 @@
 
 namespace fm {
 
+// Caller-owned output buffers of raw mode (e.g. page-locked host memory the GPU copies from):
+// a batch is assembled straight into a free slot, so it needs no staging copy before its
+// host-to-device transfer.  The consumer returns a slot with release() once the copy is done.
+struct RawSlot {
+  uint8_t* bytes = nullptr;
+  size_t bytes_cap = 0;
+  int64_t* line_start = nullptr;
+  size_t ls_cap = 0;          // entries (lines + 1)
+};
+
 struct LoaderOptions {
   std::vector<std::string> files;
   std::vector<std::string> weight_files;  // empty, or one per data file
@@ -61,6 +71,7 @@ struct LoaderOptions {
   bool raw = false;           // emit the batch's line bytes (GPU tokenizer) instead of parsed CSR
   bool binary = false;        // files are .fmb binary CSR caches (weights inside; weight_files empty)
   bool rows = false;          // binary: emit row numbers + offsets instead of the data
+  std::vector<RawSlot> raw_slots;  // raw mode: assemble into these (a batch too large for a slot: heap)
 };
 
 struct LoadedBatch {
@@ -76,6 +87,9 @@ struct LoadedBatch {
   std::vector<int64_t> rows;
   bool has_vals = false;
   int max_feats = 0;
+  // raw mode into a RawSlot: its index, bytes and lines (bytes / line_start above stay empty)
+  int slot = -1;
+  size_t nbytes = 0, nlines = 0;
   int epoch = 0;
   int64_t count = 0;              // batches of this epoch consumed after this one
 };
@@ -95,10 +109,16 @@ class TextLoader {
   // reference's -m "shuffle_queue" figure (run_tffm.py:52-63, shuffle_batch queue size).
   float window_fill() const { return fill_.load(std::memory_order_relaxed); }
   void close();
+  // Raw slots: hand slot `s` (of a batch returned by next()) back to the producer.
+  void release(int slot);
 
  private:
   void run();
   bool push(LoadedBatch&& b);
+  int acquire_slot();         // a free raw slot (blocks), -1 once stopped
+
+  std::deque<int> free_slots_;
+  std::condition_variable cv_slot_;
 
   LoaderOptions o_;
   std::thread th_;

@@ -201,20 +201,29 @@ PYBIND11_MODULE(_fm_cpu, m) {
       .def(py::init([](std::vector<std::string> files, std::vector<std::string> weight_files, long long batch_size,
                        long long vocab_size, bool hash_feature_id, bool shuffle, int num_epochs,
                        unsigned long long seed, int threads, int rank, int world, int queue_size, int start_epoch,
-                       long long skip_batches, bool raw, bool binary, bool rows) {
+                       long long skip_batches, bool raw, bool binary, bool rows,
+                       std::vector<std::vector<unsigned long long>> raw_slots) {
              fm::LoaderOptions o;
              o.files = std::move(files); o.weight_files = std::move(weight_files); o.batch_size = batch_size;
              o.vocab_size = vocab_size; o.hash_feature_id = hash_feature_id; o.shuffle = shuffle;
              o.num_epochs = num_epochs; o.seed = seed; o.threads = threads; o.rank = rank; o.world = world;
              o.queue_size = queue_size; o.start_epoch = start_epoch; o.skip_batches = skip_batches; o.raw = raw;
              o.binary = binary; o.rows = rows;
+             for (const auto& s : raw_slots) {  // [bytes ptr, bytes cap, line_start ptr, line_start entries]
+               if (s.size() != 4 || !s[0] || !s[2]) throw std::invalid_argument("raw slot: [bytes, cap, ls, cap]");
+               fm::RawSlot r;
+               r.bytes = reinterpret_cast<uint8_t*>(s[0]); r.bytes_cap = s[1];
+               r.line_start = reinterpret_cast<int64_t*>(s[2]); r.ls_cap = s[3];
+               o.raw_slots.push_back(r);
+             }
              return new fm::TextLoader(std::move(o));
            }),
            py::arg("files"), py::arg("weight_files"), py::arg("batch_size"), py::arg("vocab_size"),
            py::arg("hash_feature_id") = false, py::arg("shuffle") = true, py::arg("num_epochs") = 1,
            py::arg("seed") = 0, py::arg("threads") = 4, py::arg("rank") = 0, py::arg("world") = 1,
            py::arg("queue_size") = 4, py::arg("start_epoch") = 0, py::arg("skip_batches") = 0,
-           py::arg("raw") = false, py::arg("binary") = false, py::arg("rows") = false)
+           py::arg("raw") = false, py::arg("binary") = false, py::arg("rows") = false,
+           py::arg("raw_slots") = std::vector<std::vector<unsigned long long>>{})
       // -> (labels, offsets, ids, vals | None, weights | None, max_feats, epoch, count) or None at the end
       .def("next",
            [](fm::TextLoader& L) -> py::object {
@@ -229,6 +238,10 @@ PYBIND11_MODULE(_fm_cpu, m) {
                return py::make_tuple(to_numpy(std::move(b.rows)), to_numpy(std::move(b.offsets)), b.has_vals,
                                      b.max_feats, b.epoch, b.count);
              }
+             if (b.slot >= 0) {  // raw mode into a slot: (slot, nbytes, nlines, weights | None, epoch, count)
+               py::object w = b.weights.empty() ? py::object(py::none()) : py::object(to_numpy(std::move(b.weights)));
+               return py::make_tuple(b.slot, b.nbytes, b.nlines, w, b.epoch, b.count);
+             }
              if (!b.line_start.empty()) {  // raw mode: (bytes, line_start, weights | None, epoch, count)
                py::object w = b.weights.empty() ? py::object(py::none()) : py::object(to_numpy(std::move(b.weights)));
                return py::make_tuple(to_numpy(std::move(b.bytes)), to_numpy(std::move(b.line_start)), w, b.epoch,
@@ -240,6 +253,7 @@ PYBIND11_MODULE(_fm_cpu, m) {
                                    to_numpy(std::move(b.ids)), vals, w, b.max_feats, b.epoch, b.count);
            })
       .def("queued", &fm::TextLoader::queued)
+      .def("release", &fm::TextLoader::release, py::arg("slot"))
       .def("window_fill", &fm::TextLoader::window_fill)
       .def("close", [](fm::TextLoader& L) {
         py::gil_scoped_release nogil;

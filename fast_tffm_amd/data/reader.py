@@ -262,10 +262,32 @@ class NativeTextReader:
         """Shuffle-window fill (0..1) at the loader's latest draw (-m "shuffle_queue")."""
         return float(self._loader.window_fill()) if self._loader is not None else 0.0
 
+    def _raw_slots(self) -> list[list[int]]:
+        """Page-locked output slots of the loader's raw mode (GPU tokenizer): batches are assembled
+        straight into them, so the host-to-device copy needs no staging copy.  queue_size + 3
+        slots (queued batches, the one being copied / parsed, the one being finished, one spare)
+        of 1.5x the batch's estimated bytes (average line length of the first file's head); a
+        larger batch falls back to a heap buffer."""
+        if getattr(self, "_slots", None) is None:
+            B = self.args["batch_size"]
+            avg = 256.0
+            try:
+                with open(self.args["files"][0], "rb") as f:
+                    head = f.read(4 << 20)
+                avg = max(16.0, len(head) / max(1, head.count(b"\n")))
+            except OSError:
+                pass
+            nb, nl = int(B * avg * 1.5) + 4096, B + 1
+            self._slots = [(torch.empty(nb, dtype=torch.uint8, pin_memory=True),
+                            torch.empty(nl, dtype=torch.int64, pin_memory=True))
+                           for _ in range(self.args["queue_size"] + 3)]
+        return [[b.data_ptr(), b.numel(), ls.data_ptr(), ls.numel()] for b, ls in self._slots]
+
     def __iter__(self):
+        slots = self._raw_slots() if self.gpu is not None else []
         L = native.cpu().TextLoader(start_epoch=self.state.epoch, skip_batches=self.state.batches_in_epoch,
                                     raw=self.gpu is not None, binary=self.binary, rows=self.dds is not None,
-                                    **self.args)
+                                    raw_slots=slots, **self.args)
         self._loader = L
         dev = self.gpu if self.gpu is not None else (self.dds.device if self.dds is not None else None)
         stream = torch.cuda.Stream(dev) if dev is not None else None
@@ -339,25 +361,33 @@ class NativeTextReader:
         return hb, hl
 
     def _gpu_launch(self, item, stream):
-        """Stage the raw lines of a loader item in pinned memory, copy them to the device and
-        launch the GPU tokenizer on ``stream`` -- without waiting: the host stages the next
-        batch while this one is copied and parsed (``_gpu_finish`` collects it)."""
+        """Copy the raw lines of a loader item to the device (from its page-locked slot, or staged
+        there first when the batch did not fit one) and launch the GPU tokenizer on ``stream`` --
+        without waiting: the host takes the next batch while this one is copied and parsed
+        (``_gpu_finish`` collects it and returns the slot to the loader)."""
         from ..ops import kernels as K
 
-        buf, line_start, weights, epoch, count = item
+        slot = None
+        if isinstance(item[0], int):  # (slot, nbytes, nlines, weights, epoch, count)
+            slot, nbytes, nlines, weights, epoch, count = item
+            hb, hl = self._slots[slot][0][:nbytes], self._slots[slot][1][: nlines + 1]
+            buf = hb.numpy()
+        else:
+            buf, line_start, weights, epoch, count = item
         dev = self.gpu
         with torch.cuda.stream(stream):
-            hb, hl = self._stage(buf, line_start)
+            if slot is None:
+                hb, hl = self._stage(buf, line_start)
             db = hb.to(dev, non_blocking=True)
             dl = hl.to(dev, non_blocking=True)
             pp = K.parse_gpu_start(db, dl, self.args["vocab_size"], self.args["hash_feature_id"], stream=stream)
             w = None if weights is None else torch.from_numpy(weights).to(dev, non_blocking=True)
-        return pp, buf, w, int(epoch), int(count)
+        return pp, buf, w, int(epoch), int(count), slot
 
     def _gpu_finish(self, launched) -> Batch:
         """Wait for a launched tokenizer pass and wrap its outputs (CPU parser when the batch has
         syntax outside the GPU subset or errors); the returned device batch is complete."""
-        pp, buf, w, epoch, count = launched
+        pp, buf, w, epoch, count, slot = launched
         pg = pp.finish()
         dev = self.gpu
         if pg.fallback:
@@ -370,6 +400,8 @@ class NativeTextReader:
             torch.cuda.current_stream(dev).synchronize()
         else:
             b = Batch(pg.labels, pg.offsets, pg.ids, pg.vals, w, pg.nnz, max_feats=pg.max_feats)
+        if slot is not None:  # its copy and parse are complete (finish synchronised them)
+            self._loader.release(slot)
         self.state.epoch, self.state.batches_in_epoch = epoch, count
         b.reader_pos = (epoch, count)
         return b

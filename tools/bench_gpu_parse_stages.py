@@ -39,21 +39,25 @@ def main():
     n_ex = a.files * a.lines * a.epochs
     args = dict(files=files, weight_files=[], batch_size=a.batch, vocab_size=800_000, hash_feature_id=False,
                 shuffle=True, num_epochs=a.epochs, seed=1, threads=a.threads, rank=0, world=1, queue_size=4)
-    # 1) the loader alone (raw batches: shuffled line bytes + line starts)
-    L = native.cpu().TextLoader(start_epoch=0, skip_batches=0, raw=True, binary=False, rows=False, **args)
+    r = NativeTextReader(files, None, a.batch, vocab_size=800_000, num_epochs=a.epochs, seed=1,
+                         parse_threads=a.threads, gpu_parse="cuda")
+    # 1) the loader alone: raw batches assembled into the reader's page-locked slots (released at once)
+    L = native.cpu().TextLoader(start_epoch=0, skip_batches=0, raw=True, binary=False, rows=False,
+                                raw_slots=r._raw_slots(), **args)
     t = time.time()
     nb = 0
     while True:
         item = L.next()
         if item is None:
             break
+        if isinstance(item[0], int):
+            L.release(item[0])
         nb += 1
     L.close()
     dt = time.time() - t
-    print(f"loader raw assembly     : {n_ex / dt / 1e6:7.2f} M ex/s ({nb} batches, {dt:.2f}s)", flush=True)
-    # 2) + pinned staging copy
-    r = NativeTextReader(files, None, a.batch, vocab_size=800_000, num_epochs=a.epochs, seed=1,
-                         parse_threads=a.threads, gpu_parse="cuda")
+    print(f"loader raw assembly (pinned slots): {n_ex / dt / 1e6:7.2f} M ex/s ({nb} batches, {dt:.2f}s)", flush=True)
+    # 2) the same into heap buffers + the reader's pinned staging copy (the path of a batch that
+    #    does not fit a slot)
     L = native.cpu().TextLoader(start_epoch=0, skip_batches=0, raw=True, binary=False, rows=False, **args)
     t = time.time()
     while True:
@@ -63,7 +67,7 @@ def main():
         r._stage(item[0], item[1])
     L.close()
     dt = time.time() - t
-    print(f"+ pinned staging copy   : {n_ex / dt / 1e6:7.2f} M ex/s ({dt:.2f}s)", flush=True)
+    print(f"heap batches + pinned staging copy: {n_ex / dt / 1e6:7.2f} M ex/s ({dt:.2f}s)", flush=True)
     # 3) the full reader: + H2D + GPU tokenizer (+ one stream sync per batch)
     t = time.time()
     n = 0
@@ -71,7 +75,8 @@ def main():
         n += b.B
     torch.cuda.synchronize()
     dt = time.time() - t
-    print(f"+ H2D + GPU tokenizer   : {n / dt / 1e6:7.2f} M ex/s ({dt:.2f}s, {r.fallbacks} CPU fallbacks)", flush=True)
+    print(f"reader: slots + H2D + GPU tokenizer: {n / dt / 1e6:7.2f} M ex/s ({dt:.2f}s, {r.fallbacks} CPU fallbacks)",
+          flush=True)
 
 
 if __name__ == "__main__":

@@ -1,15 +1,14 @@
 #!/bin/bash
-# Input paths on the GPU box: loader throughput (CPU parse / GPU tokenizer / .fmb cache)
-# and end-to-end run.py train on the reference's sample workload shape.
-# usage: tools/gpu_input.sh <tag>
+# Input-path checks and throughput: GPU tokenizer tests, reader stage timing, file-fed e2e training.
 set -o pipefail
 TAG=${1:-input}
-R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/$TAG
-mkdir -p $OUT
+cd ${GRAFT_REPO_ROOT:-$(pwd)}
 export FM_NO_AUTOBUILD=1
-cd $R
-timeout -k 10 400 python -u tools/bench_input.py --skip-python --threads 16 --dir /tmp/fm_in > $OUT/bench_input.txt 2>&1 || { echo "bench_input failed"; tail -30 $OUT/bench_input.txt; exit 1; }
-cat $OUT/bench_input.txt
-timeout -k 10 500 python -u tools/bench_train_e2e.py --threads 16 --epochs 6 --dir /tmp/fm_e2e > $OUT/bench_e2e.txt 2>&1 || { echo "bench_e2e failed"; tail -30 $OUT/bench_e2e.txt; exit 1; }
-cat $OUT/bench_e2e.txt
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_parse_gpu.py tests/test_loader_slots.py > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
+tail -1 $OUT/pytest.log
+timeout -k 10 300 python -u tools/bench_gpu_parse_stages.py --threads 16 > $OUT/stages.txt 2>&1 || { tail -20 $OUT/stages.txt; exit 1; }
+cat $OUT/stages.txt
+timeout -k 10 600 python -u tools/bench_train_e2e.py --lines 250000 --files 4 --epochs 8 > $OUT/e2e.txt 2>&1 || { tail -20 $OUT/e2e.txt; exit 1; }
+cat $OUT/e2e.txt
