@@ -60,6 +60,7 @@ struct RleArgs {
   int* sorted_ex;                 // [n] (payload = occurrence)
   const float* vals;              // [n] (payload = occurrence)
   float* sorted_x;                // [n] (payload = occurrence)
+  uint8_t* single_flag;           // [n] occurrence -> 1 if its key occurs once (zeroed before), or null
 };
 
 __device__ inline int sorted_example(const RleArgs& a, int j) {
@@ -297,14 +298,30 @@ __global__ __launch_bounds__(kBlock) void rle_tile_emit_kernel(RleArgs a) {
       if (sliced) atomicAdd(&sc[chunk_slice(a, r.hot[q], r.ex[q], ch)], 1u);
     }
   }
-  if (a.inv || a.sorted_ex || a.sorted_x) {
+  // one-occurrence rows (the forward's fused singleton update, fm_fwd.hip): head whose key
+  // differs from the next sorted key
+  bool sg[kRleItems];
+  bool any_sg = false;
+  const bool need_all = a.inv || a.sorted_ex || a.sorted_x;
+#pragma unroll
+  for (int q = 0; q < kRleItems; ++q) sg[q] = false;
+  if (a.single_flag) {
+    const uint32_t knext = j0 + kRleItems < a.n ? a.skeys[j0 + kRleItems] : 0xffffffffu;
+#pragma unroll
+    for (int q = 0; q < kRleItems; ++q) {
+      sg[q] = r.hd[q] && (q + 1 < kRleItems ? r.k[q + 1] : knext) != r.k[q];
+      any_sg |= sg[q];
+    }
+  }
+  if (need_all || any_sg) {
     // payload = occurrence (or packed code): all 8 random gathers / scatters of the thread in flight at once
     int p[kRleItems];
     load8(a.spay, j0, a.n, p, 0);
     if (a.ex_shift > 0) {  // packed code -> occurrence index (offsets is small and L2-resident)
       const int mask = (1 << a.ex_shift) - 1;
 #pragma unroll
-      for (int q = 0; q < kRleItems; ++q) p[q] = j0 + q < a.n ? a.offsets[p[q] >> a.ex_shift] + (p[q] & mask) : 0;
+      for (int q = 0; q < kRleItems; ++q)
+        p[q] = j0 + q < a.n && (need_all || sg[q]) ? a.offsets[p[q] >> a.ex_shift] + (p[q] & mask) : 0;
     }
     int exv[kRleItems];
     float xv[kRleItems];
@@ -318,6 +335,7 @@ __global__ __launch_bounds__(kBlock) void rle_tile_emit_kernel(RleArgs a) {
     for (int q = 0; q < kRleItems; ++q) {
       if (j0 + q >= a.n) break;
       if (a.inv) a.inv[p[q]] = sq[q];
+      if (a.single_flag && sg[q]) a.single_flag[p[q]] = 1;
       if (a.sorted_ex) a.sorted_ex[j0 + q] = exv[q];
       if (a.sorted_x) a.sorted_x[j0 + q] = xv[q];
     }
@@ -447,6 +465,7 @@ struct DedupArgs {
   int* sorted_ex;          // nullable
   const float* vals;       // nullable
   float* sorted_x;         // nullable
+  uint8_t* single_flag;    // nullable: [n] 1 = the occurrence's key occurs once (needs occurrence-decodable payloads)
   int payload_is_ex;       // payload carries the example index (sorted payload == sorted example)
   int ex_shift;            // > 0: the payload is the packed code (example << ex_shift | slot), see csr_rows
   const int* offsets;      // [B+1] (ex_shift > 0)
@@ -479,6 +498,10 @@ int launch_dedup(const DedupArgs& a, hipStream_t st) {
   unsigned* tile_off = reinterpret_cast<unsigned*>(base + tmp + align_up(3 * (size_t)ntiles * sizeof(unsigned)));
   if (tmp + 2 * align_up(3 * (size_t)ntiles * sizeof(unsigned)) + slice_scan_bytes(a.n) > a.ws_bytes) return -2;
 
+  if (a.single_flag) {
+    if (a.payload_is_ex && a.ex_shift <= 0) return -7;  // sorted payload must decode to the occurrence
+    (void)hipMemsetAsync(a.single_flag, 0, (size_t)a.n, st);
+  }
   size_t sort_bytes = tmp;
   hipError_t e = sort_pairs(a.ws, sort_bytes, a.keys, a.skeys, a.payload, a.spay, a.n, a.end_bit, st);
   if (e != hipSuccess) return (int)e;
@@ -492,7 +515,7 @@ int launch_dedup(const DedupArgs& a, hipStream_t st) {
   RleArgs r{a.n, a.CH, ntiles, sliced ? a.slice_shift : -1, sliced ? a.nslices : 0, 8 * a.CH,
             a.dense_list ? a.dense_min : 0, a.dense_list, a.skeys, a.spay,
             a.payload_is_ex ? a.spay : nullptr, a.ex_shift, a.offsets, tile_cnt, tile_off, cnt, a.uniq, a.seg_start, a.seg_chunk,
-            a.chunk_start, a.chunk_seg, a.chunk_key, a.counts, a.inv, a.ex_of_occ, a.sorted_ex, a.vals, a.sorted_x};
+            a.chunk_start, a.chunk_seg, a.chunk_key, a.counts, a.inv, a.ex_of_occ, a.sorted_ex, a.vals, a.sorted_x, a.single_flag};
   hipLaunchKernelGGL(rle_tile_count_kernel, dim3(ntiles), dim3(kBlock), 0, st, r);
   hipLaunchKernelGGL(rle_tile_scan_kernel, dim3(1), dim3(1024), 0, st, r);
   hipLaunchKernelGGL(rle_tile_emit_kernel, dim3(ntiles), dim3(kBlock), 0, st, r);

@@ -87,6 +87,7 @@ struct BwdArgs {
   const uint8_t* dense_A;   // [nex, kMaxDense] occurrence counts of the dense rows (written by the forward)
   int cold_split;           // 1: chunks of <= kColdMax occurrences go to fm_bwd_cold_kernel, the chunk kernel skips them
   SelfRows self;            // EMIT (row-sharded step): segments that are this rank's own table rows
+  int fwd_single;           // 1 (LOCAL): rows with one occurrence were updated by the forward (fm_fwd.hip)
 };
 
 constexpr int kColdMax = 4;  // occurrences of a "cold" chunk
@@ -313,6 +314,7 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
     }
     if (dense) continue;  // gradient from the MFMA path (fm_bwd_dense_kernel)
     const int len = j1 - j0;
+    if (a.fwd_single && single && len == 1) continue;  // updated by the forward (fused singleton)
     if (a.cold_split && len <= kColdMax) continue;  // fm_bwd_cold_kernel's
     RowState<EPL> rs;
     if (single) bwd_load<TV, EPL>(a, u, (long long)key, tE, rs);
@@ -474,6 +476,7 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_cold_kernel(BwdArgs a) {
     if (seg & kChunkDense) continue;
     const int u = seg & kChunkSegMask;
     const bool single = (unsigned)seg & kChunkSingle;
+    if (a.fwd_single && single && len == 1) continue;  // updated by the forward (fused singleton)
     RowState<EPL> rs;
     if (single) bwd_load<TV, EPL>(a, u, (long long)a.chunk_key[c], tE, rs);
     int pex = 0;

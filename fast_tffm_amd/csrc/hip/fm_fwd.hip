@@ -42,6 +42,15 @@ struct FwdArgs {
   const int* dense_count;  // device scalar: number of dense rows (capped at kMaxDense here)
   uint8_t* dense_A;        // [B, kMaxDense] occurrence counts (saturated at 255)
   SelfRows self;           // row-sharded step: segments read from this rank's own table rows
+  // Fused singleton update: single_flag[o] = 1 when occurrence o's row occurs
+  // nowhere else in the batch (written by the dedup, which ran before this forward).  Its
+  // whole gradient is c * (r1_i - x v) with c = dpred_i * x, and this kernel holds r1_i and
+  // dpred_i in registers when it finishes example i, so it applies the optimizer to the row
+  // right there (upd: the backward's arguments -- LOCAL: table + optimizer; EMIT, the
+  // row-sharded step: wire rows, gradient rows, self rows) and the backward skips the row's
+  // one-occurrence chunk.  Null: off.
+  const uint8_t* single_flag;
+  BwdArgs upd;
 };
 
 // A/B build knob (variant "fp8packed"): fp8 rows kept packed in flight, a whole example per
@@ -96,9 +105,74 @@ struct FwdUnrollPacked {
   static constexpr int v = ((40 + G - 1) / G) > 24 ? 24 : ((40 + G - 1) / G);
 };
 
-template <int LPR, typename TV>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(fwd_min_waves<LPR, TV>())))
-void fm_fwd_kernel(FwdArgs a) {
+// Lane of the k-th (0-based) set bit of m (k < popcount(m)): the largest p with
+// popcount(m & ((1 << p) - 1)) <= k.
+__device__ inline int nth_set_bit(uint64_t m, int k) {
+  int p = 0;
+#pragma unroll
+  for (int step = 32; step > 0; step >>= 1)
+    if (__popcll(m & ((1ull << (p + step)) - 1ull)) <= k) p += step;
+  return p;
+}
+
+// r1 as the backward reads it back (bf16 for fp8 tables, R1Bf16)
+template <typename TV>
+__device__ inline float r1_stored(float s) {
+  if constexpr (R1Bf16<TV>::v) return bf16_bits_to_f32(f32_to_bf16_bits(s));
+  else return s;
+}
+
+// Optimizer step (LOCAL) or gradient row (EMIT) for the rows of example i [s, e) that occur
+// only there (see FwdArgs::single_flag).  Row group g takes the flagged occurrences g, g + G, ... of each 64-wide
+// window; the gradient is formed exactly as the chunk kernel forms a one-occurrence chunk
+// (A = c r1, Scx = c x, Sc = c, n_u = 1), so the table ends up bitwise as without the fusion.
+template <int LPR, typename TV, int EPL>
+__device__ inline void fwd_single_update(const FwdArgs& a, int s, int e, int lane, int g, int t, bool tact, int tE,
+                                         float dp, const float (&s1)[EPL], uint32_t sr) {
+  constexpr int G = kWave / LPR;
+  float r1q[EPL];
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) r1q[k] = r1_stored<TV>(s1[k]);
+  for (int base = s; base < e; base += kWave) {
+    const int m = min(kWave, e - base);
+    const bool f = lane < m && a.single_flag[base + lane] != 0;
+    const uint64_t mask = __ballot(f);
+    if (mask == 0ull) continue;
+    const int my_row = f ? a.rows[base + lane] : 0;
+    const float my_x = f ? (a.vals ? a.vals[base + lane] : 1.f) : 0.f;
+    const int n1 = __popcll(mask);
+    for (int q = 0; q < n1; q += G) {
+      const int kth = q + g;
+      const int src = kth < n1 ? nth_set_bit(mask, kth) : 0;
+      const int row = __shfl(my_row, src, kWave);
+      const float x = __shfl(my_x, src, kWave);
+      if (kth < n1) {  // (uniform per row group: store_row's group shuffles stay inside it)
+        // LOCAL: `row` is the table row; EMIT (row-sharded step): the segment id, whose
+        // gradient row goes to grad_out[u] (or, a self row no other rank asked for, whose
+        // optimizer step is applied in place)
+        const bool local = a.upd.mode == kBwdLocal;
+        const int u = local ? 0 : row;
+        const long long key = local ? (long long)row : (long long)a.upd.uniq[row];
+        RowState<EPL> rs;
+        bwd_load<TV, EPL>(a.upd, u, key, tE, rs);
+        const float c = dp * x;
+        // the chunk kernel's sums start at 0 and accumulate with fma: same roundings here, and
+        // explicit fmas, so that the compiler cannot contract c * r1 into bwd_finish's
+        // A - Scx v (which would round differently)
+        float A[EPL];
+#pragma unroll
+        for (int k = 0; k < EPL; ++k) A[k] = __builtin_fmaf(c, r1q[k], 0.f);
+        bwd_finish<LPR, TV, EPL>(a.upd, u, t, tact, rs, A, __builtin_fmaf(c, x, 0.f), c, 1, sr);
+      }
+    }
+  }
+}
+
+// (FUSED: the fused singleton update is compiled in; a separate instantiation, so the plain
+// forward keeps its register budget -- the update's code raised the k=64 fp32 kernel from 124
+// to 132 VGPRs, one wave per SIMD less, when it was only switched off at run time)
+template <int LPR, typename TV, bool FUSED>
+__device__ __forceinline__ void fwd_body(const FwdArgs& a) {
   using F = Frag<TV>;
   constexpr int EPL = F::N;
   constexpr int G = kWave / LPR;
@@ -116,6 +190,8 @@ void fm_fwd_kernel(FwdArgs a) {
   const int wave = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   const int nwaves = gridDim.x * kWavesPerBlock;
   const bool want_reg = a.reg_partial != nullptr;
+  constexpr bool fused = FUSED;
+  const uint32_t sr = fused ? sr_step_seed(a.upd.sr_counter) : 0u;
 
   // dense rows: key -> dense index hash (built once per workgroup) and per-wave counters
   __shared__ int hkey[kDenseHash], hval[kDenseHash];
@@ -244,25 +320,29 @@ void fm_fwd_kernel(FwdArgs a) {
       regv_acc += rv;
       regw_acc += rw;
     }
+    // loss and dL/dpred (every lane holds the same pred: butterfly sums are lane-symmetric)
+    float l = 0.f, d = 0.f;
+    if (a.loss_type != kLossNone && (lane == 0 || fused)) {
+      const float y = a.labels[i];
+      const float wt = a.weights ? a.weights[i] : 1.f;
+      if (a.loss_type == kLossMse) {
+        const float diff = pred - y;
+        l = wt * diff * diff;
+        d = 2.f * wt * diff;
+      } else {
+        // sigmoid_cross_entropy_with_logits, numerically stable form
+        l = wt * (fmaxf(pred, 0.f) - pred * y + softplus_neg_abs(pred));
+        d = wt * (sigmoidf(pred) - y);
+      }
+    }
     if (lane == 0) {
       a.pred[i] = pred;
       if (a.loss_type != kLossNone) {
-        const float y = a.labels[i];
-        const float wt = a.weights ? a.weights[i] : 1.f;
-        float l, d;
-        if (a.loss_type == kLossMse) {
-          const float diff = pred - y;
-          l = wt * diff * diff;
-          d = 2.f * wt * diff;
-        } else {
-          // sigmoid_cross_entropy_with_logits, numerically stable form
-          l = wt * (fmaxf(pred, 0.f) - pred * y + softplus_neg_abs(pred));
-          d = wt * (sigmoidf(pred) - y);
-        }
         loss_acc += l;
         if (a.dpred) a.dpred[i] = d * a.grad_scale;
       }
     }
+    if constexpr (fused) fwd_single_update<LPR, TV, EPL>(a, s, e, lane, g, t, tact, tE, d * a.grad_scale, s1, sr);
   }
   if (a.loss_partial == nullptr && a.reg_partial == nullptr) return;
   __shared__ float red[3][kWavesPerBlock];
@@ -278,6 +358,19 @@ void fm_fwd_kernel(FwdArgs a) {
     if (a.loss_partial) a.loss_partial[blockIdx.x] = l;
     if (a.reg_partial) { a.reg_partial[2 * blockIdx.x] = r0; a.reg_partial[2 * blockIdx.x + 1] = r1v; }
   }
+}
+
+template <int LPR, typename TV>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(fwd_min_waves<LPR, TV>())))
+void fm_fwd_kernel(FwdArgs a) {
+  fwd_body<LPR, TV, false>(a);
+}
+
+// (the 16-lane instantiations -- k=64 -- need 132-134 VGPRs uncapped: held at 4 waves / SIMD)
+template <int LPR, typename TV>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LPR == 16 ? 4 : fwd_min_waves<LPR, TV>())))
+void fm_fwd_single_kernel(FwdArgs a) {
+  fwd_body<LPR, TV, true>(a);
 }
 
 // Expand CSR offsets into the example index of every occurrence.
@@ -323,7 +416,11 @@ int fwd_grid(int B) { return fill_grid(B, kWavesPerBlock, 4096); }
 int launch_fwd(const FwdArgs& a, int dtype, int grid, hipStream_t st) {
   if (a.B <= 0) return 0;
   const int lpr = lanes_per_row(a.Kp, dtype);
-  FM_DISPATCH(dtype, lpr, fm_fwd_kernel, grid, st, a);
+  if (a.single_flag) {
+    FM_DISPATCH(dtype, lpr, fm_fwd_single_kernel, grid, st, a);
+  } else {
+    FM_DISPATCH(dtype, lpr, fm_fwd_kernel, grid, st, a);
+  }
   return (int)hipGetLastError();
 }
 

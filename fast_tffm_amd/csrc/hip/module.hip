@@ -21,8 +21,8 @@ namespace py = pybind11;
 using u64 = std::uintptr_t;
 
 // Unity build: all kernel sources are compiled in this translation unit.
+#include "fm_bwd.hip"  // (first: the forward's fused singleton update uses its row update)
 #include "fm_fwd.hip"
-#include "fm_bwd.hip"
 #include "dedup.hip"
 #include "shard.hip"
 #include "init.hip"
@@ -85,9 +85,40 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       [](int B, u64 offsets, u64 rows, u64 vals, u64 v, long long v_stride, u64 w, long long w_stride, int Kp,
          int dtype, u64 labels, u64 weights, int loss_type, float grad_scale, u64 pred, u64 r1, u64 dpred,
          u64 loss_partial, u64 reg_partial, int grid, u64 stream, u64 bias, u64 dense_list, u64 dense_uniq,
-         u64 dense_count, u64 dense_A, const std::vector<long long>& self) {
+         u64 dense_count, u64 dense_A, const std::vector<long long>& self, const std::vector<long long>& single,
+         const std::vector<float>& single_f) {
         fm::FwdArgs a{};
         a.self = self_rows(self);
+        if (!single.empty()) {
+          // fused singleton update: [single_flag, s0v, s1v, s_stride, s0w, s1w, opt_type, sr_counter, mode,
+          // uniq, grad_out, g_stride, g_wcol, g_bf16] and [reg_v, reg_w, lr, l1, l2, beta].  LOCAL: the
+          // forward's own table (v, w) + its optimizer state; EMIT: v, w are the gathered wire rows,
+          // gradient rows go to grad_out[segment], self rows (this rank's table) as in the backward
+          if (single.size() != 14 || single_f.size() != 6 || !single[0])
+            throw std::invalid_argument("fm_fwd: single = [flag, s0v, s1v, s_stride, s0w, s1w, opt, sr, mode, uniq, "
+                                        "grad_out, g_stride, g_wcol, g_bf16], 6 floats");
+          if (dense_A) throw std::runtime_error("fm_fwd: the singleton update excludes the dense-row counts");
+          const int mode = (int)single[8];
+          if (mode == fm::kBwdLocal ? (!single[1] || !single[4] || !self.empty())
+                                    : (mode != fm::kBwdEmit || !single[9] || !single[10] ||
+                                       (a.self.u1 > a.self.u0 && (!single[1] || !single[4]))))
+            throw std::runtime_error("fm_fwd: singleton update: LOCAL needs the optimizer state (no self rows), "
+                                     "EMIT needs uniq, grad_out and, with self rows, their optimizer state");
+          a.single_flag = P<const uint8_t>((u64)single[0]);
+          fm::BwdArgs& b = a.upd;
+          b.mode = mode;
+          b.self = a.self;
+          b.uniq = P<const int>((u64)single[9]);
+          b.grad_out = P<float>((u64)single[10]); b.g_stride = single[11]; b.g_wcol = (int)single[12];
+          b.g_bf16 = (int)single[13];
+          b.v = P<void>(v); b.v_stride = v_stride; b.w = P<float>(w); b.w_stride = w_stride; b.Kp = Kp;
+          b.s0v = P<float>((u64)single[1]); b.s1v = P<float>((u64)single[2]); b.s_stride = single[3];
+          b.s0w = P<float>((u64)single[4]); b.s1w = P<float>((u64)single[5]);
+          b.opt = opt_params((int)single[6], single_f[2], single_f[3], single_f[4], single_f[5]);
+          b.sr_counter = P<const int>((u64)single[7]);
+          b.reg_v = single_f[0]; b.reg_w = single_f[1];
+          if (!r1 || !dpred || loss_type == fm::kLossNone) throw std::runtime_error("fm_fwd: the singleton update needs the loss");
+        }
         a.dense_list = P<const int>(dense_list); a.dense_uniq = P<const int>(dense_uniq);
         a.dense_count = P<const int>(dense_count); a.dense_A = P<uint8_t>(dense_A);
         if (a.dense_A && (!a.dense_list || !a.dense_count)) throw std::runtime_error("fm_fwd: dense_A needs the dense list");
@@ -105,7 +136,8 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("loss_type"), py::arg("grad_scale"), py::arg("pred"), py::arg("r1"), py::arg("dpred"),
       py::arg("loss_partial"), py::arg("reg_partial"), py::arg("grid"), py::arg("stream"), py::arg("bias") = 0,
       py::arg("dense_list") = 0, py::arg("dense_uniq") = 0, py::arg("dense_count") = 0, py::arg("dense_A") = 0,
-      py::arg("self_rows") = std::vector<long long>{});
+      py::arg("self_rows") = std::vector<long long>{}, py::arg("single") = std::vector<long long>{},
+      py::arg("single_f") = std::vector<float>{});
 
   m.def(
       "bwd",
@@ -117,8 +149,10 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
          u64 dense_part, int nex, u64 dense_stream, int dtype,
          long long max_chunks, long long max_unique, u64 stream, int g_wcol, int g_bf16, u64 sr_counter,
          int counters_ready, u64 seg_bounds, int piece, int n_owners, u64 dense_A, int cold_split,
-         const std::vector<long long>& self) {
+         const std::vector<long long>& self, int fwd_single) {
         fm::BwdArgs a{};
+        a.fwd_single = fwd_single;
+        if (fwd_single && mode == fm::kBwdEmitTable) throw std::runtime_error("fm_bwd: fwd_single: LOCAL / EMIT modes");
         a.self = self_rows(self);
         if (a.self.u1 > a.self.u0 && a.self.keys != P<const int>(uniq))
           throw std::runtime_error("fm_bwd: self-row keys must be the dedup's unique keys");
@@ -159,7 +193,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("max_chunks"), py::arg("max_unique"), py::arg("stream"), py::arg("g_wcol") = -1,
       py::arg("g_bf16") = 0, py::arg("sr_counter") = 0, py::arg("counters_ready") = 0, py::arg("seg_bounds") = 0,
       py::arg("piece") = -1, py::arg("n_owners") = 0, py::arg("dense_A") = 0, py::arg("cold_split") = 0,
-      py::arg("self_rows") = std::vector<long long>{});
+      py::arg("self_rows") = std::vector<long long>{}, py::arg("fwd_single") = 0);
 
   m.def("dedup_workspace_bytes", &fm::dedup_workspace_bytes, py::arg("n"));
 
@@ -168,7 +202,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       [](int n, int end_bit, int CH, u64 keys, u64 payload, u64 skeys, u64 spay, u64 uniq, u64 seg_start,
          u64 seg_chunk, u64 chunk_start, u64 chunk_seg, u64 chunk_key, u64 counts, u64 inv, u64 ex_of_occ,
          u64 sorted_ex, u64 vals, u64 sorted_x, int payload_is_ex, int ex_shift, u64 offsets, int dense_min, u64 dense_list, int slice_shift, int nslices, u64 slice_list,
-         u64 slice_start, u64 ws, size_t ws_bytes, u64 stream) {
+         u64 slice_start, u64 ws, size_t ws_bytes, u64 stream, u64 single_flag) {
         if (CH < 1 || CH > fm::kMaxCH) throw std::invalid_argument("CH must be in [1, MAX_CH]");
         fm::DedupArgs a;
         a.n = n; a.end_bit = end_bit; a.CH = CH; a.keys = P<const uint32_t>(keys);
@@ -183,6 +217,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
         a.dense_min = dense_min; a.dense_list = P<int>(dense_list);
         a.slice_list = P<int>(slice_list); a.slice_start = P<int>(slice_start);
         a.ws_bytes = ws_bytes;
+        a.single_flag = P<uint8_t>(single_flag);
         check(fm::launch_dedup(a, S(stream)), "dedup");
       },
       py::arg("n"), py::arg("end_bit"), py::arg("CH"), py::arg("keys"), py::arg("payload"), py::arg("skeys"),
@@ -191,7 +226,8 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("sorted_ex"),
       py::arg("vals"), py::arg("sorted_x"), py::arg("payload_is_ex"), py::arg("ex_shift"), py::arg("offsets"), py::arg("dense_min"), py::arg("dense_list"),
       py::arg("slice_shift"), py::arg("nslices"),
-      py::arg("slice_list"), py::arg("slice_start"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"));
+      py::arg("slice_list"), py::arg("slice_start"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"),
+      py::arg("single_flag") = 0);
   m.attr("MAX_SLICES") = fm::kMaxSlices;
   m.attr("MAX_DENSE") = fm::kMaxDense;
   m.attr("DENSE_WG") = fm::kDenseWG;

@@ -163,7 +163,7 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
                partial: torch.Tensor | None = None, threads: int = 0,
                bias: torch.Tensor | None = None, dense: "DedupOut | None" = None,
                dense_A: torch.Tensor | None = None, dense_by_segment: bool = False,
-               self_rows: SelfRows | None = None) -> FwdOut:
+               self_rows: SelfRows | None = None, single: "SingleUpdate | None" = None) -> FwdOut:
     """FM score of a CSR batch (reference FmScorer, cc/fm_scorer_op.h:101-140), fused with the loss.
 
     pred_i = sum_j x_j w_j + 1/2 sum_k [(sum_j x_j v_jk)^2 - sum_j x_j^2 v_jk^2]  (+ bias[0], optional
@@ -176,6 +176,9 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
     MFMA backward; ``rows`` are table rows (``dense.uniq`` maps segments to them) or, with
     ``dense_by_segment``, the segment ids themselves (the sharded step's inverse map).
     ``self_rows`` (GPU, ``rows`` = segment ids): segments in its range read this rank's table.
+    ``single`` (GPU, training loss, ``rows`` = table rows of ``v``): fused singleton update --
+    the rows the batch's dedup flagged as occurring once get their optimizer step here
+    (``fm_backward(..., fwd_single=True)`` then skips them).
     """
     dev = rows.device
     B = offsets.numel() - 1
@@ -224,6 +227,32 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
         if self_rows is not None and self_rows.u1 > self_rows.u0:
             _self_check(self_rows, v, None)
             dkw["self_rows"] = self_rows.packed()
+        if single is not None:
+            t, o = single.table, single.opt
+            _check(lt != 0 and want_r1 and "dense_A" not in dkw,
+                   "fused singleton update: training loss, r1, no dense rows")
+            _check(single.flag is not None and single.flag.numel() >= nnz, "fused singleton update: dedup flags")
+            if single.mode == BWD_LOCAL:
+                _check("self_rows" not in dkw and t is not None and t.v.data_ptr() == v.data_ptr()
+                       and t.w.data_ptr() == w.data_ptr() and t.s0v is not None and t.s0w is not None
+                       and o.name in ("adagrad", "ftrl"),
+                       "fused singleton update (LOCAL): the forward's own table with Adagrad / FTRL state")
+                gptr, gstride, gwcol = 0, 0, Kp
+            else:
+                _check(single.mode == BWD_EMIT and single.uniq is not None and single.grad_out is not None
+                       and single.grad_out.dtype == torch.float32 and single.grad_out.stride(1) == 1,
+                       "fused singleton update (EMIT): uniq + fp32 gradient rows")
+                _check(("self_rows" not in dkw) or (t is not None and t.s0v is not None and t.s0w is not None),
+                       "fused singleton update (EMIT): self rows need their optimizer state")
+                gptr, gstride = _p(single.grad_out), single.grad_out.stride(0)
+                gwcol = (Kp * 2 + 15) // 16 * 4 if single.grad_bf16 else Kp
+            s0v = t.s0v if t is not None else None
+            sst = s0v.stride(0) if s0v is not None else 0
+            dkw["single"] = [_p(single.flag), _p(s0v), _p(t.s1v if t else None), sst,
+                             _p(t.s0w if t else None), _p(t.s1w if t else None), o.code, _p(single.sr_counter),
+                             int(single.mode), _p(single.uniq), gptr, gstride, gwcol, int(bool(single.grad_bf16))]
+            dkw["single_f"] = [float(single.reg_v), float(single.reg_w), float(o.lr), float(o.l1), float(o.l2),
+                               float(o.beta)]
         h.fwd(B=B, offsets=_p(offsets), rows=_p(rows), vals=_p(vals), v=_p(v), v_stride=v_stride, w=_p(w),
               w_stride=w_stride, Kp=Kp, dtype=dt, labels=_p(labels), weights=_p(weights), loss_type=lt,
               grad_scale=float(grad_scale), pred=_p(pred), r1=_p(r1), dpred=_p(dpred) if lt else 0,
@@ -262,7 +291,7 @@ class DedupOut:
     __slots__ = ("n", "skeys", "perm", "uniq", "seg_start", "seg_chunk", "chunk_start", "chunk_seg", "chunk_key",
                  "counts", "num_unique", "inv", "sorted_ex", "sorted_x", "U_host", "CH", "big_list", "big_count",
                  "multi",
-                 "slice_list", "slice_start", "nslices", "ex_shift", "dense_list", "bwd_fresh")
+                 "slice_list", "slice_start", "nslices", "ex_shift", "dense_list", "bwd_fresh", "single_flag")
 
     def __init__(self, **kw):
         for k in self.__slots__:
@@ -304,6 +333,7 @@ class DedupWorkspace:
         self.slice_list = torch.empty(n1, **i32)
         self.slice_start = torch.empty(MAX_SLICES + 1, **i32)
         self.dense_list = torch.empty(MAX_DENSE, **i32)
+        self.single_flag = torch.empty(n1, dtype=torch.uint8, device=device) if device.type == "cuda" else None
         if device.type == "cuda":
             nbytes = native.hip().dedup_workspace_bytes(n1)
             self.ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
@@ -388,7 +418,7 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
           ex_of_occ: torch.Tensor | None = None, vals: torch.Tensor | None = None, want_inv: bool = False,
           CH: int | None = None, want_perm: bool = False, num_examples: int | None = None,
           Kp: int | None = None, ex_shift: int = 0, offsets: torch.Tensor | None = None,
-          dense_min: int = 0) -> DedupOut:
+          dense_min: int = 0, want_single: bool = False) -> DedupOut:
     """Sort-based unique over non-negative int32 keys (reference tf.unique, fm_model.py:72).
 
     Unique keys come out in ascending order (the reference's first-occurrence
@@ -397,6 +427,8 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
     ``num_examples`` and ``Kp`` are given, see ``slice_plan``).  When neither the inverse
     map, per-occurrence values nor the occurrence permutation are needed, the
     sort carries the example index directly (one gather pass less).
+    ``want_single`` (GPU, with ``ex_of_occ``): also flag, per occurrence, the keys that occur
+    exactly once (``single_flag``, uint8 [n]) for the forward's fused singleton update.
     """
     dev = keys.device
     n = keys.numel()
@@ -426,7 +458,9 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
                    sorted_x=ws.sorted_x if vals is not None else None, CH=CH, big_list=ws.big_list,
                    big_count=ws.big_count, multi=ws.multi, slice_list=ws.slice_list if nsl else None,
                    slice_start=ws.slice_start, nslices=nsl, ex_shift=int(ex_shift),
-                   dense_list=ws.dense_list if dense_min > 0 and ex_of_occ is not None and _is_gpu(keys) else None)
+                   dense_list=ws.dense_list if dense_min > 0 and ex_of_occ is not None and _is_gpu(keys) else None,
+                   single_flag=ws.single_flag if want_single and ex_of_occ is not None and _is_gpu(keys)
+                   and (packed or not ex_payload) else None)
     if _is_gpu(keys):
         h = native.hip()
         _check(1 <= CH <= h.MAX_CH, f"CH must be in [1, {h.MAX_CH}]")
@@ -441,7 +475,7 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
                 dense_min=int(dense_min) if out.dense_list is not None else 0, dense_list=_p(out.dense_list),
                 slice_shift=shift, nslices=nsl,
                 slice_list=_p(out.slice_list), slice_start=_p(ws.slice_start), ws=_p(ws.ws),
-                ws_bytes=ws.ws.numel(), stream=_stream(keys))
+                ws_bytes=ws.ws.numel(), stream=_stream(keys), single_flag=_p(out.single_flag))
         out.bwd_fresh = True  # the backward counters were zeroed on this stream
     else:
         U = native.cpu().dedup(n=n, keys=_p(keys), skeys=_p(ws.skeys), perm=_p(ws.perm), uniq=_p(ws.uniq),
@@ -498,6 +532,29 @@ def _self_check(sr: SelfRows, v: torch.Tensor, keys: torch.Tensor | None) -> Non
         _check(sr.excl.numel() >= sr.u1 - sr.u0, "self excl too short")
 
 
+@dataclass
+class SingleUpdate:
+    """Fused singleton update of the forward (``fm_forward(single=...)``): the dedup's
+    one-occurrence flags and the backward's arguments for those rows (LOCAL: table, optimizer,
+    regularisation; EMIT: also the gradient rows and, for self rows, their table)."""
+
+    flag: torch.Tensor
+    table: TableState | None      # LOCAL: the forward's table; EMIT: the self rows' table (or None)
+    opt: OptConfig
+    reg_v: float
+    reg_w: float
+    sr_counter: torch.Tensor | None = None
+    mode: int = 0                 # BWD_LOCAL / BWD_EMIT (row-sharded step: rows = segment ids)
+    uniq: torch.Tensor | None = None       # EMIT: the dedup's unique keys
+    grad_out: torch.Tensor | None = None   # EMIT: gradient rows [U, g_stride]
+    grad_bf16: bool = False
+
+
+def fwd_single_enabled() -> bool:
+    """Fused singleton update in the local GPU step (FM_FWD_SINGLE=1; opt-in until measured)."""
+    return os.environ.get("FM_FWD_SINGLE", "0") != "0"
+
+
 def partial_rows(n: int, CH: int) -> int:
     """Upper bound on backward chunks (= partial rows) for n occurrences: U + n / CH."""
     return max(n, 1) + max(n, 1) // max(CH, 1) + 1
@@ -511,7 +568,8 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
                 dense_part: torch.Tensor | None = None, dense_stream=None,
                 grad_bf16: bool = False, sr_counter: torch.Tensor | None = None,
                 seg_bounds: torch.Tensor | None = None, piece: int = -1,
-                dense_A: torch.Tensor | None = None, self_rows: SelfRows | None = None) -> torch.Tensor | None:
+                dense_A: torch.Tensor | None = None, self_rows: SelfRows | None = None,
+                fwd_single: bool = False) -> torch.Tensor | None:
     """Segmented FM backward over the dedup grouping (reference FmGrad, cc/fm_grad_op.h:59-163).
 
     Per unique row u with occurrences (i, x):
@@ -524,6 +582,8 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
     second part (split backward of the row-sharded exchange); piece 1 must follow piece 0.
     ``self_rows`` (GPU, EMIT): segments in its range are read from its table; the exclusive ones
     get ``opt`` applied in place (with ``sr_counter``) and no gradient row.
+    ``fwd_single`` (GPU, LOCAL): the forward already updated the one-occurrence rows flagged in
+    ``dd.single_flag`` (``fm_forward(single=...)``, same ``sr_counter``); they are skipped.
     """
     dev = dpred.device
     _check(dd.sorted_ex is not None, "dedup must be run with ex_of_occ")
@@ -612,7 +672,7 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               seg_bounds=_p(seg_bounds), piece=int(piece),
               n_owners=(seg_bounds.numel() - 1) // 2 if seg_bounds is not None else 0,
               dense_A=_p(dense_A) if dd.dense_list is not None else 0,
-              cold_split=int(os.environ.get("FM_COLD_SPLIT", "0") == "1"), **skw)
+              cold_split=int(os.environ.get("FM_COLD_SPLIT", "0") == "1"), fwd_single=int(bool(fwd_single)), **skw)
         dd.bwd_fresh = False  # a second backward over this grouping zeroes its counters itself
     else:
         _check(self_rows is None, "self rows are a GPU path")

@@ -386,7 +386,8 @@ class ShardExchange(_Base):
                                   dense_min=K.dense_min_for(sb.B, self.m.Kp, m.cfg.dedup_chunk,
                                                             table_dtype=m.table.v.dtype,
                                                             has_vals=sb.vals is not None,
-                                                            max_feats=sb.max_feats) if train else 0)
+                                                            max_feats=sb.max_feats) if train else 0,
+                                  want_single=train and gpu and len(ranges) == 1 and self._fwd_single_ok())
                 counts.append(K.owner_counts(part.dd, self.Rps, self.W))
                 pl.parts.append(part)
             c = torch.stack(counts, dim=1)     # [W, P]: row q = what goes to rank q
@@ -623,6 +624,14 @@ class ShardExchange(_Base):
             e.gathered.index_copy_(0, base + self._tag_view(recv).to(torch.int64), recv)
         return self.wire.views(e.gathered)
 
+    def _fwd_single_ok(self) -> bool:
+        """Fused singleton update in the sharded step (one part, one-piece backward): the forward
+        emits the gradient rows of the batch's one-occurrence rows (or updates them in place, for
+        exclusive self rows) and the backward skips them (ops.kernels.fwd_single_enabled)."""
+        return (self.dev.type == "cuda" and self.nparts == 1 and not self.overlap_grads
+                and K.fwd_single_enabled() and self.m.cfg.loss_type in ("logistic", "mse")
+                and (not self.self_rows or self.m.cfg.opt.name in ("adagrad", "ftrl")))
+
     def _split_ok(self, pl: _ShardPlan, dd) -> bool:
         return (self.overlap_grads and len(pl.parts) == 1 and dd.slice_list is None
                 and (dd.dense_list is None or self.dev.type != "cuda"))
@@ -794,14 +803,19 @@ class ShardExchange(_Base):
                 work.wait()               # the compute stream waits for this part's rows
             src_v, src_w = wf.views(buf) if buf is not None else early_views
             dA = ws.dense_counts(ws.cap_b)[e0: e0 + sb.B] if dd.dense_list is not None else None
+            gs = grad_send[part.u0: part.u0 + part.U]
+            single = None
+            if dd.single_flag is not None and dA is None and not self._split_ok(pl, dd):
+                single = K.SingleUpdate(dd.single_flag, m.table.state if srows is not None else None, cfg.opt, rv, rw,
+                                        sr, mode=K.BWD_EMIT, uniq=dd.uniq, grad_out=gs, grad_bf16=wf.grad_bf16)
             with roctx_range("fwd"):
                 fo = K.fm_forward(sb.offsets, dd.inv[: sb.nnz], sb.vals, src_v, src_w, Kp, labels=sb.labels,
                                   weights=sb.weights, loss=cfg.loss_type, grad_scale=gscale, want_r1=True,
                                   pred=ws.pred[e0: e0 + sb.B], r1=ws.r1[e0: e0 + sb.B],
                                   dpred=ws.dpred[e0: e0 + sb.B], partial=ws.fwd_partial, threads=cfg.threads,
-                                  bias=m.gbias, dense=dd, dense_A=dA, dense_by_segment=True, self_rows=srows)
+                                  bias=m.gbias, dense=dd, dense_A=dA, dense_by_segment=True, self_rows=srows,
+                                  single=single)
             loss = fo.loss_sum if loss is None else loss + fo.loss_sum
-            gs = grad_send[part.u0: part.u0 + part.U]
             if self._split_ok(pl, dd):
                 with roctx_range("bwd_split+grads"):
                     gworks += self._bwd_split_exchange(pl, part, dd, fo, src_v, src_w, gs, grad_recv, rv, rw, skw)
@@ -810,7 +824,7 @@ class ShardExchange(_Base):
                 K.fm_backward(dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT, src_v=src_v, src_w=src_w, grad_out=gs,
                               reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads,
                               dense_part=ws.dense_part, dense_stream=m._dense_stream() if gpu else None,
-                              grad_bf16=wf.grad_bf16, dense_A=dA, **skw)
+                              grad_bf16=wf.grad_bf16, dense_A=dA, fwd_single=single is not None, **skw)
             if self.W > 1:
                 with roctx_range("a2a_grads"):
                     gworks.append(dist.all_to_all_single(grad_recv[part.r0: part.r0 + part.R], gs, part.rc, part.sc,
