@@ -574,7 +574,8 @@ class FactorizationMachine:
         ws, cfg = self.ws, self.cfg
         dA = ws.dense_counts(b.B) if dd.dense_list is not None else None
         rv, rw = self.reg_coeffs
-        # fused singleton update: rows occurring once in the batch (~73% of a Criteo-shaped
+        # fused singleton update (opt-in FM_FWD_SINGLE=1, measured slower: ops.kernels.
+        # fwd_single_enabled): rows occurring once in the batch (~73% of a Criteo-shaped
         # batch's unique rows) get their optimizer step in the forward, which holds their whole
         # gradient's inputs (r1_i, dpred_i) in registers; the backward skips them.  The
         # stochastic-rounding counter is advanced before the forward so both kernels use this

@@ -551,7 +551,13 @@ class SingleUpdate:
 
 
 def fwd_single_enabled() -> bool:
-    """Fused singleton update in the local GPU step (FM_FWD_SINGLE=1; opt-in until measured)."""
+    """Fused singleton update in the local / row-sharded GPU step (opt-in, FM_FWD_SINGLE=1).
+
+    Exact (bitwise equal to the unfused step) but measured slower on every preset
+    (profiles/r2/fwd_single_ab.txt: k64 fp32 0.674 -> 0.750 ms, sharded W=1 0.78 -> 0.89 ms):
+    the chunk backward sheds ~50 us of r1 gathers and descriptor chains, but the forward
+    gains ~115 us -- each wave's singleton read-modify-writes come after its example's
+    reduction, a dependent chain the forward's occupancy does not hide."""
     return os.environ.get("FM_FWD_SINGLE", "0") != "0"
 
 
