@@ -479,6 +479,37 @@ struct DedupArgs {
   size_t ws_bytes;
 };
 
+// ---------------------------------------------------------------------------
+// Segment index (key -> segment id without an inverse map).  The row-sharded forward reads
+// each occurrence's wire row by its segment id.  The dedup's inverse map delivers that as one
+// random 4-byte scatter per occurrence (5.1M per Criteo-shaped batch: rle_tile_emit 24 ->
+// 112 us, the local step +85 us when it is forced on, profiles/r2/inv_cost.txt).  Instead a
+// bucket index over the sorted unique keys is built -- idx[b] = first segment whose key >>
+// shift >= b, nb + 1 entries, every one written once per batch by the segment that starts it
+// (no clear, no atomics) -- and the forward finds a key's segment from idx[b], idx[b + 1] and,
+// only when the bucket holds several keys, a short scan of the sorted keys.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void seg_index_kernel(int n_max, const uint32_t* uniq, const int* counts, int shift,
+                                                           int nb, int* idx) {
+  const int U = min(counts[0], n_max);
+  const int tid = blockIdx.x * kBlock + threadIdx.x, nth = gridDim.x * kBlock;
+  for (int s = tid; s < U; s += nth) {  // buckets (previous key's bucket, this key's bucket]
+    const int lo = s == 0 ? 0 : (int)(uniq[s - 1] >> shift) + 1;
+    const int hi = (int)(uniq[s] >> shift);
+    for (int b = lo; b <= hi; ++b) idx[b] = s;
+  }
+  // buckets after the last key (keys rarely fill the whole 2^key_bits range: spread over the grid)
+  const int tail0 = U > 0 ? (int)(uniq[U - 1] >> shift) + 1 : 0;
+  for (int b = tail0 + tid; b <= nb; b += nth) idx[b] = U;
+}
+
+int launch_seg_index(int n_max, const uint32_t* uniq, const int* counts, int shift, int nb, int* idx, hipStream_t st) {
+  if (n_max < 0 || nb < 1 || shift < 0 || shift > 31) return -1;
+  hipLaunchKernelGGL(seg_index_kernel, dim3(fill_grid(n_max + 1, kBlock, 2048)), dim3(kBlock), 0, st, n_max, uniq,
+                     counts, shift, nb, idx);
+  return (int)hipGetLastError();
+}
+
 int launch_dedup(const DedupArgs& a, hipStream_t st) {
   // counts[0..3] = U, #chunks, #multi-chunk rows, #dense rows; counts[4] = the backward's
   // hot-row count: both backward counters start at 0 here, on the dedup's stream (off the

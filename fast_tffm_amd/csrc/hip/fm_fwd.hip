@@ -51,7 +51,23 @@ struct FwdArgs {
   // one-occurrence chunk.  Null: off.
   const uint8_t* single_flag;
   BwdArgs upd;
+  // Segment lookup (row-sharded step, dedup.hip seg_index_kernel): rows[] hold the shard keys
+  // and each occurrence's segment is found through the bucket index instead of an inverse map.
+  const int* seg_idx;      // [nb + 1] first segment of each key bucket, or null (rows are segment ids)
+  const int* seg_keys;     // [U] sorted unique keys
+  int seg_shift;           // bucket = key >> seg_shift
 };
+
+// Segment of key k (present in the batch): the bucket's first candidate, then a scan over the
+// bucket's other keys (the last candidate needs no compare).  ~0.4 keys per bucket at the
+// default sizing, so usually the idx reads only.
+__device__ inline int seg_lookup(const FwdArgs& a, int k) {
+  const int b = (int)((uint32_t)k >> a.seg_shift);
+  int s = a.seg_idx[b];
+  const int e = a.seg_idx[b + 1];
+  while (s + 1 < e && a.seg_keys[s] != k) ++s;
+  return s;
+}
 
 // A/B build knob (variant "fp8packed"): fp8 rows kept packed in flight, a whole example per
 // round.  Measured slower: k128 fp8 FTRL step 0.93 -> 1.04 ms (profiles/r2/fp8_forward_ab.txt)
@@ -138,7 +154,8 @@ __device__ inline void fwd_single_update(const FwdArgs& a, int s, int e, int lan
     const bool f = lane < m && a.single_flag[base + lane] != 0;
     const uint64_t mask = __ballot(f);
     if (mask == 0ull) continue;
-    const int my_row = f ? a.rows[base + lane] : 0;
+    int my_row = f ? a.rows[base + lane] : 0;
+    if (f && a.seg_idx) my_row = seg_lookup(a, my_row);
     const float my_x = f ? (a.vals ? a.vals[base + lane] : 1.f) : 0.f;
     const int n1 = __popcll(mask);
     for (int q = 0; q < n1; q += G) {
@@ -191,6 +208,10 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
   const int nwaves = gridDim.x * kWavesPerBlock;
   const bool want_reg = a.reg_partial != nullptr;
   constexpr bool fused = FUSED;
+  // (segment lookup + self rows: the key range of the own segments, read once)
+  const bool self_key = self_on && a.seg_idx != nullptr && a.dense_A == nullptr;
+  const int self_kmin = self_key ? a.self.keys[a.self.u0] : 0;
+  const int self_kmax = self_key ? a.self.keys[a.self.u1 - 1] : -1;
   const uint32_t sr = fused ? sr_step_seed(a.upd.sr_counter) : 0u;
 
   // dense rows: key -> dense index hash (built once per workgroup) and per-wave counters
@@ -227,13 +248,20 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
       if (lane < m) {
         my_seg = my_row = a.rows[base + lane];
         my_x = a.vals ? a.vals[base + lane] : 1.f;
+        // segment lookup mode: rows[] are keys; an own row is known by its key alone (the self
+        // segments are exactly the batch's keys in [self_kmin, self_kmax]), so it needs neither
+        // the lookup nor the segment's key load -- at world 1 every row (dense counting needs
+        // the segment: then every key is looked up)
+        const int key = my_row;
+        const bool own_key = self_key && key >= self_kmin && key <= self_kmax;
+        if (a.seg_idx && !own_key) my_seg = my_row = seg_lookup(a, key);
         // the linear weight (and fp8 scale, same cache line) of occurrence `lane`, one
         // lane-parallel load per 64 occurrences instead of one per row group: the w loads
         // were ~45% of the kernel's VMEM instructions with the TA 72% busy
         // (profiles/r2/pmc_k64_fp32_before.txt)
-        if (self_on && a.self.has(my_row)) {
+        if (own_key || (self_on && !self_key && a.self.has(my_row))) {
           // own table row: its index with the top bit set selects the table in the row loads
-          const long long trow = a.self.row(my_row);
+          const long long trow = own_key ? (long long)key - a.self.base : a.self.row(my_row);
           my_w = a.self.w[trow * a.self.w_stride];
           my_s = row_scale<TV>(a.self.w, trow, a.self.w_stride);
           my_row = (int)trow | kSelfBit;

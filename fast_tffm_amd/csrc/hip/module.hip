@@ -86,8 +86,11 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
          int dtype, u64 labels, u64 weights, int loss_type, float grad_scale, u64 pred, u64 r1, u64 dpred,
          u64 loss_partial, u64 reg_partial, int grid, u64 stream, u64 bias, u64 dense_list, u64 dense_uniq,
          u64 dense_count, u64 dense_A, const std::vector<long long>& self, const std::vector<long long>& single,
-         const std::vector<float>& single_f) {
+         const std::vector<float>& single_f, u64 seg_idx, u64 seg_keys, int seg_shift) {
         fm::FwdArgs a{};
+        a.seg_idx = P<const int>(seg_idx); a.seg_keys = P<const int>(seg_keys); a.seg_shift = seg_shift;
+        if (a.seg_idx && (!a.seg_keys || seg_shift < 0 || seg_shift > 31))
+          throw std::invalid_argument("fm_fwd: segment lookup needs the sorted keys and a shift in [0, 31]");
         a.self = self_rows(self);
         if (!single.empty()) {
           // fused singleton update: [single_flag, s0v, s1v, s_stride, s0w, s1w, opt_type, sr_counter, mode,
@@ -137,7 +140,18 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("loss_partial"), py::arg("reg_partial"), py::arg("grid"), py::arg("stream"), py::arg("bias") = 0,
       py::arg("dense_list") = 0, py::arg("dense_uniq") = 0, py::arg("dense_count") = 0, py::arg("dense_A") = 0,
       py::arg("self_rows") = std::vector<long long>{}, py::arg("single") = std::vector<long long>{},
-      py::arg("single_f") = std::vector<float>{});
+      py::arg("single_f") = std::vector<float>{}, py::arg("seg_idx") = 0, py::arg("seg_keys") = 0,
+      py::arg("seg_shift") = 0);
+
+  m.def(
+      "seg_index",
+      [](int n_max, u64 uniq, u64 counts, int shift, int nb, u64 idx, u64 stream) {
+        check(fm::launch_seg_index(n_max, P<const uint32_t>(uniq), P<const int>(counts), shift, nb, P<int>(idx),
+                                   S(stream)),
+              "seg_index");
+      },
+      py::arg("n_max"), py::arg("uniq"), py::arg("counts"), py::arg("shift"), py::arg("nb"), py::arg("idx"),
+      py::arg("stream"));
 
   m.def(
       "bwd",

@@ -163,7 +163,8 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
                partial: torch.Tensor | None = None, threads: int = 0,
                bias: torch.Tensor | None = None, dense: "DedupOut | None" = None,
                dense_A: torch.Tensor | None = None, dense_by_segment: bool = False,
-               self_rows: SelfRows | None = None, single: "SingleUpdate | None" = None) -> FwdOut:
+               self_rows: SelfRows | None = None, single: "SingleUpdate | None" = None,
+               seg_lookup: "SegIndex | None" = None) -> FwdOut:
     """FM score of a CSR batch (reference FmScorer, cc/fm_scorer_op.h:101-140), fused with the loss.
 
     pred_i = sum_j x_j w_j + 1/2 sum_k [(sum_j x_j v_jk)^2 - sum_j x_j^2 v_jk^2]  (+ bias[0], optional
@@ -179,6 +180,8 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
     ``single`` (GPU, training loss, ``rows`` = table rows of ``v``): fused singleton update --
     the rows the batch's dedup flagged as occurring once get their optimizer step here
     (``fm_backward(..., fwd_single=True)`` then skips them).
+    ``seg_lookup`` (GPU): ``rows`` are the dedup's keys and every occurrence's segment (its
+    row of ``v``) is found through the bucket index (``seg_index``) instead of an inverse map.
     """
     dev = rows.device
     B = offsets.numel() - 1
@@ -197,7 +200,10 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
     if lt:
         _chk_vec(labels, torch.float32, B, "labels", dev)
         _chk_vec(weights, torch.float32, B, "weights", dev)
-    _range_check(rows, v.shape[0], "rows")
+    if seg_lookup is None:
+        _range_check(rows, v.shape[0], "rows")
+    else:
+        _check(_is_gpu(rows), "segment lookup is a GPU path")
     if pred is None:
         pred = torch.empty(B, dtype=torch.float32, device=dev)
     if want_r1 and r1 is None:
@@ -257,7 +263,10 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
               w_stride=w_stride, Kp=Kp, dtype=dt, labels=_p(labels), weights=_p(weights), loss_type=lt,
               grad_scale=float(grad_scale), pred=_p(pred), r1=_p(r1), dpred=_p(dpred) if lt else 0,
               loss_partial=_p(lp) if lt else 0, reg_partial=_p(rp) if want_reg else 0, grid=grid,
-              stream=_stream(rows), bias=_p(bias), **dkw)
+              stream=_stream(rows), bias=_p(bias),
+              seg_idx=_p(seg_lookup.idx) if seg_lookup is not None else 0,
+              seg_keys=_p(seg_lookup.keys) if seg_lookup is not None else 0,
+              seg_shift=seg_lookup.shift if seg_lookup is not None else 0, **dkw)
         # (an in-kernel last-block reduction was measured slower: the per-block agent-scope
         # release fence writes back L2 -- fwd 211 -> 412 us; a separate reduce is ~10 us)
         loss_sum = lp.sum(dtype=torch.float32) if lt else None
@@ -548,6 +557,40 @@ class SingleUpdate:
     uniq: torch.Tensor | None = None       # EMIT: the dedup's unique keys
     grad_out: torch.Tensor | None = None   # EMIT: gradient rows [U, g_stride]
     grad_bf16: bool = False
+
+
+@dataclass
+class SegIndex:
+    """Bucket index over a dedup's sorted unique keys (``seg_index``): key -> segment."""
+
+    idx: torch.Tensor     # int32 [nb + 1]
+    keys: torch.Tensor    # the dedup's uniq (sorted keys)
+    shift: int
+
+
+def seg_lookup_enabled() -> bool:
+    """Row-sharded step: segment lookup through a bucket index instead of the dedup's inverse
+    map (FM_SEG_LOOKUP, default on; profiles/r2/inv_cost.txt)."""
+    return os.environ.get("FM_SEG_LOOKUP", "1") != "0"
+
+
+def seg_index_bits(nnz: int, key_bits: int) -> tuple[int, int]:
+    """(shift, nb): about four buckets per occurrence-capacity / 4 ... i.e. nnz / 4 buckets
+    (a power of two in [16, 2^20]), bucket = key >> shift over ``key_bits``-bit keys."""
+    bb = max(4, min(20, max(1, nnz).bit_length() - 2, key_bits))
+    shift = max(0, key_bits - bb)
+    return shift, 1 << (key_bits - shift)
+
+
+def seg_index(dd: DedupOut, key_bits: int, out: torch.Tensor | None = None) -> SegIndex:
+    """Build the bucket index of ``dd``'s unique keys on the current stream (GPU, no host sync)."""
+    _check(_is_gpu(dd.uniq), "seg_index is a GPU path")
+    shift, nb = seg_index_bits(dd.n, key_bits)
+    if out is None or out.numel() < nb + 1:
+        out = torch.empty(nb + 1, dtype=torch.int32, device=dd.uniq.device)
+    native.hip().seg_index(n_max=int(dd.n), uniq=_p(dd.uniq), counts=_p(dd.counts), shift=int(shift), nb=int(nb),
+                           idx=_p(out), stream=_stream(dd.uniq))
+    return SegIndex(out, dd.uniq, shift)
 
 
 def fwd_single_enabled() -> bool:

@@ -81,7 +81,7 @@ class _Part:
     """One micro-batch of a sharded step: its examples, dedup grouping, owner split
     sizes and the rows it requests from every owner."""
 
-    __slots__ = ("b", "e0", "dd", "sc", "rc", "U", "R", "u0", "r0", "req_send")
+    __slots__ = ("b", "e0", "dd", "sc", "rc", "U", "R", "u0", "r0", "req_send", "keys", "seg")
 
 
 class _ShardPlan:
@@ -119,6 +119,17 @@ class _PlanSlot:
         self.run_off: torch.Tensor | None = None    # device copy
         self.match: torch.Tensor | None = None      # [R, runs] cross-run match scratch (apply_runs)
         self.excl: torch.Tensor | None = None       # [own requests] exclusive flags (self rows)
+        self.segidx: list[torch.Tensor | None] = []  # per part: key-bucket index (K.seg_index)
+
+    def segidx_buf(self, k: int) -> torch.Tensor | None:
+        """Bucket-index buffer of part k (K.seg_index), sized for the workspace's capacity."""
+        d = self.dd[k]
+        nb = K.seg_index_bits(d.cap, 31)[1]
+        while len(self.segidx) <= k:
+            self.segidx.append(None)
+        if self.segidx[k] is None or self.segidx[k].numel() < nb + 1:
+            self.segidx[k] = torch.empty(nb + 1, dtype=torch.int32, device=d.uniq.device)
+        return self.segidx[k]
 
     def ensure(self, k: int, nnz: int, dev, CH: int) -> K.DedupWorkspace:
         while len(self.dd) <= k:
@@ -380,14 +391,19 @@ class ShardExchange(_Base):
                 if train:
                     shift = m._slot_bits(sb, always=True)
                     ex = K.csr_rows(sb.offsets, out=dws.ex_of_occ[: sb.nnz], nnz=sb.nnz, slot_bits=shift)
+                # training plans on the GPU find each occurrence's segment through a bucket index
+                # (K.seg_index) instead of the inverse map, a 5.1M-occurrence random scatter
+                lookup = train and gpu and K.seg_lookup_enabled()
+                part.keys = keys
                 part.dd = K.dedup(keys, ws=dws, key_bits=self.key_bits, ex_of_occ=ex,
-                                  vals=sb.vals if ex is not None else None, want_inv=True, num_examples=sb.B,
+                                  vals=sb.vals if ex is not None else None, want_inv=not lookup, num_examples=sb.B,
                                   Kp=self.m.Kp, ex_shift=shift, offsets=sb.offsets if shift else None,
                                   dense_min=K.dense_min_for(sb.B, self.m.Kp, m.cfg.dedup_chunk,
                                                             table_dtype=m.table.v.dtype,
                                                             has_vals=sb.vals is not None,
                                                             max_feats=sb.max_feats) if train else 0,
                                   want_single=train and gpu and len(ranges) == 1 and self._fwd_single_ok())
+                part.seg = K.seg_index(part.dd, self.key_bits, slot.segidx_buf(k)) if lookup else None
                 counts.append(K.owner_counts(part.dd, self.Rps, self.W))
                 pl.parts.append(part)
             c = torch.stack(counts, dim=1)     # [W, P]: row q = what goes to rank q
@@ -809,12 +825,13 @@ class ShardExchange(_Base):
                 single = K.SingleUpdate(dd.single_flag, m.table.state if srows is not None else None, cfg.opt, rv, rw,
                                         sr, mode=K.BWD_EMIT, uniq=dd.uniq, grad_out=gs, grad_bf16=wf.grad_bf16)
             with roctx_range("fwd"):
-                fo = K.fm_forward(sb.offsets, dd.inv[: sb.nnz], sb.vals, src_v, src_w, Kp, labels=sb.labels,
+                fo = K.fm_forward(sb.offsets, part.keys if part.seg is not None else dd.inv[: sb.nnz], sb.vals,
+                                  src_v, src_w, Kp, labels=sb.labels,
                                   weights=sb.weights, loss=cfg.loss_type, grad_scale=gscale, want_r1=True,
                                   pred=ws.pred[e0: e0 + sb.B], r1=ws.r1[e0: e0 + sb.B],
                                   dpred=ws.dpred[e0: e0 + sb.B], partial=ws.fwd_partial, threads=cfg.threads,
                                   bias=m.gbias, dense=dd, dense_A=dA, dense_by_segment=True, self_rows=srows,
-                                  single=single)
+                                  single=single, seg_lookup=part.seg)
             loss = fo.loss_sum if loss is None else loss + fo.loss_sum
             if self._split_ok(pl, dd):
                 with roctx_range("bwd_split+grads"):
@@ -878,9 +895,10 @@ class ShardExchange(_Base):
         part = pl.parts[0]
         buf, work = self._gather_part(pl, part, async_op=False)
         src_v, src_w = self.wire.views(buf)
-        out = K.fm_forward(b.offsets, part.dd.inv[: b.nnz], b.vals, src_v, src_w, self.Kp, labels=b.labels,
-                           weights=b.weights, loss=loss, grad_scale=1.0, want_r1=False, want_reg=want_reg,
-                           threads=self.m.cfg.threads, bias=self.m.gbias)
+        seg = getattr(part, "seg", None)  # (eval plans keep the inverse map: train=False)
+        out = K.fm_forward(b.offsets, part.keys if seg is not None else part.dd.inv[: b.nnz], b.vals, src_v, src_w,
+                           self.Kp, labels=b.labels, weights=b.weights, loss=loss, grad_scale=1.0, want_r1=False,
+                           want_reg=want_reg, threads=self.m.cfg.threads, bias=self.m.gbias, seg_lookup=seg)
         if self.dev.type == "cuda":
             done = torch.cuda.Event()
             done.record(torch.cuda.current_stream(self.dev))

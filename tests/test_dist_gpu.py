@@ -267,3 +267,50 @@ def test_rccl_world1_fused_singletons_bitwise(rccl_ctx, dtype, prefetch, monkeyp
         dm.close()
     for x, y in zip(*res):
         assert torch.equal(x.view(torch.uint8), y.view(torch.uint8))
+
+
+@pytest.mark.parametrize("k,dtype,prefetch", [(64, torch.float32, "on"), (16, torch.bfloat16, "off"),
+                                               (128, torch.float8_e4m3fn, "on")])
+def test_rccl_world1_segment_lookup_bitwise(rccl_ctx, k, dtype, prefetch, monkeypatch):
+    """The sharded forward's key -> segment bucket index (K.seg_index, FM_SEG_LOOKUP=1) finds
+    exactly the segments of the dedup's inverse map: same table bits, same predictions."""
+    import dataclasses
+
+    V = 60000
+    gen = CriteoSynth(V, device="cuda", seed=29)
+    batches = [gen.batch(2048) for _ in range(4)]
+    ev = gen.batch(777)
+    res, preds = [], []
+    for f in ("0", "1"):
+        monkeypatch.setenv("FM_SEG_LOOKUP", f)
+        cfg = dataclasses.replace(_cfg("shard", V), factor_num=k, dtype=dtype, prefetch_rows=prefetch)
+        dm = FactorizationMachine(cfg, device="cuda", dist=rccl_ctx)
+        for i, b in enumerate(batches):
+            dm.train_step(b, batches[i + 1] if i + 1 < len(batches) else None,
+                          batches[i + 2] if i + 2 < len(batches) else None)
+        torch.cuda.synchronize()
+        st = dm.table.state
+        res.append([x.clone() for x in (st.v, st.w, st.s0v, st.s0w)])
+        preds.append(dm.predict(ev).clone())
+        dm.close()
+    for x, y in zip(*res):
+        assert torch.equal(x.view(torch.uint8), y.view(torch.uint8))
+    assert torch.equal(preds[0], preds[1])
+
+
+def test_seg_index_matches_inverse_map():
+    """Bucket index lookup == inverse map for every occurrence (keys with dense and sparse buckets)."""
+    gen = CriteoSynth(1 << 20, device="cuda", seed=31)
+    b = gen.batch(4096)
+    keys = b.ids.int().contiguous()
+    dd = K.dedup(keys, key_bits=20, ex_of_occ=K.csr_rows(b.offsets), want_inv=True)
+    si = K.seg_index(dd, 20)
+    torch.cuda.synchronize()
+    U = dd.sync()
+    uniq = dd.uniq[:U].long()
+    bkt = keys.long() >> si.shift
+    lo, hi = si.idx[bkt].long(), si.idx[bkt + 1].long()
+    # the key's segment lies in [lo, hi) and is its position in the sorted keys
+    seg = torch.searchsorted(uniq, keys.long())
+    assert bool(((seg >= lo) & (seg < hi)).all())
+    assert torch.equal(seg.int(), dd.inv[: keys.numel()])

@@ -10,7 +10,7 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 export FM_NO_AUTOBUILD=1
 cd $R
-timeout -k 10 400 python -u -m pytest tests/test_fwd_single_gpu.py tests/test_step_gpu.py tests/test_dist_gpu.py -v --timeout 120 --timeout-method thread > $OUT/pytest_single.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_dist_gpu.py tests/test_fwd_single_gpu.py tests/test_step_gpu.py -v --timeout 120 --timeout-method thread > $OUT/pytest_single.log 2>&1
 rc=$?
 grep -E "PASSED|FAILED|Error|differ" $OUT/pytest_single.log | tail -40
 tail -1 $OUT/pytest_single.log
