@@ -575,8 +575,9 @@ def seg_lookup_enabled() -> bool:
 
 
 def seg_index_bits(nnz: int, key_bits: int) -> tuple[int, int]:
-    """(shift, nb): about four buckets per occurrence-capacity / 4 ... i.e. nnz / 4 buckets
-    (a power of two in [16, 2^20]), bucket = key >> shift over ``key_bits``-bit keys."""
+    """(shift, nb) of the key-bucket index: nb ~ nnz / 4 buckets (a power of two in [16, 2^20],
+    at most 2^key_bits), bucket = key >> shift over ``key_bits``-bit keys.  A Criteo-shaped
+    batch (5.1M occurrences, ~378k unique keys) gets 2^20 buckets: ~0.4 keys per bucket."""
     bb = max(4, min(20, max(1, nnz).bit_length() - 2, key_bits))
     shift = max(0, key_bits - bb)
     return shift, 1 << (key_bits - shift)

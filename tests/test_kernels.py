@@ -175,3 +175,36 @@ def test_bf16_table_forward(device):
     fo = m.forward(b)
     pref, _, _ = fm_scores(_params_ref(m), b.offsets.cpu(), b.ids.cpu(), b.vals.cpu())
     torch.testing.assert_close(fo.pred.double().cpu(), pref, rtol=1e-4, atol=1e-4)
+
+
+def test_seg_index_sizing_and_lookup_contract():
+    """Key-bucket segment index (hip/dedup.hip seg_index_kernel; the row-sharded forward's
+    key -> segment lookup): sizing, and the build / lookup contract emulated in numpy -- every
+    bucket written exactly once (no clear), keys found in [idx[b], idx[b + 1])."""
+    import numpy as np
+
+    shift, nb = K.seg_index_bits(5_111_808, 27)
+    assert nb == 1 << 20 and shift == 7
+    assert K.seg_index_bits(100, 16) == (11, 32)      # ~nnz / 4 buckets, a power of two
+    assert K.seg_index_bits(10, 16) == (12, 16)       # at least 16
+    assert K.seg_index_bits(1 << 30, 12) == (0, 4096)  # never more buckets than keys
+    rng = np.random.default_rng(0)
+    for key_bits, n in ((20, 40000), (27, 100000), (16, 3000)):
+        keys = np.unique(rng.integers(0, (1 << key_bits) * 3 // 4, n))  # top of the range unused
+        shift, nb = K.seg_index_bits(n, key_bits)
+        U = len(keys)
+        idx = np.full(nb + 1, -1, np.int64)
+        writes = np.zeros(nb + 1, np.int64)
+        for s in range(U):  # the kernel's per-segment loop
+            lo = 0 if s == 0 else (keys[s - 1] >> shift) + 1
+            hi = keys[s] >> shift
+            idx[lo:hi + 1] = s
+            writes[lo:hi + 1] += 1
+        tail0 = (keys[-1] >> shift) + 1  # the grid-strided tail
+        idx[tail0:] = U
+        writes[tail0:] += 1
+        assert bool((writes == 1).all())
+        b = keys >> shift
+        lo, hi = idx[b], idx[b + 1]
+        seg = np.arange(U)
+        assert bool(((seg >= lo) & (seg < hi)).all())
