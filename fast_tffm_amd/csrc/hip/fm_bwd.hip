@@ -88,6 +88,7 @@ struct BwdArgs {
   int cold_split;           // 1: chunks of <= kColdMax occurrences go to fm_bwd_cold_kernel, the chunk kernel skips them
   SelfRows self;            // EMIT (row-sharded step): segments that are this rank's own table rows
   int fwd_single;           // 1 (LOCAL): rows with one occurrence were updated by the forward (fm_fwd.hip)
+  int chunk_pipe;           // 1: software-pipelined chunk kernel (16 lanes per row, unsliced)
 };
 
 constexpr int kColdMax = 4;  // occurrences of a "cold" chunk
@@ -440,6 +441,181 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
       }
     }
   }
+  }
+}
+
+// Software-pipelined chunk kernel (16 lanes per row: k=64 fp32 / bf16, k=128 fp8; 145-163 VGPRs,
+// 3 waves / SIMD like the plain kernel).  The
+// chunk kernel is latency-bound (wait 66%, profiles/r2/pmc_shard_seg.txt): each chunk is a chain
+// descriptor -> occurrence (example) -> dpred / r1 rows, beside its table row's loads, and most
+// chunks are one or two occurrences long.  Here a lane group issues the NEXT chunk's occurrence
+// and table-row loads before it reduces the current one and its dpred gathers right after, so
+// the current chunk waits for its r1 rows only (one memory latency per chunk instead of about
+// three).  Same per-chunk arithmetic and summation order as fm_bwd_chunk_kernel's generic path:
+// bitwise identical results.  Opt-in (FM_CHUNK_PIPE=1): the kernel itself runs 367 -> 316 us on
+// the k64 fp32 step, but the step does not get faster (0.679 -> 0.685 ms; the next batch's dedup
+// on the side stream becomes the longer chain and loses bandwidth to the faster kernel;
+// profiles/r2/chunk_pipe_ab.txt).
+template <int LPR, typename TV>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(chunk_min_waves<LPR, TV>())))
+void fm_bwd_chunk_pipe_kernel(BwdArgs a) {
+  static_assert(LPR >= FM_CHUNK_UNR && LPR < 32, "generic-path lane counts only");
+  const uint32_t sr = sr_step_seed(a.sr_counter);
+  constexpr int EPL = Frag<TV>::N;
+  constexpr int G = kWave / LPR;
+  constexpr int PF = (kMaxCH + LPR - 1) / LPR;
+  constexpr int UNR = FM_CHUNK_UNR;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPR, t = lane % LPR;
+  const int gbase = g * LPR;
+  const int nv = a.Kp / EPL;
+  const bool tact = t < nv;
+  const int tE = tact ? t : nv - 1;
+  const int nchunks = a.counts[1];
+  __shared__ int pr_start[kMaxPieceOwners], pr_pre[kMaxPieceOwners + 1];
+  const bool pieced = a.piece >= 0;
+  if (pieced) {
+    if (threadIdx.x == 0) {
+      int acc = 0;
+      for (int q = 0; q < a.n_owners; ++q) {
+        const int c0 = a.seg_chunk[a.seg_bounds[2 * q + a.piece]];
+        const int c1 = a.seg_chunk[a.seg_bounds[2 * q + a.piece + 1]];
+        pr_start[q] = c0;
+        pr_pre[q] = acc;
+        acc += c1 - c0;
+      }
+      pr_pre[a.n_owners] = acc;
+    }
+    __syncthreads();
+  }
+  const int i1 = pieced ? pr_pre[a.n_owners] : nchunks;
+  const int stride = gridDim.x * kWavesPerBlock * G;
+  auto chunk_at = [&](int i) {
+    if (pieced) {
+      int q = 0;
+      while (q + 1 < a.n_owners && pr_pre[q + 1] <= i) ++q;
+      return pr_start[q] + (i - pr_pre[q]);
+    }
+    return i;
+  };
+  struct Desc { int c, j0, j1, seg, key; };
+  auto load_desc = [&](int i, Desc& d) {
+    d.c = chunk_at(i);
+    d.j0 = a.chunk_start[d.c]; d.j1 = a.chunk_start[d.c + 1]; d.seg = a.chunk_seg[d.c]; d.key = a.chunk_key[d.c];
+  };
+  // chunks this kernel reduces (the others: MFMA dense rows, cold kernel, fused singletons)
+  auto active = [&](const Desc& d) {
+    const int len = d.j1 - d.j0;
+    const bool single = (unsigned)d.seg & kChunkSingle;
+    return !(d.seg & kChunkDense) && !(a.cold_split && len <= kColdMax) && !(a.fwd_single && single && len == 1);
+  };
+  // stage 1 of a chunk's occurrence prefetch: example indices and values (coalesced)
+  auto load_ex = [&](const Desc& d, int (&pex)[PF], float (&px)[PF]) {
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int jj = d.j0 + q * LPR + t;
+      const int jc = jj < d.j1 ? jj : d.j0;
+      pex[q] = a.sorted_ex[jc] >> a.ex_shift;
+      px[q] = a.sorted_x ? a.sorted_x[jc] : 1.f;
+    }
+  };
+  // stage 2: c = dpred * x (a gather by example)
+  auto load_c = [&](const Desc& d, const int (&pex)[PF], const float (&px)[PF], float (&pc)[PF]) {
+#pragma unroll
+    for (int q = 0; q < PF; ++q) pc[q] = d.j0 + q * LPR + t < d.j1 ? a.dpred[pex[q]] * px[q] : 0.f;
+  };
+
+  int ii = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g;
+  Desc cur{0, 0, 0, 0, 0}, nxt{0, 0, 0, 0, 0};
+  RowState<EPL> rs;
+  int pex[PF];
+  float pc[PF], px[PF];
+  bool cur_act = false;
+  if (ii < i1) {
+    load_desc(ii, cur);
+    cur_act = active(cur);
+    if (cur_act) {
+      if ((unsigned)cur.seg & kChunkSingle) bwd_load<TV, EPL>(a, cur.seg & kChunkSegMask, (long long)cur.key, tE, rs);
+      load_ex(cur, pex, px);
+      load_c(cur, pex, px, pc);
+    }
+    if (ii + stride < i1) load_desc(ii + stride, nxt);
+  }
+  for (; ii < i1; ii += stride) {
+    const bool has_next = ii + stride < i1;
+    // 1. the next chunk's descriptor after next, occurrences and table row: in flight while this
+    //    chunk is reduced
+    Desc nn{0, 0, 0, 0, 0};
+    RowState<EPL> rs_n;
+    int pex_n[PF];
+    float px_n[PF], pc_n[PF];
+    const bool nxt_act = has_next && active(nxt);
+    if (nxt_act) {
+      if ((unsigned)nxt.seg & kChunkSingle) bwd_load<TV, EPL>(a, nxt.seg & kChunkSegMask, (long long)nxt.key, tE, rs_n);
+      load_ex(nxt, pex_n, px_n);
+    }
+    if (ii + 2 * stride < i1) load_desc(ii + 2 * stride, nn);
+    // 2. this chunk: r1 gathers + reduction (fm_bwd_chunk_kernel's generic path)
+    float A[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) A[k] = 0.f;
+    float Scx = 0.f, Sc = 0.f;
+    const int len = cur.j1 - cur.j0;
+    if (cur_act) {
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        if (q * LPR < len) {
+          for (int l = 0; l < LPR && q * LPR + l < len; l += UNR) {
+            float rr[UNR][EPL], cc[UNR], xx[UNR];
+#pragma unroll
+            for (int uu = 0; uu < UNR; ++uu) {
+              const int li = l + uu;
+              const bool ok = li < LPR && q * LPR + li < len;
+              const int src = gbase + (ok ? li : 0);
+              const int ex = __shfl(pex[q], src, kWave);
+              const float cs = __shfl(pc[q], src, kWave);
+              cc[uu] = ok ? cs : 0.f;
+              xx[uu] = __shfl(px[q], src, kWave);
+              load_r1<TV, EPL>(a.r1, (long long)ex * a.Kp + tE * EPL, rr[uu]);
+            }
+#pragma unroll
+            for (int uu = 0; uu < UNR; ++uu) {
+#pragma unroll
+              for (int k = 0; k < EPL; ++k) A[k] += cc[uu] * rr[uu][k];
+              Scx += cc[uu] * xx[uu];
+              Sc += cc[uu];
+            }
+          }
+        }
+      }
+    }
+    // 3. the next chunk's dpred gathers (its example indices have arrived by now)
+    if (nxt_act) load_c(nxt, pex_n, px_n, pc_n);
+    // 4. finish this chunk
+    if (cur_act) {
+      const int u = cur.seg & kChunkSegMask;
+      if ((unsigned)cur.seg & kChunkSingle) {
+        bwd_finish<LPR, TV, EPL>(a, u, t, tact, rs, A, Scx, Sc, len, sr);
+      } else {
+        float* dst = a.partial + (long long)cur.c * (a.Kp + 4);
+        if (tact) {
+#pragma unroll
+          for (int k = 0; k < EPL; k += 4)
+            *reinterpret_cast<float4*>(dst + t * EPL + k) = make_float4(A[k], A[k + 1], A[k + 2], A[k + 3]);
+        }
+        if (t == 0) {
+          dst[a.Kp] = Scx;
+          dst[a.Kp + 1] = Sc;
+          if (cur.seg & kChunkFirst) a.multi[atomicAdd(&a.counts_rw[2], 1)] = u;
+        }
+      }
+    }
+    cur = nxt;
+    nxt = nn;
+    cur_act = nxt_act;
+    rs = rs_n;
+#pragma unroll
+    for (int q = 0; q < PF; ++q) { pex[q] = pex_n[q]; px[q] = px_n[q]; pc[q] = pc_n[q]; }
   }
 }
 
@@ -912,7 +1088,13 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
     const int gc = fill_grid(max_chunks, kWavesPerBlock * G, 16384);
     FM_DISPATCH(dtype, lpr, fm_bwd_cold_kernel, gc, st, ac);
   }
-  FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, ac);
+  if (a.chunk_pipe && !a.slice_list && lpr == 16) {  // (8 lanes: 169-173 VGPRs, 2 waves / SIMD)
+    if (dtype == kBF16) hipLaunchKernelGGL((fm_bwd_chunk_pipe_kernel<16, __hip_bfloat16>), dim3(g1), dim3(kBlock), 0, st, ac);
+    else if (dtype == kFP8) hipLaunchKernelGGL((fm_bwd_chunk_pipe_kernel<16, fp8e4m3>), dim3(g1), dim3(kBlock), 0, st, ac);
+    else hipLaunchKernelGGL((fm_bwd_chunk_pipe_kernel<16, float>), dim3(g1), dim3(kBlock), 0, st, ac);
+  } else {
+    FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, ac);
+  }
   const int g2 = fill_grid(max_unique, kWavesPerBlock * G, 2048);
   FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, a);
   FM_DISPATCH(dtype, lpr, fm_bwd_big_kernel, 1024, st, a);

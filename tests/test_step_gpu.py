@@ -6,6 +6,7 @@ import torch
 from fast_tffm_amd.data.synthetic import CriteoSynth, random_batch
 from fast_tffm_amd.models.fm import FactorizationMachine, FMConfig
 from fast_tffm_amd.ops import kernels as K
+from fast_tffm_amd.ops import native
 
 from oracle import reference_train_step
 
@@ -260,3 +261,27 @@ def test_csr_rows_matches_torch(B, maxf):
     torch.testing.assert_close(K.csr_rows(d, nnz=nnz).cpu(), ex, rtol=0, atol=0)
     bits = max(1, int(max(int(sizes.max()), 1) - 1).bit_length())
     torch.testing.assert_close(K.csr_rows(d, nnz=nnz, slot_bits=bits).cpu(), (ex << bits) | slot, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("k,dtype,opt", [(64, torch.float32, "adagrad"), (64, torch.bfloat16, "adagrad"),
+                                         (64, torch.float8_e4m3fn, "ftrl"), (60, torch.float32, "ftrl")])
+def test_pipelined_chunk_kernel_bitwise(monkeypatch, k, dtype, opt):
+    """fm_bwd_chunk_pipe_kernel (16-lane rows, FM_CHUNK_PIPE=1) == the plain chunk kernel, bit for bit."""
+    gen = CriteoSynth(30000, device="cuda", seed=17)
+    batches = [gen.batch(4096) for _ in range(3)]
+    o = K.OptConfig(opt, lr=0.05, l1=0.001, l2=0.001, beta=1.0)
+    res = []
+    for f in ("0", "1"):
+        monkeypatch.setenv("FM_CHUNK_PIPE", f)
+        m = FactorizationMachine(
+            FMConfig(vocabulary_size=30000, factor_num=k, loss_type="logistic", init_value_range=0.05, seed=3,
+                     opt=o, batch_size=512, factor_lambda=0.01, bias_lambda=0.01, dtype=dtype), device="cuda")
+        assert native.hip().lanes_per_row(m.Kp, K.dtype_code(m.table.v.dtype)) == 16
+        for i, bt in enumerate(batches):
+            m.train_step(bt, batches[i + 1] if i + 1 < len(batches) else None)
+        torch.cuda.synchronize()
+        st = m.table.state
+        res.append([x.clone() for x in (st.v, st.w, st.s0v, st.s0w) if x is not None])
+        m.close()
+    for x, y in zip(*res):
+        assert torch.equal(x.view(torch.uint8), y.view(torch.uint8))
