@@ -289,9 +289,12 @@ class FactorizationMachine:
         self.ws = _Workspace(self.device, self.Kp, cfg.dedup_chunk, K.r1_dtype(cfg.dtype))
         self.global_step = 0
         self._side = None
-        self._lslots = [_LocalSlot(), _LocalSlot()]   # lookahead dedup plans (eager local path)
+        # lookahead dedup plans (eager local path): the current step's plan and up to two pending
+        # ones (next batch, and the one after with the depth-2 lookahead) each own a slot
+        self._lslots = [_LocalSlot(), _LocalSlot(), _LocalSlot()]
         self._lpending = None
-        self._llast = 1
+        self._lpending2 = None
+        self._llast = 2
         self._ring = None
         self._graph = None
         self._graph_pool: list[_GraphedStep] = []
@@ -351,8 +354,8 @@ class FactorizationMachine:
         if self._exchange is not None:
             self._exchange.close()
             self._exchange = None
-        self._lpending = None
-        self._lslots = [_LocalSlot(), _LocalSlot()]
+        self._lpending = self._lpending2 = None
+        self._lslots = [_LocalSlot(), _LocalSlot(), _LocalSlot()]
         self._side = None
         self._dense_st = None
         if self.device.type == "cuda" and torch.cuda.is_initialized():
@@ -465,7 +468,7 @@ class FactorizationMachine:
             elif self._exchange is not None:
                 out = self._exchange.train_step(b)
             elif self.device.type == "cuda" and (next_batch is not None or self._lpending is not None):
-                out = self._local_lookahead_step(b, next_batch)
+                out = self._local_lookahead_step(b, next_batch, next2)
             else:
                 out = self._local_train_step(b)
         self.global_step += 1
@@ -525,8 +528,12 @@ class FactorizationMachine:
 
     # ------------------------------------------------------------------
     def _local_plan(self, b: Batch, inputs_ready=None) -> "_LocalPlan":
-        """dedup (+ csr_rows) of ``b`` on the side stream into a double-buffered slot."""
-        idx = (self._lpending.slot ^ 1) if self._lpending is not None else (self._llast ^ 1)
+        """dedup (+ csr_rows) of ``b`` on the side stream into the next of the plan slots.
+
+        Slots are taken round robin, so the live plans -- the current step's and at most two
+        pending ones, the last three created -- never share one; ``slot.done`` orders the reuse
+        after the step that last read it."""
+        idx = (self._llast + 1) % len(self._lslots)
         self._llast = idx
         slot = self._lslots[idx]
         cfg = self.cfg
@@ -597,10 +604,12 @@ class FactorizationMachine:
                           fwd_single=single is not None)
         return StepOut(fo.loss_sum, b.B)
 
-    def _local_lookahead_step(self, b: Batch, next_batch: Batch | None) -> StepOut:
+    def _local_lookahead_step(self, b: Batch, next_batch: Batch | None, next2: Batch | None = None) -> StepOut:
         """Eager local step with lookahead: the dedup of ``next_batch`` runs on the side stream
         concurrently with this step's forward + backward (the dedup of ``b`` was done the same
-        way during the previous step), taking the sort off the critical path."""
+        way during the previous step), taking the sort off the critical path.  With ``next2``
+        (depth-2 lookahead, FM_LOCAL_DEPTH2 != 0) the dedup of the batch after that is started
+        too, so a plan has a whole step of slack before its step needs it."""
         ws, cfg = self.ws, self.cfg
         main = torch.cuda.current_stream(self.device)
         nb_ready = None
@@ -609,16 +618,24 @@ class FactorizationMachine:
             nb_ready.record(main)
         pl = self._lpending
         if pl is not None and pl.b is b:
-            self._lpending = None
+            self._lpending, self._lpending2 = self._lpending2, None
         else:
+            self._lpending = self._lpending2 = None
             pl = self._local_plan(b)
         main.wait_event(pl.ready)
         out = self._fwd_bwd_local(b, pl.rows, pl.dd)
         done = torch.cuda.Event()
         done.record(main)
         self._lslots[pl.slot].done = done
-        if next_batch is not None:
+        if next_batch is not None and (self._lpending is None or self._lpending.b is not next_batch):
             self._lpending = self._local_plan(next_batch, nb_ready)
+            self._lpending2 = None
+        if (next2 is not None and self._lpending is not None and self._lpending2 is None
+                and os.environ.get("FM_LOCAL_DEPTH2", "1") != "0"):
+            if getattr(next2, "ready", None) is None and nb_ready is None:
+                nb_ready = torch.cuda.Event()
+                nb_ready.record(main)
+            self._lpending2 = self._local_plan(next2, nb_ready)
         return out
 
     def lookahead_graph_buffers(self, example: Batch, n: int = 4) -> list[Batch]:

@@ -1006,6 +1006,7 @@ class DPDenseExchange(DPExchange):
         if pl is not None and pl.b is b:
             m._lpending = None
         else:
+            m._lpending = m._lpending2 = None
             pl = m._local_plan(b)
         main.wait_event(pl.ready)
         dA = ws.dense_counts(b.B) if pl.dd.dense_list is not None else None
