@@ -236,8 +236,8 @@ def main() -> int:
                 "split_grads": bool(model._exchange.overlap_grads) if model.mode == "shard" else None,
                 "comm": getattr(model._exchange, "comm_mode", None),
                 "seg_lookup": K.seg_lookup_enabled() if model.mode == "shard" else None,
-                "lookahead": 2 if model.mode == "local" and os.environ.get("FM_LOCAL_DEPTH2", "1") != "0"
-                and len(pool) > 2 else (1 if model.mode == "local" else None),
+                "lookahead": (2 if os.environ.get("FM_LOCAL_DEPTH2", "1") != "0" and len(pool) > 2 else 1)
+                if model.mode == "local" and dev.type == "cuda" and not graphed else None,
                 "pool": len(pool),
                 "native_build": native_hashes(),
             },
