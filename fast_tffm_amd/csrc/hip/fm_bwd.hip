@@ -89,6 +89,7 @@ struct BwdArgs {
   SelfRows self;            // EMIT (row-sharded step): segments that are this rank's own table rows
   int fwd_single;           // 1 (LOCAL): rows with one occurrence were updated by the forward (fm_fwd.hip)
   int chunk_pipe;           // 1: software-pipelined chunk kernel (16 lanes per row, unsliced)
+  int chunk_grid;           // chunk kernel workgroup cap: 0 = per-row-width default, > 0 = this, < 0 = none
 };
 
 constexpr int kColdMax = 4;  // occurrences of a "cold" chunk
@@ -1056,7 +1057,14 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
     (void)hipMemsetAsync(a.big_count, 0, sizeof(int), st);
     (void)hipMemsetAsync(a.counts_rw + 2, 0, sizeof(int), st);  // #multi-chunk rows, appended by the chunk kernel
   }
-  const int g1 = (fill_grid(max_chunks, kWavesPerBlock * G) + 7) / 8 * 8;  // multiple of 8: XCD groups
+  int g1 = (fill_grid(max_chunks, kWavesPerBlock * G) + 7) / 8 * 8;  // multiple of 8: XCD groups
+  // Cap on the chunk kernel's workgroups (the grid-stride walk covers every chunk either way).
+  // Same-box sweeps (profiles/r2/chunk_grid_ab.txt): 16-lane rows (k=64 fp32 / bf16) 3456-4608
+  // blocks beat the 8192 fill cap by 2.5-3% (k64 fp32 0.677-0.685 -> 0.661-0.662 ms), 4-lane
+  // rows (k=16 bf16) 512-576 by 5.5% (0.519-0.522 -> 0.491-0.495 ms); for 32-lane rows (k=128)
+  // every cap tried was slower.  FM_CHUNK_GRID: > 0 overrides, < 0 disables.
+  const int cap = a.chunk_grid != 0 ? a.chunk_grid : (lpr == 16 ? 3840 : lpr == 4 ? 512 : -1);
+  if (cap > 0 && g1 > cap) g1 = (cap + 7) / 8 * 8;
   const bool dense = a.dense_list && a.dense_part && a.dense_A && a.piece < 0;
   if (a.piece >= 0 && (a.n_owners > kMaxPieceOwners || a.slice_list)) return -6;
   const bool fork = dense && dense_st && dense_st != st;
