@@ -219,6 +219,9 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
     if _is_gpu(rows):
         h = native.hip()
         grid = h.fwd_grid(max(B, 1))
+        fg = int(os.environ.get("FM_FWD_GRID", "0"))  # A/B knob: workgroup cap of the forward
+        if fg > 0:
+            grid = max(1, min(grid, fg))
         if partial is None or partial.numel() < 3 * grid:
             partial = torch.zeros(3 * grid, dtype=torch.float32, device=dev)
         lp = partial[:grid]
