@@ -1062,8 +1062,11 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   // Same-box sweeps (profiles/r2/chunk_grid_ab.txt): 16-lane rows (k=64 fp32 / bf16) 3456-4608
   // blocks beat the 8192 fill cap by 2.5-3% (k64 fp32 0.677-0.685 -> 0.661-0.662 ms), 4-lane
   // rows (k=16 bf16) 512-576 by 5.5% (0.519-0.522 -> 0.491-0.495 ms); for 32-lane rows (k=128)
-  // every cap tried was slower.  FM_CHUNK_GRID: > 0 overrides, < 0 disables.
-  const int cap = a.chunk_grid != 0 ? a.chunk_grid : (lpr == 16 ? 3840 : lpr == 4 ? 512 : -1);
+  // every cap tried was slower.  The local step only: the row-sharded step at world 1 runs
+  // steadiest without a cap (0.701-0.702 ms vs 0.68-0.73 with 3840; chunk_grid_ab.txt).
+  // FM_CHUNK_GRID: > 0 overrides, < 0 disables.
+  const int cap = a.chunk_grid != 0 ? a.chunk_grid
+                  : a.mode != kBwdLocal ? -1 : (lpr == 16 ? 3840 : lpr == 4 ? 512 : -1);
   if (cap > 0 && g1 > cap) g1 = (cap + 7) / 8 * 8;
   const bool dense = a.dense_list && a.dense_part && a.dense_A && a.piece < 0;
   if (a.piece >= 0 && (a.n_owners > kMaxPieceOwners || a.slice_list)) return -6;
