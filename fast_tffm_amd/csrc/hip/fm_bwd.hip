@@ -1057,7 +1057,8 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
     (void)hipMemsetAsync(a.big_count, 0, sizeof(int), st);
     (void)hipMemsetAsync(a.counts_rw + 2, 0, sizeof(int), st);  // #multi-chunk rows, appended by the chunk kernel
   }
-  int g1 = (fill_grid(max_chunks, kWavesPerBlock * G) + 7) / 8 * 8;  // multiple of 8: XCD groups
+  // (an explicit FM_CHUNK_GRID above fill_grid's 8192 cap raises the grid: A/B knob)
+  int g1 = (fill_grid(max_chunks, kWavesPerBlock * G, a.chunk_grid > 8192 ? a.chunk_grid : 8192) + 7) / 8 * 8;
   // Cap on the chunk kernel's workgroups (the grid-stride walk covers every chunk either way).
   // Same-box sweeps (profiles/r2/chunk_grid_ab.txt): 16-lane rows (k=64 fp32 / bf16) 3456-4608
   // blocks beat the 8192 fill cap by 2.5-3% (k64 fp32 0.677-0.685 -> 0.661-0.662 ms), 4-lane
