@@ -90,6 +90,7 @@ struct BwdArgs {
   int fwd_single;           // 1 (LOCAL): rows with one occurrence were updated by the forward (fm_fwd.hip)
   int chunk_pipe;           // 1: software-pipelined chunk kernel (16 lanes per row, unsliced)
   int chunk_grid;           // chunk kernel workgroup cap: 0 = per-row-width default, > 0 = this, < 0 = none
+  int combine_grid, big_grid;  // > 0: workgroups of the combine (cap) / big-row kernels (A/B knobs)
 };
 
 constexpr int kColdMax = 4;  // occurrences of a "cold" chunk
@@ -1107,9 +1108,10 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   } else {
     FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, ac);
   }
-  const int g2 = fill_grid(max_unique, kWavesPerBlock * G, 2048);
+  // (A/B knobs: combine_grid / big_grid > 0 replace the 2048 cap / the 1024 workgroups)
+  const int g2 = fill_grid(max_unique, kWavesPerBlock * G, a.combine_grid > 0 ? a.combine_grid : 2048);
   FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, a);
-  FM_DISPATCH(dtype, lpr, fm_bwd_big_kernel, 1024, st, a);
+  FM_DISPATCH(dtype, lpr, fm_bwd_big_kernel, a.big_grid > 0 ? a.big_grid : 1024, st, a);
   if (dense) {
     if (fork) (void)hipStreamWaitEvent(st, dense_join_event(), 0);
     FM_DISPATCH(dtype, lpr, fm_bwd_dense_apply_kernel, kMaxDense, st, a);

@@ -163,9 +163,10 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
          u64 dense_part, int nex, u64 dense_stream, int dtype,
          long long max_chunks, long long max_unique, u64 stream, int g_wcol, int g_bf16, u64 sr_counter,
          int counters_ready, u64 seg_bounds, int piece, int n_owners, u64 dense_A, int cold_split,
-         const std::vector<long long>& self, int fwd_single, int chunk_pipe, int chunk_grid) {
+         const std::vector<long long>& self, int fwd_single, int chunk_pipe, int chunk_grid, int combine_grid,
+         int big_grid) {
         fm::BwdArgs a{};
-        a.chunk_grid = chunk_grid;
+        a.chunk_grid = chunk_grid; a.combine_grid = combine_grid; a.big_grid = big_grid;
         a.fwd_single = fwd_single;
         a.chunk_pipe = chunk_pipe;
         if (fwd_single && mode == fm::kBwdEmitTable) throw std::runtime_error("fm_bwd: fwd_single: LOCAL / EMIT modes");
@@ -210,7 +211,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("g_bf16") = 0, py::arg("sr_counter") = 0, py::arg("counters_ready") = 0, py::arg("seg_bounds") = 0,
       py::arg("piece") = -1, py::arg("n_owners") = 0, py::arg("dense_A") = 0, py::arg("cold_split") = 0,
       py::arg("self_rows") = std::vector<long long>{}, py::arg("fwd_single") = 0, py::arg("chunk_pipe") = 0,
-      py::arg("chunk_grid") = 0);
+      py::arg("chunk_grid") = 0, py::arg("combine_grid") = 0, py::arg("big_grid") = 0);
 
   m.def("dedup_workspace_bytes", &fm::dedup_workspace_bytes, py::arg("n"));
 

@@ -727,7 +727,9 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               dense_A=_p(dense_A) if dd.dense_list is not None else 0,
               cold_split=int(os.environ.get("FM_COLD_SPLIT", "0") == "1"), fwd_single=int(bool(fwd_single)),
               chunk_pipe=int(os.environ.get("FM_CHUNK_PIPE", "0") == "1"),
-              chunk_grid=int(os.environ.get("FM_CHUNK_GRID", "0")), **skw)
+              chunk_grid=int(os.environ.get("FM_CHUNK_GRID", "0")),
+              combine_grid=int(os.environ.get("FM_COMBINE_GRID", "0")),
+              big_grid=int(os.environ.get("FM_BIG_GRID", "0")), **skw)
         dd.bwd_fresh = False  # a second backward over this grouping zeroes its counters itself
     else:
         _check(self_rows is None, "self rows are a GPU path")
