@@ -106,8 +106,9 @@ def main() -> int:
     ctx = fmdist.init_distributed(force_pg=mode not in ("auto", "local"), device=p.get("device"),
                                   timeout_s=float(os.environ.get("FM_PG_TIMEOUT", "300")))
     W, rank = ctx.world, ctx.rank
-    if W != a.gpus and rank == 0:
-        print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={W}; using {W}", file=sys.stderr)
+    if W != a.gpus:  # (the __main__ guard already refused this; library callers of main() too)
+        print(f"[bench] error: --gpus {a.gpus} but WORLD_SIZE={W}", file=sys.stderr)
+        return 2
     dev = ctx.device
     if dev.type != "cuda":
         print("[bench] no GPU visible: running on CPU (not a valid measurement)", file=sys.stderr)
@@ -181,6 +182,8 @@ def main() -> int:
     if dev.type == "cuda":
         torch.cuda.synchronize()
 
+    ex = model._exchange
+    comm0 = getattr(ex, "bytes_sent", 0)
     t_start = time.perf_counter()
     last = None
     for i in range(a.steps):
@@ -190,8 +193,17 @@ def main() -> int:
     ctx.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t_start
-    elapsed = ctx.all_reduce_scalar(elapsed, op="max")
+    elapsed_own = time.perf_counter() - t_start
+    elapsed = ctx.all_reduce_scalar(elapsed_own, op="max")
+    elapsed_min = ctx.all_reduce_scalar(elapsed_own, op="min")
+    # bytes this rank put on the wire to OTHER ranks per timed step (all-to-all rows / ids /
+    # gradients, all-reduce / all-gather payloads: parallel/exchange.py accounting), max over ranks
+    comm_own = (getattr(ex, "bytes_sent", 0) - comm0) / max(a.steps, 1)
+    comm_max = ctx.all_reduce_scalar(comm_own, op="max")
+    import torch.distributed as tdist
+
+    rccl_world = tdist.get_world_size(ctx.group) if (ctx.group is not None and tdist.is_initialized()) else 1
+    comm_backend = tdist.get_backend(ctx.group) if (ctx.group is not None and tdist.is_initialized()) else None
 
     loss = last.mean_loss() if last is not None else float("nan")
     if a.profile_steps and rank == 0:
@@ -239,6 +251,12 @@ def main() -> int:
                 "lookahead": (2 if os.environ.get("FM_LOCAL_DEPTH2", "1") != "0" and len(pool) > 2 else 1)
                 if model.mode == "local" and dev.type == "cuda" and not graphed else None,
                 "pool": len(pool),
+                # world size of the process group the step's collectives ran on (RCCL on GPUs)
+                "rccl_world": rccl_world,
+                "comm_backend": comm_backend,
+                # timed-loop wall time per step, slowest / fastest rank (value uses the slowest)
+                "per_rank_ms": {"max": elapsed / a.steps * 1e3, "min": elapsed_min / a.steps * 1e3},
+                "comm_bytes_per_rank": int(round(comm_max)),
                 "native_build": native_hashes(),
             },
         })
@@ -253,7 +271,44 @@ def main() -> int:
 # lines there when the CPU side-group is created) -- goes to stderr
 _RESULT_FD = 1
 
+
+def _launch_guard(argv: list[str]) -> int | None:
+    """Multi-GPU invocations without a launcher.  ``--gpus N`` (N > 1) with no torchrun
+    environment: start the N ranks here through ``torch.distributed.run`` (one process per GPU,
+    rendezvous on 127.0.0.1, like the driver's own launch) and return its exit code -- this
+    process never touches the GPU (``import torch`` does not initialise HIP), so the ranks own
+    the devices.  ``--gpus N`` disagreeing with an existing WORLD_SIZE is an error (exit 2): a
+    1-rank measurement must never be reported as an N-GPU one.  None: run in this process."""
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=1)
+    known, _ = pre.parse_known_args(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != known.gpus:
+            print(f"[bench] error: --gpus {known.gpus} but WORLD_SIZE={env_world} (launch {known.gpus} ranks, or "
+                  f"pass --gpus {env_world})", file=sys.stderr)
+            return 2
+        return None
+    if known.gpus <= 1:
+        return None
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(known.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    print(f"[bench] launching {known.gpus} ranks: {' '.join(cmd)}", file=sys.stderr)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
 if __name__ == "__main__":
+    _rc = _launch_guard(sys.argv[1:])
+    if _rc is not None:
+        sys.exit(_rc)
     _RESULT_FD = os.dup(1)
     os.dup2(2, 1)
     sys.exit(main())

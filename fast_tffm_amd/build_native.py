@@ -32,15 +32,10 @@ ARCH = os.environ.get("FM_OFFLOAD_ARCH", "gfx950")
 CPU_SOURCES = ["cpu/module.cpp", "cpu/parser.cpp", "cpu/kernels.cpp", "cpu/loader.cpp", "cpu/bincsr.cpp"]
 HIP_SOURCES = ["hip/module.hip"]
 # A/B build variants of the gfx950 module: name -> preprocessor defines (module _fm_hip_<name>,
-# selected at run time with FM_HIP_VARIANT=<name>; tools/gpu_ab.sh).  Used for same-box kernel
-# comparisons, e.g. {"pipe": ["-DFM_VARIANT_PIPE"]} measured the software-pipelined fwd/chunk
-# kernels at -0.6% step time under the lookahead step (not kept: no clear win).
-HIP_VARIANTS: dict[str, list[str]] = {"nocap": ["-DFM_CHUNK_NOCAP"], "capf32": ["-DFM_CHUNK_CAP_F32"],
-                                      "unr4": ["-DFM_CHUNK_UNR=4"], "unr6": ["-DFM_CHUNK_UNR=6"],
-                                      "unr16": ["-DFM_CHUNK_UNR=16"], "unr12": ["-DFM_CHUNK_UNR=12"],
-                                      "fwdw5": ["-DFM_FWD_WAVES_LPR16=5"],
-                                      "fwdw6": ["-DFM_FWD_WAVES_LPR16=6"], "noshort": ["-DFM_NO_SHORT_CHUNK"],
-                                      "fp8packed": ["-DFM_FWD_FP8_PACKED=1"]}
+# selected at run time with FM_HIP_VARIANT=<name>; tools/gpu_ab.sh).  Same-box kernel comparisons
+# of a change against its predecessor; a variant is deleted with the losing code path once the
+# A/B is recorded under profiles/ (round 1-2's nocap / unr* / fwdw* / fp8packed went that way).
+HIP_VARIANTS: dict[str, list[str]] = {"fwdnopf": ["-DFM_FWD_PREFETCH=0"]}
 
 
 _EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"  # resolved once (lazy init is not thread-safe)

@@ -76,8 +76,7 @@ def main(argv: list[str] | None = None) -> int:
     if dist_info.get("world", int(os.environ.get("WORLD_SIZE", "1"))) > 1 or cfg.mode not in ("auto", "local"):
         # multi-rank step: compute, lookahead and RCCL streams need their own hardware
         # queues (HIP's default 4 makes them share and serialize); before HIP starts
-        if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
-            os.environ["GPU_MAX_HW_QUEUES"] = "8"
+        fmdist.ensure_hw_queues()
 
     if args.task == "predict" and cfg.log_dir is None:
         print("Missing log directory. Must include a checkpoint file.")

@@ -15,11 +15,9 @@
 //        tile_scan   -- one workgroup scans the tile totals (U, #chunks)
 //        tile_emit   -- re-reads its tile, block-scans the flags and writes
 //                       unique keys, segment starts, first chunk of each
-//                       segment, chunk starts, chunk->segment, the optional
+//                       segment, chunk starts, chunk->segment and the optional
 //                       inverse map / per-sorted-occurrence example index and
-//                       value, and (sliced schedule) per-slice chunk counts;
-//   3. (sliced schedule) scan of the per-(slice, tile) counts and a scatter of
-//      the chunk ids into per-example-slice lists for the backward.
+//                       value.
 // Chunks cut every segment at CH-aligned sorted positions, so no chunk is
 // longer than CH and a hot id (tens of thousands of occurrences in Criteo's
 // low-cardinality fields) is spread over many lane groups in the backward.
@@ -31,23 +29,17 @@ namespace fm {
 constexpr int kRleItems = 8;                     // elements per thread
 constexpr int kRleTile = kBlock * kRleItems;     // 2048 elements per tile
 constexpr int kMaxTiles = 1024 * 64;             // single-workgroup tile scan limit (n < 134M)
-constexpr int kMaxSlices = 64;
 
 struct RleArgs {
   int n, CH, ntiles;
-  int slice_shift;                // example slice = ex >> slice_shift; < 0: no slicing
-  int nslices;                    // example slices (<= kMaxSlices)
-  int hot;                        // a row is "hot" at j when skeys[j -/+ hot] has its key (multiple of 8)
   int dense_min;                  // rows with >= dense_min occurrences are "dense" (0: none)
   int* dense_list;                // [kMaxDense] segment ids of the first dense rows in key order
   const uint32_t* skeys;          // sorted keys
   const int* spay;                // sorted payload (occurrence or example index)
-  const int* sex;                 // sorted example index (== spay when the payload is the example), or null
   int ex_shift;                   // > 0: payload / ex_of_occ hold packed codes (example << ex_shift | slot)
   const int* offsets;             // [B+1] CSR offsets (packed codes -> occurrence index)
   unsigned* tile_cnt;             // [3][ntiles] heads, chunk starts, dense heads per tile
   unsigned* tile_off;             // [3][ntiles] exclusive offsets
-  unsigned* slice_cnt;            // [nslices][ntiles] chunks per (slice, tile)
   uint32_t* uniq;                 // [n] unique keys (first U valid)
   int* seg_start;                 // [n+1]
   int* seg_chunk;                 // [n+1] first chunk of each segment
@@ -60,12 +52,7 @@ struct RleArgs {
   int* sorted_ex;                 // [n] (payload = occurrence)
   const float* vals;              // [n] (payload = occurrence)
   float* sorted_x;                // [n] (payload = occurrence)
-  uint8_t* single_flag;           // [n] occurrence -> 1 if its key occurs once (zeroed before), or null
 };
-
-__device__ inline int sorted_example(const RleArgs& a, int j) {
-  return (a.sex ? a.sex[j] : a.ex_of_occ[a.spay[j]]) >> a.ex_shift;
-}
 
 // v[q] = p[j0 + q] (fill outside [0, n)); two 16-byte loads when in range (j0 % 8 == 0).
 template <typename T>
@@ -83,17 +70,10 @@ __device__ inline void load8(const T* p, int j0, int n, T (&v)[8], T fill) {
 
 // Flags of one thread's 8 consecutive sorted positions j0..j0+7.
 //   head:   first occurrence of a key;
-//   cstart: chunk boundary = head, CH-aligned position, or -- for hot rows --
-//           a change of example slice (a hot row's occurrences are sorted by
-//           example, so each of its chunks reads r1 from one slice; see
-//           fm_bwd.hip, XCD-sliced schedule);
-//   slice:  (chunk starts) list the chunk goes to: its example slice for a
-//           hot row, chunk id mod nslices otherwise (no locality to exploit:
-//           spread evenly).
+//   cstart: chunk boundary = head or CH-aligned position.
 struct Rle8 {
   uint32_t k[8];
-  bool hd[8], cs[8], hot[8];
-  int ex[8];
+  bool hd[8], cs[8];
 };
 
 __device__ inline void rle_flags8(const RleArgs& a, int j0, Rle8& r) {
@@ -106,37 +86,12 @@ __device__ inline void rle_flags8(const RleArgs& a, int j0, Rle8& r) {
     const bool ok = j < a.n;
     r.hd[q] = ok && (j == 0 || r.k[q] != (q ? r.k[q - 1] : kp));
     r.cs[q] = r.hd[q] || (ok && j % a.CH == 0);
-    r.hot[q] = false;
-    r.ex[q] = 0;
-  }
-  if (a.slice_shift < 0) return;
-  uint32_t kl[8], kr[8];
-  load8(a.skeys, j0 - a.hot, a.n, kl, kNone);
-  load8(a.skeys, j0 + a.hot, a.n, kr, kNone);
-  if (a.sex) {
-    load8(a.sex, j0, a.n, r.ex, 0);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) r.ex[q] >>= a.ex_shift;
-  } else {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) r.ex[q] = j0 + q < a.n ? sorted_example(a, j0 + q) : 0;
-  }
-  const int ep = (j0 > 0 && j0 <= a.n) ? sorted_example(a, j0 - 1) : 0;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    r.hot[q] = r.k[q] != kNone && (kl[q] == r.k[q] || kr[q] == r.k[q]);
-    if (r.hot[q] && !r.cs[q])  // not a head: j > 0
-      r.cs[q] = (r.ex[q] >> a.slice_shift) != ((q ? r.ex[q - 1] : ep) >> a.slice_shift);
   }
 }
 
 // Head of a row with at least dense_min occurrences (the MFMA backward path, fm_bwd.hip).
 __device__ inline bool dense_head(const RleArgs& a, int j, uint32_t k) {
   return a.dense_min > 0 && j + a.dense_min - 1 < a.n && a.skeys[j + a.dense_min - 1] == k;
-}
-
-__device__ inline int chunk_slice(const RleArgs& a, bool hot, int ex, int c) {
-  return hot ? min(ex >> a.slice_shift, a.nslices - 1) : c % a.nslices;
 }
 
 // Block-wide exclusive scan of NC per-thread counts (segment heads, chunk
@@ -248,12 +203,8 @@ __global__ __launch_bounds__(1024) void rle_tile_scan_kernel(RleArgs a) {
 }
 
 __global__ __launch_bounds__(kBlock) void rle_tile_emit_kernel(RleArgs a) {
-  __shared__ unsigned sc[kMaxSlices];
   const int tile = blockIdx.x;
   const int j0 = tile * kRleTile + threadIdx.x * kRleItems;
-  const bool sliced = a.slice_shift >= 0;
-  if (sliced)
-    for (int sl = threadIdx.x; sl < kMaxSlices; sl += kBlock) sc[sl] = 0;
   Rle8 r;
   rle_flags8(a, j0, r);
   unsigned v[3] = {0u, 0u, 0u}, ex[3], tot[3];
@@ -265,7 +216,7 @@ __global__ __launch_bounds__(kBlock) void rle_tile_emit_kernel(RleArgs a) {
     v[1] += r.cs[q];
     v[2] += dn[q];
   }
-  block_excl_scan<3>(v, ex, tot);  // (its barriers also order the sc[] reset)
+  block_excl_scan<3>(v, ex, tot);
   // running (inclusive) segment / chunk / dense-row ids of this thread's elements
   int s = (int)(a.tile_off[tile] + ex[0]) - 1;
   int ch = (int)(a.tile_off[a.ntiles + tile] + ex[1]) - 1;
@@ -289,31 +240,15 @@ __global__ __launch_bounds__(kBlock) void rle_tile_emit_kernel(RleArgs a) {
     }
     if (r.cs[q]) {
       // a head chunk is the row's only one iff the row ends before the next CH-aligned cut
-      // (slice cuts only split rows longer than 8 CH)
       const int b = (j / a.CH + 1) * a.CH;
       const bool single = r.hd[q] && (b >= a.n || a.skeys[b] != r.k[q]);
       a.chunk_start[ch] = j;
       a.chunk_seg[ch] = (int)((unsigned)s | (r.hd[q] ? (unsigned)kChunkFirst : 0u) | (single ? kChunkSingle : 0u));
       a.chunk_key[ch] = (int)r.k[q];
-      if (sliced) atomicAdd(&sc[chunk_slice(a, r.hot[q], r.ex[q], ch)], 1u);
     }
   }
-  // one-occurrence rows (the forward's fused singleton update, fm_fwd.hip): head whose key
-  // differs from the next sorted key
-  bool sg[kRleItems];
-  bool any_sg = false;
   const bool need_all = a.inv || a.sorted_ex || a.sorted_x;
-#pragma unroll
-  for (int q = 0; q < kRleItems; ++q) sg[q] = false;
-  if (a.single_flag) {
-    const uint32_t knext = j0 + kRleItems < a.n ? a.skeys[j0 + kRleItems] : 0xffffffffu;
-#pragma unroll
-    for (int q = 0; q < kRleItems; ++q) {
-      sg[q] = r.hd[q] && (q + 1 < kRleItems ? r.k[q + 1] : knext) != r.k[q];
-      any_sg |= sg[q];
-    }
-  }
-  if (need_all || any_sg) {
+  if (need_all) {
     // payload = occurrence (or packed code): all 8 random gathers / scatters of the thread in flight at once
     int p[kRleItems];
     load8(a.spay, j0, a.n, p, 0);
@@ -321,7 +256,7 @@ __global__ __launch_bounds__(kBlock) void rle_tile_emit_kernel(RleArgs a) {
       const int mask = (1 << a.ex_shift) - 1;
 #pragma unroll
       for (int q = 0; q < kRleItems; ++q)
-        p[q] = j0 + q < a.n && (need_all || sg[q]) ? a.offsets[p[q] >> a.ex_shift] + (p[q] & mask) : 0;
+        p[q] = j0 + q < a.n ? a.offsets[p[q] >> a.ex_shift] + (p[q] & mask) : 0;
     }
     int exv[kRleItems];
     float xv[kRleItems];
@@ -335,14 +270,9 @@ __global__ __launch_bounds__(kBlock) void rle_tile_emit_kernel(RleArgs a) {
     for (int q = 0; q < kRleItems; ++q) {
       if (j0 + q >= a.n) break;
       if (a.inv) a.inv[p[q]] = sq[q];
-      if (a.single_flag && sg[q]) a.single_flag[p[q]] = 1;
       if (a.sorted_ex) a.sorted_ex[j0 + q] = exv[q];
       if (a.sorted_x) a.sorted_x[j0 + q] = xv[q];
     }
-  }
-  if (sliced) {
-    __syncthreads();
-    for (int sl = threadIdx.x; sl < a.nslices; sl += kBlock) a.slice_cnt[sl * a.ntiles + tile] = sc[sl];
   }
 }
 
@@ -356,42 +286,6 @@ __global__ __launch_bounds__(kBlock) void mark_dense_chunks_kernel(RleArgs a) {
 }
 
 static size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
-
-// ---------------------------------------------------------------------------
-// Per-slice chunk lists for the XCD-sliced backward schedule.  The emit kernel
-// counted the chunks of every (slice, RLE tile); after an exclusive scan of
-// those counts (slice-major) each tile scatters its chunk ids into the lists.
-// Order inside a list is irrelevant to the results.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void slice_scatter_kernel(RleArgs a, const unsigned* off, int* list,
-                                                               int* slice_start) {
-  __shared__ unsigned cur[kMaxSlices];
-  for (int s = threadIdx.x; s < kMaxSlices; s += kBlock) cur[s] = 0;
-  __syncthreads();
-  const int tile = blockIdx.x;
-  const int C = a.counts[1];
-  const int c0 = (int)a.tile_off[a.ntiles + tile];
-  const int c1 = tile + 1 < a.ntiles ? (int)a.tile_off[a.ntiles + tile + 1] : C;
-  for (int c = c0 + threadIdx.x; c < c1; c += kBlock) {
-    const int j = a.chunk_start[c];
-    const uint32_t k = a.skeys[j];
-    const bool hot = (j >= a.hot && a.skeys[j - a.hot] == k) || (j + a.hot < a.n && a.skeys[j + a.hot] == k);
-    const int s = chunk_slice(a, hot, hot ? sorted_example(a, j) : 0, c);
-    list[off[s * a.ntiles + tile] + atomicAdd(&cur[s], 1u)] = c;
-  }
-  if (tile == 0) {
-    for (int s = threadIdx.x; s < a.nslices; s += kBlock) slice_start[s] = (int)off[s * a.ntiles];
-    if (threadIdx.x == 0) slice_start[a.nslices] = C;
-  }
-}
-
-static size_t slice_scan_bytes(int n) {
-  const size_t m = (size_t)kMaxSlices * (((size_t)n + kRleTile - 1) / kRleTile);
-  size_t b = 0;
-  (void)rocprim::exclusive_scan((void*)nullptr, b, (const unsigned*)nullptr, (unsigned*)nullptr, 0u, m,
-                                rocprim::plus<unsigned>(), 0);
-  return align_up(b) + 2 * align_up(m * sizeof(unsigned));
-}
 
 // Onesweep configuration measured on MI355X for 5.1M (key, int32) pairs with
 // 27-bit keys (tools/bench_sort.hip, interleaved rounds): rocPRIM's default
@@ -438,11 +332,11 @@ static size_t sort_temp_bytes(int n, hipStream_t st) {
   return align_up(best);
 }
 
-// Workspace layout: [rocprim sort temp | tile_cnt(3*ntiles) | tile_off(3*ntiles) | slice scan temp | cnt | off]
+// Workspace layout: [rocprim sort temp | tile_cnt(3*ntiles) | tile_off(3*ntiles)]
 size_t dedup_workspace_bytes(int n) {
   if (n <= 0) return 256;
   const size_t ntiles = ((size_t)n + kRleTile - 1) / kRleTile;
-  return sort_temp_bytes(n, 0) + 2 * align_up(3 * ntiles * sizeof(unsigned)) + slice_scan_bytes(n) + 256;
+  return sort_temp_bytes(n, 0) + 2 * align_up(3 * ntiles * sizeof(unsigned)) + 256;
 }
 
 struct DedupArgs {
@@ -465,16 +359,11 @@ struct DedupArgs {
   int* sorted_ex;          // nullable
   const float* vals;       // nullable
   float* sorted_x;         // nullable
-  uint8_t* single_flag;    // nullable: [n] 1 = the occurrence's key occurs once (needs occurrence-decodable payloads)
   int payload_is_ex;       // payload carries the example index (sorted payload == sorted example)
   int ex_shift;            // > 0: the payload is the packed code (example << ex_shift | slot), see csr_rows
   const int* offsets;      // [B+1] (ex_shift > 0)
-  int slice_shift;         // < 0: no slicing; else example slice = ex >> slice_shift
   int dense_min;           // rows with >= dense_min occurrences go to the MFMA backward (0: off)
   int* dense_list;         // [kMaxDense]
-  int nslices;             // slices (<= kMaxSlices)
-  int* slice_list;         // [n] chunk ids grouped by slice
-  int* slice_start;        // [nslices + 1]
   void* ws;
   size_t ws_bytes;
 };
@@ -527,42 +416,18 @@ int launch_dedup(const DedupArgs& a, hipStream_t st) {
   char* base = static_cast<char*>(a.ws);
   unsigned* tile_cnt = reinterpret_cast<unsigned*>(base + tmp);
   unsigned* tile_off = reinterpret_cast<unsigned*>(base + tmp + align_up(3 * (size_t)ntiles * sizeof(unsigned)));
-  if (tmp + 2 * align_up(3 * (size_t)ntiles * sizeof(unsigned)) + slice_scan_bytes(a.n) > a.ws_bytes) return -2;
+  if (tmp + 2 * align_up(3 * (size_t)ntiles * sizeof(unsigned)) > a.ws_bytes) return -2;
 
-  if (a.single_flag) {
-    if (a.payload_is_ex && a.ex_shift <= 0) return -7;  // sorted payload must decode to the occurrence
-    (void)hipMemsetAsync(a.single_flag, 0, (size_t)a.n, st);
-  }
   size_t sort_bytes = tmp;
   hipError_t e = sort_pairs(a.ws, sort_bytes, a.keys, a.skeys, a.payload, a.spay, a.n, a.end_bit, st);
   if (e != hipSuccess) return (int)e;
-  const bool sliced = a.slice_shift >= 0 && a.nslices > 0 && a.nslices <= kMaxSlices && a.slice_list;
-  // slice scan scratch: [rocprim temp | cnt | off], m = nslices * ntiles
-  const size_t m = (size_t)kMaxSlices * (size_t)ntiles;
-  char* sbase = base + tmp + 2 * align_up(3 * (size_t)ntiles * sizeof(unsigned));
-  const size_t scan_cap = slice_scan_bytes(a.n) - 2 * align_up(m * sizeof(unsigned));
-  unsigned* cnt = reinterpret_cast<unsigned*>(sbase + scan_cap);
-  unsigned* off = reinterpret_cast<unsigned*>(sbase + scan_cap + align_up(m * sizeof(unsigned)));
-  RleArgs r{a.n, a.CH, ntiles, sliced ? a.slice_shift : -1, sliced ? a.nslices : 0, 8 * a.CH,
-            a.dense_list ? a.dense_min : 0, a.dense_list, a.skeys, a.spay,
-            a.payload_is_ex ? a.spay : nullptr, a.ex_shift, a.offsets, tile_cnt, tile_off, cnt, a.uniq, a.seg_start, a.seg_chunk,
-            a.chunk_start, a.chunk_seg, a.chunk_key, a.counts, a.inv, a.ex_of_occ, a.sorted_ex, a.vals, a.sorted_x, a.single_flag};
+  RleArgs r{a.n, a.CH, ntiles, a.dense_list ? a.dense_min : 0, a.dense_list, a.skeys, a.spay, a.ex_shift,
+            a.offsets, tile_cnt, tile_off, a.uniq, a.seg_start, a.seg_chunk, a.chunk_start, a.chunk_seg,
+            a.chunk_key, a.counts, a.inv, a.ex_of_occ, a.sorted_ex, a.vals, a.sorted_x};
   hipLaunchKernelGGL(rle_tile_count_kernel, dim3(ntiles), dim3(kBlock), 0, st, r);
   hipLaunchKernelGGL(rle_tile_scan_kernel, dim3(1), dim3(1024), 0, st, r);
   hipLaunchKernelGGL(rle_tile_emit_kernel, dim3(ntiles), dim3(kBlock), 0, st, r);
   if (r.dense_min > 0) hipLaunchKernelGGL(mark_dense_chunks_kernel, dim3(kMaxDense), dim3(kBlock), 0, st, r);
-  if (!sliced) return (int)hipGetLastError();
-
-  // per-slice chunk lists
-  const size_t ms = (size_t)a.nslices * ntiles;
-  size_t scan_bytes = 0;
-  (void)rocprim::exclusive_scan((void*)nullptr, scan_bytes, (const unsigned*)nullptr, (unsigned*)nullptr, 0u, ms,
-                                rocprim::plus<unsigned>(), st);
-  if (scan_bytes > scan_cap) return -4;
-  e = rocprim::exclusive_scan(sbase, scan_bytes, cnt, off, 0u, ms, rocprim::plus<unsigned>(), st);
-  if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(slice_scatter_kernel, dim3(ntiles), dim3(kBlock), 0, st, r, off, a.slice_list,
-                     a.slice_start);
   return (int)hipGetLastError();
 }
 

@@ -35,6 +35,9 @@ enum BwdMode : int { kBwdLocal = 0, kBwdEmit = 1, kBwdEmitTable = 2 };
 constexpr int kMaxCH = 32;        // chunk length cap (prefetch registers)
 constexpr int kSmallChunks = 16;  // rows with more chunks go to the workgroup combine
 constexpr int kMaxPieceOwners = 64;  // owners of a split backward piece
+// r1 rows in flight per lane in the chunk kernel: 8 beats 4 / 6 (fewer VGPRs, more waves) and 12 /
+// 16 on k64 fp32, k64 bf16 and k128 fp8 (profiles/r1s3/chunk_unroll_ab.txt)
+constexpr int kChunkUnr = 8;
 
 struct BwdArgs {
   int mode;                 // BwdMode
@@ -78,22 +81,13 @@ struct BwdArgs {
   int* big_count;           // device scalar, zeroed by the launcher
   int* multi;               // [counts[2]] rows spanning more than one chunk (filled by the chunk kernel)
   int* counts_rw;           // == counts, writable (counts[2] = #multi, zeroed by the launcher)
-  const int* slice_list;    // chunk ids grouped by example slice, or null
-  const int* slice_start;   // [nslices + 1]
-  int nslices;
   const int* dense_list;    // [kMaxDense] dense rows (dedup), counts[3] of them; null: no dense path
   float* dense_part;        // [gridDim(dense) * kMaxDense, Kp + 4] per-workgroup partial rows
   int nex;                  // examples in the batch (dense path)
   const uint8_t* dense_A;   // [nex, kMaxDense] occurrence counts of the dense rows (written by the forward)
-  int cold_split;           // 1: chunks of <= kColdMax occurrences go to fm_bwd_cold_kernel, the chunk kernel skips them
   SelfRows self;            // EMIT (row-sharded step): segments that are this rank's own table rows
-  int fwd_single;           // 1 (LOCAL): rows with one occurrence were updated by the forward (fm_fwd.hip)
-  int chunk_pipe;           // 1: software-pipelined chunk kernel (16 lanes per row, unsliced)
   int chunk_grid;           // chunk kernel workgroup cap: 0 = per-row-width default, > 0 = this, < 0 = none
-  int combine_grid, big_grid;  // > 0: workgroups of the combine (cap) / big-row kernels (A/B knobs)
 };
-
-constexpr int kColdMax = 4;  // occurrences of a "cold" chunk
 
 // Parameter row + optimizer slots of one segment, read before its gradient is
 // known so that the loads overlap the occurrence reduction.
@@ -227,14 +221,10 @@ __device__ inline void bwd_finalize(const BwdArgs& a, int u, int t, bool tact, i
 // 128 costs no spills.  1 = no constraint (the compiler's own choice).
 template <int LPR, typename TV>
 constexpr int chunk_min_waves() {
-#if defined(FM_CHUNK_NOCAP)
-  return 1;
-#elif defined(FM_CHUNK_CAP_F32)  // A/B: also the fp32 k=64 kernel (135 VGPRs -> 128 + 44 B/lane of spills)
-  return ((sizeof(TV) == 1 && LPR == 32) || (sizeof(TV) == 4 && LPR == 16)) ? 4 : 1;
-#else
-  // (bf16 LPR 32 -- k=128 bf16 -- crossed to 129 VGPRs with the short-chunk path: capped too)
+  // (bf16 LPR 32 -- k=128 bf16 -- crossed to 129 VGPRs with the short-chunk path: capped too; the
+  // same cap on the fp32 k=64 kernel, 135 -> 128 VGPRs + 44 B/lane of spills, made the k=64 step
+  // 10% slower: profiles/r1s3/chunk_vgpr_cap_ab.txt)
   return LPR == 32 ? 4 : 1;
-#endif
 }
 
 // One lane group per chunk of <= CH (<= kMaxCH) sorted occurrences of one row.
@@ -245,10 +235,7 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
   constexpr int EPL = Frag<TV>::N;  // elements per lane of the table dtype
   constexpr int G = kWave / LPR;
   constexpr int PF = (kMaxCH + LPR - 1) / LPR;  // prefetched occurrences per lane
-#ifndef FM_CHUNK_UNR
-#define FM_CHUNK_UNR 8
-#endif
-  constexpr int UNR = LPR < FM_CHUNK_UNR ? LPR : FM_CHUNK_UNR;  // r1 rows in flight per lane
+  constexpr int UNR = LPR < kChunkUnr ? LPR : kChunkUnr;  // r1 rows in flight per lane
   constexpr bool kShortPath = LPR >= 32;                          // short-chunk block (below)
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR, t = lane % LPR;
@@ -274,23 +261,13 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
     }
     __syncthreads();
   }
-  // XCD-sliced schedule: workgroups b = x (mod 8) share an XCD under the observed
-  // round-robin dispatch (speed only, never correctness) and walk the chunk lists
-  // of example slices x, x+8, ... in order, so the r1 rows they gather stay in
-  // that XCD's L2.  Unsliced: one linear walk over all chunks.
-  const int nslc = a.slice_list ? a.nslices : 0;
-  const int nx = nslc ? 8 : 1;
-  const int wave_in_x = (blockIdx.x / nx) * kWavesPerBlock + (threadIdx.x >> 6);
-  const int stride = (gridDim.x / nx) * kWavesPerBlock * G;
-  for (int s = nslc ? (int)(blockIdx.x % nx) : 0; s < (nslc ? nslc : 1); s += nx) {
-  const int i0 = nslc ? a.slice_start[s] : 0;
-  const int i1 = nslc ? a.slice_start[s + 1] : (pieced ? pr_pre[a.n_owners] : nchunks);
+  const int i1 = pieced ? pr_pre[a.n_owners] : nchunks;
+  const int stride = gridDim.x * kWavesPerBlock * G;
   // Software pipeline over this lane group's chunks: the descriptor of the next
   // chunk (and the list entry of the one after) load while the current one is
   // reduced, so the dependent metadata chain is off the critical path.
-  int ii = i0 + wave_in_x * G + g;
+  int ii = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g;
   auto chunk_at = [&](int i) {
-    if (nslc) return a.slice_list[i];
     if (pieced) {
       int q = 0;
       while (q + 1 < a.n_owners && pr_pre[q + 1] <= i) ++q;
@@ -317,8 +294,6 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
     }
     if (dense) continue;  // gradient from the MFMA path (fm_bwd_dense_kernel)
     const int len = j1 - j0;
-    if (a.fwd_single && single && len == 1) continue;  // updated by the forward (fused singleton)
-    if (a.cold_split && len <= kColdMax) continue;  // fm_bwd_cold_kernel's
     RowState<EPL> rs;
     if (single) bwd_load<TV, EPL>(a, u, (long long)key, tE, rs);
     // lane-parallel prefetch of the chunk's (example, dpred*x, x)
@@ -339,13 +314,13 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
 #pragma unroll
     for (int k = 0; k < EPL; ++k) A[k] = 0.f;
     float Scx = 0.f, Sc = 0.f;
-    if constexpr (LPR < FM_CHUNK_UNR) {
+    if constexpr (LPR < kChunkUnr) {
       // narrow rows (k=16 bf16: LPR 2): flat walk over the chunk's occurrences with
-      // FM_CHUNK_UNR r1 rows in flight per lane (the q-major walk below keeps only LPR in
+      // kChunkUnr r1 rows in flight per lane (the q-major walk below keeps only LPR in
       // flight); same summation order.  k16 bf16 step 0.525 -> 0.497 ms; for LPR >= 8 the
       // flat walk measured slower (k64 0.652 -> 0.665, k128 fp8 0.989 -> 1.039 ms):
       // profiles/r1s4/chunk_flat_ab.txt
-      constexpr int UNRF = FM_CHUNK_UNR;
+      constexpr int UNRF = kChunkUnr;
 #pragma unroll
       for (int o0 = 0; o0 < PF * LPR; o0 += UNRF) {
         if (o0 >= len) break;
@@ -370,7 +345,6 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
           Sc += cc[uu];
         }
       }
-#ifndef FM_NO_SHORT_CHUNK
     } else if (kShortPath && len <= 4) {
       // short chunks (275k of the 378k rows of a Criteo-shaped batch occur once, 341k of
       // the 510k chunks have <= 4 occurrences): one block of 4 r1 rows instead of UNR,
@@ -396,7 +370,6 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
         Scx += cc[uu] * xx[uu];
         Sc += cc[uu];
       }
-#endif
     } else {
 #pragma unroll
       for (int q = 0; q < PF; ++q) {
@@ -440,266 +413,6 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
         dst[a.Kp + 1] = Sc;
         // the row's first chunk registers the row for the combine kernels
         if (first) a.multi[atomicAdd(&a.counts_rw[2], 1)] = u;
-      }
-    }
-  }
-  }
-}
-
-// Software-pipelined chunk kernel (16 lanes per row: k=64 fp32 / bf16, k=128 fp8; 145-163 VGPRs,
-// 3 waves / SIMD like the plain kernel).  The
-// chunk kernel is latency-bound (wait 66%, profiles/r2/pmc_shard_seg.txt): each chunk is a chain
-// descriptor -> occurrence (example) -> dpred / r1 rows, beside its table row's loads, and most
-// chunks are one or two occurrences long.  Here a lane group issues the NEXT chunk's occurrence
-// and table-row loads before it reduces the current one and its dpred gathers right after, so
-// the current chunk waits for its r1 rows only (one memory latency per chunk instead of about
-// three).  Same per-chunk arithmetic and summation order as fm_bwd_chunk_kernel's generic path:
-// bitwise identical results.  Opt-in (FM_CHUNK_PIPE=1): the kernel itself runs 367 -> 316 us on
-// the k64 fp32 step, but the step does not get faster (0.679 -> 0.685 ms; the next batch's dedup
-// on the side stream becomes the longer chain and loses bandwidth to the faster kernel;
-// profiles/r2/chunk_pipe_ab.txt).
-template <int LPR, typename TV>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(chunk_min_waves<LPR, TV>())))
-void fm_bwd_chunk_pipe_kernel(BwdArgs a) {
-  static_assert(LPR >= FM_CHUNK_UNR && LPR < 32, "generic-path lane counts only");
-  const uint32_t sr = sr_step_seed(a.sr_counter);
-  constexpr int EPL = Frag<TV>::N;
-  constexpr int G = kWave / LPR;
-  constexpr int PF = (kMaxCH + LPR - 1) / LPR;
-  constexpr int UNR = FM_CHUNK_UNR;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int g = lane / LPR, t = lane % LPR;
-  const int gbase = g * LPR;
-  const int nv = a.Kp / EPL;
-  const bool tact = t < nv;
-  const int tE = tact ? t : nv - 1;
-  const int nchunks = a.counts[1];
-  __shared__ int pr_start[kMaxPieceOwners], pr_pre[kMaxPieceOwners + 1];
-  const bool pieced = a.piece >= 0;
-  if (pieced) {
-    if (threadIdx.x == 0) {
-      int acc = 0;
-      for (int q = 0; q < a.n_owners; ++q) {
-        const int c0 = a.seg_chunk[a.seg_bounds[2 * q + a.piece]];
-        const int c1 = a.seg_chunk[a.seg_bounds[2 * q + a.piece + 1]];
-        pr_start[q] = c0;
-        pr_pre[q] = acc;
-        acc += c1 - c0;
-      }
-      pr_pre[a.n_owners] = acc;
-    }
-    __syncthreads();
-  }
-  const int i1 = pieced ? pr_pre[a.n_owners] : nchunks;
-  const int stride = gridDim.x * kWavesPerBlock * G;
-  auto chunk_at = [&](int i) {
-    if (pieced) {
-      int q = 0;
-      while (q + 1 < a.n_owners && pr_pre[q + 1] <= i) ++q;
-      return pr_start[q] + (i - pr_pre[q]);
-    }
-    return i;
-  };
-  struct Desc { int c, j0, j1, seg, key; };
-  auto load_desc = [&](int i, Desc& d) {
-    d.c = chunk_at(i);
-    d.j0 = a.chunk_start[d.c]; d.j1 = a.chunk_start[d.c + 1]; d.seg = a.chunk_seg[d.c]; d.key = a.chunk_key[d.c];
-  };
-  // chunks this kernel reduces (the others: MFMA dense rows, cold kernel, fused singletons)
-  auto active = [&](const Desc& d) {
-    const int len = d.j1 - d.j0;
-    const bool single = (unsigned)d.seg & kChunkSingle;
-    return !(d.seg & kChunkDense) && !(a.cold_split && len <= kColdMax) && !(a.fwd_single && single && len == 1);
-  };
-  // stage 1 of a chunk's occurrence prefetch: example indices and values (coalesced)
-  auto load_ex = [&](const Desc& d, int (&pex)[PF], float (&px)[PF]) {
-#pragma unroll
-    for (int q = 0; q < PF; ++q) {
-      const int jj = d.j0 + q * LPR + t;
-      const int jc = jj < d.j1 ? jj : d.j0;
-      pex[q] = a.sorted_ex[jc] >> a.ex_shift;
-      px[q] = a.sorted_x ? a.sorted_x[jc] : 1.f;
-    }
-  };
-  // stage 2: c = dpred * x (a gather by example)
-  auto load_c = [&](const Desc& d, const int (&pex)[PF], const float (&px)[PF], float (&pc)[PF]) {
-#pragma unroll
-    for (int q = 0; q < PF; ++q) pc[q] = d.j0 + q * LPR + t < d.j1 ? a.dpred[pex[q]] * px[q] : 0.f;
-  };
-
-  int ii = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g;
-  Desc cur{0, 0, 0, 0, 0}, nxt{0, 0, 0, 0, 0};
-  RowState<EPL> rs;
-  int pex[PF];
-  float pc[PF], px[PF];
-  bool cur_act = false;
-  if (ii < i1) {
-    load_desc(ii, cur);
-    cur_act = active(cur);
-    if (cur_act) {
-      if ((unsigned)cur.seg & kChunkSingle) bwd_load<TV, EPL>(a, cur.seg & kChunkSegMask, (long long)cur.key, tE, rs);
-      load_ex(cur, pex, px);
-      load_c(cur, pex, px, pc);
-    }
-    if (ii + stride < i1) load_desc(ii + stride, nxt);
-  }
-  for (; ii < i1; ii += stride) {
-    const bool has_next = ii + stride < i1;
-    // 1. the next chunk's descriptor after next, occurrences and table row: in flight while this
-    //    chunk is reduced
-    Desc nn{0, 0, 0, 0, 0};
-    RowState<EPL> rs_n;
-    int pex_n[PF];
-    float px_n[PF], pc_n[PF];
-    const bool nxt_act = has_next && active(nxt);
-    if (nxt_act) {
-      if ((unsigned)nxt.seg & kChunkSingle) bwd_load<TV, EPL>(a, nxt.seg & kChunkSegMask, (long long)nxt.key, tE, rs_n);
-      load_ex(nxt, pex_n, px_n);
-    }
-    if (ii + 2 * stride < i1) load_desc(ii + 2 * stride, nn);
-    // 2. this chunk: r1 gathers + reduction (fm_bwd_chunk_kernel's generic path)
-    float A[EPL];
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) A[k] = 0.f;
-    float Scx = 0.f, Sc = 0.f;
-    const int len = cur.j1 - cur.j0;
-    if (cur_act) {
-#pragma unroll
-      for (int q = 0; q < PF; ++q) {
-        if (q * LPR < len) {
-          for (int l = 0; l < LPR && q * LPR + l < len; l += UNR) {
-            float rr[UNR][EPL], cc[UNR], xx[UNR];
-#pragma unroll
-            for (int uu = 0; uu < UNR; ++uu) {
-              const int li = l + uu;
-              const bool ok = li < LPR && q * LPR + li < len;
-              const int src = gbase + (ok ? li : 0);
-              const int ex = __shfl(pex[q], src, kWave);
-              const float cs = __shfl(pc[q], src, kWave);
-              cc[uu] = ok ? cs : 0.f;
-              xx[uu] = __shfl(px[q], src, kWave);
-              load_r1<TV, EPL>(a.r1, (long long)ex * a.Kp + tE * EPL, rr[uu]);
-            }
-#pragma unroll
-            for (int uu = 0; uu < UNR; ++uu) {
-#pragma unroll
-              for (int k = 0; k < EPL; ++k) A[k] += cc[uu] * rr[uu][k];
-              Scx += cc[uu] * xx[uu];
-              Sc += cc[uu];
-            }
-          }
-        }
-      }
-    }
-    // 3. the next chunk's dpred gathers (its example indices have arrived by now)
-    if (nxt_act) load_c(nxt, pex_n, px_n, pc_n);
-    // 4. finish this chunk
-    if (cur_act) {
-      const int u = cur.seg & kChunkSegMask;
-      if ((unsigned)cur.seg & kChunkSingle) {
-        bwd_finish<LPR, TV, EPL>(a, u, t, tact, rs, A, Scx, Sc, len, sr);
-      } else {
-        float* dst = a.partial + (long long)cur.c * (a.Kp + 4);
-        if (tact) {
-#pragma unroll
-          for (int k = 0; k < EPL; k += 4)
-            *reinterpret_cast<float4*>(dst + t * EPL + k) = make_float4(A[k], A[k + 1], A[k + 2], A[k + 3]);
-        }
-        if (t == 0) {
-          dst[a.Kp] = Scx;
-          dst[a.Kp + 1] = Sc;
-          if (cur.seg & kChunkFirst) a.multi[atomicAdd(&a.counts_rw[2], 1)] = u;
-        }
-      }
-    }
-    cur = nxt;
-    nxt = nn;
-    cur_act = nxt_act;
-    rs = rs_n;
-#pragma unroll
-    for (int q = 0; q < PF; ++q) { pex[q] = pex_n[q]; px[q] = px_n[q]; pc[q] = pc_n[q]; }
-  }
-}
-
-// Cold chunks (<= kColdMax occurrences: 341k of the 510k chunks of a Criteo-shaped batch,
-// mostly rows that occur once) in a kernel of their own.  Such a chunk is a chain of
-// dependent loads (descriptor -> occurrence -> dpred / r1 row) plus one table-row
-// read-modify-write, with almost nothing to compute: the chunk kernel's 8-deep r1
-// unroll and its 133 VGPRs (3 waves / SIMD) leave too few of them in flight to cover
-// the latency.  This kernel keeps 4 r1 rows and one row state per lane group, runs at
-// twice the occupancy and pipelines the next chunk's descriptor.  Same summation order
-// as the chunk kernel's short-chunk path (bitwise identical results).
-template <int LPR, typename TV>
-__global__ __launch_bounds__(kBlock) void fm_bwd_cold_kernel(BwdArgs a) {
-  const uint32_t sr = sr_step_seed(a.sr_counter);
-  constexpr int EPL = Frag<TV>::N;
-  constexpr int G = kWave / LPR;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int g = lane / LPR, t = lane % LPR;
-  const int gbase = g * LPR;
-  const int nv = a.Kp / EPL;
-  const bool tact = t < nv;
-  const int tE = tact ? t : nv - 1;
-  const int nchunks = a.counts[1];
-  const int stride = gridDim.x * kWavesPerBlock * G;
-  int ii = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g;
-  int d_j0 = 0, d_j1 = 0;
-  if (ii < nchunks) { d_j0 = a.chunk_start[ii]; d_j1 = a.chunk_start[ii + 1]; }
-  for (; ii < nchunks; ii += stride) {
-    const int c = ii, j0 = d_j0, j1 = d_j1;
-    if (ii + stride < nchunks) { d_j0 = a.chunk_start[ii + stride]; d_j1 = a.chunk_start[ii + stride + 1]; }
-    const int len = j1 - j0;
-    if (len > kColdMax) continue;
-    const int seg = a.chunk_seg[c];
-    if (seg & kChunkDense) continue;
-    const int u = seg & kChunkSegMask;
-    const bool single = (unsigned)seg & kChunkSingle;
-    if (a.fwd_single && single && len == 1) continue;  // updated by the forward (fused singleton)
-    RowState<EPL> rs;
-    if (single) bwd_load<TV, EPL>(a, u, (long long)a.chunk_key[c], tE, rs);
-    int pex = 0;
-    float pc = 0.f, px = 0.f;
-    if (t < len) {
-      const int jj = j0 + t;
-      pex = a.sorted_ex[jj] >> a.ex_shift;
-      px = a.sorted_x ? a.sorted_x[jj] : 1.f;
-      pc = a.dpred[pex] * px;
-    }
-    float rr[kColdMax][EPL], cc[kColdMax], xx[kColdMax];
-#pragma unroll
-    for (int uu = 0; uu < kColdMax; ++uu) {
-      const bool ok = uu < len;
-      const int src = gbase + (ok ? uu : 0);
-      const int ex = __shfl(pex, src, kWave);
-      const float cs = __shfl(pc, src, kWave);
-      cc[uu] = ok ? cs : 0.f;
-      xx[uu] = __shfl(px, src, kWave);
-      load_r1<TV, EPL>(a.r1, (long long)ex * a.Kp + tE * EPL, rr[uu]);
-    }
-    float A[EPL];
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) A[k] = 0.f;
-    float Scx = 0.f, Sc = 0.f;
-#pragma unroll
-    for (int uu = 0; uu < kColdMax; ++uu) {
-#pragma unroll
-      for (int k = 0; k < EPL; ++k) A[k] += cc[uu] * rr[uu][k];
-      Scx += cc[uu] * xx[uu];
-      Sc += cc[uu];
-    }
-    if (single) {
-      bwd_finish<LPR, TV, EPL>(a, u, t, tact, rs, A, Scx, Sc, len, sr);
-    } else {
-      float* dst = a.partial + (long long)c * (a.Kp + 4);
-      if (tact) {
-#pragma unroll
-        for (int k = 0; k < EPL; k += 4)
-          *reinterpret_cast<float4*>(dst + t * EPL + k) = make_float4(A[k], A[k + 1], A[k + 2], A[k + 3]);
-      }
-      if (t == 0) {
-        dst[a.Kp] = Scx;
-        dst[a.Kp + 1] = Sc;
-        if (seg & kChunkFirst) a.multi[atomicAdd(&a.counts_rw[2], 1)] = u;
       }
     }
   }
@@ -1071,7 +784,7 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
                   : a.mode != kBwdLocal ? -1 : (lpr == 16 ? 3840 : lpr == 4 ? 512 : -1);
   if (cap > 0 && g1 > cap) g1 = (cap + 7) / 8 * 8;
   const bool dense = a.dense_list && a.dense_part && a.dense_A && a.piece < 0;
-  if (a.piece >= 0 && (a.n_owners > kMaxPieceOwners || a.slice_list)) return -6;
+  if (a.piece >= 0 && a.n_owners > kMaxPieceOwners) return -6;
   const bool fork = dense && dense_st && dense_st != st;
   hipStream_t ds = fork ? dense_st : st;
   if (dense) {
@@ -1092,26 +805,14 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
     }
     if (fork) (void)hipEventRecord(dense_join_event(), ds);
   }
-  // cold chunks in their own kernel (full-batch walks only: not with the sliced schedule or
-  // split-backward pieces); opt-in (a.cold_split, FM_COLD_SPLIT=1): measured slower (k64 fp32
-  // 0.667 -> 0.705 ms, k128 fp8 FTRL 0.973 -> 1.081 ms; profiles/r2/cold_split_ab.txt)
-  BwdArgs ac = a;
-  ac.cold_split = a.cold_split && a.piece < 0 && !a.slice_list && lpr >= kColdMax ? 1 : 0;
-  if (ac.cold_split) {
-    const int gc = fill_grid(max_chunks, kWavesPerBlock * G, 16384);
-    FM_DISPATCH(dtype, lpr, fm_bwd_cold_kernel, gc, st, ac);
-  }
-  if (a.chunk_pipe && !a.slice_list && lpr == 16) {  // (8 lanes: 169-173 VGPRs, 2 waves / SIMD)
-    if (dtype == kBF16) hipLaunchKernelGGL((fm_bwd_chunk_pipe_kernel<16, __hip_bfloat16>), dim3(g1), dim3(kBlock), 0, st, ac);
-    else if (dtype == kFP8) hipLaunchKernelGGL((fm_bwd_chunk_pipe_kernel<16, fp8e4m3>), dim3(g1), dim3(kBlock), 0, st, ac);
-    else hipLaunchKernelGGL((fm_bwd_chunk_pipe_kernel<16, float>), dim3(g1), dim3(kBlock), 0, st, ac);
-  } else {
-    FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, ac);
-  }
-  // (A/B knobs: combine_grid / big_grid > 0 replace the 2048 cap / the 1024 workgroups)
-  const int g2 = fill_grid(max_unique, kWavesPerBlock * G, a.combine_grid > 0 ? a.combine_grid : 2048);
+  // (a software-pipelined variant that issued the next chunk's occurrence and row loads before
+  // reducing the current one ran 367 -> 316 us alone but made the step slower twice:
+  // profiles/r2/chunk_pipe_ab.txt, profiles/r3/fwd_prefetch_ab.txt; removed)
+  FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, a);
+  // (workgroup counts: a 2048 cap / 1024 measured best among 512-8192, profiles/r2/combine_grid_ab.txt)
+  const int g2 = fill_grid(max_unique, kWavesPerBlock * G, 2048);
   FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, a);
-  FM_DISPATCH(dtype, lpr, fm_bwd_big_kernel, a.big_grid > 0 ? a.big_grid : 1024, st, a);
+  FM_DISPATCH(dtype, lpr, fm_bwd_big_kernel, 1024, st, a);
   if (dense) {
     if (fork) (void)hipStreamWaitEvent(st, dense_join_event(), 0);
     FM_DISPATCH(dtype, lpr, fm_bwd_dense_apply_kernel, kMaxDense, st, a);

@@ -42,15 +42,6 @@ struct FwdArgs {
   const int* dense_count;  // device scalar: number of dense rows (capped at kMaxDense here)
   uint8_t* dense_A;        // [B, kMaxDense] occurrence counts (saturated at 255)
   SelfRows self;           // row-sharded step: segments read from this rank's own table rows
-  // Fused singleton update: single_flag[o] = 1 when occurrence o's row occurs
-  // nowhere else in the batch (written by the dedup, which ran before this forward).  Its
-  // whole gradient is c * (r1_i - x v) with c = dpred_i * x, and this kernel holds r1_i and
-  // dpred_i in registers when it finishes example i, so it applies the optimizer to the row
-  // right there (upd: the backward's arguments -- LOCAL: table + optimizer; EMIT, the
-  // row-sharded step: wire rows, gradient rows, self rows) and the backward skips the row's
-  // one-occurrence chunk.  Null: off.
-  const uint8_t* single_flag;
-  BwdArgs upd;
   // Segment lookup (row-sharded step, dedup.hip seg_index_kernel): rows[] hold the shard keys
   // and each occurrence's segment is found through the bucket index instead of an inverse map.
   const int* seg_idx;      // [nb + 1] first segment of each key bucket, or null (rows are segment ids)
@@ -69,10 +60,8 @@ __device__ inline int seg_lookup(const FwdArgs& a, int k) {
   return s;
 }
 
-// A/B build knob (variant "fp8packed"): fp8 rows kept packed in flight, a whole example per
-// round.  Measured slower: k128 fp8 FTRL step 0.93 -> 1.04 ms (profiles/r2/fp8_forward_ab.txt)
-#ifndef FM_FWD_FP8_PACKED
-#define FM_FWD_FP8_PACKED 0
+#ifndef FM_FWD_PREFETCH
+#define FM_FWD_PREFETCH 1
 #endif
 constexpr int kSelfBit = (int)0x80000000u;   // row index tag: this rank's own table row (SelfRows)
 constexpr int kDenseHash = 4 * kMaxDense;  // open-addressing table of the dense keys (LDS, load <= 1/4)
@@ -103,98 +92,19 @@ struct FwdUnroll {
 // Minimum waves per SIMD of the forward (amdgpu_waves_per_eu; 1 = compiler's choice): the
 // 32/64-lane instantiations (k>=128) need 132-136 VGPRs -> 3 waves/SIMD uncapped; capped at
 // 4 the k=128 FTRL step runs 1.038 -> 0.992 ms (fp32) and 1.033 -> 0.987 ms (fp8)
-// (profiles/r1s3/fwd_cap_ab.txt).  FM_FWD_WAVES_LPR16=N forces a floor on the k=64 (16-lane)
-// instantiations (A/B build knob: 5 or 6 waves spill, 0.65 -> 0.73 / 0.86 ms).
+// (profiles/r1s3/fwd_cap_ab.txt).  A floor of 5 or 6 on the k=64 (16-lane) instantiations spills:
+// 0.65 -> 0.73 / 0.86 ms (round 1 A/B variants, since removed).
 template <int LPR, typename TV>
 constexpr int fwd_min_waves() {
-#if defined(FM_FWD_WAVES_LPR16)
-  if (LPR == 16) return FM_FWD_WAVES_LPR16;
-#endif
   return LPR >= 32 ? 4 : 1;
 }
 
-// FM_FWD_FP8_PACKED: fp8 rows stay packed while in flight (one VGPR per row per lane instead
-// of four, converted at use), so a whole Criteo-shaped example is issued in one round:
-// ceil(40 / G) rows per lane group, up to 24 (k=128: 20 instead of 12).
-template <int G>
-struct FwdUnrollPacked {
-  static constexpr int v = ((40 + G - 1) / G) > 24 ? 24 : ((40 + G - 1) / G);
-};
-
-// Lane of the k-th (0-based) set bit of m (k < popcount(m)): the largest p with
-// popcount(m & ((1 << p) - 1)) <= k.
-__device__ inline int nth_set_bit(uint64_t m, int k) {
-  int p = 0;
-#pragma unroll
-  for (int step = 32; step > 0; step >>= 1)
-    if (__popcll(m & ((1ull << (p + step)) - 1ull)) <= k) p += step;
-  return p;
-}
-
-// r1 as the backward reads it back (bf16 for fp8 tables, R1Bf16)
-template <typename TV>
-__device__ inline float r1_stored(float s) {
-  if constexpr (R1Bf16<TV>::v) return bf16_bits_to_f32(f32_to_bf16_bits(s));
-  else return s;
-}
-
-// Optimizer step (LOCAL) or gradient row (EMIT) for the rows of example i [s, e) that occur
-// only there (see FwdArgs::single_flag).  Row group g takes the flagged occurrences g, g + G, ... of each 64-wide
-// window; the gradient is formed exactly as the chunk kernel forms a one-occurrence chunk
-// (A = c r1, Scx = c x, Sc = c, n_u = 1), so the table ends up bitwise as without the fusion.
-template <int LPR, typename TV, int EPL>
-__device__ inline void fwd_single_update(const FwdArgs& a, int s, int e, int lane, int g, int t, bool tact, int tE,
-                                         float dp, const float (&s1)[EPL], uint32_t sr) {
-  constexpr int G = kWave / LPR;
-  float r1q[EPL];
-#pragma unroll
-  for (int k = 0; k < EPL; ++k) r1q[k] = r1_stored<TV>(s1[k]);
-  for (int base = s; base < e; base += kWave) {
-    const int m = min(kWave, e - base);
-    const bool f = lane < m && a.single_flag[base + lane] != 0;
-    const uint64_t mask = __ballot(f);
-    if (mask == 0ull) continue;
-    int my_row = f ? a.rows[base + lane] : 0;
-    if (f && a.seg_idx) my_row = seg_lookup(a, my_row);
-    const float my_x = f ? (a.vals ? a.vals[base + lane] : 1.f) : 0.f;
-    const int n1 = __popcll(mask);
-    for (int q = 0; q < n1; q += G) {
-      const int kth = q + g;
-      const int src = kth < n1 ? nth_set_bit(mask, kth) : 0;
-      const int row = __shfl(my_row, src, kWave);
-      const float x = __shfl(my_x, src, kWave);
-      if (kth < n1) {  // (uniform per row group: store_row's group shuffles stay inside it)
-        // LOCAL: `row` is the table row; EMIT (row-sharded step): the segment id, whose
-        // gradient row goes to grad_out[u] (or, a self row no other rank asked for, whose
-        // optimizer step is applied in place)
-        const bool local = a.upd.mode == kBwdLocal;
-        const int u = local ? 0 : row;
-        const long long key = local ? (long long)row : (long long)a.upd.uniq[row];
-        RowState<EPL> rs;
-        bwd_load<TV, EPL>(a.upd, u, key, tE, rs);
-        const float c = dp * x;
-        // the chunk kernel's sums start at 0 and accumulate with fma: same roundings here, and
-        // explicit fmas, so that the compiler cannot contract c * r1 into bwd_finish's
-        // A - Scx v (which would round differently)
-        float A[EPL];
-#pragma unroll
-        for (int k = 0; k < EPL; ++k) A[k] = __builtin_fmaf(c, r1q[k], 0.f);
-        bwd_finish<LPR, TV, EPL>(a.upd, u, t, tact, rs, A, __builtin_fmaf(c, x, 0.f), c, 1, sr);
-      }
-    }
-  }
-}
-
-// (FUSED: the fused singleton update is compiled in; a separate instantiation, so the plain
-// forward keeps its register budget -- the update's code raised the k=64 fp32 kernel from 124
-// to 132 VGPRs, one wave per SIMD less, when it was only switched off at run time)
-template <int LPR, typename TV, bool FUSED>
+template <int LPR, typename TV>
 __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
   using F = Frag<TV>;
   constexpr int EPL = F::N;
   constexpr int G = kWave / LPR;
-  constexpr bool kPacked = F::kScaled && FM_FWD_FP8_PACKED;
-  constexpr int UNR = kPacked ? FwdUnrollPacked<G>::v : FwdUnroll<G>::v;
+  constexpr int UNR = FwdUnroll<G>::v;
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR, t = lane % LPR;
   const int nv = a.Kp / EPL;
@@ -207,12 +117,10 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
   const int wave = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   const int nwaves = gridDim.x * kWavesPerBlock;
   const bool want_reg = a.reg_partial != nullptr;
-  constexpr bool fused = FUSED;
   // (segment lookup + self rows: the key range of the own segments, read once)
   const bool self_key = self_on && a.seg_idx != nullptr && a.dense_A == nullptr;
   const int self_kmin = self_key ? a.self.keys[a.self.u0] : 0;
   const int self_kmax = self_key ? a.self.keys[a.self.u1 - 1] : -1;
-  const uint32_t sr = fused ? sr_step_seed(a.upd.sr_counter) : 0u;
 
   // dense rows: key -> dense index hash (built once per workgroup) and per-wave counters
   __shared__ int hkey[kDenseHash], hval[kDenseHash];
@@ -235,8 +143,50 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
   }
 
   float loss_acc = 0.f, regv_acc = 0.f, regw_acc = 0.f;
+  // Software pipeline over the wave's examples i, i + nwaves, ...: an example's chain is CSR
+  // offsets -> its (row, value) pairs -> its rows (and w); without the pipeline each example paid
+  // the three dependent latencies in turn (the forward ran latency-bound: 4 waves / SIMD, one
+  // example each).  Here the offsets are loaded two examples ahead and the first 64 (row, value)
+  // pairs one example ahead, so while example i's rows are in flight the next example's pairs
+  // are too, and example i starts with its pairs already in registers: one latency per example.
+  // (Longer examples load their further 64-wide pieces in place.)
+  constexpr bool kPrefetch = FM_FWD_PREFETCH;  // (A/B build variant "fwdnopf": 0)
+  auto pairs = [&](int base, int m, int& row, float& x) {
+    row = 0;
+    x = 0.f;
+    if (lane < m) {
+      row = a.rows[base + lane];
+      x = a.vals ? a.vals[base + lane] : 1.f;
+    }
+  };
+  int s = 0, e = 0, sn = 0, en = 0;
+  int p_row = 0;
+  float p_x = 0.f;
+  if (wave < a.B) {
+    s = a.offsets[wave];
+    e = a.offsets[wave + 1];
+    if (kPrefetch) pairs(s, min(kWave, e - s), p_row, p_x);
+  }
+  if (wave + nwaves < a.B) {
+    sn = a.offsets[wave + nwaves];
+    en = a.offsets[wave + nwaves + 1];
+  }
   for (int i = wave; i < a.B; i += nwaves) {
-    const int s = a.offsets[i], e = a.offsets[i + 1];
+    // next example's first pairs (its offsets arrived an example ago), the offsets after it
+    int n_row = 0;
+    float n_x = 0.f;
+    if (kPrefetch) pairs(sn, i + nwaves < a.B ? min(kWave, en - sn) : 0, n_row, n_x);
+    int snn = 0, enn = 0;
+    if (i + 2 * nwaves < a.B) {
+      snn = a.offsets[i + 2 * nwaves];
+      enn = a.offsets[i + 2 * nwaves + 1];
+    }
+    // label / weight of example i: needed after the reduction, loaded now
+    float y_pre = 0.f, wt_pre = 1.f;
+    if (kPrefetch && a.loss_type != kLossNone && lane == 0) {
+      y_pre = a.labels[i];
+      if (a.weights) wt_pre = a.weights[i];
+    }
     float s1[EPL], s2[EPL];
 #pragma unroll
     for (int k = 0; k < EPL; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
@@ -245,9 +195,14 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
       const int m = min(kWave, e - base);
       int my_row = 0, my_seg = 0;
       float my_x = 0.f, my_w = 0.f, my_s = 1.f;
+      if (kPrefetch && base == s) {
+        my_row = p_row;
+        my_x = p_x;
+      } else {
+        pairs(base, m, my_row, my_x);
+      }
       if (lane < m) {
-        my_seg = my_row = a.rows[base + lane];
-        my_x = a.vals ? a.vals[base + lane] : 1.f;
+        my_seg = my_row;
         // segment lookup mode: rows[] are keys; an own row is known by its key alone (the self
         // segments are exactly the batch's keys in [self_kmin, self_kmax]), so it needs neither
         // the lookup nor the segment's key load -- at world 1 every row (dense counting needs
@@ -270,15 +225,12 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
           my_s = row_scale<TV>(a.w, my_row, a.w_stride);
         }
       }
-      lin += my_x * my_w;
-      if (want_reg) rw += my_w * my_w;
       if (dense && lane < m) {
         const int h = dense_probe(hkey, hval, my_seg);
         if (h >= 0) atomicAdd(&dcnt[wv][h], 1u);  // integer: order-independent
       }
       for (int q = 0; q < m; q += G * UNR) {
-        float fr[kPacked ? 1 : UNR][EPL], fx[UNR], fs[UNR];
-        int raw[kPacked ? UNR : 1];
+        float fr[UNR][EPL], fx[UNR], fs[UNR];
         // Issue every row load of the round before the first use.  Loads are
         // unconditional (slots past the example re-read a valid row of it and are
         // masked to zero afterwards), so hipcc keeps all UNR loads in flight.
@@ -292,14 +244,12 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
           // (one load either way: the tagged index selects the base, not the instruction)
           const TV* rp = row < 0 ? tbase + (long long)(row & ~kSelfBit) * a.self.v_stride
                                  : vbase + (long long)row * a.v_stride;
-          if constexpr (kPacked) raw[u] = *reinterpret_cast<const int*>(rp);
-          else F::load(rp, fr[u]);
+          F::load(rp, fr[u]);
           if constexpr (F::kScaled) fs[u] = __shfl(my_s, src, kWave);
         }
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
-          float (&fv)[EPL] = fr[kPacked ? 0 : u];
-          if constexpr (kPacked) F::cvt(raw[u], fv);
+          float (&fv)[EPL] = fr[u];
           if constexpr (F::kScaled) {
 #pragma unroll
             for (int k = 0; k < EPL; ++k) fv[k] *= fs[u];
@@ -318,6 +268,9 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
           }
         }
       }
+      // (w is used after the row loads were issued: its load latency hides under theirs)
+      lin += my_x * my_w;
+      if (want_reg) rw += my_w * my_w;
     }
     if (dense) {  // flush this example's dense-row counts: 4 per lane, one coalesced row
       // (LDS instructions of one wave complete in issue order, and the compiler keeps these
@@ -350,9 +303,9 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
     }
     // loss and dL/dpred (every lane holds the same pred: butterfly sums are lane-symmetric)
     float l = 0.f, d = 0.f;
-    if (a.loss_type != kLossNone && (lane == 0 || fused)) {
-      const float y = a.labels[i];
-      const float wt = a.weights ? a.weights[i] : 1.f;
+    if (a.loss_type != kLossNone && lane == 0) {
+      const float y = kPrefetch ? y_pre : a.labels[i];
+      const float wt = kPrefetch ? wt_pre : (a.weights ? a.weights[i] : 1.f);
       if (a.loss_type == kLossMse) {
         const float diff = pred - y;
         l = wt * diff * diff;
@@ -370,7 +323,8 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
         if (a.dpred) a.dpred[i] = d * a.grad_scale;
       }
     }
-    if constexpr (fused) fwd_single_update<LPR, TV, EPL>(a, s, e, lane, g, t, tact, tE, d * a.grad_scale, s1, sr);
+    s = sn; e = en; sn = snn; en = enn;
+    p_row = n_row; p_x = n_x;
   }
   if (a.loss_partial == nullptr && a.reg_partial == nullptr) return;
   __shared__ float red[3][kWavesPerBlock];
@@ -391,14 +345,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
 template <int LPR, typename TV>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(fwd_min_waves<LPR, TV>())))
 void fm_fwd_kernel(FwdArgs a) {
-  fwd_body<LPR, TV, false>(a);
-}
-
-// (the 16-lane instantiations -- k=64 -- need 132-134 VGPRs uncapped: held at 4 waves / SIMD)
-template <int LPR, typename TV>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(LPR == 16 ? 4 : fwd_min_waves<LPR, TV>())))
-void fm_fwd_single_kernel(FwdArgs a) {
-  fwd_body<LPR, TV, true>(a);
+  fwd_body<LPR, TV>(a);
 }
 
 // Expand CSR offsets into the example index of every occurrence.
@@ -444,11 +391,7 @@ int fwd_grid(int B) { return fill_grid(B, kWavesPerBlock, 4096); }
 int launch_fwd(const FwdArgs& a, int dtype, int grid, hipStream_t st) {
   if (a.B <= 0) return 0;
   const int lpr = lanes_per_row(a.Kp, dtype);
-  if (a.single_flag) {
-    FM_DISPATCH(dtype, lpr, fm_fwd_single_kernel, grid, st, a);
-  } else {
-    FM_DISPATCH(dtype, lpr, fm_fwd_kernel, grid, st, a);
-  }
+  FM_DISPATCH(dtype, lpr, fm_fwd_kernel, grid, st, a);
   return (int)hipGetLastError();
 }
 

@@ -21,7 +21,7 @@ namespace py = pybind11;
 using u64 = std::uintptr_t;
 
 // Unity build: all kernel sources are compiled in this translation unit.
-#include "fm_bwd.hip"  // (first: the forward's fused singleton update uses its row update)
+#include "fm_bwd.hip"
 #include "fm_fwd.hip"
 #include "dedup.hip"
 #include "shard.hip"
@@ -85,43 +85,13 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       [](int B, u64 offsets, u64 rows, u64 vals, u64 v, long long v_stride, u64 w, long long w_stride, int Kp,
          int dtype, u64 labels, u64 weights, int loss_type, float grad_scale, u64 pred, u64 r1, u64 dpred,
          u64 loss_partial, u64 reg_partial, int grid, u64 stream, u64 bias, u64 dense_list, u64 dense_uniq,
-         u64 dense_count, u64 dense_A, const std::vector<long long>& self, const std::vector<long long>& single,
-         const std::vector<float>& single_f, u64 seg_idx, u64 seg_keys, int seg_shift) {
+         u64 dense_count, u64 dense_A, const std::vector<long long>& self, u64 seg_idx, u64 seg_keys,
+         int seg_shift) {
         fm::FwdArgs a{};
         a.seg_idx = P<const int>(seg_idx); a.seg_keys = P<const int>(seg_keys); a.seg_shift = seg_shift;
         if (a.seg_idx && (!a.seg_keys || seg_shift < 0 || seg_shift > 31))
           throw std::invalid_argument("fm_fwd: segment lookup needs the sorted keys and a shift in [0, 31]");
         a.self = self_rows(self);
-        if (!single.empty()) {
-          // fused singleton update: [single_flag, s0v, s1v, s_stride, s0w, s1w, opt_type, sr_counter, mode,
-          // uniq, grad_out, g_stride, g_wcol, g_bf16] and [reg_v, reg_w, lr, l1, l2, beta].  LOCAL: the
-          // forward's own table (v, w) + its optimizer state; EMIT: v, w are the gathered wire rows,
-          // gradient rows go to grad_out[segment], self rows (this rank's table) as in the backward
-          if (single.size() != 14 || single_f.size() != 6 || !single[0])
-            throw std::invalid_argument("fm_fwd: single = [flag, s0v, s1v, s_stride, s0w, s1w, opt, sr, mode, uniq, "
-                                        "grad_out, g_stride, g_wcol, g_bf16], 6 floats");
-          if (dense_A) throw std::runtime_error("fm_fwd: the singleton update excludes the dense-row counts");
-          const int mode = (int)single[8];
-          if (mode == fm::kBwdLocal ? (!single[1] || !single[4] || !self.empty())
-                                    : (mode != fm::kBwdEmit || !single[9] || !single[10] ||
-                                       (a.self.u1 > a.self.u0 && (!single[1] || !single[4]))))
-            throw std::runtime_error("fm_fwd: singleton update: LOCAL needs the optimizer state (no self rows), "
-                                     "EMIT needs uniq, grad_out and, with self rows, their optimizer state");
-          a.single_flag = P<const uint8_t>((u64)single[0]);
-          fm::BwdArgs& b = a.upd;
-          b.mode = mode;
-          b.self = a.self;
-          b.uniq = P<const int>((u64)single[9]);
-          b.grad_out = P<float>((u64)single[10]); b.g_stride = single[11]; b.g_wcol = (int)single[12];
-          b.g_bf16 = (int)single[13];
-          b.v = P<void>(v); b.v_stride = v_stride; b.w = P<float>(w); b.w_stride = w_stride; b.Kp = Kp;
-          b.s0v = P<float>((u64)single[1]); b.s1v = P<float>((u64)single[2]); b.s_stride = single[3];
-          b.s0w = P<float>((u64)single[4]); b.s1w = P<float>((u64)single[5]);
-          b.opt = opt_params((int)single[6], single_f[2], single_f[3], single_f[4], single_f[5]);
-          b.sr_counter = P<const int>((u64)single[7]);
-          b.reg_v = single_f[0]; b.reg_w = single_f[1];
-          if (!r1 || !dpred || loss_type == fm::kLossNone) throw std::runtime_error("fm_fwd: the singleton update needs the loss");
-        }
         a.dense_list = P<const int>(dense_list); a.dense_uniq = P<const int>(dense_uniq);
         a.dense_count = P<const int>(dense_count); a.dense_A = P<uint8_t>(dense_A);
         if (a.dense_A && (!a.dense_list || !a.dense_count)) throw std::runtime_error("fm_fwd: dense_A needs the dense list");
@@ -139,8 +109,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("loss_type"), py::arg("grad_scale"), py::arg("pred"), py::arg("r1"), py::arg("dpred"),
       py::arg("loss_partial"), py::arg("reg_partial"), py::arg("grid"), py::arg("stream"), py::arg("bias") = 0,
       py::arg("dense_list") = 0, py::arg("dense_uniq") = 0, py::arg("dense_count") = 0, py::arg("dense_A") = 0,
-      py::arg("self_rows") = std::vector<long long>{}, py::arg("single") = std::vector<long long>{},
-      py::arg("single_f") = std::vector<float>{}, py::arg("seg_idx") = 0, py::arg("seg_keys") = 0,
+      py::arg("self_rows") = std::vector<long long>{}, py::arg("seg_idx") = 0, py::arg("seg_keys") = 0,
       py::arg("seg_shift") = 0);
 
   m.def(
@@ -159,24 +128,19 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
          u64 sorted_ex, int ex_shift, u64 sorted_x, u64 dpred, u64 r1, int Kp, u64 v, long long v_stride, u64 w,
          long long w_stride, u64 s0v, u64 s1v, long long s_stride, u64 s0w, u64 s1w, float reg_v, float reg_w,
          int opt_type, float lr, float l1, float l2, float beta, u64 grad_out, long long g_stride, u64 partial,
-         u64 big_list, u64 big_count, u64 multi, u64 slice_list, u64 slice_start, int nslices, u64 dense_list,
+         u64 big_list, u64 big_count, u64 multi, u64 dense_list,
          u64 dense_part, int nex, u64 dense_stream, int dtype,
          long long max_chunks, long long max_unique, u64 stream, int g_wcol, int g_bf16, u64 sr_counter,
-         int counters_ready, u64 seg_bounds, int piece, int n_owners, u64 dense_A, int cold_split,
-         const std::vector<long long>& self, int fwd_single, int chunk_pipe, int chunk_grid, int combine_grid,
-         int big_grid) {
+         int counters_ready, u64 seg_bounds, int piece, int n_owners, u64 dense_A,
+         const std::vector<long long>& self, int chunk_grid) {
         fm::BwdArgs a{};
-        a.chunk_grid = chunk_grid; a.combine_grid = combine_grid; a.big_grid = big_grid;
-        a.fwd_single = fwd_single;
-        a.chunk_pipe = chunk_pipe;
-        if (fwd_single && mode == fm::kBwdEmitTable) throw std::runtime_error("fm_bwd: fwd_single: LOCAL / EMIT modes");
+        a.chunk_grid = chunk_grid;
         a.self = self_rows(self);
         if (a.self.u1 > a.self.u0 && a.self.keys != P<const int>(uniq))
           throw std::runtime_error("fm_bwd: self-row keys must be the dedup's unique keys");
         if (a.self.u1 > a.self.u0 && (mode != 1 || !s0v || !s0w))
           throw std::runtime_error("fm_bwd: self rows are an EMIT-mode path and need the table's optimizer state");
         a.dense_A = P<const uint8_t>(dense_A);
-        a.cold_split = cold_split;
         a.counters_ready = counters_ready;
         a.seg_bounds = P<const int>(seg_bounds); a.piece = piece; a.n_owners = n_owners;
         a.sr_counter = P<const int>(sr_counter);
@@ -193,8 +157,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
         a.grad_out = P<float>(grad_out); a.g_stride = g_stride; a.g_wcol = g_wcol < 0 ? Kp : g_wcol;
         a.g_bf16 = g_bf16; a.partial = P<float>(partial);
         a.big_list = P<int>(big_list); a.big_count = P<int>(big_count); a.multi = P<int>(multi);
-        a.counts_rw = P<int>(counts); a.slice_list = P<const int>(slice_list);
-        a.slice_start = P<const int>(slice_start); a.nslices = nslices;
+        a.counts_rw = P<int>(counts);
         a.dense_list = P<const int>(dense_list); a.dense_part = P<float>(dense_part); a.nex = nex;
         check(fm::launch_bwd(a, dtype, max_chunks, max_unique, S(stream), S(dense_stream)), "fm_bwd");
       },
@@ -205,13 +168,12 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("s0v"), py::arg("s1v"), py::arg("s_stride"), py::arg("s0w"), py::arg("s1w"), py::arg("reg_v"),
       py::arg("reg_w"), py::arg("opt_type"), py::arg("lr"), py::arg("l1"), py::arg("l2"), py::arg("beta"),
       py::arg("grad_out"), py::arg("g_stride"), py::arg("partial"), py::arg("big_list"), py::arg("big_count"),
-      py::arg("multi"), py::arg("slice_list"), py::arg("slice_start"), py::arg("nslices"), py::arg("dense_list"),
+      py::arg("multi"), py::arg("dense_list"),
       py::arg("dense_part"), py::arg("nex"), py::arg("dense_stream"), py::arg("dtype"),
       py::arg("max_chunks"), py::arg("max_unique"), py::arg("stream"), py::arg("g_wcol") = -1,
       py::arg("g_bf16") = 0, py::arg("sr_counter") = 0, py::arg("counters_ready") = 0, py::arg("seg_bounds") = 0,
-      py::arg("piece") = -1, py::arg("n_owners") = 0, py::arg("dense_A") = 0, py::arg("cold_split") = 0,
-      py::arg("self_rows") = std::vector<long long>{}, py::arg("fwd_single") = 0, py::arg("chunk_pipe") = 0,
-      py::arg("chunk_grid") = 0, py::arg("combine_grid") = 0, py::arg("big_grid") = 0);
+      py::arg("piece") = -1, py::arg("n_owners") = 0, py::arg("dense_A") = 0,
+      py::arg("self_rows") = std::vector<long long>{}, py::arg("chunk_grid") = 0);
 
   m.def("dedup_workspace_bytes", &fm::dedup_workspace_bytes, py::arg("n"));
 
@@ -219,8 +181,8 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       "dedup",
       [](int n, int end_bit, int CH, u64 keys, u64 payload, u64 skeys, u64 spay, u64 uniq, u64 seg_start,
          u64 seg_chunk, u64 chunk_start, u64 chunk_seg, u64 chunk_key, u64 counts, u64 inv, u64 ex_of_occ,
-         u64 sorted_ex, u64 vals, u64 sorted_x, int payload_is_ex, int ex_shift, u64 offsets, int dense_min, u64 dense_list, int slice_shift, int nslices, u64 slice_list,
-         u64 slice_start, u64 ws, size_t ws_bytes, u64 stream, u64 single_flag) {
+         u64 sorted_ex, u64 vals, u64 sorted_x, int payload_is_ex, int ex_shift, u64 offsets, int dense_min,
+         u64 dense_list, u64 ws, size_t ws_bytes, u64 stream) {
         if (CH < 1 || CH > fm::kMaxCH) throw std::invalid_argument("CH must be in [1, MAX_CH]");
         fm::DedupArgs a;
         a.n = n; a.end_bit = end_bit; a.CH = CH; a.keys = P<const uint32_t>(keys);
@@ -231,22 +193,16 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
         a.inv = P<int>(inv); a.ex_of_occ = P<const int>(ex_of_occ); a.sorted_ex = P<int>(sorted_ex);
         a.vals = P<const float>(vals); a.sorted_x = P<float>(sorted_x); a.ws = P<void>(ws);
         a.payload_is_ex = payload_is_ex; a.ex_shift = ex_shift; a.offsets = P<const int>(offsets);
-        a.slice_shift = slice_shift; a.nslices = nslices;
         a.dense_min = dense_min; a.dense_list = P<int>(dense_list);
-        a.slice_list = P<int>(slice_list); a.slice_start = P<int>(slice_start);
         a.ws_bytes = ws_bytes;
-        a.single_flag = P<uint8_t>(single_flag);
         check(fm::launch_dedup(a, S(stream)), "dedup");
       },
       py::arg("n"), py::arg("end_bit"), py::arg("CH"), py::arg("keys"), py::arg("payload"), py::arg("skeys"),
       py::arg("spay"), py::arg("uniq"), py::arg("seg_start"), py::arg("seg_chunk"), py::arg("chunk_start"),
       py::arg("chunk_seg"), py::arg("chunk_key"), py::arg("counts"), py::arg("inv"), py::arg("ex_of_occ"),
       py::arg("sorted_ex"),
-      py::arg("vals"), py::arg("sorted_x"), py::arg("payload_is_ex"), py::arg("ex_shift"), py::arg("offsets"), py::arg("dense_min"), py::arg("dense_list"),
-      py::arg("slice_shift"), py::arg("nslices"),
-      py::arg("slice_list"), py::arg("slice_start"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"),
-      py::arg("single_flag") = 0);
-  m.attr("MAX_SLICES") = fm::kMaxSlices;
+      py::arg("vals"), py::arg("sorted_x"), py::arg("payload_is_ex"), py::arg("ex_shift"), py::arg("offsets"),
+      py::arg("dense_min"), py::arg("dense_list"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"));
   m.attr("MAX_DENSE") = fm::kMaxDense;
   m.attr("DENSE_WG") = fm::kDenseWG;
 
@@ -369,6 +325,15 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
               "owner_counts");
       },
       py::arg("uniq"), py::arg("num_unique"), py::arg("Rps"), py::arg("W"), py::arg("out"), py::arg("stream"));
+
+  m.def(
+      "zero_listed_rows",
+      [](u64 buf, long long row_words, u64 list, u64 count, int max_n, u64 stream) {
+        check(fm::launch_zero_listed_rows(P<float>(buf), row_words, P<const int>(list), P<const int>(count), max_n,
+                                          S(stream)),
+              "zero_listed_rows");
+      },
+      py::arg("buf"), py::arg("row_words"), py::arg("list"), py::arg("count"), py::arg("max_n"), py::arg("stream"));
 
   m.def(
       "shard_keys",

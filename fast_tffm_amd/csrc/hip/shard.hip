@@ -628,4 +628,28 @@ int launch_owner_counts(const uint32_t* uniq, const int* num_unique, long long R
   return (int)hipGetLastError();
 }
 
+// Zero the rows buf[list[i]] for i < *count (device count, capped at max_n): the data-parallel
+// dense step's gradient buffer keeps this rank's scattered rows of the slices other ranks own
+// after its in-place reduce-scatter; they are cleared here instead of the whole buffer.  One
+// wave per row, 16 bytes per lane (row_words a multiple of 4).
+__global__ __launch_bounds__(kBlock) void zero_listed_rows_kernel(float* buf, long long row_words, const int* list,
+                                                                 const int* count, int max_n) {
+  const int n = min(*count, max_n);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int nq = (int)(row_words / 4);
+  for (int i = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); i < n; i += gridDim.x * kWavesPerBlock) {
+    float4* r = reinterpret_cast<float4*>(buf + (long long)list[i] * row_words);
+    for (int q = lane; q < nq; q += kWave) r[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+int launch_zero_listed_rows(float* buf, long long row_words, const int* list, const int* count, int max_n,
+                            hipStream_t st) {
+  if (max_n <= 0) return 0;
+  if (row_words % 4 != 0) return -1;
+  hipLaunchKernelGGL(zero_listed_rows_kernel, dim3(fill_grid(max_n, kWavesPerBlock, 4096)), dim3(kBlock), 0, st, buf,
+                     row_words, list, count, max_n);
+  return (int)hipGetLastError();
+}
+
 }  // namespace fm

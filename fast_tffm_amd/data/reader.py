@@ -380,8 +380,13 @@ class NativeTextReader:
                 hb, hl = self._stage(buf, line_start)
             db = hb.to(dev, non_blocking=True)
             dl = hl.to(dev, non_blocking=True)
+            # the weights' copy is queued BEFORE the tokenizer launch: parse_gpu_start records the
+            # event that _gpu_finish waits on, so the event covers this copy too (a copy queued
+            # after it could still be in flight when the compute stream reads b.weights).  The
+            # source is page-locked (the caching host allocator keeps it alive until the copy ran)
+            w = (None if weights is None
+                 else torch.from_numpy(np.ascontiguousarray(weights)).pin_memory().to(dev, non_blocking=True))
             pp = K.parse_gpu_start(db, dl, self.args["vocab_size"], self.args["hash_feature_id"], stream=stream)
-            w = None if weights is None else torch.from_numpy(weights).to(dev, non_blocking=True)
         return pp, buf, w, int(epoch), int(count), slot
 
     def _gpu_finish(self, launched) -> Batch:

@@ -281,9 +281,11 @@ class FactorizationMachine:
             raise ValueError("mode=local needs world_size == 1")
         self.mode = mode
         sharded = mode == "shard"
+        # (dp_dense: the replica is cut into W equal row slices, one updated per rank)
         self.table = FMTable(cfg.vocabulary_size, cfg.factor_num, world=self.world if sharded else 1,
                              rank=self.rank if sharded else 0, dtype=cfg.dtype, opt=cfg.opt,
-                             init_range=cfg.init_value_range, seed=cfg.seed, device=self.device)
+                             init_range=cfg.init_value_range, seed=cfg.seed, device=self.device,
+                             rows_multiple=self.world if mode == "dp_dense" else 1)
         self.K, self.Kp = self.table.K, self.table.Kp
         self.rps = rows_per_shard(cfg.vocabulary_size, self.world) if sharded else cfg.vocabulary_size
         self.ws = _Workspace(self.device, self.Kp, cfg.dedup_chunk, K.r1_dtype(cfg.dtype))
@@ -559,49 +561,31 @@ class FactorizationMachine:
         cfg = self.cfg
         slot.ensure(b.nnz, self.device, cfg.dedup_chunk)
         rows = b.ids if b.ids.dtype == torch.int32 else slot.rows32[: b.nnz].copy_(b.ids)
-        single = self._fwd_single_ok()
-        # (the singleton flags are scattered by occurrence: the sort carries packed codes)
-        sb = self._slot_bits(b, always=single)
+        sb = self._slot_bits(b)
         ex = K.csr_rows(b.offsets, out=slot.dd.ex_of_occ[: b.nnz], nnz=b.nnz, slot_bits=sb)
         dd = K.dedup(rows, ws=slot.dd, key_bits=bits_for(self.table.rows), ex_of_occ=ex, vals=b.vals,
                      num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets,
                      dense_min=K.dense_min_for(b.B, self.Kp, cfg.dedup_chunk, table_dtype=self.table.v.dtype,
                                                has_vals=b.vals is not None,
-                                               max_feats=b.max_feats),
-                     want_single=single and sb > 0)
+                                               max_feats=b.max_feats))
         return rows, dd
-
-    def _fwd_single_ok(self) -> bool:
-        """Fused singleton update for this model's local GPU step (ops.kernels.fwd_single_enabled)."""
-        return (self.device.type == "cuda" and K.fwd_single_enabled() and self.cfg.opt.name in ("adagrad", "ftrl")
-                and self.table.state.s0v is not None and self.cfg.loss_type in ("logistic", "mse"))
 
     def _fwd_bwd_local(self, b: Batch, rows: torch.Tensor, dd) -> StepOut:
         """Forward + loss + backward/update of ``b`` on the current stream (dedup ``dd`` ready)."""
         ws, cfg = self.ws, self.cfg
         dA = ws.dense_counts(b.B) if dd.dense_list is not None else None
         rv, rw = self.reg_coeffs
-        # fused singleton update (opt-in FM_FWD_SINGLE=1, measured slower: ops.kernels.
-        # fwd_single_enabled): rows occurring once in the batch (~73% of a Criteo-shaped
-        # batch's unique rows) get their optimizer step in the forward, which holds their whole
-        # gradient's inputs (r1_i, dpred_i) in registers; the backward skips them.  The
-        # stochastic-rounding counter is advanced before the forward so both kernels use this
-        # step's value.
-        single = None
-        if dd.single_flag is not None and dA is None:
-            single = K.SingleUpdate(dd.single_flag, self.table.state, cfg.opt, rv, rw, self.sr_tick())
         with roctx_range("fwd"):
             fo = K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,
                               weights=b.weights, loss=cfg.loss_type, grad_scale=self.grad_scale(b.B), want_r1=True,
                               pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
-                              threads=cfg.threads, bias=self.gbias, dense=dd, dense_A=dA, single=single)
+                              threads=cfg.threads, bias=self.gbias, dense=dd, dense_A=dA)
             self.bias_step(fo.dpred)
         with roctx_range("bwd+update"):
             K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
                           reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, dense_part=ws.dense_part,
                           dense_stream=self._dense_stream(),
-                          sr_counter=single.sr_counter if single is not None else self.sr_tick(), dense_A=dA,
-                          fwd_single=single is not None)
+                          sr_counter=self.sr_tick(), dense_A=dA)
         return StepOut(fo.loss_sum, b.B)
 
     def _local_lookahead_step(self, b: Batch, next_batch: Batch | None, next2: Batch | None = None) -> StepOut:

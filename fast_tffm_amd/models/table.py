@@ -42,7 +42,7 @@ def shard_rows(vocab_size: int, world: int, rank: int) -> int:
 class FMTable:
     def __init__(self, vocab_size: int, factor_num: int, *, world: int = 1, rank: int = 0,
                  dtype: torch.dtype = torch.float32, opt: K.OptConfig | None = None, init_range: float = 0.01,
-                 seed: int = 0, device: torch.device | str = "cpu", init: bool = True):
+                 seed: int = 0, device: torch.device | str = "cpu", init: bool = True, rows_multiple: int = 1):
         self.vocab_size = int(vocab_size)
         self.K = int(factor_num)
         self.world, self.rank = int(world), int(rank)
@@ -50,7 +50,12 @@ class FMTable:
         self.Kp = K.padded_k(self.K, dtype)
         self.opt = opt or K.OptConfig()
         self.device = torch.device(device)
-        self.rows = max(1, shard_rows(self.vocab_size, self.world, self.rank))
+        # allocated rows: the shard's ids, rounded up to ``rows_multiple`` (the replicated table of
+        # the dense data-parallel step is cut into equal row slices, one per rank: dead rows at the
+        # end are zero and never addressed)
+        m = max(1, int(rows_multiple))
+        self.real_rows = shard_rows(self.vocab_size, self.world, self.rank)
+        self.rows = max(1, -(-self.real_rows // m) * m)
         self.init_range = float(init_range)
         self.seed = int(seed)
         dev = self.device
@@ -80,6 +85,12 @@ class FMTable:
 
     # ------------------------------------------------------------------
     @property
+    def saved_rows(self) -> int:
+        """Rows a checkpoint / reference view covers: the allocated rows without the dead padding
+        of ``rows_multiple`` (an empty shard keeps its one allocated row)."""
+        return max(1, min(self.rows, self.real_rows))
+
+    @property
     def state(self) -> K.TableState:
         return K.TableState(self.v, self.w, self.s0v, self.s1v, self.s0w, self.s1w)
 
@@ -96,8 +107,8 @@ class FMTable:
         self._zero_dead_rows()
 
     def _zero_dead_rows(self) -> None:
-        # the last shard may own fewer real ids than allocated rows (rows >= 1)
-        real = shard_rows(self.vocab_size, self.world, self.rank)
+        # the last shard may own fewer real ids than allocated rows (rows >= 1, rows_multiple)
+        real = self.real_rows
         if real < self.rows:
             self.v[real:].zero_()
             self.w[real:].zero_()
@@ -118,7 +129,8 @@ class FMTable:
     def reference_rows(self, local_rows: torch.Tensor | None = None) -> torch.Tensor:
         """Rows in the reference layout [n, K+1] (col 0 = w, cols 1..K = v), fp32."""
         if local_rows is None:
-            v, w = self.dense_v(), self.w
+            n = self.saved_rows
+            v, w = self.dense_v(slice(0, n)), self.w[:n]
         else:
             v, w = self.dense_v(local_rows), self.w[local_rows]
         return torch.cat([w.unsqueeze(1), v[:, : self.K].float()], dim=1)

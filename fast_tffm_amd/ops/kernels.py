@@ -163,8 +163,7 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
                partial: torch.Tensor | None = None, threads: int = 0,
                bias: torch.Tensor | None = None, dense: "DedupOut | None" = None,
                dense_A: torch.Tensor | None = None, dense_by_segment: bool = False,
-               self_rows: SelfRows | None = None, single: "SingleUpdate | None" = None,
-               seg_lookup: "SegIndex | None" = None) -> FwdOut:
+               self_rows: SelfRows | None = None, seg_lookup: "SegIndex | None" = None) -> FwdOut:
     """FM score of a CSR batch (reference FmScorer, cc/fm_scorer_op.h:101-140), fused with the loss.
 
     pred_i = sum_j x_j w_j + 1/2 sum_k [(sum_j x_j v_jk)^2 - sum_j x_j^2 v_jk^2]  (+ bias[0], optional
@@ -177,9 +176,6 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
     MFMA backward; ``rows`` are table rows (``dense.uniq`` maps segments to them) or, with
     ``dense_by_segment``, the segment ids themselves (the sharded step's inverse map).
     ``self_rows`` (GPU, ``rows`` = segment ids): segments in its range read this rank's table.
-    ``single`` (GPU, training loss, ``rows`` = table rows of ``v``): fused singleton update --
-    the rows the batch's dedup flagged as occurring once get their optimizer step here
-    (``fm_backward(..., fwd_single=True)`` then skips them).
     ``seg_lookup`` (GPU): ``rows`` are the dedup's keys and every occurrence's segment (its
     row of ``v``) is found through the bucket index (``seg_index``) instead of an inverse map.
     """
@@ -219,9 +215,6 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
     if _is_gpu(rows):
         h = native.hip()
         grid = h.fwd_grid(max(B, 1))
-        fg = int(os.environ.get("FM_FWD_GRID", "0"))  # A/B knob: workgroup cap of the forward
-        if fg > 0:
-            grid = max(1, min(grid, fg))
         if partial is None or partial.numel() < 3 * grid:
             partial = torch.zeros(3 * grid, dtype=torch.float32, device=dev)
         lp = partial[:grid]
@@ -236,32 +229,6 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
         if self_rows is not None and self_rows.u1 > self_rows.u0:
             _self_check(self_rows, v, None)
             dkw["self_rows"] = self_rows.packed()
-        if single is not None:
-            t, o = single.table, single.opt
-            _check(lt != 0 and want_r1 and "dense_A" not in dkw,
-                   "fused singleton update: training loss, r1, no dense rows")
-            _check(single.flag is not None and single.flag.numel() >= nnz, "fused singleton update: dedup flags")
-            if single.mode == BWD_LOCAL:
-                _check("self_rows" not in dkw and t is not None and t.v.data_ptr() == v.data_ptr()
-                       and t.w.data_ptr() == w.data_ptr() and t.s0v is not None and t.s0w is not None
-                       and o.name in ("adagrad", "ftrl"),
-                       "fused singleton update (LOCAL): the forward's own table with Adagrad / FTRL state")
-                gptr, gstride, gwcol = 0, 0, Kp
-            else:
-                _check(single.mode == BWD_EMIT and single.uniq is not None and single.grad_out is not None
-                       and single.grad_out.dtype == torch.float32 and single.grad_out.stride(1) == 1,
-                       "fused singleton update (EMIT): uniq + fp32 gradient rows")
-                _check(("self_rows" not in dkw) or (t is not None and t.s0v is not None and t.s0w is not None),
-                       "fused singleton update (EMIT): self rows need their optimizer state")
-                gptr, gstride = _p(single.grad_out), single.grad_out.stride(0)
-                gwcol = (Kp * 2 + 15) // 16 * 4 if single.grad_bf16 else Kp
-            s0v = t.s0v if t is not None else None
-            sst = s0v.stride(0) if s0v is not None else 0
-            dkw["single"] = [_p(single.flag), _p(s0v), _p(t.s1v if t else None), sst,
-                             _p(t.s0w if t else None), _p(t.s1w if t else None), o.code, _p(single.sr_counter),
-                             int(single.mode), _p(single.uniq), gptr, gstride, gwcol, int(bool(single.grad_bf16))]
-            dkw["single_f"] = [float(single.reg_v), float(single.reg_w), float(o.lr), float(o.l1), float(o.l2),
-                               float(o.beta)]
         h.fwd(B=B, offsets=_p(offsets), rows=_p(rows), vals=_p(vals), v=_p(v), v_stride=v_stride, w=_p(w),
               w_stride=w_stride, Kp=Kp, dtype=dt, labels=_p(labels), weights=_p(weights), loss_type=lt,
               grad_scale=float(grad_scale), pred=_p(pred), r1=_p(r1), dpred=_p(dpred) if lt else 0,
@@ -302,8 +269,7 @@ class DedupOut:
 
     __slots__ = ("n", "skeys", "perm", "uniq", "seg_start", "seg_chunk", "chunk_start", "chunk_seg", "chunk_key",
                  "counts", "num_unique", "inv", "sorted_ex", "sorted_x", "U_host", "CH", "big_list", "big_count",
-                 "multi",
-                 "slice_list", "slice_start", "nslices", "ex_shift", "dense_list", "bwd_fresh", "single_flag")
+                 "multi", "ex_shift", "dense_list", "bwd_fresh")
 
     def __init__(self, **kw):
         for k in self.__slots__:
@@ -342,10 +308,7 @@ class DedupWorkspace:
         self.ex_of_occ = torch.empty(n1, **i32)
         self.big_list = torch.empty(n1, **i32)
         self.big_count = self.counts[4:5]     # zeroed with the counts by every GPU dedup
-        self.slice_list = torch.empty(n1, **i32)
-        self.slice_start = torch.empty(MAX_SLICES + 1, **i32)
         self.dense_list = torch.empty(MAX_DENSE, **i32)
-        self.single_flag = torch.empty(n1, dtype=torch.uint8, device=device) if device.type == "cuda" else None
         if device.type == "cuda":
             nbytes = native.hip().dedup_workspace_bytes(n1)
             self.ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
@@ -382,7 +345,6 @@ def csr_rows(offsets: torch.Tensor, out: torch.Tensor | None = None, nnz: int | 
     return out
 
 
-MAX_SLICES = 64            # = fm::kMaxSlices (dedup.hip)
 MAX_DENSE = 256            # = fm::kMaxDense: rows on the MFMA backward path
 DENSE_WG = 256             # = fm::kDenseWG: workgroups (partial rows) of the dense kernel
 
@@ -402,45 +364,19 @@ def dense_min_for(num_examples: int, Kp: int, CH: int = 32, *, has_vals: bool = 
             or max_feats > 255 or r1_dtype(table_dtype) != torch.float32):
         return 0
     return max(8 * CH, num_examples // 40)
-SLICE_BYTES = 2 << 20      # r1 bytes per example slice of the XCD-sliced backward (XCD L2 = 4 MB)
-
-
-def slice_plan(num_examples: int, Kp: int) -> tuple[int, int]:
-    """(slice_shift, nslices) of the XCD-sliced backward schedule, or (-1, 0) when not worth it.
-
-    Example slice = ex >> slice_shift.  The backward's chunks are listed per
-    slice and workgroup b walks the lists of slices b%8, b%8+8, ...: the r1
-    rows (Kp fp32 per example) a slice's chunks gather stay in one XCD's L2.
-    """
-    row = Kp * 4
-    # measured on MI355X (B=131072, K=64, profiles/README.md): sliced 0.782 ms/step vs
-    # linear 0.726 -- the L2 hit rate of the chunk kernel rises 34% -> 48% but the list
-    # indirection and the extra hot-row chunks cost more; opt-in via FM_BWD_SLICES=1
-    if os.environ.get("FM_BWD_SLICES", "0") != "1" or num_examples * row <= 8 * SLICE_BYTES:
-        return -1, 0
-    shift = max(0, (SLICE_BYTES // row).bit_length() - 1)
-    while shift > 0 and -(-num_examples >> shift) < 8:
-        shift -= 1
-    while -(-num_examples >> shift) > MAX_SLICES:
-        shift += 1
-    return shift, -(-num_examples >> shift)
-
-
 def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int = 32,
           ex_of_occ: torch.Tensor | None = None, vals: torch.Tensor | None = None, want_inv: bool = False,
           CH: int | None = None, want_perm: bool = False, num_examples: int | None = None,
           Kp: int | None = None, ex_shift: int = 0, offsets: torch.Tensor | None = None,
-          dense_min: int = 0, want_single: bool = False) -> DedupOut:
+          dense_min: int = 0) -> DedupOut:
     """Sort-based unique over non-negative int32 keys (reference tf.unique, fm_model.py:72).
 
     Unique keys come out in ascending order (the reference's first-occurrence
     order is an implementation detail no result depends on).  On the GPU the
-    result also carries the backward's chunk plan (per example slice when
-    ``num_examples`` and ``Kp`` are given, see ``slice_plan``).  When neither the inverse
+    result also carries the backward's chunk plan.  When neither the inverse
     map, per-occurrence values nor the occurrence permutation are needed, the
     sort carries the example index directly (one gather pass less).
-    ``want_single`` (GPU, with ``ex_of_occ``): also flag, per occurrence, the keys that occur
-    exactly once (``single_flag``, uint8 [n]) for the forward's fused singleton update.
+    (``num_examples`` / ``Kp`` are accepted for interface stability; the plan does not use them.)
     """
     dev = keys.device
     n = keys.numel()
@@ -459,20 +395,14 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
                "packed occurrence codes need the GPU, codes and offsets")
     ex_payload = ex_of_occ is not None and _is_gpu(keys) and not want_perm and (
         packed or (vals is None and not want_inv))
-    shift, nsl = -1, 0
-    if ex_of_occ is not None and num_examples and Kp and _is_gpu(keys):
-        shift, nsl = slice_plan(int(num_examples), int(Kp))
     out = DedupOut(n=n, skeys=ws.skeys, perm=ws.perm, uniq=ws.uniq, seg_start=ws.seg_start,
                    seg_chunk=ws.seg_chunk, chunk_start=ws.chunk_start, chunk_seg=ws.chunk_seg,
                    chunk_key=ws.chunk_key, counts=ws.counts,
                    num_unique=ws.counts[:1], inv=ws.inv if want_inv else None,
                    sorted_ex=(ws.perm if ex_payload else ws.sorted_ex) if ex_of_occ is not None else None,
                    sorted_x=ws.sorted_x if vals is not None else None, CH=CH, big_list=ws.big_list,
-                   big_count=ws.big_count, multi=ws.multi, slice_list=ws.slice_list if nsl else None,
-                   slice_start=ws.slice_start, nslices=nsl, ex_shift=int(ex_shift),
-                   dense_list=ws.dense_list if dense_min > 0 and ex_of_occ is not None and _is_gpu(keys) else None,
-                   single_flag=ws.single_flag if want_single and ex_of_occ is not None and _is_gpu(keys)
-                   and (packed or not ex_payload) else None)
+                   big_count=ws.big_count, multi=ws.multi, ex_shift=int(ex_shift),
+                   dense_list=ws.dense_list if dense_min > 0 and ex_of_occ is not None and _is_gpu(keys) else None)
     if _is_gpu(keys):
         h = native.hip()
         _check(1 <= CH <= h.MAX_CH, f"CH must be in [1, {h.MAX_CH}]")
@@ -485,9 +415,7 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
                 sorted_ex=0 if ex_payload else _p(out.sorted_ex), vals=_p(vals), sorted_x=_p(out.sorted_x),
                 payload_is_ex=int(ex_payload), ex_shift=int(ex_shift), offsets=_p(offsets),
                 dense_min=int(dense_min) if out.dense_list is not None else 0, dense_list=_p(out.dense_list),
-                slice_shift=shift, nslices=nsl,
-                slice_list=_p(out.slice_list), slice_start=_p(ws.slice_start), ws=_p(ws.ws),
-                ws_bytes=ws.ws.numel(), stream=_stream(keys), single_flag=_p(out.single_flag))
+                ws=_p(ws.ws), ws_bytes=ws.ws.numel(), stream=_stream(keys))
         out.bwd_fresh = True  # the backward counters were zeroed on this stream
     else:
         U = native.cpu().dedup(n=n, keys=_p(keys), skeys=_p(ws.skeys), perm=_p(ws.perm), uniq=_p(ws.uniq),
@@ -545,24 +473,6 @@ def _self_check(sr: SelfRows, v: torch.Tensor, keys: torch.Tensor | None) -> Non
 
 
 @dataclass
-class SingleUpdate:
-    """Fused singleton update of the forward (``fm_forward(single=...)``): the dedup's
-    one-occurrence flags and the backward's arguments for those rows (LOCAL: table, optimizer,
-    regularisation; EMIT: also the gradient rows and, for self rows, their table)."""
-
-    flag: torch.Tensor
-    table: TableState | None      # LOCAL: the forward's table; EMIT: the self rows' table (or None)
-    opt: OptConfig
-    reg_v: float
-    reg_w: float
-    sr_counter: torch.Tensor | None = None
-    mode: int = 0                 # BWD_LOCAL / BWD_EMIT (row-sharded step: rows = segment ids)
-    uniq: torch.Tensor | None = None       # EMIT: the dedup's unique keys
-    grad_out: torch.Tensor | None = None   # EMIT: gradient rows [U, g_stride]
-    grad_bf16: bool = False
-
-
-@dataclass
 class SegIndex:
     """Bucket index over a dedup's sorted unique keys (``seg_index``): key -> segment."""
 
@@ -597,17 +507,6 @@ def seg_index(dd: DedupOut, key_bits: int, out: torch.Tensor | None = None) -> S
     return SegIndex(out, dd.uniq, shift)
 
 
-def fwd_single_enabled() -> bool:
-    """Fused singleton update in the local / row-sharded GPU step (opt-in, FM_FWD_SINGLE=1).
-
-    Exact (bitwise equal to the unfused step) but measured slower on every preset
-    (profiles/r2/fwd_single_ab.txt: k64 fp32 0.674 -> 0.750 ms, sharded W=1 0.78 -> 0.89 ms):
-    the chunk backward sheds ~50 us of r1 gathers and descriptor chains, but the forward
-    gains ~115 us -- each wave's singleton read-modify-writes come after its example's
-    reduction, a dependent chain the forward's occupancy does not hide."""
-    return os.environ.get("FM_FWD_SINGLE", "0") != "0"
-
-
 def partial_rows(n: int, CH: int) -> int:
     """Upper bound on backward chunks (= partial rows) for n occurrences: U + n / CH."""
     return max(n, 1) + max(n, 1) // max(CH, 1) + 1
@@ -621,8 +520,7 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
                 dense_part: torch.Tensor | None = None, dense_stream=None,
                 grad_bf16: bool = False, sr_counter: torch.Tensor | None = None,
                 seg_bounds: torch.Tensor | None = None, piece: int = -1,
-                dense_A: torch.Tensor | None = None, self_rows: SelfRows | None = None,
-                fwd_single: bool = False) -> torch.Tensor | None:
+                dense_A: torch.Tensor | None = None, self_rows: SelfRows | None = None) -> torch.Tensor | None:
     """Segmented FM backward over the dedup grouping (reference FmGrad, cc/fm_grad_op.h:59-163).
 
     Per unique row u with occurrences (i, x):
@@ -635,8 +533,6 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
     second part (split backward of the row-sharded exchange); piece 1 must follow piece 0.
     ``self_rows`` (GPU, EMIT): segments in its range are read from its table; the exclusive ones
     get ``opt`` applied in place (with ``sr_counter``) and no gradient row.
-    ``fwd_single`` (GPU, LOCAL): the forward already updated the one-occurrence rows flagged in
-    ``dd.single_flag`` (``fm_forward(single=...)``, same ``sr_counter``); they are skipped.
     """
     dev = dpred.device
     _check(dd.sorted_ex is not None, "dedup must be run with ex_of_occ")
@@ -688,8 +584,8 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
     _check(r1.dtype == torch.float32 or dd.dense_list is None, "the dense-row MFMA backward reads an fp32 r1")
     o = opt or OptConfig()
     if piece >= 0:
-        _check(_is_gpu(dpred) and seg_bounds is not None and mode == BWD_EMIT and dd.slice_list is None
-               and dd.dense_list is None, "split backward pieces: GPU, EMIT mode, seg_bounds, no sliced / dense path")
+        _check(_is_gpu(dpred) and seg_bounds is not None and mode == BWD_EMIT and dd.dense_list is None,
+               "split backward pieces: GPU, EMIT mode, seg_bounds, no dense path")
         _chk_vec(seg_bounds, torch.int32, 3, "seg_bounds", dev)
     if _is_gpu(dpred):
         h = native.hip()
@@ -715,8 +611,7 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               s_stride=s_stride, s0w=_p(s0w), s1w=_p(s1w), reg_v=float(reg_v), reg_w=float(reg_w),
               opt_type=o.code, lr=float(o.lr), l1=float(o.l1), l2=float(o.l2), beta=float(o.beta),
               grad_out=gptr, g_stride=gstride, partial=_p(partial), big_list=_p(dd.big_list),
-              big_count=_p(dd.big_count), multi=_p(dd.multi), slice_list=_p(dd.slice_list),
-              slice_start=_p(dd.slice_start), nslices=int(dd.nslices or 0), dense_list=_p(dd.dense_list),
+              big_count=_p(dd.big_count), multi=_p(dd.multi), dense_list=_p(dd.dense_list),
               dense_part=_p(dp), nex=int(dpred.numel()),
               dense_stream=dense_stream.cuda_stream if dense_stream is not None else 0, dtype=dt, max_chunks=dd.n,
               max_unique=dd.n,
@@ -725,11 +620,7 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               seg_bounds=_p(seg_bounds), piece=int(piece),
               n_owners=(seg_bounds.numel() - 1) // 2 if seg_bounds is not None else 0,
               dense_A=_p(dense_A) if dd.dense_list is not None else 0,
-              cold_split=int(os.environ.get("FM_COLD_SPLIT", "0") == "1"), fwd_single=int(bool(fwd_single)),
-              chunk_pipe=int(os.environ.get("FM_CHUNK_PIPE", "0") == "1"),
-              chunk_grid=int(os.environ.get("FM_CHUNK_GRID", "0")),
-              combine_grid=int(os.environ.get("FM_COMBINE_GRID", "0")),
-              big_grid=int(os.environ.get("FM_BIG_GRID", "0")), **skw)
+              chunk_grid=int(os.environ.get("FM_CHUNK_GRID", "0")), **skw)
         dd.bwd_fresh = False  # a second backward over this grouping zeroes its counters itself
     else:
         _check(self_rows is None, "self rows are a GPU path")
@@ -842,6 +733,16 @@ def dense_apply(grad: torch.Tensor, table: TableState, opt: OptConfig, Kp: int, 
                              s0w=_p(table.s0w), s1w=_p(table.s1w), opt_type=opt.code, lr=float(opt.lr),
                              l1=float(opt.l1), l2=float(opt.l2), beta=float(opt.beta),
                              dtype=dtype_code(table.v.dtype), stream=_stream(grad), sr_counter=_p(sr_counter))
+
+
+def zero_listed_rows(buf: torch.Tensor, rows: torch.Tensor, count: torch.Tensor, max_n: int) -> None:
+    """buf[rows[i]] = 0 for i < count (device int32 scalar, capped at ``max_n``); GPU, no host sync."""
+    _check(_is_gpu(buf) and buf.dtype == torch.float32 and buf.is_contiguous() and buf.shape[1] % 4 == 0,
+           "buf: contiguous fp32 rows, width a multiple of 4")
+    _chk_vec(rows, torch.int32, None, "rows", buf.device)
+    _chk_vec(count, torch.int32, 1, "count", buf.device)
+    native.hip().zero_listed_rows(buf=_p(buf), row_words=buf.stride(0), list=_p(rows), count=_p(count),
+                                  max_n=int(min(max_n, rows.numel())), stream=_stream(buf))
 
 
 def apply_runs(req: torch.Tensor, run_off: torch.Tensor, splits: list[int], grad_in: torch.Tensor,

@@ -48,7 +48,8 @@ class DistContext:
         if self.world == 1:
             return float(x)
         t = torch.tensor([float(x)], dtype=torch.float64, device=self.device)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX, group=self.group)
+        rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+        dist.all_reduce(t, op=rop, group=self.group)
         return float(t.item())
 
 
@@ -82,6 +83,14 @@ def parse_dist_args(dist_args: list[str] | None) -> dict:
 
 
 MIN_HW_QUEUES = 8
+# GPU_MAX_HW_QUEUES as it stood when HIP initialised in this process (None: not known yet).
+# HIP reads the variable once, at its first device call; later edits of the environment change
+# nothing, so code that picks a stream layout by the queue count reads this, not the env.
+_HWQ_IN_FORCE: int | None = None
+
+
+def _env_hw_queues() -> int:
+    return int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
 
 
 def ensure_hw_queues(n: int = MIN_HW_QUEUES) -> int:
@@ -91,11 +100,39 @@ def ensure_hw_queues(n: int = MIN_HW_QUEUES) -> int:
     stream per communicator busy at once; on shared queues they serialise (sharded step 1.43 ->
     1.18 ms measured with 8), and two communicators' collective kernels queued in opposite
     orders on two ranks could wait on each other.  Only effective before HIP initialises (the
-    first device call); returns the value in force."""
-    cur = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+    first device call): once it has, the environment is left alone, a warning is printed when
+    the count in force is below ``n``, and the count in force is returned (``hw_queues()``)."""
+    if _cuda_initialized():
+        cur = hw_queues()
+        if cur < n:
+            import sys
+
+            print(f"[fast_tffm_amd] warning: HIP already initialised with GPU_MAX_HW_QUEUES={cur} (< {n}); "
+                  "multi-stream steps share hardware queues (single-communicator mode)", file=sys.stderr)
+        return cur
+    cur = _env_hw_queues()
     if cur < n:
         os.environ["GPU_MAX_HW_QUEUES"] = str(n)
         cur = n
+    return cur
+
+
+def _cuda_initialized() -> bool:
+    try:
+        return bool(torch.cuda.is_initialized())
+    except Exception:  # noqa: BLE001
+        return False
+
+
+def hw_queues() -> int:
+    """Hardware queues of this process: the value HIP initialised with when known (recorded at
+    the first call after initialisation), else the environment's current value."""
+    global _HWQ_IN_FORCE
+    if _HWQ_IN_FORCE is not None:
+        return _HWQ_IN_FORCE
+    cur = _env_hw_queues()
+    if _cuda_initialized():
+        _HWQ_IN_FORCE = cur   # (first look after HIP started: the environment has not moved since)
     return cur
 
 
@@ -122,6 +159,7 @@ def init_distributed(*, backend: str | None = None, rank: int | None = None, wor
         n = torch.cuda.device_count()
         dev = torch.device("cuda", local_rank % max(n, 1))
         torch.cuda.set_device(dev)
+        hw_queues()  # record the queue count HIP started with
     else:
         dev = torch.device("cpu")
     backend = backend or ("nccl" if use_gpu else "gloo")

@@ -66,6 +66,14 @@ class _Base:
         self.gs = model.Kp + 4          # exchange row: [v(Kp) | w | pad 3]
         self.dev = model.device
         self.dd2ws: K.DedupWorkspace | None = None
+        # payload bytes this rank has put on the wire to OTHER ranks (collective inputs, counted
+        # on the host from the split sizes it already knows; bench.py reports the per-step mean)
+        self.bytes_sent = 0
+
+    def _to_others(self, splits: list[int]) -> int:
+        """Items of an all-to-all split list that leave this rank."""
+        me = self.ctx.rank
+        return int(sum(s for q, s in enumerate(splits) if q != me))
 
     def close(self) -> None:
         """Release device resources (model.close() calls this after a device sync)."""
@@ -276,7 +284,9 @@ class ShardExchange(_Base):
         # dual needs the RCCL streams of both communicators on hardware queues of their own
         # (dist.ensure_hw_queues); with fewer queues (GPU_MAX_HW_QUEUES forced low by the user)
         # every collective goes through the main communicator in program order
-        few_queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8
+        from .dist import MIN_HW_QUEUES, hw_queues
+
+        few_queues = hw_queues() < MIN_HW_QUEUES   # (the count HIP started with, not the env's now)
         self.comm_mode = forced if forced in ("single", "dual") else (
             "single" if (single or self.W == 1 or few_queues) else "dual")
         self.plan_group = (dist.new_group(ranks=list(range(self.W)), backend=dist.get_backend(self.group))
@@ -401,8 +411,7 @@ class ShardExchange(_Base):
                                   dense_min=K.dense_min_for(sb.B, self.m.Kp, m.cfg.dedup_chunk,
                                                             table_dtype=m.table.v.dtype,
                                                             has_vals=sb.vals is not None,
-                                                            max_feats=sb.max_feats) if train else 0,
-                                  want_single=train and gpu and len(ranges) == 1 and self._fwd_single_ok())
+                                                            max_feats=sb.max_feats) if train else 0)
                 part.seg = K.seg_index(part.dd, self.key_bits, slot.segidx_buf(k)) if lookup else None
                 counts.append(K.owner_counts(part.dd, self.Rps, self.W))
                 pl.parts.append(part)
@@ -464,6 +473,7 @@ class ShardExchange(_Base):
                 else:
                     req_send = torch.remainder(part.dd.uniq[: part.U], self.Rps)
                     _a2a(dst, req_send, part.rc, part.sc, self.plan_group)
+                    self.bytes_sent += 4 * self._to_others(part.sc) + 8 * 2 * (self.W - 1) * len(pl.parts)
             # owner-side grouping of the received requests (W * P ascending runs): device
             # run offsets + match scratch for apply_runs; the CPU path sorts inside apply_runs
             pl.splits = [c for part in pl.parts for c in part.rc]
@@ -553,6 +563,7 @@ class ShardExchange(_Base):
             e.rows_send = rows_send
             e.work = dist.all_to_all_single(e.gathered, rows_send, part.sc, part.rc, group=self.plan_group,
                                             async_op=True)
+            self.bytes_sent += self.wire.rb * self._to_others(part.rc)
         return e
 
     def _patch_gpu(self, pl: _ShardPlan) -> tuple[torch.Tensor, torch.Tensor]:
@@ -571,6 +582,7 @@ class ShardExchange(_Base):
         else:
             recv = self.wire.empty(Dr, dev)
             _a2a(recv, patch, dr, ds, self.group)
+            self.bytes_sent += self.wire.rb * self._to_others(ds)
         if e.work is not None:
             e.work.wait()   # the early rows have arrived (compute stream waits on the RCCL stream)
             e.work = e.rows_send = None
@@ -607,6 +619,7 @@ class ShardExchange(_Base):
         else:
             e.gathered = self.wire.empty(U, self.dev)
             _a2a(e.gathered, rows_send, part.sc, part.rc, self.plan_group)
+            self.bytes_sent += self.wire.rb * self._to_others(part.rc)
         return e
 
     def _tag_view(self, buf: torch.Tensor) -> torch.Tensor:
@@ -635,21 +648,14 @@ class ShardExchange(_Base):
         else:
             recv = self.wire.empty(int(sum(dr)), self.dev)
             _a2a(recv, patch, dr, ds, self.group)
+            self.bytes_sent += self.wire.rb * self._to_others(ds)
         if recv.shape[0]:
             base = torch.repeat_interleave(e.dpos, drecv)
             e.gathered.index_copy_(0, base + self._tag_view(recv).to(torch.int64), recv)
         return self.wire.views(e.gathered)
 
-    def _fwd_single_ok(self) -> bool:
-        """Fused singleton update in the sharded step (one part, one-piece backward): the forward
-        emits the gradient rows of the batch's one-occurrence rows (or updates them in place, for
-        exclusive self rows) and the backward skips them (ops.kernels.fwd_single_enabled)."""
-        return (self.dev.type == "cuda" and self.nparts == 1 and not self.overlap_grads
-                and K.fwd_single_enabled() and self.m.cfg.loss_type in ("logistic", "mse")
-                and (not self.self_rows or self.m.cfg.opt.name in ("adagrad", "ftrl")))
-
     def _split_ok(self, pl: _ShardPlan, dd) -> bool:
-        return (self.overlap_grads and len(pl.parts) == 1 and dd.slice_list is None
+        return (self.overlap_grads and len(pl.parts) == 1
                 and (dd.dense_list is None or self.dev.type != "cuda"))
 
     def _half_bounds(self, part: _Part) -> tuple[list[int], list[int], list[int], list[int]]:
@@ -693,6 +699,8 @@ class ShardExchange(_Base):
         the first piece's gradient rows sent while the second is reduced."""
         m, ws, cfg, Kp, wf = self.m, self.m.ws, self.m.cfg, self.Kp, self.wire
         bounds = self._half_bounds(part)
+        if self.W > 1:
+            self.bytes_sent += 4 * wf.g_words * self._to_others(part.sc)
         kw = dict(mode=K.BWD_EMIT, src_v=src_v, src_w=src_w, grad_out=gs, reg_v=rv, reg_w=rw,
                   partial=ws.bwd_partial, threads=cfg.threads, grad_bf16=wf.grad_bf16, **skw)
         if self.dev.type != "cuda":  # CPU reference: one backward, the exchange still in two pieces
@@ -764,6 +772,7 @@ class ShardExchange(_Base):
             return rows_send, None
         gathered = self.wire.empty(part.U, self.dev)
         work = dist.all_to_all_single(gathered, rows_send, part.sc, part.rc, group=self.group, async_op=async_op)
+        self.bytes_sent += self.wire.rb * self._to_others(part.rc)
         return gathered, work
 
     def train_step(self, b: Batch, next_batch: Batch | None = None, next2: Batch | None = None):
@@ -820,10 +829,6 @@ class ShardExchange(_Base):
             src_v, src_w = wf.views(buf) if buf is not None else early_views
             dA = ws.dense_counts(ws.cap_b)[e0: e0 + sb.B] if dd.dense_list is not None else None
             gs = grad_send[part.u0: part.u0 + part.U]
-            single = None
-            if dd.single_flag is not None and dA is None and not self._split_ok(pl, dd):
-                single = K.SingleUpdate(dd.single_flag, m.table.state if srows is not None else None, cfg.opt, rv, rw,
-                                        sr, mode=K.BWD_EMIT, uniq=dd.uniq, grad_out=gs, grad_bf16=wf.grad_bf16)
             with roctx_range("fwd"):
                 fo = K.fm_forward(sb.offsets, part.keys if part.seg is not None else dd.inv[: sb.nnz], sb.vals,
                                   src_v, src_w, Kp, labels=sb.labels,
@@ -831,7 +836,7 @@ class ShardExchange(_Base):
                                   pred=ws.pred[e0: e0 + sb.B], r1=ws.r1[e0: e0 + sb.B],
                                   dpred=ws.dpred[e0: e0 + sb.B], partial=ws.fwd_partial, threads=cfg.threads,
                                   bias=m.gbias, dense=dd, dense_A=dA, dense_by_segment=True, self_rows=srows,
-                                  single=single, seg_lookup=part.seg)
+                                  seg_lookup=part.seg)
             loss = fo.loss_sum if loss is None else loss + fo.loss_sum
             if self._split_ok(pl, dd):
                 with roctx_range("bwd_split+grads"):
@@ -841,11 +846,12 @@ class ShardExchange(_Base):
                 K.fm_backward(dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT, src_v=src_v, src_w=src_w, grad_out=gs,
                               reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads,
                               dense_part=ws.dense_part, dense_stream=m._dense_stream() if gpu else None,
-                              grad_bf16=wf.grad_bf16, dense_A=dA, fwd_single=single is not None, **skw)
+                              grad_bf16=wf.grad_bf16, dense_A=dA, **skw)
             if self.W > 1:
                 with roctx_range("a2a_grads"):
                     gworks.append(dist.all_to_all_single(grad_recv[part.r0: part.r0 + part.R], gs, part.rc, part.sc,
                                                          group=self.group, async_op=True))
+                    self.bytes_sent += 4 * wf.g_words * self._to_others(part.sc)
         m.bias_step(ws.dpred[: b.B])
         for w in gworks:
             w.wait()
@@ -948,6 +954,8 @@ class DPExchange(_Base):
         g_all = [torch.empty_like(g_pad) for _ in range(self.W)]
         dist.all_gather(ids_all, ids_pad, group=self.group)
         dist.all_gather(g_all, g_pad, group=self.group)
+        # (ring all-gather: each rank forwards W - 1 chunks of its padded size)
+        self.bytes_sent += (self.W - 1) * (ids_pad.numel() * 4 + g_pad.numel() * 4 + 8)
         ids_cat = torch.cat([ids_all[r][: sizes[r]] for r in range(self.W)])
         g_cat = torch.cat([g_all[r][: sizes[r]] for r in range(self.W)])
         n = ids_cat.numel()
@@ -965,23 +973,37 @@ class DPExchange(_Base):
 
 
 class DPDenseExchange(DPExchange):
-    """Replicated table; dense all-reduce of a [vocab, Kp+4] gradient buffer (small vocabularies,
-    BASELINE config 3).
+    """Replicated table; dense gradient buffer reduce-scattered over the ranks, each rank updating
+    its own slice of rows, the updated rows all-gathered (small vocabularies, BASELINE config 3).
 
     GPU step (no host synchronisation, lookahead dedup as in the local step):
-      dedup of this batch (side stream, done during the previous step) -> forward on the
-      replica -> backward in EMIT_TABLE mode: each unique row's [g_v | g_w | 1] is scattered
-      straight into the persistent dense buffer ``G`` (the touch word marks it) -> all-reduce of
-      ``G`` over the ranks (RCCL ring / tree over xGMI; ``comm_dtype = bf16`` halves the bytes)
-      -> ``dense_apply``: every touched row gets one optimizer step on every replica (identical
-      inputs -> identical replicas) and is zeroed in ``G``, so ``G`` is never cleared wholesale.
-    The CPU (gloo) path keeps the plain-torch reference (gather, index_copy, nonzero)."""
+      dedup of this batch (side stream, done during the previous step) -> forward on the replica
+      -> backward in EMIT_TABLE mode: each unique row's [g_v | g_w | 1] is scattered straight into
+      the persistent dense buffer ``G`` [V, Kp+4] (the touch word marks it; V is padded to a
+      multiple of W, FMTable ``rows_multiple``) -> in-place reduce-scatter of ``G`` (rank r
+      receives the sums of its slice, rows [r S, (r+1) S), S = V / W; ``comm_dtype = bf16``
+      halves the bytes) -> ``dense_apply`` on that slice only: the optimizer's read-modify-write
+      of rows and state is split W ways and every touched row of the slice is zeroed in ``G`` ->
+      this rank's scattered rows of the OTHER slices are zeroed (``zero_listed_rows`` over the
+      dedup's unique rows), so ``G`` is never cleared wholesale -> in-place all-gather of every
+      slice's updated [v] and [w] rows: identical replicas.  The next batch's dedup (side stream)
+      runs beside the collectives.
+    Bytes per rank and step: (W-1)/W of the buffer (reduce-scatter) + (W-1)/W of the parameter
+    rows (all-gather), the same as the all-reduce it replaces, but the apply work no longer
+    repeats on every rank and the optimizer state is only ever touched by its slice's owner
+    (``sync_state`` all-gathers it for checkpoints).
+    The CPU (gloo) path follows the same structure with plain torch ops (gloo has no
+    reduce-scatter: the all-reduced buffer's slice is the same sum)."""
 
     supports_lookahead = True
 
     def __init__(self, model):
         super().__init__(model)
         V = model.table.rows
+        if V % self.W:
+            raise ValueError("dp_dense: the replicated table's rows must be a multiple of the world size")
+        self.S = V // self.W
+        self.r0 = self.ctx.rank * self.S
         self.dense = torch.zeros((V, self.gs), dtype=torch.float32, device=self.dev)
         self.arange = torch.arange(V + 1, dtype=torch.int32, device=self.dev)
         self.wire16 = (torch.empty((V, self.gs), dtype=torch.bfloat16, device=self.dev)
@@ -990,6 +1012,38 @@ class DPDenseExchange(DPExchange):
     def close(self) -> None:
         self.dense = self.wire16 = None
         super().close()
+
+    def _param_tensors(self) -> list[torch.Tensor]:
+        """The replica's parameter tensors, rows first (all-gathered after the sharded apply)."""
+        t = self.m.table
+        v = t.v.view(torch.uint8) if t.fp8 else t.v
+        return [v, t.wx if t.fp8 else t.w]
+
+    def _state_tensors(self) -> list[torch.Tensor]:
+        t = self.m.table
+        return [x for x in (t.s0v, t.s0w, t.s1v, t.s1w) if x is not None]
+
+    def _all_gather_rows(self, tensors: list[torch.Tensor]) -> None:
+        """Every rank's slice of each tensor (rows [q S, (q+1) S)) to every rank, in place."""
+        if self.W == 1:
+            return
+        r0, r1 = self.r0, self.r0 + self.S
+        for t in tensors:
+            if self.dev.type == "cuda":
+                dist.all_gather_into_tensor(t, t[r0:r1], group=self.group)
+                self.bytes_sent += (self.W - 1) * t[r0:r1].numel() * t.element_size()
+            else:
+                parts = [torch.empty_like(t[r0:r1]) for _ in range(self.W)]
+                dist.all_gather(parts, t[r0:r1].contiguous(), group=self.group)
+                t.copy_(torch.cat(parts))
+                self.bytes_sent += (self.W - 1) * t[r0:r1].numel() * t.element_size()
+
+    def sync_state(self) -> None:
+        """All-gather the optimizer state slices (each rank's apply only updates its own rows'
+        state): after this every replica holds the full state (checkpoints, re-sharding)."""
+        if self.dev.type == "cuda":
+            torch.cuda.current_stream(self.dev).synchronize()
+        self._all_gather_rows(self._state_tensors())
 
     def train_step(self, b: Batch, next_batch: Batch | None = None, next2: Batch | None = None):
         from ..models.fm import StepOut
@@ -1021,21 +1075,32 @@ class DPDenseExchange(DPExchange):
             K.fm_backward(pl.dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT_TABLE, table=m.table.state,
                           grad_out=self.dense, reg_v=rv, reg_w=rw, partial=ws.bwd_partial,
                           dense_part=ws.dense_part, dense_stream=m._dense_stream(), dense_A=dA)
+        if next_batch is not None:
+            # the next batch's dedup (side stream) overlaps the collectives and the apply below
+            m._lpending = m._local_plan(next_batch, nb_ready)
+        r0, S = self.r0, self.S
+        own = self.dense[r0: r0 + S]
+        if self.W > 1:
+            with roctx_range("reduce_scatter_grads"):
+                if self.wire16 is not None:
+                    self.wire16.copy_(self.dense)
+                    dist.reduce_scatter_tensor(self.wire16[r0: r0 + S], self.wire16, group=self.group)
+                    own.copy_(self.wire16[r0: r0 + S])
+                    self.bytes_sent += (self.W - 1) * S * self.gs * 2
+                else:
+                    dist.reduce_scatter_tensor(own, self.dense, group=self.group)
+                    self.bytes_sent += (self.W - 1) * S * self.gs * 4
+        with roctx_range("dense_apply"):
+            K.dense_apply(own, m.table.state, cfg.opt, Kp, row0=r0, rows=S, sr_counter=m.sr_tick())
+        if self.W > 1:
+            # this rank's contributions to the other slices (its own slice's touched rows were
+            # zeroed by the apply; re-zeroing them is harmless)
+            K.zero_listed_rows(self.dense, pl.dd.uniq, pl.dd.counts[:1], pl.dd.n)
+            with roctx_range("all_gather_rows"):
+                self._all_gather_rows(self._param_tensors())
         done = torch.cuda.Event()
         done.record(main)
         m._lslots[pl.slot].done = done
-        if next_batch is not None:
-            m._lpending = m._local_plan(next_batch, nb_ready)
-        if self.W > 1:
-            with roctx_range("allreduce_grads"):
-                if self.wire16 is not None:
-                    self.wire16.copy_(self.dense)
-                    dist.all_reduce(self.wire16, group=self.group)
-                    self.dense.copy_(self.wire16)
-                else:
-                    dist.all_reduce(self.dense, group=self.group)
-        with roctx_range("dense_apply"):
-            K.dense_apply(self.dense, m.table.state, cfg.opt, Kp, sr_counter=m.sr_tick())
         return StepOut(fo.loss_sum, b.B)
 
     def _train_step_reference(self, b: Batch):
@@ -1049,10 +1114,14 @@ class DPDenseExchange(DPExchange):
         dense[idx, self.Kp + 1] = 1.0  # touch counter travels in a pad column
         if self.W > 1:
             dist.all_reduce(dense, group=self.group)
-        touched = torch.nonzero(dense[:, self.Kp + 1] > 0).flatten().to(torch.int32)
+            self.bytes_sent += 2 * (self.W - 1) * dense.numel() * 4 // self.W
+        r0, S = self.r0, self.S
+        own = dense[r0: r0 + S]
+        touched = torch.nonzero(own[:, self.Kp + 1] > 0).flatten().to(torch.int32)
         T = touched.numel()
-        dd = K.DedupOut(n=T, uniq=touched, perm=touched, seg_start=self.arange[: T + 1],
+        dd = K.DedupOut(n=T, uniq=touched + r0, perm=touched, seg_start=self.arange[: T + 1],
                         num_unique=torch.tensor([T], dtype=torch.int32, device=self.dev), U_host=T)
-        K.apply_rows(dd, dense, self.m.table.state, self.m.cfg.opt, self.Kp, threads=self.m.cfg.threads,
+        K.apply_rows(dd, own, self.m.table.state, self.m.cfg.opt, self.Kp, threads=self.m.cfg.threads,
                      sr_counter=self.m.sr_tick())
+        self._all_gather_rows(self._param_tensors())
         return StepOut(fo.loss_sum, b.B)

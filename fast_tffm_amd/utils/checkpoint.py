@@ -72,7 +72,7 @@ def _table_sources(table) -> dict:
 
     Chunked so that a checkpoint of a 125M-row shard never holds more than one chunk of
     any table tensor in host memory (nor a full-size dequantised copy on the device)."""
-    K, n = table.K, table.rows
+    K, n = table.K, table.saved_rows
 
     def rows(t, cols=None):
         return lambda r0, r1: (t[r0:r1] if cols is None else t[r0:r1, :cols])
@@ -133,6 +133,9 @@ def save_checkpoint(model, log_dir: str, step: int, *, reader_state: dict | None
     sharded = model.mode == "shard"
     path = os.path.join(log_dir, f"model.ckpt-{step}")
     os.makedirs(path, exist_ok=True)
+    ex = getattr(model, "_exchange", None)
+    if ex is not None and hasattr(ex, "sync_state"):  # (collective: every rank) sharded optimizer state
+        ex.sync_state()
     if sharded or rank == 0:
         shard_rank, shard_world = (table.rank, table.world)
         tmp = os.path.join(path, _shard_name(shard_rank, shard_world) + ".tmp")

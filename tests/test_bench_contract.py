@@ -55,3 +55,33 @@ def test_bench_two_ranks_one_json_line():
     d = json.loads(lines[0])
     assert KEYS <= set(d) and d["n_gpus"] == 2 and d["config"]["global_batch"] == 512
     assert d["config"]["parallelism"] == "rowshard2" and d["config"]["early_rows"] and not d["config"]["split_grads"]
+    assert d["config"]["rccl_world"] == 2 and d["config"]["comm_backend"] == "gloo"
+    assert d["config"]["per_rank_ms"]["max"] >= d["config"]["per_rank_ms"]["min"] > 0
+    assert d["config"]["comm_bytes_per_rank"] > 0
+
+
+def test_bench_self_launches_ranks():
+    """``bench.py --gpus 2`` with no launcher environment starts the 2 ranks itself (through
+    torch.distributed.run, before any device call) instead of measuring one process."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                          "MASTER_PORT")}
+    env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup",
+                        "1", "--batch", "256", "--slots-per-gpu", "20000"],
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["rccl_world"] == 2 and d["config"]["global_batch"] == 512
+
+
+def test_bench_world_mismatch_exits_nonzero():
+    """An existing WORLD_SIZE that disagrees with --gpus is refused (exit 2, no JSON line)."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", WORLD_SIZE="1", RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup",
+                        "0", "--batch", "64", "--slots-per-gpu", "2000"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert not r.stdout.strip()
+    assert "WORLD_SIZE" in r.stderr

@@ -243,32 +243,6 @@ def test_rccl_world1_pipelined_shard_step_is_bitwise_deterministic(rccl_ctx, dty
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and a[2] == b[2]
 
 
-@pytest.mark.parametrize("dtype,prefetch", [(torch.float32, "off"), (torch.bfloat16, "on"), (torch.float32, "on")])
-def test_rccl_world1_fused_singletons_bitwise(rccl_ctx, dtype, prefetch, monkeypatch):
-    """Sharded step with the fused singleton update (the forward emits / applies the one-occurrence
-    rows, EMIT mode with self rows) == the same step without it, bit for bit."""
-    import dataclasses
-
-    V = 50000
-    gen = CriteoSynth(V, device="cuda", seed=23)
-    batches = [gen.batch(2048) for _ in range(4)]
-    res = []
-    for f in ("0", "1"):
-        monkeypatch.setenv("FM_FWD_SINGLE", f)
-        cfg = dataclasses.replace(_cfg("shard", V), dtype=dtype, prefetch_rows=prefetch)
-        dm = FactorizationMachine(cfg, device="cuda", dist=rccl_ctx)
-        assert dm._exchange._fwd_single_ok() == (f == "1")
-        for i, b in enumerate(batches):
-            dm.train_step(b, batches[i + 1] if i + 1 < len(batches) else None,
-                          batches[i + 2] if i + 2 < len(batches) else None)
-        torch.cuda.synchronize()
-        st = dm.table.state
-        res.append([x.clone() for x in (st.v, st.w, st.s0v, st.s0w)])
-        dm.close()
-    for x, y in zip(*res):
-        assert torch.equal(x.view(torch.uint8), y.view(torch.uint8))
-
-
 @pytest.mark.parametrize("k,dtype,prefetch", [(64, torch.float32, "on"), (16, torch.bfloat16, "off"),
                                                (128, torch.float8_e4m3fn, "on")])
 def test_rccl_world1_segment_lookup_bitwise(rccl_ctx, k, dtype, prefetch, monkeypatch):

@@ -119,6 +119,8 @@ def test_multi_rank_equals_single_process(tmp_path, mode, grad_reduce, mb):
         for r in res:
             torch.testing.assert_close(r["rows"], ref_rows, rtol=1e-5, atol=1e-7)
         assert torch.equal(res[0]["rows"], res[1]["rows"])
+        if mode == "dp_dense":
+            _check_dense_checkpoint(tmp_path, ref)
     # predictions of rank r's eval batch match the single model's
     for rank, r in enumerate(res):
         torch.testing.assert_close(r["pred"], ref.predict(_batch(99, rank)), rtol=1e-5, atol=1e-6)
@@ -137,7 +139,7 @@ def test_multi_rank_equals_single_process(tmp_path, mode, grad_reduce, mb):
         assert torch.equal(m2.table.reference_rows(), _assemble(res))  # bit-exact round trip of the shards
 
 
-@pytest.mark.parametrize("world,mode", [(4, "shard"), (8, "shard"), (4, "dp_dense")])
+@pytest.mark.parametrize("world,mode", [(4, "shard"), (8, "shard"), (4, "dp_dense"), (8, "dp_dense")])
 def test_larger_worlds_equal_single_process(tmp_path, world, mode):
     """World 4 / 8 (the node sizes of the scaling runs): the sharded step with its N>1
     pipelining (depth-2 plan, early row exchange with dirty-row patches, split backward
@@ -155,5 +157,16 @@ def test_larger_worlds_equal_single_process(tmp_path, world, mode):
     else:
         for r in res:
             torch.testing.assert_close(r["rows"], ref_rows, rtol=1e-5, atol=1e-7)
+        _check_dense_checkpoint(tmp_path, ref)
     for rank, r in enumerate(res):
         torch.testing.assert_close(r["pred"], ref.predict(_batch(99, rank)), rtol=1e-5, atol=1e-6)
+
+
+def _check_dense_checkpoint(tmp_path, ref):
+    """dp_dense keeps each row's optimizer state on its slice's owner only (sharded apply); the
+    checkpoint all-gathers it first, so the restored table matches one process in rows AND state."""
+    m1 = FactorizationMachine(_cfg("local", "sum", 16), device="cpu")
+    ckpt.restore_checkpoint(m1, ckpt.latest_checkpoint(str(tmp_path / "log")))
+    torch.testing.assert_close(m1.table.reference_rows(), ref.table.reference_rows(), rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(m1.table.s0v[:V, :KF], ref.table.s0v[:V, :KF], rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(m1.table.s0w[:V], ref.table.s0w[:V], rtol=1e-5, atol=1e-7)

@@ -6,7 +6,6 @@ import torch
 from fast_tffm_amd.data.synthetic import CriteoSynth, random_batch
 from fast_tffm_amd.models.fm import FactorizationMachine, FMConfig
 from fast_tffm_amd.ops import kernels as K
-from fast_tffm_amd.ops import native
 
 from oracle import reference_train_step
 
@@ -72,29 +71,6 @@ def test_bf16_table_step_close_to_fp32():
     torch.testing.assert_close(m16.table.reference_rows(), m32.table.reference_rows(), rtol=2e-2, atol=2e-3)
 
 
-@pytest.mark.parametrize("k", [16, 64])
-def test_xcd_sliced_schedule_matches_oracle(monkeypatch, k):
-    """Per-slice chunk lists + slice-cut hot rows (the large-batch schedule) forced on a small batch."""
-    monkeypatch.setattr(K, "SLICE_BYTES", 4096)
-    monkeypatch.setenv("FM_BWD_SLICES", "1")
-    V = 5000
-    gen = CriteoSynth(V, device="cuda", seed=8)
-    b = gen.batch(2048)
-    m = _model(V=V, k=k)
-    assert K.slice_plan(b.B, m.Kp)[1] > 8
-    p0 = m.table.reference_rows().double().cpu()
-    m.train_step(b)
-    p1, _, _ = reference_train_step(p0, torch.full_like(p0, 0.1), b.to("cpu"), "logistic", 0.05, 0.01, 0.01, 512)
-    torch.testing.assert_close(m.table.reference_rows().double().cpu(), p1, rtol=2e-4, atol=5e-6)
-    # the plan: every chunk listed exactly once, slice lists cover [0, #chunks)
-    dd = K.dedup(m._rows32(b), key_bits=32, ex_of_occ=K.csr_rows(b.offsets), num_examples=b.B, Kp=m.Kp)
-    C = int(dd.counts[1])
-    lst = dd.slice_list[:C].sort().values.cpu()
-    assert torch.equal(lst, torch.arange(C, dtype=torch.int32))
-    st = dd.slice_start[: dd.nslices + 1].cpu()
-    assert int(st[0]) == 0 and int(st[-1]) == C and bool((st[1:] >= st[:-1]).all())
-
-
 @pytest.mark.parametrize("k,dtype", [(16, torch.float32), (64, torch.float32), (100, torch.float32),
                                      (64, torch.bfloat16), (128, torch.bfloat16)])
 def test_dense_mfma_backward_matches_oracle(monkeypatch, k, dtype):
@@ -140,24 +116,6 @@ def test_forward_dense_counts_match_torch():
     assert torch.equal(A[:, :nd], want)
     if nd < K.MAX_DENSE:
         assert int(A[:, nd:].max()) == 0
-
-
-@pytest.mark.parametrize("k,dtype", [(64, torch.float32), (16, torch.bfloat16), (128, K.FP8)])
-def test_cold_split_backward_matches_default_bitwise(monkeypatch, k, dtype):
-    """Opt-in cold-chunk kernel (FM_COLD_SPLIT=1) == the chunk kernel's short-chunk path (same
-    summation order; the two kernels may contract multiply-adds differently: fp32 rounding)."""
-    gen = CriteoSynth(20000, device="cuda", seed=41)
-    batches = [gen.batch(4096) for _ in range(3)]
-    runs = []
-    for cold in ("0", "1"):
-        monkeypatch.setenv("FM_COLD_SPLIT", cold)
-        m = _model(V=20000, k=k, dtype=dtype)
-        for bt in batches:
-            m.train_step(bt)
-        torch.cuda.synchronize()
-        runs.append(_state(m))
-    for x, y in zip(*runs):
-        torch.testing.assert_close(x.float(), y.float(), rtol=1e-5, atol=1e-7)
 
 
 def test_dense_mfma_backward_is_deterministic(monkeypatch):
@@ -261,27 +219,3 @@ def test_csr_rows_matches_torch(B, maxf):
     torch.testing.assert_close(K.csr_rows(d, nnz=nnz).cpu(), ex, rtol=0, atol=0)
     bits = max(1, int(max(int(sizes.max()), 1) - 1).bit_length())
     torch.testing.assert_close(K.csr_rows(d, nnz=nnz, slot_bits=bits).cpu(), (ex << bits) | slot, rtol=0, atol=0)
-
-
-@pytest.mark.parametrize("k,dtype,opt", [(64, torch.float32, "adagrad"), (64, torch.bfloat16, "adagrad"),
-                                         (64, torch.float8_e4m3fn, "ftrl"), (60, torch.float32, "ftrl")])
-def test_pipelined_chunk_kernel_bitwise(monkeypatch, k, dtype, opt):
-    """fm_bwd_chunk_pipe_kernel (16-lane rows, FM_CHUNK_PIPE=1) == the plain chunk kernel, bit for bit."""
-    gen = CriteoSynth(30000, device="cuda", seed=17)
-    batches = [gen.batch(4096) for _ in range(3)]
-    o = K.OptConfig(opt, lr=0.05, l1=0.001, l2=0.001, beta=1.0)
-    res = []
-    for f in ("0", "1"):
-        monkeypatch.setenv("FM_CHUNK_PIPE", f)
-        m = FactorizationMachine(
-            FMConfig(vocabulary_size=30000, factor_num=k, loss_type="logistic", init_value_range=0.05, seed=3,
-                     opt=o, batch_size=512, factor_lambda=0.01, bias_lambda=0.01, dtype=dtype), device="cuda")
-        assert native.hip().lanes_per_row(m.Kp, K.dtype_code(m.table.v.dtype)) == 16
-        for i, bt in enumerate(batches):
-            m.train_step(bt, batches[i + 1] if i + 1 < len(batches) else None)
-        torch.cuda.synchronize()
-        st = m.table.state
-        res.append([x.clone() for x in (st.v, st.w, st.s0v, st.s0w) if x is not None])
-        m.close()
-    for x, y in zip(*res):
-        assert torch.equal(x.view(torch.uint8), y.view(torch.uint8))
