@@ -8,16 +8,17 @@
 //      use (rocPRIM onesweep).  The payload is the occurrence index, or -- when
 //      the caller needs neither the inverse map nor per-occurrence values --
 //      directly the example index, which saves the gather in step 3;
-//   2. run-length encoding with a 3-kernel tile scan of two flags per sorted
-//      position: "segment head" (key differs from its left neighbour) and
-//      "chunk start" (head, or position % CH == 0):
-//        tile_count  -- per 2048-element tile: #heads, #chunk starts
-//        tile_scan   -- one workgroup scans the tile totals (U, #chunks)
-//        tile_emit   -- re-reads its tile, block-scans the flags and writes
-//                       unique keys, segment starts, first chunk of each
-//                       segment, chunk starts, chunk->segment and the optional
-//                       inverse map / per-sorted-occurrence example index and
-//                       value.
+//   2. run-length encoding in ONE pass over the sorted keys (rle_onepass_kernel):
+//      each 2048-element tile flags "segment head" (key differs from its left
+//      neighbour) and "chunk start" (head, or position % CH == 0), block-scans
+//      the flags, finds its global offsets by a decoupled look-back over the
+//      preceding tiles' published counts (64-bit status words, agent-scope
+//      atomics on both sides: the per-XCD L2s are not coherent), and writes the
+//      unique keys, segment starts, first chunk of each segment, chunk starts,
+//      chunk->segment and the optional inverse map / per-sorted-occurrence
+//      example index and value.  (Round 2 ran this as three kernels -- tile
+//      count, a one-workgroup scan of the tile totals, tile emit -- reading the
+//      keys twice: 42 + 27 + 86 us next to the backward, profiles/r3.)
 // Chunks cut every segment at CH-aligned sorted positions, so no chunk is
 // longer than CH and a hot id (tens of thousands of occurrences in Criteo's
 // low-cardinality fields) is spread over many lane groups in the backward.
@@ -28,7 +29,7 @@ namespace fm {
 
 constexpr int kRleItems = 8;                     // elements per thread
 constexpr int kRleTile = kBlock * kRleItems;     // 2048 elements per tile
-constexpr int kMaxTiles = 1024 * 64;             // single-workgroup tile scan limit (n < 134M)
+constexpr int kMaxTiles = 1 << 20;               // look-back status words per call (n < 2^31)
 
 struct RleArgs {
   int n, CH, ntiles;
@@ -38,8 +39,11 @@ struct RleArgs {
   const int* spay;                // sorted payload (occurrence or example index)
   int ex_shift;                   // > 0: payload / ex_of_occ hold packed codes (example << ex_shift | slot)
   const int* offsets;             // [B+1] CSR offsets (packed codes -> occurrence index)
-  unsigned* tile_cnt;             // [3][ntiles] heads, chunk starts, dense heads per tile
-  unsigned* tile_off;             // [3][ntiles] exclusive offsets
+  unsigned long long* status;     // [ntiles] look-back words (zeroed before the launch)
+  int* tile_ctr;                  // dynamic tile ids (zeroed before the launch)
+  int* dense_tmp;                 // dense-row heads as found (unordered), dense_cnt of them
+  int* dense_cnt;
+  int dense_cap;
   uint32_t* uniq;                 // [n] unique keys (first U valid)
   int* seg_start;                 // [n+1]
   int* seg_chunk;                 // [n+1] first chunk of each segment
@@ -130,97 +134,74 @@ __device__ inline void block_excl_scan(const unsigned (&v)[NC], unsigned (&ex)[N
   __syncthreads();
 }
 
-__global__ __launch_bounds__(kBlock) void rle_tile_count_kernel(RleArgs a) {
-  const int tile = blockIdx.x;
-  Rle8 r;
-  const int j0 = tile * kRleTile + threadIdx.x * kRleItems;
-  rle_flags8(a, j0, r);
-  unsigned v[3] = {0u, 0u, 0u}, ex[3], tot[3];
-#pragma unroll
-  for (int q = 0; q < kRleItems; ++q) {
-    v[0] += r.hd[q];
-    v[1] += r.cs[q];
-    v[2] += r.hd[q] && dense_head(a, j0 + q, r.k[q]);
-  }
-  block_excl_scan<3>(v, ex, tot);
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i) a.tile_cnt[i * a.ntiles + tile] = tot[i];
-  }
+// Look-back status word of a tile: [flag:2 | heads:31 | chunk starts:31]; flag 1 = the tile's
+// own counts, 2 = inclusive prefix over tiles 0..t.
+constexpr unsigned long long kLbAgg = 1ull << 62, kLbPre = 2ull << 62;
+constexpr unsigned long long kLbMask31 = (1ull << 31) - 1;
+constexpr int kLbSpinLimit = 1 << 22;   // bounded wait: a lost predecessor ends the kernel, not the GPU
+
+__device__ inline unsigned long long lb_pack(unsigned long long flag, unsigned h, unsigned c) {
+  return flag | ((unsigned long long)h << 31) | (unsigned long long)c;
 }
 
-// One workgroup of 1024 threads: exclusive scan of the tile totals.
-__global__ __launch_bounds__(1024) void rle_tile_scan_kernel(RleArgs a) {
-  __shared__ unsigned carry[3];
-  __shared__ unsigned wsum[3][16];
-  if (threadIdx.x < 3) carry[threadIdx.x] = 0;
+// One pass: flags, block scan, decoupled look-back for the tile's global offsets, emit.
+__global__ __launch_bounds__(kBlock) void rle_onepass_kernel(RleArgs a) {
+  __shared__ int s_tile;
+  __shared__ unsigned s_pre[2];
+  if (threadIdx.x == 0) s_tile = atomicAdd(a.tile_ctr, 1);  // tiles start in id order: no look-back deadlock
   __syncthreads();
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int base = 0; base < a.ntiles; base += 1024) {
-    const int t = base + threadIdx.x;
-    unsigned v[3], inc[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) inc[i] = v[i] = t < a.ntiles ? a.tile_cnt[i * a.ntiles + t] : 0u;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const unsigned up = __shfl_up(inc[i], o, 64);
-        if (lane >= o) inc[i] += up;
-      }
-    }
-    if (lane == 63) {
-#pragma unroll
-      for (int i = 0; i < 3; ++i) wsum[i][wv] = inc[i];
-    }
-    __syncthreads();
-    unsigned b[3], tot[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      b[i] = carry[i];
-      tot[i] = 0;
-      for (int w = 0; w < 16; ++w) {
-        if (w < wv) b[i] += wsum[i][w];
-        tot[i] += wsum[i][w];
-      }
-      if (t < a.ntiles) a.tile_off[i * a.ntiles + t] = b[i] + inc[i] - v[i];
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-#pragma unroll
-      for (int i = 0; i < 3; ++i) carry[i] += tot[i];
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    a.counts[0] = (int)carry[0];
-    a.counts[1] = (int)carry[1];
-    a.counts[3] = (int)carry[2];  // dense rows (all of them; the first kMaxDense are listed)
-    a.seg_start[carry[0]] = a.n;
-    a.seg_chunk[carry[0]] = (int)carry[1];
-    a.chunk_start[carry[1]] = a.n;
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void rle_tile_emit_kernel(RleArgs a) {
-  const int tile = blockIdx.x;
+  const int tile = s_tile;
   const int j0 = tile * kRleTile + threadIdx.x * kRleItems;
   Rle8 r;
   rle_flags8(a, j0, r);
-  unsigned v[3] = {0u, 0u, 0u}, ex[3], tot[3];
+  unsigned v[2] = {0u, 0u}, ex[2], tot[2];
   bool dn[kRleItems];
 #pragma unroll
   for (int q = 0; q < kRleItems; ++q) {
     dn[q] = r.hd[q] && dense_head(a, j0 + q, r.k[q]);
     v[0] += r.hd[q];
     v[1] += r.cs[q];
-    v[2] += dn[q];
   }
-  block_excl_scan<3>(v, ex, tot);
-  // running (inclusive) segment / chunk / dense-row ids of this thread's elements
-  int s = (int)(a.tile_off[tile] + ex[0]) - 1;
-  int ch = (int)(a.tile_off[a.ntiles + tile] + ex[1]) - 1;
-  int dslot = (int)(a.tile_off[2 * a.ntiles + tile] + ex[2]);
+  block_excl_scan<2>(v, ex, tot);
+  if (threadIdx.x == 0) {
+    unsigned long long* st = a.status;
+    unsigned ph = 0, pc = 0;
+    if (tile == 0) {
+      __hip_atomic_exchange(&st[0], lb_pack(kLbPre, tot[0], tot[1]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_exchange(&st[tile], lb_pack(kLbAgg, tot[0], tot[1]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int t = tile - 1; t >= 0; --t) {
+        unsigned long long w = 0;
+        for (int spin = 0; spin < kLbSpinLimit; ++spin) {
+          // (a read-only atomic: executed at the memory side, never a stale L2 copy)
+          w = __hip_atomic_fetch_or(&st[t], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (w >> 62) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        ph += (unsigned)((w >> 31) & kLbMask31);
+        pc += (unsigned)(w & kLbMask31);
+        if ((w >> 62) == 2) break;
+      }
+      __hip_atomic_exchange(&st[tile], lb_pack(kLbPre, ph + tot[0], pc + tot[1]), __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_pre[0] = ph;
+    s_pre[1] = pc;
+    if (tile == a.ntiles - 1) {  // totals, sentinels; the backward's two counters start at 0
+      const unsigned U = ph + tot[0], C = pc + tot[1];
+      a.counts[0] = (int)U;
+      a.counts[1] = (int)C;
+      a.counts[2] = 0;
+      a.counts[4] = 0;
+      a.seg_start[U] = a.n;
+      a.seg_chunk[U] = (int)C;
+      a.chunk_start[C] = a.n;
+    }
+  }
+  __syncthreads();
+  // running (inclusive) segment / chunk ids of this thread's elements
+  int s = (int)(s_pre[0] + ex[0]) - 1;
+  int ch = (int)(s_pre[1] + ex[1]) - 1;
   int sq[kRleItems];
 #pragma unroll
   for (int q = 0; q < kRleItems; ++q) {
@@ -233,9 +214,9 @@ __global__ __launch_bounds__(kBlock) void rle_tile_emit_kernel(RleArgs a) {
       a.uniq[s] = r.k[q];
       a.seg_start[s] = j;
       a.seg_chunk[s] = ch;
-      if (dn[q]) {  // dense rows in key order: the first kMaxDense take the MFMA path
-        if (dslot < kMaxDense) a.dense_list[dslot] = s;
-        ++dslot;
+      if (dn[q]) {  // dense rows as found; dense_select_kernel keeps the first kMaxDense in key order
+        const int slot = atomicAdd(a.dense_cnt, 1);
+        if (slot < a.dense_cap) a.dense_tmp[slot] = s;
       }
     }
     if (r.cs[q]) {
@@ -274,6 +255,53 @@ __global__ __launch_bounds__(kBlock) void rle_tile_emit_kernel(RleArgs a) {
       if (a.sorted_x) a.sorted_x[j0 + q] = xv[q];
     }
   }
+}
+
+// Dense rows (MFMA backward, opt-in): the first kMaxDense of the found heads in key (= segment)
+// order, deterministic whatever order the tiles appended them in.  One workgroup: the cut value is
+// found by a bitwise binary search on counts, the kept ids (<= kMaxDense, distinct) ranked by
+// counting.
+__global__ __launch_bounds__(kBlock) void dense_select_kernel(RleArgs a) {
+  __shared__ int keep[kMaxDense];
+  __shared__ int red[kWavesPerBlock];
+  __shared__ int s_cut;
+  const int n = min(*a.dense_cnt, a.dense_cap);
+  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x >> 6;
+  auto count_le = [&](int x) {  // #entries <= x, block-wide
+    int c = 0;
+    for (int i = threadIdx.x; i < n; i += kBlock) c += a.dense_tmp[i] <= x;
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) c += __shfl_xor(c, o, kWave);
+    if (lane == 0) red[wv] = c;
+    __syncthreads();
+    int t = 0;
+    for (int w = 0; w < kWavesPerBlock; ++w) t += red[w];
+    __syncthreads();
+    return t;
+  };
+  // cut = smallest x with count_le(x) >= min(n, kMaxDense)
+  const int want = min(n, kMaxDense);
+  int lo = 0, hi = 0x7fffffff;
+  if (want > 0) {
+    while (lo < hi) {
+      const int mid = lo + ((hi - lo) >> 1);
+      if (count_le(mid) >= want) hi = mid; else lo = mid + 1;
+    }
+  }
+  if (threadIdx.x == 0) s_cut = lo;
+  __syncthreads();
+  const int cut = s_cut;
+  for (int i = threadIdx.x; i < n; i += kBlock) {
+    const int x = a.dense_tmp[i];
+    if (want > 0 && x <= cut) {
+      int rank = 0;
+      for (int j = 0; j < n; ++j) rank += a.dense_tmp[j] < x;
+      if (rank < kMaxDense) keep[rank] = x;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < want; i += kBlock) a.dense_list[i] = keep[i];
+  if (threadIdx.x == 0) a.counts[3] = *a.dense_cnt;
 }
 
 // Flag every chunk of a listed dense row: the chunk kernel skips them (their
@@ -332,11 +360,17 @@ static size_t sort_temp_bytes(int n, hipStream_t st) {
   return align_up(best);
 }
 
-// Workspace layout: [rocprim sort temp | tile_cnt(3*ntiles) | tile_off(3*ntiles)]
+// Dense-row candidates the RLE can list (dense_min >= kDenseMinFloor: at most n / kDenseMinFloor rows)
+constexpr int kDenseMinFloor = 32;
+static size_t dense_cap_for(int n) { return (size_t)n / kDenseMinFloor + 1; }
+
+// Workspace layout: [rocprim sort temp | tile_ctr, dense_cnt, status[ntiles] (zeroed per call) | dense_tmp]
+static size_t lb_bytes(int ntiles) { return 8 + 8 * (size_t)ntiles; }
+
 size_t dedup_workspace_bytes(int n) {
   if (n <= 0) return 256;
   const size_t ntiles = ((size_t)n + kRleTile - 1) / kRleTile;
-  return sort_temp_bytes(n, 0) + 2 * align_up(3 * ntiles * sizeof(unsigned)) + 256;
+  return sort_temp_bytes(n, 0) + align_up(lb_bytes((int)ntiles)) + align_up(dense_cap_for(n) * sizeof(int)) + 256;
 }
 
 struct DedupArgs {
@@ -414,20 +448,25 @@ int launch_dedup(const DedupArgs& a, hipStream_t st) {
   if (ntiles > kMaxTiles) return -3;
   const size_t tmp = sort_temp_bytes(a.n, st);
   char* base = static_cast<char*>(a.ws);
-  unsigned* tile_cnt = reinterpret_cast<unsigned*>(base + tmp);
-  unsigned* tile_off = reinterpret_cast<unsigned*>(base + tmp + align_up(3 * (size_t)ntiles * sizeof(unsigned)));
-  if (tmp + 2 * align_up(3 * (size_t)ntiles * sizeof(unsigned)) > a.ws_bytes) return -2;
+  char* lb = base + tmp;
+  int* dense_tmp = reinterpret_cast<int*>(lb + align_up(lb_bytes(ntiles)));
+  if (tmp + align_up(lb_bytes(ntiles)) + align_up(dense_cap_for(a.n) * sizeof(int)) > a.ws_bytes) return -2;
+  if (a.dense_list && a.dense_min > 0 && a.dense_min < kDenseMinFloor) return -8;
+  (void)hipMemsetAsync(lb, 0, lb_bytes(ntiles), st);
 
   size_t sort_bytes = tmp;
   hipError_t e = sort_pairs(a.ws, sort_bytes, a.keys, a.skeys, a.payload, a.spay, a.n, a.end_bit, st);
   if (e != hipSuccess) return (int)e;
   RleArgs r{a.n, a.CH, ntiles, a.dense_list ? a.dense_min : 0, a.dense_list, a.skeys, a.spay, a.ex_shift,
-            a.offsets, tile_cnt, tile_off, a.uniq, a.seg_start, a.seg_chunk, a.chunk_start, a.chunk_seg,
-            a.chunk_key, a.counts, a.inv, a.ex_of_occ, a.sorted_ex, a.vals, a.sorted_x};
-  hipLaunchKernelGGL(rle_tile_count_kernel, dim3(ntiles), dim3(kBlock), 0, st, r);
-  hipLaunchKernelGGL(rle_tile_scan_kernel, dim3(1), dim3(1024), 0, st, r);
-  hipLaunchKernelGGL(rle_tile_emit_kernel, dim3(ntiles), dim3(kBlock), 0, st, r);
-  if (r.dense_min > 0) hipLaunchKernelGGL(mark_dense_chunks_kernel, dim3(kMaxDense), dim3(kBlock), 0, st, r);
+            a.offsets, reinterpret_cast<unsigned long long*>(lb + 8), reinterpret_cast<int*>(lb),
+            dense_tmp, reinterpret_cast<int*>(lb + 4), (int)dense_cap_for(a.n), a.uniq, a.seg_start,
+            a.seg_chunk, a.chunk_start, a.chunk_seg, a.chunk_key, a.counts, a.inv, a.ex_of_occ, a.sorted_ex,
+            a.vals, a.sorted_x};
+  hipLaunchKernelGGL(rle_onepass_kernel, dim3(ntiles), dim3(kBlock), 0, st, r);
+  if (r.dense_min > 0) {
+    hipLaunchKernelGGL(dense_select_kernel, dim3(1), dim3(kBlock), 0, st, r);
+    hipLaunchKernelGGL(mark_dense_chunks_kernel, dim3(kMaxDense), dim3(kBlock), 0, st, r);
+  }
   return (int)hipGetLastError();
 }
 
