@@ -135,10 +135,13 @@ __device__ inline void block_excl_scan(const unsigned (&v)[NC], unsigned (&ex)[N
 }
 
 // Look-back status word of a tile: [flag:2 | heads:31 | chunk starts:31]; flag 1 = the tile's
-// own counts, 2 = inclusive prefix over tiles 0..t.
+// own counts, 2 = inclusive prefix over tiles 0..t.  (A first version read the predecessors one
+// at a time with read-only atomics -- executed at the memory side, ~1-3 us each under load -- and
+// made the one-pass RLE 67 us, slower than the three kernels it replaced; the wave-wide look-back
+// with agent-scope loads reads 64 predecessors per step.)
 constexpr unsigned long long kLbAgg = 1ull << 62, kLbPre = 2ull << 62;
 constexpr unsigned long long kLbMask31 = (1ull << 31) - 1;
-constexpr int kLbSpinLimit = 1 << 22;   // bounded wait: a lost predecessor ends the kernel, not the GPU
+constexpr int kLbSpinLimit = 1 << 18;   // bounded wait: a lost predecessor ends the kernel, not the GPU
 
 __device__ inline unsigned long long lb_pack(unsigned long long flag, unsigned h, unsigned c) {
   return flag | ((unsigned long long)h << 31) | (unsigned long long)c;
@@ -163,39 +166,63 @@ __global__ __launch_bounds__(kBlock) void rle_onepass_kernel(RleArgs a) {
     v[1] += r.cs[q];
   }
   block_excl_scan<2>(v, ex, tot);
-  if (threadIdx.x == 0) {
+  // Wave 0: publish this tile's counts, then look back over the predecessors 64 at a time (lane l
+  // reads tile - 1 - l): the nearest inclusive prefix ends the walk, the aggregates in front of it
+  // are summed; a window with an unpublished tile is re-read.  Status words are written with
+  // agent-scope atomics and read with agent-scope loads (L2-served, never a stale L1 line).
+  if (threadIdx.x < kWave) {
+    const int lane = threadIdx.x;
     unsigned long long* st = a.status;
-    unsigned ph = 0, pc = 0;
-    if (tile == 0) {
-      __hip_atomic_exchange(&st[0], lb_pack(kLbPre, tot[0], tot[1]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __hip_atomic_exchange(&st[tile], lb_pack(kLbAgg, tot[0], tot[1]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int t = tile - 1; t >= 0; --t) {
-        unsigned long long w = 0;
-        for (int spin = 0; spin < kLbSpinLimit; ++spin) {
-          // (a read-only atomic: executed at the memory side, never a stale L2 copy)
-          w = __hip_atomic_fetch_or(&st[t], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (w >> 62) break;
-          __builtin_amdgcn_s_sleep(1);
-        }
-        ph += (unsigned)((w >> 31) & kLbMask31);
-        pc += (unsigned)(w & kLbMask31);
-        if ((w >> 62) == 2) break;
-      }
-      __hip_atomic_exchange(&st[tile], lb_pack(kLbPre, ph + tot[0], pc + tot[1]), __ATOMIC_RELAXED,
+    if (lane == 0)
+      __hip_atomic_exchange(&st[tile], lb_pack(tile == 0 ? kLbPre : kLbAgg, tot[0], tot[1]), __ATOMIC_RELAXED,
                             __HIP_MEMORY_SCOPE_AGENT);
+    unsigned ph = 0, pc = 0;
+    int base = tile - 1;  // next window: tiles base, base - 1, ..., base - 63
+    int spins = 0;
+    while (base >= 0) {
+      const int t = base - lane;
+      const unsigned long long w =
+          t >= 0 ? __hip_atomic_load(&st[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbPre;
+      const unsigned flag = (unsigned)(w >> 62);
+      const uint64_t pre = __ballot(flag == 2);
+      const uint64_t unset = __ballot(flag == 0);
+      // lanes up to (and including) the first prefix; an unset tile before it: wait and re-read
+      const int stop = pre ? __ffsll((long long)pre) - 1 : kWave - 1;
+      const uint64_t need = stop == kWave - 1 ? ~0ull : ((2ull << stop) - 1ull);
+      if (unset & need) {
+        if (++spins > kLbSpinLimit) break;  // (a lost predecessor: give up rather than hang the GPU)
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      const bool take = lane <= stop && t >= 0;
+      unsigned h = take ? (unsigned)((w >> 31) & kLbMask31) : 0u;
+      unsigned c = take ? (unsigned)(w & kLbMask31) : 0u;
+#pragma unroll
+      for (int o = kWave / 2; o > 0; o >>= 1) {
+        h += __shfl_xor(h, o, kWave);
+        c += __shfl_xor(c, o, kWave);
+      }
+      ph += h;
+      pc += c;
+      if (pre) break;
+      base -= kWave;
     }
-    s_pre[0] = ph;
-    s_pre[1] = pc;
-    if (tile == a.ntiles - 1) {  // totals, sentinels; the backward's two counters start at 0
-      const unsigned U = ph + tot[0], C = pc + tot[1];
-      a.counts[0] = (int)U;
-      a.counts[1] = (int)C;
-      a.counts[2] = 0;
-      a.counts[4] = 0;
-      a.seg_start[U] = a.n;
-      a.seg_chunk[U] = (int)C;
-      a.chunk_start[C] = a.n;
+    if (lane == 0) {
+      if (tile > 0)
+        __hip_atomic_exchange(&st[tile], lb_pack(kLbPre, ph + tot[0], pc + tot[1]), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+      s_pre[0] = ph;
+      s_pre[1] = pc;
+      if (tile == a.ntiles - 1) {  // totals, sentinels; the backward's two counters start at 0
+        const unsigned U = ph + tot[0], C = pc + tot[1];
+        a.counts[0] = (int)U;
+        a.counts[1] = (int)C;
+        a.counts[2] = 0;
+        a.counts[4] = 0;
+        a.seg_start[U] = a.n;
+        a.seg_chunk[U] = (int)C;
+        a.chunk_start[C] = a.n;
+      }
     }
   }
   __syncthreads();

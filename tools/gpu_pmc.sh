@@ -14,3 +14,5 @@ for CTRS in "TCC_HIT_sum TCC_MISS_sum" "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_IN
   timeout -k 10 300 rocprofv3 --pmc $CTRS --kernel-trace --output-format csv -d $OUT/p$i -o run -- python3 $R/bench.py --steps 5 --warmup 2 --graph 0 "$@" > $OUT/p$i.log 2>&1 || { echo "pmc pass $i failed"; tail -20 $OUT/p$i.log; exit 1; }
 done
 python3 $R/tools/pmc_summary.py $OUT | tee $OUT/pmc_summary.txt
+# per-dispatch CSVs can pass gpurun's 64 MiB merge-back limit: keep the summary only
+find $OUT -name '*.csv' -delete
