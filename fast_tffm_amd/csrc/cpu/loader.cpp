@@ -4,6 +4,7 @@
 #include <cerrno>
 #include <cstring>
 #include <memory>
+#include <omp.h>
 #include <random>
 #include <stdexcept>
 
@@ -34,9 +35,12 @@ void split_lines(const MappedFile& f, std::vector<Span>& out) {
   }
 }
 
-// A window entry of the text path: a line (+ its weight line).
+// A window entry of the text path (8 bytes: the window is shuffled in place, B random swaps per
+// batch over 4.5 B entries, so it pays to keep it cache-sized): the line's file visit (index
+// into the epoch's span tables) and its line number there; the spans are looked up only for the
+// chosen lines, by the assembling threads.
 struct Item {
-  Span line, weight;
+  uint32_t f, l;
 };
 
 // A window entry of the binary path (16 bytes: the window is shuffled in place, so it
@@ -48,15 +52,29 @@ struct BinItem {
   uint32_t file;
 };
 
+// Uniform integer in [0, range) from one 64-bit draw (multiply-high, no division: the partial
+// Fisher-Yates below takes one per drawn line, B per batch on the loader's single thread).
+template <class R>
+inline uint64_t bounded(R& rng, uint64_t range) {
+  return static_cast<uint64_t>((static_cast<unsigned __int128>(rng()) * range) >> 64);
+}
+
 // Take n entries from the window into `out`: a uniform sample moved to the back by a
 // partial Fisher-Yates when shuffling, else the FIFO head.
 template <class T, class R>
 void draw(std::vector<T>& win, size_t& head, size_t n, bool shuffle, R& rng, std::vector<T>& out) {
   if (shuffle) {
+    // the swap partners first (the RNG stream does not depend on the data), then the swaps with
+    // the random partner prefetched 16 swaps ahead: the window is larger than L2, and a swap
+    // waiting on its cache miss was ~30 ns of the loader thread's serial time per drawn line
     const size_t w = win.size();
+    thread_local std::vector<size_t> js;
+    js.resize(n);
+    for (size_t i = 0; i < n; ++i) js[i] = w - 1 - (i + static_cast<size_t>(bounded(rng, w - i)));
+    constexpr size_t kAhead = 16;
     for (size_t i = 0; i < n; ++i) {
-      const size_t j = i + static_cast<size_t>(rng() % (w - i));
-      std::swap(win[w - 1 - i], win[w - 1 - j]);
+      if (i + kAhead < n) __builtin_prefetch(&win[js[i + kAhead]], 1);
+      std::swap(win[w - 1 - i], win[js[i]]);
     }
     out.assign(win.end() - static_cast<std::ptrdiff_t>(n), win.end());
     win.resize(w - n);
@@ -163,9 +181,105 @@ void assemble_binary(const std::vector<BinItem>& its, const BinSet& bs, bool wei
     if (x) throw std::runtime_error("binary CSR cache holds a feature id outside [0, vocabulary_size)");
 }
 
+void copy_err(const char* msg, char* err, int errlen) {
+  if (!err || errlen <= 0) return;
+  std::strncpy(err, msg, static_cast<size_t>(errlen) - 1);
+  err[errlen - 1] = 0;
+}
+
+// ---- C API (loader_api.h) ----
+int api_next(void* h, FmRawView* v, char* err, int errlen) {
+  TextLoader* L = static_cast<TextLoader*>(h);
+  try {
+    auto b = std::make_unique<LoadedBatch>();
+    if (!L->next(*b)) return 0;
+    if (b->slot < 0 && b->line_start.empty()) {
+      copy_err("the loader is not in raw mode", err, errlen);
+      return -2;
+    }
+    v->slot = b->slot;
+    v->epoch = b->epoch;
+    v->count = b->count;
+    if (b->slot >= 0) {
+      const RawSlot& rs = L->options().raw_slots[static_cast<size_t>(b->slot)];
+      v->bytes = rs.bytes;
+      v->line_start = rs.line_start;
+      v->nbytes = static_cast<int64_t>(b->nbytes);
+      v->nlines = static_cast<int64_t>(b->nlines);
+      v->weights = b->weights_in_slot ? rs.weights : (b->weights.empty() ? nullptr : b->weights.data());
+    } else {
+      v->bytes = b->bytes.data();
+      v->line_start = b->line_start.data();
+      v->nbytes = static_cast<int64_t>(b->bytes.size());
+      v->nlines = static_cast<int64_t>(b->line_start.size()) - 1;
+      v->weights = b->weights.empty() ? nullptr : b->weights.data();
+    }
+    v->owner = b.release();
+    return 1;
+  } catch (const ParseError& e) {
+    copy_err(e.what(), err, errlen);
+    return -1;
+  } catch (const std::exception& e) {
+    copy_err(e.what(), err, errlen);
+    return -2;
+  }
+}
+
+void api_done(void* h, FmRawView* v) {
+  TextLoader* L = static_cast<TextLoader*>(h);
+  LoadedBatch* b = static_cast<LoadedBatch*>(v->owner);
+  if (!b) return;
+  if (b->slot >= 0) {
+    try {
+      L->release(b->slot);
+    } catch (const std::exception&) {
+    }
+  }
+  delete b;
+  v->owner = nullptr;
+}
+
 }  // namespace
 
+int TextLoader::api_parse(void* h, const FmRawView* v, FmParsedOut* out, char* err, int errlen) {
+  TextLoader* L = static_cast<TextLoader*>(h);
+  try {
+    const int64_t n = v->nlines;
+    std::vector<const char*> ptrs(static_cast<size_t>(n));
+    std::vector<size_t> lens(static_cast<size_t>(n));
+    for (int64_t i = 0; i < n; ++i) {  // lines are '\n'-terminated in the raw buffer
+      const int64_t s = v->line_start[i], e = v->line_start[i + 1];
+      ptrs[i] = reinterpret_cast<const char*>(v->bytes) + s;
+      lens[i] = static_cast<size_t>(e > s && v->bytes[e - 1] == '\n' ? e - s - 1 : e - s);
+    }
+    Csr32 c;
+    parse_lines32(ptrs.data(), lens.data(), static_cast<size_t>(n), L->o_.vocab_size, L->o_.hash_feature_id,
+                  L->o_.threads, c, &L->api_ws_);
+    if (static_cast<int64_t>(c.ids.size()) > out->cap) return -3;
+    std::memcpy(out->labels, c.labels.data(), 4 * c.labels.size());
+    std::memcpy(out->offsets, c.offsets.data(), 4 * c.offsets.size());
+    if (!c.ids.empty()) std::memcpy(out->ids, c.ids.data(), 4 * c.ids.size());
+    if (c.has_vals && !c.vals.empty()) std::memcpy(out->vals, c.vals.data(), 4 * c.vals.size());
+    out->nnz = static_cast<int64_t>(c.ids.size());
+    out->max_feats = c.max_feats;
+    out->has_vals = c.has_vals ? 1 : 0;
+    return 0;
+  } catch (const ParseError& e) {
+    copy_err(e.what(), err, errlen);
+    return -1;
+  } catch (const std::exception& e) {
+    copy_err(e.what(), err, errlen);
+    return -2;
+  }
+}
+
 TextLoader::TextLoader(LoaderOptions o) : o_(std::move(o)) {
+  api_.version = kFmLoaderApiVersion;
+  api_.handle = this;
+  api_.next = &api_next;
+  api_.done = &api_done;
+  api_.parse = &TextLoader::api_parse;
+  api_.stop = &TextLoader::api_stop;
   if (o_.batch_size < 1) throw std::invalid_argument("batch_size must be >= 1");
   if (!o_.weight_files.empty() && o_.weight_files.size() != o_.files.size())
     throw std::invalid_argument("The numbers of train files and weight files do not match.");
@@ -269,9 +383,9 @@ void TextLoader::run() {
     std::vector<BinItem> bwindow, bchosen;
     std::vector<const char*> ptrs, wptrs;
     std::vector<size_t> lens, wlens;
-    std::vector<Span> lines, wlines;
-    CsrBatch csr;
-    ParseWorkspace pws;  // per-thread parse pieces, reused batch after batch
+    std::vector<Span> rline, rweight;
+    Csr32 csr;
+    Csr32Workspace pws;  // per-thread parse pieces, reused batch after batch
     // Text files stay mapped and their line index is kept across epochs (up to kMaxCachedLines
     // lines in all): re-mapping and re-splitting every file each epoch (page-table faults +
     // a memchr pass over every byte) was most of the loader's per-batch host time.
@@ -279,21 +393,24 @@ void TextLoader::run() {
     size_t cached_lines = 0;
     std::vector<std::unique_ptr<MappedFile>> cmap(2 * nf);
     std::vector<std::vector<Span>> clines(2 * nf);
+    // (a file beyond the cache is mapped and split once per epoch; its spans live in `elines`
+    // until the epoch's batches are built)
     auto file_lines = [&](size_t fi, bool weight, std::vector<std::unique_ptr<MappedFile>>& maps,
-                          std::vector<Span>& scratch) -> const std::vector<Span>& {
+                          std::vector<std::vector<Span>>& elines) -> const std::vector<Span>& {
       const size_t slot = 2 * fi + (weight ? 1 : 0);
       if (cmap[slot]) return clines[slot];
       auto m = std::make_unique<MappedFile>(weight ? o_.weight_files[fi] : o_.files[fi]);
-      split_lines(*m, scratch);
-      if (cached_lines + scratch.size() <= kMaxCachedLines) {
-        cached_lines += scratch.size();
-        clines[slot] = std::move(scratch);
-        scratch = std::vector<Span>();
+      std::vector<Span> sp;
+      split_lines(*m, sp);
+      if (cached_lines + sp.size() <= kMaxCachedLines) {
+        cached_lines += sp.size();
+        clines[slot] = std::move(sp);
         cmap[slot] = std::move(m);
         return clines[slot];
       }
-      maps.push_back(std::move(m));  // (alive until the epoch's batches are parsed)
-      return scratch;
+      maps.push_back(std::move(m));
+      elines.push_back(std::move(sp));
+      return elines.back();
     };
 
     for (int epoch = o_.start_epoch; epoch < o_.num_epochs; ++epoch) {
@@ -317,6 +434,9 @@ void TextLoader::run() {
       bwindow.clear();
       size_t head = 0;  // FIFO start (no-shuffle mode)
       std::vector<std::unique_ptr<MappedFile>> maps;  // alive until the epoch's batches are parsed
+      std::vector<std::vector<Span>> elines;          // spans of the files outside the cache
+      elines.reserve(2 * nf);                         // (no reallocation: references stay valid)
+      std::vector<const Span*> ftab, wtab;            // per file visit: its line / weight spans
 
       // Draw n items from the window (random when shuffling, FIFO otherwise) and build the
       // batch unless it is skipped (resume).
@@ -338,20 +458,34 @@ void TextLoader::run() {
         }
         draw(window, head, n, o_.shuffle, rng, chosen);
         if (count <= skip) return true;
-        ptrs.clear(); lens.clear(); wptrs.clear(); wlens.clear();
-        for (const Item& it : chosen) {
-          ptrs.push_back(it.line.p); lens.push_back(it.line.len);
-          wptrs.push_back(it.weight.p); wlens.push_back(it.weight.len);
-        }
         LoadedBatch b;
+        // the chosen lines' spans, resolved by the thread team (random reads of the span tables)
+        rline.resize(n);
+        if (weighted) rweight.resize(n);
+        {
+          const Item* const ch = chosen.data();
+          const Span* const* const ft = ftab.data();
+          const Span* const* const wt = wtab.data();
+          Span* const rl = rline.data();
+          Span* const rw = weighted ? rweight.data() : nullptr;
+#pragma omp parallel for num_threads(std::max(1, o_.threads)) schedule(static) if (n >= 8192)
+          for (long long i = 0; i < (long long)n; ++i) {
+            if (i + 16 < (long long)n) __builtin_prefetch(&ft[ch[i + 16].f][ch[i + 16].l]);
+            rl[i] = ft[ch[i].f][ch[i].l];
+            if (rw) rw[i] = wt[ch[i].f][ch[i].l];
+          }
+        }
+        const Span* const rl = rline.data();
+        const Span* const rw = weighted ? rweight.data() : nullptr;
         if (o_.raw) {
-          // offsets first, then the line copies in parallel (one thread copying ~15 MB of
-          // 300-byte lines per 50k-line batch capped the GPU-tokenizer path near 1e7 ex/s);
-          // into a caller's (pinned) slot when one is configured and the batch fits
+          // into a caller's (page-locked) slot when one is configured and the batch fits; the
+          // line offsets, the copies and the weights are all built by the thread team (a serial
+          // pass over 50k lines + strtof per weight line capped this path near 2e7 ex/s)
           size_t total = 0;
-          for (size_t i = 0; i < n; ++i) total += lens[i] + 1;
+          for (size_t i = 0; i < n; ++i) total += rl[i].len + 1;
           int64_t* ls = nullptr;
           uint8_t* dst = nullptr;
+          float* wdst = nullptr;
           if (!o_.raw_slots.empty()) {
             const int s = acquire_slot();
             if (s < 0) return false;  // stopped
@@ -360,6 +494,10 @@ void TextLoader::run() {
               b.slot = s;
               ls = rs.line_start;
               dst = rs.bytes;
+              if (weighted && rs.weights && n <= rs.w_cap) {
+                wdst = rs.weights;
+                b.weights_in_slot = true;
+              }
             } else {
               release(s);
             }
@@ -370,51 +508,81 @@ void TextLoader::run() {
             ls = b.line_start.data();
             dst = b.bytes.data();
           }
-          size_t off = 0;
-          for (size_t i = 0; i < n; ++i) {
-            ls[i] = static_cast<int64_t>(off);
-            off += lens[i] + 1;
-          }
-          ls[n] = static_cast<int64_t>(off);
-          b.nbytes = off;
-          b.nlines = n;
-#pragma omp parallel for num_threads(std::max(1, o_.threads)) schedule(static, 1024) if (n >= 4096)
-          for (long long i = 0; i < (long long)n; ++i) {
-            std::memcpy(dst + ls[i], ptrs[i], lens[i]);
-            dst[ls[i] + lens[i]] = '\n';
-          }
-          if (weighted) {
+          if (weighted && !wdst) {
             b.weights.resize(n);
-            parse_floats(wptrs.data(), wlens.data(), n, b.weights.data());
+            wdst = b.weights.data();
           }
+          const int T = static_cast<int>(std::max<size_t>(1, std::min<size_t>(std::max(o_.threads, 1), n / 2048)));
+          std::vector<size_t> part(static_cast<size_t>(T) + 1, 0);
+          std::vector<size_t> werr(static_cast<size_t>(T), SIZE_MAX);
+#pragma omp parallel num_threads(T)
+          {
+            const int t = omp_get_thread_num(), nt = omp_get_num_threads();
+            const size_t i0 = n * t / nt, i1 = n * (t + 1) / nt;
+            size_t sum = 0;
+            for (size_t i = i0; i < i1; ++i) sum += rl[i].len + 1;
+            part[t + 1] = sum;
+#pragma omp barrier
+#pragma omp single
+            for (int k = 0; k < nt; ++k) part[k + 1] += part[k];
+            size_t off = part[t];
+            for (size_t i = i0; i < i1; ++i) {
+              if (i + 8 < i1) __builtin_prefetch(rl[i + 8].p);
+              const uint32_t len = rl[i].len;
+              ls[i] = static_cast<int64_t>(off);
+              std::memcpy(dst + off, rl[i].p, len);
+              dst[off + len] = '\n';
+              off += len + 1;
+            }
+            if (wdst) {
+              std::string scratch;
+              for (size_t i = i0; i < i1; ++i) {
+                try {
+                  if (i + 8 < i1) __builtin_prefetch(rw[i + 8].p);
+                  wdst[i] = parse_float_line(rw[i].p, rw[i].len, scratch);
+                } catch (const ParseError&) {
+                  werr[t] = i;
+                  break;
+                }
+              }
+            }
+          }
+          ls[n] = static_cast<int64_t>(total);
+          for (size_t t = 0; t < werr.size(); ++t)
+            if (werr[t] != SIZE_MAX) {  // the first bad weight line, with parse_floats' message
+              std::string scratch;
+              if (b.slot >= 0) release(b.slot);
+              parse_float_line(rw[werr[t]].p, rw[werr[t]].len, scratch);
+            }
+          b.nbytes = total;
+          b.nlines = n;
           b.epoch = epoch;
           b.count = count;
           return push(std::move(b));
         }
-        parse_lines(ptrs.data(), lens.data(), ptrs.size(), o_.vocab_size, o_.hash_feature_id, o_.threads, csr,
-                    &pws);
-        const size_t nb = csr.labels.size(), nnz = csr.ids.size();
-        b.labels = std::move(csr.labels);
-        b.offsets.resize(nb + 1);
-        b.offsets[0] = 0;
-        int mf = 0;
-        for (size_t i = 0; i < nb; ++i) {
-          b.offsets[i + 1] = b.offsets[i] + csr.sizes[i];
-          mf = std::max(mf, csr.sizes[i]);
+        ptrs.resize(n); lens.resize(n);
+        for (size_t i = 0; i < n; ++i) {
+          ptrs[i] = rl[i].p;
+          lens[i] = rl[i].len;
         }
-        b.max_feats = mf;
-        b.ids.resize(nnz);
-        for (size_t i = 0; i < nnz; ++i) b.ids[i] = static_cast<int32_t>(csr.ids[i]);  // ids < vocab < 2^31
-        bool unit = true;
-        for (size_t i = 0; i < nnz && unit; ++i) unit = csr.vals[i] == 1.f;
-        if (!unit) b.vals = std::move(csr.vals);
+        parse_lines32(ptrs.data(), lens.data(), n, o_.vocab_size, o_.hash_feature_id, o_.threads, csr, &pws);
+        b.labels = std::move(csr.labels);
+        b.offsets = std::move(csr.offsets);
+        b.ids = std::move(csr.ids);
+        if (csr.has_vals) b.vals = std::move(csr.vals);
+        b.max_feats = csr.max_feats;
         if (weighted) {
-          b.weights.resize(nb);
-          parse_floats(wptrs.data(), wlens.data(), nb, b.weights.data());
+          wptrs.resize(n); wlens.resize(n);
+          for (size_t i = 0; i < n; ++i) {
+            wptrs[i] = rw[i].p;
+            wlens[i] = rw[i].len;
+          }
+          b.weights.resize(n);
+          parse_floats(wptrs.data(), wlens.data(), n, b.weights.data(), o_.threads);
         }
         b.epoch = epoch;
         b.count = count;
-        csr = CsrBatch();
+        csr = Csr32();
         return push(std::move(b));
       };
 
@@ -433,15 +601,19 @@ void TextLoader::run() {
           if (stop_) return;
           continue;
         }
-        const std::vector<Span>& fl = file_lines(fi, false, maps, lines);
-        const std::vector<Span>* wl = weighted ? &file_lines(fi, true, maps, wlines) : nullptr;
+        const std::vector<Span>& fl = file_lines(fi, false, maps, elines);
+        const std::vector<Span>* wl = weighted ? &file_lines(fi, true, maps, elines) : nullptr;
         if (wl && wl->size() != fl.size())
           throw std::runtime_error(o_.weight_files[fi] + ": " + std::to_string(wl->size()) + " lines but " +
                                    o_.files[fi] + " has " + std::to_string(fl.size()));
+        if (fl.size() >= (size_t(1) << 32)) throw std::runtime_error(o_.files[fi] + ": more than 2^32 lines");
+        const uint32_t fid = static_cast<uint32_t>(ftab.size());
+        ftab.push_back(fl.data());
+        wtab.push_back(wl ? wl->data() : nullptr);
         const size_t step = line_shard ? static_cast<size_t>(o_.world) : 1;
         for (size_t i = line_shard ? static_cast<size_t>(o_.rank) : 0; i < fl.size(); i += step) {
           if (fl[i].len == 0) continue;
-          window.push_back({fl[i], wl ? (*wl)[i] : Span{nullptr, 0}});
+          window.push_back({fid, static_cast<uint32_t>(i)});
           if (window.size() - head >= cap) {
             if (!emit(static_cast<size_t>(B))) return;
           }

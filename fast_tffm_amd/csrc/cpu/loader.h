@@ -39,6 +39,7 @@
 #include <thread>
 #include <vector>
 
+#include "../loader_api.h"
 #include "parser.h"
 
 namespace fm {
@@ -51,6 +52,8 @@ struct RawSlot {
   size_t bytes_cap = 0;
   int64_t* line_start = nullptr;
   size_t ls_cap = 0;          // entries (lines + 1)
+  float* weights = nullptr;   // optional: the batch's weights are parsed straight into it
+  size_t w_cap = 0;
 };
 
 struct LoaderOptions {
@@ -87,8 +90,10 @@ struct LoadedBatch {
   std::vector<int64_t> rows;
   bool has_vals = false;
   int max_feats = 0;
-  // raw mode into a RawSlot: its index, bytes and lines (bytes / line_start above stay empty)
+  // raw mode into a RawSlot: its index, bytes and lines (bytes / line_start above stay empty;
+  // weights too when the slot has a weights buffer: weights_in_slot)
   int slot = -1;
+  bool weights_in_slot = false;
   size_t nbytes = 0, nlines = 0;
   int epoch = 0;
   int64_t count = 0;              // batches of this epoch consumed after this one
@@ -111,7 +116,16 @@ class TextLoader {
   void close();
   // Raw slots: hand slot `s` (of a batch returned by next()) back to the producer.
   void release(int slot);
+  // C function table over this loader (loader_api.h) for a native consumer in another module
+  // (the GPU feeder, hip/feeder.hip); valid while the loader lives.
+  const FmLoaderApi* c_api() { return &api_; }
+  const LoaderOptions& options() const { return o_; }
 
+ private:
+  static int api_parse(void* h, const FmRawView* v, FmParsedOut* out, char* err, int errlen);
+  static void api_stop(void* h) { static_cast<TextLoader*>(h)->close(); }
+
+ public:
  private:
   void run();
   bool push(LoadedBatch&& b);
@@ -129,6 +143,8 @@ class TextLoader {
   bool failed_ = false, parse_error_ = false;
   std::string error_;
   std::atomic<float> fill_{0.f};
+  FmLoaderApi api_{};
+  Csr32Workspace api_ws_;     // CPU parses requested through api_ (one consumer thread)
 };
 
 }  // namespace fm

@@ -209,11 +209,16 @@ PYBIND11_MODULE(_fm_cpu, m) {
              o.num_epochs = num_epochs; o.seed = seed; o.threads = threads; o.rank = rank; o.world = world;
              o.queue_size = queue_size; o.start_epoch = start_epoch; o.skip_batches = skip_batches; o.raw = raw;
              o.binary = binary; o.rows = rows;
-             for (const auto& s : raw_slots) {  // [bytes ptr, bytes cap, line_start ptr, line_start entries]
-               if (s.size() != 4 || !s[0] || !s[2]) throw std::invalid_argument("raw slot: [bytes, cap, ls, cap]");
+             for (const auto& s : raw_slots) {
+               // [bytes ptr, bytes cap, line_start ptr, line_start entries (, weights ptr, weights cap)]
+               if ((s.size() != 4 && s.size() != 6) || !s[0] || !s[2])
+                 throw std::invalid_argument("raw slot: [bytes, cap, ls, cap(, weights, cap)]");
                fm::RawSlot r;
                r.bytes = reinterpret_cast<uint8_t*>(s[0]); r.bytes_cap = s[1];
                r.line_start = reinterpret_cast<int64_t*>(s[2]); r.ls_cap = s[3];
+               if (s.size() == 6) {
+                 r.weights = reinterpret_cast<float*>(s[4]); r.w_cap = s[5];
+               }
                o.raw_slots.push_back(r);
              }
              return new fm::TextLoader(std::move(o));
@@ -239,6 +244,10 @@ PYBIND11_MODULE(_fm_cpu, m) {
                                      b.max_feats, b.epoch, b.count);
              }
              if (b.slot >= 0) {  // raw mode into a slot: (slot, nbytes, nlines, weights | None, epoch, count)
+               if (b.weights_in_slot) {
+                 const float* sw = L.options().raw_slots[static_cast<size_t>(b.slot)].weights;
+                 b.weights.assign(sw, sw + b.nlines);
+               }
                py::object w = b.weights.empty() ? py::object(py::none()) : py::object(to_numpy(std::move(b.weights)));
                return py::make_tuple(b.slot, b.nbytes, b.nlines, w, b.epoch, b.count);
              }
@@ -252,6 +261,8 @@ PYBIND11_MODULE(_fm_cpu, m) {
              return py::make_tuple(to_numpy(std::move(b.labels)), to_numpy(std::move(b.offsets)),
                                    to_numpy(std::move(b.ids)), vals, w, b.max_feats, b.epoch, b.count);
            })
+      // address of the loader's C function table (loader_api.h) for the GPU feeder (_fm_hip)
+      .def("c_api", [](fm::TextLoader& L) { return reinterpret_cast<std::uintptr_t>(L.c_api()); })
       .def("queued", &fm::TextLoader::queued)
       .def("release", &fm::TextLoader::release, py::arg("slot"))
       .def("window_fill", &fm::TextLoader::window_fill)

@@ -4,6 +4,7 @@
 #include <cerrno>
 #include <cstdlib>
 #include <cstring>
+#include <omp.h>
 #include <thread>
 
 #include "../hash64.h"
@@ -50,18 +51,79 @@ inline bool fast_parse_small_int(const char* p, const char** end, float* out) {
   return true;
 }
 
+// Fast path for plain decimals ("0.25", "-3", "7.", ".5", "2") read from [p, lim) (a char at
+// or past lim reads as '\0'): the digits form an integer m < 2^24 with at most 10 of them after
+// the point, so m and 10^f are exact floats and ONE IEEE division gives the correctly rounded
+// value -- bit-identical to strtof.  The number must be followed by a character strtof cannot
+// continue with (' ', ':', '\0', '\t', '\r', '\n'); anything else -- exponents, longer mantissas,
+// hex, inf / nan, leading blanks -- returns false and the caller uses strtof.
+constexpr float kPow10f[11] = {1e0f, 1e1f, 1e2f, 1e3f, 1e4f, 1e5f, 1e6f, 1e7f, 1e8f, 1e9f, 1e10f};
+
+inline bool fast_parse_decimal(const char* p, const char* lim, const char** end, float* out) {
+  auto at = [&](const char* q) -> char { return q < lim ? *q : '\0'; };
+  const char* q = p;
+  bool neg = false;
+  if (at(q) == '-' || at(q) == '+') {
+    neg = at(q) == '-';
+    ++q;
+  }
+  uint32_t m = 0;
+  int digits = 0, frac = -1;
+  for (;; ++q) {
+    const char c = at(q);
+    if (c >= '0' && c <= '9') {
+      m = m * 10 + static_cast<uint32_t>(c - '0');
+      if (m >= (1u << 24)) return false;
+      ++digits;
+      if (frac >= 0 && ++frac > 10) return false;
+    } else if (c == '.' && frac < 0) {
+      frac = 0;
+    } else {
+      break;
+    }
+  }
+  if (digits == 0) return false;
+  const char c = at(q);
+  if (!(c == ' ' || c == ':' || c == '\0' || c == '\t' || c == '\r' || c == '\n')) return false;
+  float v = static_cast<float>(m);
+  if (frac > 0) v = v / kPow10f[frac];
+  *out = neg ? -v : v;
+  *end = q;
+  return true;
+}
+
+// One line into (labels, sizes, ids, vals); IdVec holds int64 (CsrBatch) or int32 (Csr32) ids.
+template <class IdVec>
+void parse_line_into(const char* s, size_t len, int64_t vocab_size, bool hash_feature_id, std::vector<float>& labels,
+                     std::vector<int32_t>& sizes, IdVec& ids, std::vector<float>& vals, std::string& scratch);
+
 }  // namespace
 
 void parse_line(const char* s, size_t len, int64_t vocab_size, bool hash_feature_id, CsrBatch& out,
                 std::string& scratch) {
+  parse_line_into(s, len, vocab_size, hash_feature_id, out.labels, out.sizes, out.ids, out.vals, scratch);
+}
+
+namespace {
+
+template <class IdVec>
+void parse_line_into(const char* s, size_t len, int64_t vocab_size, bool hash_feature_id, std::vector<float>& labels,
+                     std::vector<int32_t>& sizes, IdVec& ids, std::vector<float>& vals, std::string& scratch) {
   scratch.assign(s, len);  // NUL-terminated private copy: strto* never read past the line
   const char* line = scratch.c_str();
+  const char* const lim = line + len;
   const char* p = line;
   char* nextptr = nullptr;
-  float fv = strtof(p, &nextptr);
-  if (p == nextptr) throw ParseError(std::string("Label could not be read in example: ") + line);
-  out.labels.push_back(fv);
-  p = nextptr;
+  float fv;
+  const char* lend = nullptr;
+  if (fast_parse_decimal(p, lim, &lend, &fv)) {
+    p = lend;
+  } else {
+    fv = strtof(p, &nextptr);
+    if (p == nextptr) throw ParseError(std::string("Label could not be read in example: ") + line);
+    p = nextptr;
+  }
+  labels.push_back(fv);
   int32_t cnt = 0;
   for (; *p != '\0'; ++cnt) {
     if (*p != ' ') throw ParseError(std::string("Invalid format in example: ") + line);
@@ -89,7 +151,7 @@ void parse_line(const char* s, size_t len, int64_t vocab_size, bool hash_feature
     if (*p == ':') {
       p += 1;
       const char* e2 = nullptr;
-      if (!fast_parse_small_int(p, &e2, &fv)) {
+      if (!fast_parse_small_int(p, &e2, &fv) && !fast_parse_decimal(p, lim, &e2, &fv)) {
         fv = strtof(p, &nextptr);
         if (p == nextptr) throw ParseError(std::string("Invalid feature value. ") + line);
         e2 = nextptr;
@@ -98,11 +160,13 @@ void parse_line(const char* s, size_t len, int64_t vocab_size, bool hash_feature
     } else {
       fv = 1.f;
     }
-    out.ids.push_back(ori_id);
-    out.vals.push_back(fv);
+    ids.push_back(static_cast<typename IdVec::value_type>(ori_id));
+    vals.push_back(fv);
   }
-  out.sizes.push_back(cnt);
+  sizes.push_back(cnt);
 }
+
+}  // namespace
 
 void parse_lines(const char* const* ptrs, const size_t* lens, size_t n, int64_t vocab_size,
                  bool hash_feature_id, int threads, CsrBatch& out, ParseWorkspace* ws) {
@@ -176,19 +240,137 @@ void parse_lines(const char* const* ptrs, const size_t* lens, size_t n, int64_t 
   }
 }
 
-void parse_floats(const char* const* ptrs, const size_t* lens, size_t n, float* out) {
-  std::string scratch;
-  for (size_t i = 0; i < n; ++i) {
-    scratch.assign(ptrs[i], lens[i]);
-    const char* p = scratch.c_str();
-    char* e = nullptr;
-    errno = 0;
-    const float v = strtof(p, &e);
-    if (e == p) throw ParseError("StringToNumberOp could not correctly convert string: " + scratch);
-    while (*e == ' ' || *e == '\t' || *e == '\r' || *e == '\n') ++e;
-    if (*e != '\0') throw ParseError("StringToNumberOp could not correctly convert string: " + scratch);
-    out[i] = v;
+void parse_lines32(const char* const* ptrs, const size_t* lens, size_t n, int64_t vocab_size, bool hash_feature_id,
+                   int threads, Csr32& out, Csr32Workspace* ws) {
+  out.labels.resize(n);
+  out.offsets.assign(n + 1, 0);
+  out.ids.clear();
+  out.vals.clear();
+  out.max_feats = 0;
+  out.has_vals = false;
+  if (n == 0) return;
+  Csr32Workspace local;
+  if (!ws) ws = &local;
+  const int T = static_cast<int>(std::max<size_t>(1, std::min<size_t>(std::max(threads, 1), n / 512)));
+  if (ws->parts.size() < static_cast<size_t>(T)) ws->parts.resize(T);
+  std::vector<std::string> errors(T);
+  std::vector<size_t> err_line(T, SIZE_MAX);
+  std::vector<size_t> nz_off(T + 1, 0);
+  std::vector<int> mf(T, 0);
+  std::vector<char> nonunit(T, 0);
+  int nt_used = T;
+  // phase 1: each thread parses a contiguous line range into its own part; phase 2 (after the
+  // barrier and a serial prefix over the parts): each copies its part into place, building the
+  // offsets as it goes -- int32 ids straight from the parser, no pass over the batch on one thread
+#pragma omp parallel num_threads(T)
+  {
+    const int t = omp_get_thread_num(), nt = omp_get_num_threads();
+#pragma omp single
+    nt_used = nt;
+    const size_t b = n * t / nt, e = n * (t + 1) / nt;
+    Csr32Workspace::Part& o = ws->parts[t];
+    o.labels.clear(); o.sizes.clear(); o.ids.clear(); o.vals.clear();
+    o.labels.reserve(e - b); o.sizes.reserve(e - b);
+    size_t bytes = 0;
+    for (size_t i = b; i < e; ++i) bytes += lens[i];
+    o.ids.reserve(bytes / 4 + 16); o.vals.reserve(bytes / 4 + 16);
+    std::string scratch;
+    for (size_t i = b; i < e; ++i) {
+      try {
+        parse_line_into(ptrs[i], lens[i], vocab_size, hash_feature_id, o.labels, o.sizes, o.ids, o.vals, scratch);
+      } catch (const ParseError& ex) {
+        errors[t] = ex.what();
+        err_line[t] = i;
+        break;
+      }
+    }
+    nz_off[t + 1] = o.ids.size();
+#pragma omp barrier
+#pragma omp single
+    {
+      for (int k = 0; k < nt; ++k) nz_off[k + 1] += nz_off[k];
+      bool failed = false;
+      for (int k = 0; k < nt; ++k) failed |= err_line[k] != SIZE_MAX;
+      if (!failed) {
+        out.ids.resize(nz_off[nt]);
+        out.vals.resize(nz_off[nt]);
+      }
+    }
+    if (out.ids.size() == nz_off[nt] && err_line[t] == SIZE_MAX) {
+      std::copy(o.labels.begin(), o.labels.end(), out.labels.begin() + b);
+      std::copy(o.ids.begin(), o.ids.end(), out.ids.begin() + nz_off[t]);
+      std::copy(o.vals.begin(), o.vals.end(), out.vals.begin() + nz_off[t]);
+      int32_t off = static_cast<int32_t>(nz_off[t]), m = 0;
+      for (size_t i = b; i < e; ++i) {
+        const int32_t c = o.sizes[i - b];
+        off += c;
+        out.offsets[i + 1] = off;
+        m = std::max(m, c);
+      }
+      mf[t] = m;
+      bool nu = false;
+      for (float v : o.vals) nu |= v != 1.f;
+      nonunit[t] = nu;
+    }
   }
+  // the first failing line in input order (same as a sequential parse)
+  for (int t = 0; t < nt_used; ++t)
+    if (err_line[t] != SIZE_MAX) throw ParseError(errors[t]);
+  for (int t = 0; t < nt_used; ++t) {
+    out.max_feats = std::max(out.max_feats, mf[t]);
+    out.has_vals |= nonunit[t] != 0;
+  }
+  if (!out.has_vals) out.vals.clear();
+}
+
+namespace {
+
+bool is_ws(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\n'; }
+
+}  // namespace
+
+// tf.string_to_number on one weight line: the fast decimal path when the whole line is a plain
+// decimal (+ trailing blanks), else strtof on a NUL-terminated copy.
+float parse_float_line(const char* p, size_t len, std::string& scratch) {
+  const char* const lim = p + len;
+  const char* e = nullptr;
+  float v;
+  if (fast_parse_decimal(p, lim, &e, &v)) {
+    while (e < lim && is_ws(*e)) ++e;
+    if (e == lim) return v;
+  }
+  scratch.assign(p, len);
+  const char* q = scratch.c_str();
+  char* qe = nullptr;
+  errno = 0;
+  v = strtof(q, &qe);
+  if (qe == q) throw ParseError("StringToNumberOp could not correctly convert string: " + scratch);
+  while (is_ws(*qe)) ++qe;
+  if (*qe != '\0') throw ParseError("StringToNumberOp could not correctly convert string: " + scratch);
+  return v;
+}
+
+void parse_floats(const char* const* ptrs, const size_t* lens, size_t n, float* out, int threads) {
+  const int T = static_cast<int>(std::max<size_t>(1, std::min<size_t>(std::max(threads, 1), n / 4096)));
+  std::vector<size_t> err_line(T, SIZE_MAX);
+  std::vector<std::string> errors(T);
+#pragma omp parallel num_threads(T)
+  {
+    const int t = omp_get_thread_num(), nt = omp_get_num_threads();
+    const size_t b = n * t / nt, e = n * (t + 1) / nt;
+    std::string scratch;
+    for (size_t i = b; i < e; ++i) {
+      try {
+        out[i] = parse_float_line(ptrs[i], lens[i], scratch);
+      } catch (const ParseError& ex) {
+        errors[t] = ex.what();
+        err_line[t] = i;
+        break;
+      }
+    }
+  }
+  for (int t = 0; t < T; ++t)
+    if (err_line[t] != SIZE_MAX) throw ParseError(errors[t]);
 }
 
 }  // namespace fm

@@ -49,8 +49,38 @@ struct ParseWorkspace {
 void parse_lines(const char* const* ptrs, const size_t* lens, size_t n, int64_t vocab_size,
                  bool hash_feature_id, int threads, CsrBatch& out, ParseWorkspace* ws = nullptr);
 
+// int32 CSR of a batch (the loader's and the device's layout): labels [n], offsets [n + 1],
+// ids / vals [nnz] (vals empty when every value is 1), max features per line.
+struct Csr32 {
+  std::vector<float> labels;
+  std::vector<int32_t> offsets;
+  std::vector<int32_t> ids;
+  std::vector<float> vals;
+  int max_feats = 0;
+  bool has_vals = false;
+};
+
+struct Csr32Workspace {
+  struct Part {
+    std::vector<float> labels;
+    std::vector<int32_t> sizes;
+    std::vector<int32_t> ids;
+    std::vector<float> vals;
+  };
+  std::vector<Part> parts;
+};
+
+// parse_lines into int32 CSR with an OpenMP team of up to `threads` (ids < vocab_size < 2^31):
+// the per-thread pieces are copied into place and the offsets built in parallel, so no pass over
+// the batch runs on one thread.  Same grammar, results and first-error message as parse_lines.
+void parse_lines32(const char* const* ptrs, const size_t* lens, size_t n, int64_t vocab_size, bool hash_feature_id,
+                   int threads, Csr32& out, Csr32Workspace* ws = nullptr);
+
 // Parse one float per line (weight files; tf.string_to_number semantics:
-// the whole line must be a number, surrounding whitespace allowed).
-void parse_floats(const char* const* ptrs, const size_t* lens, size_t n, float* out);
+// the whole line must be a number, surrounding whitespace allowed), with up to `threads`
+// threads; the first failing line (in order) is reported.
+void parse_floats(const char* const* ptrs, const size_t* lens, size_t n, float* out, int threads = 1);
+// One weight line ([p, p + len), not NUL-terminated) with parse_floats' semantics and message.
+float parse_float_line(const char* p, size_t len, std::string& scratch);
 
 }  // namespace fm

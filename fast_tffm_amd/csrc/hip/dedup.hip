@@ -8,17 +8,18 @@
 //      use (rocPRIM onesweep).  The payload is the occurrence index, or -- when
 //      the caller needs neither the inverse map nor per-occurrence values --
 //      directly the example index, which saves the gather in step 3;
-//   2. run-length encoding in ONE pass over the sorted keys (rle_onepass_kernel):
-//      each 2048-element tile flags "segment head" (key differs from its left
-//      neighbour) and "chunk start" (head, or position % CH == 0), block-scans
-//      the flags, finds its global offsets by a decoupled look-back over the
-//      preceding tiles' published counts (64-bit status words, agent-scope
-//      atomics on both sides: the per-XCD L2s are not coherent), and writes the
-//      unique keys, segment starts, first chunk of each segment, chunk starts,
-//      chunk->segment and the optional inverse map / per-sorted-occurrence
-//      example index and value.  (Round 2 ran this as three kernels -- tile
-//      count, a one-workgroup scan of the tile totals, tile emit -- reading the
-//      keys twice: 42 + 27 + 86 us next to the backward, profiles/r3.)
+//   2. run-length encoding in two passes over the sorted keys: rle_count_kernel
+//      flags "segment head" (key differs from its left neighbour) and "chunk
+//      start" (head, or position % CH == 0) per 2048-element tile and stores
+//      the tile's two counts; rle_emit_kernel re-derives the flags, sums the
+//      counts of the tiles before it (<= a few thousand 8-byte words, L2
+//      resident: no scan kernel, no cross-workgroup wait), block-scans, and
+//      writes the unique keys, segment starts, first chunk of each segment,
+//      chunk starts, chunk->segment and the optional inverse map /
+//      per-sorted-occurrence example index and value.  (A one-pass version with
+//      a decoupled look-back over published tile counts measured 55-131 us next
+//      to the backward vs ~30 here: the first ~2000 tiles start together and
+//      walk back serially over each other's status words, profiles/r3.)
 // Chunks cut every segment at CH-aligned sorted positions, so no chunk is
 // longer than CH and a hot id (tens of thousands of occurrences in Criteo's
 // low-cardinality fields) is spread over many lane groups in the backward.
@@ -29,7 +30,7 @@ namespace fm {
 
 constexpr int kRleItems = 8;                     // elements per thread
 constexpr int kRleTile = kBlock * kRleItems;     // 2048 elements per tile
-constexpr int kMaxTiles = 1 << 20;               // look-back status words per call (n < 2^31)
+constexpr int kMaxTiles = 1 << 20;               // tile-count words per call (n < 2^31)
 
 struct RleArgs {
   int n, CH, ntiles;
@@ -39,8 +40,7 @@ struct RleArgs {
   const int* spay;                // sorted payload (occurrence or example index)
   int ex_shift;                   // > 0: payload / ex_of_occ hold packed codes (example << ex_shift | slot)
   const int* offsets;             // [B+1] CSR offsets (packed codes -> occurrence index)
-  unsigned long long* status;     // [ntiles] look-back words (zeroed before the launch)
-  int* tile_ctr;                  // dynamic tile ids (zeroed before the launch)
+  unsigned long long* tile_cnt;   // [ntiles] heads << 32 | chunk starts (rle_count_kernel)
   int* dense_tmp;                 // dense-row heads as found (unordered), dense_cnt of them
   int* dense_cnt;
   int dense_cap;
@@ -134,26 +134,40 @@ __device__ inline void block_excl_scan(const unsigned (&v)[NC], unsigned (&ex)[N
   __syncthreads();
 }
 
-// Look-back status word of a tile: [flag:2 | heads:31 | chunk starts:31]; flag 1 = the tile's
-// own counts, 2 = inclusive prefix over tiles 0..t.  (A first version read the predecessors one
-// at a time with read-only atomics -- executed at the memory side, ~1-3 us each under load -- and
-// made the one-pass RLE 67 us, slower than the three kernels it replaced; the wave-wide look-back
-// with agent-scope loads reads 64 predecessors per step.)
-constexpr unsigned long long kLbAgg = 1ull << 62, kLbPre = 2ull << 62;
-constexpr unsigned long long kLbMask31 = (1ull << 31) - 1;
-constexpr int kLbSpinLimit = 1 << 18;   // bounded wait: a lost predecessor ends the kernel, not the GPU
-
-__device__ inline unsigned long long lb_pack(unsigned long long flag, unsigned h, unsigned c) {
-  return flag | ((unsigned long long)h << 31) | (unsigned long long)c;
+// Per tile: head and chunk-start counts.  Block 0 also zeroes what the emit pass appends to
+// (dense heads) and the counts no later kernel of the chain writes (no memset launches).
+__global__ __launch_bounds__(kBlock) void rle_count_kernel(RleArgs a) {
+  const int tile = blockIdx.x;
+  Rle8 r;
+  rle_flags8(a, tile * kRleTile + threadIdx.x * kRleItems, r);
+  unsigned v[2] = {0u, 0u}, ex[2], tot[2];
+#pragma unroll
+  for (int q = 0; q < kRleItems; ++q) {
+    v[0] += r.hd[q];
+    v[1] += r.cs[q];
+  }
+  block_excl_scan<2>(v, ex, tot);
+  if (threadIdx.x == 0) {
+    a.tile_cnt[tile] = ((unsigned long long)tot[0] << 32) | tot[1];
+    if (tile == 0) {
+      *a.dense_cnt = 0;
+      a.counts[3] = 0;
+      a.counts[5] = a.counts[6] = a.counts[7] = 0;
+    }
+  }
 }
 
-// One pass: flags, block scan, decoupled look-back for the tile's global offsets, emit.
-__global__ __launch_bounds__(kBlock) void rle_onepass_kernel(RleArgs a) {
-  __shared__ int s_tile;
+__global__ __launch_bounds__(kBlock) void rle_emit_kernel(RleArgs a) {
   __shared__ unsigned s_pre[2];
-  if (threadIdx.x == 0) s_tile = atomicAdd(a.tile_ctr, 1);  // tiles start in id order: no look-back deadlock
-  __syncthreads();
-  const int tile = s_tile;
+  const int tile = blockIdx.x;
+  // global offsets: the counts of tiles 0..tile-1 (written by rle_count_kernel)
+  unsigned pv[2] = {0u, 0u}, pex[2], ptot[2];
+  for (int i = threadIdx.x; i < tile; i += kBlock) {
+    const unsigned long long w = a.tile_cnt[i];
+    pv[0] += (unsigned)(w >> 32);
+    pv[1] += (unsigned)w;
+  }
+  block_excl_scan<2>(pv, pex, ptot);
   const int j0 = tile * kRleTile + threadIdx.x * kRleItems;
   Rle8 r;
   rle_flags8(a, j0, r);
@@ -166,63 +180,18 @@ __global__ __launch_bounds__(kBlock) void rle_onepass_kernel(RleArgs a) {
     v[1] += r.cs[q];
   }
   block_excl_scan<2>(v, ex, tot);
-  // Wave 0: publish this tile's counts, then look back over the predecessors 64 at a time (lane l
-  // reads tile - 1 - l): the nearest inclusive prefix ends the walk, the aggregates in front of it
-  // are summed; a window with an unpublished tile is re-read.  Status words are written with
-  // agent-scope atomics and read with agent-scope loads (L2-served, never a stale L1 line).
-  if (threadIdx.x < kWave) {
-    const int lane = threadIdx.x;
-    unsigned long long* st = a.status;
-    if (lane == 0)
-      __hip_atomic_exchange(&st[tile], lb_pack(tile == 0 ? kLbPre : kLbAgg, tot[0], tot[1]), __ATOMIC_RELAXED,
-                            __HIP_MEMORY_SCOPE_AGENT);
-    unsigned ph = 0, pc = 0;
-    int base = tile - 1;  // next window: tiles base, base - 1, ..., base - 63
-    int spins = 0;
-    while (base >= 0) {
-      const int t = base - lane;
-      const unsigned long long w =
-          t >= 0 ? __hip_atomic_load(&st[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbPre;
-      const unsigned flag = (unsigned)(w >> 62);
-      const uint64_t pre = __ballot(flag == 2);
-      const uint64_t unset = __ballot(flag == 0);
-      // lanes up to (and including) the first prefix; an unset tile before it: wait and re-read
-      const int stop = pre ? __ffsll((long long)pre) - 1 : kWave - 1;
-      const uint64_t need = stop == kWave - 1 ? ~0ull : ((2ull << stop) - 1ull);
-      if (unset & need) {
-        if (++spins > kLbSpinLimit) break;  // (a lost predecessor: give up rather than hang the GPU)
-        __builtin_amdgcn_s_sleep(1);
-        continue;
-      }
-      const bool take = lane <= stop && t >= 0;
-      unsigned h = take ? (unsigned)((w >> 31) & kLbMask31) : 0u;
-      unsigned c = take ? (unsigned)(w & kLbMask31) : 0u;
-#pragma unroll
-      for (int o = kWave / 2; o > 0; o >>= 1) {
-        h += __shfl_xor(h, o, kWave);
-        c += __shfl_xor(c, o, kWave);
-      }
-      ph += h;
-      pc += c;
-      if (pre) break;
-      base -= kWave;
-    }
-    if (lane == 0) {
-      if (tile > 0)
-        __hip_atomic_exchange(&st[tile], lb_pack(kLbPre, ph + tot[0], pc + tot[1]), __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_AGENT);
-      s_pre[0] = ph;
-      s_pre[1] = pc;
-      if (tile == a.ntiles - 1) {  // totals, sentinels; the backward's two counters start at 0
-        const unsigned U = ph + tot[0], C = pc + tot[1];
-        a.counts[0] = (int)U;
-        a.counts[1] = (int)C;
-        a.counts[2] = 0;
-        a.counts[4] = 0;
-        a.seg_start[U] = a.n;
-        a.seg_chunk[U] = (int)C;
-        a.chunk_start[C] = a.n;
-      }
+  if (threadIdx.x == 0) {
+    s_pre[0] = ptot[0];
+    s_pre[1] = ptot[1];
+    if (tile == a.ntiles - 1) {  // totals, sentinels; the backward's two counters start at 0
+      const unsigned U = ptot[0] + tot[0], C = ptot[1] + tot[1];
+      a.counts[0] = (int)U;
+      a.counts[1] = (int)C;
+      a.counts[2] = 0;
+      a.counts[4] = 0;
+      a.seg_start[U] = a.n;
+      a.seg_chunk[U] = (int)C;
+      a.chunk_start[C] = a.n;
     }
   }
   __syncthreads();
@@ -391,7 +360,7 @@ static size_t sort_temp_bytes(int n, hipStream_t st) {
 constexpr int kDenseMinFloor = 32;
 static size_t dense_cap_for(int n) { return (size_t)n / kDenseMinFloor + 1; }
 
-// Workspace layout: [rocprim sort temp | tile_ctr, dense_cnt, status[ntiles] (zeroed per call) | dense_tmp]
+// Workspace layout: [rocprim sort temp | dense_cnt (8 B), tile_cnt[ntiles] | dense_tmp]
 static size_t lb_bytes(int ntiles) { return 8 + 8 * (size_t)ntiles; }
 
 size_t dedup_workspace_bytes(int n) {
@@ -463,9 +432,9 @@ int launch_seg_index(int n_max, const uint32_t* uniq, const int* counts, int shi
 int launch_dedup(const DedupArgs& a, hipStream_t st) {
   // counts[0..3] = U, #chunks, #multi-chunk rows, #dense rows; counts[4] = the backward's
   // hot-row count: both backward counters start at 0 here, on the dedup's stream (off the
-  // compute stream's critical path)
-  (void)hipMemsetAsync(a.counts, 0, 8 * sizeof(int), st);
+  // compute stream's critical path), written by the RLE kernels
   if (a.n <= 0) {
+    (void)hipMemsetAsync(a.counts, 0, 8 * sizeof(int), st);
     (void)hipMemsetAsync(a.seg_start, 0, sizeof(int), st);
     (void)hipMemsetAsync(a.seg_chunk, 0, sizeof(int), st);
     (void)hipMemsetAsync(a.chunk_start, 0, sizeof(int), st);
@@ -479,17 +448,17 @@ int launch_dedup(const DedupArgs& a, hipStream_t st) {
   int* dense_tmp = reinterpret_cast<int*>(lb + align_up(lb_bytes(ntiles)));
   if (tmp + align_up(lb_bytes(ntiles)) + align_up(dense_cap_for(a.n) * sizeof(int)) > a.ws_bytes) return -2;
   if (a.dense_list && a.dense_min > 0 && a.dense_min < kDenseMinFloor) return -8;
-  (void)hipMemsetAsync(lb, 0, lb_bytes(ntiles), st);
 
   size_t sort_bytes = tmp;
   hipError_t e = sort_pairs(a.ws, sort_bytes, a.keys, a.skeys, a.payload, a.spay, a.n, a.end_bit, st);
   if (e != hipSuccess) return (int)e;
   RleArgs r{a.n, a.CH, ntiles, a.dense_list ? a.dense_min : 0, a.dense_list, a.skeys, a.spay, a.ex_shift,
-            a.offsets, reinterpret_cast<unsigned long long*>(lb + 8), reinterpret_cast<int*>(lb),
-            dense_tmp, reinterpret_cast<int*>(lb + 4), (int)dense_cap_for(a.n), a.uniq, a.seg_start,
+            a.offsets, reinterpret_cast<unsigned long long*>(lb + 8), dense_tmp, reinterpret_cast<int*>(lb),
+            (int)dense_cap_for(a.n), a.uniq, a.seg_start,
             a.seg_chunk, a.chunk_start, a.chunk_seg, a.chunk_key, a.counts, a.inv, a.ex_of_occ, a.sorted_ex,
             a.vals, a.sorted_x};
-  hipLaunchKernelGGL(rle_onepass_kernel, dim3(ntiles), dim3(kBlock), 0, st, r);
+  hipLaunchKernelGGL(rle_count_kernel, dim3(ntiles), dim3(kBlock), 0, st, r);
+  hipLaunchKernelGGL(rle_emit_kernel, dim3(ntiles), dim3(kBlock), 0, st, r);
   if (r.dense_min > 0) {
     hipLaunchKernelGGL(dense_select_kernel, dim3(1), dim3(kBlock), 0, st, r);
     hipLaunchKernelGGL(mark_dense_chunks_kernel, dim3(kMaxDense), dim3(kBlock), 0, st, r);

@@ -1,0 +1,337 @@
+// GPU-tokenizer feeder: the host loader's raw batches -> CSR batches on the device, driven by a
+// native thread (no Python, no GIL between file bytes and a ready device batch).
+//
+// The reference's input path is a set of TF queue runners feeding the step (tffm/fm_model.py:
+// 34-126, run_tffm.py:79-81: examples/s is measured file-fed).  Here the host side is the C++
+// loader (csrc/cpu/loader.h: mmap'ed files, shuffle window, lines gathered into page-locked
+// slots by a thread pool) and this feeder owns everything between that and the training step:
+//   * a ring of device slots (input bytes / line starts / weights, tokenizer outputs), allocated
+//     by the caller (torch tensors, so the batches it returns are views of them);
+//   * its own non-blocking HIP stream: per batch, wait for the slot's release event, copy the
+//     raw lines (page-locked -> HBM), launch the tokenizer (parse.hip), copy its 5-int status
+//     back, wait, hand the host slot back to the loader and queue the batch as ready;
+//   * a batch the GPU subset declines (syntax outside it, any malformed line) is parsed by the
+//     loader's CPU parser (the reference grammar and error strings) and uploaded instead;
+//   * release(d, stream) from the consumer records an event on the consumer's stream: the slot
+//     is overwritten only after the work queued there (the step that read the batch) has run.
+// The loader crosses into this module only as a table of C function pointers (loader_api.h).
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../loader_api.h"
+
+namespace fm {
+
+struct FeederSlot {
+  uint8_t* bytes = nullptr;
+  size_t bytes_cap = 0;
+  int64_t* ls = nullptr;
+  size_t ls_cap = 0;            // entries: lines + 1
+  float* weights = nullptr;     // [ls_cap - 1]
+  float* labels = nullptr;      // [ls_cap - 1]
+  int* offsets = nullptr;       // [ls_cap]
+  int* counts = nullptr;        // [ls_cap]
+  int* ids = nullptr;           // [ids_cap]
+  size_t ids_cap = 0;
+  float* vals = nullptr;        // [ids_cap]
+  int* status = nullptr;        // [>= 5]
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  hipEvent_t ready = nullptr;   // the slot's batch is complete
+  hipEvent_t freed = nullptr;   // recorded by release() on the consumer's stream
+  int* info_h = nullptr;        // page-locked [8]: fallback, max_feats, non-unit, -, nnz
+};
+
+struct FeederBatch {
+  int d = -1;
+  int64_t n = 0, nnz = 0;
+  int max_feats = 0;
+  bool has_vals = false, weighted = false;
+  int epoch = 0;
+  int64_t count = 0;
+};
+
+class GpuTextFeeder {
+ public:
+  GpuTextFeeder(const FmLoaderApi* api, int device, long long vocab, bool hash)
+      : api_(api), device_(device), vocab_(vocab), hash_(hash) {
+    if (!api_ || api_->version != kFmLoaderApiVersion) throw std::invalid_argument("loader C API version mismatch");
+  }
+  ~GpuTextFeeder() { close(); }
+  GpuTextFeeder(const GpuTextFeeder&) = delete;
+  GpuTextFeeder& operator=(const GpuTextFeeder&) = delete;
+
+  void add_slot(FeederSlot s) {
+    if (!s.bytes || !s.ls || !s.labels || !s.offsets || !s.counts || !s.ids || !s.vals || !s.status || s.ls_cap < 2)
+      throw std::invalid_argument("feeder slot: null buffer");
+    hip_ok(hipSetDevice(device_), "hipSetDevice");
+    hip_ok(hipEventCreateWithFlags(&s.ready, hipEventDisableTiming), "hipEventCreate");
+    hip_ok(hipEventCreateWithFlags(&s.freed, hipEventDisableTiming), "hipEventCreate");
+    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&s.info_h), 8 * sizeof(int), hipHostMallocDefault), "hipHostMalloc");
+    std::lock_guard<std::mutex> lk(mu_);
+    slots_.push_back(s);
+    free_.push_back(static_cast<int>(slots_.size()) - 1);
+    cv_slot_.notify_one();
+  }
+
+  void start() {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (th_.joinable() || closed_) return;
+    th_ = std::thread([this] { run(); });
+  }
+
+  // 1: *out is the next batch; 0: no more batches; -1: timed out while the producer waits for a
+  // free slot (every slot is held by the consumer); -2: timed out; -3: failed (*err, *parse_err)
+  int next(FeederBatch* out, int timeout_ms, std::string* err, bool* parse_err) {
+    std::unique_lock<std::mutex> lk(mu_);
+    const auto pred = [&] { return !ready_.empty() || done_; };
+    if (timeout_ms < 0) {
+      cv_ready_.wait(lk, pred);
+    } else if (!cv_ready_.wait_for(lk, std::chrono::milliseconds(timeout_ms), pred)) {
+      return starving_ ? -1 : -2;
+    }
+    if (!ready_.empty()) {
+      *out = ready_.front();
+      ready_.pop_front();
+      return 1;
+    }
+    if (failed_) {
+      *err = error_;
+      *parse_err = parse_error_;
+      return -3;
+    }
+    return 0;
+  }
+
+  void release(int d, hipStream_t consumer) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (closed_ || d < 0 || d >= static_cast<int>(slots_.size())) return;
+    for (int s : free_)
+      if (s == d) throw std::logic_error("feeder slot released twice");
+    hip_ok(hipSetDevice(device_), "hipSetDevice");
+    hip_ok(hipEventRecord(slots_[d].freed, consumer), "hipEventRecord");
+    free_.push_back(d);
+    cv_slot_.notify_one();
+  }
+
+  size_t queued() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return ready_.size();
+  }
+  long long fallbacks() const { return fallbacks_.load(); }
+  long long batches() const { return batches_.load(); }
+
+  void close() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (closed_) return;
+      closed_ = stop_ = true;
+    }
+    cv_slot_.notify_all();
+    cv_ready_.notify_all();
+    // the thread may be blocked in the loader's next(): stop the loader first
+    api_->stop(api_->handle);
+    if (th_.joinable()) th_.join();
+    if (st_) {
+      (void)hipStreamSynchronize(st_);
+      (void)hipStreamDestroy(st_);
+      st_ = nullptr;
+    }
+    for (FeederSlot& s : slots_) {
+      if (s.ready) (void)hipEventDestroy(s.ready);
+      if (s.freed) (void)hipEventDestroy(s.freed);
+      if (s.info_h) (void)hipHostFree(s.info_h);
+      s.ready = s.freed = nullptr;
+      s.info_h = nullptr;
+    }
+  }
+
+ private:
+  static void hip_ok(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+  }
+
+  int acquire() {
+    std::unique_lock<std::mutex> lk(mu_);
+    starving_ = free_.empty();
+    cv_slot_.wait(lk, [&] { return stop_ || !free_.empty(); });
+    starving_ = false;
+    if (stop_) return -1;
+    const int d = free_.front();
+    free_.pop_front();
+    return d;
+  }
+
+  void give_back(int d) {
+    std::lock_guard<std::mutex> lk(mu_);
+    free_.push_front(d);
+  }
+
+  void publish(const FeederBatch& b) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      ready_.push_back(b);
+    }
+    batches_.fetch_add(1);
+    cv_ready_.notify_one();
+  }
+
+  void fail(const std::string& msg, bool parse) {
+    std::lock_guard<std::mutex> lk(mu_);
+    failed_ = true;
+    parse_error_ = parse;
+    error_ = msg;
+  }
+
+  // CPU parse of a raw batch (declined by the tokenizer, or larger than the slot) into slot d
+  bool cpu_parse(const FeederSlot& s, const FmRawView& v, FeederBatch& b) {
+    const int64_t n = v.nlines;
+    if (static_cast<size_t>(n) + 1 > s.ls_cap) {
+      fail("batch of " + std::to_string(n) + " lines exceeds the feeder's slots", false);
+      return false;
+    }
+    const int64_t cap = static_cast<int64_t>(v.nbytes) / 2 + n + 1;
+    h_labels_.resize(n);
+    h_offsets_.resize(n + 1);
+    h_ids_.resize(cap);
+    h_vals_.resize(cap);
+    FmParsedOut o{h_labels_.data(), h_offsets_.data(), h_ids_.data(), h_vals_.data(), cap, 0, 0, 0};
+    char err[4096];
+    err[0] = 0;
+    const int r = api_->parse(api_->handle, &v, &o, err, sizeof(err));
+    if (r != 0) {
+      fail(r == -1 ? std::string(err) : std::string("CPU parse of a raw batch failed: ") + err, r == -1);
+      return false;
+    }
+    if (static_cast<size_t>(o.nnz) > s.ids_cap) {
+      fail("batch of " + std::to_string(o.nnz) + " features exceeds the feeder's slots", false);
+      return false;
+    }
+    hip_ok(hipStreamWaitEvent(st_, s.freed, 0), "hipStreamWaitEvent");
+    hip_ok(hipMemcpyAsync(s.labels, o.labels, 4 * n, hipMemcpyHostToDevice, st_), "H2D");
+    hip_ok(hipMemcpyAsync(s.offsets, o.offsets, 4 * (n + 1), hipMemcpyHostToDevice, st_), "H2D");
+    if (o.nnz > 0) hip_ok(hipMemcpyAsync(s.ids, o.ids, 4 * o.nnz, hipMemcpyHostToDevice, st_), "H2D");
+    if (o.has_vals && o.nnz > 0) hip_ok(hipMemcpyAsync(s.vals, o.vals, 4 * o.nnz, hipMemcpyHostToDevice, st_), "H2D");
+    if (v.weights && s.weights) hip_ok(hipMemcpyAsync(s.weights, v.weights, 4 * n, hipMemcpyHostToDevice, st_), "H2D");
+    hip_ok(hipStreamSynchronize(st_), "hipStreamSynchronize");
+    b.nnz = o.nnz;
+    b.max_feats = o.max_feats;
+    b.has_vals = o.has_vals != 0;
+    fallbacks_.fetch_add(1);
+    return true;
+  }
+
+  void run() {
+    try {
+      hip_ok(hipSetDevice(device_), "hipSetDevice");
+      hip_ok(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking), "hipStreamCreate");
+      char err[4096];
+      while (true) {
+        const int d = acquire();
+        if (d < 0) break;
+        FmRawView v{};
+        err[0] = 0;
+        const int r = api_->next(api_->handle, &v, err, sizeof(err));
+        if (r <= 0) {
+          give_back(d);
+          if (r < 0) fail(err, r == -1);
+          break;
+        }
+        FeederSlot s;
+        {
+          std::lock_guard<std::mutex> lk(mu_);
+          s = slots_[d];
+        }
+        FeederBatch b;
+        b.d = d;
+        b.n = v.nlines;
+        b.weighted = v.weights != nullptr;
+        b.epoch = v.epoch;
+        b.count = v.count;
+        const int64_t n = v.nlines;
+        const bool fits = static_cast<size_t>(v.nbytes) <= s.bytes_cap && static_cast<size_t>(n) + 1 <= s.ls_cap &&
+                          n < (int64_t(1) << 31);
+        bool ok = true;
+        if (n == 0) {
+          b.nnz = 0;
+          hip_ok(hipStreamWaitEvent(st_, s.freed, 0), "hipStreamWaitEvent");
+          hip_ok(hipMemsetAsync(s.offsets, 0, sizeof(int), st_), "hipMemsetAsync");
+          hip_ok(hipStreamSynchronize(st_), "hipStreamSynchronize");
+        } else if (!fits) {
+          ok = cpu_parse(s, v, b);
+        } else {
+          hip_ok(hipStreamWaitEvent(st_, s.freed, 0), "hipStreamWaitEvent");
+          hip_ok(hipMemcpyAsync(s.bytes, v.bytes, v.nbytes, hipMemcpyHostToDevice, st_), "H2D");
+          hip_ok(hipMemcpyAsync(s.ls, v.line_start, 8 * (n + 1), hipMemcpyHostToDevice, st_), "H2D");
+          if (v.weights && s.weights)
+            hip_ok(hipMemcpyAsync(s.weights, v.weights, 4 * n, hipMemcpyHostToDevice, st_), "H2D");
+          ParseArgs a{};
+          a.buf = reinterpret_cast<const char*>(s.bytes);
+          a.line_start = reinterpret_cast<const long long*>(s.ls);
+          a.n = static_cast<int>(n);
+          a.vocab = vocab_;
+          a.hash = hash_ ? 1 : 0;
+          a.require_vals = 0;
+          a.counts = s.counts;
+          a.labels = s.labels;
+          a.ids = s.ids;
+          a.vals = s.vals;
+          a.status = s.status;
+          const int pr = launch_parse(a, s.ws, s.ws_bytes, s.offsets, st_);
+          if (pr != 0) throw std::runtime_error("GPU tokenizer launch failed: " + std::to_string(pr));
+          hip_ok(hipMemcpyAsync(s.info_h, s.status, 4 * sizeof(int), hipMemcpyDeviceToHost, st_), "D2H");
+          hip_ok(hipMemcpyAsync(s.info_h + 4, s.offsets + n, sizeof(int), hipMemcpyDeviceToHost, st_), "D2H");
+          hip_ok(hipEventRecord(s.ready, st_), "hipEventRecord");
+          hip_ok(hipEventSynchronize(s.ready), "hipEventSynchronize");
+          if (s.info_h[0]) {
+            ok = cpu_parse(s, v, b);  // syntax outside the GPU subset, or an error to report exactly
+          } else {
+            b.nnz = s.info_h[4];
+            b.max_feats = s.info_h[1];
+            b.has_vals = s.info_h[2] != 0;
+          }
+        }
+        api_->done(api_->handle, &v);  // the host bytes are on the device (or parsed): slot back to the loader
+        if (!ok) {
+          give_back(d);
+          break;
+        }
+        publish(b);
+      }
+    } catch (const std::exception& e) {
+      fail(e.what(), false);
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      done_ = true;
+    }
+    cv_ready_.notify_all();
+  }
+
+  const FmLoaderApi* api_;
+  int device_;
+  long long vocab_;
+  bool hash_;
+  hipStream_t st_ = nullptr;
+  std::deque<FeederSlot> slots_;  // (guarded by mu_; the thread works on copies)
+  std::deque<int> free_;
+  std::deque<FeederBatch> ready_;
+  std::mutex mu_;
+  std::condition_variable cv_slot_, cv_ready_;
+  std::thread th_;
+  bool stop_ = false, closed_ = false, done_ = false, starving_ = false;
+  bool failed_ = false, parse_error_ = false;
+  std::string error_;
+  std::atomic<long long> fallbacks_{0}, batches_{0};
+  std::vector<float> h_labels_, h_vals_;
+  std::vector<int32_t> h_offsets_, h_ids_;
+};
+
+}  // namespace fm

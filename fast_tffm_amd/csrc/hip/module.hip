@@ -28,6 +28,7 @@ using u64 = std::uintptr_t;
 #include "init.hip"
 #include "parse.hip"
 #include "batch_gather.hip"
+#include "feeder.hip"
 
 namespace {
 
@@ -404,6 +405,53 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("buf"), py::arg("line_start"), py::arg("n"), py::arg("vocab"), py::arg("hash"), py::arg("counts"),
       py::arg("offsets"), py::arg("labels"), py::arg("ids"), py::arg("vals"), py::arg("status"), py::arg("ws"),
       py::arg("ws_bytes"), py::arg("stream"), py::arg("require_vals") = 0);
+
+  // GPU-tokenizer feeder (feeder.hip): a native thread from the loader's raw batches to device CSR
+  py::class_<fm::GpuTextFeeder>(m, "GpuTextFeeder")
+      .def(py::init([](u64 api, int device, long long vocab, bool hash) {
+             return new fm::GpuTextFeeder(P<const FmLoaderApi>(api), device, vocab, hash);
+           }),
+           py::arg("api"), py::arg("device"), py::arg("vocab"), py::arg("hash"))
+      // [bytes, bytes cap, ls, ls entries, weights, labels, offsets, counts, ids, ids cap, vals, status, ws, ws bytes]
+      .def("add_slot",
+           [](fm::GpuTextFeeder& F, std::vector<u64> p) {
+             if (p.size() != 14) throw std::invalid_argument("feeder slot: 14 entries");
+             fm::FeederSlot s;
+             s.bytes = P<uint8_t>(p[0]); s.bytes_cap = p[1]; s.ls = P<int64_t>(p[2]); s.ls_cap = p[3];
+             s.weights = P<float>(p[4]); s.labels = P<float>(p[5]); s.offsets = P<int>(p[6]); s.counts = P<int>(p[7]);
+             s.ids = P<int>(p[8]); s.ids_cap = p[9]; s.vals = P<float>(p[10]); s.status = P<int>(p[11]);
+             s.ws = P<void>(p[12]); s.ws_bytes = p[13];
+             F.add_slot(s);
+           })
+      .def("start", &fm::GpuTextFeeder::start)
+      // -> (slot, n, nnz, max_feats, has_vals, weighted, epoch, count) | None at the end | -1 (timed out,
+      //    the feeder waits for a free slot) | -2 (timed out) | ("error", is_parse_error, message)
+      .def("next",
+           [](fm::GpuTextFeeder& F, int timeout_ms) -> py::object {
+             fm::FeederBatch b;
+             std::string err;
+             bool perr = false;
+             int r;
+             {
+               py::gil_scoped_release nogil;
+               r = F.next(&b, timeout_ms, &err, &perr);
+             }
+             if (r == 1)
+               return py::make_tuple(b.d, b.n, b.nnz, b.max_feats, b.has_vals, b.weighted, b.epoch, b.count);
+             if (r == 0) return py::none();
+             if (r == -3) return py::make_tuple(std::string("error"), perr, err);
+             return py::int_(r);
+           },
+           py::arg("timeout_ms") = -1)
+      .def("release", [](fm::GpuTextFeeder& F, int d, u64 stream) { F.release(d, S(stream)); }, py::arg("slot"),
+           py::arg("stream"))
+      .def("queued", &fm::GpuTextFeeder::queued)
+      .def("fallbacks", &fm::GpuTextFeeder::fallbacks)
+      .def("batches", &fm::GpuTextFeeder::batches)
+      .def("close", [](fm::GpuTextFeeder& F) {
+        py::gil_scoped_release nogil;
+        F.close();
+      });
 
   m.def(
       "batch_gather",

@@ -1,0 +1,58 @@
+// C ABI between the host loader (module _fm_cpu, csrc/cpu/loader.h) and the GPU feeder
+// (module _fm_hip, csrc/hip/feeder.hip).
+//
+// The two extension modules are built by different compilers and keep their C++ symbols
+// hidden, so no C++ object crosses between them: the loader hands out a table of plain C
+// function pointers plus an opaque handle (TextLoader::c_api(), exposed to Python as an
+// integer address), and the feeder's thread calls through it without ever touching Python.
+// The table lives inside the TextLoader and is valid until that loader is destroyed; the
+// Python side keeps the loader alive for as long as a feeder uses it.
+#pragma once
+#include <cstdint>
+
+extern "C" {
+
+// One raw (GPU-tokenizer) batch as the loader produced it: '\n'-terminated lines in page-locked
+// memory when it came from one of the caller's slots (`slot` >= 0), else in a heap buffer owned
+// by the loader (`owner`).  Valid until handed back with FmLoaderApi::done.
+struct FmRawView {
+  int32_t slot;                 // host slot index, -1 for a heap batch
+  int32_t epoch;
+  int64_t count;                // batches of `epoch` consumed once this one is
+  const uint8_t* bytes;
+  const int64_t* line_start;    // [nlines + 1]
+  const float* weights;         // [nlines] or null (no weight files)
+  int64_t nbytes, nlines;
+  void* owner;                  // loader-private (heap batch)
+};
+
+// Host CSR written by FmLoaderApi::parse into caller-owned arrays.
+struct FmParsedOut {
+  float* labels;                // [nlines]
+  int32_t* offsets;             // [nlines + 1]
+  int32_t* ids;                 // [cap]
+  float* vals;                  // [cap]
+  int64_t cap;
+  int64_t nnz;                  // out
+  int32_t max_feats;            // out
+  int32_t has_vals;             // out: some value != 1
+};
+
+struct FmLoaderApi {
+  int32_t version;              // kFmLoaderApiVersion
+  void* handle;
+  // 1: a batch in *v; 0: no more batches; -1: parse error, -2: other failure (message in err)
+  int (*next)(void* handle, FmRawView* v, char* err, int errlen);
+  // the consumer is done with v's host memory (its slot goes back to the loader)
+  void (*done)(void* handle, FmRawView* v);
+  // the CPU parser (the reference grammar and error strings) over a raw view, with the loader's
+  // thread count: 0 ok, -1 parse error (message in err), -3 output capacity too small
+  int (*parse)(void* handle, const FmRawView* v, FmParsedOut* out, char* err, int errlen);
+  // stop the loader (a consumer blocked in next() returns 0): lets the consumer's own shutdown
+  // join a thread that is waiting for the next batch
+  void (*stop)(void* handle);
+};
+
+}  // extern "C"
+
+constexpr int32_t kFmLoaderApiVersion = 1;

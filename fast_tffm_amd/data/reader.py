@@ -27,6 +27,7 @@ from __future__ import annotations
 import queue
 import random
 import threading
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
@@ -255,7 +256,18 @@ class NativeTextReader:
 
             self.dds = DeviceDataset(self.args["files"], device_cache, int(vocab_size), bool(hash_feature_id))
 
+    def close(self) -> None:
+        """Stop the native producer threads (feeder, loader); the iterator ends."""
+        F = getattr(self, "_feeder", None)
+        if F is not None:
+            F.close()
+        if self._loader is not None:
+            self._loader.close()
+
     def queued(self) -> int:
+        F = getattr(self, "_feeder", None)
+        if F is not None:
+            return int(F.queued())
         return self._loader.queued() if self._loader is not None else 0
 
     def window_fill(self) -> float:
@@ -278,12 +290,24 @@ class NativeTextReader:
             except OSError:
                 pass
             nb, nl = int(B * avg * 1.5) + 4096, B + 1
+            self._slot_bytes = nb
             self._slots = [(torch.empty(nb, dtype=torch.uint8, pin_memory=True),
-                            torch.empty(nl, dtype=torch.int64, pin_memory=True))
+                            torch.empty(nl, dtype=torch.int64, pin_memory=True),
+                            torch.empty(B, dtype=torch.float32, pin_memory=True))
                            for _ in range(self.args["queue_size"] + 3)]
-        return [[b.data_ptr(), b.numel(), ls.data_ptr(), ls.numel()] for b, ls in self._slots]
+        return [[b.data_ptr(), b.numel(), ls.data_ptr(), ls.numel(), w.data_ptr(), w.numel()]
+                for b, ls, w in self._slots]
+
+    @property
+    def inline(self) -> bool:
+        """Batches come out complete and on the device (GPU tokenizer fed by the C++ feeder thread):
+        a consumer needs no producer thread of its own (``Prefetcher`` iterates inline)."""
+        return self.gpu is not None and _feeder_available()
 
     def __iter__(self):
+        if self.inline:
+            yield from self._iter_feeder()
+            return
         slots = self._raw_slots() if self.gpu is not None else []
         L = native.cpu().TextLoader(start_epoch=self.state.epoch, skip_batches=self.state.batches_in_epoch,
                                     raw=self.gpu is not None, binary=self.binary, rows=self.dds is not None,
@@ -323,6 +347,82 @@ class NativeTextReader:
                 pending = None
             self.state.epoch, self.state.batches_in_epoch = self.num_epochs, 0
         finally:
+            L.close()
+
+    # ------------------------------------------------------------------ C++ feeder (GPU tokenizer)
+    def _device_slot(self) -> dict:
+        """Device buffers of one feeder slot: raw bytes / line starts / weights copied in, the
+        tokenizer's CSR out (ids / values sized for the densest possible batch: a token takes >= 2
+        bytes), its counts / status / scan workspace."""
+        dev, B, nb = self.gpu, self.args["batch_size"], self._slot_bytes
+        cap = nb // 2 + B + 1
+        i32 = dict(dtype=torch.int32, device=dev)
+        f32 = dict(dtype=torch.float32, device=dev)
+        return dict(bytes=torch.empty(nb, dtype=torch.uint8, device=dev),
+                    ls=torch.empty(B + 1, dtype=torch.int64, device=dev), weights=torch.empty(B, **f32),
+                    labels=torch.empty(B, **f32), offsets=torch.empty(B + 1, **i32), counts=torch.empty(B + 1, **i32),
+                    ids=torch.empty(cap, **i32), vals=torch.empty(cap, **f32), status=torch.empty(8, **i32),
+                    ws=torch.empty(max(1, int(native.hip().parse_workspace_bytes(B))), dtype=torch.uint8, device=dev))
+
+    @staticmethod
+    def _slot_ptrs(t: dict) -> list[int]:
+        return [t["bytes"].data_ptr(), t["bytes"].numel(), t["ls"].data_ptr(), t["ls"].numel(), t["weights"].data_ptr(),
+                t["labels"].data_ptr(), t["offsets"].data_ptr(), t["counts"].data_ptr(), t["ids"].data_ptr(),
+                t["ids"].numel(), t["vals"].data_ptr(), t["status"].data_ptr(), t["ws"].data_ptr(), t["ws"].numel()]
+
+    def _iter_feeder(self):
+        """GPU-tokenizer batches from the C++ feeder (hip/feeder.hip): its thread takes the loader's
+        raw batches (page-locked slots), copies them to a free device slot, launches the tokenizer,
+        waits for it (CPU parse of a batch the GPU subset declines) and queues the finished batch;
+        this generator only wraps the slot's tensors.  A device slot is handed back when the batch
+        object dies: the feeder's stream then waits for the work queued so far on the releasing
+        thread's current stream (the step that read it) before overwriting the slot."""
+        slots = self._raw_slots()
+        L = native.cpu().TextLoader(start_epoch=self.state.epoch, skip_batches=self.state.batches_in_epoch,
+                                    raw=True, binary=False, rows=False, raw_slots=slots, **self.args)
+        self._loader = L
+        dev = self.gpu
+        if dev.index is None:
+            dev = self.gpu = torch.device("cuda", torch.cuda.current_device())
+        F = native.hip().GpuTextFeeder(L.c_api(), dev.index, self.args["vocab_size"], self.args["hash_feature_id"])
+        dslots = []
+
+        def add_slot():
+            with torch.cuda.device(dev):
+                t = self._device_slot()
+            torch.cuda.synchronize(dev)  # (allocation-time work done before the feeder's stream uses it)
+            dslots.append(t)
+            F.add_slot(self._slot_ptrs(t))
+
+        for _ in range(max(6, self.args["queue_size"] + 4)):
+            add_slot()
+        F.start()
+        self._feeder = F
+        try:
+            while True:
+                r = F.next(100)
+                if r is None:
+                    break
+                if isinstance(r, int):
+                    # every slot is held by the consumer (e.g. list(reader)) while the feeder waits for one
+                    if r == -1 and len(dslots) < 256:
+                        add_slot()
+                    continue
+                if r[0] == "error":
+                    raise (native.cpu().ParseError if r[1] else RuntimeError)(r[2])
+                d, n, nnz, mf, has_vals, weighted, epoch, count = r
+                t = dslots[d]
+                b = Batch(t["labels"][:n], t["offsets"][: n + 1], t["ids"][:nnz], t["vals"][:nnz] if has_vals else None,
+                          t["weights"][:n] if weighted else None, nnz, max_feats=mf)
+                weakref.finalize(b, _feeder_release, F, d, dev)
+                self.state.epoch, self.state.batches_in_epoch = int(epoch), int(count)
+                b.reader_pos = (int(epoch), int(count))
+                yield b
+            self.fallbacks = int(F.fallbacks())
+            self.state.epoch, self.state.batches_in_epoch = self.num_epochs, 0
+        finally:
+            self.fallbacks = int(F.fallbacks())
+            F.close()
             L.close()
 
     def _gather_batch(self, rows: np.ndarray, offsets: np.ndarray, has_vals: bool, max_feats: int, stream) -> Batch:
@@ -412,6 +512,20 @@ class NativeTextReader:
         return b
 
 
+def _feeder_available() -> bool:
+    try:
+        return hasattr(native.hip(), "GpuTextFeeder")
+    except Exception:  # noqa: BLE001  (no HIP module: the Python-driven GPU tokenizer path)
+        return False
+
+
+def _feeder_release(F, d: int, dev: torch.device) -> None:
+    try:
+        F.release(d, torch.cuda.current_stream(dev).cuda_stream)
+    except Exception:  # noqa: BLE001  (interpreter shutdown / feeder closed: nothing to hand back)
+        pass
+
+
 class Prefetcher:
     """Background producer threads + bounded queue + pinned H2D on a side stream.
 
@@ -428,6 +542,12 @@ class Prefetcher:
         self.queue_size = max(1, queue_size)
         self._err: BaseException | None = None
         self._stop = threading.Event()
+        # a reader whose batches come out complete on the device from a native producer thread
+        # (NativeTextReader + C++ feeder) is iterated inline: no Python thread, no queue hop
+        self.inline = bool(getattr(reader, "inline", False))
+        self._stream = None
+        if self.inline:
+            return
         self._th = threading.Thread(target=self._run, name="fm-reader", daemon=True)
         self._stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
         self._th.start()
@@ -454,6 +574,8 @@ class Prefetcher:
             self.q.put((self._END, None, None))
 
     def size(self) -> int:
+        if self.inline:
+            return min(self.queue_size, int(self.reader.queued()))
         return self.q.qsize()
 
     def shuffle_fill(self) -> float:
@@ -462,6 +584,9 @@ class Prefetcher:
         return float(f()) if f is not None else 0.0
 
     def __iter__(self):
+        if self.inline:
+            yield from self.reader
+            return
         while True:
             item, ev, _host = self.q.get()
             if item is self._END:
@@ -489,3 +614,5 @@ class Prefetcher:
 
     def close(self):
         self._stop.set()
+        if self.inline and hasattr(self.reader, "close"):
+            self.reader.close()

@@ -23,11 +23,38 @@ static int check(const std::vector<std::string>& lines, long long vocab, bool ha
     lens.push_back(l.size());
   }
   fm::CsrBatch out;
+  fm::Csr32 o32;
+  std::string e64, e32;
   try {
     fm::parse_lines(ptrs.data(), lens.data(), lines.size(), vocab, hash, threads, out);
-  } catch (const fm::ParseError&) {
-    return 0;  // rejected input: fine
+  } catch (const fm::ParseError& e) {
+    e64 = e.what();
   }
+  try {  // the int32 loader parser: same acceptance, same first error, same CSR
+    fm::parse_lines32(ptrs.data(), lens.data(), lines.size(), vocab, hash, threads, o32);
+  } catch (const fm::ParseError& e) {
+    e32 = e.what();
+  }
+  if (e64 != e32) {
+    std::fprintf(stderr, "parse_lines32 error differs: '%s' vs '%s'\n", e64.c_str(), e32.c_str());
+    return 1;
+  }
+  if (!e64.empty()) return 0;  // rejected input: fine
+  if (o32.labels.size() != out.labels.size() || o32.ids.size() != out.ids.size() ||
+      o32.offsets.size() != lines.size() + 1) {
+    std::fprintf(stderr, "parse_lines32 sizes differ\n");
+    return 1;
+  }
+  for (size_t i = 0; i < out.ids.size(); ++i)
+    if (o32.ids[i] != out.ids[i] || (o32.has_vals ? o32.vals[i] : 1.f) != out.vals[i]) {
+      std::fprintf(stderr, "parse_lines32 ids / values differ at %zu\n", i);
+      return 1;
+    }
+  for (size_t i = 0; i < out.labels.size(); ++i)
+    if (std::memcmp(&o32.labels[i], &out.labels[i], 4) != 0 || o32.offsets[i + 1] - o32.offsets[i] != out.sizes[i]) {
+      std::fprintf(stderr, "parse_lines32 labels / offsets differ at %zu\n", i);
+      return 1;
+    }
   size_t nnz = 0;
   for (int s : out.sizes) nnz += (size_t)s;
   if (out.labels.size() != lines.size() || out.sizes.size() != lines.size() || out.ids.size() != nnz ||
@@ -40,6 +67,35 @@ static int check(const std::vector<std::string>& lines, long long vocab, bool ha
       std::fprintf(stderr, "id out of range: %lld\n", id);
       return 1;
     }
+  return 0;
+}
+
+// tf.string_to_number semantics with strtof only (the pre-fast-path implementation)
+static bool ref_float(const std::string& l, float* v) {
+  const char* p = l.c_str();
+  char* e = nullptr;
+  *v = std::strtof(p, &e);
+  if (e == p) return false;
+  while (*e == ' ' || *e == '\t' || *e == '\r' || *e == '\n') ++e;
+  return *e == '\0';
+}
+
+// parse_floats (decimal fast path + strtof fallback) must equal strtof bit for bit, errors included
+static int check_float(const std::string& l, int threads) {
+  const char* p = l.data();
+  size_t len = l.size();
+  float ref = 0.f, got = 0.f;
+  const bool ok = ref_float(l, &ref) && l.find('\0') == std::string::npos;
+  bool got_ok = true;
+  try {
+    fm::parse_floats(&p, &len, 1, &got, threads);
+  } catch (const fm::ParseError&) {
+    got_ok = false;
+  }
+  if (ok != got_ok || (ok && std::memcmp(&ref, &got, 4) != 0)) {
+    std::fprintf(stderr, "parse_floats('%s') = %d %.9g, strtof %d %.9g\n", l.c_str(), got_ok, got, ok, ref);
+    return 1;
+  }
   return 0;
 }
 
@@ -70,6 +126,24 @@ int main() {
     std::vector<std::string> batch = {l, base[1], l};
     bad += check(batch, 1 + rng() % 100000, rng() % 2, 1 + rng() % 4);
   }
+  // decimal fast path vs strtof: random plain decimals (up to 9 digits, up to 12 after the point,
+  // signs, leading / trailing points) and mutations of them
+  const std::string falpha = "0123456789.-+eE \tx";
+  for (int it = 0; it < 200000; ++it) {
+    std::string l;
+    if (rng() % 4 == 0) l += (rng() % 2) ? '-' : '+';
+    const int id = rng() % 10, fd = rng() % 13;
+    for (int k = 0; k < id; ++k) l += char('0' + rng() % 10);
+    if (fd > 0 || rng() % 3 == 0) l += '.';
+    for (int k = 0; k < fd; ++k) l += char('0' + rng() % 10);
+    if (rng() % 5 == 0) l += (rng() % 2) ? " " : "\r";
+    if (rng() % 8 == 0 && !l.empty()) l[rng() % l.size()] = falpha[rng() % falpha.size()];
+    bad += check_float(l, 1);
+    if (bad > 20) break;
+  }
+  for (const char* l : {"1", "2", "0.1", "1e5", " 1", "1 ", "nan", "inf", "0x10", "-0", "16777216", "16777215.5",
+                        "0.3333333", "1234567.8", ".5", "5.", ".", "-", "1.0000000001", "3.40282347e38"})
+    bad += check_float(l, 1);
   std::printf("parser_fuzz: %s\n", bad ? "FAILED" : "ok");
   return bad ? 1 : 0;
 }

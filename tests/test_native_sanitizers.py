@@ -21,7 +21,7 @@ CSRC = os.path.join(ROOT, "fast_tffm_amd", "csrc")
 def test_parser_under_asan_ubsan(tmp_path):
     exe = str(tmp_path / "parser_fuzz")
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
-           "-fno-sanitize-recover=undefined", "-pthread", "-I", CSRC,
+           "-fno-sanitize-recover=undefined", "-pthread", "-fopenmp", "-I", CSRC,
            os.path.join(ROOT, "tests", "native", "parser_fuzz.cpp"), os.path.join(CSRC, "cpu", "parser.cpp"),
            "-o", exe]
     r = subprocess.run(cmd, capture_output=True, text=True)
