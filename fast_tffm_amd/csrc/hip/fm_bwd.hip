@@ -58,8 +58,8 @@ struct BwdArgs {
   long long v_stride;
   float* w;
   long long w_stride;
-  float* s0v;               // optimizer state, same row layout as v (fp32)
-  float* s1v;
+  void* s0v;                // optimizer state, same row layout as v (fp32; bf16 for fp8 tables)
+  void* s1v;
   long long s_stride;
   float* s0w;
   float* s1w;
@@ -124,20 +124,10 @@ __device__ inline void bwd_load(const BwdArgs& a, int u, long long key, int tE, 
     for (int k = 0; k < EPL; ++k) r.vv[k] *= s;
   }
   if (!r.apply) return;
-  const float* s0 = a.s0v + r.row * a.s_stride + tE * EPL;
-#pragma unroll
-  for (int k = 0; k < EPL; k += 4) {
-    const float4 q = *reinterpret_cast<const float4*>(s0 + k);
-    r.st0[k] = q.x; r.st0[k + 1] = q.y; r.st0[k + 2] = q.z; r.st0[k + 3] = q.w;
-  }
+  load_state<TV, EPL>(a.s0v, r.row * a.s_stride + tE * EPL, r.st0);
   r.q0 = a.s0w[r.row];
   if (a.s1v) {
-    const float* s1 = a.s1v + r.row * a.s_stride + tE * EPL;
-#pragma unroll
-    for (int k = 0; k < EPL; k += 4) {
-      const float4 z = *reinterpret_cast<const float4*>(s1 + k);
-      r.st1[k] = z.x; r.st1[k + 1] = z.y; r.st1[k + 2] = z.z; r.st1[k + 3] = z.w;
-    }
+    load_state<TV, EPL>(a.s1v, r.row * a.s_stride + tE * EPL, r.st1);
     r.q1 = a.s1w[r.row];
   } else {
 #pragma unroll
@@ -188,16 +178,10 @@ __device__ inline void bwd_finish(const BwdArgs& a, int u, int t, bool tact, Row
   for (int k = 0; k < EPL; ++k) opt_step(a.opt, gr[k], r.vv[k], r.st0[k], r.st1[k]);
   store_row<LPR, TV>(tv + r.row * tvs + t * EPL, r.vv, tw, r.row, tws, t, tact, sr);
   if (tact) {
-    float* s0 = a.s0v + r.row * a.s_stride + t * EPL;
-#pragma unroll
-    for (int k = 0; k < EPL; k += 4)
-      *reinterpret_cast<float4*>(s0 + k) = make_float4(r.st0[k], r.st0[k + 1], r.st0[k + 2], r.st0[k + 3]);
-    if (a.s1v) {
-      float* s1 = a.s1v + r.row * a.s_stride + t * EPL;
-#pragma unroll
-      for (int k = 0; k < EPL; k += 4)
-        *reinterpret_cast<float4*>(s1 + k) = make_float4(r.st1[k], r.st1[k + 1], r.st1[k + 2], r.st1[k + 3]);
-    }
+    const long long off = r.row * a.s_stride + t * EPL;
+    store_state<TV, EPL>(a.s0v, off, r.st0, sr ? sr ^ kSrSalt0 : 0u, (uint32_t)r.row, (uint32_t)(t * EPL));
+    if (a.s1v)
+      store_state<TV, EPL>(a.s1v, off, r.st1, sr ? sr ^ kSrSalt1 : 0u, (uint32_t)r.row, (uint32_t)(t * EPL));
   }
   if (t == 0) {
     opt_step(a.opt, gw, r.wv, r.q0, r.q1);

@@ -211,6 +211,64 @@ __device__ inline void store_r1(void* r1, long long off, const float (&s)[EPL]) 
   }
 }
 
+// Optimizer state rows (Adagrad accumulator / FTRL n; FTRL z): fp32, except for fp8 tables.
+// Their factors carry 3 mantissa bits, so the state is kept in bf16 (8 bits), stored with
+// stochastic rounding when a step seed is given -- sums of small squared gradients survive in
+// expectation -- which halves the state's share of the row read-modify-write (k=128 FTRL:
+// 1032 -> 516 of 1.17 KB per row).  The bias state (s0w / s1w) stays fp32.
+template <typename TV> struct StateBf16 { static constexpr bool v = false; };
+template <> struct StateBf16<fp8e4m3> { static constexpr bool v = true; };
+
+template <typename TV, int EPL>
+__device__ inline void load_state(const void* s, long long off, float (&o)[EPL]) {
+  if constexpr (StateBf16<TV>::v) {
+    const uint16_t* p = reinterpret_cast<const uint16_t*>(s) + off;
+#pragma unroll
+    for (int k = 0; k < EPL; k += 4) {
+      const uint2 h = *reinterpret_cast<const uint2*>(p + k);
+      o[k] = bf16_bits_to_f32(h.x & 0xffffu); o[k + 1] = bf16_bits_to_f32(h.x >> 16);
+      o[k + 2] = bf16_bits_to_f32(h.y & 0xffffu); o[k + 3] = bf16_bits_to_f32(h.y >> 16);
+    }
+  } else {
+    const float* p = reinterpret_cast<const float*>(s) + off;
+#pragma unroll
+    for (int k = 0; k < EPL; k += 4) {
+      const float4 f = *reinterpret_cast<const float4*>(p + k);
+      o[k] = f.x; o[k + 1] = f.y; o[k + 2] = f.z; o[k + 3] = f.w;
+    }
+  }
+}
+
+// seed: the step's stochastic-rounding seed (0: round to nearest even), salted per state slot
+template <typename TV, int EPL>
+__device__ inline void store_state(void* s, long long off, const float (&o)[EPL], uint32_t seed, uint32_t row,
+                                   uint32_t col) {
+  if constexpr (StateBf16<TV>::v) {
+    uint16_t* p = reinterpret_cast<uint16_t*>(s) + off;
+#pragma unroll
+    for (int k = 0; k < EPL; k += 4) {
+      uint32_t b[4];
+      if (seed) {
+        uint32_t r = sr_hash(seed, row, col + (uint32_t)k);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          b[i] = f32_to_bf16_bits_sr(o[k + i], r);
+          r = sr_next(r);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) b[i] = f32_to_bf16_bits(o[k + i]);
+      }
+      *reinterpret_cast<uint2*>(p + k) = make_uint2(b[0] | (b[1] << 16), b[2] | (b[3] << 16));
+    }
+  } else {
+    float* p = reinterpret_cast<float*>(s) + off;
+#pragma unroll
+    for (int k = 0; k < EPL; k += 4) *reinterpret_cast<float4*>(p + k) = make_float4(o[k], o[k + 1], o[k + 2], o[k + 3]);
+  }
+}
+constexpr uint32_t kSrSalt0 = 0x68e31da4u, kSrSalt1 = 0xb5297a4du;  // per state slot
+
 // Dequantisation factor of a table row (1 for unscaled dtypes).
 template <typename TV>
 __device__ inline float row_scale(const float* w, long long row, long long w_stride) {

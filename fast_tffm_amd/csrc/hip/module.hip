@@ -152,7 +152,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
         a.sorted_ex = P<const int>(sorted_ex); a.ex_shift = ex_shift; a.sorted_x = P<const float>(sorted_x);
         a.dpred = P<const float>(dpred); a.r1 = P<const void>(r1); a.Kp = Kp;
         a.v = P<void>(v); a.v_stride = v_stride; a.w = P<float>(w); a.w_stride = w_stride;
-        a.s0v = P<float>(s0v); a.s1v = P<float>(s1v); a.s_stride = s_stride; a.s0w = P<float>(s0w);
+        a.s0v = P<void>(s0v); a.s1v = P<void>(s1v); a.s_stride = s_stride; a.s0w = P<float>(s0w);
         a.s1w = P<float>(s1w); a.reg_v = reg_v; a.reg_w = reg_w;
         a.opt = opt_params(opt_type, lr, l1, l2, beta);
         a.grad_out = P<float>(grad_out); a.g_stride = g_stride; a.g_wcol = g_wcol < 0 ? Kp : g_wcol;
@@ -250,7 +250,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
         a.num_unique = P<const int>(num_unique); a.seg_start = P<const int>(seg_start);
         a.uniq = P<const int>(uniq); a.perm = P<const int>(perm); a.grad_in = P<const float>(grad_in);
         a.g_stride = g_stride; a.Kp = Kp; a.v = P<void>(v); a.v_stride = v_stride; a.w = P<float>(w);
-        a.w_stride = w_stride; a.s0v = P<float>(s0v); a.s1v = P<float>(s1v); a.s_stride = s_stride;
+        a.w_stride = w_stride; a.s0v = P<void>(s0v); a.s1v = P<void>(s1v); a.s_stride = s_stride;
         a.s0w = P<float>(s0w); a.s1w = P<float>(s1w); a.opt = opt_params(opt_type, lr, l1, l2, beta);
         check(fm::launch_apply_rows(a, dtype, max_unique, S(stream)), "apply_rows");
       },
@@ -273,7 +273,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
         a.R = R; a.W = W; a.run_off = P<const int>(run_off); a.req = P<const int>(req);
         a.match = P<const int>(match); a.grad_in = P<const float>(grad_in);
         a.g_stride = g_stride; a.Kp = Kp; a.v = P<void>(v); a.v_stride = v_stride; a.w = P<float>(w);
-        a.w_stride = w_stride; a.s0v = P<float>(s0v); a.s1v = P<float>(s1v); a.s_stride = s_stride;
+        a.w_stride = w_stride; a.s0v = P<void>(s0v); a.s1v = P<void>(s1v); a.s_stride = s_stride;
         a.s0w = P<float>(s0w); a.s1w = P<float>(s1w); a.opt = opt_params(opt_type, lr, l1, l2, beta);
         check(fm::launch_apply_runs(a, P<int>(match), dtype, S(stream)), "apply_runs");
       },
@@ -295,7 +295,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
         a.R = (int)R; a.row0 = row0; a.touch_col = touch_col;
         a.grad_in = P<const float>(grad); a.grad_zero = zero ? P<float>(grad) : nullptr;
         a.g_stride = g_stride; a.Kp = Kp; a.v = P<void>(v); a.v_stride = v_stride; a.w = P<float>(w);
-        a.w_stride = w_stride; a.s0v = P<float>(s0v); a.s1v = P<float>(s1v); a.s_stride = s_stride;
+        a.w_stride = w_stride; a.s0v = P<void>(s0v); a.s1v = P<void>(s1v); a.s_stride = s_stride;
         a.s0w = P<float>(s0w); a.s1w = P<float>(s1w); a.opt = opt_params(opt_type, lr, l1, l2, beta);
         check(fm::launch_dense_apply(a, dtype, S(stream)), "dense_apply");
       },

@@ -165,7 +165,7 @@ struct ApplyArgs {
   int Kp;
   void* v; long long v_stride;
   float* w; long long w_stride;
-  float* s0v; float* s1v; long long s_stride;
+  void* s0v; void* s1v; long long s_stride;  // fp32 (bf16 for fp8 tables: fm_common.h StateBf16)
   float* s0w; float* s1w;
   OptParams opt;
   // run-merge form (apply_runs): R received rows forming W ascending runs (one per
@@ -195,7 +195,8 @@ struct RowUpdate {
   static constexpr int EPL = F::N;
   float vv[EPL], st0[EPL], st1[EPL];
   float pw, q0, q1;
-  TV* vrow; float* s0; float* s1;
+  TV* vrow;
+  long long soff;
 
   __device__ inline void load(const ApplyArgs& a, long long row, int tE) {
     vrow = reinterpret_cast<TV*>(a.v) + row * a.v_stride + tE * EPL;
@@ -205,14 +206,13 @@ struct RowUpdate {
 #pragma unroll
       for (int k = 0; k < EPL; ++k) vv[k] *= s;
     }
-    s0 = a.s0v + row * a.s_stride + tE * EPL;
-    s1 = a.s1v ? a.s1v + row * a.s_stride + tE * EPL : nullptr;
+    soff = row * a.s_stride + tE * EPL;
+    load_state<TV, EPL>(a.s0v, soff, st0);
+    if (a.s1v) {
+      load_state<TV, EPL>(a.s1v, soff, st1);
+    } else {
 #pragma unroll
-    for (int k = 0; k < EPL; k += 4) {
-      const float4 q = *reinterpret_cast<const float4*>(s0 + k);
-      st0[k] = q.x; st0[k + 1] = q.y; st0[k + 2] = q.z; st0[k + 3] = q.w;
-      const float4 z = s1 ? *reinterpret_cast<const float4*>(s1 + k) : make_float4(0.f, 0.f, 0.f, 0.f);
-      st1[k] = z.x; st1[k + 1] = z.y; st1[k + 2] = z.z; st1[k + 3] = z.w;
+      for (int k = 0; k < EPL; ++k) st1[k] = 0.f;
     }
     pw = a.w[row * a.w_stride];
     q0 = a.s0w[row];
@@ -225,11 +225,9 @@ struct RowUpdate {
     for (int k = 0; k < EPL; ++k) opt_step(a.opt, gr[k], vv[k], st0[k], st1[k]);
     store_row<LPR, TV>(vrow, vv, a.w, row, a.w_stride, t, tact, sr);
     if (tact) {
-#pragma unroll
-      for (int k = 0; k < EPL; k += 4) {
-        *reinterpret_cast<float4*>(s0 + k) = make_float4(st0[k], st0[k + 1], st0[k + 2], st0[k + 3]);
-        if (s1) *reinterpret_cast<float4*>(s1 + k) = make_float4(st1[k], st1[k + 1], st1[k + 2], st1[k + 3]);
-      }
+      const uint32_t col = (uint32_t)(t * EPL);
+      store_state<TV, EPL>(a.s0v, soff, st0, sr ? sr ^ kSrSalt0 : 0u, (uint32_t)row, col);
+      if (a.s1v) store_state<TV, EPL>(a.s1v, soff, st1, sr ? sr ^ kSrSalt1 : 0u, (uint32_t)row, col);
     }
     if (t == 0) {
       opt_step(a.opt, gw, pw, q0, q1);

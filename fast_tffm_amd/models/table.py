@@ -14,8 +14,10 @@ storage is HBM-friendly rather than reference-shaped:
 * ``w``   [rows]      fp32 (linear weight, kept separate so v rows stay aligned);
   fp8 tables store [w, scale] pairs (``wx`` [rows, 2], ``w`` = wx[:, 0]) so the
   row's dequantisation scale arrives with w;
-* ``s0v``/``s0w``     optimizer slot 0 (Adagrad accumulator / FTRL n), fp32;
-* ``s1v``/``s1w``     optimizer slot 1 (FTRL z), fp32.
+* ``s0v``/``s0w``     optimizer slot 0 (Adagrad accumulator / FTRL n);
+* ``s1v``/``s1w``     optimizer slot 1 (FTRL z);
+  fp32, except ``s0v`` / ``s1v`` of fp8 tables: bf16 with stochastic rounding
+  (``K.state_dtype``), half the state bytes next to factors of 3 mantissa bits.
 
 The checkpoint module converts to and from the reference layout.
 """
@@ -74,11 +76,12 @@ class FMTable:
             self.scale = None
         acc0 = float(self.opt.initial_accumulator)
         n_state = max(1, self.opt.n_state)  # kernels always address slot 0
+        sdt = self.state_dtype = K.state_dtype(dtype)
         self.s0v = torch.full((self.rows, self.Kp), acc0 if self.opt.name in ("adagrad", "ftrl") else 0.0,
-                              dtype=torch.float32, device=dev)
+                              dtype=sdt, device=dev)
         self.s0w = torch.full((self.rows,), acc0 if self.opt.name in ("adagrad", "ftrl") else 0.0,
                               dtype=torch.float32, device=dev)
-        self.s1v = torch.zeros((self.rows, self.Kp), dtype=torch.float32, device=dev) if n_state > 1 else None
+        self.s1v = torch.zeros((self.rows, self.Kp), dtype=sdt, device=dev) if n_state > 1 else None
         self.s1w = torch.zeros((self.rows,), dtype=torch.float32, device=dev) if n_state > 1 else None
         if init:
             self.reinit()

@@ -433,12 +433,25 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
 class TableState:
     """Parameters and optimizer slots of one (local) table shard."""
 
-    v: torch.Tensor                 # [rows, Kp] fp32 / bf16
+    v: torch.Tensor                 # [rows, Kp] fp32 / bf16 / fp8
     w: torch.Tensor                 # [rows] fp32
-    s0v: torch.Tensor | None = None  # adagrad accumulator / ftrl n   [rows, Kp] fp32
-    s1v: torch.Tensor | None = None  # ftrl z                          [rows, Kp] fp32
-    s0w: torch.Tensor | None = None  # [rows]
-    s1w: torch.Tensor | None = None  # [rows]
+    s0v: torch.Tensor | None = None  # adagrad accumulator / ftrl n   [rows, Kp] state_dtype(v.dtype)
+    s1v: torch.Tensor | None = None  # ftrl z                          [rows, Kp] state_dtype(v.dtype)
+    s0w: torch.Tensor | None = None  # [rows] fp32
+    s1w: torch.Tensor | None = None  # [rows] fp32
+
+    def __post_init__(self):
+        want = state_dtype(self.v.dtype)
+        for name in ("s0v", "s1v"):
+            t = getattr(self, name)
+            _check(t is None or t.dtype == want, f"{name}: {want} optimizer state for a {self.v.dtype} table")
+
+
+def state_dtype(table_dtype: torch.dtype) -> torch.dtype:
+    """Storage of the per-factor optimizer state: fp32, bf16 for fp8 tables (hip/fm_common.h
+    StateBf16: 8 mantissa bits with stochastic rounding next to factors carrying 3; halves the
+    state bytes of the row read-modify-write)."""
+    return torch.bfloat16 if table_dtype == FP8 else torch.float32
 
 
 @dataclass
