@@ -278,18 +278,23 @@ class NativeTextReader:
         """Page-locked output slots of the loader's raw mode (GPU tokenizer): batches are assembled
         straight into them, so the host-to-device copy needs no staging copy.  queue_size + 3
         slots (queued batches, the one being copied / parsed, the one being finished, one spare)
-        of 1.5x the batch's estimated bytes (average line length of the first file's head); a
-        larger batch falls back to a heap buffer."""
+        of twice the batch's estimated bytes (the longest average line over the heads of the
+        files: files of one run can differ, e.g. with and without values); a larger batch falls
+        back to a heap buffer (and, with the feeder, to the CPU parser)."""
         if getattr(self, "_slots", None) is None:
             B = self.args["batch_size"]
             avg = 256.0
-            try:
-                with open(self.args["files"][0], "rb") as f:
-                    head = f.read(4 << 20)
-                avg = max(16.0, len(head) / max(1, head.count(b"\n")))
-            except OSError:
-                pass
-            nb, nl = int(B * avg * 1.5) + 4096, B + 1
+            est = []
+            for path in self.args["files"][:64]:
+                try:
+                    with open(path, "rb") as f:
+                        head = f.read(1 << 20)
+                    est.append(len(head) / max(1, head.count(b"\n")))
+                except OSError:
+                    pass
+            if est:
+                avg = max(16.0, max(est))
+            nb, nl = int(B * avg * 2.0) + 4096, B + 1
             self._slot_bytes = nb
             self._slots = [(torch.empty(nb, dtype=torch.uint8, pin_memory=True),
                             torch.empty(nl, dtype=torch.int64, pin_memory=True),
