@@ -193,13 +193,16 @@ int api_next(void* h, FmRawView* v, char* err, int errlen) {
   try {
     auto b = std::make_unique<LoadedBatch>();
     if (!L->next(*b)) return 0;
-    if (b->slot < 0 && b->line_start.empty()) {
-      copy_err("the loader is not in raw mode", err, errlen);
-      return -2;
-    }
+    v->kind = 0;
     v->slot = b->slot;
     v->epoch = b->epoch;
     v->count = b->count;
+    v->max_feats = b->max_feats;
+    v->labels = nullptr;
+    v->offsets = nullptr;
+    v->ids = nullptr;
+    v->vals = nullptr;
+    v->nnz = 0;
     if (b->slot >= 0) {
       const RawSlot& rs = L->options().raw_slots[static_cast<size_t>(b->slot)];
       v->bytes = rs.bytes;
@@ -207,12 +210,27 @@ int api_next(void* h, FmRawView* v, char* err, int errlen) {
       v->nbytes = static_cast<int64_t>(b->nbytes);
       v->nlines = static_cast<int64_t>(b->nlines);
       v->weights = b->weights_in_slot ? rs.weights : (b->weights.empty() ? nullptr : b->weights.data());
-    } else {
+    } else if (!b->line_start.empty()) {
       v->bytes = b->bytes.data();
       v->line_start = b->line_start.data();
       v->nbytes = static_cast<int64_t>(b->bytes.size());
       v->nlines = static_cast<int64_t>(b->line_start.size()) - 1;
       v->weights = b->weights.empty() ? nullptr : b->weights.data();
+    } else if (b->rows.empty() && !b->offsets.empty()) {  // parsed / binary CSR
+      v->kind = 1;
+      v->bytes = nullptr;
+      v->line_start = nullptr;
+      v->nbytes = 0;
+      v->nlines = static_cast<int64_t>(b->labels.size());
+      v->labels = b->labels.data();
+      v->offsets = b->offsets.data();
+      v->ids = b->ids.data();
+      v->vals = b->vals.empty() ? nullptr : b->vals.data();
+      v->nnz = static_cast<int64_t>(b->ids.size());
+      v->weights = b->weights.empty() ? nullptr : b->weights.data();
+    } else {
+      copy_err("row-number batches (device-resident caches) have no host data for the feeder", err, errlen);
+      return -2;
     }
     v->owner = b.release();
     return 1;

@@ -1,5 +1,6 @@
-// GPU-tokenizer feeder: the host loader's raw batches -> CSR batches on the device, driven by a
-// native thread (no Python, no GIL between file bytes and a ready device batch).
+// Device feeder: the host loader's batches -> CSR batches on the device, driven by a native
+// thread (no Python, no GIL between file bytes and a ready device batch).  Raw batches go
+// through the GPU tokenizer; batches the loader parsed itself (CPU parser) are copied over.
 //
 // The reference's input path is a set of TF queue runners feeding the step (tffm/fm_model.py:
 // 34-126, run_tffm.py:79-81: examples/s is measured file-fed).  Here the host side is the C++
@@ -259,7 +260,26 @@ class GpuTextFeeder {
         const bool fits = static_cast<size_t>(v.nbytes) <= s.bytes_cap && static_cast<size_t>(n) + 1 <= s.ls_cap &&
                           n < (int64_t(1) << 31);
         bool ok = true;
-        if (n == 0) {
+        if (v.kind == 1) {  // parsed on the host (CPU parser / binary cache): copy the CSR over
+          if (static_cast<size_t>(n) + 1 > s.ls_cap || static_cast<size_t>(v.nnz) > s.ids_cap) {
+            fail("batch of " + std::to_string(n) + " lines / " + std::to_string(v.nnz) +
+                 " features exceeds the feeder's slots", false);
+            ok = false;
+          } else {
+            hip_ok(hipStreamWaitEvent(st_, s.freed, 0), "hipStreamWaitEvent");
+            hip_ok(hipMemcpyAsync(s.labels, v.labels, 4 * n, hipMemcpyHostToDevice, st_), "H2D");
+            hip_ok(hipMemcpyAsync(s.offsets, v.offsets, 4 * (n + 1), hipMemcpyHostToDevice, st_), "H2D");
+            if (v.nnz > 0) hip_ok(hipMemcpyAsync(s.ids, v.ids, 4 * v.nnz, hipMemcpyHostToDevice, st_), "H2D");
+            if (v.vals && v.nnz > 0)
+              hip_ok(hipMemcpyAsync(s.vals, v.vals, 4 * v.nnz, hipMemcpyHostToDevice, st_), "H2D");
+            if (v.weights && s.weights)
+              hip_ok(hipMemcpyAsync(s.weights, v.weights, 4 * n, hipMemcpyHostToDevice, st_), "H2D");
+            hip_ok(hipStreamSynchronize(st_), "hipStreamSynchronize");
+            b.nnz = v.nnz;
+            b.max_feats = v.max_feats;
+            b.has_vals = v.vals != nullptr;
+          }
+        } else if (n == 0) {
           b.nnz = 0;
           hip_ok(hipStreamWaitEvent(st_, s.freed, 0), "hipStreamWaitEvent");
           hip_ok(hipMemsetAsync(s.offsets, 0, sizeof(int), st_), "hipMemsetAsync");

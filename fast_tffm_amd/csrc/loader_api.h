@@ -12,18 +12,26 @@
 
 extern "C" {
 
-// One raw (GPU-tokenizer) batch as the loader produced it: '\n'-terminated lines in page-locked
-// memory when it came from one of the caller's slots (`slot` >= 0), else in a heap buffer owned
-// by the loader (`owner`).  Valid until handed back with FmLoaderApi::done.
+// One batch as the loader produced it, valid until handed back with FmLoaderApi::done:
+//  * kind 0 (raw mode, GPU tokenizer): '\n'-terminated lines, in page-locked memory when it came
+//    from one of the caller's slots (`slot` >= 0), else in a heap buffer owned by the loader;
+//  * kind 1 (parse mode): the CPU parser's int32 CSR in loader-owned (pageable) memory.
 struct FmRawView {
+  int32_t kind;
   int32_t slot;                 // host slot index, -1 for a heap batch
   int32_t epoch;
+  int32_t max_feats;            // kind 1
   int64_t count;                // batches of `epoch` consumed once this one is
-  const uint8_t* bytes;
-  const int64_t* line_start;    // [nlines + 1]
+  const uint8_t* bytes;         // kind 0
+  const int64_t* line_start;    // kind 0: [nlines + 1]
   const float* weights;         // [nlines] or null (no weight files)
   int64_t nbytes, nlines;
-  void* owner;                  // loader-private (heap batch)
+  const float* labels;          // kind 1: [nlines]
+  const int32_t* offsets;       // kind 1: [nlines + 1]
+  const int32_t* ids;           // kind 1: [nnz]
+  const float* vals;            // kind 1: [nnz] or null (every value 1)
+  int64_t nnz;                  // kind 1
+  void* owner;                  // loader-private (the batch)
 };
 
 // Host CSR written by FmLoaderApi::parse into caller-owned arrays.
@@ -55,4 +63,4 @@ struct FmLoaderApi {
 
 }  // extern "C"
 
-constexpr int32_t kFmLoaderApiVersion = 1;
+constexpr int32_t kFmLoaderApiVersion = 2;

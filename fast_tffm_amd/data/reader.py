@@ -225,7 +225,7 @@ class NativeTextReader:
                  hash_feature_id: bool = False, num_epochs: int = 1, shuffle: bool = True, seed: int = 0,
                  parse_threads: int = 4, rank: int = 0, world: int = 1, state: ReaderState | None = None,
                  queue_size: int = 4, gpu_parse: torch.device | str | None = None,
-                 device_cache: torch.device | str | None = None):
+                 device_cache: torch.device | str | None = None, feed_device: torch.device | str | None = None):
         if weight_files and len(weight_files) != len(files):
             raise ValueError("The numbers of train files and weight files do not match.")
         kinds = {bool(native.cpu().is_bin_file(f)) for f in files}
@@ -250,6 +250,12 @@ class NativeTextReader:
         if self.gpu is not None and self.gpu.type != "cuda":
             self.gpu = None
         self.fallbacks = 0
+        # feed_device (CPU parser, text files): the C++ feeder copies each parsed batch to this
+        # device from its own thread, so batches come out on the device like the tokenizer's
+        self.feed = None
+        if feed_device is not None and not self.binary and self.gpu is None:
+            fd = torch.device(feed_device)
+            self.feed = fd if fd.type == "cuda" else None
         self.dds = None
         if device_cache is not None and self.binary and torch.device(device_cache).type == "cuda":
             from .device_cache import DeviceDataset
@@ -274,16 +280,12 @@ class NativeTextReader:
         """Shuffle-window fill (0..1) at the loader's latest draw (-m "shuffle_queue")."""
         return float(self._loader.window_fill()) if self._loader is not None else 0.0
 
-    def _raw_slots(self) -> list[list[int]]:
-        """Page-locked output slots of the loader's raw mode (GPU tokenizer): batches are assembled
-        straight into them, so the host-to-device copy needs no staging copy.  queue_size + 3
-        slots (queued batches, the one being copied / parsed, the one being finished, one spare)
-        of twice the batch's estimated bytes (the longest average line over the heads of the
-        files: files of one run can differ, e.g. with and without values); a larger batch falls
-        back to a heap buffer (and, with the feeder, to the CPU parser)."""
-        if getattr(self, "_slots", None) is None:
+    def _estimate_slot_bytes(self) -> int:
+        """Bytes of one batch slot: twice the batch's estimated text bytes (the longest average
+        line over the heads of the files: files of one run can differ, e.g. with and without
+        values)."""
+        if getattr(self, "_slot_bytes", None) is None:
             B = self.args["batch_size"]
-            avg = 256.0
             est = []
             for path in self.args["files"][:64]:
                 try:
@@ -292,10 +294,19 @@ class NativeTextReader:
                     est.append(len(head) / max(1, head.count(b"\n")))
                 except OSError:
                     pass
-            if est:
-                avg = max(16.0, max(est))
-            nb, nl = int(B * avg * 2.0) + 4096, B + 1
-            self._slot_bytes = nb
+            avg = max(16.0, max(est)) if est else 256.0
+            self._slot_bytes = int(B * avg * 2.0) + 4096
+        return self._slot_bytes
+
+    def _raw_slots(self) -> list[list[int]]:
+        """Page-locked output slots of the loader's raw mode (GPU tokenizer): batches are assembled
+        straight into them, so the host-to-device copy needs no staging copy.  queue_size + 3
+        slots (queued batches, the one being copied / parsed, the one being finished, one spare)
+        of ``_estimate_slot_bytes``; a larger batch falls back to a heap buffer (and, with the
+        feeder, to the CPU parser)."""
+        if getattr(self, "_slots", None) is None:
+            B = self.args["batch_size"]
+            nb, nl = self._estimate_slot_bytes(), B + 1
             self._slots = [(torch.empty(nb, dtype=torch.uint8, pin_memory=True),
                             torch.empty(nl, dtype=torch.int64, pin_memory=True),
                             torch.empty(B, dtype=torch.float32, pin_memory=True))
@@ -305,9 +316,10 @@ class NativeTextReader:
 
     @property
     def inline(self) -> bool:
-        """Batches come out complete and on the device (GPU tokenizer fed by the C++ feeder thread):
-        a consumer needs no producer thread of its own (``Prefetcher`` iterates inline)."""
-        return self.gpu is not None and _feeder_available()
+        """Batches come out complete and on the device (GPU tokenizer or CPU parser, fed by the C++
+        feeder thread): a consumer needs no producer thread of its own (``Prefetcher`` iterates
+        inline)."""
+        return (self.gpu is not None or self.feed is not None) and _feeder_available()
 
     def __iter__(self):
         if self.inline:
@@ -359,8 +371,10 @@ class NativeTextReader:
         """Device buffers of one feeder slot: raw bytes / line starts / weights copied in, the
         tokenizer's CSR out (ids / values sized for the densest possible batch: a token takes >= 2
         bytes), its counts / status / scan workspace."""
-        dev, B, nb = self.gpu, self.args["batch_size"], self._slot_bytes
+        dev, B, nb = self._feed_dev, self.args["batch_size"], self._slot_bytes
         cap = nb // 2 + B + 1
+        if self.gpu is None:
+            nb = 1  # (parse mode: no raw bytes on the device)
         i32 = dict(dtype=torch.int32, device=dev)
         f32 = dict(dtype=torch.float32, device=dev)
         return dict(bytes=torch.empty(nb, dtype=torch.uint8, device=dev),
@@ -382,13 +396,16 @@ class NativeTextReader:
         this generator only wraps the slot's tensors.  A device slot is handed back when the batch
         object dies: the feeder's stream then waits for the work queued so far on the releasing
         thread's current stream (the step that read it) before overwriting the slot."""
-        slots = self._raw_slots()
+        raw = self.gpu is not None  # else the loader's CPU parser, the feeder copies the CSR over
+        slots = self._raw_slots() if raw else []
+        self._estimate_slot_bytes()
         L = native.cpu().TextLoader(start_epoch=self.state.epoch, skip_batches=self.state.batches_in_epoch,
-                                    raw=True, binary=False, rows=False, raw_slots=slots, **self.args)
+                                    raw=raw, binary=False, rows=False, raw_slots=slots, **self.args)
         self._loader = L
-        dev = self.gpu
+        dev = self.gpu if raw else self.feed
         if dev.index is None:
-            dev = self.gpu = torch.device("cuda", torch.cuda.current_device())
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self._feed_dev = dev
         F = native.hip().GpuTextFeeder(L.c_api(), dev.index, self.args["vocab_size"], self.args["hash_feature_id"])
         dslots = []
 

@@ -157,6 +157,7 @@ class Trainer:
         if c.loader == "native":
             reader = NativeTextReader(c.train_files, c.weight_files or None, c.batch_size,
                                       gpu_parse=self.device if c.gpu_parse else None,
+                                      feed_device=self.device if self.device.type == "cuda" else None,
                                       device_cache=self._device_cache(), **kw)
             if reader.dds is not None:
                 self.print(f"Training data resident on {self.device}: {reader.dds.N} examples, "

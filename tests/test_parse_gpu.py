@@ -99,6 +99,31 @@ def test_reader_gpu_parse_equals_cpu_parse(tmp_path):
         assert torch.equal(ax, bx)
 
 
+def test_reader_cpu_parse_fed_to_device_equals_host_batches(tmp_path):
+    """CPU parser + the C++ feeder (feed_device): the loader's CSR batches are copied to the device
+    by the feeder thread; they equal the host batches of the same reader configuration, and list()
+    holding every batch at once (more than the feeder's initial slots) still completes."""
+    files, wfiles = [], []
+    for i in range(2):
+        p, w = str(tmp_path / f"t{i}"), str(tmp_path / f"w{i}")
+        write_libsvm(p, 2500, shape="criteo", vocab_size=100_000, seed=i, weights_path=w, with_values=i == 0)
+        files.append(p)
+        wfiles.append(w)
+    kw = dict(vocab_size=100_000, num_epochs=2, seed=3, parse_threads=2)
+    host = list(NativeTextReader(files, wfiles, 600, **kw))
+    r = NativeTextReader(files, wfiles, 600, feed_device="cuda", **kw)
+    assert r.inline
+    dev = list(r)
+    assert len(host) == len(dev) > 6
+    for a, b in zip(host, dev):
+        assert a.reader_pos == b.reader_pos and a.nnz == b.nnz and b.ids.is_cuda and b.max_feats == a.max_feats
+        for x, y in ((a.labels, b.labels), (a.offsets, b.offsets), (a.ids, b.ids), (a.weights, b.weights)):
+            assert torch.equal(x, y.cpu())
+        assert (a.vals is None) == (b.vals is None)
+        if a.vals is not None:
+            assert torch.equal(a.vals, b.vals.cpu())
+
+
 def test_reader_gpu_parse_fallback_reports_errors(tmp_path):
     p = tmp_path / "bad"
     p.write_text("1 2 3\n1 2:xyz\n")

@@ -6,8 +6,9 @@ examples; students with fp32, bf16 + stochastic rounding and fp8 (e4m3 + per-row
 held-out logloss must agree with the fp32 student's within 0.5% (relative).  The fp32
 student must also beat the label-prior baseline clearly (the comparison is between models
 that actually learned something).  fp32 is the reference's precision
-(tffm/fm_model.py:269-284); the low-precision tables keep fp32 arithmetic, accumulators and
-optimizer state.  Adagrad (the reference optimizer) and FTRL (BASELINE config 5) both.
+(tffm/fm_model.py:269-284); the low-precision tables keep fp32 arithmetic and accumulation,
+bf16 tables fp32 optimizer state, fp8 tables bf16 optimizer state with stochastic rounding
+(ops/kernels.py state_dtype).  Adagrad (the reference optimizer) and FTRL (BASELINE config 5) both.
 """
 
 import math

@@ -11,3 +11,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-
 grep ms/step $OUT/prof.log
 python3 $R/tools/kstats.py $OUT/prof/run_kernel_stats.csv 25 > $OUT/kernel_summary.txt
 python3 $R/tools/timeline.py $OUT/prof/run_kernel_trace.csv $MARK > $OUT/timeline.txt
+rm -f $OUT/prof/*.csv  # (per-dispatch traces: keep the summaries, stay under gpurun's merge-back limit)
