@@ -1058,7 +1058,7 @@ class DPDenseExchange(DPExchange):
             nb_ready.record(main)
         pl = m._lpending
         if pl is not None and pl.b is b:
-            m._lpending = None
+            m._lpending, m._lpending2 = m._lpending2, None
         else:
             m._lpending = m._lpending2 = None
             pl = m._local_plan(b)
@@ -1075,9 +1075,17 @@ class DPDenseExchange(DPExchange):
             K.fm_backward(pl.dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT_TABLE, table=m.table.state,
                           grad_out=self.dense, reg_v=rv, reg_w=rw, partial=ws.bwd_partial,
                           dense_part=ws.dense_part, dense_stream=m._dense_stream(), dense_A=dA)
-        if next_batch is not None:
-            # the next batch's dedup (side stream) overlaps the collectives and the apply below
+        # the next batches' dedup (side stream) overlaps the collectives, the apply and -- depth 2,
+        # like the local step -- the next step's forward / backward
+        if next_batch is not None and (m._lpending is None or m._lpending.b is not next_batch):
             m._lpending = m._local_plan(next_batch, nb_ready)
+            m._lpending2 = None
+        if (next2 is not None and m._lpending is not None and m._lpending2 is None
+                and os.environ.get("FM_LOCAL_DEPTH2", "1") != "0"):
+            if getattr(next2, "ready", None) is None and nb_ready is None:
+                nb_ready = torch.cuda.Event()
+                nb_ready.record(main)
+            m._lpending2 = m._local_plan(next2, nb_ready)
         r0, S = self.r0, self.S
         own = self.dense[r0: r0 + S]
         if self.W > 1:

@@ -40,7 +40,7 @@ def workdir(tmp_path, ref_data_dir):
 
 def _write_cfg(workdir, **over):
     vals = dict(loss_type="logistic", batch_size=1000, epoch_num=2, save_steps=3, extra_train="",
-                log_dir=str(workdir / "log"), factor_num=8, extra_general="")
+                log_dir=str(workdir / "log"), factor_num=8, extra_general="", device="cpu")
     vals.update(over)
     text = f"""[General]
 vocabulary_size = 200000
@@ -49,7 +49,7 @@ factor_num = {vals['factor_num']}
 hash_feature_id = False
 log_dir = {vals['log_dir']}
 save_summaries_steps = 1
-device = cpu
+device = {vals['device']}
 {vals['extra_general']}
 
 [Train]
@@ -191,3 +191,21 @@ def test_trace_file_written(workdir):
     fills = [float(x) for x in re.findall(r"shuffle_queue: ([0-9.]+)%", out)]
     assert fills and all(0.0 <= f <= 100.0 for f in fills)
     assert len(set(fills)) > 1 or fills[0] < 100.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gpu_parse", [False, True], ids=["cpu_parser", "gpu_tokenizer"])
+def test_train_and_resume_on_gpu(workdir, gpu_parse):
+    """run.py train on the GPU with the file-fed input path (native loader + the C++ device
+    feeder: CPU parser or GPU tokenizer), stopped after 5 steps and auto-resumed to the end."""
+    cfg_path = _write_cfg(workdir, device="cuda", extra_train="gpu_parse = true" if gpu_parse else "")
+    rc, out = _run(["train", cfg_path, "--max-steps", "5"])
+    assert rc == 0
+    losses = [float(m) for m in re.findall(r"-- Global Step: \d+; Avg loss: ([0-9.]+);", out)]
+    assert len(losses) == 5
+    rc, out2 = _run(["train", cfg_path])
+    assert rc == 0 and "Restored checkpoint" in out2
+    steps2 = [int(m) for m in re.findall(r"-- Global Step: (\d+);", out2)]
+    assert steps2 == list(range(6, 13))
+    losses += [float(m) for m in re.findall(r"-- Global Step: \d+; Avg loss: ([0-9.]+);", out2)]
+    assert np.isfinite(losses).all() and np.mean(losses[-3:]) < np.mean(losses[:3])
