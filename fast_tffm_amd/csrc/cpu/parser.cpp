@@ -97,6 +97,77 @@ template <class IdVec>
 void parse_line_into(const char* s, size_t len, int64_t vocab_size, bool hash_feature_id, std::vector<float>& labels,
                      std::vector<int32_t>& sizes, IdVec& ids, std::vector<float>& vals, std::string& scratch);
 
+// The common case without a private copy of the line: plain decimal label / values, plain
+// digit ids (or hashed tokens), single spaces, no NUL byte.  Anything else -- including every
+// malformed line -- returns false with the outputs untouched, and the caller parses the line
+// with parse_line_general, whose results and error messages are the reference's.
+template <class IdVec>
+bool parse_line_fast(const char* s, size_t len, int64_t vocab_size, bool hash_feature_id, std::vector<float>& labels,
+                     std::vector<int32_t>& sizes, IdVec& ids, std::vector<float>& vals) {
+  if (len == 0 || std::memchr(s, 0, len) != nullptr) return false;
+  const char* const lim = s + len;
+  const char* p = s;
+  const char* e = nullptr;
+  float label;
+  if (!fast_parse_decimal(p, lim, &e, &label)) return false;
+  p = e;
+  const size_t mark = ids.size();
+  int32_t cnt = 0;
+  while (p < lim) {
+    if (*p != ' ') goto general;
+    ++p;
+    if (p == lim) break;  // one trailing space
+    {
+      int64_t id;
+      const char* q = p;
+      if (hash_feature_id) {
+        while (q < lim && *q != ' ' && *q != ':') ++q;
+        id = static_cast<int64_t>(hash64(p, static_cast<size_t>(q - p)) % static_cast<uint64_t>(vocab_size));
+      } else {
+        uint64_t v = 0;
+        int digits = 0;
+        while (q < lim && *q >= '0' && *q <= '9' && digits < 18) {
+          v = v * 10 + static_cast<unsigned>(*q - '0');
+          ++q;
+          ++digits;
+        }
+        if (digits == 0 || (q < lim && *q >= '0' && *q <= '9') || v >= static_cast<uint64_t>(vocab_size))
+          goto general;
+        id = static_cast<int64_t>(v);
+      }
+      p = q;
+      float fv = 1.f;
+      if (p < lim && *p == ':') {
+        ++p;
+        if (!fast_parse_decimal(p, lim, &e, &fv)) goto general;
+        p = e;
+      }
+      ids.push_back(static_cast<typename IdVec::value_type>(id));
+      vals.push_back(fv);
+      ++cnt;
+    }
+  }
+  labels.push_back(label);
+  sizes.push_back(cnt);
+  return true;
+general:
+  ids.resize(mark);
+  vals.resize(mark);
+  return false;
+}
+
+template <class IdVec>
+void parse_line_general(const char* s, size_t len, int64_t vocab_size, bool hash_feature_id,
+                        std::vector<float>& labels, std::vector<int32_t>& sizes, IdVec& ids, std::vector<float>& vals,
+                        std::string& scratch);
+
+template <class IdVec>
+void parse_line_into(const char* s, size_t len, int64_t vocab_size, bool hash_feature_id, std::vector<float>& labels,
+                     std::vector<int32_t>& sizes, IdVec& ids, std::vector<float>& vals, std::string& scratch) {
+  if (!parse_line_fast(s, len, vocab_size, hash_feature_id, labels, sizes, ids, vals))
+    parse_line_general(s, len, vocab_size, hash_feature_id, labels, sizes, ids, vals, scratch);
+}
+
 }  // namespace
 
 void parse_line(const char* s, size_t len, int64_t vocab_size, bool hash_feature_id, CsrBatch& out,
@@ -107,8 +178,9 @@ void parse_line(const char* s, size_t len, int64_t vocab_size, bool hash_feature
 namespace {
 
 template <class IdVec>
-void parse_line_into(const char* s, size_t len, int64_t vocab_size, bool hash_feature_id, std::vector<float>& labels,
-                     std::vector<int32_t>& sizes, IdVec& ids, std::vector<float>& vals, std::string& scratch) {
+void parse_line_general(const char* s, size_t len, int64_t vocab_size, bool hash_feature_id,
+                        std::vector<float>& labels, std::vector<int32_t>& sizes, IdVec& ids, std::vector<float>& vals,
+                        std::string& scratch) {
   scratch.assign(s, len);  // NUL-terminated private copy: strto* never read past the line
   const char* line = scratch.c_str();
   const char* const lim = line + len;
@@ -276,6 +348,10 @@ void parse_lines32(const char* const* ptrs, const size_t* lens, size_t n, int64_
     o.ids.reserve(bytes / 4 + 16); o.vals.reserve(bytes / 4 + 16);
     std::string scratch;
     for (size_t i = b; i < e; ++i) {
+      if (i + 6 < e) {  // lines are scattered over the mapped files: fetch a few ahead
+        const char* q = ptrs[i + 6];
+        for (size_t k = 0; k < lens[i + 6]; k += 64) __builtin_prefetch(q + k);
+      }
       try {
         parse_line_into(ptrs[i], lens[i], vocab_size, hash_feature_id, o.labels, o.sizes, o.ids, o.vals, scratch);
       } catch (const ParseError& ex) {
