@@ -126,6 +126,24 @@ bool parse_line_fast(const char* s, size_t len, int64_t vocab_size, bool hash_fe
       } else {
         uint64_t v = 0;
         int digits = 0;
+        if (lim - q >= 8) {  // up to 8 leading digits at once (SWAR), then the scalar loop
+          uint64_t w;
+          std::memcpy(&w, q, 8);
+          const uint64_t x = w - 0x3030303030303030ull;
+          // high bit of a byte: below '0' (borrow) or above '9' (+0x46 carries into it); a borrow
+          // only disturbs the bytes after the first non-digit, whose position is all that is used
+          const uint64_t nd = ((w + 0x4646464646464646ull) | x) & 0x8080808080808080ull;
+          const int lead = nd ? __builtin_ctzll(nd) >> 3 : 8;
+          if (lead > 0) {
+            uint64_t d = (x & 0x0F0F0F0F0F0F0F0Full) << (8 * (8 - lead));
+            d = (d * 2561) >> 8;
+            d = ((d & 0x00FF00FF00FF00FFull) * 6553601) >> 16;
+            d = ((d & 0x0000FFFF0000FFFFull) * 42949672960001ull) >> 32;
+            v = d;
+            digits = lead;
+            q += lead;
+          }
+        }
         while (q < lim && *q >= '0' && *q <= '9' && digits < 18) {
           v = v * 10 + static_cast<unsigned>(*q - '0');
           ++q;
@@ -173,6 +191,11 @@ void parse_line_into(const char* s, size_t len, int64_t vocab_size, bool hash_fe
 void parse_line(const char* s, size_t len, int64_t vocab_size, bool hash_feature_id, CsrBatch& out,
                 std::string& scratch) {
   parse_line_into(s, len, vocab_size, hash_feature_id, out.labels, out.sizes, out.ids, out.vals, scratch);
+}
+
+void parse_line_general_only(const char* s, size_t len, int64_t vocab_size, bool hash_feature_id, CsrBatch& out,
+                             std::string& scratch) {
+  parse_line_general(s, len, vocab_size, hash_feature_id, out.labels, out.sizes, out.ids, out.vals, scratch);
 }
 
 namespace {

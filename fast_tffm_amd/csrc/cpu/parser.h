@@ -39,6 +39,11 @@ struct CsrBatch {
 void parse_line(const char* s, size_t len, int64_t vocab_size, bool hash_feature_id, CsrBatch& out,
                 std::string& scratch);
 
+// The general (strto*-based) line parser alone, without the fast path: the fast path's
+// differential-test reference (tests/native/parser_fuzz.cpp).
+void parse_line_general_only(const char* s, size_t len, int64_t vocab_size, bool hash_feature_id, CsrBatch& out,
+                             std::string& scratch);
+
 // Per-thread scratch of parse_lines, reusable across calls (a long-lived caller,
 // e.g. the loader, keeps it so the pieces' memory stays mapped: no page faults).
 struct ParseWorkspace {

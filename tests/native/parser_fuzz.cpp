@@ -15,7 +15,35 @@
 
 #include "cpu/parser.h"
 
+// the fast line path (parse_line) must equal the general parser, results and error messages
+static int check_fast_vs_general(const std::string& l, long long vocab, bool hash) {
+  fm::CsrBatch a, b;
+  std::string sa, sb, ea, eb;
+  try {
+    fm::parse_line(l.data(), l.size(), vocab, hash, a, sa);
+  } catch (const fm::ParseError& e) {
+    ea = e.what();
+  }
+  try {
+    fm::parse_line_general_only(l.data(), l.size(), vocab, hash, b, sb);
+  } catch (const fm::ParseError& e) {
+    eb = e.what();
+  }
+  bool same = ea == eb && a.ids == b.ids && a.sizes == b.sizes && a.labels.size() == b.labels.size() &&
+              a.vals.size() == b.vals.size();
+  for (size_t i = 0; same && i < a.labels.size(); ++i) same = std::memcmp(&a.labels[i], &b.labels[i], 4) == 0;
+  for (size_t i = 0; same && i < a.vals.size(); ++i) same = std::memcmp(&a.vals[i], &b.vals[i], 4) == 0;
+  if (!same) {
+    std::fprintf(stderr, "fast path differs on '%s': '%s' vs '%s'\n", l.c_str(), ea.c_str(), eb.c_str());
+    return 1;
+  }
+  return 0;
+}
+
 static int check(const std::vector<std::string>& lines, long long vocab, bool hash, int threads) {
+  int bad = 0;
+  for (const auto& l : lines) bad += check_fast_vs_general(l, vocab, hash);
+  if (bad) return bad;
   std::vector<const char*> ptrs;
   std::vector<size_t> lens;
   for (const auto& l : lines) {
@@ -111,6 +139,20 @@ int main() {
       for (const auto& l : base) bad += check({l}, 1000, hash, th);
     }
   std::mt19937 rng(12345);
+  // ids of 1..20 digits around the 8-digit SWAR boundary, values and labels of every plain form
+  for (int it = 0; it < 50000; ++it) {
+    std::string l = (rng() % 2) ? "1" : "0.5";
+    const int nt = rng() % 6;
+    for (int t = 0; t < nt; ++t) {
+      l += ' ';
+      const int nd = 1 + rng() % 20;
+      for (int k = 0; k < nd; ++k) l += char('0' + rng() % 10);
+      if (rng() % 3 == 0) l += ":" + std::to_string(rng() % 1000) + ((rng() % 2) ? ".25" : "");
+    }
+    if (rng() % 7 == 0) l += ' ';
+    bad += check({l}, 1 + (long long)(rng() % 2000000000ll), false, 1);
+    if (bad > 20) break;
+  }
   const std::string alphabet = "0123456789 :.-+eE\tab\n";
   for (int it = 0; it < 20000; ++it) {
     std::string l = base[rng() % 4];
