@@ -193,11 +193,26 @@ def test_trace_file_written(workdir):
     assert len(set(fills)) > 1 or fills[0] < 100.0
 
 
+@pytest.fixture()
+def synth_workdir(tmp_path):
+    """Criteo-shaped synthetic train / weight / test files (no reference data needed: GPU boxes)."""
+    from fast_tffm_amd.data.synthetic import write_libsvm
+
+    d = tmp_path / "data"
+    d.mkdir()
+    for i in range(2):
+        write_libsvm(str(d / f"train_{i}"), 3000, shape="criteo", vocab_size=200_000, seed=i,
+                     weights_path=str(d / f"weight_{i}"))
+    write_libsvm(str(d / "test_0"), 1500, shape="criteo", vocab_size=200_000, seed=9)
+    return tmp_path
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("gpu_parse", [False, True], ids=["cpu_parser", "gpu_tokenizer"])
-def test_train_and_resume_on_gpu(workdir, gpu_parse):
+def test_train_and_resume_on_gpu(synth_workdir, gpu_parse):
     """run.py train on the GPU with the file-fed input path (native loader + the C++ device
     feeder: CPU parser or GPU tokenizer), stopped after 5 steps and auto-resumed to the end."""
+    workdir = synth_workdir
     cfg_path = _write_cfg(workdir, device="cuda", extra_train="gpu_parse = true" if gpu_parse else "")
     rc, out = _run(["train", cfg_path, "--max-steps", "5"])
     assert rc == 0
