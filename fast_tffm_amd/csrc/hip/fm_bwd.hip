@@ -82,6 +82,8 @@ struct BwdArgs {
   int* multi;               // [counts[2]] rows spanning more than one chunk (filled by the chunk kernel)
   int* counts_rw;           // == counts, writable (counts[2] = #multi, zeroed by the launcher)
   const int* dense_list;    // [kMaxDense] dense rows (dedup), counts[3] of them; null: no dense path
+  const int* dense_n;       // device scalar: number of dense rows (null: counts[3])
+  const int* hot_keys;      // hot rows (hot.hip): dense_list holds table rows, not segments; null: segments
   float* dense_part;        // [gridDim(dense) * kMaxDense, Kp + 4] per-workgroup partial rows
   int nex;                  // examples in the batch (dense path)
   const uint8_t* dense_A;   // [nex, kMaxDense] occurrence counts of the dense rows (written by the forward)
@@ -541,136 +543,93 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_big_kernel(BwdArgs a) {
 // with A[e, h] = occurrences of dense row h in example e (binary features, so
 // x = 1; counted by the forward kernel into a coalesced [B, 256] byte matrix).
 // Each workgroup owns a contiguous example range and streams it in 64-example
-// tiles: A^T and D are staged in LDS as bf16 images transposed so that every MFMA
-// operand fragment is one 16-byte read, and the product runs on
-// v_mfma_f32_16x16x32_bf16 with D split into three bf16 parts (hi + mid + lo carry
-// D's 24-bit mantissa; A's small integer counts are exact in bf16), accumulated in
-// fp32: the result matches an fp32 GEMM to fp32 accumulation error at 3/16 of the
-// fp32-MFMA cost.  r1 is read once, coalesced, instead of once per occurrence.
-// Per-workgroup partial rows are summed in a fixed order by
-// fm_bwd_dense_apply_kernel, which applies the optimizer (deterministic).
+// tiles through LDS -- A's rows as they are (bytes, pitch 272: conflict-free
+// reads) and D = [dpred * r1 | dpred | 1] as fp32 rows -- and multiplies on
+// v_mfma_f32_16x16x4_f32: its operand maps (A[l&15][k = l>>4], B[k = l>>4][l&15])
+// read both tiles in their natural example-major layout, so nothing is transposed,
+// and f32-in MFMA is exact fp32 (an fmaf chain).  The two extra D columns give
+// every row's Sc = sum_e A dpred and its occurrence count in the same product.
+// r1 is read once, coalesced, instead of once per occurrence.  Per-workgroup
+// partial rows are summed in a fixed order by fm_bwd_dense_apply_kernel, which
+// applies the optimizer (deterministic).  (Round 2's version split D into three
+// bf16 parts for v_mfma_f32_16x16x32_bf16 and transposed both tiles through LDS:
+// 356 us next to the chunk kernel, profiles/r3.)
 // ---------------------------------------------------------------------------
-constexpr int kDenseE = 64;                 // examples per staged tile (2 MFMA k-steps of 32)
-constexpr int kDenseEP = kDenseE + 8;       // LDS row pitch in bf16 (144 B: conflict-free 16-B fragment reads)
+constexpr int kDenseE = 64;                 // examples per staged tile (16 MFMA k-steps of 4)
+constexpr int kDenseAP = kMaxDense + 16;    // LDS pitch of an A row in bytes (272: rows 4 banks apart)
 constexpr int kDenseWG = 256;               // workgroups of the dense kernel (partial rows)
 static_assert(kMaxDense == 4 * kWave, "dense rows: 4 per lane in the forward's count rows, 64 per wave here");
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
-typedef short bf16x8 __attribute__((ext_vector_type(8)));
 
-template <int NB>  // 16-column blocks of Kp (Kp <= NB * 16)
+template <int NB>  // 16-column blocks of D (Kp + 2 <= NB * 16)
 __global__ __launch_bounds__(kBlock) void fm_bwd_dense_kernel(BwdArgs a) {
-  __shared__ __align__(16) uint16_t At[kMaxDense * kDenseEP];      // A^T tile: [dense row][example]
-  __shared__ __align__(16) uint16_t Dt[3 * NB * 16 * kDenseEP];    // D^T tile, 3 bf16 parts: [part][col][example]
-  __shared__ float dps[kDenseE];
-  const int nd = min(a.counts[3], kMaxDense);
+  constexpr int NC = NB * 16;
+  __shared__ __align__(16) uint8_t At[kDenseE * kDenseAP];   // A rows of the tile
+  __shared__ __align__(16) float Dt[kDenseE * NC];           // D rows of the tile
+  const int nd = min(a.dense_n ? *a.dense_n : a.counts[3], kMaxDense);
   if (nd == 0) return;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid >> 6;
   const int per = ((a.nex + (int)gridDim.x - 1) / (int)gridDim.x + kDenseE - 1) / kDenseE * kDenseE;
   const int e_begin = blockIdx.x * per, e_end = min(a.nex, e_begin + per);
+  const int Kp = a.Kp, kq = Kp / 4;
   floatx4 acc[4][NB];
 #pragma unroll
   for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) acc[rb][nb] = floatx4{0.f, 0.f, 0.f, 0.f};
-  float sc = 0.f;  // thread tid = dense row h: sum_e A[e, h] * dpred_e (= Sc = Scx for x = 1)
-  const int kq = a.Kp / 4;
+  const float* r1 = reinterpret_cast<const float*>(a.r1);
   for (int e0 = e_begin; e0 < e_end; e0 += kDenseE) {
-    // Staging writes pack two examples into one dword (lanes 0-31: consecutive example
-    // pairs -> consecutive dwords; lanes 32-63: rows 8 apart = 288 dwords = +32 banks), so
-    // every ds_write_b32 wave instruction is bank-conflict free.  (The first version wrote
-    // one bf16 per ds_write_b16 with 16 rows of one wave on one bank: 215 us for this kernel,
-    // profiles/r2/timeline_dense_v1.txt.)
-    const int ep = lane & 31, half = lane >> 5;
-    const int ea = e0 + 2 * ep, eb = ea + 1;
-    // A^T: wave wv, pass it: dense rows 16 q .. 16 q + 15 with q = 4 it + wv; 8 of them per lane
-    for (int it = 0; it < kMaxDense / 64; ++it) {
-      const int q = 4 * it + wv;
-      const int hb = 16 * q + 8 * half;
-      uint2 ca = make_uint2(0u, 0u), cb = make_uint2(0u, 0u);
-      if (ea < e_end) ca = *reinterpret_cast<const uint2*>(a.dense_A + (long long)ea * kMaxDense + hb);
-      if (eb < e_end) cb = *reinterpret_cast<const uint2*>(a.dense_A + (long long)eb * kMaxDense + hb);
+    // A: 64 rows x 256 bytes, 64 bytes per thread (four 16-byte loads)
+    {
+      const int row = tid >> 2, seg = (tid & 3) * 64;
+      const int e = e0 + row;
+      uint4 q[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t xa = ((j < 4 ? ca.x : ca.y) >> (8 * (j & 3))) & 0xffu;
-        const uint32_t xb = ((j < 4 ? cb.x : cb.y) >> (8 * (j & 3))) & 0xffu;
-        const uint32_t pk = f32_to_bf16_bits((float)xa) | (f32_to_bf16_bits((float)xb) << 16);  // exact
-        *reinterpret_cast<uint32_t*>(At + (hb + j) * kDenseEP + 2 * ep) = pk;
+      for (int k = 0; k < 4; ++k) {
+        q[k] = make_uint4(0u, 0u, 0u, 0u);
+        if (e < e_end) q[k] = *reinterpret_cast<const uint4*>(a.dense_A + (long long)e * kMaxDense + seg + 16 * k);
       }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) *reinterpret_cast<uint4*>(At + row * kDenseAP + seg + 16 * k) = q[k];
     }
-    // D^T = (dpred * r1)^T as hi / mid / lo bf16 parts: lane = (example pair, column quad);
-    // the two lane halves take column quads 2 apart (rows 8 apart)
-    for (int cq = wv; cq < 2 * NB; cq += kWavesPerBlock) {  // pairs of column quads {4c+0|4c+2, ...}
-      const int qd = (cq / 2) * 4 + (cq & 1) + 2 * half;     // column quad: columns 4 qd .. 4 qd + 3
-      float fa[4] = {0.f, 0.f, 0.f, 0.f}, fb[4] = {0.f, 0.f, 0.f, 0.f};
-      if (qd < kq) {
-        if (ea < e_end) {
-          const float d = a.dpred[ea];
-          const float4 r = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.r1) + (long long)ea * a.Kp + 4 * qd);
-          fa[0] = d * r.x; fa[1] = d * r.y; fa[2] = d * r.z; fa[3] = d * r.w;
-        }
-        if (eb < e_end) {
-          const float d = a.dpred[eb];
-          const float4 r = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.r1) + (long long)eb * a.Kp + 4 * qd);
-          fb[0] = d * r.x; fb[1] = d * r.y; fb[2] = d * r.z; fb[3] = d * r.w;
+    // D: row e = [dpred_e * r1_e (Kp) | dpred_e | 1 | 0 ...], a float4 quad per thread and step
+    for (int i = tid; i < kDenseE * (NC / 4); i += kBlock) {
+      const int row = i / (NC / 4), qd = i % (NC / 4);
+      const int e = e0 + row;
+      float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < e_end) {
+        const float d = a.dpred[e];
+        if (qd < kq) {
+          const float4 r = *reinterpret_cast<const float4*>(r1 + (long long)e * Kp + 4 * qd);
+          f = make_float4(d * r.x, d * r.y, d * r.z, d * r.w);
+        } else if (qd == kq) {
+          f = make_float4(d, 1.f, 0.f, 0.f);
         }
       }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = 4 * qd + j;
-        if (n >= NB * 16) continue;
-        uint32_t pa[3], pb[3];
-        {
-          pa[0] = f32_to_bf16_bits(fa[j]);
-          const float r = fa[j] - bf16_bits_to_f32(pa[0]);
-          pa[1] = f32_to_bf16_bits(r);
-          pa[2] = f32_to_bf16_bits(r - bf16_bits_to_f32(pa[1]));
-        }
-        {
-          pb[0] = f32_to_bf16_bits(fb[j]);
-          const float r = fb[j] - bf16_bits_to_f32(pb[0]);
-          pb[1] = f32_to_bf16_bits(r);
-          pb[2] = f32_to_bf16_bits(r - bf16_bits_to_f32(pb[1]));
-        }
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-          *reinterpret_cast<uint32_t*>(Dt + ((p * NB * 16) + n) * kDenseEP + 2 * ep) = pa[p] | (pb[p] << 16);
-      }
+      *reinterpret_cast<float4*>(Dt + row * NC + 4 * qd) = f;
     }
-    if (tid < kDenseE) dps[tid] = e0 + tid < e_end ? a.dpred[e0 + tid] : 0.f;
     __syncthreads();
-    if (tid < nd) {  // 16-byte reads of the row (16 rows per lane group: conflict free)
-      const bf16x8* row = reinterpret_cast<const bf16x8*>(At + tid * kDenseEP);
+    // G[h, n] += sum_e A[e, h] D[e, n]; wave wv owns dense rows 64 wv .. 64 wv + 63
+#pragma unroll 4
+    for (int ks = 0; ks < kDenseE / 4; ++ks) {
+      const int er = 4 * ks + (lane >> 4);
+      float af[4], bf[NB];
 #pragma unroll
-      for (int c8 = 0; c8 < kDenseE / 8; ++c8) {
-        const bf16x8 v8 = row[c8];
+      for (int rb = 0; rb < 4; ++rb) af[rb] = (float)At[er * kDenseAP + 64 * wv + 16 * rb + (lane & 15)];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) sc += bf16_bits_to_f32((uint16_t)v8[j]) * dps[8 * c8 + j];
-      }
-    }
-    // G[h, n] += sum_e A^T[h, e] D^T[n, e]; wave wv owns dense rows 64 wv .. 64 wv + 63
-#pragma unroll
-    for (int ks = 0; ks < kDenseE / 32; ++ks) {
-      const int kofs = 32 * ks + 8 * (lane >> 4);
-      bf16x8 af[4];
+      for (int nb = 0; nb < NB; ++nb) bf[nb] = Dt[er * NC + 16 * nb + (lane & 15)];
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb)
-        af[rb] = *reinterpret_cast<const bf16x8*>(At + (64 * wv + 16 * rb + (lane & 15)) * kDenseEP + kofs);
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb) {
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(Dt + ((p * NB + nb) * 16 + (lane & 15)) * kDenseEP + kofs);
-#pragma unroll
-          for (int rb = 0; rb < 4; ++rb)
-            acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[rb], bfr, acc[rb][nb], 0, 0, 0);
-        }
-      }
+        for (int nb = 0; nb < NB; ++nb)
+          acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[rb], bf[nb], acc[rb][nb], 0, 0, 0);
     }
     __syncthreads();
   }
-  // partial rows: C/D map of the 16x16 tiles: col = lane & 15, row = (lane >> 4) * 4 + i
-  const int PS = a.Kp + 4;
+  // partial rows [G (Kp) | Sc | Sc | count | -]: C/D map of the 16x16 tiles: col = lane & 15,
+  // row = (lane >> 4) * 4 + i
+  const int PS = Kp + 4;
   float* part = a.dense_part + (long long)blockIdx.x * kMaxDense * PS;
 #pragma unroll
   for (int rb = 0; rb < 4; ++rb)
@@ -679,12 +638,18 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_dense_kernel(BwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = 64 * wv + 16 * rb + (lane >> 4) * 4 + i, n = nb * 16 + (lane & 15);
-        if (m < nd && n < a.Kp) part[(long long)m * PS + n] = acc[rb][nb][i];
+        if (m >= nd || n > Kp + 1) continue;
+        float* pr = part + (long long)m * PS;
+        const float v = acc[rb][nb][i];
+        if (n < Kp) {
+          pr[n] = v;
+        } else if (n == Kp) {
+          pr[Kp] = v;
+          pr[Kp + 1] = v;
+        } else {
+          pr[Kp + 2] = v;
+        }
       }
-  if (tid < nd) {
-    part[(long long)tid * PS + a.Kp] = sc;
-    part[(long long)tid * PS + a.Kp + 1] = sc;
-  }
 }
 
 // One workgroup per dense row: ordered sum of the per-workgroup partials
@@ -695,7 +660,7 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_dense_apply_kernel(BwdArgs a) {
   constexpr int EPL = Frag<TV>::N;
   __shared__ float4 red[kWavesPerBlock][kWave];
   __shared__ float row[kWave * 4];
-  const int nd = min(a.counts[3], kMaxDense);
+  const int nd = min(a.dense_n ? *a.dense_n : a.counts[3], kMaxDense);
   const int h = blockIdx.x;
   if (h >= nd) return;
   const int tid = threadIdx.x, q = tid & (kWave - 1), stripe = tid >> 6;
@@ -727,8 +692,15 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_dense_apply_kernel(BwdArgs a) {
     float A[EPL];
 #pragma unroll
     for (int k = 0; k < EPL; ++k) A[k] = row[tE * EPL + k];
-    const int u = a.dense_list[h];
-    bwd_finalize<LPR, TV, EPL>(a, u, t, tact, tE, A, row[a.Kp], row[a.Kp + 1], a.seg_start[u + 1] - a.seg_start[u], sr);
+    if (a.hot_keys) {  // hot row (local step): table row key, occurrences from the GEMM's count column
+      RowState<EPL> r;
+      bwd_load<TV, EPL>(a, 0, (long long)a.hot_keys[h], tE, r);
+      bwd_finish<LPR, TV, EPL>(a, 0, t, tact, r, A, row[a.Kp], row[a.Kp + 1], (int)(row[a.Kp + 2] + 0.5f), sr);
+    } else {
+      const int u = a.dense_list[h];
+      bwd_finalize<LPR, TV, EPL>(a, u, t, tact, tE, A, row[a.Kp], row[a.Kp + 1], a.seg_start[u + 1] - a.seg_start[u],
+                                 sr);
+    }
   }
 }
 
@@ -777,7 +749,7 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
       (void)hipEventRecord(dense_fork_event(), st);
       (void)hipStreamWaitEvent(ds, dense_fork_event(), 0);
     }
-    switch ((a.Kp + 15) / 16) {
+    switch ((a.Kp + 2 + 15) / 16) {  // D columns: Kp + dpred + 1
       case 1: hipLaunchKernelGGL(fm_bwd_dense_kernel<1>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
       case 2: hipLaunchKernelGGL(fm_bwd_dense_kernel<2>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
       case 3: hipLaunchKernelGGL(fm_bwd_dense_kernel<3>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
@@ -785,7 +757,8 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
       case 5: hipLaunchKernelGGL(fm_bwd_dense_kernel<5>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
       case 6: hipLaunchKernelGGL(fm_bwd_dense_kernel<6>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
       case 7: hipLaunchKernelGGL(fm_bwd_dense_kernel<7>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
-      default: hipLaunchKernelGGL(fm_bwd_dense_kernel<8>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
+      case 8: hipLaunchKernelGGL(fm_bwd_dense_kernel<8>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
+      default: hipLaunchKernelGGL(fm_bwd_dense_kernel<9>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
     }
     if (fork) (void)hipEventRecord(dense_join_event(), ds);
   }

@@ -23,6 +23,7 @@ using u64 = std::uintptr_t;
 // Unity build: all kernel sources are compiled in this translation unit.
 #include "fm_bwd.hip"
 #include "fm_fwd.hip"
+#include "hot.hip"
 #include "dedup.hip"
 #include "shard.hip"
 #include "init.hip"
@@ -133,9 +134,12 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
          u64 dense_part, int nex, u64 dense_stream, int dtype,
          long long max_chunks, long long max_unique, u64 stream, int g_wcol, int g_bf16, u64 sr_counter,
          int counters_ready, u64 seg_bounds, int piece, int n_owners, u64 dense_A,
-         const std::vector<long long>& self, int chunk_grid) {
+         const std::vector<long long>& self, int chunk_grid, u64 dense_n, u64 hot_keys) {
         fm::BwdArgs a{};
         a.chunk_grid = chunk_grid;
+        a.dense_n = P<const int>(dense_n);
+        a.hot_keys = P<const int>(hot_keys);
+        if (hot_keys && (mode != 0 || !dense_n)) throw std::runtime_error("fm_bwd: hot rows are a LOCAL-mode path with a count");
         a.self = self_rows(self);
         if (a.self.u1 > a.self.u0 && a.self.keys != P<const int>(uniq))
           throw std::runtime_error("fm_bwd: self-row keys must be the dedup's unique keys");
@@ -174,9 +178,21 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("max_chunks"), py::arg("max_unique"), py::arg("stream"), py::arg("g_wcol") = -1,
       py::arg("g_bf16") = 0, py::arg("sr_counter") = 0, py::arg("counters_ready") = 0, py::arg("seg_bounds") = 0,
       py::arg("piece") = -1, py::arg("n_owners") = 0, py::arg("dense_A") = 0,
-      py::arg("self_rows") = std::vector<long long>{}, py::arg("chunk_grid") = 0);
+      py::arg("self_rows") = std::vector<long long>{}, py::arg("chunk_grid") = 0, py::arg("dense_n") = 0,
+      py::arg("hot_keys") = 0);
 
   m.def("dedup_workspace_bytes", &fm::dedup_workspace_bytes, py::arg("n"));
+  // hot-row filter of the dedup input (hot.hip): kept (key, code) pairs in CSR order + their count
+  m.def(
+      "hot_filter",
+      [](int B, u64 offsets, u64 ids, u64 hot, u64 hot_n, int slot_bits, u64 gcnt, u64 keys_out, u64 codes_out,
+         u64 n_out, u64 stream) {
+        fm::HotFilterArgs a{B, P<const int>(offsets), P<const int>(ids), P<const int>(hot), P<const int>(hot_n),
+                            slot_bits, P<int>(gcnt), P<int>(keys_out), P<int>(codes_out), P<int>(n_out)};
+        check(fm::launch_hot_filter(a, S(stream)), "hot_filter");
+      },
+      py::arg("B"), py::arg("offsets"), py::arg("ids"), py::arg("hot"), py::arg("hot_n"), py::arg("slot_bits"),
+      py::arg("gcnt"), py::arg("keys_out"), py::arg("codes_out"), py::arg("n_out"), py::arg("stream"));
 
   m.def(
       "dedup",

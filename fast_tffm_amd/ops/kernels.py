@@ -163,7 +163,8 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
                partial: torch.Tensor | None = None, threads: int = 0,
                bias: torch.Tensor | None = None, dense: "DedupOut | None" = None,
                dense_A: torch.Tensor | None = None, dense_by_segment: bool = False,
-               self_rows: SelfRows | None = None, seg_lookup: "SegIndex | None" = None) -> FwdOut:
+               self_rows: SelfRows | None = None, seg_lookup: "SegIndex | None" = None,
+               hot: HotRows | None = None) -> FwdOut:
     """FM score of a CSR batch (reference FmScorer, cc/fm_scorer_op.h:101-140), fused with the loss.
 
     pred_i = sum_j x_j w_j + 1/2 sum_k [(sum_j x_j v_jk)^2 - sum_j x_j^2 v_jk^2]  (+ bias[0], optional
@@ -178,6 +179,8 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
     ``self_rows`` (GPU, ``rows`` = segment ids): segments in its range read this rank's table.
     ``seg_lookup`` (GPU): ``rows`` are the dedup's keys and every occurrence's segment (its
     row of ``v``) is found through the bucket index (``seg_index``) instead of an inverse map.
+    ``hot`` (GPU, with ``dense_A``): count the occurrences of these table rows instead of a
+    dedup's dense rows.
     """
     dev = rows.device
     B = offsets.numel() - 1
@@ -226,6 +229,11 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
                    and dense_A.shape[0] >= B, "dense_A: contiguous uint8 [>= B, MAX_DENSE]")
             dkw = dict(dense_list=_p(dense.dense_list), dense_uniq=0 if dense_by_segment else _p(dense.uniq),
                        dense_count=_p(dense.counts) + 12, dense_A=_p(dense_A))
+        elif hot is not None and dense_A is not None:
+            _check(vals is None, "hot-row counts are for binary-feature batches (vals is None)")
+            _check(dense_A.dtype == torch.uint8 and dense_A.is_contiguous() and dense_A.shape[1] == MAX_DENSE
+                   and dense_A.shape[0] >= B, "dense_A: contiguous uint8 [>= B, MAX_DENSE]")
+            dkw = dict(dense_list=_p(hot.keys), dense_uniq=0, dense_count=_p(hot.n), dense_A=_p(dense_A))
         if self_rows is not None and self_rows.u1 > self_rows.u0:
             _self_check(self_rows, v, None)
             dkw["self_rows"] = self_rows.packed()
@@ -347,6 +355,61 @@ def csr_rows(offsets: torch.Tensor, out: torch.Tensor | None = None, nnz: int | 
 
 MAX_DENSE = 256            # = fm::kMaxDense: rows on the MFMA backward path
 DENSE_WG = 256             # = fm::kDenseWG: workgroups (partial rows) of the dense kernel
+
+
+@dataclass
+class HotRows:
+    """A set of <= MAX_DENSE hot table rows of the local step (hip/hot.hip): their occurrences
+    are filtered out of the dedup input, counted per example by the forward into ``dense_A`` and
+    reduced by the dense-row GEMM.  ``keys`` int32 [MAX_DENSE] (first ``n`` valid, ascending),
+    ``n`` int32 [1] on the device (kernels read it there), ``n_host`` the same on the host."""
+
+    keys: torch.Tensor
+    n: torch.Tensor
+    n_host: int = 0
+
+    @staticmethod
+    def empty(dev) -> "HotRows":
+        return HotRows(torch.zeros(MAX_DENSE, dtype=torch.int32, device=dev),
+                       torch.zeros(1, dtype=torch.int32, device=dev), 0)
+
+    def set(self, keys: torch.Tensor) -> None:
+        """Load (host or device) keys, <= MAX_DENSE distinct table rows; stored ascending."""
+        k = torch.sort(keys.to(torch.int64).flatten().cpu()).values
+        _check(k.numel() <= MAX_DENSE, f"at most {MAX_DENSE} hot rows")
+        _check(k.numel() < 2 or bool((k[1:] > k[:-1]).all()), "hot rows must be distinct")
+        buf = torch.zeros(MAX_DENSE, dtype=torch.int32)
+        buf[: k.numel()] = k.to(torch.int32)
+        self.keys.copy_(buf, non_blocking=False)
+        self.n.fill_(int(k.numel()))
+        self.n_host = int(k.numel())
+
+    def copy_from(self, other: "HotRows") -> None:
+        """Snapshot ``other`` on the current stream (plans keep the set they were filtered with)."""
+        self.keys.copy_(other.keys, non_blocking=True)
+        self.n.copy_(other.n, non_blocking=True)
+        self.n_host = other.n_host
+
+
+def hot_filter(offsets: torch.Tensor, ids: torch.Tensor, hot: HotRows, *, slot_bits: int, gcnt: torch.Tensor,
+               keys_out: torch.Tensor, codes_out: torch.Tensor, n_out: torch.Tensor) -> None:
+    """Dedup input without the hot rows' occurrences (GPU, hip/hot.hip): ``keys_out`` / ``codes_out``
+    get the kept (table row, packed occurrence code) pairs in CSR order, ``n_out`` (int32 [1],
+    device) their number.  ``gcnt``: int32 scratch of >= ceil(B / 64)."""
+    B = offsets.numel() - 1
+    dev = offsets.device
+    _check(_is_gpu(offsets), "hot_filter is a GPU path")
+    _chk_vec(offsets, torch.int32, B + 1, "offsets", dev)
+    nnz = ids.numel()
+    _chk_vec(ids, torch.int32, nnz, "ids", dev)
+    _check(gcnt.dtype == torch.int32 and gcnt.numel() >= (B + 63) // 64, "gcnt: int32 [>= ceil(B / 64)]")
+    for name, t in (("keys_out", keys_out), ("codes_out", codes_out)):
+        _check(t.dtype == torch.int32 and t.numel() >= nnz and t.device == dev, f"{name}: int32 [>= nnz]")
+    _check(n_out.dtype == torch.int32 and n_out.numel() >= 1, "n_out: int32 [1]")
+    _check(slot_bits >= 0 and (B << slot_bits) < 2 ** 31, "packed codes must fit int32")
+    native.hip().hot_filter(B=B, offsets=_p(offsets), ids=_p(ids), hot=_p(hot.keys), hot_n=_p(hot.n),
+                            slot_bits=int(slot_bits), gcnt=_p(gcnt), keys_out=_p(keys_out),
+                            codes_out=_p(codes_out), n_out=_p(n_out), stream=_stream(offsets))
 
 
 def dense_min_for(num_examples: int, Kp: int, CH: int = 32, *, has_vals: bool = False,
@@ -533,7 +596,8 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
                 dense_part: torch.Tensor | None = None, dense_stream=None,
                 grad_bf16: bool = False, sr_counter: torch.Tensor | None = None,
                 seg_bounds: torch.Tensor | None = None, piece: int = -1,
-                dense_A: torch.Tensor | None = None, self_rows: SelfRows | None = None) -> torch.Tensor | None:
+                dense_A: torch.Tensor | None = None, self_rows: SelfRows | None = None,
+                hot: HotRows | None = None) -> torch.Tensor | None:
     """Segmented FM backward over the dedup grouping (reference FmGrad, cc/fm_grad_op.h:59-163).
 
     Per unique row u with occurrences (i, x):
@@ -546,6 +610,8 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
     second part (split backward of the row-sharded exchange); piece 1 must follow piece 0.
     ``self_rows`` (GPU, EMIT): segments in its range are read from its table; the exclusive ones
     get ``opt`` applied in place (with ``sr_counter``) and no gradient row.
+    ``hot`` (GPU, LOCAL, with the forward's ``dense_A``): rows filtered out of ``dd`` (``hot_filter``)
+    whose gradient comes from the dense-row GEMM; ``opt`` is applied to them here too.
     """
     dev = dpred.device
     _check(dd.sorted_ex is not None, "dedup must be run with ex_of_occ")
@@ -594,7 +660,10 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
             s_stride = s0v.stride(0)
     v_stride = _chk_rows(v, Kp, "v")
     _check(r1.dtype == r1_dtype(v.dtype), f"r1: {r1_dtype(v.dtype)} for {v.dtype} rows (the forward's r1)")
-    _check(r1.dtype == torch.float32 or dd.dense_list is None, "the dense-row MFMA backward reads an fp32 r1")
+    _check(r1.dtype == torch.float32 or (dd.dense_list is None and hot is None),
+           "the dense-row MFMA backward reads an fp32 r1")
+    _check(hot is None or (mode == BWD_LOCAL and dd.dense_list is None and _is_gpu(dpred) and Kp <= 128),
+           "hot rows: GPU LOCAL step, Kp <= 128, no dedup dense rows")
     o = opt or OptConfig()
     if piece >= 0:
         _check(_is_gpu(dpred) and seg_bounds is not None and mode == BWD_EMIT and dd.dense_list is None,
@@ -606,7 +675,7 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
             partial = torch.empty((partial_rows(dd.n, dd.CH), Kp + 4), dtype=torch.float32, device=dev)
         _check(partial.numel() >= partial_rows(dd.n, dd.CH) * (Kp + 4), "partial scratch too small")
         dp = None
-        if dd.dense_list is not None:  # MFMA path for the dense rows (counts written by the forward)
+        if dd.dense_list is not None or hot is not None:  # MFMA path (counts written by the forward)
             _check(dense_A is not None and dense_A.dtype == torch.uint8 and dense_A.shape[1] == MAX_DENSE
                    and dense_A.shape[0] >= dpred.numel(), "dense rows need the forward's dense_A counts")
             dp = dense_part if dense_part is not None else torch.empty(
@@ -624,7 +693,8 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               s_stride=s_stride, s0w=_p(s0w), s1w=_p(s1w), reg_v=float(reg_v), reg_w=float(reg_w),
               opt_type=o.code, lr=float(o.lr), l1=float(o.l1), l2=float(o.l2), beta=float(o.beta),
               grad_out=gptr, g_stride=gstride, partial=_p(partial), big_list=_p(dd.big_list),
-              big_count=_p(dd.big_count), multi=_p(dd.multi), dense_list=_p(dd.dense_list),
+              big_count=_p(dd.big_count), multi=_p(dd.multi),
+              dense_list=_p(hot.keys) if hot is not None else _p(dd.dense_list),
               dense_part=_p(dp), nex=int(dpred.numel()),
               dense_stream=dense_stream.cuda_stream if dense_stream is not None else 0, dtype=dt, max_chunks=dd.n,
               max_unique=dd.n,
@@ -632,8 +702,10 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               sr_counter=_p(sr_counter), counters_ready=int(bool(dd.bwd_fresh)),
               seg_bounds=_p(seg_bounds), piece=int(piece),
               n_owners=(seg_bounds.numel() - 1) // 2 if seg_bounds is not None else 0,
-              dense_A=_p(dense_A) if dd.dense_list is not None else 0,
-              chunk_grid=int(os.environ.get("FM_CHUNK_GRID", "0")), **skw)
+              dense_A=_p(dense_A) if (dd.dense_list is not None or hot is not None) else 0,
+              chunk_grid=int(os.environ.get("FM_CHUNK_GRID", "0")),
+              dense_n=_p(hot.n) if hot is not None else 0, hot_keys=_p(hot.keys) if hot is not None else 0,
+              **skw)
         dd.bwd_fresh = False  # a second backward over this grouping zeroes its counters itself
     else:
         _check(self_rows is None, "self rows are a GPU path")
