@@ -273,11 +273,12 @@ class DedupOut:
     ``num_unique`` is a view of counts[0]; ``U_host`` is set on CPU and after
     ``.sync()``.  ``perm`` is the sorted payload: the occurrence index, unless
     the dedup ran with the example index as payload (then ``sorted_ex is perm``).
+    ``hot``: the HotRows set whose occurrences were filtered out of this grouping (or None).
     """
 
     __slots__ = ("n", "skeys", "perm", "uniq", "seg_start", "seg_chunk", "chunk_start", "chunk_seg", "chunk_key",
                  "counts", "num_unique", "inv", "sorted_ex", "sorted_x", "U_host", "CH", "big_list", "big_count",
-                 "multi", "ex_shift", "dense_list", "bwd_fresh")
+                 "multi", "ex_shift", "dense_list", "bwd_fresh", "hot")
 
     def __init__(self, **kw):
         for k in self.__slots__:
