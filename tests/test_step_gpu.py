@@ -133,8 +133,10 @@ def test_dense_mfma_backward_is_deterministic(monkeypatch):
         assert torch.equal(x, y)
 
 
-def test_local_lookahead_matches_plain_steps_bitwise():
-    """Eager lookahead (next batch's dedup on the side stream during this step) == plain steps."""
+def test_local_lookahead_matches_plain_steps_bitwise(monkeypatch):
+    """Eager lookahead (next batch's dedup on the side stream during this step) == plain steps.
+    (Hot rows off: the plain step has none; tests/test_hot_rows_gpu.py covers them.)"""
+    monkeypatch.setenv("FM_HOT_ROWS", "0")
     gen = CriteoSynth(20000, device="cuda", seed=15)
     batches = [gen.batch(1024) for _ in range(4)]
     a, b = _model(), _model()
