@@ -562,7 +562,7 @@ static_assert(kMaxDense == 4 * kWave, "dense rows: 4 per lane in the forward's c
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-template <int NB>  // 16-column blocks of D (Kp + 2 <= NB * 16)
+template <int NB, bool R1B>  // 16-column blocks of D (Kp + 2 <= NB * 16); R1B: bf16 r1 (fp8 tables)
 __global__ __launch_bounds__(kBlock) void fm_bwd_dense_kernel(BwdArgs a) {
   constexpr int NC = NB * 16;
   __shared__ __align__(16) uint8_t At[kDenseE * kDenseAP];   // A rows of the tile
@@ -578,7 +578,6 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_dense_kernel(BwdArgs a) {
   for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) acc[rb][nb] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const float* r1 = reinterpret_cast<const float*>(a.r1);
   for (int e0 = e_begin; e0 < e_end; e0 += kDenseE) {
     // A: 64 rows x 256 bytes, 64 bytes per thread (four 16-byte loads)
     {
@@ -601,8 +600,9 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_dense_kernel(BwdArgs a) {
       if (e < e_end) {
         const float d = a.dpred[e];
         if (qd < kq) {
-          const float4 r = *reinterpret_cast<const float4*>(r1 + (long long)e * Kp + 4 * qd);
-          f = make_float4(d * r.x, d * r.y, d * r.z, d * r.w);
+          float r[4];
+          load_r1<typename std::conditional<R1B, fp8e4m3, float>::type, 4>(a.r1, (long long)e * Kp + 4 * qd, r);
+          f = make_float4(d * r[0], d * r[1], d * r[2], d * r[3]);
         } else if (qd == kq) {
           f = make_float4(d, 1.f, 0.f, 0.f);
         }
@@ -744,22 +744,31 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   const bool fork = dense && dense_st && dense_st != st;
   hipStream_t ds = fork ? dense_st : st;
   if (dense) {
-    if (a.Kp > 128 || a.Kp % 4 != 0 || dtype == kFP8) return -5;  // (fp32 r1 only: not with fp8 tables)
+    if (a.Kp > 128 || a.Kp % 4 != 0) return -5;
     if (fork) {
       (void)hipEventRecord(dense_fork_event(), st);
       (void)hipStreamWaitEvent(ds, dense_fork_event(), 0);
     }
+    const bool r1b = dtype == kFP8;  // (fp8 tables keep a bf16 r1: fm_common.h R1Bf16)
+#define FM_DENSE_LAUNCH(NB)                                                                          \
+  do {                                                                                               \
+    if (r1b)                                                                                         \
+      hipLaunchKernelGGL((fm_bwd_dense_kernel<NB, true>), dim3(kDenseWG), dim3(kBlock), 0, ds, a);   \
+    else                                                                                             \
+      hipLaunchKernelGGL((fm_bwd_dense_kernel<NB, false>), dim3(kDenseWG), dim3(kBlock), 0, ds, a);  \
+  } while (0)
     switch ((a.Kp + 2 + 15) / 16) {  // D columns: Kp + dpred + 1
-      case 1: hipLaunchKernelGGL(fm_bwd_dense_kernel<1>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
-      case 2: hipLaunchKernelGGL(fm_bwd_dense_kernel<2>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
-      case 3: hipLaunchKernelGGL(fm_bwd_dense_kernel<3>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
-      case 4: hipLaunchKernelGGL(fm_bwd_dense_kernel<4>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
-      case 5: hipLaunchKernelGGL(fm_bwd_dense_kernel<5>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
-      case 6: hipLaunchKernelGGL(fm_bwd_dense_kernel<6>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
-      case 7: hipLaunchKernelGGL(fm_bwd_dense_kernel<7>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
-      case 8: hipLaunchKernelGGL(fm_bwd_dense_kernel<8>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
-      default: hipLaunchKernelGGL(fm_bwd_dense_kernel<9>, dim3(kDenseWG), dim3(kBlock), 0, ds, a); break;
+      case 1: FM_DENSE_LAUNCH(1); break;
+      case 2: FM_DENSE_LAUNCH(2); break;
+      case 3: FM_DENSE_LAUNCH(3); break;
+      case 4: FM_DENSE_LAUNCH(4); break;
+      case 5: FM_DENSE_LAUNCH(5); break;
+      case 6: FM_DENSE_LAUNCH(6); break;
+      case 7: FM_DENSE_LAUNCH(7); break;
+      case 8: FM_DENSE_LAUNCH(8); break;
+      default: FM_DENSE_LAUNCH(9); break;
     }
+#undef FM_DENSE_LAUNCH
     if (fork) (void)hipEventRecord(dense_join_event(), ds);
   }
   // (a software-pipelined variant that issued the next chunk's occurrence and row loads before

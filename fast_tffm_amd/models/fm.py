@@ -316,10 +316,9 @@ class FactorizationMachine:
         self._ring = None
         # hot rows of the local lookahead step (hip/hot.hip, FM_HOT_ROWS=1): the most frequent rows
         # of the first planned batch leave the dedup and the occurrence-gather backward for the
-        # dense-row GEMM (binary features, fp32 r1, Kp <= 128)
+        # dense-row GEMM (binary features, Kp <= 128)
         self._hot: K.HotRows | None = None
         self._hot_want = (self.device.type == "cuda" and mode == "local" and self.Kp <= 128
-                          and K.r1_dtype(cfg.dtype) == torch.float32
                           and os.environ.get("FM_HOT_ROWS", "1") != "0")
         self._graph = None
         self._graph_pool: list[_GraphedStep] = []

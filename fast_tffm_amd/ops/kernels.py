@@ -661,8 +661,6 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
             s_stride = s0v.stride(0)
     v_stride = _chk_rows(v, Kp, "v")
     _check(r1.dtype == r1_dtype(v.dtype), f"r1: {r1_dtype(v.dtype)} for {v.dtype} rows (the forward's r1)")
-    _check(r1.dtype == torch.float32 or (dd.dense_list is None and hot is None),
-           "the dense-row MFMA backward reads an fp32 r1")
     _check(hot is None or (mode == BWD_LOCAL and dd.dense_list is None and _is_gpu(dpred) and Kp <= 128),
            "hot rows: GPU LOCAL step, Kp <= 128, no dedup dense rows")
     o = opt or OptConfig()

@@ -3,7 +3,7 @@
 * the filter keeps exactly the non-hot (key, packed code) pairs, in CSR order;
 * a training run with hot rows (FM_HOT_ROWS=1, the default) matches the same run without them
   (FM_HOT_ROWS=0: every row through the sort-based dedup and the chunk backward) to fp32
-  summation-order error, for Adagrad and FTRL, fp32 and bf16 tables;
+  summation-order error, for Adagrad and FTRL, fp32 and bf16 tables (fp8: the losses);
 * it is deterministic: two runs give bitwise-identical tables.
 """
 
@@ -74,14 +74,18 @@ def _run(monkeypatch, hot: str, dtype, opt, steps=12):
 
 @pytest.mark.parametrize("dtype,opt", [(torch.float32, K.OptConfig("adagrad", lr=0.05)),
                                        (torch.bfloat16, K.OptConfig("adagrad", lr=0.05)),
-                                       (torch.float32, K.OptConfig("ftrl", lr=0.05, l1=0.001, l2=0.001))],
-                         ids=["fp32_adagrad", "bf16_adagrad", "fp32_ftrl"])
+                                       (torch.float32, K.OptConfig("ftrl", lr=0.05, l1=0.001, l2=0.001)),
+                                       (K.FP8, K.OptConfig("ftrl", lr=0.05, l1=0.001, l2=0.001))],
+                         ids=["fp32_adagrad", "bf16_adagrad", "fp32_ftrl", "fp8_ftrl"])
 def test_hot_rows_match_the_plain_step(monkeypatch, dtype, opt):
     l0, s0, used0 = _run(monkeypatch, "0", dtype, opt)
     l1, s1, used1 = _run(monkeypatch, "1", dtype, opt)
     assert not used0 and used1
+    ltol = 2e-3 if dtype == K.FP8 else 1e-4
     for a, b in zip(l0, l1):
-        assert abs(a - b) <= 1e-4 * abs(a), (l0, l1)
+        assert abs(a - b) <= ltol * abs(a), (l0, l1)
+    if dtype == K.FP8:  # (stochastic rounding to 3 mantissa bits: one flip is a whole step; the losses say it)
+        return
     tol = 1e-5 if dtype == torch.float32 else 2e-2  # (bf16: a 1-ulp rounding flip on a row is 2^-8)
     for a, b in zip(s0, s1):
         assert torch.allclose(a, b, rtol=tol, atol=tol * 1e-2), float((a - b).abs().max())
