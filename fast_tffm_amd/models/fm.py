@@ -320,6 +320,7 @@ class FactorizationMachine:
         self._hot: K.HotRows | None = None
         self._hot_want = (self.device.type == "cuda" and mode == "local" and self.Kp <= 128
                           and os.environ.get("FM_HOT_ROWS", "1") != "0")
+        self._hot_refresh = max(0, int(os.environ.get("FM_HOT_REFRESH", "0")))  # steps; 0: pick once
         self._graph = None
         self._graph_pool: list[_GraphedStep] = []
         self._exchange = None
@@ -668,8 +669,10 @@ class FactorizationMachine:
             pl = self._local_plan(b)
         main.wait_event(pl.ready)
         out = self._fwd_bwd_local(b, pl.rows, pl.dd)
-        if self._hot_want and self._hot is None and b.vals is None:
-            self._hot_from_plan(pl.dd)  # (once: plans created from here on leave these rows out)
+        if self._hot_want and self._hot is None and b.vals is None and getattr(pl.dd, "hot", None) is None:
+            self._hot_from_plan(pl.dd)  # (plans created from here on leave these rows out)
+        elif self._hot_refresh and self._hot is not None and self.global_step % self._hot_refresh == 0:
+            self._hot = None  # re-pick from the next unfiltered plan (the pending ones keep their set)
         done = torch.cuda.Event()
         done.record(main)
         self._lslots[pl.slot].done = done
