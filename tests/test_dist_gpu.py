@@ -5,7 +5,6 @@ must reproduce the local single-GPU step.  World > 1 is covered on CPU with
 gloo (test_distributed.py)."""
 
 import os
-import socket
 
 import pytest
 import torch
@@ -18,9 +17,9 @@ pytestmark = pytest.mark.gpu
 
 
 def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from ports import free_port
+
+    return free_port()
 
 
 @pytest.fixture(scope="module")

@@ -10,7 +10,6 @@ must equal one process training on the concatenated batches (grad_reduce = mean)
 fp32 / bf16 / fp8 tables (the latter two travel as uint8 wire rows)."""
 
 import os
-import socket
 
 import pytest
 import torch
@@ -22,9 +21,9 @@ V, KF, B, STEPS = 6007, 64, 512, 5
 
 
 def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from ports import free_port
+
+    return free_port()
 
 
 class _Done:

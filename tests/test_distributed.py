@@ -12,7 +12,6 @@ drop-in replacement for the single-process step.
 """
 
 import os
-import socket
 
 import pytest
 import torch
@@ -28,9 +27,9 @@ V, KF, B, STEPS, WORLD = 997, 8, 24, 3, 2
 
 
 def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from ports import free_port
+
+    return free_port()
 
 
 def _cfg(mode, grad_reduce, bcfg, mb=0):

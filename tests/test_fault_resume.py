@@ -7,7 +7,6 @@ lost steps.  CPU / gloo, world size 2, row-sharded table.
 """
 
 import os
-import socket
 import subprocess
 import sys
 
@@ -21,9 +20,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from ports import free_port
+
+    return free_port()
 
 
 def _cfg(tmp, log_dir):

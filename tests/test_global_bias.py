@@ -4,7 +4,6 @@ table's optimizer; multi-rank runs all-reduce the gradient so every rank holds t
 same b0."""
 
 import os
-import socket
 
 import torch
 import torch.multiprocessing as mp
@@ -42,9 +41,9 @@ def test_bias_gradient_and_adagrad_update():
 
 
 def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from ports import free_port
+
+    return free_port()
 
 
 def _worker(rank, world, port, out):

@@ -16,7 +16,6 @@ pool of batches that they cycle through (the 3-slot rotation wraps several times
 """
 
 import os
-import socket
 
 import pytest
 import torch
@@ -75,9 +74,9 @@ def test_local_depth2_lookahead_bitwise(production, k, dtype):
 
 
 def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from ports import free_port
+
+    return free_port()
 
 
 @pytest.fixture(scope="module")

@@ -13,7 +13,6 @@ CPU, gloo, world 2 (reference C3/C4/C6 sites: /root/reference/run_tffm.py:181-22
 """
 
 import os
-import socket
 
 import torch
 import torch.multiprocessing as mp
@@ -26,9 +25,9 @@ V, KF, B, STEPS, WORLD = 1499, 8, 32, 6, 2
 
 
 def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from ports import free_port
+
+    return free_port()
 
 
 def _worker(rank, world, port, variant, out_dir):

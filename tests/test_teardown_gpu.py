@@ -7,7 +7,6 @@ exchanges hold the model through weak proxies, so the last reference going away 
 the model at once (``FactorizationMachine.__del__`` -> ``close()``); ``dist.shutdown()``
 closes whatever is still alive before destroying the groups."""
 
-import socket
 
 import pytest
 import torch
@@ -20,9 +19,9 @@ pytestmark = pytest.mark.gpu
 
 
 def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from ports import free_port
+
+    return free_port()
 
 
 def _cfg(mode="auto"):
