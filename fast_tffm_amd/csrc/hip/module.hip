@@ -199,10 +199,10 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       [](int n, int end_bit, int CH, u64 keys, u64 payload, u64 skeys, u64 spay, u64 uniq, u64 seg_start,
          u64 seg_chunk, u64 chunk_start, u64 chunk_seg, u64 chunk_key, u64 counts, u64 inv, u64 ex_of_occ,
          u64 sorted_ex, u64 vals, u64 sorted_x, int payload_is_ex, int ex_shift, u64 offsets, int dense_min,
-         u64 dense_list, u64 ws, size_t ws_bytes, u64 stream) {
+         u64 dense_list, u64 ws, size_t ws_bytes, u64 stream, u64 n_dev, int algo) {
         if (CH < 1 || CH > fm::kMaxCH) throw std::invalid_argument("CH must be in [1, MAX_CH]");
         fm::DedupArgs a;
-        a.n = n; a.end_bit = end_bit; a.CH = CH; a.keys = P<const uint32_t>(keys);
+        a.n = n; a.n_dev = P<const int>(n_dev); a.algo = algo; a.end_bit = end_bit; a.CH = CH; a.keys = P<const uint32_t>(keys);
         a.payload = P<const int>(payload); a.skeys = P<uint32_t>(skeys); a.spay = P<int>(spay);
         a.uniq = P<uint32_t>(uniq); a.seg_start = P<int>(seg_start); a.seg_chunk = P<int>(seg_chunk);
         a.chunk_start = P<int>(chunk_start); a.chunk_seg = P<int>(chunk_seg); a.counts = P<int>(counts);
@@ -219,7 +219,10 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("chunk_seg"), py::arg("chunk_key"), py::arg("counts"), py::arg("inv"), py::arg("ex_of_occ"),
       py::arg("sorted_ex"),
       py::arg("vals"), py::arg("sorted_x"), py::arg("payload_is_ex"), py::arg("ex_shift"), py::arg("offsets"),
-      py::arg("dense_min"), py::arg("dense_list"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"));
+      py::arg("dense_min"), py::arg("dense_list"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"),
+      py::arg("n_dev") = 0, py::arg("algo") = (int)fm::kSortBucket);
+  m.attr("DEDUP_BUCKET") = (int)fm::kSortBucket;
+  m.attr("DEDUP_ONESWEEP") = (int)fm::kSortOnesweep;
   m.attr("MAX_DENSE") = fm::kMaxDense;
   m.attr("DENSE_WG") = fm::kDenseWG;
 

@@ -319,7 +319,7 @@ class FactorizationMachine:
         # dense-row GEMM (binary features, Kp <= 128)
         self._hot: K.HotRows | None = None
         self._hot_want = (self.device.type == "cuda" and mode == "local" and self.Kp <= 128
-                          and os.environ.get("FM_HOT_ROWS", "1") != "0")
+                          and os.environ.get("FM_HOT_ROWS", "0") == "1")
         self._hot_refresh = max(0, int(os.environ.get("FM_HOT_REFRESH", "0")))  # steps; 0: pick once
         self._graph = None
         self._graph_pool: list[_GraphedStep] = []
@@ -585,7 +585,8 @@ class FactorizationMachine:
         ``hot_ok`` (lookahead plans): with a hot-row set, the dedup input is the batch without the
         hot rows' occurrences (``K.hot_filter``); the DedupOut then carries the set it was filtered
         with as ``dd.hot`` (the forward counts those rows, the backward reduces them as a GEMM).
-        The sort needs the kept count on the host: one wait for the filter on this (side) stream."""
+        The bucket sort reads the kept count on the device; the onesweep sort (FM_DEDUP_SORT)
+        needs it on the host: one wait for the filter on this (side) stream."""
         cfg = self.cfg
         slot.ensure(b.nnz, self.device, cfg.dedup_chunk)
         rows = b.ids if b.ids.dtype == torch.int32 else slot.rows32[: b.nnz].copy_(b.ids)
@@ -596,12 +597,17 @@ class FactorizationMachine:
             slot.hot.copy_from(self._hot)
             K.hot_filter(b.offsets, rows, slot.hot, slot_bits=sb, gcnt=slot.gcnt, keys_out=slot.fkeys,
                          codes_out=slot.fcodes, n_out=slot.fn)
-            slot.fn_host.copy_(slot.fn, non_blocking=True)
-            slot.fn_ev.record()
-            slot.fn_ev.synchronize()
-            n = int(slot.fn_host[0])
-            dd = K.dedup(slot.fkeys[:n], ws=slot.dd, key_bits=kb, ex_of_occ=slot.fcodes[:n], vals=None,
-                         num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets, dense_min=0)
+            if K.dedup_sort_algo() == K.native.hip().DEDUP_BUCKET:  # kept count read on the device
+                dd = K.dedup(slot.fkeys[: b.nnz], ws=slot.dd, key_bits=kb, ex_of_occ=slot.fcodes[: b.nnz],
+                             vals=None, num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets,
+                             dense_min=0, n_dev=slot.fn)
+            else:  # the onesweep sort needs it on the host: one wait for the filter on this stream
+                slot.fn_host.copy_(slot.fn, non_blocking=True)
+                slot.fn_ev.record()
+                slot.fn_ev.synchronize()
+                n = int(slot.fn_host[0])
+                dd = K.dedup(slot.fkeys[:n], ws=slot.dd, key_bits=kb, ex_of_occ=slot.fcodes[:n], vals=None,
+                             num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets, dense_min=0)
             dd.hot = slot.hot
             return rows, dd
         ex = K.csr_rows(b.offsets, out=slot.dd.ex_of_occ[: b.nnz], nnz=b.nnz, slot_bits=sb)

@@ -428,11 +428,20 @@ def dense_min_for(num_examples: int, Kp: int, CH: int = 32, *, has_vals: bool = 
             or max_feats > 255 or r1_dtype(table_dtype) != torch.float32):
         return 0
     return max(8 * CH, num_examples // 40)
+def dedup_sort_algo() -> int:
+    """GPU dedup sort: FM_DEDUP_SORT=onesweep (rocPRIM, default: measured faster in the step) or
+    bucket (hip/dedup.hip; profiles/r3/dedup_sort_ab.txt)."""
+    h = native.hip()
+    v = os.environ.get("FM_DEDUP_SORT", "onesweep")
+    _check(v in ("bucket", "onesweep"), "FM_DEDUP_SORT must be bucket or onesweep")
+    return h.DEDUP_BUCKET if v == "bucket" else h.DEDUP_ONESWEEP
+
+
 def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int = 32,
           ex_of_occ: torch.Tensor | None = None, vals: torch.Tensor | None = None, want_inv: bool = False,
           CH: int | None = None, want_perm: bool = False, num_examples: int | None = None,
           Kp: int | None = None, ex_shift: int = 0, offsets: torch.Tensor | None = None,
-          dense_min: int = 0) -> DedupOut:
+          dense_min: int = 0, n_dev: torch.Tensor | None = None) -> DedupOut:
     """Sort-based unique over non-negative int32 keys (reference tf.unique, fm_model.py:72).
 
     Unique keys come out in ascending order (the reference's first-occurrence
@@ -441,6 +450,11 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
     map, per-occurrence values nor the occurrence permutation are needed, the
     sort carries the example index directly (one gather pass less).
     (``num_examples`` / ``Kp`` are accepted for interface stability; the plan does not use them.)
+
+    GPU sort: rocPRIM's onesweep radix sort, or with ``FM_DEDUP_SORT=bucket`` the bucket sort
+    (hip/dedup.hip: stable MSD partition by the top key bits + per-bucket LDS sort; same order).
+    ``n_dev`` (GPU, bucket sort): int32 [1] device count of the valid leading keys (``keys`` is then
+    the capacity): the plan is made without a host sync.
     """
     dev = keys.device
     n = keys.numel()
@@ -470,6 +484,10 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
     if _is_gpu(keys):
         h = native.hip()
         _check(1 <= CH <= h.MAX_CH, f"CH must be in [1, {h.MAX_CH}]")
+        algo = dedup_sort_algo()
+        if n_dev is not None:
+            _check(algo == h.DEDUP_BUCKET, "a device count needs the bucket sort (FM_DEDUP_SORT=bucket)")
+            _chk_vec(n_dev, torch.int32, None, "n_dev", dev)
         h.dedup(n=n, end_bit=key_bits, CH=CH, keys=_p(keys), payload=_p(ex_of_occ if ex_payload else ws.iota),
                 skeys=_p(ws.skeys), spay=_p(ws.perm), uniq=_p(ws.uniq), seg_start=_p(ws.seg_start),
                 seg_chunk=_p(ws.seg_chunk), chunk_start=_p(ws.chunk_start), chunk_seg=_p(ws.chunk_seg),
@@ -479,9 +497,10 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
                 sorted_ex=0 if ex_payload else _p(out.sorted_ex), vals=_p(vals), sorted_x=_p(out.sorted_x),
                 payload_is_ex=int(ex_payload), ex_shift=int(ex_shift), offsets=_p(offsets),
                 dense_min=int(dense_min) if out.dense_list is not None else 0, dense_list=_p(out.dense_list),
-                ws=_p(ws.ws), ws_bytes=ws.ws.numel(), stream=_stream(keys))
+                ws=_p(ws.ws), ws_bytes=ws.ws.numel(), stream=_stream(keys), n_dev=_p(n_dev), algo=algo)
         out.bwd_fresh = True  # the backward counters were zeroed on this stream
     else:
+        _check(n_dev is None, "a device count is a GPU path")
         U = native.cpu().dedup(n=n, keys=_p(keys), skeys=_p(ws.skeys), perm=_p(ws.perm), uniq=_p(ws.uniq),
                                seg_start=_p(ws.seg_start), inv=_p(out.inv), ex_of_occ=_p(ex_of_occ),
                                sorted_ex=_p(out.sorted_ex), vals=_p(vals), sorted_x=_p(out.sorted_x))

@@ -35,6 +35,8 @@ def main() -> int:
     ap.add_argument("--pool", type=int, default=8)
     ap.add_argument("--k", type=int, default=64)
     ap.add_argument("--dtype", default="fp32")
+    ap.add_argument("--only", default="", help="'dedup': after the warm-up steps time only the dedup chain "
+                    "(for a kernel profile of it alone)")
     a = ap.parse_args()
     K.set_debug_checks(False)
     dev = torch.device("cuda:0")
@@ -54,17 +56,23 @@ def main() -> int:
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / n * 1e3
 
-    # full step (bench's call pattern, depth-2 lookahead)
-    for i in range(6):
+    # full step (bench's call pattern, depth-2 lookahead); --only dedup: 3 steps (the hot-row pick)
+    for i in range(3 if a.only == "dedup" else 6):
         m.train_step(pool[i % P], pool[(i + 1) % P], pool[(i + 2) % P])
-    full = timed(lambda i: m.train_step(pool[i % P], pool[(i + 1) % P], pool[(i + 2) % P]), a.steps)
-    # precomputed plans, one slot per pool batch
+    full = (0.0 if a.only == "dedup" else
+            timed(lambda i: m.train_step(pool[i % P], pool[(i + 1) % P], pool[(i + 2) % P]), a.steps))
+    # precomputed plans, one slot per pool batch (filtered by the hot-row set when the step uses one)
     m.ws.ensure(pool[0].B, max(b.nnz for b in pool))
     slots = [_LocalSlot() for _ in range(P)]
-    plans = [m._plan_into(slots[j], pool[j]) for j in range(P)]
+    if a.only == "dedup":
+        dedup = timed(lambda i: m._plan_into(slots[i % P], pool[i % P], hot_ok=True), a.steps)
+        print(f"[side_chain] k={a.k} {a.dtype}: full {full:.3f} ms/step, dedup-only {dedup:.3f}", flush=True)
+        m.close()
+        return 0
+    plans = [m._plan_into(slots[j], pool[j], hot_ok=True) for j in range(P)]
     torch.cuda.synchronize()
     compute = timed(lambda i: m._fwd_bwd_local(pool[i % P], *plans[i % P]), a.steps)
-    dedup = timed(lambda i: m._plan_into(slots[i % P], pool[i % P]), a.steps)
+    dedup = timed(lambda i: m._plan_into(slots[i % P], pool[i % P], hot_ok=True), a.steps)
     print(f"[side_chain] k={a.k} {a.dtype}: full {full:.3f} ms/step, compute-only {compute:.3f}, "
           f"dedup-only {dedup:.3f}", flush=True)
     m.close()
