@@ -89,6 +89,7 @@ struct BwdArgs {
   const uint8_t* dense_A;   // [nex, kMaxDense] occurrence counts of the dense rows (written by the forward)
   SelfRows self;            // EMIT (row-sharded step): segments that are this rank's own table rows
   int chunk_grid;           // chunk kernel workgroup cap: 0 = per-row-width default, > 0 = this, < 0 = none
+  int chunk_class;          // chunk kernel: 0 = every chunk, 1 = chunks of multi-chunk rows, 2 = single-chunk rows
 };
 
 // Parameter row + optimizer slots of one segment, read before its gradient is
@@ -279,6 +280,7 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
       cn = ii + 2 * stride < i1 ? chunk_at(ii + 2 * stride) : 0;
     }
     if (dense) continue;  // gradient from the MFMA path (fm_bwd_dense_kernel)
+    if (a.chunk_class != 0 && single != (a.chunk_class == 2)) continue;  // the other launch's rows
     const int len = j1 - j0;
     RowState<EPL> rs;
     if (single) bwd_load<TV, EPL>(a, u, (long long)key, tE, rs);
@@ -717,9 +719,19 @@ static hipEvent_t dense_join_event() {
   if (!ev) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
   return ev;
 }
+static hipEvent_t split_fork_event() {
+  static hipEvent_t ev = nullptr;
+  if (!ev) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  return ev;
+}
+static hipEvent_t split_join_event() {
+  static hipEvent_t ev = nullptr;
+  if (!ev) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  return ev;
+}
 
 int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_unique, hipStream_t st,
-               hipStream_t dense_st) {
+               hipStream_t dense_st, hipStream_t split_st) {
   if (max_chunks <= 0) return 0;
   const int lpr = lanes_per_row(a.Kp, dtype);
   const int G = kWave / lpr;
@@ -774,11 +786,29 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   // (a software-pipelined variant that issued the next chunk's occurrence and row loads before
   // reducing the current one ran 367 -> 316 us alone but made the step slower twice:
   // profiles/r2/chunk_pipe_ab.txt, profiles/r3/fwd_prefetch_ab.txt; removed)
-  FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, a);
   // (workgroup counts: a 2048 cap / 1024 measured best among 512-8192, profiles/r2/combine_grid_ab.txt)
   const int g2 = fill_grid(max_unique, kWavesPerBlock * G, 2048);
-  FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, a);
-  FM_DISPATCH(dtype, lpr, fm_bwd_big_kernel, 1024, st, a);
+  if (split_st && split_st != st && a.piece < 0) {
+    // Split chunk walk: the chunks of multi-chunk rows first; then the combine / big kernels that
+    // finish those rows run on split_st beside the second launch, which reduces and updates the
+    // single-chunk rows (disjoint rows: the two halves never touch the same table row).  The
+    // compute stream joins behind its own work, so the combine leaves the critical path.
+    BwdArgs am = a, as = a;
+    am.chunk_class = 1;
+    as.chunk_class = 2;
+    FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, am);
+    (void)hipEventRecord(split_fork_event(), st);
+    (void)hipStreamWaitEvent(split_st, split_fork_event(), 0);
+    FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, split_st, am);
+    FM_DISPATCH(dtype, lpr, fm_bwd_big_kernel, 1024, split_st, am);
+    (void)hipEventRecord(split_join_event(), split_st);
+    FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, as);
+    (void)hipStreamWaitEvent(st, split_join_event(), 0);
+  } else {
+    FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, a);
+    FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, a);
+    FM_DISPATCH(dtype, lpr, fm_bwd_big_kernel, 1024, st, a);
+  }
   if (dense) {
     if (fork) (void)hipStreamWaitEvent(st, dense_join_event(), 0);
     FM_DISPATCH(dtype, lpr, fm_bwd_dense_apply_kernel, kMaxDense, st, a);

@@ -1,0 +1,73 @@
+"""Dedup chain alone (csr_rows codes + sort + RLE plan) on Criteo-shaped batches, per sort algorithm.
+
+Times K.dedup back to back on a pool of batches (no step beside it), for the full batch and for the
+batch without the occurrences of its 256 most frequent rows (the hot-row filter's output shape).
+Run under ``rocprofv3 --kernel-trace --stats`` for per-kernel times of the chain alone.
+
+    python tools/bench_dedup.py [--algo onesweep,bucket] [--iters 30]
+"""
+
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from fast_tffm_amd.data.synthetic import CriteoSynth  # noqa: E402
+from fast_tffm_amd.ops import kernels as K  # noqa: E402
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--algo", default="onesweep,bucket")
+    ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--pool", type=int, default=4)
+    ap.add_argument("--vocab", type=int, default=125_000_000)
+    a = ap.parse_args()
+    K.set_debug_checks(False)
+    dev = torch.device("cuda:0")
+    gen = CriteoSynth(a.vocab, seed=1000, device=dev)
+    kb = max(1, (a.vocab - 1).bit_length())
+    cases = {}
+    full, filt = [], []
+    for _ in range(a.pool):
+        b = gen.batch(131072)
+        ids = b.ids.to(torch.int32)
+        sb = K.slot_bits_for(b.B, b.max_feats)
+        codes = K.csr_rows(b.offsets, nnz=b.nnz, slot_bits=sb)
+        full.append((ids, codes, sb, b.offsets))
+        u, c = torch.unique(ids, return_counts=True)
+        hot = u[torch.argsort(c, descending=True)[:256]]
+        keep = ~torch.isin(ids, hot)
+        filt.append((ids[keep].contiguous(), codes[keep].contiguous(), sb, b.offsets))
+    cases["full"], cases["no_hot256"] = full, filt
+    for algo in a.algo.split(","):
+        os.environ["FM_DEDUP_SORT"] = algo
+        for name, pool in cases.items():
+            ws = K.DedupWorkspace(max(p[0].numel() for p in pool), dev, 32)
+
+            def run(i):
+                ids, codes, sb, off = pool[i % len(pool)]
+                K.dedup(ids, ws=ws, key_bits=kb, ex_of_occ=codes, ex_shift=sb, offsets=off)
+
+            for i in range(3):
+                run(i)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(a.iters):
+                run(i)
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) / a.iters * 1e3
+            n = sum(p[0].numel() for p in pool) / len(pool)
+            print(f"[bench_dedup] {algo:8s} {name:9s} n={n / 1e6:.2f}M: {ms:.3f} ms per dedup", flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
