@@ -736,7 +736,8 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               dense_A=_p(dense_A) if (dd.dense_list is not None or hot is not None) else 0,
               chunk_grid=int(os.environ.get("FM_CHUNK_GRID", "0")),
               dense_n=_p(hot.n) if hot is not None else 0, hot_keys=_p(hot.keys) if hot is not None else 0,
-              split_stream=split_stream.cuda_stream if split_stream is not None else 0, **skw)
+              split_stream=split_stream.cuda_stream if split_stream is not None else 0,
+              split_mode=int(os.environ.get("FM_BWD_SPLIT", "1") or 1), **skw)
         dd.bwd_fresh = False  # a second backward over this grouping zeroes its counters itself
     else:
         _check(self_rows is None, "self rows are a GPU path")
