@@ -89,8 +89,6 @@ struct BwdArgs {
   const uint8_t* dense_A;   // [nex, kMaxDense] occurrence counts of the dense rows (written by the forward)
   SelfRows self;            // EMIT (row-sharded step): segments that are this rank's own table rows
   int chunk_grid;           // chunk kernel workgroup cap: 0 = per-row-width default, > 0 = this, < 0 = none
-  int chunk_class;          // chunk kernel: 0 = every chunk, 1 = chunks of multi-chunk rows, 2 = single-chunk rows
-  int split_mode;           // launch_bwd with a split stream: 1 = multi then single (combine beside), 2 = concurrent
 };
 
 // Parameter row + optimizer slots of one segment, read before its gradient is
@@ -281,7 +279,6 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
       cn = ii + 2 * stride < i1 ? chunk_at(ii + 2 * stride) : 0;
     }
     if (dense) continue;  // gradient from the MFMA path (fm_bwd_dense_kernel)
-    if (a.chunk_class != 0 && single != (a.chunk_class == 2)) continue;  // the other launch's rows
     const int len = j1 - j0;
     RowState<EPL> rs;
     if (single) bwd_load<TV, EPL>(a, u, (long long)key, tE, rs);
@@ -720,19 +717,9 @@ static hipEvent_t dense_join_event() {
   if (!ev) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
   return ev;
 }
-static hipEvent_t split_fork_event() {
-  static hipEvent_t ev = nullptr;
-  if (!ev) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-  return ev;
-}
-static hipEvent_t split_join_event() {
-  static hipEvent_t ev = nullptr;
-  if (!ev) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-  return ev;
-}
 
 int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_unique, hipStream_t st,
-               hipStream_t dense_st, hipStream_t split_st) {
+               hipStream_t dense_st) {
   if (max_chunks <= 0) return 0;
   const int lpr = lanes_per_row(a.Kp, dtype);
   const int G = kWave / lpr;
@@ -789,41 +776,12 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   // profiles/r2/chunk_pipe_ab.txt, profiles/r3/fwd_prefetch_ab.txt; removed)
   // (workgroup counts: a 2048 cap / 1024 measured best among 512-8192, profiles/r2/combine_grid_ab.txt)
   const int g2 = fill_grid(max_unique, kWavesPerBlock * G, 2048);
-  if (split_st && split_st != st && a.piece < 0 && a.split_mode == 2) {
-    // Split mode 2: the single-chunk rows' launch runs on split_st CONCURRENTLY with the multi-chunk
-    // rows' launch; combine / big follow the latter on the compute stream, which joins split_st.
-    BwdArgs am = a, as = a;
-    am.chunk_class = 1;
-    as.chunk_class = 2;
-    (void)hipEventRecord(split_fork_event(), st);
-    (void)hipStreamWaitEvent(split_st, split_fork_event(), 0);
-    FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, split_st, as);
-    (void)hipEventRecord(split_join_event(), split_st);
-    FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, am);
-    FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, am);
-    FM_DISPATCH(dtype, lpr, fm_bwd_big_kernel, 1024, st, am);
-    (void)hipStreamWaitEvent(st, split_join_event(), 0);
-  } else if (split_st && split_st != st && a.piece < 0) {
-    // Split chunk walk: the chunks of multi-chunk rows first; then the combine / big kernels that
-    // finish those rows run on split_st beside the second launch, which reduces and updates the
-    // single-chunk rows (disjoint rows: the two halves never touch the same table row).  The
-    // compute stream joins behind its own work, so the combine leaves the critical path.
-    BwdArgs am = a, as = a;
-    am.chunk_class = 1;
-    as.chunk_class = 2;
-    FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, am);
-    (void)hipEventRecord(split_fork_event(), st);
-    (void)hipStreamWaitEvent(split_st, split_fork_event(), 0);
-    FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, split_st, am);
-    FM_DISPATCH(dtype, lpr, fm_bwd_big_kernel, 1024, split_st, am);
-    (void)hipEventRecord(split_join_event(), split_st);
-    FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, as);
-    (void)hipStreamWaitEvent(st, split_join_event(), 0);
-  } else {
-    FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, a);
-    FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, a);
-    FM_DISPATCH(dtype, lpr, fm_bwd_big_kernel, 1024, st, a);
-  }
+  // (a split walk -- the chunks of multi-chunk rows first, their combine beside the single-chunk
+  // rows' launch, or both launches concurrent -- measured slower: k64 0.669 -> 0.72-0.78 ms, each
+  // launch as long as the whole walk; profiles/r3/bwd_split_ab.txt)
+  FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, a);
+  FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, a);
+  FM_DISPATCH(dtype, lpr, fm_bwd_big_kernel, 1024, st, a);
   if (dense) {
     if (fork) (void)hipStreamWaitEvent(st, dense_join_event(), 0);
     FM_DISPATCH(dtype, lpr, fm_bwd_dense_apply_kernel, kMaxDense, st, a);

@@ -134,9 +134,8 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
          u64 dense_part, int nex, u64 dense_stream, int dtype,
          long long max_chunks, long long max_unique, u64 stream, int g_wcol, int g_bf16, u64 sr_counter,
          int counters_ready, u64 seg_bounds, int piece, int n_owners, u64 dense_A,
-         const std::vector<long long>& self, int chunk_grid, u64 dense_n, u64 hot_keys, u64 split_stream, int split_mode) {
+         const std::vector<long long>& self, int chunk_grid, u64 dense_n, u64 hot_keys) {
         fm::BwdArgs a{};
-        a.split_mode = split_mode;
         a.chunk_grid = chunk_grid;
         a.dense_n = P<const int>(dense_n);
         a.hot_keys = P<const int>(hot_keys);
@@ -165,7 +164,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
         a.big_list = P<int>(big_list); a.big_count = P<int>(big_count); a.multi = P<int>(multi);
         a.counts_rw = P<int>(counts);
         a.dense_list = P<const int>(dense_list); a.dense_part = P<float>(dense_part); a.nex = nex;
-        check(fm::launch_bwd(a, dtype, max_chunks, max_unique, S(stream), S(dense_stream), S(split_stream)), "fm_bwd");
+        check(fm::launch_bwd(a, dtype, max_chunks, max_unique, S(stream), S(dense_stream)), "fm_bwd");
       },
       py::arg("mode"), py::arg("counts"), py::arg("chunk_start"), py::arg("chunk_seg"), py::arg("chunk_key"),
       py::arg("seg_start"),
@@ -180,7 +179,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("g_bf16") = 0, py::arg("sr_counter") = 0, py::arg("counters_ready") = 0, py::arg("seg_bounds") = 0,
       py::arg("piece") = -1, py::arg("n_owners") = 0, py::arg("dense_A") = 0,
       py::arg("self_rows") = std::vector<long long>{}, py::arg("chunk_grid") = 0, py::arg("dense_n") = 0,
-      py::arg("hot_keys") = 0, py::arg("split_stream") = 0, py::arg("split_mode") = 1);
+      py::arg("hot_keys") = 0);
 
   m.def("dedup_workspace_bytes", &fm::dedup_workspace_bytes, py::arg("n"));
   // hot-row filter of the dedup input (hot.hip): kept (key, code) pairs in CSR order + their count

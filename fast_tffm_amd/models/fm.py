@@ -508,29 +508,6 @@ class FactorizationMachine:
             self._dense_st = torch.cuda.Stream(self.device)
         return self._dense_st
 
-    def _aux(self):
-        if getattr(self, "_aux_st", None) is None:
-            self._aux_st = torch.cuda.Stream(self.device)
-        return self._aux_st
-
-    def _loss_stream(self):
-        """Stream of the loss-partial reduce (GPU, opt-in FM_LOSS_STREAM=1): the ~10-20 us sum leaves
-        the compute stream's forward -> backward seam and runs beside the backward.  Measured slower
-        (k64 0.668-0.671 -> 0.676 ms, profiles/r3/loss_stream_ab.txt): the cross-stream event pair
-        costs more than the reduce."""
-        if self.device.type != "cuda" or os.environ.get("FM_LOSS_STREAM", "0") != "1":
-            return None
-        return self._aux()
-
-    def _split_stream(self):
-        """Stream of the backward's combine / big kernels (GPU, FM_BWD_SPLIT != 0): the chunk walk
-        runs the multi-chunk rows first, their combine then overlaps the single-chunk rows' launch
-        (hip/fm_bwd.hip launch_bwd).  The same auxiliary stream as the loss reduce: HIP has 4 hardware
-        queues by default and a fifth stream would share one with the dedup's side stream."""
-        if self.device.type != "cuda" or os.environ.get("FM_BWD_SPLIT", "1") == "0":
-            return None
-        return self._aux()
-
     def _side_stream(self):
         if self._side is None:
             self._side = side_stream(self.device)
@@ -669,16 +646,13 @@ class FactorizationMachine:
             fo = K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,
                               weights=b.weights, loss=cfg.loss_type, grad_scale=self.grad_scale(b.B), want_r1=True,
                               pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
-                              threads=cfg.threads, bias=self.gbias, dense=dd, dense_A=dA, hot=hot,
-                              loss_stream=self._loss_stream())
+                              threads=cfg.threads, bias=self.gbias, dense=dd, dense_A=dA, hot=hot)
             self.bias_step(fo.dpred)
         with roctx_range("bwd+update"):
             K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
                           reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, dense_part=ws.dense_part,
-                          dense_stream=self._dense_stream(), split_stream=self._split_stream(),
+                          dense_stream=self._dense_stream(),
                           sr_counter=self.sr_tick(), dense_A=dA, hot=hot)
-        if fo.loss_ready is not None:  # joined behind the backward: nothing waits for it
-            torch.cuda.current_stream(self.device).wait_event(fo.loss_ready)
         return StepOut(fo.loss_sum, b.B)
 
     def _local_lookahead_step(self, b: Batch, next_batch: Batch | None, next2: Batch | None = None) -> StepOut:

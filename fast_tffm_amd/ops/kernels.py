@@ -148,12 +148,11 @@ def _range_check(idx: torch.Tensor, hi: int, name: str) -> None:
 class FwdOut:
     """Outputs of fm_forward. ``loss_sum``/``regv``/``regw`` are 0-d tensors on the op's device."""
 
-    __slots__ = ("pred", "r1", "dpred", "loss_sum", "regv", "regw", "loss_ready")
+    __slots__ = ("pred", "r1", "dpred", "loss_sum", "regv", "regw")
 
-    def __init__(self, pred, r1, dpred, loss_sum, regv, regw, loss_ready=None):
+    def __init__(self, pred, r1, dpred, loss_sum, regv, regw):
         self.pred, self.r1, self.dpred = pred, r1, dpred
         self.loss_sum, self.regv, self.regw = loss_sum, regv, regw
-        self.loss_ready = loss_ready  # event after the loss sum on ``loss_stream`` (None: same stream)
 
 
 def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | None, v: torch.Tensor,
@@ -165,7 +164,7 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
                bias: torch.Tensor | None = None, dense: "DedupOut | None" = None,
                dense_A: torch.Tensor | None = None, dense_by_segment: bool = False,
                self_rows: SelfRows | None = None, seg_lookup: "SegIndex | None" = None,
-               hot: HotRows | None = None, loss_stream: torch.cuda.Stream | None = None) -> FwdOut:
+               hot: HotRows | None = None) -> FwdOut:
     """FM score of a CSR batch (reference FmScorer, cc/fm_scorer_op.h:101-140), fused with the loss.
 
     pred_i = sum_j x_j w_j + 1/2 sum_k [(sum_j x_j v_jk)^2 - sum_j x_j^2 v_jk^2]  (+ bias[0], optional
@@ -247,20 +246,10 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
               seg_keys=_p(seg_lookup.keys) if seg_lookup is not None else 0,
               seg_shift=seg_lookup.shift if seg_lookup is not None else 0, **dkw)
         # (an in-kernel last-block reduction was measured slower: the per-block agent-scope
-        # release fence writes back L2 -- fwd 211 -> 412 us; a separate reduce is ~10 us).
-        # ``loss_stream``: the reduce runs there, beside the backward, off the compute stream;
-        # the caller makes its stream wait on ``loss_ready`` before the loss or ``partial`` is used.
-        loss_ready = None
-        if lt and loss_stream is not None:
-            fwd_done = torch.cuda.Event()
-            fwd_done.record(torch.cuda.current_stream(dev))
-            loss_stream.wait_event(fwd_done)
-            with torch.cuda.stream(loss_stream):
-                loss_sum = lp.sum(dtype=torch.float32)
-                loss_ready = torch.cuda.Event()
-                loss_ready.record(loss_stream)
-        else:
-            loss_sum = lp.sum(dtype=torch.float32) if lt else None
+        # release fence writes back L2 -- fwd 211 -> 412 us; a separate reduce is ~10 us; the same
+        # reduce on a second stream beside the backward measured slower too: 0.668-0.671 -> 0.676 ms,
+        # profiles/r3/loss_stream_ab.txt)
+        loss_sum = lp.sum(dtype=torch.float32) if lt else None
         regv = rp.view(grid, 2)[:, 0].sum() if want_reg else None
         regw = rp.view(grid, 2)[:, 1].sum() if want_reg else None
     else:
@@ -273,7 +262,7 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
         loss_sum = torch.tensor(ls, dtype=torch.float32) if lt else None
         regv = torch.tensor(rv, dtype=torch.float32) if want_reg else None
         regw = torch.tensor(rw, dtype=torch.float32) if want_reg else None
-    return FwdOut(pred, r1, dpred if lt else None, loss_sum, regv, regw, loss_ready if _is_gpu(rows) else None)
+    return FwdOut(pred, r1, dpred if lt else None, loss_sum, regv, regw)
 
 
 # ---------------------------------------------------------------------------
@@ -626,7 +615,7 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
                 src_v: torch.Tensor | None = None, src_w: torch.Tensor | None = None,
                 grad_out: torch.Tensor | None = None, reg_v: float = 0.0, reg_w: float = 0.0,
                 partial: torch.Tensor | None = None, threads: int = 0,
-                dense_part: torch.Tensor | None = None, dense_stream=None, split_stream=None,
+                dense_part: torch.Tensor | None = None, dense_stream=None,
                 grad_bf16: bool = False, sr_counter: torch.Tensor | None = None,
                 seg_bounds: torch.Tensor | None = None, piece: int = -1,
                 dense_A: torch.Tensor | None = None, self_rows: SelfRows | None = None,
@@ -736,8 +725,7 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               dense_A=_p(dense_A) if (dd.dense_list is not None or hot is not None) else 0,
               chunk_grid=int(os.environ.get("FM_CHUNK_GRID", "0")),
               dense_n=_p(hot.n) if hot is not None else 0, hot_keys=_p(hot.keys) if hot is not None else 0,
-              split_stream=split_stream.cuda_stream if split_stream is not None else 0,
-              split_mode=int(os.environ.get("FM_BWD_SPLIT", "1") or 1), **skw)
+              **skw)
         dd.bwd_fresh = False  # a second backward over this grouping zeroes its counters itself
     else:
         _check(self_rows is None, "self rows are a GPU path")
