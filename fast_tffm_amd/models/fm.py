@@ -646,13 +646,14 @@ class FactorizationMachine:
             fo = K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,
                               weights=b.weights, loss=cfg.loss_type, grad_scale=self.grad_scale(b.B), want_r1=True,
                               pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
-                              threads=cfg.threads, bias=self.gbias, dense=dd, dense_A=dA, hot=hot)
+                              threads=cfg.threads, bias=self.gbias, dense=dd, dense_A=dA, hot=hot,
+                              defer_loss=os.environ.get("FM_FUSED_LOSS", "1") != "0")
             self.bias_step(fo.dpred)
-        with roctx_range("bwd+update"):
+        with roctx_range("bwd+update"):  # (its chunk kernel also sums the forward's loss partials)
             K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
                           reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, dense_part=ws.dense_part,
                           dense_stream=self._dense_stream(),
-                          sr_counter=self.sr_tick(), dense_A=dA, hot=hot)
+                          sr_counter=self.sr_tick(), dense_A=dA, hot=hot, loss_from=fo)
         return StepOut(fo.loss_sum, b.B)
 
     def _local_lookahead_step(self, b: Batch, next_batch: Batch | None, next2: Batch | None = None) -> StepOut:
