@@ -96,6 +96,10 @@ struct BwdArgs {
   float* loss_out;
 };
 
+#ifndef FM_FUSED_LOSS
+#define FM_FUSED_LOSS 1  // (A/B build variant "nofl": 0)
+#endif
+
 // Ordered block sum of the forward's loss partials (fixed per-thread stride, fixed tree):
 // deterministic.  Called by one whole workgroup.
 __device__ inline void block_loss_sum(const BwdArgs& a) {
@@ -242,7 +246,9 @@ constexpr int chunk_min_waves() {
 template <int LPR, typename TV>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(chunk_min_waves<LPR, TV>())))
 void fm_bwd_chunk_kernel(BwdArgs a) {
+#if FM_FUSED_LOSS
   if (a.loss_partial && blockIdx.x == 0) block_loss_sum(a);  // (uniform: the whole workgroup 0)
+#endif
   const uint32_t sr = sr_step_seed(a.sr_counter);  // stochastic rounding seed (0: nearest)
   constexpr int EPL = Frag<TV>::N;  // elements per lane of the table dtype
   constexpr int G = kWave / LPR;
