@@ -89,36 +89,7 @@ struct BwdArgs {
   const uint8_t* dense_A;   // [nex, kMaxDense] occurrence counts of the dense rows (written by the forward)
   SelfRows self;            // EMIT (row-sharded step): segments that are this rank's own table rows
   int chunk_grid;           // chunk kernel workgroup cap: 0 = per-row-width default, > 0 = this, < 0 = none
-  // the forward's per-workgroup loss partials, summed by the chunk kernel's workgroup 0 into loss_out
-  // (nullable): the separate reduce kernel between forward and backward leaves the critical path
-  const float* loss_partial;
-  int loss_n;
-  float* loss_out;
 };
-
-#ifndef FM_FUSED_LOSS
-#define FM_FUSED_LOSS 1  // (A/B build variant "nofl": 0)
-#endif
-
-// Ordered block sum of the forward's loss partials (fixed per-thread stride, fixed tree):
-// deterministic.  Called by one whole workgroup.
-__device__ inline void block_loss_sum(const BwdArgs& a) {
-  __shared__ float red[kWavesPerBlock];
-  float s = 0.f;
-  for (int i = threadIdx.x; i < a.loss_n; i += kBlock) s += a.loss_partial[i];
-#pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, kWave);
-  if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float t = 0.f;
-#pragma unroll
-    for (int w = 0; w < kWavesPerBlock; ++w) t += red[w];
-    a.loss_out[0] = t;
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void loss_sum_kernel(BwdArgs a) { block_loss_sum(a); }
 
 // Parameter row + optimizer slots of one segment, read before its gradient is
 // known so that the loads overlap the occurrence reduction.
@@ -246,9 +217,6 @@ constexpr int chunk_min_waves() {
 template <int LPR, typename TV>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(chunk_min_waves<LPR, TV>())))
 void fm_bwd_chunk_kernel(BwdArgs a) {
-#if FM_FUSED_LOSS
-  if (a.loss_partial && blockIdx.x == 0) block_loss_sum(a);  // (uniform: the whole workgroup 0)
-#endif
   const uint32_t sr = sr_step_seed(a.sr_counter);  // stochastic rounding seed (0: nearest)
   constexpr int EPL = Frag<TV>::N;  // elements per lane of the table dtype
   constexpr int G = kWave / LPR;
@@ -752,10 +720,7 @@ static hipEvent_t dense_join_event() {
 
 int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_unique, hipStream_t st,
                hipStream_t dense_st) {
-  if (max_chunks <= 0) {  // (no chunk kernel to carry the loss sum)
-    if (a.loss_partial) hipLaunchKernelGGL(loss_sum_kernel, dim3(1), dim3(kBlock), 0, st, a);
-    return (int)hipGetLastError();
-  }
+  if (max_chunks <= 0) return 0;
   const int lpr = lanes_per_row(a.Kp, dtype);
   const int G = kWave / lpr;
   if (!a.counters_ready) {  // (a fresh dedup zeroed both on its own stream)

@@ -134,12 +134,8 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
          u64 dense_part, int nex, u64 dense_stream, int dtype,
          long long max_chunks, long long max_unique, u64 stream, int g_wcol, int g_bf16, u64 sr_counter,
          int counters_ready, u64 seg_bounds, int piece, int n_owners, u64 dense_A,
-         const std::vector<long long>& self, int chunk_grid, u64 dense_n, u64 hot_keys, u64 loss_partial,
-         int loss_n, u64 loss_out) {
+         const std::vector<long long>& self, int chunk_grid, u64 dense_n, u64 hot_keys) {
         fm::BwdArgs a{};
-        if ((loss_partial != 0) != (loss_out != 0) || (loss_partial && loss_n < 1))
-          throw std::invalid_argument("fm_bwd: loss_partial / loss_n / loss_out go together");
-        a.loss_partial = P<const float>(loss_partial); a.loss_n = loss_n; a.loss_out = P<float>(loss_out);
         a.chunk_grid = chunk_grid;
         a.dense_n = P<const int>(dense_n);
         a.hot_keys = P<const int>(hot_keys);
@@ -183,7 +179,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("g_bf16") = 0, py::arg("sr_counter") = 0, py::arg("counters_ready") = 0, py::arg("seg_bounds") = 0,
       py::arg("piece") = -1, py::arg("n_owners") = 0, py::arg("dense_A") = 0,
       py::arg("self_rows") = std::vector<long long>{}, py::arg("chunk_grid") = 0, py::arg("dense_n") = 0,
-      py::arg("hot_keys") = 0, py::arg("loss_partial") = 0, py::arg("loss_n") = 0, py::arg("loss_out") = 0);
+      py::arg("hot_keys") = 0);
 
   m.def("dedup_workspace_bytes", &fm::dedup_workspace_bytes, py::arg("n"));
   // hot-row filter of the dedup input (hot.hip): kept (key, code) pairs in CSR order + their count

@@ -508,12 +508,6 @@ class FactorizationMachine:
             self._dense_st = torch.cuda.Stream(self.device)
         return self._dense_st
 
-    @staticmethod
-    def _fused_loss() -> bool:
-        """Local GPU steps: the chunk backward's first workgroup sums the forward's loss partials
-        (FM_FUSED_LOSS=0: a separate reduce kernel between forward and backward)."""
-        return os.environ.get("FM_FUSED_LOSS", "1") != "0"
-
     def _side_stream(self):
         if self._side is None:
             self._side = side_stream(self.device)
@@ -544,7 +538,7 @@ class FactorizationMachine:
             fo = K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,
                               weights=b.weights, loss=cfg.loss_type, grad_scale=self.grad_scale(b.B), want_r1=True,
                               pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
-                              threads=cfg.threads, bias=self.gbias, defer_loss=self._fused_loss())
+                              threads=cfg.threads, bias=self.gbias)
             self.bias_step(fo.dpred)
         if gpu:
             main.wait_stream(side)
@@ -554,8 +548,7 @@ class FactorizationMachine:
         with roctx_range("bwd+update"):
             K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
                           reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, dense_part=ws.dense_part,
-                          dense_stream=self._dense_stream() if gpu else None, sr_counter=self.sr_tick(),
-                          loss_from=fo)
+                          dense_stream=self._dense_stream() if gpu else None, sr_counter=self.sr_tick())
         return StepOut(fo.loss_sum, b.B)
 
     # ------------------------------------------------------------------
@@ -653,14 +646,13 @@ class FactorizationMachine:
             fo = K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,
                               weights=b.weights, loss=cfg.loss_type, grad_scale=self.grad_scale(b.B), want_r1=True,
                               pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
-                              threads=cfg.threads, bias=self.gbias, dense=dd, dense_A=dA, hot=hot,
-                              defer_loss=self._fused_loss())
+                              threads=cfg.threads, bias=self.gbias, dense=dd, dense_A=dA, hot=hot)
             self.bias_step(fo.dpred)
-        with roctx_range("bwd+update"):  # (its chunk kernel also sums the forward's loss partials)
+        with roctx_range("bwd+update"):
             K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
                           reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, dense_part=ws.dense_part,
                           dense_stream=self._dense_stream(),
-                          sr_counter=self.sr_tick(), dense_A=dA, hot=hot, loss_from=fo)
+                          sr_counter=self.sr_tick(), dense_A=dA, hot=hot)
         return StepOut(fo.loss_sum, b.B)
 
     def _local_lookahead_step(self, b: Batch, next_batch: Batch | None, next2: Batch | None = None) -> StepOut:

@@ -148,14 +148,11 @@ def _range_check(idx: torch.Tensor, hi: int, name: str) -> None:
 class FwdOut:
     """Outputs of fm_forward. ``loss_sum``/``regv``/``regw`` are 0-d tensors on the op's device."""
 
-    __slots__ = ("pred", "r1", "dpred", "loss_sum", "regv", "regw", "loss_partial")
+    __slots__ = ("pred", "r1", "dpred", "loss_sum", "regv", "regw")
 
-    def __init__(self, pred, r1, dpred, loss_sum, regv, regw, loss_partial=None):
+    def __init__(self, pred, r1, dpred, loss_sum, regv, regw):
         self.pred, self.r1, self.dpred = pred, r1, dpred
         self.loss_sum, self.regv, self.regw = loss_sum, regv, regw
-        # defer_loss: the forward's per-workgroup loss partials; fm_backward(loss_from=...) sums them
-        # into loss_sum (which holds nothing until then)
-        self.loss_partial = loss_partial
 
 
 def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | None, v: torch.Tensor,
@@ -167,7 +164,7 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
                bias: torch.Tensor | None = None, dense: "DedupOut | None" = None,
                dense_A: torch.Tensor | None = None, dense_by_segment: bool = False,
                self_rows: SelfRows | None = None, seg_lookup: "SegIndex | None" = None,
-               hot: HotRows | None = None, defer_loss: bool = False) -> FwdOut:
+               hot: HotRows | None = None) -> FwdOut:
     """FM score of a CSR batch (reference FmScorer, cc/fm_scorer_op.h:101-140), fused with the loss.
 
     pred_i = sum_j x_j w_j + 1/2 sum_k [(sum_j x_j v_jk)^2 - sum_j x_j^2 v_jk^2]  (+ bias[0], optional
@@ -252,13 +249,11 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
         # release fence writes back L2 -- fwd 211 -> 412 us; a separate reduce is ~10 us; the same
         # reduce on a second stream beside the backward measured slower too: 0.668-0.671 -> 0.676 ms,
         # profiles/r3/loss_stream_ab.txt)
-        # ``defer_loss`` (GPU): the chunk backward's first workgroup sums the partials instead (the
-        # caller passes ``loss_from=`` this FwdOut to fm_backward): no reduce kernel between them.
-        deferred = lp if (lt and defer_loss) else None
-        if deferred is not None:
-            loss_sum = torch.empty((), dtype=torch.float32, device=dev)
-        else:
-            loss_sum = lp.sum(dtype=torch.float32) if lt else None
+        # A sum by the chunk backward's first workgroup (no reduce kernel between forward and
+        # backward) made the chunk kernel itself ~30% slower even when not taken -- a workgroup
+        # barrier in the chunk kernel changes its code (k64 0.668 -> 0.88 ms, same box;
+        # profiles/r3/fused_loss_ab.txt)
+        loss_sum = lp.sum(dtype=torch.float32) if lt else None
         regv = rp.view(grid, 2)[:, 0].sum() if want_reg else None
         regw = rp.view(grid, 2)[:, 1].sum() if want_reg else None
     else:
@@ -271,8 +266,7 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
         loss_sum = torch.tensor(ls, dtype=torch.float32) if lt else None
         regv = torch.tensor(rv, dtype=torch.float32) if want_reg else None
         regw = torch.tensor(rw, dtype=torch.float32) if want_reg else None
-    return FwdOut(pred, r1, dpred if lt else None, loss_sum, regv, regw,
-                  deferred if _is_gpu(rows) else None)
+    return FwdOut(pred, r1, dpred if lt else None, loss_sum, regv, regw)
 
 
 # ---------------------------------------------------------------------------
@@ -625,7 +619,7 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
                 src_v: torch.Tensor | None = None, src_w: torch.Tensor | None = None,
                 grad_out: torch.Tensor | None = None, reg_v: float = 0.0, reg_w: float = 0.0,
                 partial: torch.Tensor | None = None, threads: int = 0,
-                dense_part: torch.Tensor | None = None, dense_stream=None, loss_from: FwdOut | None = None,
+                dense_part: torch.Tensor | None = None, dense_stream=None,
                 grad_bf16: bool = False, sr_counter: torch.Tensor | None = None,
                 seg_bounds: torch.Tensor | None = None, piece: int = -1,
                 dense_A: torch.Tensor | None = None, self_rows: SelfRows | None = None,
@@ -711,11 +705,6 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
             dp = dense_part if dense_part is not None else torch.empty(
                 (DENSE_WG * MAX_DENSE, Kp + 4), dtype=torch.float32, device=dev)
             _check(dp.numel() >= DENSE_WG * MAX_DENSE * (Kp + 4), "dense_part scratch too small")
-        lkw = {}
-        if loss_from is not None and loss_from.loss_partial is not None:
-            _check(piece < 0, "the deferred loss sum rides on a whole backward, not a piece")
-            lp = loss_from.loss_partial
-            lkw = dict(loss_partial=_p(lp), loss_n=lp.numel(), loss_out=_p(loss_from.loss_sum))
         skw = {}
         if mode == BWD_EMIT and self_rows is not None and self_rows.u1 > self_rows.u0:
             skw = dict(self_rows=self_rows.packed())
@@ -740,7 +729,7 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               dense_A=_p(dense_A) if (dd.dense_list is not None or hot is not None) else 0,
               chunk_grid=int(os.environ.get("FM_CHUNK_GRID", "0")),
               dense_n=_p(hot.n) if hot is not None else 0, hot_keys=_p(hot.keys) if hot is not None else 0,
-              **lkw, **skw)
+              **skw)
         dd.bwd_fresh = False  # a second backward over this grouping zeroes its counters itself
     else:
         _check(self_rows is None, "self rows are a GPU path")

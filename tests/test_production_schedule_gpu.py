@@ -124,22 +124,3 @@ def test_dp_dense_lookahead_matches_local(production, rccl_ctx):
     torch.testing.assert_close(dm.table.reference_rows(), loc.table.reference_rows(), rtol=1e-5, atol=1e-7)
     dm.close()
 
-
-def test_fused_loss_sum_matches_reduce_kernel(production, monkeypatch):
-    """The chunk kernel's workgroup 0 sums the forward's loss partials (FM_FUSED_LOSS=1, default):
-    the same loss as the separate reduce (to fp32 summation order) and bitwise the same tables."""
-    V = 40000
-    gen = CriteoSynth(V, device="cuda", seed=64)
-    pool = [gen.batch(4096) for _ in range(POOL)]
-    runs = {}
-    for fused in ("0", "1"):
-        monkeypatch.setenv("FM_FUSED_LOSS", fused)
-        m = FactorizationMachine(_cfg(V), device="cuda")
-        losses = [m.train_step(pool[i % POOL], pool[(i + 1) % POOL], pool[(i + 2) % POOL]).loss_sum.clone()
-                  for i in range(STEPS)]
-        torch.cuda.synchronize()
-        runs[fused] = (torch.stack(losses), _state(m))
-        m.close()
-    torch.testing.assert_close(runs["1"][0], runs["0"][0], rtol=2e-6, atol=0)
-    for x, y in zip(runs["0"][1], runs["1"][1]):
-        assert torch.equal(x.view(torch.uint8), y.view(torch.uint8))
