@@ -29,7 +29,7 @@ Extensions (new keys, all optional):
                 microbatches = 1|2|... (row-sharded step parts overlapping the exchange; default 1),
                 prefetch_rows = auto|on|off (exchange the next step's rows early, re-send updated ones),
                 overlap_grads = auto|on|off (split backward; first half's gradients sent while the rest runs;
-                                auto = off)
+                                auto = on with one microbatch)
 """
 
 from __future__ import annotations

@@ -70,7 +70,7 @@ class FMConfig:
     comm_dtype: str = "auto"          # row-sharded wire rows: auto (= storage dtype) | fp32 | bf16
     microbatches: int = 0             # row-sharded step: parts per batch overlapping the exchange (0/1 = one)
     prefetch_rows: str = "auto"       # row-sharded step: early row exchange + patch (auto = on when world > 1)
-    overlap_grads: str = "auto"       # row-sharded step: split backward, first half's grads sent early (auto: off)
+    overlap_grads: str = "auto"       # row-sharded step: split backward, first half's grads sent early (auto: on)
     dedup_chunk: int = 32             # CH of the segmented backward
     threads: int = 0                  # CPU kernels (0 = OpenMP default)
     global_bias: bool = False         # learned global bias b0 (extension; the reference has none)

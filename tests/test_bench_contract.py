@@ -54,7 +54,7 @@ def test_bench_two_ranks_one_json_line():
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert KEYS <= set(d) and d["n_gpus"] == 2 and d["config"]["global_batch"] == 512
-    assert d["config"]["parallelism"] == "rowshard2" and d["config"]["early_rows"] and not d["config"]["split_grads"]
+    assert d["config"]["parallelism"] == "rowshard2" and d["config"]["early_rows"] and d["config"]["split_grads"]
     assert d["config"]["rccl_world"] == 2 and d["config"]["comm_backend"] == "gloo"
     assert d["config"]["per_rank_ms"]["max"] >= d["config"]["per_rank_ms"]["min"] > 0
     assert d["config"]["comm_bytes_per_rank"] > 0

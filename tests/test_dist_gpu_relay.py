@@ -108,7 +108,7 @@ def _worker(rank, world, port, out_dir, variant):
 
 @pytest.mark.parametrize("world,variant", [
     (2, dict()), (2, dict(prefetch_rows="off")), (4, dict()), (3, dict(dtype="bf16")), (2, dict(dtype="fp8")),
-    (3, dict(overlap_grads="on")), (2, dict(overlap_grads="on", env={"FM_SELF_ROWS": "0"})),
+    (3, dict(overlap_grads="off")), (2, dict(overlap_grads="off", env={"FM_SELF_ROWS": "0"})),
     (3, dict(dtype="bf16", env={"FM_SELF_ROWS": "0"}))])
 def test_ranks_on_one_gpu_equal_one_process(tmp_path, world, variant):
     """Self rows (the default) at world 2-4: each rank reads its own rows from its table and
@@ -120,7 +120,7 @@ def test_ranks_on_one_gpu_equal_one_process(tmp_path, world, variant):
     res = [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(world)]
     if "prefetch_rows" not in variant:  # default at world > 1: early row exchange on
         assert all(r["early"] == STEPS - 1 for r in res)
-    assert all(r["split"] == (variant.get("overlap_grads") == "on") for r in res)  # (split backward: opt-in)
+    assert all(r["split"] == (variant.get("overlap_grads", "auto") != "off") for r in res)  # (split: default on)
     ref = FactorizationMachine(_cfg("local", B * world, dtype=variant.get("dtype", "fp32")), device="cuda")
     for s in range(STEPS):
         parts = [_batch(s, r) for r in range(world)]

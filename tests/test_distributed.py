@@ -36,7 +36,7 @@ def _cfg(mode, grad_reduce, bcfg, mb=0):
     return FMConfig(vocabulary_size=V, factor_num=KF, loss_type="logistic", factor_lambda=0.05, bias_lambda=0.02,
                     batch_size=bcfg, init_value_range=0.1, seed=11, mode=mode, grad_reduce=grad_reduce,
                     opt=K.OptConfig("adagrad", lr=0.1, initial_accumulator=0.1), threads=1, microbatches=mb,
-                    overlap_grads="on")  # (split backward: opt-in, covered here with one part)
+                    overlap_grads="on")  # (split backward: the default with one part)
 
 
 def _batch(step, rank):
