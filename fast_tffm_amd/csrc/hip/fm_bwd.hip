@@ -214,9 +214,9 @@ constexpr int chunk_min_waves() {
 }
 
 // One lane group per chunk of <= CH (<= kMaxCH) sorted occurrences of one row.
-// kPieces: the walk can follow a split backward's piece ranges (a.piece >= 0, LDS + a barrier).
-template <int LPR, typename TV, bool kPieces>
-__device__ __forceinline__ void chunk_body(const BwdArgs& a) {
+template <int LPR, typename TV>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(chunk_min_waves<LPR, TV>())))
+void fm_bwd_chunk_kernel(BwdArgs a) {
   const uint32_t sr = sr_step_seed(a.sr_counter);  // stochastic rounding seed (0: nearest)
   constexpr int EPL = Frag<TV>::N;  // elements per lane of the table dtype
   constexpr int G = kWave / LPR;
@@ -232,7 +232,7 @@ __device__ __forceinline__ void chunk_body(const BwdArgs& a) {
   const int nchunks = a.counts[1];
   // split-backward piece: this piece's chunk ranges (one per owner) and their prefix sums
   __shared__ int pr_start[kMaxPieceOwners], pr_pre[kMaxPieceOwners + 1];
-  const bool pieced = kPieces && a.piece >= 0;
+  const bool pieced = a.piece >= 0;
   if (pieced) {
     if (threadIdx.x == 0) {
       int acc = 0;
@@ -402,22 +402,6 @@ __device__ __forceinline__ void chunk_body(const BwdArgs& a) {
       }
     }
   }
-}
-
-template <int LPR, typename TV>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(chunk_min_waves<LPR, TV>())))
-void fm_bwd_chunk_kernel(BwdArgs a) {
-  chunk_body<LPR, TV, true>(a);
-}
-
-// The same walk compiled without the piece support (no LDS, no barrier).  Codegen alone moves the
-// chunk kernel: same-box A/B of a build with the pieces compiled out (profiles/r3/chunk_flat_ab.txt):
-// k128 fp8 FTRL 0.925 -> 0.885 ms, k64 fp32 0.667 -> 0.666, k16 bf16 0.499 -> 0.529 (slower):
-// used for fp8 tables only, when the backward is not split.
-template <int LPR, typename TV>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(chunk_min_waves<LPR, TV>())))
-void fm_bwd_chunk_flat_kernel(BwdArgs a) {
-  chunk_body<LPR, TV, false>(a);
 }
 
 // Rows split over 2..kSmallChunks chunks: one lane group, ordered sum of the partials.
@@ -795,15 +779,7 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   // (a split walk -- the chunks of multi-chunk rows first, their combine beside the single-chunk
   // rows' launch, or both launches concurrent -- measured slower: k64 0.669 -> 0.72-0.78 ms, each
   // launch as long as the whole walk; profiles/r3/bwd_split_ab.txt)
-  static const bool flat_ok = [] {  // FM_CHUNK_FLAT=0: the piece-capable kernel for every dtype (A/B)
-    const char* e = getenv("FM_CHUNK_FLAT");
-    return !(e && e[0] == '0');
-  }();
-  if (dtype == kFP8 && a.piece < 0 && flat_ok) {
-    FM_DISPATCH_LPR(lpr, fm_bwd_chunk_flat_kernel, fp8e4m3, g1, st, a)
-  } else {
-    FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, a);
-  }
+  FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, a);
   FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, a);
   FM_DISPATCH(dtype, lpr, fm_bwd_big_kernel, 1024, st, a);
   if (dense) {
