@@ -25,6 +25,7 @@ using u64 = std::uintptr_t;
 #include "fm_fwd.hip"
 #include "hot.hip"
 #include "dedup.hip"
+#include "hdedup.hip"
 #include "shard.hip"
 #include "init.hip"
 #include "parse.hip"
@@ -56,6 +57,16 @@ fm::SelfRows self_rows(const std::vector<long long>& f) {
   r.keys = P<const int>((u64)f[3]); r.excl = P<const int>((u64)f[4]);
   r.v = P<const void>((u64)f[5]); r.v_stride = f[6]; r.w = P<float>((u64)f[7]); r.w_stride = f[8];
   return r;
+}
+
+fm::HdDict hd_dict(const std::vector<long long>& f) {
+  if (f.size() != 6) throw std::invalid_argument("hot dictionary: [keys, n, ht_key, ht_idx, sel, meta]");
+  for (long long x : f)
+    if (!x) throw std::invalid_argument("hot dictionary: null buffer");
+  fm::HdDict d;
+  d.keys = P<int>((u64)f[0]); d.n = P<int>((u64)f[1]); d.ht_key = P<int>((u64)f[2]); d.ht_idx = P<int>((u64)f[3]);
+  d.sel = P<int>((u64)f[4]); d.meta = P<int>((u64)f[5]);
+  return d;
 }
 
 fm::OptParams opt_params(int type, float lr, float l1, float l2, float beta) {
@@ -221,6 +232,42 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("vals"), py::arg("sorted_x"), py::arg("payload_is_ex"), py::arg("ex_shift"), py::arg("offsets"),
       py::arg("dense_min"), py::arg("dense_list"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"),
       py::arg("n_dev") = 0, py::arg("algo") = (int)fm::kSortBucket);
+  // hot-dictionary dedup (hdedup.hip): the dictionary travels as [keys, n, ht_key, ht_idx, sel, meta]
+  m.def("hd_workspace_bytes", &fm::hd_workspace_bytes, py::arg("n"));
+  m.attr("HD_MAX_H") = fm::kHdMaxH;
+  m.attr("HD_SLOTS") = fm::kHdSlots;
+  // phase 1 (classify, cold count -> hc[0], hot counts) / phase 2 (cold sort of n_c pairs, merge, plan)
+  m.def(
+      "dedup_hd",
+      [](int phase, int n_c, int n, int kb, int CH, u64 keys, u64 payload, const std::vector<long long>& dict, u64 ws,
+         size_t ws_bytes, u64 hc, u64 skeys, u64 spay, u64 uniq, u64 seg_start, u64 seg_chunk, u64 chunk_start,
+         u64 chunk_seg, u64 chunk_key, u64 counts, u64 stream) {
+        fm::HdLaunch p{};
+        p.n = n; p.kb = kb; p.CH = CH; p.keys = P<const uint32_t>(keys); p.pay = P<const int>(payload);
+        p.d = hd_dict(dict);
+        p.ws = P<void>(ws); p.ws_bytes = ws_bytes; p.hc = P<int>(hc);
+        p.skeys = P<uint32_t>(skeys); p.spay = P<int>(spay); p.uniq = P<uint32_t>(uniq);
+        p.seg_start = P<int>(seg_start); p.seg_chunk = P<int>(seg_chunk); p.chunk_start = P<int>(chunk_start);
+        p.chunk_seg = P<int>(chunk_seg); p.chunk_key = P<int>(chunk_key); p.counts = P<int>(counts);
+        if (!p.keys || !p.pay || !p.spay || !p.uniq || !p.seg_start || !p.seg_chunk || !p.chunk_start ||
+            !p.chunk_seg || !p.chunk_key || !p.counts || !p.ws || !p.hc)
+          throw std::invalid_argument("dedup_hd: null buffer");
+        if (phase == 1) check(fm::launch_hd_phase1(p, S(stream)), "dedup_hd phase 1");
+        else if (phase == 2) check(fm::launch_hd_phase2(p, n_c, S(stream)), "dedup_hd phase 2");
+        else throw std::invalid_argument("dedup_hd: phase 1 or 2");
+      },
+      py::arg("phase"), py::arg("n_c"), py::arg("n"), py::arg("kb"), py::arg("CH"), py::arg("keys"),
+      py::arg("payload"), py::arg("dict"), py::arg("ws"), py::arg("ws_bytes"), py::arg("hc"), py::arg("skeys"),
+      py::arg("spay"), py::arg("uniq"), py::arg("seg_start"), py::arg("seg_chunk"), py::arg("chunk_start"),
+      py::arg("chunk_seg"), py::arg("chunk_key"), py::arg("counts"), py::arg("stream"));
+  m.def(
+      "hd_dict_refresh",
+      [](const std::vector<long long>& dict, u64 counts, u64 seg_start, u64 uniq, int n_max, u64 stream) {
+        check(fm::launch_hd_dict_refresh(hd_dict(dict), P<const int>(counts), P<const int>(seg_start),
+                                         P<const uint32_t>(uniq), n_max, S(stream)),
+              "hd_dict_refresh");
+      },
+      py::arg("dict"), py::arg("counts"), py::arg("seg_start"), py::arg("uniq"), py::arg("n_max"), py::arg("stream"));
   m.attr("DEDUP_BUCKET") = (int)fm::kSortBucket;
   m.attr("DEDUP_ONESWEEP") = (int)fm::kSortOnesweep;
   m.attr("MAX_DENSE") = fm::kMaxDense;

@@ -297,11 +297,16 @@ class FactorizationMachine:
             raise ValueError("mode=local needs world_size == 1")
         self.mode = mode
         sharded = mode == "shard"
-        # (dp_dense: the replica is cut into W equal row slices, one updated per rank)
+        # (dp_dense: the replica is cut into P blocks of W equal row ranges, one per rank)
+        rows_multiple = 1
+        if mode == "dp_dense":
+            from ..parallel.exchange import dp_dense_blocks
+
+            rows_multiple = self.world * dp_dense_blocks(self.world)
         self.table = FMTable(cfg.vocabulary_size, cfg.factor_num, world=self.world if sharded else 1,
                              rank=self.rank if sharded else 0, dtype=cfg.dtype, opt=cfg.opt,
                              init_range=cfg.init_value_range, seed=cfg.seed, device=self.device,
-                             rows_multiple=self.world if mode == "dp_dense" else 1)
+                             rows_multiple=rows_multiple)
         self.K, self.Kp = self.table.K, self.table.Kp
         self.rps = rows_per_shard(cfg.vocabulary_size, self.world) if sharded else cfg.vocabulary_size
         self.ws = _Workspace(self.device, self.Kp, cfg.dedup_chunk, K.r1_dtype(cfg.dtype))
@@ -321,6 +326,9 @@ class FactorizationMachine:
         self._hot_want = (self.device.type == "cuda" and mode == "local" and self.Kp <= 128
                           and os.environ.get("FM_HOT_ROWS", "0") == "1")
         self._hot_refresh = max(0, int(os.environ.get("FM_HOT_REFRESH", "0")))  # steps; 0: pick once
+        # hot-row dictionary of the GPU dedup (hip/hdedup.hip): the frequent rows of earlier plans skip
+        # the radix sort (FM_DEDUP=onesweep: every occurrence sorted); plans are the same either way
+        self._hot_dict = K.HotDict(self.device) if self.device.type == "cuda" and mode == "local" else None
         self._graph = None
         self._graph_pool: list[_GraphedStep] = []
         self._exchange = None
@@ -531,14 +539,15 @@ class FactorizationMachine:
                 ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz, slot_bits=sb)
                 dd = K.dedup(rows, ws=ws.dd, key_bits=bits_for(self.table.rows), ex_of_occ=ex, vals=b.vals,
                              num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets,
-                             dense_min=0)  # (runs beside the forward, which counts dense rows: off here)
+                             dense_min=0,  # (runs beside the forward, which counts dense rows: off here)
+                             hot_dict=self._hot_dict, want_skeys=False)
         else:
             ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz)
         with roctx_range("fwd"):
             fo = K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,
                               weights=b.weights, loss=cfg.loss_type, grad_scale=self.grad_scale(b.B), want_r1=True,
                               pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
-                              threads=cfg.threads, bias=self.gbias)
+                              threads=cfg.threads, bias=self.gbias, defer_loss=gpu)
             self.bias_step(fo.dpred)
         if gpu:
             main.wait_stream(side)
@@ -549,16 +558,19 @@ class FactorizationMachine:
             K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
                           reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, dense_part=ws.dense_part,
                           dense_stream=self._dense_stream() if gpu else None, sr_counter=self.sr_tick())
-        return StepOut(fo.loss_sum, b.B)
+        return StepOut(fo.finish_loss(), b.B)
 
     # ------------------------------------------------------------------
-    def _local_plan(self, b: Batch, inputs_ready=None) -> "_LocalPlan":
+    def _local_plan(self, b: Batch, inputs_ready=None, avoid: int | None = None) -> "_LocalPlan":
         """dedup (+ csr_rows) of ``b`` on the side stream into the next of the plan slots.
 
         Slots are taken round robin, so the live plans -- the current step's and at most two
         pending ones, the last three created -- never share one; ``slot.done`` orders the reuse
-        after the step that last read it."""
+        after the step that last read it.  ``avoid``: the slot of a plan whose step has not
+        recorded its ``done`` yet (dp_dense plans ahead before the current step's collectives)."""
         idx = (self._llast + 1) % len(self._lslots)
+        if idx == avoid:
+            idx = (idx + 1) % len(self._lslots)
         self._llast = idx
         slot = self._lslots[idx]
         cfg = self.cfg
@@ -615,7 +627,8 @@ class FactorizationMachine:
                      num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets,
                      dense_min=K.dense_min_for(b.B, self.Kp, cfg.dedup_chunk, table_dtype=self.table.v.dtype,
                                                has_vals=b.vals is not None,
-                                               max_feats=b.max_feats))
+                                               max_feats=b.max_feats),
+                     hot_dict=self._hot_dict, want_skeys=False)
         return rows, dd
 
     def _hot_from_plan(self, dd) -> None:
@@ -646,14 +659,14 @@ class FactorizationMachine:
             fo = K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,
                               weights=b.weights, loss=cfg.loss_type, grad_scale=self.grad_scale(b.B), want_r1=True,
                               pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
-                              threads=cfg.threads, bias=self.gbias, dense=dd, dense_A=dA, hot=hot)
+                              threads=cfg.threads, bias=self.gbias, dense=dd, dense_A=dA, hot=hot, defer_loss=True)
             self.bias_step(fo.dpred)
         with roctx_range("bwd+update"):
             K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
                           reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, dense_part=ws.dense_part,
                           dense_stream=self._dense_stream(),
                           sr_counter=self.sr_tick(), dense_A=dA, hot=hot)
-        return StepOut(fo.loss_sum, b.B)
+        return StepOut(fo.finish_loss(), b.B)
 
     def _local_lookahead_step(self, b: Batch, next_batch: Batch | None, next2: Batch | None = None) -> StepOut:
         """Eager local step with lookahead: the dedup of ``next_batch`` runs on the side stream

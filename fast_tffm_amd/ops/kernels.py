@@ -148,11 +148,19 @@ def _range_check(idx: torch.Tensor, hi: int, name: str) -> None:
 class FwdOut:
     """Outputs of fm_forward. ``loss_sum``/``regv``/``regw`` are 0-d tensors on the op's device."""
 
-    __slots__ = ("pred", "r1", "dpred", "loss_sum", "regv", "regw")
+    __slots__ = ("pred", "r1", "dpred", "loss_sum", "regv", "regw", "loss_partial")
 
-    def __init__(self, pred, r1, dpred, loss_sum, regv, regw):
+    def __init__(self, pred, r1, dpred, loss_sum, regv, regw, loss_partial=None):
         self.pred, self.r1, self.dpred = pred, r1, dpred
         self.loss_sum, self.regv, self.regw = loss_sum, regv, regw
+        self.loss_partial = loss_partial  # per-workgroup loss sums when the reduction was deferred
+
+    def finish_loss(self) -> torch.Tensor | None:
+        """The summed loss; a deferred reduction (``fm_forward(defer_loss=True)``) is enqueued now,
+        on the current stream."""
+        if self.loss_sum is None and self.loss_partial is not None:
+            self.loss_sum = self.loss_partial.sum(dtype=torch.float32)
+        return self.loss_sum
 
 
 def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | None, v: torch.Tensor,
@@ -164,7 +172,7 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
                bias: torch.Tensor | None = None, dense: "DedupOut | None" = None,
                dense_A: torch.Tensor | None = None, dense_by_segment: bool = False,
                self_rows: SelfRows | None = None, seg_lookup: "SegIndex | None" = None,
-               hot: HotRows | None = None) -> FwdOut:
+               hot: HotRows | None = None, defer_loss: bool = False) -> FwdOut:
     """FM score of a CSR batch (reference FmScorer, cc/fm_scorer_op.h:101-140), fused with the loss.
 
     pred_i = sum_j x_j w_j + 1/2 sum_k [(sum_j x_j v_jk)^2 - sum_j x_j^2 v_jk^2]  (+ bias[0], optional
@@ -181,6 +189,8 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
     row of ``v``) is found through the bucket index (``seg_index``) instead of an inverse map.
     ``hot`` (GPU, with ``dense_A``): count the occurrences of these table rows instead of a
     dedup's dense rows.
+    (``defer_loss``, GPU: the per-workgroup loss partials are left for ``FwdOut.finish_loss``, so the
+    reduction can be enqueued after the backward instead of between forward and backward.)
     """
     dev = rows.device
     B = offsets.numel() - 1
@@ -253,9 +263,12 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
         # backward) made the chunk kernel itself ~30% slower even when not taken -- a workgroup
         # barrier in the chunk kernel changes its code (k64 0.668 -> 0.88 ms, same box;
         # profiles/r3/fused_loss_ab.txt)
-        loss_sum = lp.sum(dtype=torch.float32) if lt else None
+        # (the local step defers this reduction past the backward: nothing reads the loss before it)
+        loss_sum = lp.sum(dtype=torch.float32) if lt and not defer_loss else None
         regv = rp.view(grid, 2)[:, 0].sum() if want_reg else None
         regw = rp.view(grid, 2)[:, 1].sum() if want_reg else None
+        if lt and defer_loss:
+            return FwdOut(pred, r1, dpred, None, regv, regw, loss_partial=lp)
     else:
         _check(self_rows is None, "self rows are a GPU path")
         c = native.cpu()
@@ -443,11 +456,53 @@ def dedup_sort_algo() -> int:
     return h.DEDUP_BUCKET if v == "bucket" else h.DEDUP_ONESWEEP
 
 
+class HotDict:
+    """Dictionary of the hot-dictionary GPU dedup (hip/hdedup.hip): up to HD_MAX_H frequent table
+    rows (ascending, with their LDS hash table), rebuilt on the device from a finished plan every
+    ``refresh`` plans (the first plan's included).  Its occurrences skip the radix sort; the plan
+    is the same whatever the dictionary holds, so staleness costs speed only."""
+
+    def __init__(self, device: torch.device, refresh: int | None = None):
+        h = native.hip()
+        i32 = dict(dtype=torch.int32, device=device)
+        self.keys = torch.zeros(h.HD_MAX_H, **i32)
+        self.n = torch.zeros(1, **i32)
+        self.ht_key = torch.full((h.HD_SLOTS,), -1, **i32)
+        self.ht_idx = torch.zeros(h.HD_SLOTS, **i32)
+        self.sel = torch.zeros(h.HD_MAX_H, **i32)
+        self.meta = torch.zeros(40, **i32)
+        self.refresh = max(1, int(refresh if refresh is not None else os.environ.get("FM_HD_REFRESH", "8")))
+        self.plans = 0
+
+    def packed(self) -> list[int]:
+        return [_p(self.keys), _p(self.n), _p(self.ht_key), _p(self.ht_idx), _p(self.sel), _p(self.meta)]
+
+    def rebuild(self, dd: "DedupOut") -> None:
+        """Re-derive the dictionary from plan ``dd`` (on the current stream, after the plan)."""
+        native.hip().hd_dict_refresh(dict=self.packed(), counts=_p(dd.counts), seg_start=_p(dd.seg_start),
+                                     uniq=_p(dd.uniq), n_max=int(dd.n), stream=_stream(dd.counts))
+
+    def after_plan(self, dd: "DedupOut") -> None:
+        """Count a finished plan; rebuild from it when due (plans 0, refresh, 2 * refresh, ...)."""
+        if self.plans % self.refresh == 0:
+            self.rebuild(dd)
+        self.plans += 1
+
+
+def hd_dedup_enabled() -> bool:
+    """FM_DEDUP=hd: the hot-dictionary dedup where it applies; onesweep (default): the radix sort
+    of every occurrence."""
+    v = os.environ.get("FM_DEDUP", "onesweep")
+    _check(v in ("hd", "onesweep"), "FM_DEDUP must be hd or onesweep")
+    return v == "hd"
+
+
 def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int = 32,
           ex_of_occ: torch.Tensor | None = None, vals: torch.Tensor | None = None, want_inv: bool = False,
           CH: int | None = None, want_perm: bool = False, num_examples: int | None = None,
           Kp: int | None = None, ex_shift: int = 0, offsets: torch.Tensor | None = None,
-          dense_min: int = 0, n_dev: torch.Tensor | None = None) -> DedupOut:
+          dense_min: int = 0, n_dev: torch.Tensor | None = None, hot_dict: HotDict | None = None,
+          want_skeys: bool = True) -> DedupOut:
     """Sort-based unique over non-negative int32 keys (reference tf.unique, fm_model.py:72).
 
     Unique keys come out in ascending order (the reference's first-occurrence
@@ -487,7 +542,32 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
                    sorted_x=ws.sorted_x if vals is not None else None, CH=CH, big_list=ws.big_list,
                    big_count=ws.big_count, multi=ws.multi, ex_shift=int(ex_shift),
                    dense_list=ws.dense_list if dense_min > 0 and ex_of_occ is not None and _is_gpu(keys) else None)
-    if _is_gpu(keys):
+    if (_is_gpu(keys) and hot_dict is not None and ex_payload and not want_inv and vals is None and n_dev is None
+            and out.dense_list is None and 0 < n and key_bits <= 31 and hd_dedup_enabled()
+            and not torch.cuda.is_current_stream_capturing()):  # (a host wait between its two phases)
+        # hot-dictionary dedup (hip/hdedup.hip): the same plan, sorting only the long tail
+        h = native.hip()
+        _check(1 <= CH <= h.MAX_CH, f"CH must be in [1, {h.MAX_CH}]")
+        need = h.hd_workspace_bytes(n)
+        if getattr(ws, "hd_ws", None) is None or ws.hd_ws.numel() < need:
+            ws.hd_ws = torch.empty(h.hd_workspace_bytes(max(n, ws.cap)), dtype=torch.uint8, device=dev)
+            ws.hd_hc = torch.zeros(8, dtype=torch.int32, device=dev)
+            ws.hd_hc_host = torch.zeros(8, dtype=torch.int32, pin_memory=True)
+            ws.hd_ev = torch.cuda.Event()
+        kw = dict(n=n, kb=key_bits, CH=CH, keys=_p(keys), payload=_p(ex_of_occ), dict=hot_dict.packed(),
+                  ws=_p(ws.hd_ws), ws_bytes=ws.hd_ws.numel(), hc=_p(ws.hd_hc), skeys=_p(ws.skeys) if want_skeys else 0,
+                  spay=_p(ws.perm), uniq=_p(ws.uniq), seg_start=_p(ws.seg_start), seg_chunk=_p(ws.seg_chunk),
+                  chunk_start=_p(ws.chunk_start), chunk_seg=_p(ws.chunk_seg), chunk_key=_p(ws.chunk_key),
+                  counts=_p(ws.counts), stream=_stream(keys))
+        h.dedup_hd(phase=1, n_c=0, **kw)
+        # the cold count sizes the radix sort: one host wait, on this (side) stream, for phase 1
+        ws.hd_hc_host.copy_(ws.hd_hc, non_blocking=True)
+        ws.hd_ev.record()
+        ws.hd_ev.synchronize()
+        h.dedup_hd(phase=2, n_c=int(ws.hd_hc_host[0]), **kw)
+        out.bwd_fresh = True
+        hot_dict.after_plan(out)
+    elif _is_gpu(keys):
         h = native.hip()
         _check(1 <= CH <= h.MAX_CH, f"CH must be in [1, {h.MAX_CH}]")
         algo = dedup_sort_algo()
@@ -690,8 +770,8 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
            "hot rows: GPU LOCAL step, Kp <= 128, no dedup dense rows")
     o = opt or OptConfig()
     if piece >= 0:
-        _check(_is_gpu(dpred) and seg_bounds is not None and mode == BWD_EMIT and dd.dense_list is None,
-               "split backward pieces: GPU, EMIT mode, seg_bounds, no dense path")
+        _check(_is_gpu(dpred) and seg_bounds is not None and mode in (BWD_EMIT, BWD_EMIT_TABLE)
+               and dd.dense_list is None, "split backward pieces: GPU, EMIT / EMIT_TABLE, seg_bounds, no dense rows")
         _chk_vec(seg_bounds, torch.int32, 3, "seg_bounds", dev)
     if _is_gpu(dpred):
         h = native.hip()

@@ -973,46 +973,67 @@ class DPExchange(_Base):
                             threads=self.m.cfg.threads, bias=self.m.gbias)
 
 
+def dp_dense_blocks(world: int) -> int:
+    """Row blocks of the dp_dense step's pipeline (FM_DP_BLOCKS; default 4 at world > 1, 1 alone)."""
+    v = os.environ.get("FM_DP_BLOCKS")
+    return max(1, int(v)) if v else (4 if world > 1 else 1)
+
+
 class DPDenseExchange(DPExchange):
     """Replicated table; dense gradient buffer reduce-scattered over the ranks, each rank updating
-    its own slice of rows, the updated rows all-gathered (small vocabularies, BASELINE config 3).
+    its own rows, the updated rows all-gathered (small vocabularies, BASELINE config 3).
 
-    GPU step (no host synchronisation, lookahead dedup as in the local step):
+    Ownership: the replica's V rows form P blocks of Vb = V / P rows (FM_DP_BLOCKS, ``dp_dense_blocks``);
+    block p's rows [p Vb + r Sb, p Vb + (r+1) Sb), Sb = Vb / W, belong to rank r (V is padded to a
+    multiple of W P, FMTable ``rows_multiple``), so every block's reduce-scatter / all-gather is
+    one in-place collective over a contiguous range.
+
+    GPU step (no host synchronisation, lookahead dedup as in the local step), pipelined over the
+    blocks -- each collective is issued asynchronously on the communicator's stream right after its
+    inputs are enqueued, so it runs beside the compute stream's next piece:
       dedup of this batch (side stream, done during the previous step) -> forward on the replica
-      -> backward in EMIT_TABLE mode: each unique row's [g_v | g_w | 1] is scattered straight into
-      the persistent dense buffer ``G`` [V, Kp+4] (the touch word marks it; V is padded to a
-      multiple of W, FMTable ``rows_multiple``) -> in-place reduce-scatter of ``G`` (rank r
-      receives the sums of its slice, rows [r S, (r+1) S), S = V / W; ``comm_dtype = bf16``
-      halves the bytes) -> ``dense_apply`` on that slice only: the optimizer's read-modify-write
-      of rows and state is split W ways and every touched row of the slice is zeroed in ``G`` ->
-      this rank's scattered rows of the OTHER slices are zeroed (``zero_listed_rows`` over the
-      dedup's unique rows), so ``G`` is never cleared wholesale -> in-place all-gather of every
-      slice's updated [v] and [w] rows: identical replicas.  The next batch's dedup (side stream)
-      runs beside the collectives.
+      -> per block p: backward piece p in EMIT_TABLE mode (the segments whose keys fall in block p:
+      each unique row's [g_v | g_w | 1] scattered into the persistent dense buffer ``G`` [V, Kp+4],
+      the touch word marking it) -> reduce-scatter of block p of ``G`` (RS(p) runs while piece
+      p+1 is reduced; ``comm_dtype = bf16`` halves the bytes)
+      -> per block p: wait RS(p) -> ``dense_apply`` of the own rows of block p (the optimizer's
+      read-modify-write split W ways, every touched own row zeroed in ``G``) -> all-gather of
+      block p's [v] and [w] rows (AG(p) runs while block p+1 is applied)
+      -> this rank's scattered rows of the OTHER ranks' ranges are zeroed (``zero_listed_rows`` over
+      the dedup's unique rows), so ``G`` is never cleared wholesale -> the compute stream waits
+      for the all-gathers: identical replicas.  The next batch's dedup (side stream) runs beside.
     Bytes per rank and step: (W-1)/W of the buffer (reduce-scatter) + (W-1)/W of the parameter
     rows (all-gather), the same as the all-reduce it replaces, but the apply work no longer
-    repeats on every rank and the optimizer state is only ever touched by its slice's owner
-    (``sync_state`` all-gathers it for checkpoints).
-    The CPU (gloo) path follows the same structure with plain torch ops (gloo has no
-    reduce-scatter: the all-reduced buffer's slice is the same sum)."""
+    repeats on every rank and the optimizer state is only ever touched by its rows' owner
+    (``sync_state`` all-gathers it for checkpoints).  What cannot overlap in a synchronous step:
+    the forward (it reads every block's updated rows) and the last block's collectives
+    (``tools/comm_model.py``).  The CPU (gloo) path follows the same ownership with plain torch
+    ops (gloo has no reduce-scatter: the all-reduced buffer's rows are the same sums)."""
 
     supports_lookahead = True
 
     def __init__(self, model):
         super().__init__(model)
         V = model.table.rows
-        if V % self.W:
-            raise ValueError("dp_dense: the replicated table's rows must be a multiple of the world size")
-        self.S = V // self.W
-        self.r0 = self.ctx.rank * self.S
+        self.P = dp_dense_blocks(self.W)
+        if V % (self.W * self.P):
+            raise ValueError("dp_dense: the replicated table's rows must be a multiple of world size x blocks")
+        self.Vb = V // self.P
+        self.Sb = self.Vb // self.W
         self.dense = torch.zeros((V, self.gs), dtype=torch.float32, device=self.dev)
         self.arange = torch.arange(V + 1, dtype=torch.int32, device=self.dev)
         self.wire16 = (torch.empty((V, self.gs), dtype=torch.bfloat16, device=self.dev)
                        if self.dev.type == "cuda" and model.cfg.comm_dtype == "bf16" else None)
+        self.bounds = torch.zeros(self.P + 2, dtype=torch.int32, device=self.dev)
 
     def close(self) -> None:
         self.dense = self.wire16 = None
         super().close()
+
+    def own_range(self, p: int) -> tuple[int, int]:
+        """Rows [a, b) of block p owned by this rank."""
+        a = p * self.Vb + self.ctx.rank * self.Sb
+        return a, a + self.Sb
 
     def _param_tensors(self) -> list[torch.Tensor]:
         """The replica's parameter tensors, rows first (all-gathered after the sharded apply)."""
@@ -1024,27 +1045,54 @@ class DPDenseExchange(DPExchange):
         t = self.m.table
         return [x for x in (t.s0v, t.s0w, t.s1v, t.s1w) if x is not None]
 
-    def _all_gather_rows(self, tensors: list[torch.Tensor]) -> None:
-        """Every rank's slice of each tensor (rows [q S, (q+1) S)) to every rank, in place."""
+    def _all_gather_block(self, tensors: list[torch.Tensor], p: int, async_op: bool = False) -> list:
+        """Every rank's own rows of block p of each tensor to every rank, in place."""
         if self.W == 1:
-            return
-        r0, r1 = self.r0, self.r0 + self.S
+            return []
+        a, b = self.own_range(p)
+        blk = slice(p * self.Vb, (p + 1) * self.Vb)
+        works = []
         for t in tensors:
             if self.dev.type == "cuda":
-                dist.all_gather_into_tensor(t, t[r0:r1], group=self.group)
-                self.bytes_sent += (self.W - 1) * t[r0:r1].numel() * t.element_size()
+                w = dist.all_gather_into_tensor(t[blk], t[a:b], group=self.group, async_op=async_op)
+                if w is not None:
+                    works.append(w)
             else:
-                parts = [torch.empty_like(t[r0:r1]) for _ in range(self.W)]
-                dist.all_gather(parts, t[r0:r1].contiguous(), group=self.group)
-                t.copy_(torch.cat(parts))
-                self.bytes_sent += (self.W - 1) * t[r0:r1].numel() * t.element_size()
+                parts = [torch.empty_like(t[a:b]) for _ in range(self.W)]
+                dist.all_gather(parts, t[a:b].contiguous(), group=self.group)
+                t[blk].copy_(torch.cat(parts))
+            self.bytes_sent += (self.W - 1) * t[a:b].numel() * t.element_size()
+        return works
+
+    def _all_gather_rows(self, tensors: list[torch.Tensor]) -> None:
+        for p in range(self.P):
+            self._all_gather_block(tensors, p)
 
     def sync_state(self) -> None:
-        """All-gather the optimizer state slices (each rank's apply only updates its own rows'
-        state): after this every replica holds the full state (checkpoints, re-sharding)."""
+        """All-gather the optimizer state (each rank's apply only updates its own rows' state):
+        after this every replica holds the full state (checkpoints, re-sharding)."""
         if self.dev.type == "cuda":
             torch.cuda.current_stream(self.dev).synchronize()
         self._all_gather_rows(self._state_tensors())
+
+    def _block_bounds(self, dd) -> torch.Tensor:
+        """int32 [P + 2] device: first segment of each block (keys ascending), U twice at the end."""
+        cnt = K.owner_counts(dd, self.Vb, self.P)
+        self.bounds[1: self.P + 1].copy_(torch.cumsum(cnt, 0))
+        self.bounds[self.P + 1: self.P + 2].copy_(self.bounds[self.P: self.P + 1])
+        return self.bounds
+
+    def _reduce_scatter_block(self, p: int):
+        a, b = self.own_range(p)
+        blk = slice(p * self.Vb, (p + 1) * self.Vb)
+        if self.wire16 is not None:
+            self.wire16[blk].copy_(self.dense[blk])
+            w = dist.reduce_scatter_tensor(self.wire16[a:b], self.wire16[blk], group=self.group, async_op=True)
+            self.bytes_sent += (self.W - 1) * self.Sb * self.gs * 2
+        else:
+            w = dist.reduce_scatter_tensor(self.dense[a:b], self.dense[blk], group=self.group, async_op=True)
+            self.bytes_sent += (self.W - 1) * self.Sb * self.gs * 4
+        return w
 
     def train_step(self, b: Batch, next_batch: Batch | None = None, next2: Batch | None = None):
         from ..models.fm import StepOut
@@ -1072,41 +1120,50 @@ class DPDenseExchange(DPExchange):
                               bias=m.gbias, dense=pl.dd, dense_A=dA)
             m.bias_step(fo.dpred)
         rv, rw = m.reg_coeffs
-        with roctx_range("bwd_scatter"):
-            K.fm_backward(pl.dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT_TABLE, table=m.table.state,
-                          grad_out=self.dense, reg_v=rv, reg_w=rw, partial=ws.bwd_partial,
-                          dense_part=ws.dense_part, dense_stream=m._dense_stream(), dense_A=dA)
+        # backward pieces by key block, each block's reduce-scatter issued behind its piece
+        pieces = self.W > 1 and self.P > 1 and dA is None
+        bounds = self._block_bounds(pl.dd) if pieces else None
+        rs = []
+        with roctx_range("bwd_scatter+reduce_scatter"):
+            for p in range(self.P if pieces else 1):
+                K.fm_backward(pl.dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT_TABLE, table=m.table.state,
+                              grad_out=self.dense, reg_v=rv, reg_w=rw, partial=ws.bwd_partial,
+                              dense_part=ws.dense_part, dense_stream=m._dense_stream(), dense_A=dA,
+                              piece=0 if pieces else -1, seg_bounds=bounds[p: p + 3] if pieces else None)
+                if pieces:
+                    rs.append(self._reduce_scatter_block(p))
+            if self.W > 1 and not pieces:
+                rs = [self._reduce_scatter_block(p) for p in range(self.P)]
         # the next batches' dedup (side stream) overlaps the collectives, the apply and -- depth 2,
         # like the local step -- the next step's forward / backward
+        # (this step's slot has no done event yet -- the apply and zero_listed_rows below still read
+        # its plan -- so the new plans avoid it)
         if next_batch is not None and (m._lpending is None or m._lpending.b is not next_batch):
-            m._lpending = m._local_plan(next_batch, nb_ready)
+            m._lpending = m._local_plan(next_batch, nb_ready, avoid=pl.slot)
             m._lpending2 = None
         if (next2 is not None and m._lpending is not None and m._lpending2 is None
                 and os.environ.get("FM_LOCAL_DEPTH2", "1") != "0"):
             if getattr(next2, "ready", None) is None and nb_ready is None:
                 nb_ready = torch.cuda.Event()
                 nb_ready.record(main)
-            m._lpending2 = m._local_plan(next2, nb_ready)
-        r0, S = self.r0, self.S
-        own = self.dense[r0: r0 + S]
+            m._lpending2 = m._local_plan(next2, nb_ready, avoid=pl.slot)
+        ag = []
+        sr = m.sr_tick()
+        with roctx_range("apply+all_gather"):
+            for p in range(self.P):
+                a, e = self.own_range(p)
+                if self.W > 1:
+                    rs[p].wait()  # (the compute stream waits for the communicator's stream)
+                    if self.wire16 is not None:
+                        self.dense[a:e].copy_(self.wire16[a:e])
+                K.dense_apply(self.dense[a:e], m.table.state, cfg.opt, Kp, row0=a, rows=self.Sb, sr_counter=sr)
+                ag += self._all_gather_block(self._param_tensors(), p, async_op=True)
         if self.W > 1:
-            with roctx_range("reduce_scatter_grads"):
-                if self.wire16 is not None:
-                    self.wire16.copy_(self.dense)
-                    dist.reduce_scatter_tensor(self.wire16[r0: r0 + S], self.wire16, group=self.group)
-                    own.copy_(self.wire16[r0: r0 + S])
-                    self.bytes_sent += (self.W - 1) * S * self.gs * 2
-                else:
-                    dist.reduce_scatter_tensor(own, self.dense, group=self.group)
-                    self.bytes_sent += (self.W - 1) * S * self.gs * 4
-        with roctx_range("dense_apply"):
-            K.dense_apply(own, m.table.state, cfg.opt, Kp, row0=r0, rows=S, sr_counter=m.sr_tick())
-        if self.W > 1:
-            # this rank's contributions to the other slices (its own slice's touched rows were
-            # zeroed by the apply; re-zeroing them is harmless)
+            # this rank's contributions to the other ranks' rows (its own touched rows were zeroed
+            # by the apply; re-zeroing them is harmless); every reduce-scatter has been waited for
             K.zero_listed_rows(self.dense, pl.dd.uniq, pl.dd.counts[:1], pl.dd.n)
-            with roctx_range("all_gather_rows"):
-                self._all_gather_rows(self._param_tensors())
+            for w in ag:
+                w.wait()
         done = torch.cuda.Event()
         done.record(main)
         m._lslots[pl.slot].done = done
@@ -1124,13 +1181,15 @@ class DPDenseExchange(DPExchange):
         if self.W > 1:
             dist.all_reduce(dense, group=self.group)
             self.bytes_sent += 2 * (self.W - 1) * dense.numel() * 4 // self.W
-        r0, S = self.r0, self.S
-        own = dense[r0: r0 + S]
-        touched = torch.nonzero(own[:, self.Kp + 1] > 0).flatten().to(torch.int32)
-        T = touched.numel()
-        dd = K.DedupOut(n=T, uniq=touched + r0, perm=touched, seg_start=self.arange[: T + 1],
-                        num_unique=torch.tensor([T], dtype=torch.int32, device=self.dev), U_host=T)
-        K.apply_rows(dd, own, self.m.table.state, self.m.cfg.opt, self.Kp, threads=self.m.cfg.threads,
-                     sr_counter=self.m.sr_tick())
+        sr = self.m.sr_tick()
+        for p in range(self.P):
+            r0, r1 = self.own_range(p)
+            own = dense[r0:r1]
+            touched = torch.nonzero(own[:, self.Kp + 1] > 0).flatten().to(torch.int32)
+            T = touched.numel()
+            dd = K.DedupOut(n=T, uniq=touched + r0, perm=touched, seg_start=self.arange[: T + 1],
+                            num_unique=torch.tensor([T], dtype=torch.int32, device=self.dev), U_host=T)
+            K.apply_rows(dd, own, self.m.table.state, self.m.cfg.opt, self.Kp, threads=self.m.cfg.threads,
+                         sr_counter=sr)
         self._all_gather_rows(self._param_tensors())
         return StepOut(fo.loss_sum, b.B)

@@ -44,6 +44,11 @@ def _resolve_device(cfg: FMRunConfig, ctx: DistContext | None) -> torch.device:
     return torch.device("cuda" if torch.cuda.is_available() else "cpu")
 
 
+# Version of the loader's shuffle draws (csrc/cpu/loader.cpp ``bounded``): 1 = ``rng() % range``
+# (round 2), 2 = multiply-high.  Stored with every reader position; a resume across versions warns.
+DRAW_VERSION = 2
+
+
 class Trainer:
     def __init__(self, cfg: FMRunConfig, ctx: DistContext | None = None, *, monitor: bool = False,
                  trace: str | None = None, printer=print, trace_steps: int = 5):
@@ -89,6 +94,12 @@ class Trainer:
                            f"every rank resumes at rank 0's position")
         self.reader_state = ReaderState(epoch=int(rs.get("epoch", 0)),
                                         batches_in_epoch=int(rs.get("batches_in_epoch", 0)))
+        if rs and int(rs.get("draw_version", 1)) != DRAW_VERSION:
+            # the loader's shuffle draws changed between the builds: the same seed gives another line
+            # order, so replaying batches_in_epoch batches does not land on the same examples
+            self.print(f"Warning: checkpoint reader position was written with shuffle draw version "
+                       f"{rs.get('draw_version', 1)} (this build: {DRAW_VERSION}); the resumed epoch repeats "
+                       f"or skips some examples")
         self.restored_from = path
         self.print(f"Restored checkpoint {path} (global step {self.model.global_step})")
         return True
@@ -96,7 +107,8 @@ class Trainer:
     def save(self) -> str | None:
         if not self.cfg.log_dir:
             return None
-        rs = {"epoch": self.reader_state.epoch, "batches_in_epoch": self.reader_state.batches_in_epoch}
+        rs = {"epoch": self.reader_state.epoch, "batches_in_epoch": self.reader_state.batches_in_epoch,
+              "draw_version": DRAW_VERSION}
         return ckpt.save_checkpoint(self.model, self.cfg.log_dir, self.model.global_step, reader_state=rs,
                                     ctx=self.ctx if self.world > 1 else None)
 

@@ -1,8 +1,11 @@
-"""The row-sharded GPU executor at world 2-4 on ONE GPU.
+"""The multi-rank GPU executors at world 2-8 on ONE GPU.
 
-RCCL refuses two ranks on one device, so the ranks talk over gloo through a relay:
-``torch.distributed`` collectives / P2P ops called by the exchange on GPU tensors are
-staged through host memory.  Everything else is the real multi-rank GPU path --
+RCCL refuses two ranks on one device, so the ranks talk over gloo through an asynchronous relay
+(tests/relay.py): ``torch.distributed`` collectives / P2P ops called on GPU tensors are staged
+through host memory, and their results land late on a per-group comm stream behind a spin, with
+RCCL's stream semantics -- a missing work.wait / stream wait / record_stream in the executor
+reads stale rows or trips the relay's input-unchanged check.  Everything else is the real
+multi-rank GPU path --
 dedup + owner counts, run-merge apply over 2 runs, the early row exchange with its
 dirty scan / compaction / tagged patch gather / patch scatter between two ranks, the
 split backward with several owners and its send/recv pieces, depth-2 lookahead -- and
@@ -26,46 +29,6 @@ def _free_port() -> int:
     return free_port()
 
 
-class _Done:
-    def wait(self):
-        return True
-
-    def is_completed(self):
-        return True
-
-
-def _install_relay():
-    import torch.distributed as tdist
-
-    real_a2a, real_isend, real_irecv = tdist.all_to_all_single, tdist.isend, tdist.irecv
-
-    def a2a(out, inp, output_split_sizes=None, input_split_sizes=None, group=None, async_op=False):
-        if not (out.is_cuda or inp.is_cuda):
-            return real_a2a(out, inp, output_split_sizes, input_split_sizes, group=group, async_op=async_op)
-        o = torch.empty(out.shape, dtype=out.dtype)
-        real_a2a(o, inp.cpu(), output_split_sizes, input_split_sizes, group=group)
-        out.copy_(o)
-        return _Done() if async_op else None
-
-    def batch_isend_irecv(ops):
-        works, recvs = [], []
-        for op in ops:
-            if op.op in (tdist.isend, real_isend):
-                works.append(real_isend(op.tensor.cpu(), op.peer, group=op.group))
-            else:
-                buf = torch.empty(op.tensor.shape, dtype=op.tensor.dtype)
-                works.append(real_irecv(buf, op.peer, group=op.group))
-                recvs.append((op.tensor, buf))
-        for w in works:
-            w.wait()
-        for t, buf in recvs:
-            t.copy_(buf)
-        return [_Done()]
-
-    tdist.all_to_all_single = a2a
-    tdist.batch_isend_irecv = batch_isend_irecv
-
-
 def _cfg(mode, bcfg, **kw):
     from fast_tffm_amd.models.fm import FMConfig
     from fast_tffm_amd.ops import kernels as K
@@ -83,16 +46,18 @@ def _batch(step, rank):
     return CriteoSynth(V, seed=1000 * step + rank, device="cuda").batch(B)
 
 
-def _worker(rank, world, port, out_dir, variant):
+def _worker(rank, world, port, out_dir, variant, mode="shard"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    _install_relay()
+    import relay
+
+    relay.install()
     from fast_tffm_amd.models.fm import FactorizationMachine
     from fast_tffm_amd.parallel import dist as fmdist
 
     variant = dict(variant)
     os.environ.update(variant.pop("env", {}))
     ctx = fmdist.init_distributed(backend="gloo", rank=rank, world=world, device="cuda:0")
-    m = FactorizationMachine(_cfg("shard", B, **variant), device="cuda:0", dist=ctx)
+    m = FactorizationMachine(_cfg(mode, B, **variant), device="cuda:0", dist=ctx)
     bs = [_batch(s, rank) for s in range(STEPS)]
     losses = []
     for s in range(STEPS):
@@ -102,26 +67,17 @@ def _worker(rank, world, port, out_dir, variant):
     torch.cuda.synchronize()
     ex = m._exchange
     torch.save({"gids": m.table.global_ids().cpu(), "rows": m.table.reference_rows().cpu(), "losses": losses,
-                "early": ex.early_steps, "split": ex.overlap_grads}, os.path.join(out_dir, f"rank{rank}.pt"))
+                "early": getattr(ex, "early_steps", 0), "split": getattr(ex, "overlap_grads", False),
+                "comm": getattr(ex, "comm_mode", None), "violations": relay.violations()},
+               os.path.join(out_dir, f"rank{rank}.pt"))
     fmdist.shutdown()
 
 
-@pytest.mark.parametrize("world,variant", [
-    (2, dict()), (2, dict(prefetch_rows="off")), (4, dict()), (3, dict(dtype="bf16")), (2, dict(dtype="fp8")),
-    (3, dict(overlap_grads="off")), (2, dict(overlap_grads="off", env={"FM_SELF_ROWS": "0"})),
-    (3, dict(dtype="bf16", env={"FM_SELF_ROWS": "0"}))])
-def test_ranks_on_one_gpu_equal_one_process(tmp_path, world, variant):
-    """Self rows (the default) at world 2-4: each rank reads its own rows from its table and
-    updates the ones no other rank requested in place; FM_SELF_ROWS=0 exchanges them too."""
+def _reference(world, dtype):
     from fast_tffm_amd.data.batch import Batch
     from fast_tffm_amd.models.fm import FactorizationMachine
 
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), variant), nprocs=world, join=True)
-    res = [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(world)]
-    if "prefetch_rows" not in variant:  # default at world > 1: early row exchange on
-        assert all(r["early"] == STEPS - 1 for r in res)
-    assert all(r["split"] == (variant.get("overlap_grads", "auto") != "off") for r in res)  # (split: default on)
-    ref = FactorizationMachine(_cfg("local", B * world, dtype=variant.get("dtype", "fp32")), device="cuda")
+    ref = FactorizationMachine(_cfg("local", B * world, dtype=dtype), device="cuda")
     for s in range(STEPS):
         parts = [_batch(s, r) for r in range(world)]
         offs = torch.cat([parts[0].offsets] + [p.offsets[1:] + parts[0].nnz * i  # (every part: B x 39 features)
@@ -129,7 +85,33 @@ def test_ranks_on_one_gpu_equal_one_process(tmp_path, world, variant):
         ref.train_step(Batch(torch.cat([p.labels for p in parts]), offs, torch.cat([p.ids for p in parts]), None, None,
                              sum(p.nnz for p in parts)))
     torch.cuda.synchronize()
-    want = ref.table.reference_rows().cpu()
+    return ref.table.reference_rows().cpu()
+
+
+def _run(tmp_path, world, variant, mode="shard"):
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), variant, mode), nprocs=world, join=True)
+    res = [torch.load(os.path.join(tmp_path, f"rank{r}.pt"), weights_only=True) for r in range(world)]
+    assert all(r["violations"] == 0 for r in res), [r["violations"] for r in res]
+    return res
+
+
+@pytest.mark.parametrize("world,variant", [
+    (2, dict()), (2, dict(prefetch_rows="off")), (4, dict()), (3, dict(dtype="bf16")), (2, dict(dtype="fp8")),
+    (3, dict(overlap_grads="off")), (2, dict(overlap_grads="off", env={"FM_SELF_ROWS": "0"})),
+    (3, dict(dtype="bf16", env={"FM_SELF_ROWS": "0"})),
+    (8, dict()), (8, dict(env={"FM_SINGLE_COMM": "1"})), (8, dict(dtype="bf16", overlap_grads="off"))])
+def test_ranks_on_one_gpu_equal_one_process(tmp_path, world, variant):
+    """Self rows (the default) at world 2-8: each rank reads its own rows from its table and
+    updates the ones no other rank requested in place; FM_SELF_ROWS=0 exchanges them too.
+    World 8 (the node size of the scaling runs): 8 owners in the split-backward piece walk, the
+    segment lookup and the dirty scan, with the dual (default) and the single communicator."""
+    res = _run(tmp_path, world, variant)
+    if "prefetch_rows" not in variant:  # default at world > 1: early row exchange on
+        assert all(r["early"] == STEPS - 1 for r in res)
+    assert all(r["split"] == (variant.get("overlap_grads", "auto") != "off") for r in res)  # (split: default on)
+    single = variant.get("env", {}).get("FM_SINGLE_COMM") == "1"
+    assert all(r["comm"] == ("single" if single else "dual") for r in res)
+    want = _reference(world, variant.get("dtype", "fp32"))
     got = torch.zeros_like(want)
     for r in res:
         g = r["gids"]
@@ -137,3 +119,16 @@ def test_ranks_on_one_gpu_equal_one_process(tmp_path, world, variant):
         got[g[ok]] = r["rows"][ok]
     tol = dict(rtol=1e-5, atol=1e-6) if variant.get("dtype", "fp32") == "fp32" else dict(rtol=2e-2, atol=2e-3)
     torch.testing.assert_close(got, want, **tol)
+
+
+@pytest.mark.parametrize("world,mode", [(2, "dp_dense"), (4, "dp_dense"), (8, "dp_dense"), (2, "dp")])
+def test_replicated_modes_on_one_gpu_equal_one_process(tmp_path, world, mode):
+    """The replicated-table executors at world > 1 on the GPU: dp_dense (in-place reduce-scatter of
+    the [vocab, Kp + 4] gradient buffer, sharded apply of the own slice, zeroing of the listed
+    rows, in-place all-gather of the replica) and dp (sparse all-gather); every replica equals
+    one process on the concatenated batches."""
+    res = _run(tmp_path, world, dict(), mode)
+    want = _reference(world, "fp32")
+    for r in res:
+        torch.testing.assert_close(r["rows"], want, rtol=1e-5, atol=1e-6)
+    assert all(torch.equal(r["rows"], res[0]["rows"]) for r in res)

@@ -25,7 +25,7 @@ from fast_tffm_amd.ops import kernels as K  # noqa: E402
 
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--algo", default="onesweep,bucket")
+    ap.add_argument("--algo", default="onesweep,hd", help="onesweep | bucket | hd (hot-dictionary dedup)")
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--pool", type=int, default=4)
     ap.add_argument("--vocab", type=int, default=125_000_000)
@@ -48,13 +48,22 @@ def main() -> int:
         filt.append((ids[keep].contiguous(), codes[keep].contiguous(), sb, b.offsets))
     cases["full"], cases["no_hot256"] = full, filt
     for algo in a.algo.split(","):
-        os.environ["FM_DEDUP_SORT"] = algo
+        os.environ["FM_DEDUP_SORT"] = "bucket" if algo == "bucket" else "onesweep"
+        os.environ["FM_DEDUP"] = "hd" if algo == "hd" else "onesweep"
         for name, pool in cases.items():
             ws = K.DedupWorkspace(max(p[0].numel() for p in pool), dev, 32)
+            hd = None
+            if algo == "hd":  # dictionary from a batch outside the timed pool, frozen
+                hd = K.HotDict(dev, refresh=1)
+                b0 = gen.batch(131072)
+                K.dedup(b0.ids.to(torch.int32), ws=ws, key_bits=kb,
+                        ex_of_occ=K.csr_rows(b0.offsets, nnz=b0.nnz, slot_bits=pool[0][2]), hot_dict=hd)
+                hd.refresh = 10 ** 9
 
             def run(i):
                 ids, codes, sb, off = pool[i % len(pool)]
-                K.dedup(ids, ws=ws, key_bits=kb, ex_of_occ=codes, ex_shift=sb, offsets=off)
+                K.dedup(ids, ws=ws, key_bits=kb, ex_of_occ=codes, ex_shift=sb, offsets=off, hot_dict=hd,
+                        want_skeys=False)
 
             for i in range(3):
                 run(i)

@@ -94,6 +94,10 @@ def main() -> int:
     ap.add_argument("--ranks", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--link-gbs", type=float, default=64.0, help="unidirectional GB/s per xGMI link (effective)")
     ap.add_argument("--step-ms", type=float, default=0.67, help="measured 1-GPU step (compute) time")
+    ap.add_argument("--dp-fwd-ms", type=float, default=0.20, help="dp_dense forward at world 1")
+    ap.add_argument("--dp-bwd-ms", type=float, default=0.45, help="dp_dense backward (EMIT_TABLE) at world 1")
+    ap.add_argument("--dp-apply-ms", type=float, default=0.10, help="dp_dense dense_apply of all V rows at world 1")
+    ap.add_argument("--dp-blocks", type=int, default=4, help="dp_dense pipeline blocks (FM_DP_BLOCKS)")
     a = ap.parse_args()
     mb = 1e6
     print(f"row-sharded k=64 fp32 wire, B={a.batch}/rank, {a.slots / 1e6:.0f}M slots/rank; "
@@ -112,13 +116,26 @@ def main() -> int:
               f"{d['critical'] / mb:>8.1f} {t_crit:>9.3f} {pred:>8.3f} {a.step_ms / pred:>8.2f}")
     print()
     print("dp_dense k=64 (V = 1M replicated, fp32 gradient buffer): reduce-scatter + sharded apply + all-gather")
-    print(f"{'N':>2} {'RS MB':>8} {'AG MB':>8} {'total MB':>9} {'allreduce MB':>12} {'t ring ms':>9}")
+    print(f"  compute at world 1: forward {a.dp_fwd_ms:.3f} ms, backward {a.dp_bwd_ms:.3f} ms, "
+          f"apply {a.dp_apply_ms:.3f} ms; P = {a.dp_blocks} row blocks")
+    print("  serial:    fwd + bwd + RS + apply + AG")
+    print("  pipelined: fwd + max(bwd, bwd/P + RS) + apply/P + AG   (RS(p) beside backward piece p+1, apply(p) beside")
+    print("             RS(p+1), AG(p) beside apply(p+1); the forward reads every block's updated rows, so the")
+    print("             all-gather cannot run beside the next step in a synchronous step)")
+    print(f"{'N':>2} {'RS MB':>8} {'AG MB':>8} {'total MB':>9} {'allreduce MB':>12} {'t ring ms':>9} {'serial ms':>9} "
+          f"{'pipe ms':>8} {'max+10% ms':>10}")
     for N in a.ranks:
         d = dp_dense_model(N)
         # RCCL runs its rings over every peer link of the fully connected mesh (N - 1 links)
-        t = d["total"] / (max(N - 1, 1) * a.link_gbs * 1e9) * 1e3
+        bw = max(N - 1, 1) * a.link_gbs * 1e9
+        t = d["total"] / bw * 1e3
+        rs, ag = d["reduce_scatter"] / bw * 1e3, d["all_gather"] / bw * 1e3
+        comp = a.dp_fwd_ms + a.dp_bwd_ms + a.dp_apply_ms / max(N, 1)
+        serial = comp + rs + ag
+        P = a.dp_blocks if N > 1 else 1
+        pipe = (a.dp_fwd_ms + max(a.dp_bwd_ms, a.dp_bwd_ms / P + rs) + a.dp_apply_ms / max(N, 1) / P + ag)
         print(f"{N:>2} {d['reduce_scatter'] / mb:>8.1f} {d['all_gather'] / mb:>8.1f} {d['total'] / mb:>9.1f} "
-              f"{d['allreduce_equiv'] / mb:>12.1f} {t:>9.3f}")
+              f"{d['allreduce_equiv'] / mb:>12.1f} {t:>9.3f} {serial:>9.3f} {pipe:>8.3f} {1.1 * max(comp, t):>10.3f}")
     return 0
 
 
