@@ -33,8 +33,7 @@ constexpr int kRleTile = kBlock * kRleItems;     // 2048 elements per tile
 constexpr int kMaxTiles = 1 << 20;               // tile-count words per call (n < 2^31)
 
 struct RleArgs {
-  int n, CH, ntiles;              // n: occurrences (the capacity when n_dev is set), ntiles over n
-  const int* n_dev;               // device occurrence count (nullable; <= n)
+  int n, CH, ntiles;              // n: occurrences, ntiles over n
   int dense_min;                  // rows with >= dense_min occurrences are "dense" (0: none)
   int* dense_list;                // [kMaxDense] segment ids of the first dense rows in key order
   const uint32_t* skeys;          // sorted keys
@@ -137,14 +136,7 @@ __device__ inline void block_excl_scan(const unsigned (&v)[NC], unsigned (&ex)[N
 
 // Per tile: head and chunk-start counts.  Block 0 also zeroes what the emit pass appends to
 // (dense heads) and the counts no later kernel of the chain writes (no memset launches).
-// The count read on the device (bucket path: the hot-row filter's kept total) caps n.
-__device__ inline RleArgs rle_resolve(RleArgs a) {
-  if (a.n_dev) a.n = min(*a.n_dev, a.n);
-  return a;
-}
-
-__global__ __launch_bounds__(kBlock) void rle_count_kernel(RleArgs a0) {
-  const RleArgs a = rle_resolve(a0);
+__global__ __launch_bounds__(kBlock) void rle_count_kernel(RleArgs a) {
   const int tile = blockIdx.x;
   Rle8 r;
   rle_flags8(a, tile * kRleTile + threadIdx.x * kRleItems, r);
@@ -165,9 +157,8 @@ __global__ __launch_bounds__(kBlock) void rle_count_kernel(RleArgs a0) {
   }
 }
 
-__global__ __launch_bounds__(kBlock) void rle_emit_kernel(RleArgs a0) {
+__global__ __launch_bounds__(kBlock) void rle_emit_kernel(RleArgs a) {
   __shared__ unsigned s_pre[2];
-  const RleArgs a = rle_resolve(a0);
   const int tile = blockIdx.x;
   const int last = a.n > 0 ? (a.n - 1) / kRleTile : 0;  // the last tile holding elements writes the totals
   if (tile > last) return;
@@ -268,8 +259,7 @@ __global__ __launch_bounds__(kBlock) void rle_emit_kernel(RleArgs a0) {
 // order, deterministic whatever order the tiles appended them in.  One workgroup: the cut value is
 // found by a bitwise binary search on counts, the kept ids (<= kMaxDense, distinct) ranked by
 // counting.
-__global__ __launch_bounds__(kBlock) void dense_select_kernel(RleArgs a0) {
-  const RleArgs a = rle_resolve(a0);
+__global__ __launch_bounds__(kBlock) void dense_select_kernel(RleArgs a) {
   __shared__ int keep[kMaxDense];
   __shared__ int red[kWavesPerBlock];
   __shared__ int s_cut;
@@ -372,16 +362,17 @@ static size_t sort_temp_bytes(int n, hipStream_t st) {
 constexpr int kDenseMinFloor = 32;
 static size_t dense_cap_for(int n) { return (size_t)n / kDenseMinFloor + 1; }
 
-// Workspace layout: [sort workspace (the larger of onesweep temp / bucket path) | dense_cnt (8 B),
-// tile_cnt[ntiles] | dense_tmp]
+// Workspace layout: [onesweep temp | dense_cnt (8 B), tile_cnt[ntiles] | dense_tmp]
 static size_t lb_bytes(int ntiles) { return 8 + 8 * (size_t)ntiles; }
 
-enum DedupSort : int { kSortBucket = 0, kSortOnesweep = 1 };
+size_t dedup_workspace_bytes(int n) {
+  if (n <= 0) return 256;
+  const size_t ntiles = ((size_t)n + kRleTile - 1) / kRleTile;
+  return sort_temp_bytes(n, 0) + align_up(lb_bytes((int)ntiles)) + align_up(dense_cap_for(n) * sizeof(int)) + 256;
+}
 
 struct DedupArgs {
-  int n;                   // occurrences (the capacity when n_dev is set)
-  const int* n_dev;        // device occurrence count (nullable; bucket sort only)
-  int algo;                // DedupSort
+  int n;                   // occurrences
   int end_bit;             // number of key bits to sort on
   int CH;                  // chunk length of the backward plan
   const uint32_t* keys;    // [n]
@@ -408,240 +399,6 @@ struct DedupArgs {
   void* ws;
   size_t ws_bytes;
 };
-
-// ---------------------------------------------------------------------------
-// Bucket sort: the default GPU dedup sort.  The same stable order as the LSD radix sort of
-// (key, payload) pairs over end_bit key bits, in three steps instead of three full passes:
-//   1. part_hist_kernel: per tile of kPartTile elements, an LDS histogram of the top bb key bits
-//      (the bucket), written bucket-major: hist[bucket * ntiles + tile];
-//   2. an exclusive scan of hist (rocPRIM): off[bucket * ntiles + tile] = where that tile's
-//      elements of that bucket start in the partitioned arrays; off[bucket * ntiles] is the
-//      bucket's start;
-//   3. part_scatter_kernel: per tile, a stable rank by bucket (rocPRIM block_radix_rank, match:
-//      one ballot per digit bit, per-wave counters), an LDS exchange into bucket order and
-//      contiguous stores of each bucket's run at its offset -- a stable MSD partition;
-//   4. bucket_sort_kernel<T, IPT>: one workgroup per bucket sorts the bucket's low end_bit - bb
-//      bits in registers / LDS (rocPRIM block_radix_sort, stable) and writes the final arrays.
-//      Three size classes (<= 2048, <= 4096, <= 16384 elements); larger buckets (a very hot
-//      row whose occurrences were not filtered out) go to rocPRIM's segmented radix sort, which
-//      gets empty segments for every other bucket.
-// Every size is read on the device (n_dev: the hot-row filter's kept count), so the plan needs
-// no host sync.  Buckets are sized from the capacity (~2k elements each at full occupancy).
-// ---------------------------------------------------------------------------
-constexpr int kPartThreads = 256;
-constexpr int kPartItems = 32;
-constexpr int kPartTile = kPartThreads * kPartItems;  // 8192 elements
-constexpr int kPartMaxBits = 11;                       // <= 2048 buckets
-constexpr int kBucketCap = 16384;                      // largest in-LDS bucket
-
-struct BsortArgs {
-  int n_cap;              // capacity: grid sizes
-  const int* n_dev;       // device element count (nullable: n_cap)
-  int kb, bb;             // key bits sorted on, bucket bits (the top bb of them)
-  int ntiles;             // tiles of kPartTile over n_cap
-  const uint32_t* keys;   // [n]
-  const int* pay;         // [n]
-  const int* off;         // [NB * ntiles] scanned hist
-  uint32_t* pk;           // [n] partitioned keys
-  int* pv;                // [n] partitioned payload
-  uint32_t* skeys;        // [n] sorted keys
-  int* spay;              // [n] sorted payload
-  int* seg_b;             // [NB] oversize buckets' ranges for the segmented sort (else empty)
-  int* seg_e;
-};
-
-__device__ inline int bs_count(const BsortArgs& a) { return a.n_dev ? min(*a.n_dev, a.n_cap) : a.n_cap; }
-
-__device__ inline int bucket_of(const BsortArgs& a, uint32_t key) {
-  return (int)min(key >> (a.kb - a.bb), (1u << a.bb) - 1u);
-}
-
-__global__ __launch_bounds__(kPartThreads) void part_hist_kernel(BsortArgs a, int* hist) {
-  __shared__ int h[1 << kPartMaxBits];
-  const int NB = 1 << a.bb, tile = blockIdx.x;
-  for (int d = threadIdx.x; d < NB; d += kPartThreads) h[d] = 0;
-  __syncthreads();
-  const int n = bs_count(a), base = tile * kPartTile;
-#pragma unroll 8
-  for (int i = 0; i < kPartItems; ++i) {
-    const int j = base + i * kPartThreads + threadIdx.x;
-    if (j < n) atomicAdd(&h[bucket_of(a, a.keys[j])], 1);
-  }
-  __syncthreads();
-  for (int d = threadIdx.x; d < NB; d += kPartThreads) hist[(size_t)d * a.ntiles + tile] = h[d];
-}
-
-__global__ __launch_bounds__(kPartThreads) void part_scatter_kernel(BsortArgs a) {
-  using Rank = rocprim::block_radix_rank<kPartThreads, kPartMaxBits, rocprim::block_radix_rank_algorithm::match>;
-  __shared__ union {
-    typename Rank::storage_type rank;
-    struct {
-      uint32_t k[kPartTile];
-      int v[kPartTile];
-    } x;
-  } s;
-  __shared__ int s_base[1 << kPartMaxBits];
-  const int n = bs_count(a), tile = blockIdx.x, base = tile * kPartTile;
-  if (base >= n) return;
-  const int cnt = min(kPartTile, n - base);
-  // warp-striped arrangement (item i of lane l of wave w = element w * 64 * IPT + i * 64 + l): the
-  // match ranking orders a wave's elements by (item, lane), so this is the input order -> stable
-  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x >> 6;
-  const int w0 = wv * kWave * kPartItems + lane;
-  uint32_t k[kPartItems];
-  int v[kPartItems];
-#pragma unroll
-  for (int i = 0; i < kPartItems; ++i) {
-    const int j = w0 + i * kWave;
-    const bool ok = j < cnt;
-    k[i] = ok ? a.keys[base + j] : 0xffffffffu;  // padding ranks last (top digit, after the real ones)
-    v[i] = ok ? a.pay[base + j] : 0;
-  }
-  unsigned r[kPartItems];
-  const int sh = a.kb - a.bb;
-  Rank().rank_keys(k, r, s.rank, (unsigned)sh, (unsigned)a.bb);
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < kPartItems; ++i) {
-    s.x.k[r[i]] = k[i];
-    s.x.v[r[i]] = v[i];
-  }
-  __syncthreads();
-  // run heads: each bucket's first position p0 in the tile -> s_base = global offset - p0
-  for (int p = threadIdx.x; p < cnt; p += kPartThreads) {
-    const int d = bucket_of(a, s.x.k[p]);
-    if (p == 0 || bucket_of(a, s.x.k[p - 1]) != d) s_base[d] = a.off[(size_t)d * a.ntiles + tile] - p;
-  }
-  __syncthreads();
-  for (int p = threadIdx.x; p < cnt; p += kPartThreads) {
-    const uint32_t key = s.x.k[p];
-    const int q = s_base[bucket_of(a, key)] + p;
-    a.pk[q] = key;
-    a.pv[q] = s.x.v[p];
-  }
-}
-
-__device__ inline void bucket_range(const BsortArgs& a, int d, int n, int& b, int& e) {
-  const int NB = 1 << a.bb;
-  b = a.off[(size_t)d * a.ntiles];
-  e = d + 1 < NB ? a.off[(size_t)(d + 1) * a.ntiles] : n;
-}
-
-// Buckets with lo < size <= T * IPT; the largest class also records the oversize buckets.
-template <int T, int IPT>
-__global__ __launch_bounds__(T) void bucket_sort_kernel(BsortArgs a, int lo, int record_oversize) {
-  using Sort = rocprim::block_radix_sort<uint32_t, T, IPT, int>;
-  __shared__ typename Sort::storage_type st;
-  const int n = bs_count(a), d = blockIdx.x;
-  int b, e;
-  bucket_range(a, d, n, b, e);
-  const int sz = e - b;
-  if (record_oversize && threadIdx.x == 0) {
-    const bool big = sz > T * IPT;
-    a.seg_b[d] = big ? b : 0;
-    a.seg_e[d] = big ? e : 0;
-  }
-  if (sz <= lo || sz > T * IPT) return;
-  uint32_t k[IPT];
-  int v[IPT];
-#pragma unroll
-  for (int i = 0; i < IPT; ++i) {  // blocked arrangement (block_radix_sort's input and output)
-    const int j = threadIdx.x * IPT + i;
-    k[i] = j < sz ? a.pk[b + j] : 0xffffffffu;
-    v[i] = j < sz ? a.pv[b + j] : 0;
-  }
-  Sort().sort(k, v, st, 0, (unsigned)(a.kb - a.bb));  // stable: padding (all-ones) stays behind
-#pragma unroll
-  for (int i = 0; i < IPT; ++i) {
-    const int j = threadIdx.x * IPT + i;
-    if (j < sz) {
-      a.skeys[b + j] = k[i];
-      a.spay[b + j] = v[i];
-    }
-  }
-}
-
-static int bucket_bits(int n_cap, int key_bits) {
-  int bb = 4;
-  while (bb < kPartMaxBits && ((long long)n_cap >> bb) > 2048) ++bb;
-  return std::max(1, std::min(bb, key_bits));
-}
-
-static size_t scan_temp_bytes(int len, hipStream_t st) {
-  size_t b = 0;
-  (void)rocprim::exclusive_scan(nullptr, b, (const int*)nullptr, (int*)nullptr, 0, (size_t)len,
-                                rocprim::plus<int>(), st);
-  return align_up(b);
-}
-
-static size_t segsort_temp_bytes(int n, int NB, hipStream_t st) {
-  size_t b = 0;
-  (void)rocprim::segmented_radix_sort_pairs(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                            (const int*)nullptr, (int*)nullptr, (unsigned)n, (unsigned)NB,
-                                            (const int*)nullptr, (const int*)nullptr, 0, 32, st);
-  return align_up(b);
-}
-
-// Bucket-path workspace: [pk | pv | hist | off | seg_b | seg_e | scan temp | segmented-sort temp]
-struct BsortLayout {
-  int bb, NB, ntiles;
-  size_t pk, pv, hist, off, seg_b, seg_e, scan, seg, total;
-};
-
-static BsortLayout bsort_layout(int n_cap, int key_bits, hipStream_t st) {
-  BsortLayout L;
-  L.bb = bucket_bits(n_cap, key_bits);
-  L.NB = 1 << L.bb;
-  L.ntiles = (n_cap + kPartTile - 1) / kPartTile;
-  const size_t cells = (size_t)L.NB * L.ntiles;
-  size_t o = 0;
-  L.pk = o; o += align_up((size_t)n_cap * 4);
-  L.pv = o; o += align_up((size_t)n_cap * 4);
-  L.hist = o; o += align_up(cells * 4);
-  L.off = o; o += align_up(cells * 4);
-  L.seg_b = o; o += align_up((size_t)L.NB * 4);
-  L.seg_e = o; o += align_up((size_t)L.NB * 4);
-  L.scan = o; o += scan_temp_bytes((int)cells, st);
-  L.seg = o; o += segsort_temp_bytes(n_cap, L.NB, st);
-  L.total = o;
-  return L;
-}
-
-static size_t bsort_bytes(int n_cap) {  // the largest layout over the key widths a caller may pass
-  size_t best = 0;
-  for (int kb : {1, 8, 16, 24, 32}) best = std::max(best, bsort_layout(n_cap, kb, 0).total);
-  return best;
-}
-
-static size_t sort_ws_bytes(int n) { return std::max(sort_temp_bytes(n, 0), bsort_bytes(n)); }
-
-size_t dedup_workspace_bytes(int n) {
-  if (n <= 0) return 256;
-  const size_t ntiles = ((size_t)n + kRleTile - 1) / kRleTile;
-  return sort_ws_bytes(n) + align_up(lb_bytes((int)ntiles)) + align_up(dense_cap_for(n) * sizeof(int)) + 256;
-}
-
-static hipError_t bucket_sort(const DedupArgs& a, char* ws, hipStream_t st) {
-  const int kb = std::max(1, std::min(32, a.end_bit));
-  const BsortLayout L = bsort_layout(a.n, kb, st);
-  BsortArgs b{a.n, a.n_dev, kb, L.bb, L.ntiles, a.keys, a.payload,
-              reinterpret_cast<const int*>(ws + L.off), reinterpret_cast<uint32_t*>(ws + L.pk),
-              reinterpret_cast<int*>(ws + L.pv), a.skeys, a.spay, reinterpret_cast<int*>(ws + L.seg_b),
-              reinterpret_cast<int*>(ws + L.seg_e)};
-  int* hist = reinterpret_cast<int*>(ws + L.hist);
-  hipLaunchKernelGGL(part_hist_kernel, dim3(L.ntiles), dim3(kPartThreads), 0, st, b, hist);
-  size_t sb = L.seg - L.scan;
-  hipError_t e = rocprim::exclusive_scan(ws + L.scan, sb, hist, reinterpret_cast<int*>(ws + L.off), 0,
-                                         (size_t)L.NB * L.ntiles, rocprim::plus<int>(), st);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(part_scatter_kernel, dim3(L.ntiles), dim3(kPartThreads), 0, st, b);
-  hipLaunchKernelGGL((bucket_sort_kernel<256, 8>), dim3(L.NB), dim3(256), 0, st, b, 0, 0);
-  hipLaunchKernelGGL((bucket_sort_kernel<256, 16>), dim3(L.NB), dim3(256), 0, st, b, 2048, 0);
-  hipLaunchKernelGGL((bucket_sort_kernel<1024, 16>), dim3(L.NB), dim3(1024), 0, st, b, 4096, 1);
-  size_t gb = L.total - L.seg;
-  return rocprim::segmented_radix_sort_pairs(ws + L.seg, gb, b.pk, a.skeys, b.pv, a.spay, (unsigned)a.n,
-                                             (unsigned)L.NB, b.seg_b, b.seg_e, 0, kb - L.bb, st);
-}
 
 // ---------------------------------------------------------------------------
 // Segment index (key -> segment id without an inverse map).  The row-sharded forward reads
@@ -687,23 +444,17 @@ int launch_dedup(const DedupArgs& a, hipStream_t st) {
   }
   const int ntiles = (a.n + kRleTile - 1) / kRleTile;
   if (ntiles > kMaxTiles) return -3;
-  if (a.n_dev && a.algo != kSortBucket) return -9;  // the onesweep sort needs the count on the host
-  const size_t tmp = sort_ws_bytes(a.n);
+  const size_t tmp = sort_temp_bytes(a.n, st);
   char* base = static_cast<char*>(a.ws);
   char* lb = base + tmp;
   int* dense_tmp = reinterpret_cast<int*>(lb + align_up(lb_bytes(ntiles)));
   if (tmp + align_up(lb_bytes(ntiles)) + align_up(dense_cap_for(a.n) * sizeof(int)) > a.ws_bytes) return -2;
   if (a.dense_list && a.dense_min > 0 && a.dense_min < kDenseMinFloor) return -8;
 
-  hipError_t e;
-  if (a.algo == kSortBucket) {
-    e = bucket_sort(a, base, st);
-  } else {
-    size_t sort_bytes = tmp;
-    e = sort_pairs(a.ws, sort_bytes, a.keys, a.skeys, a.payload, a.spay, a.n, a.end_bit, st);
-  }
+  size_t sort_bytes = tmp;
+  const hipError_t e = sort_pairs(a.ws, sort_bytes, a.keys, a.skeys, a.payload, a.spay, a.n, a.end_bit, st);
   if (e != hipSuccess) return (int)e;
-  RleArgs r{a.n, a.CH, ntiles, a.n_dev, a.dense_list ? a.dense_min : 0, a.dense_list, a.skeys, a.spay, a.ex_shift,
+  RleArgs r{a.n, a.CH, ntiles, a.dense_list ? a.dense_min : 0, a.dense_list, a.skeys, a.spay, a.ex_shift,
             a.offsets, reinterpret_cast<unsigned long long*>(lb + 8), dense_tmp, reinterpret_cast<int*>(lb),
             (int)dense_cap_for(a.n), a.uniq, a.seg_start,
             a.seg_chunk, a.chunk_start, a.chunk_seg, a.chunk_key, a.counts, a.inv, a.ex_of_occ, a.sorted_ex,

@@ -82,8 +82,6 @@ struct BwdArgs {
   int* multi;               // [counts[2]] rows spanning more than one chunk (filled by the chunk kernel)
   int* counts_rw;           // == counts, writable (counts[2] = #multi, zeroed by the launcher)
   const int* dense_list;    // [kMaxDense] dense rows (dedup), counts[3] of them; null: no dense path
-  const int* dense_n;       // device scalar: number of dense rows (null: counts[3])
-  const int* hot_keys;      // hot rows (hot.hip): dense_list holds table rows, not segments; null: segments
   float* dense_part;        // [gridDim(dense) * kMaxDense, Kp + 4] per-workgroup partial rows
   int nex;                  // examples in the batch (dense path)
   const uint8_t* dense_A;   // [nex, kMaxDense] occurrence counts of the dense rows (written by the forward)
@@ -567,7 +565,7 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_dense_kernel(BwdArgs a) {
   constexpr int NC = NB * 16;
   __shared__ __align__(16) uint8_t At[kDenseE * kDenseAP];   // A rows of the tile
   __shared__ __align__(16) float Dt[kDenseE * NC];           // D rows of the tile
-  const int nd = min(a.dense_n ? *a.dense_n : a.counts[3], kMaxDense);
+  const int nd = min(a.counts[3], kMaxDense);
   if (nd == 0) return;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid >> 6;
   const int per = ((a.nex + (int)gridDim.x - 1) / (int)gridDim.x + kDenseE - 1) / kDenseE * kDenseE;
@@ -660,7 +658,7 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_dense_apply_kernel(BwdArgs a) {
   constexpr int EPL = Frag<TV>::N;
   __shared__ float4 red[kWavesPerBlock][kWave];
   __shared__ float row[kWave * 4];
-  const int nd = min(a.dense_n ? *a.dense_n : a.counts[3], kMaxDense);
+  const int nd = min(a.counts[3], kMaxDense);
   const int h = blockIdx.x;
   if (h >= nd) return;
   const int tid = threadIdx.x, q = tid & (kWave - 1), stripe = tid >> 6;
@@ -692,15 +690,8 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_dense_apply_kernel(BwdArgs a) {
     float A[EPL];
 #pragma unroll
     for (int k = 0; k < EPL; ++k) A[k] = row[tE * EPL + k];
-    if (a.hot_keys) {  // hot row (local step): table row key, occurrences from the GEMM's count column
-      RowState<EPL> r;
-      bwd_load<TV, EPL>(a, 0, (long long)a.hot_keys[h], tE, r);
-      bwd_finish<LPR, TV, EPL>(a, 0, t, tact, r, A, row[a.Kp], row[a.Kp + 1], (int)(row[a.Kp + 2] + 0.5f), sr);
-    } else {
-      const int u = a.dense_list[h];
-      bwd_finalize<LPR, TV, EPL>(a, u, t, tact, tE, A, row[a.Kp], row[a.Kp + 1], a.seg_start[u + 1] - a.seg_start[u],
-                                 sr);
-    }
+    const int u = a.dense_list[h];
+    bwd_finalize<LPR, TV, EPL>(a, u, t, tact, tE, A, row[a.Kp], row[a.Kp + 1], a.seg_start[u + 1] - a.seg_start[u], sr);
   }
 }
 

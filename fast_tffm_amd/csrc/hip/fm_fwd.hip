@@ -99,7 +99,14 @@ constexpr int fwd_min_waves() {
   return LPR >= 32 ? 4 : 1;
 }
 
-template <int LPR, typename TV>
+// LDS of the dense-row counting (FM_DENSE_BWD): only the dense instantiation carries it
+template <bool DENSE> struct DenseLds {
+  int hkey[kDenseHash], hval[kDenseHash];
+  unsigned dcnt[kWavesPerBlock][kMaxDense];
+};
+template <> struct DenseLds<false> {};
+
+template <int LPR, typename TV, bool DENSE>
 __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
   using F = Frag<TV>;
   constexpr int EPL = F::N;
@@ -118,26 +125,25 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
   const int nwaves = gridDim.x * kWavesPerBlock;
   const bool want_reg = a.reg_partial != nullptr;
   // (segment lookup + self rows: the key range of the own segments, read once)
-  const bool self_key = self_on && a.seg_idx != nullptr && a.dense_A == nullptr;
+  const bool self_key = self_on && a.seg_idx != nullptr && !DENSE;
   const int self_kmin = self_key ? a.self.keys[a.self.u0] : 0;
   const int self_kmax = self_key ? a.self.keys[a.self.u1 - 1] : -1;
 
-  // dense rows: key -> dense index hash (built once per workgroup) and per-wave counters
-  __shared__ int hkey[kDenseHash], hval[kDenseHash];
-  __shared__ unsigned dcnt[kWavesPerBlock][kMaxDense];
-  const bool dense = a.dense_A != nullptr;
+  // dense rows (the dense instantiation only): key -> dense index hash (built once per
+  // workgroup) and per-wave counters
+  __shared__ DenseLds<DENSE> dl;
   const int wv = threadIdx.x >> 6;
-  if (dense) {
+  if constexpr (DENSE) {
     const int nd = min(*a.dense_count, kMaxDense);
-    for (int k = threadIdx.x; k < kDenseHash; k += kBlock) hkey[k] = -1;
-    for (int k = threadIdx.x; k < kWavesPerBlock * kMaxDense; k += kBlock) (&dcnt[0][0])[k] = 0u;
+    for (int k = threadIdx.x; k < kDenseHash; k += kBlock) dl.hkey[k] = -1;
+    for (int k = threadIdx.x; k < kWavesPerBlock * kMaxDense; k += kBlock) (&dl.dcnt[0][0])[k] = 0u;
     __syncthreads();
     for (int h = threadIdx.x; h < nd; h += kBlock) {
       const int sg = a.dense_list[h];
       const int key = a.dense_uniq ? a.dense_uniq[sg] : sg;
       int slot = dense_hash(key);
-      while (atomicCAS(&hkey[slot], -1, key) != -1) slot = (slot + 1) & (kDenseHash - 1);
-      hval[slot] = h;  // (keys are distinct; read only after the barrier)
+      while (atomicCAS(&dl.hkey[slot], -1, key) != -1) slot = (slot + 1) & (kDenseHash - 1);
+      dl.hval[slot] = h;  // (keys are distinct; read only after the barrier)
     }
     __syncthreads();
   }
@@ -225,9 +231,11 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
           my_s = row_scale<TV>(a.w, my_row, a.w_stride);
         }
       }
-      if (dense && lane < m) {
-        const int h = dense_probe(hkey, hval, my_seg);
-        if (h >= 0) atomicAdd(&dcnt[wv][h], 1u);  // integer: order-independent
+      if constexpr (DENSE) {
+        if (lane < m) {
+          const int h = dense_probe(dl.hkey, dl.hval, my_seg);
+          if (h >= 0) atomicAdd(&dl.dcnt[wv][h], 1u);  // integer: order-independent
+        }
       }
       for (int q = 0; q < m; q += G * UNR) {
         float fr[UNR][EPL], fx[UNR], fs[UNR];
@@ -272,14 +280,14 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
       lin += my_x * my_w;
       if (want_reg) rw += my_w * my_w;
     }
-    if (dense) {  // flush this example's dense-row counts: 4 per lane, one coalesced row
+    if constexpr (DENSE) {  // flush this example's dense-row counts: 4 per lane, one coalesced row
       // (LDS instructions of one wave complete in issue order, and the compiler keeps these
       // reads after the possibly-aliasing atomics above)
       uint32_t packed = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        unsigned c = dcnt[wv][4 * lane + j];
-        dcnt[wv][4 * lane + j] = 0u;
+        unsigned c = dl.dcnt[wv][4 * lane + j];
+        dl.dcnt[wv][4 * lane + j] = 0u;
         packed |= (c > 255u ? 255u : c) << (8 * j);
       }
       reinterpret_cast<uint32_t*>(a.dense_A + (long long)i * kMaxDense)[lane] = packed;
@@ -345,7 +353,16 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
 template <int LPR, typename TV>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(fwd_min_waves<LPR, TV>())))
 void fm_fwd_kernel(FwdArgs a) {
-  fwd_body<LPR, TV>(a);
+  fwd_body<LPR, TV, false>(a);
+}
+
+// The forward that also counts every example's dense-row occurrences (FM_DENSE_BWD's MFMA
+// backward; fp32 r1, Kp <= 128): a separate instantiation keeps the counting's LDS and branches
+// out of the default kernel.
+template <int LPR, typename TV>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(fwd_min_waves<LPR, TV>())))
+void fm_fwd_dense_kernel(FwdArgs a) {
+  fwd_body<LPR, TV, true>(a);
 }
 
 // Expand CSR offsets into the example index of every occurrence.
@@ -391,6 +408,26 @@ int fwd_grid(int B) { return fill_grid(B, kWavesPerBlock, 4096); }
 int launch_fwd(const FwdArgs& a, int dtype, int grid, hipStream_t st) {
   if (a.B <= 0) return 0;
   const int lpr = lanes_per_row(a.Kp, dtype);
+  if (a.dense_A) {
+    if (dtype == kFP8 || lpr > 32) return -5;
+#define FM_FWD_DENSE(TV)                                                                                  \
+  switch (lpr) {                                                                                          \
+    case 1: hipLaunchKernelGGL((fm_fwd_dense_kernel<1, TV>), dim3(grid), dim3(kBlock), 0, st, a); break;   \
+    case 2: hipLaunchKernelGGL((fm_fwd_dense_kernel<2, TV>), dim3(grid), dim3(kBlock), 0, st, a); break;   \
+    case 4: hipLaunchKernelGGL((fm_fwd_dense_kernel<4, TV>), dim3(grid), dim3(kBlock), 0, st, a); break;   \
+    case 8: hipLaunchKernelGGL((fm_fwd_dense_kernel<8, TV>), dim3(grid), dim3(kBlock), 0, st, a); break;   \
+    case 16: hipLaunchKernelGGL((fm_fwd_dense_kernel<16, TV>), dim3(grid), dim3(kBlock), 0, st, a); break; \
+    case 32: hipLaunchKernelGGL((fm_fwd_dense_kernel<32, TV>), dim3(grid), dim3(kBlock), 0, st, a); break; \
+    default: return -5;                                                                                   \
+  }
+    if (dtype == kBF16) {
+      FM_FWD_DENSE(__hip_bfloat16)
+    } else {
+      FM_FWD_DENSE(float)
+    }
+#undef FM_FWD_DENSE
+    return (int)hipGetLastError();
+  }
   FM_DISPATCH(dtype, lpr, fm_fwd_kernel, grid, st, a);
   return (int)hipGetLastError();
 }

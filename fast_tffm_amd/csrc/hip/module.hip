@@ -23,7 +23,6 @@ using u64 = std::uintptr_t;
 // Unity build: all kernel sources are compiled in this translation unit.
 #include "fm_bwd.hip"
 #include "fm_fwd.hip"
-#include "hot.hip"
 #include "dedup.hip"
 #include "hdedup.hip"
 #include "shard.hip"
@@ -145,12 +144,9 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
          u64 dense_part, int nex, u64 dense_stream, int dtype,
          long long max_chunks, long long max_unique, u64 stream, int g_wcol, int g_bf16, u64 sr_counter,
          int counters_ready, u64 seg_bounds, int piece, int n_owners, u64 dense_A,
-         const std::vector<long long>& self, int chunk_grid, u64 dense_n, u64 hot_keys) {
+         const std::vector<long long>& self, int chunk_grid) {
         fm::BwdArgs a{};
         a.chunk_grid = chunk_grid;
-        a.dense_n = P<const int>(dense_n);
-        a.hot_keys = P<const int>(hot_keys);
-        if (hot_keys && (mode != 0 || !dense_n)) throw std::runtime_error("fm_bwd: hot rows are a LOCAL-mode path with a count");
         a.self = self_rows(self);
         if (a.self.u1 > a.self.u0 && a.self.keys != P<const int>(uniq))
           throw std::runtime_error("fm_bwd: self-row keys must be the dedup's unique keys");
@@ -189,31 +185,18 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("max_chunks"), py::arg("max_unique"), py::arg("stream"), py::arg("g_wcol") = -1,
       py::arg("g_bf16") = 0, py::arg("sr_counter") = 0, py::arg("counters_ready") = 0, py::arg("seg_bounds") = 0,
       py::arg("piece") = -1, py::arg("n_owners") = 0, py::arg("dense_A") = 0,
-      py::arg("self_rows") = std::vector<long long>{}, py::arg("chunk_grid") = 0, py::arg("dense_n") = 0,
-      py::arg("hot_keys") = 0);
+      py::arg("self_rows") = std::vector<long long>{}, py::arg("chunk_grid") = 0);
 
   m.def("dedup_workspace_bytes", &fm::dedup_workspace_bytes, py::arg("n"));
-  // hot-row filter of the dedup input (hot.hip): kept (key, code) pairs in CSR order + their count
-  m.def(
-      "hot_filter",
-      [](int B, u64 offsets, u64 ids, u64 hot, u64 hot_n, int slot_bits, u64 gcnt, u64 keys_out, u64 codes_out,
-         u64 n_out, u64 stream) {
-        fm::HotFilterArgs a{B, P<const int>(offsets), P<const int>(ids), P<const int>(hot), P<const int>(hot_n),
-                            slot_bits, P<int>(gcnt), P<int>(keys_out), P<int>(codes_out), P<int>(n_out)};
-        check(fm::launch_hot_filter(a, S(stream)), "hot_filter");
-      },
-      py::arg("B"), py::arg("offsets"), py::arg("ids"), py::arg("hot"), py::arg("hot_n"), py::arg("slot_bits"),
-      py::arg("gcnt"), py::arg("keys_out"), py::arg("codes_out"), py::arg("n_out"), py::arg("stream"));
-
   m.def(
       "dedup",
       [](int n, int end_bit, int CH, u64 keys, u64 payload, u64 skeys, u64 spay, u64 uniq, u64 seg_start,
          u64 seg_chunk, u64 chunk_start, u64 chunk_seg, u64 chunk_key, u64 counts, u64 inv, u64 ex_of_occ,
          u64 sorted_ex, u64 vals, u64 sorted_x, int payload_is_ex, int ex_shift, u64 offsets, int dense_min,
-         u64 dense_list, u64 ws, size_t ws_bytes, u64 stream, u64 n_dev, int algo) {
+         u64 dense_list, u64 ws, size_t ws_bytes, u64 stream) {
         if (CH < 1 || CH > fm::kMaxCH) throw std::invalid_argument("CH must be in [1, MAX_CH]");
         fm::DedupArgs a;
-        a.n = n; a.n_dev = P<const int>(n_dev); a.algo = algo; a.end_bit = end_bit; a.CH = CH; a.keys = P<const uint32_t>(keys);
+        a.n = n; a.end_bit = end_bit; a.CH = CH; a.keys = P<const uint32_t>(keys);
         a.payload = P<const int>(payload); a.skeys = P<uint32_t>(skeys); a.spay = P<int>(spay);
         a.uniq = P<uint32_t>(uniq); a.seg_start = P<int>(seg_start); a.seg_chunk = P<int>(seg_chunk);
         a.chunk_start = P<int>(chunk_start); a.chunk_seg = P<int>(chunk_seg); a.counts = P<int>(counts);
@@ -230,8 +213,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("chunk_seg"), py::arg("chunk_key"), py::arg("counts"), py::arg("inv"), py::arg("ex_of_occ"),
       py::arg("sorted_ex"),
       py::arg("vals"), py::arg("sorted_x"), py::arg("payload_is_ex"), py::arg("ex_shift"), py::arg("offsets"),
-      py::arg("dense_min"), py::arg("dense_list"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"),
-      py::arg("n_dev") = 0, py::arg("algo") = (int)fm::kSortBucket);
+      py::arg("dense_min"), py::arg("dense_list"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"));
   // hot-dictionary dedup (hdedup.hip): the dictionary travels as [keys, n, ht_key, ht_idx, sel, meta]
   m.def("hd_workspace_bytes", &fm::hd_workspace_bytes, py::arg("n"));
   m.attr("HD_MAX_H") = fm::kHdMaxH;
@@ -268,8 +250,6 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
               "hd_dict_refresh");
       },
       py::arg("dict"), py::arg("counts"), py::arg("seg_start"), py::arg("uniq"), py::arg("n_max"), py::arg("stream"));
-  m.attr("DEDUP_BUCKET") = (int)fm::kSortBucket;
-  m.attr("DEDUP_ONESWEEP") = (int)fm::kSortOnesweep;
   m.attr("MAX_DENSE") = fm::kMaxDense;
   m.attr("DENSE_WG") = fm::kDenseWG;
 

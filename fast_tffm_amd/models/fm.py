@@ -132,22 +132,6 @@ class _LocalSlot:
         self.dd: K.DedupWorkspace | None = None
         self.rows32: torch.Tensor | None = None
         self.done = None
-        self.hot: K.HotRows | None = None   # the hot-row set this slot's plan was filtered with
-        self.fcap = 0
-
-    def ensure_hot(self, nnz: int, B: int, dev) -> None:
-        """Buffers of the hot-row filter (hip/hot.hip): kept keys / codes, group counts, kept count."""
-        if self.hot is None:
-            self.hot = K.HotRows.empty(dev)
-            self.fn = torch.zeros(1, dtype=torch.int32, device=dev)
-            self.fn_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
-            self.fn_ev = torch.cuda.Event()
-        if nnz > self.fcap or (B + 63) // 64 > getattr(self, "gcnt", torch.empty(0)).numel():
-            cap = max(nnz, int(1.25 * self.fcap), 1)
-            self.fkeys = torch.empty(cap, dtype=torch.int32, device=dev)
-            self.fcodes = torch.empty(cap, dtype=torch.int32, device=dev)
-            self.gcnt = torch.empty(max(1, (max(B, 1) * 5 // 4 + 63) // 64), dtype=torch.int32, device=dev)
-            self.fcap = cap
 
     def ensure(self, nnz: int, dev, CH: int) -> None:
         if self.dd is None or self.dd.cap < nnz:
@@ -319,13 +303,6 @@ class FactorizationMachine:
         self._lpending2 = None
         self._llast = 2
         self._ring = None
-        # hot rows of the local lookahead step (hip/hot.hip, FM_HOT_ROWS=1): the most frequent rows
-        # of the first planned batch leave the dedup and the occurrence-gather backward for the
-        # dense-row GEMM (binary features, Kp <= 128)
-        self._hot: K.HotRows | None = None
-        self._hot_want = (self.device.type == "cuda" and mode == "local" and self.Kp <= 128
-                          and os.environ.get("FM_HOT_ROWS", "0") == "1")
-        self._hot_refresh = max(0, int(os.environ.get("FM_HOT_REFRESH", "0")))  # steps; 0: pick once
         # hot-row dictionary of the GPU dedup (hip/hdedup.hip): the frequent rows of earlier plans skip
         # the radix sort (FM_DEDUP=onesweep: every occurrence sorted); plans are the same either way
         self._hot_dict = K.HotDict(self.device) if self.device.type == "cuda" and mode == "local" else None
@@ -586,42 +563,18 @@ class FactorizationMachine:
             if t is not None:
                 t.record_stream(st)
         with torch.cuda.stream(st), roctx_range("dedup_next"):
-            rows, dd = self._plan_into(slot, b, hot_ok=True)
+            rows, dd = self._plan_into(slot, b)
             ev = torch.cuda.Event()
             ev.record(st)
         return _LocalPlan(b, idx, rows, dd, ev)
 
-    def _plan_into(self, slot: "_LocalSlot", b: Batch, hot_ok: bool = False):
-        """csr_rows + dedup of ``b`` into ``slot`` on the current stream; returns (rows, DedupOut).
-
-        ``hot_ok`` (lookahead plans): with a hot-row set, the dedup input is the batch without the
-        hot rows' occurrences (``K.hot_filter``); the DedupOut then carries the set it was filtered
-        with as ``dd.hot`` (the forward counts those rows, the backward reduces them as a GEMM).
-        The bucket sort reads the kept count on the device; the onesweep sort (FM_DEDUP_SORT)
-        needs it on the host: one wait for the filter on this (side) stream."""
+    def _plan_into(self, slot: "_LocalSlot", b: Batch):
+        """csr_rows + dedup of ``b`` into ``slot`` on the current stream; returns (rows, DedupOut)."""
         cfg = self.cfg
         slot.ensure(b.nnz, self.device, cfg.dedup_chunk)
         rows = b.ids if b.ids.dtype == torch.int32 else slot.rows32[: b.nnz].copy_(b.ids)
         sb = self._slot_bits(b)
         kb = bits_for(self.table.rows)
-        if hot_ok and self._hot is not None and self._hot.n_host > 0 and b.vals is None:
-            slot.ensure_hot(b.nnz, b.B, self.device)
-            slot.hot.copy_from(self._hot)
-            K.hot_filter(b.offsets, rows, slot.hot, slot_bits=sb, gcnt=slot.gcnt, keys_out=slot.fkeys,
-                         codes_out=slot.fcodes, n_out=slot.fn)
-            if K.dedup_sort_algo() == K.native.hip().DEDUP_BUCKET:  # kept count read on the device
-                dd = K.dedup(slot.fkeys[: b.nnz], ws=slot.dd, key_bits=kb, ex_of_occ=slot.fcodes[: b.nnz],
-                             vals=None, num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets,
-                             dense_min=0, n_dev=slot.fn)
-            else:  # the onesweep sort needs it on the host: one wait for the filter on this stream
-                slot.fn_host.copy_(slot.fn, non_blocking=True)
-                slot.fn_ev.record()
-                slot.fn_ev.synchronize()
-                n = int(slot.fn_host[0])
-                dd = K.dedup(slot.fkeys[:n], ws=slot.dd, key_bits=kb, ex_of_occ=slot.fcodes[:n], vals=None,
-                             num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets, dense_min=0)
-            dd.hot = slot.hot
-            return rows, dd
         ex = K.csr_rows(b.offsets, out=slot.dd.ex_of_occ[: b.nnz], nnz=b.nnz, slot_bits=sb)
         dd = K.dedup(rows, ws=slot.dd, key_bits=kb, ex_of_occ=ex, vals=b.vals,
                      num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets,
@@ -631,41 +584,22 @@ class FactorizationMachine:
                      hot_dict=self._hot_dict, want_skeys=False)
         return rows, dd
 
-    def _hot_from_plan(self, dd) -> None:
-        """The hot-row set from an unfiltered plan: its MAX_DENSE most frequent rows (ties by key)
-        with at least two chunks' worth of occurrences (host-side selection: once)."""
-        import numpy as np
-
-        torch.cuda.synchronize(self.device)
-        U = int(dd.counts[0].item())
-        hot = K.HotRows.empty(self.device)
-        if U > 0:
-            seg = dd.seg_start[: U + 1].cpu().numpy().astype(np.int64)
-            keys = dd.uniq[:U].cpu().numpy().astype(np.int64)
-            cnt = np.diff(seg)
-            order = np.lexsort((keys, -cnt))[: K.MAX_DENSE]
-            sel = order[cnt[order] >= 2 * self.cfg.dedup_chunk]
-            hot.set(torch.from_numpy(keys[sel]))
-        torch.cuda.synchronize(self.device)
-        self._hot = hot
-
     def _fwd_bwd_local(self, b: Batch, rows: torch.Tensor, dd) -> StepOut:
         """Forward + loss + backward/update of ``b`` on the current stream (dedup ``dd`` ready)."""
         ws, cfg = self.ws, self.cfg
-        hot = getattr(dd, "hot", None)
-        dA = ws.dense_counts(b.B) if (dd.dense_list is not None or hot is not None) else None
+        dA = ws.dense_counts(b.B) if dd.dense_list is not None else None
         rv, rw = self.reg_coeffs
         with roctx_range("fwd"):
             fo = K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,
                               weights=b.weights, loss=cfg.loss_type, grad_scale=self.grad_scale(b.B), want_r1=True,
                               pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
-                              threads=cfg.threads, bias=self.gbias, dense=dd, dense_A=dA, hot=hot, defer_loss=True)
+                              threads=cfg.threads, bias=self.gbias, dense=dd, dense_A=dA, defer_loss=True)
             self.bias_step(fo.dpred)
         with roctx_range("bwd+update"):
             K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
                           reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, dense_part=ws.dense_part,
                           dense_stream=self._dense_stream(),
-                          sr_counter=self.sr_tick(), dense_A=dA, hot=hot)
+                          sr_counter=self.sr_tick(), dense_A=dA)
         return StepOut(fo.finish_loss(), b.B)
 
     def _local_lookahead_step(self, b: Batch, next_batch: Batch | None, next2: Batch | None = None) -> StepOut:
@@ -688,10 +622,6 @@ class FactorizationMachine:
             pl = self._local_plan(b)
         main.wait_event(pl.ready)
         out = self._fwd_bwd_local(b, pl.rows, pl.dd)
-        if self._hot_want and self._hot is None and b.vals is None and getattr(pl.dd, "hot", None) is None:
-            self._hot_from_plan(pl.dd)  # (plans created from here on leave these rows out)
-        elif self._hot_refresh and self._hot is not None and self.global_step % self._hot_refresh == 0:
-            self._hot = None  # re-pick from the next unfiltered plan (the pending ones keep their set)
         done = torch.cuda.Event()
         done.record(main)
         self._lslots[pl.slot].done = done

@@ -172,7 +172,7 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
                bias: torch.Tensor | None = None, dense: "DedupOut | None" = None,
                dense_A: torch.Tensor | None = None, dense_by_segment: bool = False,
                self_rows: SelfRows | None = None, seg_lookup: "SegIndex | None" = None,
-               hot: HotRows | None = None, defer_loss: bool = False) -> FwdOut:
+               defer_loss: bool = False) -> FwdOut:
     """FM score of a CSR batch (reference FmScorer, cc/fm_scorer_op.h:101-140), fused with the loss.
 
     pred_i = sum_j x_j w_j + 1/2 sum_k [(sum_j x_j v_jk)^2 - sum_j x_j^2 v_jk^2]  (+ bias[0], optional
@@ -187,8 +187,6 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
     ``self_rows`` (GPU, ``rows`` = segment ids): segments in its range read this rank's table.
     ``seg_lookup`` (GPU): ``rows`` are the dedup's keys and every occurrence's segment (its
     row of ``v``) is found through the bucket index (``seg_index``) instead of an inverse map.
-    ``hot`` (GPU, with ``dense_A``): count the occurrences of these table rows instead of a
-    dedup's dense rows.
     (``defer_loss``, GPU: the per-workgroup loss partials are left for ``FwdOut.finish_loss``, so the
     reduction can be enqueued after the backward instead of between forward and backward.)
     """
@@ -239,11 +237,6 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
                    and dense_A.shape[0] >= B, "dense_A: contiguous uint8 [>= B, MAX_DENSE]")
             dkw = dict(dense_list=_p(dense.dense_list), dense_uniq=0 if dense_by_segment else _p(dense.uniq),
                        dense_count=_p(dense.counts) + 12, dense_A=_p(dense_A))
-        elif hot is not None and dense_A is not None:
-            _check(vals is None, "hot-row counts are for binary-feature batches (vals is None)")
-            _check(dense_A.dtype == torch.uint8 and dense_A.is_contiguous() and dense_A.shape[1] == MAX_DENSE
-                   and dense_A.shape[0] >= B, "dense_A: contiguous uint8 [>= B, MAX_DENSE]")
-            dkw = dict(dense_list=_p(hot.keys), dense_uniq=0, dense_count=_p(hot.n), dense_A=_p(dense_A))
         if self_rows is not None and self_rows.u1 > self_rows.u0:
             _self_check(self_rows, v, None)
             dkw["self_rows"] = self_rows.packed()
@@ -292,12 +285,11 @@ class DedupOut:
     ``num_unique`` is a view of counts[0]; ``U_host`` is set on CPU and after
     ``.sync()``.  ``perm`` is the sorted payload: the occurrence index, unless
     the dedup ran with the example index as payload (then ``sorted_ex is perm``).
-    ``hot``: the HotRows set whose occurrences were filtered out of this grouping (or None).
     """
 
     __slots__ = ("n", "skeys", "perm", "uniq", "seg_start", "seg_chunk", "chunk_start", "chunk_seg", "chunk_key",
                  "counts", "num_unique", "inv", "sorted_ex", "sorted_x", "U_host", "CH", "big_list", "big_count",
-                 "multi", "ex_shift", "dense_list", "bwd_fresh", "hot")
+                 "multi", "ex_shift", "dense_list", "bwd_fresh")
 
     def __init__(self, **kw):
         for k in self.__slots__:
@@ -328,7 +320,7 @@ class DedupWorkspace:
         self.chunk_start = torch.empty(n1 + 1, **i32)
         self.chunk_seg = torch.empty(n1, **i32)   # segment id | first (bit 30) | single (bit 31)
         self.chunk_key = torch.empty(n1, **i32)
-        self.counts = torch.zeros(8, **i32)   # U, #chunks, #multi-chunk rows, #dense rows, bwd hot rows, -
+        self.counts = torch.zeros(8, **i32)   # U, #chunks, #multi-chunk rows, #dense rows, bwd big rows, -
         self.multi = torch.empty(n1, **i32)
         self.inv = torch.empty(n1, **i32)
         self.sorted_ex = torch.empty(n1, **i32)
@@ -377,61 +369,6 @@ MAX_DENSE = 256            # = fm::kMaxDense: rows on the MFMA backward path
 DENSE_WG = 256             # = fm::kDenseWG: workgroups (partial rows) of the dense kernel
 
 
-@dataclass
-class HotRows:
-    """A set of <= MAX_DENSE hot table rows of the local step (hip/hot.hip): their occurrences
-    are filtered out of the dedup input, counted per example by the forward into ``dense_A`` and
-    reduced by the dense-row GEMM.  ``keys`` int32 [MAX_DENSE] (first ``n`` valid, ascending),
-    ``n`` int32 [1] on the device (kernels read it there), ``n_host`` the same on the host."""
-
-    keys: torch.Tensor
-    n: torch.Tensor
-    n_host: int = 0
-
-    @staticmethod
-    def empty(dev) -> "HotRows":
-        return HotRows(torch.zeros(MAX_DENSE, dtype=torch.int32, device=dev),
-                       torch.zeros(1, dtype=torch.int32, device=dev), 0)
-
-    def set(self, keys: torch.Tensor) -> None:
-        """Load (host or device) keys, <= MAX_DENSE distinct table rows; stored ascending."""
-        k = torch.sort(keys.to(torch.int64).flatten().cpu()).values
-        _check(k.numel() <= MAX_DENSE, f"at most {MAX_DENSE} hot rows")
-        _check(k.numel() < 2 or bool((k[1:] > k[:-1]).all()), "hot rows must be distinct")
-        buf = torch.zeros(MAX_DENSE, dtype=torch.int32)
-        buf[: k.numel()] = k.to(torch.int32)
-        self.keys.copy_(buf, non_blocking=False)
-        self.n.fill_(int(k.numel()))
-        self.n_host = int(k.numel())
-
-    def copy_from(self, other: "HotRows") -> None:
-        """Snapshot ``other`` on the current stream (plans keep the set they were filtered with)."""
-        self.keys.copy_(other.keys, non_blocking=True)
-        self.n.copy_(other.n, non_blocking=True)
-        self.n_host = other.n_host
-
-
-def hot_filter(offsets: torch.Tensor, ids: torch.Tensor, hot: HotRows, *, slot_bits: int, gcnt: torch.Tensor,
-               keys_out: torch.Tensor, codes_out: torch.Tensor, n_out: torch.Tensor) -> None:
-    """Dedup input without the hot rows' occurrences (GPU, hip/hot.hip): ``keys_out`` / ``codes_out``
-    get the kept (table row, packed occurrence code) pairs in CSR order, ``n_out`` (int32 [1],
-    device) their number.  ``gcnt``: int32 scratch of >= ceil(B / 64)."""
-    B = offsets.numel() - 1
-    dev = offsets.device
-    _check(_is_gpu(offsets), "hot_filter is a GPU path")
-    _chk_vec(offsets, torch.int32, B + 1, "offsets", dev)
-    nnz = ids.numel()
-    _chk_vec(ids, torch.int32, nnz, "ids", dev)
-    _check(gcnt.dtype == torch.int32 and gcnt.numel() >= (B + 63) // 64, "gcnt: int32 [>= ceil(B / 64)]")
-    for name, t in (("keys_out", keys_out), ("codes_out", codes_out)):
-        _check(t.dtype == torch.int32 and t.numel() >= nnz and t.device == dev, f"{name}: int32 [>= nnz]")
-    _check(n_out.dtype == torch.int32 and n_out.numel() >= 1, "n_out: int32 [1]")
-    _check(slot_bits >= 0 and (B << slot_bits) < 2 ** 31, "packed codes must fit int32")
-    native.hip().hot_filter(B=B, offsets=_p(offsets), ids=_p(ids), hot=_p(hot.keys), hot_n=_p(hot.n),
-                            slot_bits=int(slot_bits), gcnt=_p(gcnt), keys_out=_p(keys_out),
-                            codes_out=_p(codes_out), n_out=_p(n_out), stream=_stream(offsets))
-
-
 def dense_min_for(num_examples: int, Kp: int, CH: int = 32, *, has_vals: bool = False,
                   max_feats: int = 0, table_dtype: torch.dtype = torch.float32) -> int:
     """Occurrence threshold of the MFMA backward rows (0 = off).
@@ -447,15 +384,6 @@ def dense_min_for(num_examples: int, Kp: int, CH: int = 32, *, has_vals: bool = 
             or max_feats > 255 or r1_dtype(table_dtype) != torch.float32):
         return 0
     return max(8 * CH, num_examples // 40)
-def dedup_sort_algo() -> int:
-    """GPU dedup sort: FM_DEDUP_SORT=onesweep (rocPRIM, default: measured faster in the step) or
-    bucket (hip/dedup.hip; profiles/r3/dedup_sort_ab.txt)."""
-    h = native.hip()
-    v = os.environ.get("FM_DEDUP_SORT", "onesweep")
-    _check(v in ("bucket", "onesweep"), "FM_DEDUP_SORT must be bucket or onesweep")
-    return h.DEDUP_BUCKET if v == "bucket" else h.DEDUP_ONESWEEP
-
-
 class HotDict:
     """Dictionary of the hot-dictionary GPU dedup (hip/hdedup.hip): up to HD_MAX_H frequent table
     rows (ascending, with their LDS hash table), rebuilt on the device from a finished plan every
@@ -501,7 +429,7 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
           ex_of_occ: torch.Tensor | None = None, vals: torch.Tensor | None = None, want_inv: bool = False,
           CH: int | None = None, want_perm: bool = False, num_examples: int | None = None,
           Kp: int | None = None, ex_shift: int = 0, offsets: torch.Tensor | None = None,
-          dense_min: int = 0, n_dev: torch.Tensor | None = None, hot_dict: HotDict | None = None,
+          dense_min: int = 0, hot_dict: HotDict | None = None,
           want_skeys: bool = True) -> DedupOut:
     """Sort-based unique over non-negative int32 keys (reference tf.unique, fm_model.py:72).
 
@@ -512,10 +440,11 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
     sort carries the example index directly (one gather pass less).
     (``num_examples`` / ``Kp`` are accepted for interface stability; the plan does not use them.)
 
-    GPU sort: rocPRIM's onesweep radix sort, or with ``FM_DEDUP_SORT=bucket`` the bucket sort
-    (hip/dedup.hip: stable MSD partition by the top key bits + per-bucket LDS sort; same order).
-    ``n_dev`` (GPU, bucket sort): int32 [1] device count of the valid leading keys (``keys`` is then
-    the capacity): the plan is made without a host sync.
+    GPU grouping: rocPRIM's onesweep radix sort of every occurrence, or -- with ``hot_dict`` and
+    ``FM_DEDUP=hd``, for the local step's plans (example payload, no per-occurrence values or
+    inverse map) -- the hot-dictionary dedup (hip/hdedup.hip: the dictionary's rows grouped by a
+    counting sort, the rest radix-sorted; the same plan bitwise).  ``want_skeys`` (hd): also write
+    the sorted keys (the backward does not read them).
     """
     dev = keys.device
     n = keys.numel()
@@ -542,7 +471,7 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
                    sorted_x=ws.sorted_x if vals is not None else None, CH=CH, big_list=ws.big_list,
                    big_count=ws.big_count, multi=ws.multi, ex_shift=int(ex_shift),
                    dense_list=ws.dense_list if dense_min > 0 and ex_of_occ is not None and _is_gpu(keys) else None)
-    if (_is_gpu(keys) and hot_dict is not None and ex_payload and not want_inv and vals is None and n_dev is None
+    if (_is_gpu(keys) and hot_dict is not None and ex_payload and not want_inv and vals is None
             and out.dense_list is None and 0 < n and key_bits <= 31 and hd_dedup_enabled()
             and not torch.cuda.is_current_stream_capturing()):  # (a host wait between its two phases)
         # hot-dictionary dedup (hip/hdedup.hip): the same plan, sorting only the long tail
@@ -570,10 +499,6 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
     elif _is_gpu(keys):
         h = native.hip()
         _check(1 <= CH <= h.MAX_CH, f"CH must be in [1, {h.MAX_CH}]")
-        algo = dedup_sort_algo()
-        if n_dev is not None:
-            _check(algo == h.DEDUP_BUCKET, "a device count needs the bucket sort (FM_DEDUP_SORT=bucket)")
-            _chk_vec(n_dev, torch.int32, None, "n_dev", dev)
         h.dedup(n=n, end_bit=key_bits, CH=CH, keys=_p(keys), payload=_p(ex_of_occ if ex_payload else ws.iota),
                 skeys=_p(ws.skeys), spay=_p(ws.perm), uniq=_p(ws.uniq), seg_start=_p(ws.seg_start),
                 seg_chunk=_p(ws.seg_chunk), chunk_start=_p(ws.chunk_start), chunk_seg=_p(ws.chunk_seg),
@@ -583,10 +508,9 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
                 sorted_ex=0 if ex_payload else _p(out.sorted_ex), vals=_p(vals), sorted_x=_p(out.sorted_x),
                 payload_is_ex=int(ex_payload), ex_shift=int(ex_shift), offsets=_p(offsets),
                 dense_min=int(dense_min) if out.dense_list is not None else 0, dense_list=_p(out.dense_list),
-                ws=_p(ws.ws), ws_bytes=ws.ws.numel(), stream=_stream(keys), n_dev=_p(n_dev), algo=algo)
+                ws=_p(ws.ws), ws_bytes=ws.ws.numel(), stream=_stream(keys))
         out.bwd_fresh = True  # the backward counters were zeroed on this stream
     else:
-        _check(n_dev is None, "a device count is a GPU path")
         U = native.cpu().dedup(n=n, keys=_p(keys), skeys=_p(ws.skeys), perm=_p(ws.perm), uniq=_p(ws.uniq),
                                seg_start=_p(ws.seg_start), inv=_p(out.inv), ex_of_occ=_p(ex_of_occ),
                                sorted_ex=_p(out.sorted_ex), vals=_p(vals), sorted_x=_p(out.sorted_x))
@@ -702,8 +626,7 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
                 dense_part: torch.Tensor | None = None, dense_stream=None,
                 grad_bf16: bool = False, sr_counter: torch.Tensor | None = None,
                 seg_bounds: torch.Tensor | None = None, piece: int = -1,
-                dense_A: torch.Tensor | None = None, self_rows: SelfRows | None = None,
-                hot: HotRows | None = None) -> torch.Tensor | None:
+                dense_A: torch.Tensor | None = None, self_rows: SelfRows | None = None) -> torch.Tensor | None:
     """Segmented FM backward over the dedup grouping (reference FmGrad, cc/fm_grad_op.h:59-163).
 
     Per unique row u with occurrences (i, x):
@@ -716,8 +639,6 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
     second part (split backward of the row-sharded exchange); piece 1 must follow piece 0.
     ``self_rows`` (GPU, EMIT): segments in its range are read from its table; the exclusive ones
     get ``opt`` applied in place (with ``sr_counter``) and no gradient row.
-    ``hot`` (GPU, LOCAL, with the forward's ``dense_A``): rows filtered out of ``dd`` (``hot_filter``)
-    whose gradient comes from the dense-row GEMM; ``opt`` is applied to them here too.
     """
     dev = dpred.device
     _check(dd.sorted_ex is not None, "dedup must be run with ex_of_occ")
@@ -766,8 +687,6 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
             s_stride = s0v.stride(0)
     v_stride = _chk_rows(v, Kp, "v")
     _check(r1.dtype == r1_dtype(v.dtype), f"r1: {r1_dtype(v.dtype)} for {v.dtype} rows (the forward's r1)")
-    _check(hot is None or (mode == BWD_LOCAL and dd.dense_list is None and _is_gpu(dpred) and Kp <= 128),
-           "hot rows: GPU LOCAL step, Kp <= 128, no dedup dense rows")
     o = opt or OptConfig()
     if piece >= 0:
         _check(_is_gpu(dpred) and seg_bounds is not None and mode in (BWD_EMIT, BWD_EMIT_TABLE)
@@ -779,7 +698,7 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
             partial = torch.empty((partial_rows(dd.n, dd.CH), Kp + 4), dtype=torch.float32, device=dev)
         _check(partial.numel() >= partial_rows(dd.n, dd.CH) * (Kp + 4), "partial scratch too small")
         dp = None
-        if dd.dense_list is not None or hot is not None:  # MFMA path (counts written by the forward)
+        if dd.dense_list is not None:  # MFMA path (counts written by the forward)
             _check(dense_A is not None and dense_A.dtype == torch.uint8 and dense_A.shape[1] == MAX_DENSE
                    and dense_A.shape[0] >= dpred.numel(), "dense rows need the forward's dense_A counts")
             dp = dense_part if dense_part is not None else torch.empty(
@@ -798,7 +717,7 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               opt_type=o.code, lr=float(o.lr), l1=float(o.l1), l2=float(o.l2), beta=float(o.beta),
               grad_out=gptr, g_stride=gstride, partial=_p(partial), big_list=_p(dd.big_list),
               big_count=_p(dd.big_count), multi=_p(dd.multi),
-              dense_list=_p(hot.keys) if hot is not None else _p(dd.dense_list),
+              dense_list=_p(dd.dense_list),
               dense_part=_p(dp), nex=int(dpred.numel()),
               dense_stream=dense_stream.cuda_stream if dense_stream is not None else 0, dtype=dt, max_chunks=dd.n,
               max_unique=dd.n,
@@ -806,9 +725,8 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               sr_counter=_p(sr_counter), counters_ready=int(bool(dd.bwd_fresh)),
               seg_bounds=_p(seg_bounds), piece=int(piece),
               n_owners=(seg_bounds.numel() - 1) // 2 if seg_bounds is not None else 0,
-              dense_A=_p(dense_A) if (dd.dense_list is not None or hot is not None) else 0,
+              dense_A=_p(dense_A) if dd.dense_list is not None else 0,
               chunk_grid=int(os.environ.get("FM_CHUNK_GRID", "0")),
-              dense_n=_p(hot.n) if hot is not None else 0, hot_keys=_p(hot.keys) if hot is not None else 0,
               **skw)
         dd.bwd_fresh = False  # a second backward over this grouping zeroes its counters itself
     else:

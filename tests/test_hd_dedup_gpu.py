@@ -66,7 +66,11 @@ def _check(monkeypatch, keys, key_bits, hd, CH=32):
     ref, _ = _plan(monkeypatch, "onesweep", keys, payload, key_bits, CH)
     got, _ = _plan(monkeypatch, "hd", keys, payload, key_bits, CH, hd=hd)
     _same(got, ref)
+    # the ground truth too: keys ascending, ties in input order, uniq = torch.unique
     k = keys.long()
+    n = k.numel()
+    order = torch.sort(k * (n + 1) + torch.arange(n, device=DEV)).indices
+    assert torch.equal(got["perm"], payload[order])
     assert torch.equal(got["uniq"].long(), torch.unique(k))
 
 

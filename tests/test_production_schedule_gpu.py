@@ -31,13 +31,10 @@ POOL, STEPS = 4, 12
 
 @pytest.fixture
 def production(monkeypatch):
-    """FM_DEBUG_CHECKS off for the test (no host syncs inside the kernel wrappers).  Hot rows off:
-    the plain step has none, and the bitwise comparison is about the schedule (hot rows change
-    the hot rows' summation order; their match to fp32 error is tests/test_hot_rows_gpu.py)."""
+    """FM_DEBUG_CHECKS off for the test (no host syncs inside the kernel wrappers)."""
     was = K.debug_checks()
     K.set_debug_checks(False)
     monkeypatch.setenv("FM_DEBUG_CHECKS", "0")
-    monkeypatch.setenv("FM_HOT_ROWS", "0")
     yield
     K.set_debug_checks(was)
 

@@ -74,7 +74,7 @@ def test_bf16_table_step_close_to_fp32():
 @pytest.mark.parametrize("k,dtype", [(16, torch.float32), (64, torch.float32), (100, torch.float32),
                                      (64, torch.bfloat16), (128, torch.bfloat16)])
 def test_dense_mfma_backward_matches_oracle(monkeypatch, k, dtype):
-    """Rows above the density threshold go through the MFMA (3 x bf16 split GEMM) backward,
+    """Rows above the density threshold go through the MFMA (fp32-in v_mfma_f32_16x16x4f32) backward,
     with their per-example occurrence counts written by the forward; forced here with a low
     threshold so a small batch has dense rows (lookahead step: the dedup precedes the forward).
     (fp8 tables keep a bf16 r1, which the dense path does not read: dense_min_for is 0 there.)"""
@@ -134,9 +134,7 @@ def test_dense_mfma_backward_is_deterministic(monkeypatch):
 
 
 def test_local_lookahead_matches_plain_steps_bitwise(monkeypatch):
-    """Eager lookahead (next batch's dedup on the side stream during this step) == plain steps.
-    (Hot rows off: the plain step has none; tests/test_hot_rows_gpu.py covers them.)"""
-    monkeypatch.setenv("FM_HOT_ROWS", "0")
+    """Eager lookahead (next batch's dedup on the side stream during this step) == plain steps."""
     gen = CriteoSynth(20000, device="cuda", seed=15)
     batches = [gen.batch(1024) for _ in range(4)]
     a, b = _model(), _model()

@@ -1,10 +1,10 @@
-"""Dedup chain alone (csr_rows codes + sort + RLE plan) on Criteo-shaped batches, per sort algorithm.
+"""Dedup chain alone (csr_rows codes + grouping + chunk plan) on Criteo-shaped batches, per method.
 
-Times K.dedup back to back on a pool of batches (no step beside it), for the full batch and for the
-batch without the occurrences of its 256 most frequent rows (the hot-row filter's output shape).
-Run under ``rocprofv3 --kernel-trace --stats`` for per-kernel times of the chain alone.
+Times K.dedup back to back on a pool of batches (no step beside it): onesweep (rocPRIM radix sort
+of every occurrence) and hd (hot-dictionary dedup, hip/hdedup.hip, with a dictionary built from a
+batch outside the timed pool).  Run under ``rocprofv3 --kernel-trace --stats`` for per-kernel times.
 
-    python tools/bench_dedup.py [--algo onesweep,bucket] [--iters 30]
+    python tools/bench_dedup.py [--algo onesweep,hd] [--iters 30]
 """
 
 from __future__ import annotations
@@ -25,7 +25,7 @@ from fast_tffm_amd.ops import kernels as K  # noqa: E402
 
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--algo", default="onesweep,hd", help="onesweep | bucket | hd (hot-dictionary dedup)")
+    ap.add_argument("--algo", default="onesweep,hd", help="onesweep | hd")
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--pool", type=int, default=4)
     ap.add_argument("--vocab", type=int, default=125_000_000)
@@ -34,47 +34,39 @@ def main() -> int:
     dev = torch.device("cuda:0")
     gen = CriteoSynth(a.vocab, seed=1000, device=dev)
     kb = max(1, (a.vocab - 1).bit_length())
-    cases = {}
-    full, filt = [], []
+    pool = []
     for _ in range(a.pool):
         b = gen.batch(131072)
-        ids = b.ids.to(torch.int32)
         sb = K.slot_bits_for(b.B, b.max_feats)
-        codes = K.csr_rows(b.offsets, nnz=b.nnz, slot_bits=sb)
-        full.append((ids, codes, sb, b.offsets))
-        u, c = torch.unique(ids, return_counts=True)
-        hot = u[torch.argsort(c, descending=True)[:256]]
-        keep = ~torch.isin(ids, hot)
-        filt.append((ids[keep].contiguous(), codes[keep].contiguous(), sb, b.offsets))
-    cases["full"], cases["no_hot256"] = full, filt
+        pool.append((b.ids.to(torch.int32), b.offsets, b.nnz, sb))
     for algo in a.algo.split(","):
-        os.environ["FM_DEDUP_SORT"] = "bucket" if algo == "bucket" else "onesweep"
-        os.environ["FM_DEDUP"] = "hd" if algo == "hd" else "onesweep"
-        for name, pool in cases.items():
-            ws = K.DedupWorkspace(max(p[0].numel() for p in pool), dev, 32)
-            hd = None
-            if algo == "hd":  # dictionary from a batch outside the timed pool, frozen
-                hd = K.HotDict(dev, refresh=1)
-                b0 = gen.batch(131072)
-                K.dedup(b0.ids.to(torch.int32), ws=ws, key_bits=kb,
-                        ex_of_occ=K.csr_rows(b0.offsets, nnz=b0.nnz, slot_bits=pool[0][2]), hot_dict=hd)
-                hd.refresh = 10 ** 9
+        os.environ["FM_DEDUP"] = algo
+        ws = K.DedupWorkspace(max(p[0].numel() for p in pool), dev, 32)
+        hd = None
+        if algo == "hd":  # dictionary from a batch outside the timed pool, frozen
+            hd = K.HotDict(dev, refresh=1)
+            b0 = gen.batch(131072)
+            K.dedup(b0.ids.to(torch.int32), ws=ws, key_bits=kb,
+                    ex_of_occ=K.csr_rows(b0.offsets, nnz=b0.nnz, slot_bits=pool[0][3]), hot_dict=hd)
+            hd.refresh = 10 ** 9
 
-            def run(i):
-                ids, codes, sb, off = pool[i % len(pool)]
-                K.dedup(ids, ws=ws, key_bits=kb, ex_of_occ=codes, ex_shift=sb, offsets=off, hot_dict=hd,
-                        want_skeys=False)
+        def run(i):
+            ids, off, nnz, sb = pool[i % len(pool)]
+            codes = K.csr_rows(off, out=ws.ex_of_occ[:nnz], nnz=nnz, slot_bits=sb)
+            K.dedup(ids, ws=ws, key_bits=kb, ex_of_occ=codes, ex_shift=sb, offsets=off, hot_dict=hd,
+                    want_skeys=False)
 
-            for i in range(3):
-                run(i)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for i in range(a.iters):
-                run(i)
-            torch.cuda.synchronize()
-            ms = (time.perf_counter() - t0) / a.iters * 1e3
-            n = sum(p[0].numel() for p in pool) / len(pool)
-            print(f"[bench_dedup] {algo:8s} {name:9s} n={n / 1e6:.2f}M: {ms:.3f} ms per dedup", flush=True)
+        for i in range(3):
+            run(i)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(a.iters):
+            run(i)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / a.iters * 1e3
+        n = sum(p[2] for p in pool) / len(pool)
+        print(f"[bench_dedup] {algo:8s} n={n / 1e6:.2f}M: {ms:.3f} ms per dedup (csr_rows + grouping + plan)",
+              flush=True)
     return 0
 
 

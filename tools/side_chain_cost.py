@@ -56,23 +56,23 @@ def main() -> int:
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / n * 1e3
 
-    # full step (bench's call pattern, depth-2 lookahead); --only dedup: 3 steps (the hot-row pick)
+    # full step (bench's call pattern, depth-2 lookahead); --only dedup: 3 steps (the dictionary warms up)
     for i in range(3 if a.only == "dedup" else 6):
         m.train_step(pool[i % P], pool[(i + 1) % P], pool[(i + 2) % P])
     full = (0.0 if a.only == "dedup" else
             timed(lambda i: m.train_step(pool[i % P], pool[(i + 1) % P], pool[(i + 2) % P]), a.steps))
-    # precomputed plans, one slot per pool batch (filtered by the hot-row set when the step uses one)
+    # precomputed plans, one slot per pool batch
     m.ws.ensure(pool[0].B, max(b.nnz for b in pool))
     slots = [_LocalSlot() for _ in range(P)]
     if a.only == "dedup":
-        dedup = timed(lambda i: m._plan_into(slots[i % P], pool[i % P], hot_ok=True), a.steps)
+        dedup = timed(lambda i: m._plan_into(slots[i % P], pool[i % P]), a.steps)
         print(f"[side_chain] k={a.k} {a.dtype}: full {full:.3f} ms/step, dedup-only {dedup:.3f}", flush=True)
         m.close()
         return 0
-    plans = [m._plan_into(slots[j], pool[j], hot_ok=True) for j in range(P)]
+    plans = [m._plan_into(slots[j], pool[j]) for j in range(P)]
     torch.cuda.synchronize()
     compute = timed(lambda i: m._fwd_bwd_local(pool[i % P], *plans[i % P]), a.steps)
-    dedup = timed(lambda i: m._plan_into(slots[i % P], pool[i % P], hot_ok=True), a.steps)
+    dedup = timed(lambda i: m._plan_into(slots[i % P], pool[i % P]), a.steps)
     print(f"[side_chain] k={a.k} {a.dtype}: full {full:.3f} ms/step, compute-only {compute:.3f}, "
           f"dedup-only {dedup:.3f}", flush=True)
     m.close()
