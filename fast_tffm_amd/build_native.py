@@ -35,7 +35,7 @@ HIP_SOURCES = ["hip/module.hip"]
 # selected at run time with FM_HIP_VARIANT=<name>; tools/gpu_ab.sh).  Same-box kernel comparisons
 # of a change against its predecessor; a variant is deleted with the losing code path once the
 # A/B is recorded under profiles/ (round 1-2's nocap / unr* / fwdw* / fp8packed went that way).
-HIP_VARIANTS: dict[str, list[str]] = {"fwdnopf": ["-DFM_FWD_PREFETCH=0"]}
+from fast_tffm_amd.build_variants import HIP_VARIANTS  # noqa: E402  (not hashed: flags are)
 
 
 _EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"  # resolved once (lazy init is not thread-safe)

@@ -1,0 +1,10 @@
+"""A/B build variants of the HIP module (``python -m fast_tffm_amd.build_native --variant NAME``,
+selected at run time with ``FM_HIP_VARIANT=NAME``): name -> extra hipcc flags.
+
+Kept out of build_native.py because that file is part of every module's content hash: adding a
+variant here leaves the other builds current (a variant's own flags are hashed into its build).
+"""
+
+HIP_VARIANTS: dict[str, list[str]] = {"fwdnopf": ["-DFM_FWD_PREFETCH=0"], "fwdgen": ["-DFM_FWD_SPECIALIZE=0"],
+                                     "bwdgen": ["-DFM_BWD_SPECIALIZE=0"],
+                                     "allgen": ["-DFM_FWD_SPECIALIZE=0", "-DFM_BWD_SPECIALIZE=0"]}

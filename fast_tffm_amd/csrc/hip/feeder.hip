@@ -14,7 +14,10 @@
 //   * a batch the GPU subset declines (syntax outside it, any malformed line) is parsed by the
 //     loader's CPU parser (the reference grammar and error strings) and uploaded instead;
 //   * release(d, stream) from the consumer records an event on the consumer's stream: the slot
-//     is overwritten only after the work queued there (the step that read the batch) has run.
+//     is overwritten only after the work queued there (the step that read the batch) has run;
+//   * a batch with more features than its slot's ids / vals hold (slot sizes are estimated from
+//     the heads of the files) is not an error: the thread asks the consumer for larger buffers
+//     (next() -> -4, resize_ids) and waits, holding the batch, until they arrive.
 // The loader crosses into this module only as a table of C function pointers (loader_api.h).
 #include <atomic>
 #include <chrono>
@@ -89,14 +92,21 @@ class GpuTextFeeder {
   }
 
   // 1: *out is the next batch; 0: no more batches; -1: timed out while the producer waits for a
-  // free slot (every slot is held by the consumer); -2: timed out; -3: failed (*err, *parse_err)
+  // free slot (every slot is held by the consumer); -2: timed out; -3: failed (*err, *parse_err);
+  // -4: slot out->d needs ids / vals of out->nnz entries (answer with resize_ids)
   int next(FeederBatch* out, int timeout_ms, std::string* err, bool* parse_err) {
     std::unique_lock<std::mutex> lk(mu_);
-    const auto pred = [&] { return !ready_.empty() || done_; };
+    const auto pred = [&] { return !ready_.empty() || done_ || resize_ask_; };
     if (timeout_ms < 0) {
       cv_ready_.wait(lk, pred);
     } else if (!cv_ready_.wait_for(lk, std::chrono::milliseconds(timeout_ms), pred)) {
       return starving_ ? -1 : -2;
+    }
+    if (resize_ask_) {
+      resize_ask_ = false;
+      out->d = resize_d_;
+      out->nnz = resize_need_;
+      return -4;
     }
     if (!ready_.empty()) {
       *out = ready_.front();
@@ -122,11 +132,24 @@ class GpuTextFeeder {
     cv_slot_.notify_one();
   }
 
+  // New ids / vals buffers (>= the requested entries) for the slot a -4 from next() named
+  void resize_ids(int d, int* ids, float* vals, size_t cap) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (d != resize_d_ || !ids || !vals || static_cast<int64_t>(cap) < resize_need_)
+      throw std::invalid_argument("feeder resize_ids: not the requested slot / size");
+    slots_[d].ids = ids;
+    slots_[d].vals = vals;
+    slots_[d].ids_cap = cap;
+    resize_d_ = -1;
+    cv_slot_.notify_all();
+  }
+
   size_t queued() {
     std::lock_guard<std::mutex> lk(mu_);
     return ready_.size();
   }
   long long fallbacks() const { return fallbacks_.load(); }
+  long long resizes() const { return resizes_.load(); }
   long long batches() const { return batches_.load(); }
 
   void close() {
@@ -184,6 +207,23 @@ class GpuTextFeeder {
     cv_ready_.notify_one();
   }
 
+  // Slot d (the thread's copy s) holds nnz features, asking the consumer for larger buffers
+  // first; false when the feeder is stopped meanwhile
+  bool fit_ids(int d, FeederSlot& s, int64_t nnz) {
+    if (static_cast<size_t>(nnz) <= s.ids_cap) return true;
+    std::unique_lock<std::mutex> lk(mu_);
+    resize_d_ = d;
+    resize_need_ = nnz;
+    resize_ask_ = true;
+    cv_ready_.notify_all();
+    cv_slot_.wait(lk, [&] { return stop_ || resize_d_ < 0; });
+    resize_ask_ = false;
+    if (stop_) return false;
+    s = slots_[d];
+    resizes_.fetch_add(1);
+    return static_cast<size_t>(nnz) <= s.ids_cap;
+  }
+
   void fail(const std::string& msg, bool parse) {
     std::lock_guard<std::mutex> lk(mu_);
     failed_ = true;
@@ -192,7 +232,7 @@ class GpuTextFeeder {
   }
 
   // CPU parse of a raw batch (declined by the tokenizer, or larger than the slot) into slot d
-  bool cpu_parse(const FeederSlot& s, const FmRawView& v, FeederBatch& b) {
+  bool cpu_parse(int d, FeederSlot& s, const FmRawView& v, FeederBatch& b) {
     const int64_t n = v.nlines;
     if (static_cast<size_t>(n) + 1 > s.ls_cap) {
       fail("batch of " + std::to_string(n) + " lines exceeds the feeder's slots", false);
@@ -211,8 +251,8 @@ class GpuTextFeeder {
       fail(r == -1 ? std::string(err) : std::string("CPU parse of a raw batch failed: ") + err, r == -1);
       return false;
     }
-    if (static_cast<size_t>(o.nnz) > s.ids_cap) {
-      fail("batch of " + std::to_string(o.nnz) + " features exceeds the feeder's slots", false);
+    if (!fit_ids(d, s, o.nnz)) {
+      if (!stop_) fail("batch of " + std::to_string(o.nnz) + " features exceeds the feeder's slots", false);
       return false;
     }
     hip_ok(hipStreamWaitEvent(st_, s.freed, 0), "hipStreamWaitEvent");
@@ -261,9 +301,11 @@ class GpuTextFeeder {
                           n < (int64_t(1) << 31);
         bool ok = true;
         if (v.kind == 1) {  // parsed on the host (CPU parser / binary cache): copy the CSR over
-          if (static_cast<size_t>(n) + 1 > s.ls_cap || static_cast<size_t>(v.nnz) > s.ids_cap) {
-            fail("batch of " + std::to_string(n) + " lines / " + std::to_string(v.nnz) +
-                 " features exceeds the feeder's slots", false);
+          if (static_cast<size_t>(n) + 1 > s.ls_cap) {
+            fail("batch of " + std::to_string(n) + " lines exceeds the feeder's slots", false);
+            ok = false;
+          } else if (!fit_ids(d, s, v.nnz)) {
+            if (!stop_) fail("batch of " + std::to_string(v.nnz) + " features exceeds the feeder's slots", false);
             ok = false;
           } else {
             hip_ok(hipStreamWaitEvent(st_, s.freed, 0), "hipStreamWaitEvent");
@@ -285,7 +327,7 @@ class GpuTextFeeder {
           hip_ok(hipMemsetAsync(s.offsets, 0, sizeof(int), st_), "hipMemsetAsync");
           hip_ok(hipStreamSynchronize(st_), "hipStreamSynchronize");
         } else if (!fits) {
-          ok = cpu_parse(s, v, b);
+          ok = cpu_parse(d, s, v, b);
         } else {
           hip_ok(hipStreamWaitEvent(st_, s.freed, 0), "hipStreamWaitEvent");
           hip_ok(hipMemcpyAsync(s.bytes, v.bytes, v.nbytes, hipMemcpyHostToDevice, st_), "H2D");
@@ -311,7 +353,7 @@ class GpuTextFeeder {
           hip_ok(hipEventRecord(s.ready, st_), "hipEventRecord");
           hip_ok(hipEventSynchronize(s.ready), "hipEventSynchronize");
           if (s.info_h[0]) {
-            ok = cpu_parse(s, v, b);  // syntax outside the GPU subset, or an error to report exactly
+            ok = cpu_parse(d, s, v, b);  // syntax outside the GPU subset, or an error to report exactly
           } else {
             b.nnz = s.info_h[4];
             b.max_feats = s.info_h[1];
@@ -349,7 +391,10 @@ class GpuTextFeeder {
   bool stop_ = false, closed_ = false, done_ = false, starving_ = false;
   bool failed_ = false, parse_error_ = false;
   std::string error_;
-  std::atomic<long long> fallbacks_{0}, batches_{0};
+  int resize_d_ = -1;             // slot waiting for larger ids / vals (guarded by mu_)
+  int64_t resize_need_ = 0;
+  bool resize_ask_ = false;        // the request is not yet returned by next()
+  std::atomic<long long> fallbacks_{0}, batches_{0}, resizes_{0};
   std::vector<float> h_labels_, h_vals_;
   std::vector<int32_t> h_offsets_, h_ids_;
 };

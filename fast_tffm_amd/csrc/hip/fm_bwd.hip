@@ -99,6 +99,75 @@ struct RowState {
   float wv, q0, q1;
 };
 
+// Row base of `row` in a row-major array of T with `stride` elements per row: one 32 x 32 ->
+// 64-bit multiply-add (rows are non-negative and < 2^31, a row's bytes < 2^32).
+template <typename T>
+__device__ inline T* row_ptr(T* base, long long row, long long stride) {
+  using C = typename std::conditional<std::is_const<T>::value, const char, char>::type;
+  return reinterpret_cast<T*>(reinterpret_cast<C*>(base) +
+                              (uint64_t)(uint32_t)row * (uint32_t)(stride * (long long)sizeof(T)));
+}
+// Optimizer state row (fp32; bf16 for fp8 tables: StateBf16).
+template <typename TV>
+__device__ inline void* state_row(void* s, long long row, long long stride) {
+  if constexpr (StateBf16<TV>::v) return row_ptr(reinterpret_cast<uint16_t*>(s), row, stride);
+  return row_ptr(reinterpret_cast<float*>(s), row, stride);
+}
+
+// LOCAL mode known at compile time (the chunk kernel's local instantiations): table row `key`,
+// optimizer applied in place, 32 x 32-bit row addressing.
+template <typename TV, int EPL>
+__device__ inline void bwd_load_local(const BwdArgs& a, long long key, int tE, RowState<EPL>& r) {
+  using F = Frag<TV>;
+  r.apply = true;
+  r.row = key;
+  F::load(row_ptr(reinterpret_cast<const TV*>(a.v), r.row, a.v_stride) + tE * EPL, r.vv);
+  const float* wr = row_ptr(static_cast<const float*>(a.w), r.row, a.w_stride);
+  r.wv = wr[0];
+  if constexpr (F::kScaled) {
+    const float s = wr[1];  // (row_scale)
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) r.vv[k] *= s;
+  }
+  load_state<TV, EPL>(state_row<TV>(a.s0v, r.row, a.s_stride), tE * EPL, r.st0);
+  r.q0 = a.s0w[(uint32_t)r.row];
+  if (a.s1v) {
+    load_state<TV, EPL>(state_row<TV>(a.s1v, r.row, a.s_stride), tE * EPL, r.st1);
+    r.q1 = a.s1w[(uint32_t)r.row];
+  } else {
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) r.st1[k] = 0.f;
+    r.q1 = 0.f;
+  }
+}
+
+template <int LPR, typename TV, int EPL>
+__device__ inline void bwd_finish_local(const BwdArgs& a, int t, bool tact, RowState<EPL>& r, const float (&A)[EPL],
+                                        float Scx, float Sc, int n_u, uint32_t sr) {
+  const float nreg_v = a.reg_v * (float)n_u, nreg_w = a.reg_w * (float)n_u;
+  float gr[EPL];
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) gr[k] = A[k] - Scx * r.vv[k] + nreg_v * r.vv[k];
+  const float gw = Sc + nreg_w * r.wv;
+  TV* tv = reinterpret_cast<TV*>(a.v);
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) opt_step(a.opt, gr[k], r.vv[k], r.st0[k], r.st1[k]);
+  store_row<LPR, TV>(row_ptr(tv, r.row, a.v_stride) + t * EPL, r.vv, a.w, r.row, a.w_stride, t, tact, sr);
+  if (tact) {
+    store_state<TV, EPL>(state_row<TV>(a.s0v, r.row, a.s_stride), t * EPL, r.st0, sr ? sr ^ kSrSalt0 : 0u,
+                         (uint32_t)r.row, (uint32_t)(t * EPL));
+    if (a.s1v)
+      store_state<TV, EPL>(state_row<TV>(a.s1v, r.row, a.s_stride), t * EPL, r.st1, sr ? sr ^ kSrSalt1 : 0u,
+                           (uint32_t)r.row, (uint32_t)(t * EPL));
+  }
+  if (t == 0) {
+    opt_step(a.opt, gw, r.wv, r.q0, r.q1);
+    row_ptr(a.w, r.row, a.w_stride)[0] = r.wv;
+    a.s0w[(uint32_t)r.row] = r.q0;
+    if (a.s1w) a.s1w[(uint32_t)r.row] = r.q1;
+  }
+}
+
 // Parameters (and, when the row is updated here, optimizer state) of segment u with key
 // `key`: LOCAL reads table row key; EMIT reads gathered row u, or -- a self row of the
 // row-sharded step -- table row key - self.base, applied in place when exclusive;
@@ -211,10 +280,20 @@ constexpr int chunk_min_waves() {
   return LPR == 32 ? 4 : 1;
 }
 
+// Chunk-kernel instantiations: kChunkAny runs every mode (split pieces, self rows, EMIT /
+// EMIT_TABLE gradient rows, 64-bit r1 offsets); the LOCAL ones know the mode at compile time
+// (no piece walk, no self-row or gradient-row paths, 32-bit row and r1 offsets -- the launcher
+// checks that r1 fits -- and group-relative ds_bpermute sources), kChunkLocalNoX also that the
+// occurrences carry no values (x = 1: one ds_bpermute per occurrence less, Scx = Sc).
+enum ChunkKind : int { kChunkAny = 0, kChunkLocal = 1, kChunkLocalNoX = 2 };
+#ifndef FM_BWD_SPECIALIZE
+#define FM_BWD_SPECIALIZE 1  // 0: every mode runs kChunkAny (the "bwdgen" build variant, A/B)
+#endif
+
 // One lane group per chunk of <= CH (<= kMaxCH) sorted occurrences of one row.
-template <int LPR, typename TV>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(chunk_min_waves<LPR, TV>())))
-void fm_bwd_chunk_kernel(BwdArgs a) {
+template <int LPR, typename TV, int KV>
+__device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
+  constexpr bool LOC = KV != kChunkAny, NOX = KV == kChunkLocalNoX;
   const uint32_t sr = sr_step_seed(a.sr_counter);  // stochastic rounding seed (0: nearest)
   constexpr int EPL = Frag<TV>::N;  // elements per lane of the table dtype
   constexpr int G = kWave / LPR;
@@ -224,13 +303,22 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR, t = lane % LPR;
   const int gbase = g * LPR;
+  const int gb4 = gbase << 2;  // (ds_bpermute byte address of the group's lane 0)
   const int nv = a.Kp / EPL;
   const bool tact = t < nv;
   const int tE = tact ? t : nv - 1;
   const int nchunks = a.counts[1];
+  // r1 row of example ex, this lane's EPL columns (LOCAL: 32-bit byte offsets, one mad)
+  constexpr uint32_t kR1E = R1Bf16<TV>::v ? 2u : 4u;
+  const char* r1b = reinterpret_cast<const char*>(a.r1);
+  const uint32_t r1rb = (uint32_t)a.Kp * kR1E, r1cb = (uint32_t)(tE * EPL) * kR1E;
+  auto r1_at = [&](int ex, float (&o)[EPL]) {
+    if constexpr (LOC) load_r1<TV, EPL>(r1b + ((uint32_t)ex * r1rb + r1cb), 0, o);
+    else load_r1<TV, EPL>(a.r1, (long long)ex * a.Kp + tE * EPL, o);
+  };
   // split-backward piece: this piece's chunk ranges (one per owner) and their prefix sums
   __shared__ int pr_start[kMaxPieceOwners], pr_pre[kMaxPieceOwners + 1];
-  const bool pieced = a.piece >= 0;
+  const bool pieced = !LOC && a.piece >= 0;
   if (pieced) {
     if (threadIdx.x == 0) {
       int acc = 0;
@@ -279,7 +367,10 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
     if (dense) continue;  // gradient from the MFMA path (fm_bwd_dense_kernel)
     const int len = j1 - j0;
     RowState<EPL> rs;
-    if (single) bwd_load<TV, EPL>(a, u, (long long)key, tE, rs);
+    if (single) {
+      if constexpr (LOC) bwd_load_local<TV, EPL>(a, (long long)key, tE, rs);
+      else bwd_load<TV, EPL>(a, u, (long long)key, tE, rs);
+    }
     // lane-parallel prefetch of the chunk's (example, dpred*x, x)
     int pex[PF];
     float pc[PF], px[PF];
@@ -289,7 +380,7 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
       const bool ok = jj < j1;
       const int jc = ok ? jj : j0;
       const int ex = a.sorted_ex[jc] >> a.ex_shift;
-      const float x = a.sorted_x ? a.sorted_x[jc] : 1.f;
+      const float x = !NOX && a.sorted_x ? a.sorted_x[jc] : 1.f;
       pex[q] = ex;
       px[q] = x;
       pc[q] = ok ? a.dpred[ex] * x : 0.f;
@@ -298,6 +389,25 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
 #pragma unroll
     for (int k = 0; k < EPL; ++k) A[k] = 0.f;
     float Scx = 0.f, Sc = 0.f;
+    // occurrence li of prefetch slot q: (example, c masked by ok, x).  General kernel: __shfl from
+    // lane gbase + li (gbase when !ok); LOCAL: ds_bpermute from gb4 + 4 li (the constant folds into
+    // the instruction's offset; an invalid slot reads its lane's clamped, valid example, c = 0)
+    auto occ = [&](int q, int li, bool ok, int& ex, float& cs, float& xs) {
+      if constexpr (LOC) {
+        const int sb = gb4 + (li << 2);
+        ex = __builtin_amdgcn_ds_bpermute(sb, pex[q]);
+        const float c0 = __int_as_float(__builtin_amdgcn_ds_bpermute(sb, __float_as_int(pc[q])));
+        cs = ok ? c0 : 0.f;
+        xs = NOX ? 1.f : __int_as_float(__builtin_amdgcn_ds_bpermute(sb, __float_as_int(px[q])));
+      } else {
+        // shuffles are unconditional (every lane of the group takes part); mask after
+        const int src = gbase + (ok ? li : 0);
+        ex = __shfl(pex[q], src, kWave);
+        const float c0 = __shfl(pc[q], src, kWave);
+        cs = ok ? c0 : 0.f;
+        xs = __shfl(px[q], src, kWave);
+      }
+    };
     if constexpr (LPR < kChunkUnr) {
       // narrow rows (k=16 bf16: LPR 2): flat walk over the chunk's occurrences with
       // kChunkUnr r1 rows in flight per lane (the q-major walk below keeps only LPR in
@@ -314,12 +424,9 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
           const int oi = o0 + uu;
           const int q = oi / LPR < PF ? oi / LPR : PF - 1, li = oi % LPR;
           const bool ok = oi < PF * LPR && oi < len;
-          const int src = gbase + (ok ? li : 0);
-          const int ex = __shfl(pex[q], src, kWave);
-          const float cs = __shfl(pc[q], src, kWave);
-          cc[uu] = ok ? cs : 0.f;
-          xx[uu] = __shfl(px[q], src, kWave);
-          load_r1<TV, EPL>(a.r1, (long long)ex * a.Kp + tE * EPL, rr[uu]);
+          int ex;
+          occ(q, li, ok, ex, cc[uu], xx[uu]);
+          r1_at(ex, rr[uu]);
         }
 #pragma unroll
         for (int uu = 0; uu < UNRF; ++uu) {
@@ -339,13 +446,9 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
       float rr[U4][EPL], cc[U4], xx[U4];
 #pragma unroll
       for (int uu = 0; uu < U4; ++uu) {
-        const bool ok = uu < len;
-        const int src = gbase + (ok ? uu : 0);
-        const int ex = __shfl(pex[0], src, kWave);
-        const float cs = __shfl(pc[0], src, kWave);
-        cc[uu] = ok ? cs : 0.f;
-        xx[uu] = __shfl(px[0], src, kWave);
-        load_r1<TV, EPL>(a.r1, (long long)ex * a.Kp + tE * EPL, rr[uu]);
+        int ex;
+        occ(0, uu, uu < len, ex, cc[uu], xx[uu]);
+        r1_at(ex, rr[uu]);
       }
 #pragma unroll
       for (int uu = 0; uu < U4; ++uu) {
@@ -364,13 +467,9 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
             for (int uu = 0; uu < UNR; ++uu) {
               const int li = l + uu;
               const bool ok = li < LPR && q * LPR + li < len;
-              const int src = gbase + (ok ? li : 0);
-              // shuffles are unconditional (every lane of the group takes part); mask after
-              const int ex = __shfl(pex[q], src, kWave);
-              const float cs = __shfl(pc[q], src, kWave);
-              cc[uu] = ok ? cs : 0.f;
-              xx[uu] = __shfl(px[q], src, kWave);
-              load_r1<TV, EPL>(a.r1, (long long)ex * a.Kp + tE * EPL, rr[uu]);
+              int ex;
+              occ(q, li < LPR ? li : 0, ok, ex, cc[uu], xx[uu]);
+              r1_at(ex, rr[uu]);
             }
 #pragma unroll
             for (int uu = 0; uu < UNR; ++uu) {
@@ -384,7 +483,8 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
       }
     }
     if (single) {
-      bwd_finish<LPR, TV, EPL>(a, u, t, tact, rs, A, Scx, Sc, len, sr);
+      if constexpr (LOC) bwd_finish_local<LPR, TV, EPL>(a, t, tact, rs, A, Scx, Sc, len, sr);
+      else bwd_finish<LPR, TV, EPL>(a, u, t, tact, rs, A, Scx, Sc, len, sr);
     } else {
       float* dst = a.partial + (long long)cc * (a.Kp + 4);
       if (tact) {
@@ -401,6 +501,16 @@ void fm_bwd_chunk_kernel(BwdArgs a) {
     }
   }
 }
+
+template <int LPR, typename TV>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(chunk_min_waves<LPR, TV>())))
+void fm_bwd_chunk_kernel(BwdArgs a) { bwd_chunk_body<LPR, TV, kChunkAny>(a); }
+template <int LPR, typename TV>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(chunk_min_waves<LPR, TV>())))
+void fm_bwd_chunk_local_kernel(BwdArgs a) { bwd_chunk_body<LPR, TV, kChunkLocal>(a); }
+template <int LPR, typename TV>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(chunk_min_waves<LPR, TV>())))
+void fm_bwd_chunk_local_nox_kernel(BwdArgs a) { bwd_chunk_body<LPR, TV, kChunkLocalNoX>(a); }
 
 // Rows split over 2..kSmallChunks chunks: one lane group, ordered sum of the partials.
 // Hotter rows are appended to big_list for fm_bwd_big_kernel.
@@ -770,7 +880,18 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   // (a split walk -- the chunks of multi-chunk rows first, their combine beside the single-chunk
   // rows' launch, or both launches concurrent -- measured slower: k64 0.669 -> 0.72-0.78 ms, each
   // launch as long as the whole walk; profiles/r3/bwd_split_ab.txt)
-  FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, a);
+  // LOCAL-mode chunk kernels (see ChunkKind) when r1 fits 32-bit offsets
+  const long long r1_bytes = (long long)a.nex * a.Kp * (dtype == kFP8 ? 2 : 4);
+  const int kind = FM_BWD_SPECIALIZE && a.mode == kBwdLocal && a.piece < 0 && lpr >= 4 && r1_bytes < (1LL << 32)
+                       ? (a.sorted_x ? kChunkLocal : kChunkLocalNoX)
+                       : kChunkAny;
+  if (kind == kChunkLocalNoX) {
+    FM_DISPATCH_WIDE(dtype, lpr, fm_bwd_chunk_local_nox_kernel, g1, st, a);
+  } else if (kind == kChunkLocal) {
+    FM_DISPATCH_WIDE(dtype, lpr, fm_bwd_chunk_local_kernel, g1, st, a);
+  } else {
+    FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, a);
+  }
   FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, a);
   FM_DISPATCH(dtype, lpr, fm_bwd_big_kernel, 1024, st, a);
   if (dense) {

@@ -400,6 +400,26 @@ inline int fill_grid(long long work_groups, int groups_per_block, int cap = 8192
     default: return -1;                                                                             \
   }
 
+// rows of >= 4 lanes only (kernels without narrow-row instantiations)
+#define FM_DISPATCH_WIDE_LPR(LPR_VAL, KERNEL, TV, GRID, STREAM, ARGS)                              \
+  switch (LPR_VAL) {                                                                                \
+    case 4: hipLaunchKernelGGL((KERNEL<4, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break;  \
+    case 8: hipLaunchKernelGGL((KERNEL<8, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break;  \
+    case 16: hipLaunchKernelGGL((KERNEL<16, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break; \
+    case 32: hipLaunchKernelGGL((KERNEL<32, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break; \
+    case 64: hipLaunchKernelGGL((KERNEL<64, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break; \
+    default: return -1;                                                                             \
+  }
+
+#define FM_DISPATCH_WIDE(DTYPE, LPR_VAL, KERNEL, GRID, STREAM, ARGS)                  \
+  if ((DTYPE) == kBF16) {                                                            \
+    FM_DISPATCH_WIDE_LPR(LPR_VAL, KERNEL, __hip_bfloat16, GRID, STREAM, ARGS)        \
+  } else if ((DTYPE) == kFP8) {                                                      \
+    FM_DISPATCH_WIDE_LPR(LPR_VAL, KERNEL, fp8e4m3, GRID, STREAM, ARGS)               \
+  } else {                                                                           \
+    FM_DISPATCH_WIDE_LPR(LPR_VAL, KERNEL, float, GRID, STREAM, ARGS)                 \
+  }
+
 #define FM_DISPATCH(DTYPE, LPR_VAL, KERNEL, GRID, STREAM, ARGS)                       \
   if ((DTYPE) == kBF16) {                                                            \
     FM_DISPATCH_LPR(LPR_VAL, KERNEL, __hip_bfloat16, GRID, STREAM, ARGS)             \

@@ -63,6 +63,9 @@ __device__ inline int seg_lookup(const FwdArgs& a, int k) {
 #ifndef FM_FWD_PREFETCH
 #define FM_FWD_PREFETCH 1
 #endif
+#ifndef FM_FWD_SPECIALIZE  // 0: every step runs the general (sharded) forward (A/B build variant "fwdgen")
+#define FM_FWD_SPECIALIZE 1
+#endif
 constexpr int kSelfBit = (int)0x80000000u;   // row index tag: this rank's own table row (SelfRows)
 constexpr int kDenseHash = 4 * kMaxDense;  // open-addressing table of the dense keys (LDS, load <= 1/4)
 
@@ -98,6 +101,16 @@ template <int LPR, typename TV>
 constexpr int fwd_min_waves() {
   return LPR >= 32 ? 4 : 1;
 }
+// The local forward's 16-lane instantiations (k=64) at 4 waves/SIMD: a variant of the register
+// accumulation needed 136 VGPRs uncapped (3 waves), 0.674 vs 0.643 ms capped on the k64 fp32 step
+// (profiles/r4/specialize_ab.txt); the current code fits in 115 either way, the floor keeps it there
+#ifndef FM_FWD_LOCAL_W16
+#define FM_FWD_LOCAL_W16 4
+#endif
+template <int LPR, typename TV>
+constexpr int fwd_local_min_waves() {
+  return LPR == 16 ? FM_FWD_LOCAL_W16 : fwd_min_waves<LPR, TV>();
+}
 
 // LDS of the dense-row counting (FM_DENSE_BWD): only the dense instantiation carries it
 template <bool DENSE> struct DenseLds {
@@ -106,7 +119,13 @@ template <bool DENSE> struct DenseLds {
 };
 template <> struct DenseLds<false> {};
 
-template <int LPR, typename TV, bool DENSE>
+// SH: the row-sharded step's features (self rows, segment lookup: a tagged row index selects the
+// table, rows[] may be keys).  The local step's instantiation (SH = false) addresses every row as
+// base + row * stride with one 32 x 32 -> 64-bit multiply-add and reads the broadcast pairs with
+// precomputed ds_bpermute offsets: per row group ~5 address / index VALU instructions instead of
+// ~16 (the tag test, base / stride selects and a 64-bit stride multiply), on a kernel the PMC
+// table shows 62% (k64 fp32) / 82% (k128 fp8) VALU-busy (profiles/r4/pmc_*.txt).
+template <int LPR, typename TV, bool DENSE, bool SH = true>
 __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
   using F = Frag<TV>;
   constexpr int EPL = F::N;
@@ -119,13 +138,16 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
   const int tE = tact ? t : nv - 1;        // clamped: loads never leave the row
   const float tmask = tact ? 1.f : 0.f;
   const TV* vbase = reinterpret_cast<const TV*>(a.v) + tE * EPL;
-  const bool self_on = a.self.u1 > a.self.u0;  // (uniform)
+  // (local step) byte base of this lane's fragment and the row stride in bytes (< 2^32: host-checked)
+  const char* vbytes = reinterpret_cast<const char*>(vbase);
+  const uint32_t vsb = (uint32_t)(a.v_stride * (long long)sizeof(TV));
+  const bool self_on = SH && a.self.u1 > a.self.u0;  // (uniform)
   const TV* tbase = self_on ? reinterpret_cast<const TV*>(a.self.v) + tE * EPL : vbase;
   const int wave = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   const int nwaves = gridDim.x * kWavesPerBlock;
   const bool want_reg = a.reg_partial != nullptr;
   // (segment lookup + self rows: the key range of the own segments, read once)
-  const bool self_key = self_on && a.seg_idx != nullptr && !DENSE;
+  const bool self_key = SH && self_on && a.seg_idx != nullptr && !DENSE;
   const int self_kmin = self_key ? a.self.keys[a.self.u0] : 0;
   const int self_kmax = self_key ? a.self.keys[a.self.u1 - 1] : -1;
 
@@ -207,7 +229,11 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
       } else {
         pairs(base, m, my_row, my_x);
       }
-      if (lane < m) {
+      if (!SH && lane < m) {
+        my_seg = my_row;
+        my_w = a.w[(long long)my_row * a.w_stride];
+        my_s = row_scale<TV>(a.w, my_row, a.w_stride);
+      } else if (lane < m) {
         my_seg = my_row;
         // segment lookup mode: rows[] are keys; an own row is known by its key alone (the self
         // segments are exactly the batch's keys in [self_kmin, self_kmax]), so it needs neither
@@ -215,7 +241,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
         // the segment: then every key is looked up)
         const int key = my_row;
         const bool own_key = self_key && key >= self_kmin && key <= self_kmax;
-        if (a.seg_idx && !own_key) my_seg = my_row = seg_lookup(a, key);
+        if (SH && a.seg_idx && !own_key) my_seg = my_row = seg_lookup(a, key);
         // the linear weight (and fp8 scale, same cache line) of occurrence `lane`, one
         // lane-parallel load per 64 occurrences instead of one per row group: the w loads
         // were ~45% of the kernel's VMEM instructions with the TA 72% busy
@@ -245,19 +271,33 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
           const int f = q + u * G + g;
-          const int src = f < m ? f : 0;
-          const int row = __shfl(my_row, src, kWave);
-          const float x = __shfl(my_x, src, kWave);
-          fx[u] = f < m ? x : 0.f;
-          // (one load either way: the tagged index selects the base, not the instruction)
-          const TV* rp = row < 0 ? tbase + (long long)(row & ~kSelfBit) * a.self.v_stride
-                                 : vbase + (long long)row * a.v_stride;
-          F::load(rp, fr[u]);
-          if constexpr (F::kScaled) fs[u] = __shfl(my_s, src, kWave);
+          if constexpr (SH) {
+            const int src = f < m ? f : 0;
+            const int row = __shfl(my_row, src, kWave);
+            const float x = __shfl(my_x, src, kWave);
+            fx[u] = f < m ? x : 0.f;
+            // (one load either way: the tagged index selects the base, not the instruction)
+            const TV* rp = row < 0 ? tbase + (long long)(row & ~kSelfBit) * a.self.v_stride
+                                   : vbase + (long long)row * a.v_stride;
+            F::load(rp, fr[u]);
+            if constexpr (F::kScaled) fs[u] = __shfl(my_s, src, kWave);
+          } else {
+            // lanes past the round wrap around the wave (ds_bpermute takes the lane modulo 64):
+            // a valid row of this example or row 0, masked by fx = 0
+            const int fb = (f & (kWave - 1)) << 2;
+            const int row = __builtin_amdgcn_ds_bpermute(fb, my_row);
+            const float x = __int_as_float(__builtin_amdgcn_ds_bpermute(fb, __float_as_int(my_x)));
+            fx[u] = f < m ? x : 0.f;
+            F::load(reinterpret_cast<const TV*>(vbytes + (uint64_t)(uint32_t)row * vsb), fr[u]);
+            if constexpr (F::kScaled) fs[u] = __int_as_float(__builtin_amdgcn_ds_bpermute(fb, __float_as_int(my_s)));
+          }
         }
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
           float (&fv)[EPL] = fr[u];
+          // (folding the fp8 row scale into the occurrence's x instead of every element, with the
+          // reg term as a per-occurrence sum times scale^2 -- fewer VALU ops -- made the k128 fp8
+          // FTRL step slower, 0.888 -> 1.014 ms same-box: profiles/r4/specialize_ab.txt)
           if constexpr (F::kScaled) {
 #pragma unroll
             for (int k = 0; k < EPL; ++k) fv[k] *= fs[u];
@@ -351,9 +391,16 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
 }
 
 template <int LPR, typename TV>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(fwd_min_waves<LPR, TV>())))
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(fwd_local_min_waves<LPR, TV>())))
 void fm_fwd_kernel(FwdArgs a) {
-  fwd_body<LPR, TV, false>(a);
+  fwd_body<LPR, TV, false, false>(a);
+}
+
+// The row-sharded step's forward (self rows, segment lookup).
+template <int LPR, typename TV>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(fwd_min_waves<LPR, TV>())))
+void fm_fwd_shard_kernel(FwdArgs a) {
+  fwd_body<LPR, TV, false, true>(a);
 }
 
 // The forward that also counts every example's dense-row occurrences (FM_DENSE_BWD's MFMA
@@ -428,7 +475,11 @@ int launch_fwd(const FwdArgs& a, int dtype, int grid, hipStream_t st) {
 #undef FM_FWD_DENSE
     return (int)hipGetLastError();
   }
-  FM_DISPATCH(dtype, lpr, fm_fwd_kernel, grid, st, a);
+  if (a.self.u1 > a.self.u0 || a.seg_idx || !FM_FWD_SPECIALIZE) {
+    FM_DISPATCH(dtype, lpr, fm_fwd_shard_kernel, grid, st, a);
+  } else {
+    FM_DISPATCH(dtype, lpr, fm_fwd_kernel, grid, st, a);
+  }
   return (int)hipGetLastError();
 }
 

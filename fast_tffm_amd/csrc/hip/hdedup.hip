@@ -38,11 +38,11 @@ constexpr int kHdTile = 8192;                       // classify / hot-scatter ti
 constexpr int kHdQ = kHdTile / kHdWaves;            // 1024 elements per wave: one cold subtile
 constexpr int kHdR = kHdQ / kWave;                  // 16 rounds of 64
 constexpr int kHdScanWaves = 16;                    // hot column scan: tile ranges per column
-constexpr int kHdRle = 2048;                        // cold-RLE / plan tile (8 per thread)
+constexpr int kHdIt = 2;                            // cold-RLE / plan items per thread
+constexpr int kHdRle = kBlock * kHdIt;              // cold-RLE / plan tile
 constexpr int kHdInline = 8;                        // chunks a plan thread writes per segment
 constexpr int kHdMinCount = 16;                     // dictionary rows occur at least this often
 static_assert(kHdSlots == 1 << kHdSlotBits, "slot bits");
-static_assert(kHdRle == kBlock * 8, "plan tile: 8 per thread");
 static_assert(kHdQ < 65536, "16-bit per-wave counters");
 
 __device__ inline int hd_slot(uint32_t key) { return (int)((key * 0x9E3779B1u) >> (32 - kHdSlotBits)); }
@@ -228,23 +228,34 @@ __device__ inline unsigned hd_prefix_of_tiles(const int* cnt, int upto) {
   return t;
 }
 
-// cold subtile counts -> exclusive prefix (in place) and the total n_c (one workgroup)
-__global__ __launch_bounds__(kBlock) void hd_cold_prefix_kernel(HdArgs a) {
-  __shared__ unsigned s_run;
-  if (threadIdx.x == 0) s_run = 0u;
-  __syncthreads();
-  for (int i0 = 0; i0 < a.nsub; i0 += kBlock) {
-    const int i = i0 + threadIdx.x;
-    const unsigned v = i < a.nsub ? (unsigned)a.sub_cold[i] : 0u;
-    unsigned ex, tot;
-    hd_block_scan(v, ex, tot);
-    const unsigned run = s_run;
-    if (i < a.nsub) a.sub_cold[i] = (int)(run + ex);
-    __syncthreads();
-    if (threadIdx.x == 0) s_run = run + tot;
-    __syncthreads();
+// cold subtile counts -> exclusive prefix (in place) and the total n_c: one workgroup of 1024
+// threads, each owning a run of consecutive subtiles
+__global__ __launch_bounds__(1024) void hd_cold_prefix_kernel(HdArgs a) {
+  __shared__ unsigned s_w[16];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid >> 6;
+  const int per = (a.nsub + 1023) / 1024;
+  const int i0 = tid * per, i1 = min(a.nsub, i0 + per);
+  unsigned own = 0;
+  for (int i = i0; i < i1; ++i) own += (unsigned)a.sub_cold[i];
+  unsigned inc = own;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const unsigned up = __shfl_up(inc, o, kWave);
+    if (lane >= o) inc += up;
   }
-  if (threadIdx.x == 0) a.hc[0] = (int)s_run;
+  if (lane == kWave - 1) s_w[wv] = inc;
+  __syncthreads();
+  unsigned run = inc - own, tot = 0;
+  for (int w = 0; w < 16; ++w) {
+    if (w < wv) run += s_w[w];
+    tot += s_w[w];
+  }
+  for (int i = i0; i < i1; ++i) {
+    const unsigned c = (unsigned)a.sub_cold[i];
+    a.sub_cold[i] = (int)run;
+    run += c;
+  }
+  if (tid == 0) a.hc[0] = (int)tot;
 }
 
 // ---------------------------------------------------------------------------
@@ -359,9 +370,9 @@ __global__ __launch_bounds__(1024) void hd_hot_rows_kernel(HdArgs a) {
 // cold run-length encoding + final placement of the cold occurrences and segments
 __global__ __launch_bounds__(kBlock) void hd_crle_count_kernel(HdArgs a) {
   const int n_c = a.n_c, t = blockIdx.x;
-  const int j0 = t * kHdRle + threadIdx.x * 8;
+  const int j0 = t * kHdRle + threadIdx.x * kHdIt;
   unsigned v = 0;
-  for (int q = 0; q < 8; ++q) {
+  for (int q = 0; q < kHdIt; ++q) {
     const int j = j0 + q;
     if (j < n_c) v += (j == 0 || a.cks[j] != a.cks[j - 1]);
   }
@@ -378,19 +389,19 @@ __global__ __launch_bounds__(kBlock) void hd_crle_emit_kernel(HdArgs a) {
   const int last = n_c > 0 ? (n_c - 1) / kHdRle : 0;
   for (int i = tid; i < Hn; i += kBlock) s_dk[i] = a.d.keys[i];
   const unsigned pre = hd_prefix_of_tiles(a.tile_cnt, t);
-  const int j0 = t * kHdRle + tid * 8;
-  uint32_t k[8];
-  int pv[8];
-  bool hd[8];
+  const int j0 = t * kHdRle + tid * kHdIt;
+  uint32_t k[kHdIt];
+  int pv[kHdIt];
+  bool hd[kHdIt];
   unsigned v = 0;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
+  for (int q = 0; q < kHdIt; ++q) {
     const int j = j0 + q;
     k[q] = j < n_c ? a.cks[j] : 0u;
     pv[q] = j < n_c ? a.cvs[j] : 0;
   }
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
+  for (int q = 0; q < kHdIt; ++q) {
     const int j = j0 + q;
     hd[q] = j < n_c && (j == 0 || k[q] != (q ? k[q - 1] : a.cks[j - 1]));
     v += hd[q];
@@ -402,7 +413,7 @@ __global__ __launch_bounds__(kBlock) void hd_crle_emit_kernel(HdArgs a) {
   int s = (int)(s_pre + ex) - 1;
   int hb = -1;  // dictionary keys below the current key (recomputed at each head)
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
+  for (int q = 0; q < kHdIt; ++q) {
     const int j = j0 + q;
     if (j >= n_c) break;
     if (hd[q] || hb < 0) hb = lower_bound_dev(s_dk, Hn, (int)k[q]);
@@ -518,9 +529,9 @@ __global__ __launch_bounds__(kBlock) void hd_plan_count_kernel(HdArgs a) {
     if (threadIdx.x == 0) a.tile_cnt[t] = 0;
     return;
   }
-  const int s0 = t * kHdRle + threadIdx.x * 8;
+  const int s0 = t * kHdRle + threadIdx.x * kHdIt;
   unsigned v = 0;
-  for (int q = 0; q < 8; ++q) {
+  for (int q = 0; q < kHdIt; ++q) {
     const int s = s0 + q;
     if (s < U) v += (unsigned)hd_nchunks(a.seg_start[s], a.seg_start[s + 1], a.CH);
   }
@@ -535,14 +546,14 @@ __global__ __launch_bounds__(kBlock) void hd_plan_emit_kernel(HdArgs a) {
   const int last = U > 0 ? (U - 1) / kHdRle : 0;
   if (t > last) return;
   const unsigned pre = hd_prefix_of_tiles(a.tile_cnt, t);
-  const int s0 = t * kHdRle + tid * 8;
-  int st[9];
+  const int s0 = t * kHdRle + tid * kHdIt;
+  int st[kHdIt + 1];
 #pragma unroll
-  for (int q = 0; q < 9; ++q) st[q] = s0 + q <= U ? a.seg_start[s0 + q] : a.n;
+  for (int q = 0; q < kHdIt + 1; ++q) st[q] = s0 + q <= U ? a.seg_start[s0 + q] : a.n;
   unsigned v = 0;
-  int nch[8];
+  int nch[kHdIt];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
+  for (int q = 0; q < kHdIt; ++q) {
     nch[q] = s0 + q < U ? hd_nchunks(st[q], st[q + 1], a.CH) : 0;
     v += (unsigned)nch[q];
   }
@@ -551,7 +562,7 @@ __global__ __launch_bounds__(kBlock) void hd_plan_emit_kernel(HdArgs a) {
   if (tid == 0) s_pre = pre;
   __syncthreads();
   int c = (int)(s_pre + ex);
-  for (int q = 0; q < 8; ++q) {
+  for (int q = 0; q < kHdIt; ++q) {
     const int s = s0 + q;
     if (s >= U) break;
     const int key = (int)a.uniq[s];
@@ -795,7 +806,7 @@ int launch_hd_phase1(const HdLaunch& p, hipStream_t st) {
   HdLayout L;
   if (int e = hd_args(p, a, L)) return e;
   hipLaunchKernelGGL(hd_classify_kernel, dim3(L.ntiles), dim3(kHdThreads), 0, st, a);
-  hipLaunchKernelGGL(hd_cold_prefix_kernel, dim3(1), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL(hd_cold_prefix_kernel, dim3(1), dim3(1024), 0, st, a);
   hipLaunchKernelGGL(hd_hot_scan_kernel, dim3(kHdMaxH / kWave), dim3(kWave * kHdScanWaves), 0, st, a);
   hipLaunchKernelGGL(hd_hot_rows_kernel, dim3(1), dim3(1024), 0, st, a);
   return (int)hipGetLastError();

@@ -471,7 +471,8 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
            })
       .def("start", &fm::GpuTextFeeder::start)
       // -> (slot, n, nnz, max_feats, has_vals, weighted, epoch, count) | None at the end | -1 (timed out,
-      //    the feeder waits for a free slot) | -2 (timed out) | ("error", is_parse_error, message)
+      //    the feeder waits for a free slot) | -2 (timed out) | ("error", is_parse_error, message) |
+      //    ("resize", slot, entries): answer with resize_ids
       .def("next",
            [](fm::GpuTextFeeder& F, int timeout_ms) -> py::object {
              fm::FeederBatch b;
@@ -486,9 +487,16 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
                return py::make_tuple(b.d, b.n, b.nnz, b.max_feats, b.has_vals, b.weighted, b.epoch, b.count);
              if (r == 0) return py::none();
              if (r == -3) return py::make_tuple(std::string("error"), perr, err);
+             if (r == -4) return py::make_tuple(std::string("resize"), b.d, b.nnz);
              return py::int_(r);
            },
            py::arg("timeout_ms") = -1)
+      .def("resize_ids",
+           [](fm::GpuTextFeeder& F, int d, u64 ids, u64 vals, long long cap) {
+             F.resize_ids(d, P<int>(ids), P<float>(vals), static_cast<size_t>(cap));
+           },
+           py::arg("slot"), py::arg("ids"), py::arg("vals"), py::arg("cap"))
+      .def("resizes", &fm::GpuTextFeeder::resizes)
       .def("release", [](fm::GpuTextFeeder& F, int d, u64 stream) { F.release(d, S(stream)); }, py::arg("slot"),
            py::arg("stream"))
       .def("queued", &fm::GpuTextFeeder::queued)

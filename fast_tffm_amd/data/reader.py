@@ -249,18 +249,20 @@ class NativeTextReader:
         self.gpu = torch.device(gpu_parse) if gpu_parse is not None else None
         if self.gpu is not None and self.gpu.type != "cuda":
             self.gpu = None
-        self.fallbacks = 0
+        self.fallbacks = self.resizes = 0
         # feed_device (CPU parser, text files): the C++ feeder copies each parsed batch to this
         # device from its own thread, so batches come out on the device like the tokenizer's
-        self.feed = None
-        if feed_device is not None and not self.binary and self.gpu is None:
-            fd = torch.device(feed_device)
-            self.feed = fd if fd.type == "cuda" else None
         self.dds = None
         if device_cache is not None and self.binary and torch.device(device_cache).type == "cuda":
             from .device_cache import DeviceDataset
 
             self.dds = DeviceDataset(self.args["files"], device_cache, int(vocab_size), bool(hash_feature_id))
+        # (binary caches assembled on the host take the feeder too: the loader's CSR rows are
+        # copied to the device by the feeder thread, no Python producer thread)
+        self.feed = None
+        if feed_device is not None and self.gpu is None and self.dds is None:
+            fd = torch.device(feed_device)
+            self.feed = fd if fd.type == "cuda" else None
 
     def close(self) -> None:
         """Stop the native producer threads (feeder, loader); the iterator ends."""
@@ -284,6 +286,8 @@ class NativeTextReader:
         """Bytes of one batch slot: twice the batch's estimated text bytes (the longest average
         line over the heads of the files: files of one run can differ, e.g. with and without
         values)."""
+        if getattr(self, "_slot_bytes", None) is None and self.binary:
+            self._slot_bytes = 1  # (no text: the ids capacity comes from the caches' max_feats)
         if getattr(self, "_slot_bytes", None) is None:
             B = self.args["batch_size"]
             est = []
@@ -372,7 +376,7 @@ class NativeTextReader:
         tokenizer's CSR out (ids / values sized for the densest possible batch: a token takes >= 2
         bytes), its counts / status / scan workspace."""
         dev, B, nb = self._feed_dev, self.args["batch_size"], self._slot_bytes
-        cap = nb // 2 + B + 1
+        cap = B * _bin_max_feats(self.args["files"]) + 1 if self.binary else nb // 2 + B + 1
         if self.gpu is None:
             nb = 1  # (parse mode: no raw bytes on the device)
         i32 = dict(dtype=torch.int32, device=dev)
@@ -400,7 +404,7 @@ class NativeTextReader:
         slots = self._raw_slots() if raw else []
         self._estimate_slot_bytes()
         L = native.cpu().TextLoader(start_epoch=self.state.epoch, skip_batches=self.state.batches_in_epoch,
-                                    raw=raw, binary=False, rows=False, raw_slots=slots, **self.args)
+                                    raw=raw, binary=self.binary, rows=False, raw_slots=slots, **self.args)
         self._loader = L
         dev = self.gpu if raw else self.feed
         if dev.index is None:
@@ -432,6 +436,16 @@ class NativeTextReader:
                     continue
                 if r[0] == "error":
                     raise (native.cpu().ParseError if r[1] else RuntimeError)(r[2])
+                if r[0] == "resize":  # a batch denser than the slot estimate: larger ids / vals
+                    _, d, need = r
+                    cap = int(need * 1.25) + 1024
+                    torch.cuda.synchronize(dev)  # (the steps that read the slot's old buffers have run)
+                    with torch.cuda.device(dev):
+                        dslots[d] = dict(dslots[d], ids=torch.empty(cap, dtype=torch.int32, device=dev),
+                                         vals=torch.empty(cap, dtype=torch.float32, device=dev))
+                    torch.cuda.synchronize(dev)
+                    F.resize_ids(d, dslots[d]["ids"].data_ptr(), dslots[d]["vals"].data_ptr(), cap)
+                    continue
                 d, n, nnz, mf, has_vals, weighted, epoch, count = r
                 t = dslots[d]
                 b = Batch(t["labels"][:n], t["offsets"][: n + 1], t["ids"][:nnz], t["vals"][:nnz] if has_vals else None,
@@ -440,10 +454,9 @@ class NativeTextReader:
                 self.state.epoch, self.state.batches_in_epoch = int(epoch), int(count)
                 b.reader_pos = (int(epoch), int(count))
                 yield b
-            self.fallbacks = int(F.fallbacks())
             self.state.epoch, self.state.batches_in_epoch = self.num_epochs, 0
         finally:
-            self.fallbacks = int(F.fallbacks())
+            self.fallbacks, self.resizes = int(F.fallbacks()), int(F.resizes())
             F.close()
             L.close()
 
@@ -532,6 +545,19 @@ class NativeTextReader:
         self.state.epoch, self.state.batches_in_epoch = epoch, count
         b.reader_pos = (epoch, count)
         return b
+
+
+def _bin_max_feats(files: list[str]) -> int:
+    """Largest example (features) over the .fmb caches' headers (csrc/cpu/bincsr.h: i32 max_feats at
+    byte 40): a feeder slot of B times it holds any batch."""
+    import struct
+
+    m = 1
+    for f in files:
+        with open(f, "rb") as fh:
+            head = fh.read(64)
+        m = max(m, struct.unpack_from("<i", head, 40)[0])
+    return m
 
 
 def _feeder_available() -> bool:

@@ -129,3 +129,25 @@ def test_reader_gpu_parse_fallback_reports_errors(tmp_path):
     p.write_text("1 2 3\n1 2:xyz\n")
     with pytest.raises(ValueError, match="Invalid feature value"):
         list(NativeTextReader([str(p)], None, 4, vocab_size=10, gpu_parse="cuda"))
+
+
+@pytest.mark.parametrize("mode", ["feed_device", "gpu_parse"])
+def test_feeder_grows_slots_for_denser_batches(tmp_path, mode):
+    """The feeder's device slots are sized from the files' heads; batches far denser than that
+    (long lines after short ones) make it ask for larger ids / vals buffers instead of failing
+    (ADVICE r3), and the batches still equal the host reader's."""
+    p = tmp_path / "mixed"
+    with open(p, "w") as f:
+        for i in range(20000):
+            f.write(f"{i % 2} {i % 97}\n")
+        for i in range(600):
+            f.write(f"{i % 2} " + " ".join(str((i * 7 + j) % 50000) for j in range(100)) + "\n")
+    kw = dict(vocab_size=100_000, num_epochs=1, seed=5, parse_threads=2)
+    host = list(NativeTextReader([str(p)], None, 256, **kw))
+    r = NativeTextReader([str(p)], None, 256, **{mode: "cuda"}, **kw)
+    dev = list(r)
+    assert r.resizes > 0 and len(host) == len(dev)
+    for a, b in zip(host, dev):
+        assert a.reader_pos == b.reader_pos and a.nnz == b.nnz and b.ids.is_cuda
+        for x, y in ((a.labels, b.labels), (a.offsets, b.offsets), (a.ids, b.ids)):
+            assert torch.equal(x, y.cpu())

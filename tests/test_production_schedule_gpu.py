@@ -9,7 +9,7 @@ pool of batches that they cycle through (the 3-slot rotation wraps several times
 
 * the local step with the depth-2 lookahead that the headline bench runs
   (``train_step(b, next, next2)``, models/fm.py ``_local_lookahead_step``) against plain steps,
-  bit for bit;
+  bit for bit, at B=4096 and at the bench's B=131072;
 * the row-sharded step at world 1 with the depth-2 plan pipeline and early row exchange (self rows
   off, so the early exchange, dirty scan and patch really run) against the local step;
 * the dense all-reduce data-parallel step (config 3) with its lookahead dedup against the local step.
@@ -39,10 +39,10 @@ def production(monkeypatch):
     K.set_debug_checks(was)
 
 
-def _cfg(V, k=64, dtype=torch.float32, mode="local", **kw):
+def _cfg(V, k=64, dtype=torch.float32, mode="local", batch_size=4096, **kw):
     return FMConfig(vocabulary_size=V, factor_num=k, loss_type="logistic", init_value_range=0.05, seed=3,
-                    opt=K.OptConfig("adagrad", lr=0.05), batch_size=4096, factor_lambda=0.01, bias_lambda=0.01,
-                    dtype=dtype, mode=mode, **kw)
+                    opt=K.OptConfig("adagrad", lr=0.05), batch_size=batch_size, factor_lambda=0.01,
+                    bias_lambda=0.01, dtype=dtype, mode=mode, **kw)
 
 
 def _state(m):
@@ -68,6 +68,30 @@ def test_local_depth2_lookahead_bitwise(production, k, dtype):
         assert torch.equal(x, y)
     for x, y in zip(_state(plain), _state(piped)):
         assert torch.equal(x.view(torch.uint8), y.view(torch.uint8))
+
+
+def test_local_depth2_lookahead_bitwise_bench_shape(production):
+    """The same at the headline bench's batch (B=131072, k=64 fp32 + Adagrad; 10M rows instead of
+    125M to keep two tables cheap): here the side-stream dedup of batch t+2 and the compute chain of
+    batch t really overlap (a 4096-example plan finishes long before its slot is reused)."""
+    V, B = 10_000_000, 131072
+    gen = CriteoSynth(V, device="cuda", seed=64)
+    pool = [gen.batch(B) for _ in range(POOL)]
+    plain = FactorizationMachine(_cfg(V, batch_size=B), device="cuda")
+    piped = FactorizationMachine(_cfg(V, batch_size=B), device="cuda")
+    lp, lq = [], []
+    for i in range(STEPS):
+        b = pool[i % POOL]
+        lp.append(plain.train_step(b).loss_sum)
+        lq.append(piped.train_step(b, pool[(i + 1) % POOL], pool[(i + 2) % POOL]).loss_sum)
+    torch.cuda.synchronize()
+    assert piped._lpending is not None and piped._lpending2 is not None
+    for x, y in zip(lp, lq):
+        assert torch.equal(x, y)
+    for x, y in zip(_state(plain), _state(piped)):
+        assert torch.equal(x.view(torch.uint8), y.view(torch.uint8))
+    plain.close()
+    piped.close()
 
 
 def _free_port() -> int:

@@ -53,7 +53,7 @@ def fmt(v, w=7, p=1):
 
 
 cols = ["us", "inst", "VALU%", "MFMA%", "VMEMrd/w", "vmem_lat", "L2hit%", "FETCH_MB", "fetch_x2", "DRAM_MB", "WRITE_MB",
-        "TLBmiss%", "lat_cyc", "TAbusy%", "wait%"]
+        "TLBmiss%", "lat_cyc", "TAbusy%", "wait%", "VALUi/w", "LDSbc/i"]
 print(f"{'kernel':58s} " + " ".join(f"{c:>8s}" for c in cols))
 for k, c in sorted(acc.items(), key=lambda kv: -sum(dur.get(kv[0], [0]))):
     d = sorted(dur.get(k, [0]))
@@ -84,5 +84,7 @@ for k, c in sorted(acc.items(), key=lambda kv: -sum(dur.get(kv[0], [0]))):
     lat = avg("TCP_TCC_READ_REQ_LATENCY") / max(avg("TCP_TCC_READ_REQ"), 1)
     ta = 100 * avg("TA_TA_BUSY") / (cyc * CU_NUM)
     wait = 100 * avg("SQ_WAIT_ANY") / max(avg("SQ_WAVE_CYCLES"), 1)
-    vals = [us, inst, valu, mfma, vmem, vlat, l2, fetch, 2 * fetch, dram, write, tlb, lat, ta, wait]
+    valu_i = avg("SQ_INSTS_VALU") / max(avg("SQ_WAVES"), 1)          # VALU instructions per wave
+    ldsbc = avg("SQ_LDS_BANK_CONFLICT") / max(avg("SQ_INSTS_LDS"), 1)  # conflict cycles per LDS instruction
+    vals = [us, inst, valu, mfma, vmem, vlat, l2, fetch, 2 * fetch, dram, write, tlb, lat, ta, wait, valu_i, ldsbc]
     print(f"{k:58s} " + " ".join(fmt(v, 8) for v in vals))
