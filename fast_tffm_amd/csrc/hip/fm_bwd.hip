@@ -819,6 +819,15 @@ static hipEvent_t dense_join_event() {
   return ev;
 }
 
+static int chunk_wg_per_cu(int lpr, int mode) {
+  static const int env = [] {
+    const char* e = getenv("FM_CHUNK_WG_PER_CU");
+    return e ? atoi(e) : -1;
+  }();
+  if (env >= 0) return env;
+  return mode == kBwdLocal && lpr <= 16 ? 3 : 0;
+}
+
 int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_unique, hipStream_t st,
                hipStream_t dense_st) {
   if (max_chunks <= 0) return 0;
@@ -885,12 +894,21 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   const int kind = FM_BWD_SPECIALIZE && a.mode == kBwdLocal && a.piece < 0 && lpr >= 4 && r1_bytes < (1LL << 32)
                        ? (a.sorted_x ? kChunkLocal : kChunkLocalNoX)
                        : kChunkAny;
+  // Chunk workgroups resident per CU, capped through dynamic LDS the kernel does not use (a CU holds
+  // floor(LDS / bytes) of them).  The side stream's radix-sort blocks then find LDS on every CU and
+  // the capped grid spreads over more CUs: same-box, 3 per CU took k64 fp32 0.648 -> 0.621 ms and
+  // k16 bf16 0.511 -> 0.487; 32-lane rows (k128, uncapped grid) lose (fp8 FTRL 0.887 -> 0.978)
+  // (profiles/r4/wg_per_cu_ab.txt).  An earlier build's 130-VGPR k16 kernel (3 waves / SIMD) had
+  // the same effect by accident.  FM_CHUNK_WG_PER_CU overrides (0: no cap).
+  const int wg_cu = chunk_wg_per_cu(lpr, a.mode);
+  const int chunk_static_lds = kind == kChunkAny ? (int)sizeof(int) * (2 * kMaxPieceOwners + 1) : 0;  // piece walk
+  const int chunk_lds = wg_cu > 0 ? lds_for_wg_per_cu(wg_cu, chunk_static_lds) : 0;
   if (kind == kChunkLocalNoX) {
-    FM_DISPATCH_WIDE(dtype, lpr, fm_bwd_chunk_local_nox_kernel, g1, st, a);
+    FM_DISPATCH_WIDE(dtype, lpr, fm_bwd_chunk_local_nox_kernel, g1, chunk_lds, st, a);
   } else if (kind == kChunkLocal) {
-    FM_DISPATCH_WIDE(dtype, lpr, fm_bwd_chunk_local_kernel, g1, st, a);
+    FM_DISPATCH_WIDE(dtype, lpr, fm_bwd_chunk_local_kernel, g1, chunk_lds, st, a);
   } else {
-    FM_DISPATCH(dtype, lpr, fm_bwd_chunk_kernel, g1, st, a);
+    FM_DISPATCH_SHM(dtype, lpr, fm_bwd_chunk_kernel, g1, chunk_lds, st, a);
   }
   FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, a);
   FM_DISPATCH(dtype, lpr, fm_bwd_big_kernel, 1024, st, a);

@@ -381,6 +381,19 @@ inline int lanes_per_row(int Kp, int dtype) {
   return next_pow2((Kp + epl - 1) / epl);
 }
 
+// Dynamic LDS bytes that let at most n workgroups (with `static_lds` bytes of their own) share a CU.
+inline int lds_for_wg_per_cu(int n, int static_lds) {
+  static const int cu_lds = [] {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess || v <= 0)
+      v = 160 * 1024;
+    return v;
+  }();
+  const int per = cu_lds / (n + 1) + 1024 - static_lds;  // n + 1 do not fit (margin: allocation granules)
+  return per > 0 && (per + static_lds) * n <= cu_lds ? per : 0;
+}
+
 inline int fill_grid(long long work_groups, int groups_per_block, int cap = 8192) {
   long long blocks = (work_groups + groups_per_block - 1) / groups_per_block;
   if (blocks < 1) blocks = 1;
@@ -388,45 +401,43 @@ inline int fill_grid(long long work_groups, int groups_per_block, int cap = 8192
   return (int)blocks;
 }
 
-#define FM_DISPATCH_LPR(LPR_VAL, KERNEL, TV, GRID, STREAM, ARGS)                                   \
-  switch (LPR_VAL) {                                                                                \
-    case 1: hipLaunchKernelGGL((KERNEL<1, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break;  \
-    case 2: hipLaunchKernelGGL((KERNEL<2, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break;  \
-    case 4: hipLaunchKernelGGL((KERNEL<4, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break;  \
-    case 8: hipLaunchKernelGGL((KERNEL<8, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break;  \
-    case 16: hipLaunchKernelGGL((KERNEL<16, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break; \
-    case 32: hipLaunchKernelGGL((KERNEL<32, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break; \
-    case 64: hipLaunchKernelGGL((KERNEL<64, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break; \
-    default: return -1;                                                                             \
+// SHM: dynamic LDS bytes per workgroup (0 for all but the occupancy-limited chunk kernel launch)
+#define FM_DISPATCH_LPR(LPR_VAL, KERNEL, TV, GRID, SHM, STREAM, ARGS)                                   \
+  switch (LPR_VAL) {                                                                                     \
+    case 1: hipLaunchKernelGGL((KERNEL<1, TV>), dim3(GRID), dim3(kBlock), SHM, STREAM, ARGS); break;     \
+    case 2: hipLaunchKernelGGL((KERNEL<2, TV>), dim3(GRID), dim3(kBlock), SHM, STREAM, ARGS); break;     \
+    case 4: hipLaunchKernelGGL((KERNEL<4, TV>), dim3(GRID), dim3(kBlock), SHM, STREAM, ARGS); break;     \
+    case 8: hipLaunchKernelGGL((KERNEL<8, TV>), dim3(GRID), dim3(kBlock), SHM, STREAM, ARGS); break;     \
+    case 16: hipLaunchKernelGGL((KERNEL<16, TV>), dim3(GRID), dim3(kBlock), SHM, STREAM, ARGS); break;   \
+    case 32: hipLaunchKernelGGL((KERNEL<32, TV>), dim3(GRID), dim3(kBlock), SHM, STREAM, ARGS); break;   \
+    case 64: hipLaunchKernelGGL((KERNEL<64, TV>), dim3(GRID), dim3(kBlock), SHM, STREAM, ARGS); break;   \
+    default: return -1;                                                                                  \
   }
 
 // rows of >= 4 lanes only (kernels without narrow-row instantiations)
-#define FM_DISPATCH_WIDE_LPR(LPR_VAL, KERNEL, TV, GRID, STREAM, ARGS)                              \
-  switch (LPR_VAL) {                                                                                \
-    case 4: hipLaunchKernelGGL((KERNEL<4, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break;  \
-    case 8: hipLaunchKernelGGL((KERNEL<8, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break;  \
-    case 16: hipLaunchKernelGGL((KERNEL<16, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break; \
-    case 32: hipLaunchKernelGGL((KERNEL<32, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break; \
-    case 64: hipLaunchKernelGGL((KERNEL<64, TV>), dim3(GRID), dim3(kBlock), 0, STREAM, ARGS); break; \
-    default: return -1;                                                                             \
+#define FM_DISPATCH_WIDE_LPR(LPR_VAL, KERNEL, TV, GRID, SHM, STREAM, ARGS)                              \
+  switch (LPR_VAL) {                                                                                     \
+    case 4: hipLaunchKernelGGL((KERNEL<4, TV>), dim3(GRID), dim3(kBlock), SHM, STREAM, ARGS); break;     \
+    case 8: hipLaunchKernelGGL((KERNEL<8, TV>), dim3(GRID), dim3(kBlock), SHM, STREAM, ARGS); break;     \
+    case 16: hipLaunchKernelGGL((KERNEL<16, TV>), dim3(GRID), dim3(kBlock), SHM, STREAM, ARGS); break;   \
+    case 32: hipLaunchKernelGGL((KERNEL<32, TV>), dim3(GRID), dim3(kBlock), SHM, STREAM, ARGS); break;   \
+    case 64: hipLaunchKernelGGL((KERNEL<64, TV>), dim3(GRID), dim3(kBlock), SHM, STREAM, ARGS); break;   \
+    default: return -1;                                                                                  \
   }
 
-#define FM_DISPATCH_WIDE(DTYPE, LPR_VAL, KERNEL, GRID, STREAM, ARGS)                  \
-  if ((DTYPE) == kBF16) {                                                            \
-    FM_DISPATCH_WIDE_LPR(LPR_VAL, KERNEL, __hip_bfloat16, GRID, STREAM, ARGS)        \
-  } else if ((DTYPE) == kFP8) {                                                      \
-    FM_DISPATCH_WIDE_LPR(LPR_VAL, KERNEL, fp8e4m3, GRID, STREAM, ARGS)               \
-  } else {                                                                           \
-    FM_DISPATCH_WIDE_LPR(LPR_VAL, KERNEL, float, GRID, STREAM, ARGS)                 \
+#define FM_DISPATCH_TV(DTYPE, M, LPR_VAL, KERNEL, GRID, SHM, STREAM, ARGS)   \
+  if ((DTYPE) == kBF16) {                                                   \
+    M(LPR_VAL, KERNEL, __hip_bfloat16, GRID, SHM, STREAM, ARGS)             \
+  } else if ((DTYPE) == kFP8) {                                             \
+    M(LPR_VAL, KERNEL, fp8e4m3, GRID, SHM, STREAM, ARGS)                    \
+  } else {                                                                  \
+    M(LPR_VAL, KERNEL, float, GRID, SHM, STREAM, ARGS)                      \
   }
-
-#define FM_DISPATCH(DTYPE, LPR_VAL, KERNEL, GRID, STREAM, ARGS)                       \
-  if ((DTYPE) == kBF16) {                                                            \
-    FM_DISPATCH_LPR(LPR_VAL, KERNEL, __hip_bfloat16, GRID, STREAM, ARGS)             \
-  } else if ((DTYPE) == kFP8) {                                                      \
-    FM_DISPATCH_LPR(LPR_VAL, KERNEL, fp8e4m3, GRID, STREAM, ARGS)                    \
-  } else {                                                                           \
-    FM_DISPATCH_LPR(LPR_VAL, KERNEL, float, GRID, STREAM, ARGS)                      \
-  }
+#define FM_DISPATCH_WIDE(DTYPE, LPR_VAL, KERNEL, GRID, SHM, STREAM, ARGS) \
+  FM_DISPATCH_TV(DTYPE, FM_DISPATCH_WIDE_LPR, LPR_VAL, KERNEL, GRID, SHM, STREAM, ARGS)
+#define FM_DISPATCH_SHM(DTYPE, LPR_VAL, KERNEL, GRID, SHM, STREAM, ARGS) \
+  FM_DISPATCH_TV(DTYPE, FM_DISPATCH_LPR, LPR_VAL, KERNEL, GRID, SHM, STREAM, ARGS)
+#define FM_DISPATCH(DTYPE, LPR_VAL, KERNEL, GRID, STREAM, ARGS) \
+  FM_DISPATCH_SHM(DTYPE, LPR_VAL, KERNEL, GRID, 0, STREAM, ARGS)
 
 }  // namespace fm

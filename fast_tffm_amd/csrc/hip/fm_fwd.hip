@@ -475,6 +475,8 @@ int launch_fwd(const FwdArgs& a, int dtype, int grid, hipStream_t st) {
 #undef FM_FWD_DENSE
     return (int)hipGetLastError();
   }
+  // (capping the forward's workgroups per CU through dynamic LDS, as the chunk backward does, tied
+  // on k64 fp32: profiles/r4/wg_per_cu_ab.txt)
   if (a.self.u1 > a.self.u0 || a.seg_idx || !FM_FWD_SPECIALIZE) {
     FM_DISPATCH(dtype, lpr, fm_fwd_shard_kernel, grid, st, a);
   } else {
