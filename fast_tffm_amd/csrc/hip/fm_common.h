@@ -122,6 +122,19 @@ template <> struct Frag<__hip_bfloat16> {
   }
 };
 
+// Scale of an fp8 row whose largest |value| is m: the power of two s with m / s in (224, 448] -- an
+// E8M0 exponent, as the OCP MX formats use.  fp8 keeps 3 mantissa bits at any binade, so a power of
+// two costs no precision against s = m / 448 (one binade of subnormal range at most), and it makes
+// quantising (v * (1 / s)) and dequantising (q * s) exact scalings; gfx950's scaled conversion
+// v_cvt_scalef32_pk_f32_fp8 applies only the scale's exponent, so it dequantises in the conversion.
+__host__ __device__ inline float fp8_row_scale(float m) {
+  if (!(m > 0.f)) return 1.f;
+  const float t = m / kFp8Max;
+  if (t < 1.17549435e-38f) return 1.17549435e-38f;  // (2^-126: m / s < 448 still)
+  const uint32_t b = __builtin_bit_cast(uint32_t, t);
+  return (b & 0x7fffffu) ? __builtin_bit_cast(float, (b & 0x7f800000u) + 0x00800000u) : t;
+}
+
 // 4 fp8 per lane (a 4-byte load: a K=128 row is one 32-lane instruction, the
 // same lane mapping and register footprint as fp32); values are unscaled here.
 template <> struct Frag<fp8e4m3> {
@@ -133,20 +146,29 @@ template <> struct Frag<fp8e4m3> {
     o[0] = lo[0]; o[1] = lo[1]; o[2] = hi[0]; o[3] = hi[1];
   }
   __device__ static inline void load(const fp8e4m3* p, float (&o)[4]) { cvt(*reinterpret_cast<const int*>(p), o); }
-  __device__ static inline void store(fp8e4m3* p, const float (&o)[4]) {
+  // q * s for a power-of-two row scale s (fp8_row_scale) in the conversion instruction itself
+  __device__ static inline void cvt_scaled(int u, float s, float (&o)[4]) {
+    const auto lo = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(u, s, false);
+    const auto hi = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(u, s, true);
+    o[0] = lo[0]; o[1] = lo[1]; o[2] = hi[0]; o[3] = hi[1];
+  }
+  // (store / store_sr return the 4 stored bytes: the row norm is taken from them)
+  __device__ static inline int store(fp8e4m3* p, const float (&o)[4]) {
     int u = __builtin_amdgcn_cvt_pk_fp8_f32(o[0], o[1], 0, false);
     u = __builtin_amdgcn_cvt_pk_fp8_f32(o[2], o[3], u, true);
     *reinterpret_cast<int*>(p) = u;
+    return u;
   }
   // gfx950 v_cvt_sr_fp8_f32: hardware stochastic rounding with the given random bits
-  __device__ static inline void store_sr(fp8e4m3* p, const float (&o)[4], uint32_t seed, uint32_t row,
-                                         uint32_t col) {
+  __device__ static inline int store_sr(fp8e4m3* p, const float (&o)[4], uint32_t seed, uint32_t row,
+                                        uint32_t col) {
     const uint32_t r0 = sr_hash(seed, row, col), r1 = sr_next(r0), r2 = sr_next(r1), r3 = sr_next(r2);
     int u = __builtin_amdgcn_cvt_sr_fp8_f32(o[0], (int)r0, 0, 0);
     u = __builtin_amdgcn_cvt_sr_fp8_f32(o[1], (int)r1, u, 1);
     u = __builtin_amdgcn_cvt_sr_fp8_f32(o[2], (int)r2, u, 2);
     u = __builtin_amdgcn_cvt_sr_fp8_f32(o[3], (int)r3, u, 3);
     *reinterpret_cast<int*>(p) = u;
+    return u;
   }
 };
 
@@ -276,6 +298,22 @@ __device__ inline float row_scale(const float* w, long long row, long long w_str
   return 1.f;
 }
 
+// fp8 rows keep their squared L2 norm next to [w, scale] (w_row[2], kFp8Norm): the local
+// forward's s2 and reg terms are then one scalar per occurrence (sum_j x_j^2 |v_j|^2, sum_j |v_j|^2)
+// instead of two multiply-adds per element.  The norm is a function of the stored bytes only:
+// exact squares of the unscaled values, summed in a fixed order per lane and a butterfly over the
+// row's LPR lanes, times scale^2 (a power of two: exact) -- every writer (store_row, the init /
+// refresh kernels) calls this, so they agree bitwise.  `u`: the lane's 4 stored fp8 values.
+constexpr int kFp8Norm = 2;  // word of the norm in an fp8 table's w row [w, scale, |v|^2, pad]
+template <int LPR>
+__device__ inline float fp8_norm2(int u, float s, bool tact) {
+  float q[4];
+  Frag<fp8e4m3>::cvt(u, q);
+  float p = tact ? __fmaf_rn(q[0], q[0], __fmaf_rn(q[1], q[1], __fmaf_rn(q[2], q[2], q[3] * q[3]))) : 0.f;
+  p = group_sum<LPR>(p);
+  return p * (s * s);
+}
+
 // Store this lane's EPL fp32 values of a row (every lane of the LPR group must
 // call: scaled dtypes reduce the row's max |v| over the group first).
 template <int LPR, typename TV>
@@ -288,16 +326,18 @@ __device__ inline void store_row(TV* lane_ptr, const float (&o)[Frag<TV>::N], fl
 #pragma unroll
     for (int k = 0; k < F::N; ++k) m = fmaxf(m, fabsf(o[k]));
     m = group_max<LPR>(m);
-    const float s = m > 0.f ? m / kFp8Max : 1.f;
-    const float inv = 1.f / s;
+    const float s = fp8_row_scale(m);
+    const float inv = 1.f / s;  // (exact: s is a power of two)
     float q[F::N];
 #pragma unroll
     for (int k = 0; k < F::N; ++k) q[k] = fminf(fmaxf(o[k] * inv, -kFp8Max), kFp8Max);
-    if (tact) {
-      if (sr_seed) F::store_sr(lane_ptr, q, sr_seed, (uint32_t)row, col);
-      else F::store(lane_ptr, q);
+    int u = 0;
+    if (tact) u = sr_seed ? F::store_sr(lane_ptr, q, sr_seed, (uint32_t)row, col) : F::store(lane_ptr, q);
+    const float n2 = fp8_norm2<LPR>(u, s, tact);
+    if (t == 0) {
+      w[row * w_stride + 1] = s;
+      w[row * w_stride + kFp8Norm] = n2;
     }
-    if (t == 0) w[row * w_stride + 1] = s;
   } else {
     if (tact) {
       if (sr_seed) F::store_sr(lane_ptr, o, sr_seed, (uint32_t)row, col);

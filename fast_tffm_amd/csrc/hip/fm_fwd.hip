@@ -219,17 +219,26 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
 #pragma unroll
     for (int k = 0; k < EPL; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
     float lin = 0.f, rv = 0.f, rw = 0.f;
+    // local fp8 (kNorm): s2 = sum_j x_j^2 |v_j|^2 from the rows' stored norms, one occurrence per lane
+    constexpr bool kNorm = F::kScaled && !SH;
+    float s2n = 0.f;
     for (int base = s; base < e; base += kWave) {
       const int m = min(kWave, e - base);
       int my_row = 0, my_seg = 0;
-      float my_x = 0.f, my_w = 0.f, my_s = 1.f;
+      float my_x = 0.f, my_w = 0.f, my_s = 1.f, my_n2 = 0.f;
       if (kPrefetch && base == s) {
         my_row = p_row;
         my_x = p_x;
       } else {
         pairs(base, m, my_row, my_x);
       }
-      if (!SH && lane < m) {
+      if (kNorm && lane < m) {  // [w, scale, |v|^2, pad]: one 16-byte load (w_stride 4, host-checked)
+        my_seg = my_row;
+        const float4 wr = *reinterpret_cast<const float4*>(a.w + (uint64_t)(uint32_t)my_row * 4u);
+        my_w = wr.x;
+        my_s = wr.y;
+        my_n2 = wr.z;
+      } else if (!SH && lane < m) {
         my_seg = my_row;
         my_w = a.w[(long long)my_row * a.w_stride];
         my_s = row_scale<TV>(a.w, my_row, a.w_stride);
@@ -265,6 +274,10 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
       }
       for (int q = 0; q < m; q += G * UNR) {
         float fr[UNR][EPL], fx[UNR], fs[UNR];
+        // (local fp8: the raw 4-byte fragment, converted with its power-of-two row scale once that
+        // has arrived: v_cvt_scalef32_pk_f32_fp8, no per-element scale multiply)
+        constexpr bool kRaw = F::kScaled && !SH;
+        int fraw[kRaw ? UNR : 1];
         // Issue every row load of the round before the first use.  Loads are
         // unconditional (slots past the example re-read a valid row of it and are
         // masked to zero afterwards), so hipcc keeps all UNR loads in flight.
@@ -288,7 +301,9 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
             const int row = __builtin_amdgcn_ds_bpermute(fb, my_row);
             const float x = __int_as_float(__builtin_amdgcn_ds_bpermute(fb, __float_as_int(my_x)));
             fx[u] = f < m ? x : 0.f;
-            F::load(reinterpret_cast<const TV*>(vbytes + (uint64_t)(uint32_t)row * vsb), fr[u]);
+            const char* rp = vbytes + (uint64_t)(uint32_t)row * vsb;
+            if constexpr (kRaw) fraw[u] = *reinterpret_cast<const int*>(rp);
+            else F::load(reinterpret_cast<const TV*>(rp), fr[u]);
             if constexpr (F::kScaled) fs[u] = __int_as_float(__builtin_amdgcn_ds_bpermute(fb, __float_as_int(my_s)));
           }
         }
@@ -298,7 +313,9 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
           // (folding the fp8 row scale into the occurrence's x instead of every element, with the
           // reg term as a per-occurrence sum times scale^2 -- fewer VALU ops -- made the k128 fp8
           // FTRL step slower, 0.888 -> 1.014 ms same-box: profiles/r4/specialize_ab.txt)
-          if constexpr (F::kScaled) {
+          if constexpr (kRaw) {
+            F::cvt_scaled(fraw[u], fs[u], fv);
+          } else if constexpr (F::kScaled) {
 #pragma unroll
             for (int k = 0; k < EPL; ++k) fv[k] *= fs[u];
           }
@@ -307,9 +324,9 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
           for (int k = 0; k < EPL; ++k) {
             const float xv = xm * fv[k];
             s1[k] += xv;
-            s2[k] += xv * xv;
+            if constexpr (!kNorm) s2[k] += xv * xv;
           }
-          if (want_reg) {
+          if (!kNorm && want_reg) {
             const float ok = (q + u * G + g) < m ? 1.f : 0.f;
 #pragma unroll
             for (int k = 0; k < EPL; ++k) rv += ok * tmask * fv[k] * fv[k];
@@ -319,6 +336,10 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
       // (w is used after the row loads were issued: its load latency hides under theirs)
       lin += my_x * my_w;
       if (want_reg) rw += my_w * my_w;
+      if constexpr (kNorm) {  // (lanes past the example: x = 0, |v|^2 = 0)
+        s2n += my_x * my_x * my_n2;
+        if (want_reg) rv += my_n2;
+      }
     }
     if constexpr (DENSE) {  // flush this example's dense-row counts: 4 per lane, one coalesced row
       // (LDS instructions of one wave complete in issue order, and the compiler keeps these
@@ -340,6 +361,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
       part += s1[k] * s1[k] - s2[k];
     }
     part = group_sum<LPR>(part);
+    if constexpr (kNorm) part -= group_sum<kWave>(s2n);
     lin = group_sum<kWave>(lin);
     const float pred = lin + 0.5f * part + (a.bias ? a.bias[0] : 0.f);
     if (a.r1 != nullptr && g == 0 && tact) store_r1<TV, EPL>(a.r1, (long long)i * a.Kp + t * EPL, s1);
@@ -477,7 +499,9 @@ int launch_fwd(const FwdArgs& a, int dtype, int grid, hipStream_t st) {
   }
   // (capping the forward's workgroups per CU through dynamic LDS, as the chunk backward does, tied
   // on k64 fp32: profiles/r4/wg_per_cu_ab.txt)
-  if (a.self.u1 > a.self.u0 || a.seg_idx || !FM_FWD_SPECIALIZE) {
+  // (the local fp8 forward reads [w, scale, |v|^2, pad] rows: Table's layout, w_stride 4)
+  const bool fp8_norm_ok = dtype != kFP8 || a.w_stride == 4;
+  if (a.self.u1 > a.self.u0 || a.seg_idx || !FM_FWD_SPECIALIZE || !fp8_norm_ok) {
     FM_DISPATCH(dtype, lpr, fm_fwd_shard_kernel, grid, st, a);
   } else {
     FM_DISPATCH(dtype, lpr, fm_fwd_kernel, grid, st, a);

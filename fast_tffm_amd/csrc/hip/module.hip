@@ -363,6 +363,15 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("v"), py::arg("v_stride"), py::arg("w"), py::arg("w_stride"), py::arg("rows"), py::arg("K"),
       py::arg("Kp"), py::arg("dtype"), py::arg("gid_mul"), py::arg("gid_add"), py::arg("seed"), py::arg("range"),
       py::arg("stream"));
+  m.def(
+      "fp8_row_norms",
+      [](u64 v, long long v_stride, u64 w, long long w_stride, long long rows, int Kp, u64 stream) {
+        check(fm::launch_fp8_norms(P<const uint8_t>(v), v_stride, P<float>(w), w_stride, rows, Kp, S(stream)),
+              "fp8_row_norms");
+      },
+      py::arg("v"), py::arg("v_stride"), py::arg("w"), py::arg("w_stride"), py::arg("rows"), py::arg("Kp"),
+      py::arg("stream"));
+  m.attr("FP8_NORM_COL") = fm::kFp8Norm;
 
   m.def(
       "owner_counts",

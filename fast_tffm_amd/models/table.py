@@ -12,8 +12,8 @@ storage is HBM-friendly rather than reference-shaped:
 * ``v``   [rows, Kp]  fp32, bf16 or fp8 (OCP e4m3, GPU only), Kp = K padded to
   whole lanes (pads are 0);
 * ``w``   [rows]      fp32 (linear weight, kept separate so v rows stay aligned);
-  fp8 tables store [w, scale] pairs (``wx`` [rows, 2], ``w`` = wx[:, 0]) so the
-  row's dequantisation scale arrives with w;
+  fp8 tables store [w, scale, |v|^2, pad] rows (``wx`` [rows, 4], ``w`` = wx[:, 0]) so the
+  row's dequantisation scale (a power of two) and squared norm arrive with w;
 * ``s0v``/``s0w``     optimizer slot 0 (Adagrad accumulator / FTRL n);
 * ``s1v``/``s1w``     optimizer slot 1 (FTRL z);
   fp32, except ``s0v`` / ``s1v`` of fp8 tables: bf16 with stochastic rounding
@@ -66,14 +66,17 @@ class FMTable:
             raise ValueError("fp8 tables run on the GPU kernels only")
         self.v = torch.zeros((self.rows, self.Kp), dtype=dtype, device=dev)
         if self.fp8:
-            self.wx = torch.zeros((self.rows, 2), dtype=torch.float32, device=dev)
+            # [w, scale, |v|^2, pad] per row: the kernels read the scale at w[row * 4 + 1] and the
+            # squared norm of the dequantised row (hip/fm_common.h fp8_norm2) at w[row * 4 + 2]
+            self.wx = torch.zeros((self.rows, 4), dtype=torch.float32, device=dev)
             self.wx[:, 1] = 1.0
-            self.w = self.wx[:, 0]          # stride 2: the kernels read the scale at w[row * 2 + 1]
+            self.w = self.wx[:, 0]
             self.scale = self.wx[:, 1]
+            self.norm2 = self.wx[:, 2]
         else:
             self.wx = None
             self.w = torch.zeros(self.rows, dtype=torch.float32, device=dev)
-            self.scale = None
+            self.scale = self.norm2 = None
         acc0 = float(self.opt.initial_accumulator)
         n_state = max(1, self.opt.n_state)  # kernels always address slot 0
         sdt = self.state_dtype = K.state_dtype(dtype)
@@ -117,6 +120,31 @@ class FMTable:
             self.w[real:].zero_()
             if self.scale is not None:
                 self.scale[real:] = 1.0
+                self.norm2[real:] = 0.0
+
+    def adopt_fp8_rows(self) -> None:
+        """After fp8 rows and scales were written as stored bytes (checkpoint restore): rows whose
+        scale is not a power of two (written before scales were; the scaled conversion in the
+        forward applies only a scale's exponent) are re-quantised from their dequantised values,
+        then every row's norm is recomputed."""
+        if not self.fp8:
+            return
+        mant, _ = torch.frexp(self.scale)
+        bad = torch.nonzero(mant != 0.5).flatten()
+        if bad.numel():
+            vals = self.dense_v(bad)[:, : self.K]
+            self.set_v(bad, vals)  # (refreshes the norms)
+        else:
+            self.refresh_norms()
+
+    def refresh_norms(self) -> None:
+        """Recompute the fp8 rows' |v|^2 column from the stored rows and scales (after writing v or
+        the scales from the host side; the kernels keep it current themselves)."""
+        if not self.fp8:
+            return
+        native.hip().fp8_row_norms(v=self.v.data_ptr(), v_stride=self.v.stride(0), w=self.wx.data_ptr(),
+                                   w_stride=self.wx.stride(0), rows=self.rows, Kp=self.Kp,
+                                   stream=torch.cuda.current_stream(self.device).cuda_stream)
 
     def global_ids(self) -> torch.Tensor:
         return torch.arange(self.rows, device=self.device, dtype=torch.int64) * self.world + self.rank
@@ -157,6 +185,7 @@ class FMTable:
                 self.v[:n], self.scale[:n] = q, s
             else:
                 self.v[local_rows], self.scale[local_rows] = q, s
+            self.refresh_norms()
             return
         vals = vals.to(self.device, self.dtype)
         if local_rows is None:

@@ -70,12 +70,23 @@ def r1_dtype(table_dtype: torch.dtype) -> torch.dtype:
     return torch.bfloat16 if table_dtype == FP8 else torch.float32
 
 
+def fp8_row_scale(m: torch.Tensor) -> torch.Tensor:
+    """Row scales of fp8 rows with largest |value| m (hip/fm_common.h fp8_row_scale): the power of
+    two s with m / s in (224, 448]; 1 for empty rows."""
+    m = m.float()
+    t = torch.clamp(m / FP8_MAX, min=2.0 ** -126)
+    mant, e = torch.frexp(t)  # t = mant * 2^e, mant in [0.5, 1)
+    s = torch.where(mant == 0.5, t, torch.ldexp(torch.ones_like(t), e))
+    return torch.where(m > 0, s, torch.ones_like(m))
+
+
 def quantize_fp8_rows(vals: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
-    """Per-row fp8 quantisation (the kernels' store_row): scale = max|v| / 448, q = rne(v / scale)."""
+    """Per-row fp8 quantisation (the kernels' store_row): scale = fp8_row_scale(max|v|) (a power of
+    two), q = rne(v / scale)."""
     v = vals.float()
     m = v.abs().amax(dim=1) if v.shape[1] else torch.zeros(v.shape[0], device=v.device)
-    s = torch.where(m > 0, m / FP8_MAX, torch.ones_like(m))
-    q = (v / s[:, None]).clamp(-FP8_MAX, FP8_MAX).to(FP8)
+    s = fp8_row_scale(m)
+    q = (v * (1.0 / s)[:, None]).clamp(-FP8_MAX, FP8_MAX).to(FP8)
     return q, s
 
 

@@ -92,3 +92,47 @@ def test_fp8_checkpoint_round_trip_is_exact(tmp_path):
     m3 = _model(3000, 32, torch.float32)
     ckpt.restore_checkpoint(m3, path)
     torch.testing.assert_close(m3.table.reference_rows(), m.table.reference_rows())
+
+
+def test_fp8_row_norms_track_stored_rows():
+    """Every fp8 writer keeps [w, scale, |v|^2]: power-of-two scales, and the norm column equals the
+    stored rows' squared norm -- bitwise the refresh kernel's (the same reduction)."""
+    V = 6000
+    gen = CriteoSynth(V, device="cuda", seed=12)
+    opt = K.OptConfig("ftrl", lr=0.05, l1=0.001, l2=0.001, beta=1.0, initial_accumulator=0.1)
+    m = _model(V, 128, FP8, opt)
+    t = m.table
+    init_norm = t.norm2.clone()
+    for _ in range(3):
+        m.train_step(gen.batch(2048))
+    torch.cuda.synchronize()
+    mant, _ = torch.frexp(t.scale)
+    assert bool((mant == 0.5).all())
+    ref = (t.dense_v().double() ** 2).sum(1)
+    torch.testing.assert_close(t.norm2.double(), ref, rtol=1e-6, atol=1e-12)
+    assert not torch.equal(t.norm2, init_norm)  # (updated rows changed theirs)
+    kept = t.norm2.clone()
+    t.refresh_norms()
+    assert torch.equal(t.norm2, kept)
+
+
+def test_fp8_rows_with_free_scales_are_requantised():
+    """Rows restored with scales that are not powers of two (a checkpoint of an older build; the
+    restore calls Table.adopt_fp8_rows) are re-quantised from their dequantised values: the
+    forward's scaled conversion reads only a scale's exponent."""
+    m = _model(3000, 32, FP8)
+    t = m.table
+    vals = t.dense_v()[:, : t.K].clone()
+    mx = vals.abs().amax(1)
+    s = torch.where(mx > 0, mx / K.FP8_MAX, torch.ones_like(mx))  # the older rule: max / 448
+    q = torch.zeros(t.v.shape, dtype=torch.float32, device=t.v.device)
+    q[:, : t.K] = vals / s[:, None]
+    t.v.copy_(q.clamp(-K.FP8_MAX, K.FP8_MAX).to(FP8))
+    t.scale.copy_(s)
+    before = t.dense_v().clone()
+    t.adopt_fp8_rows()
+    mant, _ = torch.frexp(t.scale)
+    assert bool((mant == 0.5).all())
+    err = (t.dense_v() - before).abs()
+    assert bool((err <= 16.0 * t.scale[:, None] + 1e-12).all())
+    torch.testing.assert_close(t.norm2.double(), (t.dense_v().double() ** 2).sum(1), rtol=1e-6, atol=1e-12)

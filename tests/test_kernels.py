@@ -208,3 +208,20 @@ def test_seg_index_sizing_and_lookup_contract():
         lo, hi = idx[b], idx[b + 1]
         seg = np.arange(U)
         assert bool(((seg >= lo) & (seg < hi)).all())
+
+
+def test_fp8_row_scale_is_power_of_two():
+    """quantize_fp8_rows (the kernels' store_row rule): s = the power of two with max|v| / s in
+    (224, 448]; 1 for empty rows; the quantised row reproduces v within half an e4m3 step."""
+    g = torch.Generator().manual_seed(3)
+    v = torch.randn(257, 40, generator=g) * torch.logspace(-6, 3, 257).unsqueeze(1)
+    v[5] = 0.0
+    v[6, :] = 0.0
+    v[6, 3] = 448.0 * 2.0 ** -10  # exactly a power of two times 448: m / s == 448
+    q, s = K.quantize_fp8_rows(v)
+    mant, _ = torch.frexp(s)
+    assert bool((mant == 0.5).all()) and float(s[5]) == 1.0 and float(s[6]) == 2.0 ** -10
+    top = (v.abs().amax(1) / s)[v.abs().amax(1) > 0]
+    assert bool((top > 224.0).all() and (top <= 448.0).all())
+    err = (q.float() * s[:, None] - v).abs()
+    assert bool((err <= 16.0 * s[:, None]).all())
