@@ -10,7 +10,7 @@ run() {  # preset tag dir variant
   (cd $3 && FM_HIP_VARIANT=$4 timeout -k 10 200 python bench.py --preset $1 --steps 40 --warmup 8 > $OUT/b_$1_$2.json 2> $OUT/b_$1_$2.err) || { echo "bench $1 $2 failed"; tail -20 $OUT/b_$1_$2.err; return 1; }
   echo "$1 $2: $(grep ms/step $OUT/b_$1_$2.err)"
 }
-for P in k16_bf16 k64; do
+for P in k16_bf16 k128_ftrl k64; do
   for rep in 1 2 3; do
     run $P head $R/ab/head "" || exit 1
     run $P new $R "" || exit 1
