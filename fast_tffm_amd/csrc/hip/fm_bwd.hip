@@ -844,10 +844,12 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   // blocks beat the 8192 fill cap by 2.5-3% (k64 fp32 0.677-0.685 -> 0.661-0.662 ms), 4-lane
   // rows (k=16 bf16) 512-576 by 5.5% (0.519-0.522 -> 0.491-0.495 ms); for 32-lane rows (k=128)
   // every cap tried was slower.  The local step only: the row-sharded step at world 1 runs
-  // steadiest without a cap (0.701-0.702 ms vs 0.68-0.73 with 3840; chunk_grid_ab.txt).
+  // steadiest without a cap (0.701-0.702 ms vs 0.68-0.73 with 3840; chunk_grid_ab.txt).  Re-swept with
+  // 3 workgroups per CU (profiles/r4/chunk_grid_wg3.txt): 16-lane rows 3072 (0.616-0.618 ms) over 3840
+  // (0.620-0.624), 2304 / 5120 slower; 4-lane rows 512 still best; 32-lane rows uncapped.
   // FM_CHUNK_GRID: > 0 overrides, < 0 disables.
   const int cap = a.chunk_grid != 0 ? a.chunk_grid
-                  : a.mode != kBwdLocal ? -1 : (lpr == 16 ? 3840 : lpr == 4 ? 512 : -1);
+                  : a.mode != kBwdLocal ? -1 : (lpr == 16 ? 3072 : lpr == 4 ? 512 : -1);
   if (cap > 0 && g1 > cap) g1 = (cap + 7) / 8 * 8;
   const bool dense = a.dense_list && a.dense_part && a.dense_A && a.piece < 0;
   if (a.piece >= 0 && a.n_owners > kMaxPieceOwners) return -6;
