@@ -253,11 +253,44 @@ void api_done(void* h, FmRawView* v) {
     } catch (const std::exception&) {
     }
   }
+  L->recycle(*b);
   delete b;
   v->owner = nullptr;
 }
 
 }  // namespace
+
+namespace {
+constexpr size_t kPoolMax = 24;  // buffers of each element type kept for reuse
+}
+
+void TextLoader::recycle(LoadedBatch& b) {
+  std::lock_guard<std::mutex> lk(pool_mu_);
+  for (uvector<int32_t>* v : {&b.offsets, &b.ids})
+    if (v->capacity() && pool_i32_.size() < kPoolMax) pool_i32_.push_back(std::move(*v));
+  for (uvector<float>* v : {&b.labels, &b.vals, &b.weights})
+    if (v->capacity() && pool_f32_.size() < kPoolMax) pool_f32_.push_back(std::move(*v));
+}
+
+template <class T>
+void TextLoader::reuse(uvector<T>& v) {
+  std::lock_guard<std::mutex> lk(pool_mu_);
+  auto& pool = [this]() -> std::vector<uvector<T>>& {
+    if constexpr (std::is_same<T, int32_t>::value) return pool_i32_;
+    else return pool_f32_;
+  }();
+  if (pool.empty()) return;
+  size_t best = 0;  // the largest buffer: batches are about the same size
+  for (size_t i = 1; i < pool.size(); ++i)
+    if (pool[i].capacity() > pool[best].capacity()) best = i;
+  if (pool[best].capacity() <= v.capacity()) return;
+  v.swap(pool[best]);
+  v.clear();
+  pool[best] = std::move(pool.back());
+  pool.pop_back();
+}
+template void TextLoader::reuse<int32_t>(uvector<int32_t>&);
+template void TextLoader::reuse<float>(uvector<float>&);
 
 int TextLoader::api_parse(void* h, const FmRawView* v, FmParsedOut* out, char* err, int errlen) {
   TextLoader* L = static_cast<TextLoader*>(h);
@@ -466,10 +499,13 @@ void TextLoader::run() {
           draw(bwindow, head, n, o_.shuffle, rng, bchosen);
           if (count <= skip) return true;
           LoadedBatch b;
-          if (o_.rows)
+          if (o_.rows) {
             emit_rows(bchosen, bs, b);
-          else
+          } else {
+            reuse(b.labels); reuse(b.offsets); reuse(b.ids); reuse(b.vals);
+            if (weighted) reuse(b.weights);
             assemble_binary(bchosen, bs, weighted, o_.vocab_size, o_.threads, b);
+          }
           b.epoch = epoch;
           b.count = count;
           return push(std::move(b));
@@ -583,6 +619,7 @@ void TextLoader::run() {
           ptrs[i] = rl[i].p;
           lens[i] = rl[i].len;
         }
+        reuse(csr.labels); reuse(csr.offsets); reuse(csr.ids); reuse(csr.vals);
         parse_lines32(ptrs.data(), lens.data(), n, o_.vocab_size, o_.hash_feature_id, o_.threads, csr, &pws);
         b.labels = std::move(csr.labels);
         b.offsets = std::move(csr.offsets);
@@ -595,6 +632,7 @@ void TextLoader::run() {
             wptrs[i] = rw[i].p;
             wlens[i] = rw[i].len;
           }
+          reuse(b.weights);
           b.weights.resize(n);
           parse_floats(wptrs.data(), wlens.data(), n, b.weights.data(), o_.threads);
         }

@@ -28,6 +28,12 @@ py::array_t<T> to_numpy(std::vector<T>&& v) {
   py::capsule owner(heap, [](void* p) { delete static_cast<std::vector<T>*>(p); });
   return py::array_t<T>({static_cast<py::ssize_t>(heap->size())}, {sizeof(T)}, heap->data(), owner);
 }
+template <class T>
+py::array_t<T> to_numpy(fm::uvector<T>&& v) {
+  auto* heap = new fm::uvector<T>(std::move(v));
+  py::capsule owner(heap, [](void* p) { delete static_cast<fm::uvector<T>*>(p); });
+  return py::array_t<T>({static_cast<py::ssize_t>(heap->size())}, {sizeof(T)}, heap->data(), owner);
+}
 
 // Collect (ptr, len) spans from a list of str/bytes, stripping one trailing
 // "\n" (and a preceding "\r") like TF's TextLineReader.

@@ -18,8 +18,11 @@
 // order, so the output is identical to a sequential parse.
 #pragma once
 #include <cstdint>
+#include <memory>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 namespace fm {
@@ -54,13 +57,36 @@ struct ParseWorkspace {
 void parse_lines(const char* const* ptrs, const size_t* lens, size_t n, int64_t vocab_size,
                  bool hash_feature_id, int threads, CsrBatch& out, ParseWorkspace* ws = nullptr);
 
+// Allocator whose resize() leaves new elements default-initialised (uninitialised for scalars): a
+// batch's CSR arrays are sized once and then written in parallel, and value-initialising them --
+// a serial zero-fill that also took every first-touch page fault of a fresh 13 MB batch -- was a
+// large share of the loader's per-batch host time (profiles/r4/e2e.txt).
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind { using other = NoInitAlloc<U>; };
+  NoInitAlloc() noexcept = default;
+  template <class U>
+  NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+  template <class U>
+  void construct(U* p) noexcept(std::is_nothrow_default_constructible<U>::value) {
+    ::new (static_cast<void*>(p)) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+  }
+};
+template <class T>
+using uvector = std::vector<T, NoInitAlloc<T>>;
+
 // int32 CSR of a batch (the loader's and the device's layout): labels [n], offsets [n + 1],
 // ids / vals [nnz] (vals empty when every value is 1), max features per line.
 struct Csr32 {
-  std::vector<float> labels;
-  std::vector<int32_t> offsets;
-  std::vector<int32_t> ids;
-  std::vector<float> vals;
+  uvector<float> labels;
+  uvector<int32_t> offsets;
+  uvector<int32_t> ids;
+  uvector<float> vals;
   int max_feats = 0;
   bool has_vals = false;
 };

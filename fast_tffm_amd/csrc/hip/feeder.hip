@@ -19,6 +19,7 @@
 //     the heads of the files) is not an error: the thread asks the consumer for larger buffers
 //     (next() -> -4, resize_ids) and waits, holding the batch, until they arrive.
 // The loader crosses into this module only as a table of C function pointers (loader_api.h).
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -168,6 +169,13 @@ class GpuTextFeeder {
       (void)hipStreamDestroy(st_);
       st_ = nullptr;
     }
+    for (int i = 0; i < 2; ++i) {
+      if (pin_[i]) (void)hipHostFree(pin_[i]);
+      if (pin_ev_[i]) (void)hipEventDestroy(pin_ev_[i]);
+      pin_[i] = nullptr;
+      pin_ev_[i] = nullptr;
+      pin_cap_[i] = 0;
+    }
     for (FeederSlot& s : slots_) {
       if (s.ready) (void)hipEventDestroy(s.ready);
       if (s.freed) (void)hipEventDestroy(s.freed);
@@ -224,6 +232,51 @@ class GpuTextFeeder {
     return static_cast<size_t>(nnz) <= s.ids_cap;
   }
 
+  // Page-locked staging buffer i (of 2) of at least `bytes` (grown on demand; the thread's own).
+  uint8_t* staging(int i, size_t bytes) {
+    if (!pin_ev_[i]) hip_ok(hipEventCreateWithFlags(&pin_ev_[i], hipEventDisableTiming), "hipEventCreate");
+    if (bytes > pin_cap_[i]) {
+      if (pin_[i]) (void)hipHostFree(pin_[i]);
+      pin_[i] = nullptr;
+      pin_cap_[i] = 0;
+      const size_t cap = bytes + bytes / 4;
+      hip_ok(hipHostMalloc(reinterpret_cast<void**>(&pin_[i]), cap, hipHostMallocDefault), "hipHostMalloc");
+      pin_cap_[i] = cap;
+    }
+    return pin_[i];
+  }
+
+  // The staged batch whose copies are queued: wait for them, then hand it to the consumer.
+  void flush_pending() {
+    if (!pend_on_) return;
+    pend_on_ = false;
+    hip_ok(hipEventSynchronize(pin_ev_[pend_buf_]), "hipEventSynchronize");
+    publish(pend_b_);
+  }
+
+  // dst + offs[k] <- srcs[k] (bytes[k]) for the k with bytes: large arrays split over a few threads
+  static void parallel_copy(uint8_t* dst, const size_t* offs, const void* const* srcs, const size_t* bytes, int n) {
+    constexpr size_t kChunk = 1 << 20;
+    constexpr int kThreads = 8;
+    struct Piece { uint8_t* d; const uint8_t* s; size_t b; };
+    std::vector<Piece> pieces;
+    for (int k = 0; k < n; ++k)
+      for (size_t o = 0; o < bytes[k]; o += kChunk)
+        pieces.push_back({dst + offs[k] + o, static_cast<const uint8_t*>(srcs[k]) + o, std::min(kChunk, bytes[k] - o)});
+    const int T = static_cast<int>(std::min<size_t>(kThreads, pieces.size()));
+    auto work = [&](int t) {
+      for (size_t i = t; i < pieces.size(); i += T) std::memcpy(pieces[i].d, pieces[i].s, pieces[i].b);
+    };
+    if (T <= 1) {
+      if (T == 1) work(0);
+      return;
+    }
+    std::vector<std::thread> ths;
+    for (int t = 1; t < T; ++t) ths.emplace_back(work, t);
+    work(0);
+    for (auto& th : ths) th.join();
+  }
+
   void fail(const std::string& msg, bool parse) {
     std::lock_guard<std::mutex> lk(mu_);
     failed_ = true;
@@ -275,6 +328,14 @@ class GpuTextFeeder {
       hip_ok(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking), "hipStreamCreate");
       char err[4096];
       while (true) {
+        {  // a pending batch is published before the thread can block waiting for a free slot
+          bool none;
+          {
+            std::lock_guard<std::mutex> lk(mu_);
+            none = free_.empty();
+          }
+          if (none) flush_pending();
+        }
         const int d = acquire();
         if (d < 0) break;
         FmRawView v{};
@@ -299,7 +360,8 @@ class GpuTextFeeder {
         const int64_t n = v.nlines;
         const bool fits = static_cast<size_t>(v.nbytes) <= s.bytes_cap && static_cast<size_t>(n) + 1 <= s.ls_cap &&
                           n < (int64_t(1) << 31);
-        bool ok = true;
+        bool ok = true, deferred = false;
+        if (v.kind != 1) flush_pending();  // (keeps the batch order)
         if (v.kind == 1) {  // parsed on the host (CPU parser / binary cache): copy the CSR over
           if (static_cast<size_t>(n) + 1 > s.ls_cap) {
             fail("batch of " + std::to_string(n) + " lines exceeds the feeder's slots", false);
@@ -308,15 +370,28 @@ class GpuTextFeeder {
             if (!stop_) fail("batch of " + std::to_string(v.nnz) + " features exceeds the feeder's slots", false);
             ok = false;
           } else {
+            // the loader's CSR is in pageable memory: gather it into the feeder's page-locked staging
+            // buffer (parallel memcpy) and copy that with one DMA per array at full PCIe / xGMI rate
+            // (pageable H2D copies ran the .fmb path at 1.3e7 ex/s, profiles/r4/e2e.txt)
+            const int64_t nnz = v.nnz;
+            const size_t parts[5] = {size_t(4 * n), size_t(4 * (n + 1)), size_t(4 * nnz),
+                                     v.vals ? size_t(4 * nnz) : 0, (v.weights && s.weights) ? size_t(4 * n) : 0};
+            const void* srcs[5] = {v.labels, v.offsets, v.ids, v.vals, v.weights};
+            void* dsts[5] = {s.labels, s.offsets, s.ids, s.vals, s.weights};
+            size_t offs[5], total = 0;
+            for (int k = 0; k < 5; ++k) {
+              offs[k] = total;
+              total += (parts[k] + 255) / 256 * 256;
+            }
+            // two staging buffers: batch k's gather overlaps batch k-1's DMA, which is waited for (and
+            // k-1 published) only after k's copies are queued
+            uint8_t* pin = staging(pin_cur_, total);  // (its previous DMA completed: flushed a batch ago)
+            parallel_copy(pin, offs, srcs, parts, 5);
             hip_ok(hipStreamWaitEvent(st_, s.freed, 0), "hipStreamWaitEvent");
-            hip_ok(hipMemcpyAsync(s.labels, v.labels, 4 * n, hipMemcpyHostToDevice, st_), "H2D");
-            hip_ok(hipMemcpyAsync(s.offsets, v.offsets, 4 * (n + 1), hipMemcpyHostToDevice, st_), "H2D");
-            if (v.nnz > 0) hip_ok(hipMemcpyAsync(s.ids, v.ids, 4 * v.nnz, hipMemcpyHostToDevice, st_), "H2D");
-            if (v.vals && v.nnz > 0)
-              hip_ok(hipMemcpyAsync(s.vals, v.vals, 4 * v.nnz, hipMemcpyHostToDevice, st_), "H2D");
-            if (v.weights && s.weights)
-              hip_ok(hipMemcpyAsync(s.weights, v.weights, 4 * n, hipMemcpyHostToDevice, st_), "H2D");
-            hip_ok(hipStreamSynchronize(st_), "hipStreamSynchronize");
+            for (int k = 0; k < 5; ++k)
+              if (parts[k]) hip_ok(hipMemcpyAsync(dsts[k], pin + offs[k], parts[k], hipMemcpyHostToDevice, st_), "H2D");
+            hip_ok(hipEventRecord(pin_ev_[pin_cur_], st_), "hipEventRecord");
+            deferred = true;
             b.nnz = v.nnz;
             b.max_feats = v.max_feats;
             b.has_vals = v.vals != nullptr;
@@ -360,13 +435,23 @@ class GpuTextFeeder {
             b.has_vals = s.info_h[2] != 0;
           }
         }
-        api_->done(api_->handle, &v);  // the host bytes are on the device (or parsed): slot back to the loader
+        api_->done(api_->handle, &v);  // the host bytes are on the device / staged (or parsed): back to the loader
         if (!ok) {
+          flush_pending();
           give_back(d);
           break;
         }
-        publish(b);
+        if (deferred) {  // publish the previous staged batch (its DMA ran before this one's), keep this one
+          flush_pending();
+          pend_b_ = b;
+          pend_buf_ = pin_cur_;
+          pend_on_ = true;
+          pin_cur_ ^= 1;
+        } else {
+          publish(b);
+        }
       }
+      flush_pending();
     } catch (const std::exception& e) {
       fail(e.what(), false);
     }
@@ -395,6 +480,15 @@ class GpuTextFeeder {
   int64_t resize_need_ = 0;
   bool resize_ask_ = false;        // the request is not yet returned by next()
   std::atomic<long long> fallbacks_{0}, batches_{0}, resizes_{0};
+  // page-locked staging of host-parsed batches (the thread's; double-buffered) and the batch whose
+  // copies are queued but not yet waited for
+  uint8_t* pin_[2] = {nullptr, nullptr};
+  size_t pin_cap_[2] = {0, 0};
+  hipEvent_t pin_ev_[2] = {nullptr, nullptr};
+  int pin_cur_ = 0;
+  bool pend_on_ = false;
+  int pend_buf_ = 0;
+  FeederBatch pend_b_;
   std::vector<float> h_labels_, h_vals_;
   std::vector<int32_t> h_offsets_, h_ids_;
 };
