@@ -7,4 +7,6 @@ variant here leaves the other builds current (a variant's own flags are hashed i
 
 HIP_VARIANTS: dict[str, list[str]] = {"fwdnopf": ["-DFM_FWD_PREFETCH=0"], "fwdgen": ["-DFM_FWD_SPECIALIZE=0"],
                                      "bwdgen": ["-DFM_BWD_SPECIALIZE=0"],
-                                     "allgen": ["-DFM_FWD_SPECIALIZE=0", "-DFM_BWD_SPECIALIZE=0"]}
+                                     "allgen": ["-DFM_FWD_SPECIALIZE=0", "-DFM_BWD_SPECIALIZE=0"],
+                                     "fu10w4": ["-DFM_FWD_UNR16=10", "-DFM_FWD_LOCAL_W16=4"],
+                                     "cu32_8": ["-DFM_CHUNK_UNR32=8"]}

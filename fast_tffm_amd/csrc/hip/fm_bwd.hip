@@ -35,9 +35,24 @@ enum BwdMode : int { kBwdLocal = 0, kBwdEmit = 1, kBwdEmitTable = 2 };
 constexpr int kMaxCH = 32;        // chunk length cap (prefetch registers)
 constexpr int kSmallChunks = 16;  // rows with more chunks go to the workgroup combine
 constexpr int kMaxPieceOwners = 64;  // owners of a split backward piece
-// r1 rows in flight per lane in the chunk kernel: 8 beats 4 / 6 (fewer VGPRs, more waves) and 12 /
-// 16 on k64 fp32, k64 bf16 and k128 fp8 (profiles/r1s3/chunk_unroll_ab.txt)
-constexpr int kChunkUnr = 8;
+// r1 rows in flight per lane in the chunk kernel: 8 beat 4 / 6 (fewer VGPRs, more waves) and 12 /
+// 16 on k64 fp32, k64 bf16 and k128 fp8 in round 1 (profiles/r1s3/chunk_unroll_ab.txt); still the
+// best for k <= 64 with the round-4 kernels, but not for k = 128 (below)
+#ifndef FM_CHUNK_UNR
+#define FM_CHUNK_UNR 8
+#endif
+constexpr int kChunkUnr = FM_CHUNK_UNR;
+// The local kernels' 32-lane rows (k = 128): 12 r1 rows in flight per lane.  Same-box A/B
+// (profiles/r4/chunk_unr_ab.txt): k128 fp8 FTRL 0.874 -> 0.807 ms with 12, 0.856 with 16; 16-lane and
+// 4-lane rows (k64 / k16) lose with 12 or 16 (k64 fp32 0.615 -> 0.625-0.640), and so does the
+// row-sharded step's general kernel (k128 fp8 at world 1 1.121 -> 1.288 ms).  FM_CHUNK_UNR32 overrides.
+#ifndef FM_CHUNK_UNR32
+#define FM_CHUNK_UNR32 12
+#endif
+template <int LPR, bool LOC>
+constexpr int chunk_unr() {
+  return LOC && LPR == 32 ? FM_CHUNK_UNR32 : kChunkUnr;
+}
 
 struct BwdArgs {
   int mode;                 // BwdMode
@@ -298,7 +313,7 @@ __device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
   constexpr int EPL = Frag<TV>::N;  // elements per lane of the table dtype
   constexpr int G = kWave / LPR;
   constexpr int PF = (kMaxCH + LPR - 1) / LPR;  // prefetched occurrences per lane
-  constexpr int UNR = LPR < kChunkUnr ? LPR : kChunkUnr;  // r1 rows in flight per lane
+  constexpr int UNR = LPR < chunk_unr<LPR, LOC>() ? LPR : chunk_unr<LPR, LOC>();  // r1 rows in flight per lane
   constexpr bool kShortPath = LPR >= 32;                          // short-chunk block (below)
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR, t = lane % LPR;

@@ -101,11 +101,16 @@ template <int LPR, typename TV>
 constexpr int fwd_min_waves() {
   return LPR >= 32 ? 4 : 1;
 }
-// The local forward's 16-lane instantiations (k=64) at 4 waves/SIMD: a variant of the register
-// accumulation needed 136 VGPRs uncapped (3 waves), 0.674 vs 0.643 ms capped on the k64 fp32 step
-// (profiles/r4/specialize_ab.txt); the current code fits in 115 either way, the floor keeps it there
+// The local forward's 16-lane instantiations (k=64): 2 row groups in flight per lane at 7 waves per
+// SIMD (72 VGPRs) instead of 10 at 4 (115): k64 fp32 0.618 -> 0.607 ms same-box; 3 at 6 waves ties,
+// 4 at 5 / 6 at 4 lose (profiles/r4/fwd_occupancy_ab.txt).  Latency-bound gathers: more waves hide
+// more than more loads per wave.  (A variant of the register accumulation needed 136 VGPRs
+// uncapped -- 3 waves -- and the 4-wave floor then bought 0.674 -> 0.643 ms: specialize_ab.txt.)
 #ifndef FM_FWD_LOCAL_W16
-#define FM_FWD_LOCAL_W16 4
+#define FM_FWD_LOCAL_W16 7
+#endif
+#ifndef FM_FWD_UNR16
+#define FM_FWD_UNR16 2
 #endif
 template <int LPR, typename TV>
 constexpr int fwd_local_min_waves() {
@@ -130,7 +135,8 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
   using F = Frag<TV>;
   constexpr int EPL = F::N;
   constexpr int G = kWave / LPR;
-  constexpr int UNR = FwdUnroll<G>::v;
+  // (FM_FWD_UNR16: row groups in flight of the local kernel's 16-lane instantiations, k = 64)
+  constexpr int UNR = !SH && LPR == 16 ? FM_FWD_UNR16 : FwdUnroll<G>::v;
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR, t = lane % LPR;
   const int nv = a.Kp / EPL;
