@@ -132,8 +132,6 @@ class TextLoader {
   static int api_parse(void* h, const FmRawView* v, FmParsedOut* out, char* err, int errlen);
   static void api_stop(void* h) { static_cast<TextLoader*>(h)->close(); }
 
- public:
- private:
   void run();
   bool push(LoadedBatch&& b);
   int acquire_slot();         // a free raw slot (blocks), -1 once stopped

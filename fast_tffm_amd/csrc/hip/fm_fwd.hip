@@ -112,9 +112,34 @@ constexpr int fwd_min_waves() {
 #ifndef FM_FWD_UNR16
 #define FM_FWD_UNR16 2
 #endif
+// The same pair for the 32-lane instantiations (k = 128): fp8 rows 4 at 7 waves (72 VGPRs):
+// k128 fp8 FTRL 0.806 -> 0.784 ms; bf16 / fp32 rows keep 12 at 4 (lower pairs spill there: k128
+// bf16 FTRL 0.95 -> 1.07-1.21 ms; profiles/r4/fwd_occupancy_ab.txt).  FM_FWD_UNR32[_FP8] /
+// FM_FWD_LOCAL_W32[_FP8]: A/B knobs.
+#ifndef FM_FWD_LOCAL_W32
+#define FM_FWD_LOCAL_W32 4
+#endif
+#ifndef FM_FWD_UNR32
+#define FM_FWD_UNR32 12
+#endif
+#ifndef FM_FWD_LOCAL_W32_FP8
+#define FM_FWD_LOCAL_W32_FP8 7
+#endif
+#ifndef FM_FWD_UNR32_FP8
+#define FM_FWD_UNR32_FP8 4
+#endif
 template <int LPR, typename TV>
 constexpr int fwd_local_min_waves() {
-  return LPR == 16 ? FM_FWD_LOCAL_W16 : fwd_min_waves<LPR, TV>();
+  return LPR == 16   ? FM_FWD_LOCAL_W16
+         : LPR == 32 ? (Frag<TV>::kScaled ? FM_FWD_LOCAL_W32_FP8 : FM_FWD_LOCAL_W32)
+                     : fwd_min_waves<LPR, TV>();
+}
+template <int LPR, typename TV, bool SH>
+constexpr int fwd_unroll() {
+  return SH ? FwdUnroll<kWave / LPR>::v
+         : LPR == 16 ? FM_FWD_UNR16
+         : LPR == 32 ? (Frag<TV>::kScaled ? FM_FWD_UNR32_FP8 : FM_FWD_UNR32)
+                     : FwdUnroll<kWave / LPR>::v;
 }
 
 // LDS of the dense-row counting (FM_DENSE_BWD): only the dense instantiation carries it
@@ -136,7 +161,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
   constexpr int EPL = F::N;
   constexpr int G = kWave / LPR;
   // (FM_FWD_UNR16: row groups in flight of the local kernel's 16-lane instantiations, k = 64)
-  constexpr int UNR = !SH && LPR == 16 ? FM_FWD_UNR16 : FwdUnroll<G>::v;
+  constexpr int UNR = fwd_unroll<LPR, TV, SH>();
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR, t = lane % LPR;
   const int nv = a.Kp / EPL;
