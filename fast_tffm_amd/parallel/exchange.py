@@ -264,6 +264,13 @@ class ShardExchange(_Base):
         # the backward instead of the owner's apply.  GPU, wire dtype = table dtype, one part.
         self.self_rows = (self.dev.type == "cuda" and self.wire.dtype == tdt and self.nparts == 1
                           and os.environ.get("FM_SELF_ROWS", "1") != "0")
+        # world 1 with self rows: every row is this rank's and exclusive and a key is its table
+        # row (owner 0), so training steps run the local step's forward and backward (table rows,
+        # LOCAL-mode in-place update: the specialised kernels, one backward pass, no gradient rows,
+        # no apply) and their plans skip the key transform and the segment index
+        # (profiles/r4/shard_w1_local.txt); world > 1 keeps EMIT + the exchange
+        self.local_w1 = (self.self_rows and self.W == 1
+                         and os.environ.get("FM_SHARD_W1_LOCAL", "1") != "0")  # (0: EMIT path, A/B)
         self.cur_plan: _ShardPlan | None = None
         self.step_start = None
         self.early_steps = 0          # steps that took the early-exchange + patch path
@@ -397,17 +404,22 @@ class ShardExchange(_Base):
                 part.b = sb = b if len(ranges) == 1 else _sub_batch(b, e0, e1, n0, n1, offs)
                 part.e0 = e0
                 dws = slot.ensure(k, sb.nnz, self.dev, m.cfg.dedup_chunk)
-                keys = K.shard_keys(sb.ids, self.W, self.Rps, slot.keys[k])
+                w1 = train and self.local_w1  # (world 1: keys = ids, no segment index)
+                if w1 and sb.ids.dtype == torch.int32 and sb.ids.is_contiguous():
+                    keys = sb.ids
+                else:
+                    keys = K.shard_keys(sb.ids, self.W, self.Rps, slot.keys[k])
                 ex, shift = None, 0
                 if train:
                     shift = m._slot_bits(sb, always=True)
                     ex = K.csr_rows(sb.offsets, out=dws.ex_of_occ[: sb.nnz], nnz=sb.nnz, slot_bits=shift)
                 # training plans on the GPU find each occurrence's segment through a bucket index
                 # (K.seg_index) instead of the inverse map, a 5.1M-occurrence random scatter
-                lookup = train and gpu and K.seg_lookup_enabled()
+                lookup = train and gpu and K.seg_lookup_enabled() and not w1
                 part.keys = keys
                 part.dd = K.dedup(keys, ws=dws, key_bits=self.key_bits, ex_of_occ=ex,
-                                  vals=sb.vals if ex is not None else None, want_inv=not lookup, num_examples=sb.B,
+                                  vals=sb.vals if ex is not None else None, want_inv=not (lookup or w1),
+                                  num_examples=sb.B,
                                   Kp=self.m.Kp, ex_shift=shift, offsets=sb.offsets if shift else None,
                                   dense_min=K.dense_min_for(sb.B, self.m.Kp, m.cfg.dedup_chunk,
                                                             table_dtype=m.table.v.dtype,
@@ -497,7 +509,7 @@ class ShardExchange(_Base):
 
     def _early_ok(self, pl: _ShardPlan, cur: _ShardPlan | None) -> bool:
         gpu = self.dev.type == "cuda"
-        if pl.self_r is not None and pl.self_r[1] - pl.self_r[0] == pl.R:
+        if self.local_w1 or (pl.self_r is not None and pl.self_r[1] - pl.self_r[0] == pl.R):
             return False  # every request is this rank's own row (world 1): nothing to exchange early
         return (self.prefetch and len(pl.parts) == 1 and pl.splits is not None and cur is not None
                 and cur.splits is not None and (cur.run_off is not None or not gpu) and len(cur.parts) == 1
@@ -803,7 +815,9 @@ class ShardExchange(_Base):
         # every part's rows are gathered first and their all-to-alls queued on RCCL's stream
         # (async): part k+1's rows travel while part k computes
         with roctx_range("gather+a2a_rows"):
-            if pl.early is not None:
+            if self.local_w1:  # (the forward reads the table)
+                rows = [(None, None)] * len(pl.parts)
+            elif pl.early is not None:
                 rows = [(None, None)]
                 early_views = self._patch(pl)
                 self.early_steps += 1
@@ -823,12 +837,28 @@ class ShardExchange(_Base):
             srows = K.SelfRows(pl.self_u[0], pl.self_u[1], self.ctx.rank * self.Rps, pl.parts[0].dd.uniq,
                                m.table.state, pl.self_excl)
             skw = dict(self_rows=srows, opt=cfg.opt, sr_counter=sr)
+        local_w1 = self.local_w1  # (see __init__; its plans were built for it: keys = ids, no inverse map)
+        # one part: the loss reduction is enqueued after the backward, as in the local step
+        one_part = len(pl.parts) == 1
         for part, (buf, work) in zip(pl.parts, rows):
             sb, dd, e0 = part.b, part.dd, part.e0
             if work is not None:
                 work.wait()               # the compute stream waits for this part's rows
-            src_v, src_w = wf.views(buf) if buf is not None else early_views
             dA = ws.dense_counts(ws.cap_b)[e0: e0 + sb.B] if dd.dense_list is not None else None
+            if local_w1:  # (keys are table rows: the local step's forward over the table)
+                with roctx_range("fwd_local"):
+                    fo = K.fm_forward(sb.offsets, part.keys, sb.vals, m.table.v, m.table.w, Kp, labels=sb.labels,
+                                      weights=sb.weights, loss=cfg.loss_type, grad_scale=gscale, want_r1=True,
+                                      pred=ws.pred[: sb.B], r1=ws.r1[: sb.B], dpred=ws.dpred[: sb.B],
+                                      partial=ws.fwd_partial, threads=cfg.threads, bias=m.gbias, dense=dd,
+                                      dense_A=dA, defer_loss=True)
+                with roctx_range("bwd_local"):
+                    K.fm_backward(dd, fo.dpred, fo.r1, Kp, mode=K.BWD_LOCAL, table=m.table.state, opt=cfg.opt,
+                                  reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads,
+                                  dense_part=ws.dense_part, dense_stream=m._dense_stream(), sr_counter=sr,
+                                  dense_A=dA)
+                continue
+            src_v, src_w = wf.views(buf) if buf is not None else early_views
             gs = grad_send[part.u0: part.u0 + part.U]
             with roctx_range("fwd"):
                 fo = K.fm_forward(sb.offsets, part.keys if part.seg is not None else dd.inv[: sb.nnz], sb.vals,
@@ -837,8 +867,9 @@ class ShardExchange(_Base):
                                   pred=ws.pred[e0: e0 + sb.B], r1=ws.r1[e0: e0 + sb.B],
                                   dpred=ws.dpred[e0: e0 + sb.B], partial=ws.fwd_partial, threads=cfg.threads,
                                   bias=m.gbias, dense=dd, dense_A=dA, dense_by_segment=True, self_rows=srows,
-                                  seg_lookup=part.seg)
-            loss = fo.loss_sum if loss is None else loss + fo.loss_sum
+                                  seg_lookup=part.seg, defer_loss=one_part)
+            if not one_part:  # (the parts share the loss partials: each part's sum before the next)
+                loss = fo.loss_sum if loss is None else loss + fo.loss_sum
             if self._split_ok(pl, dd):
                 with roctx_range("bwd_split+grads"):
                     gworks += self._bwd_split_exchange(pl, part, dd, fo, src_v, src_w, gs, grad_recv, rv, rw, skw)
@@ -854,10 +885,12 @@ class ShardExchange(_Base):
                                                          group=self.group, async_op=True))
                     self.bytes_sent += 4 * wf.g_words * self._to_others(part.sc)
         m.bias_step(ws.dpred[: b.B])
+        if one_part:
+            loss = fo.finish_loss()
         for w in gworks:
             w.wait()
         with roctx_range("apply"):
-            if not (srows is not None and self.W == 1):  # (world 1: every row was updated in place)
+            if not local_w1 and not (srows is not None and self.W == 1):  # (world 1: updated in place)
                 K.apply_runs(pl.req_recv, pl.run_off, pl.splits, grad_recv, m.table.state, cfg.opt, Kp,
                              match=pl.match, threads=cfg.threads,
                              ws=self.slots[pl.slot].ensure2(pl.R, self.dev) if not gpu else None,
