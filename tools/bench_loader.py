@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Host-only timing of the native text loader (csrc/cpu/loader.cpp), per epoch: raw mode (line
-bytes for the GPU tokenizer) and parse mode (CPU parser -> CSR), with weight files, on the e2e
+bytes for the GPU tokenizer), parse mode (CPU parser -> CSR) and binary mode (.fmb caches -> CSR
+assembly, data/bincache.py), with weight files, on the e2e
 tool's shape (Criteo-shaped libsvm lines, vocabulary 800k, batch 50000).  Runs without a GPU.
 
 usage: python tools/bench_loader.py [--lines 250000] [--files 4] [--epochs 3] [--threads 8]
@@ -25,7 +26,7 @@ def main():
     ap.add_argument("--batch", type=int, default=50_000)
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--epochs", type=int, default=3)
-    ap.add_argument("--modes", default="raw,parse")
+    ap.add_argument("--modes", default="raw,parse", help="comma list of raw, parse, binary")
     ap.add_argument("--no-weights", action="store_true")
     ap.add_argument("--dir", default="/tmp/fm_loader_bench")
     a = ap.parse_args()
@@ -46,12 +47,19 @@ def main():
     nb = int(B * nbytes / a.files / a.lines * 1.5) + 4096
     bufs = [(np.empty(nb, np.uint8), np.empty(B + 1, np.int64), np.empty(B, np.float32)) for _ in range(8)]
     slots = [[b.ctypes.data, b.size, ls.ctypes.data, ls.size, w.ctypes.data, w.size] for b, ls, w in bufs]
+    bfiles = []
+    if "binary" in a.modes:
+        from fast_tffm_amd.data.bincache import convert_files
+
+        bfiles = [pth for pth, _ in convert_files(files, None if a.no_weights else wfiles,
+                                                   os.path.join(a.dir, "fmb"), 800_000, threads=a.threads)]
     for mode in a.modes.split(","):
-        L = native.cpu().TextLoader(raw_slots=slots if mode == "raw" else [], files=files,
-                                    weight_files=[] if a.no_weights else wfiles, batch_size=a.batch, vocab_size=800_000,
-                                    hash_feature_id=False, shuffle=True, num_epochs=a.epochs, seed=1,
-                                    threads=a.threads, rank=0, world=1, queue_size=4, start_epoch=0,
-                                    skip_batches=0, raw=mode == "raw", binary=False, rows=False)
+        binary = mode == "binary"
+        L = native.cpu().TextLoader(raw_slots=slots if mode == "raw" else [], files=bfiles if binary else files,
+                                    weight_files=[] if a.no_weights or binary else wfiles, batch_size=a.batch,
+                                    vocab_size=800_000, hash_feature_id=False, shuffle=True, num_epochs=a.epochs,
+                                    seed=1, threads=a.threads, rank=0, world=1, queue_size=4, start_epoch=0,
+                                    skip_batches=0, raw=mode == "raw", binary=binary, rows=False)
         t = time.time()
         per_epoch, n, cur = [], 0, 0
         while True:
