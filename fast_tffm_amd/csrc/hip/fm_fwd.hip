@@ -116,6 +116,11 @@ constexpr int fwd_min_waves() {
 // k128 fp8 FTRL 0.806 -> 0.784 ms; bf16 / fp32 rows keep 12 at 4 (lower pairs spill there: k128
 // bf16 FTRL 0.95 -> 1.07-1.21 ms; profiles/r4/fwd_occupancy_ab.txt).  FM_FWD_UNR32[_FP8] /
 // FM_FWD_LOCAL_W32[_FP8]: A/B knobs.
+// Sharded fp8 forward reads the stored row norms (wire tail word 2 / the table's); 0: per-element
+// s2 as before (the "fwdshnonorm" A/B build variant)
+#ifndef FM_FWD_SH_NORM
+#define FM_FWD_SH_NORM 1
+#endif
 #ifndef FM_FWD_LOCAL_W32
 #define FM_FWD_LOCAL_W32 4
 #endif
@@ -250,8 +255,9 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
 #pragma unroll
     for (int k = 0; k < EPL; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
     float lin = 0.f, rv = 0.f, rw = 0.f;
-    // local fp8 (kNorm): s2 = sum_j x_j^2 |v_j|^2 from the rows' stored norms, one occurrence per lane
-    constexpr bool kNorm = F::kScaled && !SH;
+    // fp8 (kNorm): s2 = sum_j x_j^2 |v_j|^2 from the rows' stored norms, one occurrence per lane
+    // (sharded step: the wire row's tail carries the norm next to [w, scale], own rows the table's)
+    constexpr bool kNorm = F::kScaled && (!SH || FM_FWD_SH_NORM);
     float s2n = 0.f;
     for (int base = s; base < e; base += kWave) {
       const int m = min(kWave, e - base);
@@ -263,7 +269,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
       } else {
         pairs(base, m, my_row, my_x);
       }
-      if (kNorm && lane < m) {  // [w, scale, |v|^2, pad]: one 16-byte load (w_stride 4, host-checked)
+      if (kNorm && !SH && lane < m) {  // [w, scale, |v|^2, pad]: one 16-byte load (w_stride 4, host-checked)
         my_seg = my_row;
         const float4 wr = *reinterpret_cast<const float4*>(a.w + (uint64_t)(uint32_t)my_row * 4u);
         my_w = wr.x;
@@ -291,10 +297,12 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
           const long long trow = own_key ? (long long)key - a.self.base : a.self.row(my_row);
           my_w = a.self.w[trow * a.self.w_stride];
           my_s = row_scale<TV>(a.self.w, trow, a.self.w_stride);
+          if constexpr (kNorm) my_n2 = a.self.w[trow * a.self.w_stride + kFp8Norm];
           my_row = (int)trow | kSelfBit;
         } else {
           my_w = a.w[(long long)my_row * a.w_stride];
           my_s = row_scale<TV>(a.w, my_row, a.w_stride);
+          if constexpr (kNorm) my_n2 = a.w[(long long)my_row * a.w_stride + kFp8Norm];
         }
       }
       if constexpr (DENSE) {

@@ -64,7 +64,7 @@ __global__ __launch_bounds__(kBlock) void gather_rows_kernel(GatherArgs a) {
 // cross xGMI at their storage size (exact: the stored bits are copied) and an
 // fp32 table can optionally be sent as bf16 (comm_dtype = bf16, RNE).
 // Wire row (RB bytes, RB % 16 == 0): [v: Kp elements of the wire dtype, padded
-// to vb bytes (vb % 16 == 0)] [w fp32] [scale fp32 (fp8) / 0] [0] [0].
+// to vb bytes (vb % 16 == 0)] [w fp32] [scale fp32 (fp8) / 0] [|v|^2 fp32 (fp8) / 0] [tag / 0].
 struct GatherWireArgs {
   int R;
   const int* req;           // [R] local table rows requested by peers
@@ -122,7 +122,8 @@ __global__ __launch_bounds__(kBlock) void gather_wire_kernel(GatherWireArgs a) {
       float* tail = reinterpret_cast<float*>(dst + a.vb);
       tail[0] = a.w[row * a.w_stride];
       tail[1] = a.scaled ? a.w[row * a.w_stride + 1] : 0.f;
-      tail[2] = 0.f;
+      // fp8: the row's stored |v|^2 ([w, scale, norm, pad] table rows), read by the sharded forward
+      tail[2] = a.scaled ? a.w[row * a.w_stride + kFp8Norm] : 0.f;
       int tag = 0;
       if (a.idx) {
         int q = 0;

@@ -212,6 +212,8 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
     _check(w.dtype == torch.float32 and w.device == dev, "w: expected float32 on the rows' device")
     w_stride = w.stride(0)
     _check(w.shape[0] >= v.shape[0], "w: fewer rows than v")
+    # fp8 rows: w is the row tails [w, scale, |v|^2, .] (Table rows / wire rows): the forward reads all three
+    _check(v.dtype != FP8 or w_stride >= 3, "fp8 rows: w must be a strided view of [w, scale, |v|^2, .] row tails")
     lt = LOSS_TYPES[loss]
     if bias is not None:
         _chk_vec(bias, torch.float32, 1, "bias", dev)
@@ -921,7 +923,8 @@ class WireFormat:
     """Row layout of the row-sharded exchange (owner gather -> all-to-all -> fwd/bwd).
 
     A wire row is ``rb`` bytes: the Kp factor values in ``dtype`` (padded to
-    ``vb`` bytes), then ``[w, scale, 0, 0]`` fp32 (scale only for fp8).  bf16 /
+    ``vb`` bytes), then ``[w, scale, |v|^2, tag]`` fp32 (scale and the stored row norm for fp8 only;
+    tag: patch gathers).  bf16 /
     fp8 tables travel at their storage size (the stored bits); an fp32 table
     travels as fp32 (``[v | w | pad]``, the same bytes as a [Kp+4] fp32 row) or,
     with ``comm_dtype = bf16``, as bf16 (rounded to nearest even).
