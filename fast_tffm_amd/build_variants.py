@@ -9,5 +9,5 @@ HIP_VARIANTS: dict[str, list[str]] = {"fwdnopf": ["-DFM_FWD_PREFETCH=0"], "fwdge
                                      "bwdgen": ["-DFM_BWD_SPECIALIZE=0"],
                                      "allgen": ["-DFM_FWD_SPECIALIZE=0", "-DFM_BWD_SPECIALIZE=0"],
                                      "fu10w4": ["-DFM_FWD_UNR16=10", "-DFM_FWD_LOCAL_W16=4"],
-                                     "fwdshnonorm": ["-DFM_FWD_SH_NORM=0"],
+                                     "f4gen": ["-DFM_FWD_UNR4=0", "-DFM_FWD_LOCAL_W4=0"],
                                      "cu32_8": ["-DFM_CHUNK_UNR32=8"]}

@@ -133,15 +133,29 @@ constexpr int fwd_min_waves() {
 #ifndef FM_FWD_UNR32_FP8
 #define FM_FWD_UNR32_FP8 4
 #endif
+// The 4-lane bf16 instantiation (k = 16 bf16): 5 row groups in flight at >= 4 waves per SIMD instead
+// of 3 at the compiler's choice: k16 bf16 0.490-0.491 -> 0.485-0.488 ms over four same-box reps; 8 waves
+// lose 4-36%, 6 at 4 / 8 at 3 / 4 at 5 tie or lose (profiles/r4/fwd_occupancy_ab.txt).  Other dtypes
+// of 4-lane rows keep the generic choice.  FM_FWD_LOCAL_W4 / FM_FWD_UNR4: A/B knobs (0 = generic).
+#ifndef FM_FWD_LOCAL_W4
+#define FM_FWD_LOCAL_W4 4
+#endif
+#ifndef FM_FWD_UNR4
+#define FM_FWD_UNR4 5
+#endif
+template <typename TV>
+constexpr bool fwd_is_bf16() { return std::is_same<TV, __hip_bfloat16>::value; }
 template <int LPR, typename TV>
 constexpr int fwd_local_min_waves() {
-  return LPR == 16   ? FM_FWD_LOCAL_W16
+  return LPR == 4 && fwd_is_bf16<TV>() && FM_FWD_LOCAL_W4 > 0 ? FM_FWD_LOCAL_W4
+         : LPR == 16 ? FM_FWD_LOCAL_W16
          : LPR == 32 ? (Frag<TV>::kScaled ? FM_FWD_LOCAL_W32_FP8 : FM_FWD_LOCAL_W32)
                      : fwd_min_waves<LPR, TV>();
 }
 template <int LPR, typename TV, bool SH>
 constexpr int fwd_unroll() {
   return SH ? FwdUnroll<kWave / LPR>::v
+         : LPR == 4 && fwd_is_bf16<TV>() && FM_FWD_UNR4 > 0 ? FM_FWD_UNR4
          : LPR == 16 ? FM_FWD_UNR16
          : LPR == 32 ? (Frag<TV>::kScaled ? FM_FWD_UNR32_FP8 : FM_FWD_UNR32)
                      : FwdUnroll<kWave / LPR>::v;
