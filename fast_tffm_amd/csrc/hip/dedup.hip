@@ -34,23 +34,18 @@ constexpr int kMaxTiles = 1 << 20;               // tile-count words per call (n
 
 struct RleArgs {
   int n, CH, ntiles;              // n: occurrences, ntiles over n
-  int dense_min;                  // rows with >= dense_min occurrences are "dense" (0: none)
-  int* dense_list;                // [kMaxDense] segment ids of the first dense rows in key order
   const uint32_t* skeys;          // sorted keys
   const int* spay;                // sorted payload (occurrence or example index)
   int ex_shift;                   // > 0: payload / ex_of_occ hold packed codes (example << ex_shift | slot)
   const int* offsets;             // [B+1] CSR offsets (packed codes -> occurrence index)
   unsigned long long* tile_cnt;   // [ntiles] heads << 32 | chunk starts (rle_count_kernel)
-  int* dense_tmp;                 // dense-row heads as found (unordered), dense_cnt of them
-  int* dense_cnt;
-  int dense_cap;
   uint32_t* uniq;                 // [n] unique keys (first U valid)
   int* seg_start;                 // [n+1]
   int* seg_chunk;                 // [n+1] first chunk of each segment
   int* chunk_start;               // [n+1]
   int* chunk_seg;                 // [n] segment id | kChunkFirst | kChunkSingle
   int* chunk_key;                 // [n] key of the chunk's segment
-  int* counts;                    // device [8]: U, #chunks, #multi-chunk rows, #dense rows, bwd hot rows, -
+  int* counts;                    // device [8]: U, #chunks, #multi-chunk rows, -, bwd hot rows, -
   int* inv;                       // [n] occurrence -> segment (payload = occurrence)
   const int* ex_of_occ;           // [n] (payload = occurrence)
   int* sorted_ex;                 // [n] (payload = occurrence)
@@ -93,13 +88,8 @@ __device__ inline void rle_flags8(const RleArgs& a, int j0, Rle8& r) {
   }
 }
 
-// Head of a row with at least dense_min occurrences (the MFMA backward path, fm_bwd.hip).
-__device__ inline bool dense_head(const RleArgs& a, int j, uint32_t k) {
-  return a.dense_min > 0 && j + a.dense_min - 1 < a.n && a.skeys[j + a.dense_min - 1] == k;
-}
-
 // Block-wide exclusive scan of NC per-thread counts (segment heads, chunk
-// starts, dense-row heads).
+// starts).
 template <int NC>
 __device__ inline void block_excl_scan(const unsigned (&v)[NC], unsigned (&ex)[NC], unsigned (&tot)[NC]) {
   __shared__ unsigned sh[NC][kWavesPerBlock];
@@ -134,8 +124,8 @@ __device__ inline void block_excl_scan(const unsigned (&v)[NC], unsigned (&ex)[N
   __syncthreads();
 }
 
-// Per tile: head and chunk-start counts.  Block 0 also zeroes what the emit pass appends to
-// (dense heads) and the counts no later kernel of the chain writes (no memset launches).
+// Per tile: head and chunk-start counts.  Block 0 also zeroes the counts no later kernel of the
+// chain writes (no memset launches).
 __global__ __launch_bounds__(kBlock) void rle_count_kernel(RleArgs a) {
   const int tile = blockIdx.x;
   Rle8 r;
@@ -150,7 +140,6 @@ __global__ __launch_bounds__(kBlock) void rle_count_kernel(RleArgs a) {
   if (threadIdx.x == 0) {
     a.tile_cnt[tile] = ((unsigned long long)tot[0] << 32) | tot[1];
     if (tile == 0) {
-      *a.dense_cnt = 0;
       a.counts[3] = 0;
       a.counts[5] = a.counts[6] = a.counts[7] = 0;
     }
@@ -174,10 +163,8 @@ __global__ __launch_bounds__(kBlock) void rle_emit_kernel(RleArgs a) {
   Rle8 r;
   rle_flags8(a, j0, r);
   unsigned v[2] = {0u, 0u}, ex[2], tot[2];
-  bool dn[kRleItems];
 #pragma unroll
   for (int q = 0; q < kRleItems; ++q) {
-    dn[q] = r.hd[q] && dense_head(a, j0 + q, r.k[q]);
     v[0] += r.hd[q];
     v[1] += r.cs[q];
   }
@@ -212,10 +199,6 @@ __global__ __launch_bounds__(kBlock) void rle_emit_kernel(RleArgs a) {
       a.uniq[s] = r.k[q];
       a.seg_start[s] = j;
       a.seg_chunk[s] = ch;
-      if (dn[q]) {  // dense rows as found; dense_select_kernel keeps the first kMaxDense in key order
-        const int slot = atomicAdd(a.dense_cnt, 1);
-        if (slot < a.dense_cap) a.dense_tmp[slot] = s;
-      }
     }
     if (r.cs[q]) {
       // a head chunk is the row's only one iff the row ends before the next CH-aligned cut
@@ -253,62 +236,6 @@ __global__ __launch_bounds__(kBlock) void rle_emit_kernel(RleArgs a) {
       if (a.sorted_x) a.sorted_x[j0 + q] = xv[q];
     }
   }
-}
-
-// Dense rows (MFMA backward, opt-in): the first kMaxDense of the found heads in key (= segment)
-// order, deterministic whatever order the tiles appended them in.  One workgroup: the cut value is
-// found by a bitwise binary search on counts, the kept ids (<= kMaxDense, distinct) ranked by
-// counting.
-__global__ __launch_bounds__(kBlock) void dense_select_kernel(RleArgs a) {
-  __shared__ int keep[kMaxDense];
-  __shared__ int red[kWavesPerBlock];
-  __shared__ int s_cut;
-  const int n = min(*a.dense_cnt, a.dense_cap);
-  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x >> 6;
-  auto count_le = [&](int x) {  // #entries <= x, block-wide
-    int c = 0;
-    for (int i = threadIdx.x; i < n; i += kBlock) c += a.dense_tmp[i] <= x;
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) c += __shfl_xor(c, o, kWave);
-    if (lane == 0) red[wv] = c;
-    __syncthreads();
-    int t = 0;
-    for (int w = 0; w < kWavesPerBlock; ++w) t += red[w];
-    __syncthreads();
-    return t;
-  };
-  // cut = smallest x with count_le(x) >= min(n, kMaxDense)
-  const int want = min(n, kMaxDense);
-  int lo = 0, hi = 0x7fffffff;
-  if (want > 0) {
-    while (lo < hi) {
-      const int mid = lo + ((hi - lo) >> 1);
-      if (count_le(mid) >= want) hi = mid; else lo = mid + 1;
-    }
-  }
-  if (threadIdx.x == 0) s_cut = lo;
-  __syncthreads();
-  const int cut = s_cut;
-  for (int i = threadIdx.x; i < n; i += kBlock) {
-    const int x = a.dense_tmp[i];
-    if (want > 0 && x <= cut) {
-      int rank = 0;
-      for (int j = 0; j < n; ++j) rank += a.dense_tmp[j] < x;
-      if (rank < kMaxDense) keep[rank] = x;
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < want; i += kBlock) a.dense_list[i] = keep[i];
-  if (threadIdx.x == 0) a.counts[3] = *a.dense_cnt;
-}
-
-// Flag every chunk of a listed dense row: the chunk kernel skips them (their
-// gradient comes from the MFMA path).
-__global__ __launch_bounds__(kBlock) void mark_dense_chunks_kernel(RleArgs a) {
-  const int nd = min(a.counts[3], kMaxDense);
-  if ((int)blockIdx.x >= nd) return;
-  const int u = a.dense_list[blockIdx.x];
-  for (int c = a.seg_chunk[u] + threadIdx.x; c < a.seg_chunk[u + 1]; c += kBlock) a.chunk_seg[c] |= kChunkDense;
 }
 
 static size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
@@ -358,17 +285,13 @@ static size_t sort_temp_bytes(int n, hipStream_t st) {
   return align_up(best);
 }
 
-// Dense-row candidates the RLE can list (dense_min >= kDenseMinFloor: at most n / kDenseMinFloor rows)
-constexpr int kDenseMinFloor = 32;
-static size_t dense_cap_for(int n) { return (size_t)n / kDenseMinFloor + 1; }
-
-// Workspace layout: [onesweep temp | dense_cnt (8 B), tile_cnt[ntiles] | dense_tmp]
+// Workspace layout: [onesweep temp | pad (8 B), tile_cnt[ntiles]]
 static size_t lb_bytes(int ntiles) { return 8 + 8 * (size_t)ntiles; }
 
 size_t dedup_workspace_bytes(int n) {
   if (n <= 0) return 256;
   const size_t ntiles = ((size_t)n + kRleTile - 1) / kRleTile;
-  return sort_temp_bytes(n, 0) + align_up(lb_bytes((int)ntiles)) + align_up(dense_cap_for(n) * sizeof(int)) + 256;
+  return sort_temp_bytes(n, 0) + align_up(lb_bytes((int)ntiles)) + 256;
 }
 
 struct DedupArgs {
@@ -394,8 +317,6 @@ struct DedupArgs {
   int payload_is_ex;       // payload carries the example index (sorted payload == sorted example)
   int ex_shift;            // > 0: the payload is the packed code (example << ex_shift | slot), see csr_rows
   const int* offsets;      // [B+1] (ex_shift > 0)
-  int dense_min;           // rows with >= dense_min occurrences go to the MFMA backward (0: off)
-  int* dense_list;         // [kMaxDense]
   void* ws;
   size_t ws_bytes;
 };
@@ -432,7 +353,7 @@ int launch_seg_index(int n_max, const uint32_t* uniq, const int* counts, int shi
 }
 
 int launch_dedup(const DedupArgs& a, hipStream_t st) {
-  // counts[0..3] = U, #chunks, #multi-chunk rows, #dense rows; counts[4] = the backward's
+  // counts[0..2] = U, #chunks, #multi-chunk rows; counts[4] = the backward's
   // hot-row count: both backward counters start at 0 here, on the dedup's stream (off the
   // compute stream's critical path), written by the RLE kernels
   if (a.n <= 0) {
@@ -447,24 +368,17 @@ int launch_dedup(const DedupArgs& a, hipStream_t st) {
   const size_t tmp = sort_temp_bytes(a.n, st);
   char* base = static_cast<char*>(a.ws);
   char* lb = base + tmp;
-  int* dense_tmp = reinterpret_cast<int*>(lb + align_up(lb_bytes(ntiles)));
-  if (tmp + align_up(lb_bytes(ntiles)) + align_up(dense_cap_for(a.n) * sizeof(int)) > a.ws_bytes) return -2;
-  if (a.dense_list && a.dense_min > 0 && a.dense_min < kDenseMinFloor) return -8;
+  if (tmp + align_up(lb_bytes(ntiles)) > a.ws_bytes) return -2;
 
   size_t sort_bytes = tmp;
   const hipError_t e = sort_pairs(a.ws, sort_bytes, a.keys, a.skeys, a.payload, a.spay, a.n, a.end_bit, st);
   if (e != hipSuccess) return (int)e;
-  RleArgs r{a.n, a.CH, ntiles, a.dense_list ? a.dense_min : 0, a.dense_list, a.skeys, a.spay, a.ex_shift,
-            a.offsets, reinterpret_cast<unsigned long long*>(lb + 8), dense_tmp, reinterpret_cast<int*>(lb),
-            (int)dense_cap_for(a.n), a.uniq, a.seg_start,
+  RleArgs r{a.n, a.CH, ntiles, a.skeys, a.spay, a.ex_shift,
+            a.offsets, reinterpret_cast<unsigned long long*>(lb + 8), a.uniq, a.seg_start,
             a.seg_chunk, a.chunk_start, a.chunk_seg, a.chunk_key, a.counts, a.inv, a.ex_of_occ, a.sorted_ex,
             a.vals, a.sorted_x};
   hipLaunchKernelGGL(rle_count_kernel, dim3(ntiles), dim3(kBlock), 0, st, r);
   hipLaunchKernelGGL(rle_emit_kernel, dim3(ntiles), dim3(kBlock), 0, st, r);
-  if (r.dense_min > 0) {
-    hipLaunchKernelGGL(dense_select_kernel, dim3(1), dim3(kBlock), 0, st, r);
-    hipLaunchKernelGGL(mark_dense_chunks_kernel, dim3(kMaxDense), dim3(kBlock), 0, st, r);
-  }
   return (int)hipGetLastError();
 }
 

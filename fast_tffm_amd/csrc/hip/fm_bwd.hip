@@ -96,10 +96,7 @@ struct BwdArgs {
   int* big_count;           // device scalar, zeroed by the launcher
   int* multi;               // [counts[2]] rows spanning more than one chunk (filled by the chunk kernel)
   int* counts_rw;           // == counts, writable (counts[2] = #multi, zeroed by the launcher)
-  const int* dense_list;    // [kMaxDense] dense rows (dedup), counts[3] of them; null: no dense path
-  float* dense_part;        // [gridDim(dense) * kMaxDense, Kp + 4] per-workgroup partial rows
-  int nex;                  // examples in the batch (dense path)
-  const uint8_t* dense_A;   // [nex, kMaxDense] occurrence counts of the dense rows (written by the forward)
+  int nex;                  // examples in the batch (r1 rows)
   SelfRows self;            // EMIT (row-sharded step): segments that are this rank's own table rows
   int chunk_grid;           // chunk kernel workgroup cap: 0 = per-row-width default, > 0 = this, < 0 = none
 };
@@ -373,13 +370,11 @@ __device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
     const int u = d_seg & kChunkSegMask;
     const bool single = (unsigned)d_seg & kChunkSingle;
     const bool first = d_seg & kChunkFirst;
-    const bool dense = d_seg & kChunkDense;
     if (ii + stride < i1) {
       c = cn;
       d_j0 = a.chunk_start[c]; d_j1 = a.chunk_start[c + 1]; d_seg = a.chunk_seg[c]; d_key = a.chunk_key[c];
       cn = ii + 2 * stride < i1 ? chunk_at(ii + 2 * stride) : 0;
     }
-    if (dense) continue;  // gradient from the MFMA path (fm_bwd_dense_kernel)
     const int len = j1 - j0;
     RowState<EPL> rs;
     if (single) {
@@ -656,184 +651,6 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_big_kernel(BwdArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// Dense rows on the matrix cores.  The hottest rows of a batch (the values of
-// Criteo's low-cardinality fields: the 256 densest cover ~47% of a Criteo-shaped
-// batch's occurrences, each present in >= 2.5% of the examples) make the
-// occurrence-gather backward fetch one random r1 row per occurrence.  For them the
-// reduction is a GEMM over example tiles instead:
-//     G[h, :] = sum_e A[e, h] * D[e, :],   D[e, :] = dpred_e * r1_e,
-// with A[e, h] = occurrences of dense row h in example e (binary features, so
-// x = 1; counted by the forward kernel into a coalesced [B, 256] byte matrix).
-// Each workgroup owns a contiguous example range and streams it in 64-example
-// tiles through LDS -- A's rows as they are (bytes, pitch 272: conflict-free
-// reads) and D = [dpred * r1 | dpred | 1] as fp32 rows -- and multiplies on
-// v_mfma_f32_16x16x4_f32: its operand maps (A[l&15][k = l>>4], B[k = l>>4][l&15])
-// read both tiles in their natural example-major layout, so nothing is transposed,
-// and f32-in MFMA is exact fp32 (an fmaf chain).  The two extra D columns give
-// every row's Sc = sum_e A dpred and its occurrence count in the same product.
-// r1 is read once, coalesced, instead of once per occurrence.  Per-workgroup
-// partial rows are summed in a fixed order by fm_bwd_dense_apply_kernel, which
-// applies the optimizer (deterministic).  (Round 2's version split D into three
-// bf16 parts for v_mfma_f32_16x16x32_bf16 and transposed both tiles through LDS:
-// 356 us next to the chunk kernel, profiles/r3.)
-// ---------------------------------------------------------------------------
-constexpr int kDenseE = 64;                 // examples per staged tile (16 MFMA k-steps of 4)
-constexpr int kDenseAP = kMaxDense + 16;    // LDS pitch of an A row in bytes (272: rows 4 banks apart)
-constexpr int kDenseWG = 256;               // workgroups of the dense kernel (partial rows)
-static_assert(kMaxDense == 4 * kWave, "dense rows: 4 per lane in the forward's count rows, 64 per wave here");
-
-typedef float floatx4 __attribute__((ext_vector_type(4)));
-
-template <int NB, bool R1B>  // 16-column blocks of D (Kp + 2 <= NB * 16); R1B: bf16 r1 (fp8 tables)
-__global__ __launch_bounds__(kBlock) void fm_bwd_dense_kernel(BwdArgs a) {
-  constexpr int NC = NB * 16;
-  __shared__ __align__(16) uint8_t At[kDenseE * kDenseAP];   // A rows of the tile
-  __shared__ __align__(16) float Dt[kDenseE * NC];           // D rows of the tile
-  const int nd = min(a.counts[3], kMaxDense);
-  if (nd == 0) return;
-  const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid >> 6;
-  const int per = ((a.nex + (int)gridDim.x - 1) / (int)gridDim.x + kDenseE - 1) / kDenseE * kDenseE;
-  const int e_begin = blockIdx.x * per, e_end = min(a.nex, e_begin + per);
-  const int Kp = a.Kp, kq = Kp / 4;
-  floatx4 acc[4][NB];
-#pragma unroll
-  for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) acc[rb][nb] = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (int e0 = e_begin; e0 < e_end; e0 += kDenseE) {
-    // A: 64 rows x 256 bytes, 64 bytes per thread (four 16-byte loads)
-    {
-      const int row = tid >> 2, seg = (tid & 3) * 64;
-      const int e = e0 + row;
-      uint4 q[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        q[k] = make_uint4(0u, 0u, 0u, 0u);
-        if (e < e_end) q[k] = *reinterpret_cast<const uint4*>(a.dense_A + (long long)e * kMaxDense + seg + 16 * k);
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) *reinterpret_cast<uint4*>(At + row * kDenseAP + seg + 16 * k) = q[k];
-    }
-    // D: row e = [dpred_e * r1_e (Kp) | dpred_e | 1 | 0 ...], a float4 quad per thread and step
-    for (int i = tid; i < kDenseE * (NC / 4); i += kBlock) {
-      const int row = i / (NC / 4), qd = i % (NC / 4);
-      const int e = e0 + row;
-      float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (e < e_end) {
-        const float d = a.dpred[e];
-        if (qd < kq) {
-          float r[4];
-          load_r1<typename std::conditional<R1B, fp8e4m3, float>::type, 4>(a.r1, (long long)e * Kp + 4 * qd, r);
-          f = make_float4(d * r[0], d * r[1], d * r[2], d * r[3]);
-        } else if (qd == kq) {
-          f = make_float4(d, 1.f, 0.f, 0.f);
-        }
-      }
-      *reinterpret_cast<float4*>(Dt + row * NC + 4 * qd) = f;
-    }
-    __syncthreads();
-    // G[h, n] += sum_e A[e, h] D[e, n]; wave wv owns dense rows 64 wv .. 64 wv + 63
-#pragma unroll 4
-    for (int ks = 0; ks < kDenseE / 4; ++ks) {
-      const int er = 4 * ks + (lane >> 4);
-      float af[4], bf[NB];
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb) af[rb] = (float)At[er * kDenseAP + 64 * wv + 16 * rb + (lane & 15)];
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb) bf[nb] = Dt[er * NC + 16 * nb + (lane & 15)];
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
-          acc[rb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[rb], bf[nb], acc[rb][nb], 0, 0, 0);
-    }
-    __syncthreads();
-  }
-  // partial rows [G (Kp) | Sc | Sc | count | -]: C/D map of the 16x16 tiles: col = lane & 15,
-  // row = (lane >> 4) * 4 + i
-  const int PS = Kp + 4;
-  float* part = a.dense_part + (long long)blockIdx.x * kMaxDense * PS;
-#pragma unroll
-  for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = 64 * wv + 16 * rb + (lane >> 4) * 4 + i, n = nb * 16 + (lane & 15);
-        if (m >= nd || n > Kp + 1) continue;
-        float* pr = part + (long long)m * PS;
-        const float v = acc[rb][nb][i];
-        if (n < Kp) {
-          pr[n] = v;
-        } else if (n == Kp) {
-          pr[Kp] = v;
-          pr[Kp + 1] = v;
-        } else {
-          pr[Kp + 2] = v;
-        }
-      }
-}
-
-// One workgroup per dense row: ordered sum of the per-workgroup partials
-// (4 stripes of workgroups, then the stripes in order), then the optimizer.
-template <int LPR, typename TV>
-__global__ __launch_bounds__(kBlock) void fm_bwd_dense_apply_kernel(BwdArgs a) {
-  const uint32_t sr = sr_step_seed(a.sr_counter);  // stochastic rounding seed (0: nearest)
-  constexpr int EPL = Frag<TV>::N;
-  __shared__ float4 red[kWavesPerBlock][kWave];
-  __shared__ float row[kWave * 4];
-  const int nd = min(a.counts[3], kMaxDense);
-  const int h = blockIdx.x;
-  if (h >= nd) return;
-  const int tid = threadIdx.x, q = tid & (kWave - 1), stripe = tid >> 6;
-  const int PS = a.Kp + 4, nq = PS / 4;
-  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (q < nq) {
-    for (int wg = stripe; wg < kDenseWG; wg += kWavesPerBlock) {
-      const float4 f = *reinterpret_cast<const float4*>(a.dense_part + ((long long)wg * kMaxDense + h) * PS + 4 * q);
-      s.x += f.x; s.y += f.y; s.z += f.z; s.w += f.w;
-    }
-  }
-  red[stripe][q] = s;
-  __syncthreads();
-  if (stripe == 0 && q < nq) {
-    float4 t = red[0][q];
-#pragma unroll
-    for (int k = 1; k < kWavesPerBlock; ++k) {
-      const float4 f = red[k][q];
-      t.x += f.x; t.y += f.y; t.z += f.z; t.w += f.w;
-    }
-    row[4 * q] = t.x; row[4 * q + 1] = t.y; row[4 * q + 2] = t.z; row[4 * q + 3] = t.w;
-  }
-  __syncthreads();
-  if (tid < LPR) {
-    const int t = tid;
-    const int nv = a.Kp / EPL;
-    const bool tact = t < nv;
-    const int tE = tact ? t : nv - 1;
-    float A[EPL];
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) A[k] = row[tE * EPL + k];
-    const int u = a.dense_list[h];
-    bwd_finalize<LPR, TV, EPL>(a, u, t, tact, tE, A, row[a.Kp], row[a.Kp + 1], a.seg_start[u + 1] - a.seg_start[u], sr);
-  }
-}
-
-// The dense kernel runs on its own stream, concurrently with the chunk kernel
-// (disjoint outputs; both only read r1 / dpred / the dedup plan): its latency-bound
-// phases (cursor search, occurrence scan) hide under the chunk kernel's traffic.
-static hipEvent_t dense_fork_event() {
-  static hipEvent_t ev = nullptr;
-  if (!ev) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-  return ev;
-}
-static hipEvent_t dense_join_event() {
-  static hipEvent_t ev = nullptr;
-  if (!ev) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-  return ev;
-}
-
 static int chunk_wg_per_cu(int lpr, int mode) {
   static const int env = [] {
     const char* e = getenv("FM_CHUNK_WG_PER_CU");
@@ -843,8 +660,7 @@ static int chunk_wg_per_cu(int lpr, int mode) {
   return mode == kBwdLocal && lpr <= 16 ? 3 : 0;
 }
 
-int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_unique, hipStream_t st,
-               hipStream_t dense_st) {
+int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_unique, hipStream_t st) {
   if (max_chunks <= 0) return 0;
   const int lpr = lanes_per_row(a.Kp, dtype);
   const int G = kWave / lpr;
@@ -866,38 +682,7 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   const int cap = a.chunk_grid != 0 ? a.chunk_grid
                   : a.mode != kBwdLocal ? -1 : (lpr == 16 ? 3072 : lpr == 4 ? 512 : -1);
   if (cap > 0 && g1 > cap) g1 = (cap + 7) / 8 * 8;
-  const bool dense = a.dense_list && a.dense_part && a.dense_A && a.piece < 0;
   if (a.piece >= 0 && a.n_owners > kMaxPieceOwners) return -6;
-  const bool fork = dense && dense_st && dense_st != st;
-  hipStream_t ds = fork ? dense_st : st;
-  if (dense) {
-    if (a.Kp > 128 || a.Kp % 4 != 0) return -5;
-    if (fork) {
-      (void)hipEventRecord(dense_fork_event(), st);
-      (void)hipStreamWaitEvent(ds, dense_fork_event(), 0);
-    }
-    const bool r1b = dtype == kFP8;  // (fp8 tables keep a bf16 r1: fm_common.h R1Bf16)
-#define FM_DENSE_LAUNCH(NB)                                                                          \
-  do {                                                                                               \
-    if (r1b)                                                                                         \
-      hipLaunchKernelGGL((fm_bwd_dense_kernel<NB, true>), dim3(kDenseWG), dim3(kBlock), 0, ds, a);   \
-    else                                                                                             \
-      hipLaunchKernelGGL((fm_bwd_dense_kernel<NB, false>), dim3(kDenseWG), dim3(kBlock), 0, ds, a);  \
-  } while (0)
-    switch ((a.Kp + 2 + 15) / 16) {  // D columns: Kp + dpred + 1
-      case 1: FM_DENSE_LAUNCH(1); break;
-      case 2: FM_DENSE_LAUNCH(2); break;
-      case 3: FM_DENSE_LAUNCH(3); break;
-      case 4: FM_DENSE_LAUNCH(4); break;
-      case 5: FM_DENSE_LAUNCH(5); break;
-      case 6: FM_DENSE_LAUNCH(6); break;
-      case 7: FM_DENSE_LAUNCH(7); break;
-      case 8: FM_DENSE_LAUNCH(8); break;
-      default: FM_DENSE_LAUNCH(9); break;
-    }
-#undef FM_DENSE_LAUNCH
-    if (fork) (void)hipEventRecord(dense_join_event(), ds);
-  }
   // (a software-pipelined variant that issued the next chunk's occurrence and row loads before
   // reducing the current one ran 367 -> 316 us alone but made the step slower twice:
   // profiles/r2/chunk_pipe_ab.txt, profiles/r3/fwd_prefetch_ab.txt; removed)
@@ -929,10 +714,6 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   }
   FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, a);
   FM_DISPATCH(dtype, lpr, fm_bwd_big_kernel, 1024, st, a);
-  if (dense) {
-    if (fork) (void)hipStreamWaitEvent(st, dense_join_event(), 0);
-    FM_DISPATCH(dtype, lpr, fm_bwd_dense_apply_kernel, kMaxDense, st, a);
-  }
   return (int)hipGetLastError();
 }
 

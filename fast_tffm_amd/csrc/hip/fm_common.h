@@ -21,11 +21,9 @@ constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
 
 // Chunk descriptor word (dedup.hip emit -> fm_bwd.hip): segment id | flags.
-constexpr int kChunkSegMask = (1 << 29) - 1;
-constexpr int kChunkDense = 1 << 29;         // the segment takes the MFMA (dense) backward path
+constexpr int kChunkSegMask = (1 << 30) - 1;
 constexpr int kChunkFirst = 1 << 30;         // first chunk of its segment
 constexpr unsigned kChunkSingle = 1u << 31;  // the segment's only chunk
-constexpr int kMaxDense = 256;               // rows on the MFMA backward path (= M of its GEMM)
 
 enum LossType : int { kLossNone = 0, kLossMse = 1, kLossLogistic = 2 };
 enum OptType : int { kOptAdagrad = 0, kOptFtrl = 1, kOptSgd = 2 };

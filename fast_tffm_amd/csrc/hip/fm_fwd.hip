@@ -33,14 +33,6 @@ struct FwdArgs {
   float* loss_partial;  // [gridDim.x] or nullptr
   float* reg_partial;   // [2*gridDim.x] (sum |v|^2, sum w^2) or nullptr
   const float* bias;    // [1] global bias (optional model extension) or nullptr
-  // Dense-row occurrence matrix for the MFMA backward (fm_bwd.hip): the forward already
-  // walks every example's rows, so it counts, per example, the occurrences of each of the
-  // batch's dense rows (listed by the dedup, which ran before this forward) and writes them
-  // as one coalesced kMaxDense-byte row.  Null dense_A: off.
-  const int* dense_list;   // [kMaxDense] segment ids of the dense rows
-  const int* dense_uniq;   // segment -> row key (local step: uniq = table rows) or null (rows ARE segment ids)
-  const int* dense_count;  // device scalar: number of dense rows (capped at kMaxDense here)
-  uint8_t* dense_A;        // [B, kMaxDense] occurrence counts (saturated at 255)
   SelfRows self;           // row-sharded step: segments read from this rank's own table rows
   // Segment lookup (row-sharded step, dedup.hip seg_index_kernel): rows[] hold the shard keys
   // and each occurrence's segment is found through the bucket index instead of an inverse map.
@@ -67,21 +59,6 @@ __device__ inline int seg_lookup(const FwdArgs& a, int k) {
 #define FM_FWD_SPECIALIZE 1
 #endif
 constexpr int kSelfBit = (int)0x80000000u;   // row index tag: this rank's own table row (SelfRows)
-constexpr int kDenseHash = 4 * kMaxDense;  // open-addressing table of the dense keys (LDS, load <= 1/4)
-
-__device__ inline int dense_hash(int key) { return (int)(((uint32_t)key * 0x9E3779B1u) >> 22) & (kDenseHash - 1); }
-
-__device__ inline int dense_probe(const int* hkey, const int* hval, int key) {
-  int slot = dense_hash(key);
-  for (int p = 0; p < kDenseHash; ++p) {
-    const int k = hkey[slot];
-    if (k == key) return hval[slot];
-    if (k == -1) return -1;
-    slot = (slot + 1) & (kDenseHash - 1);
-  }
-  return -1;
-}
-
 // Rows of one example kept in flight per lane group: enough to cover a
 // Criteo-shaped example (39 features) in one round for K=64 (G=4 -> 10 row
 // loads per lane) while bounding VGPRs for large K.
@@ -161,20 +138,13 @@ constexpr int fwd_unroll() {
                      : FwdUnroll<kWave / LPR>::v;
 }
 
-// LDS of the dense-row counting (FM_DENSE_BWD): only the dense instantiation carries it
-template <bool DENSE> struct DenseLds {
-  int hkey[kDenseHash], hval[kDenseHash];
-  unsigned dcnt[kWavesPerBlock][kMaxDense];
-};
-template <> struct DenseLds<false> {};
-
 // SH: the row-sharded step's features (self rows, segment lookup: a tagged row index selects the
 // table, rows[] may be keys).  The local step's instantiation (SH = false) addresses every row as
 // base + row * stride with one 32 x 32 -> 64-bit multiply-add and reads the broadcast pairs with
 // precomputed ds_bpermute offsets: per row group ~5 address / index VALU instructions instead of
 // ~16 (the tag test, base / stride selects and a 64-bit stride multiply), on a kernel the PMC
 // table shows 62% (k64 fp32) / 82% (k128 fp8) VALU-busy (profiles/r4/pmc_*.txt).
-template <int LPR, typename TV, bool DENSE, bool SH = true>
+template <int LPR, typename TV, bool SH>
 __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
   using F = Frag<TV>;
   constexpr int EPL = F::N;
@@ -197,28 +167,11 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
   const int nwaves = gridDim.x * kWavesPerBlock;
   const bool want_reg = a.reg_partial != nullptr;
   // (segment lookup + self rows: the key range of the own segments, read once)
-  const bool self_key = SH && self_on && a.seg_idx != nullptr && !DENSE;
+  const bool self_key = SH && self_on && a.seg_idx != nullptr;
   const int self_kmin = self_key ? a.self.keys[a.self.u0] : 0;
   const int self_kmax = self_key ? a.self.keys[a.self.u1 - 1] : -1;
 
-  // dense rows (the dense instantiation only): key -> dense index hash (built once per
-  // workgroup) and per-wave counters
-  __shared__ DenseLds<DENSE> dl;
   const int wv = threadIdx.x >> 6;
-  if constexpr (DENSE) {
-    const int nd = min(*a.dense_count, kMaxDense);
-    for (int k = threadIdx.x; k < kDenseHash; k += kBlock) dl.hkey[k] = -1;
-    for (int k = threadIdx.x; k < kWavesPerBlock * kMaxDense; k += kBlock) (&dl.dcnt[0][0])[k] = 0u;
-    __syncthreads();
-    for (int h = threadIdx.x; h < nd; h += kBlock) {
-      const int sg = a.dense_list[h];
-      const int key = a.dense_uniq ? a.dense_uniq[sg] : sg;
-      int slot = dense_hash(key);
-      while (atomicCAS(&dl.hkey[slot], -1, key) != -1) slot = (slot + 1) & (kDenseHash - 1);
-      dl.hval[slot] = h;  // (keys are distinct; read only after the barrier)
-    }
-    __syncthreads();
-  }
 
   float loss_acc = 0.f, regv_acc = 0.f, regw_acc = 0.f;
   // Software pipeline over the wave's examples i, i + nwaves, ...: an example's chain is CSR
@@ -275,7 +228,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
     float s2n = 0.f;
     for (int base = s; base < e; base += kWave) {
       const int m = min(kWave, e - base);
-      int my_row = 0, my_seg = 0;
+      int my_row = 0;
       float my_x = 0.f, my_w = 0.f, my_s = 1.f, my_n2 = 0.f;
       if (kPrefetch && base == s) {
         my_row = p_row;
@@ -284,24 +237,20 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
         pairs(base, m, my_row, my_x);
       }
       if (kNorm && !SH && lane < m) {  // [w, scale, |v|^2, pad]: one 16-byte load (w_stride 4, host-checked)
-        my_seg = my_row;
         const float4 wr = *reinterpret_cast<const float4*>(a.w + (uint64_t)(uint32_t)my_row * 4u);
         my_w = wr.x;
         my_s = wr.y;
         my_n2 = wr.z;
       } else if (!SH && lane < m) {
-        my_seg = my_row;
         my_w = a.w[(long long)my_row * a.w_stride];
         my_s = row_scale<TV>(a.w, my_row, a.w_stride);
       } else if (lane < m) {
-        my_seg = my_row;
         // segment lookup mode: rows[] are keys; an own row is known by its key alone (the self
         // segments are exactly the batch's keys in [self_kmin, self_kmax]), so it needs neither
-        // the lookup nor the segment's key load -- at world 1 every row (dense counting needs
-        // the segment: then every key is looked up)
+        // the lookup nor the segment's key load -- at world 1 every row
         const int key = my_row;
         const bool own_key = self_key && key >= self_kmin && key <= self_kmax;
-        if (SH && a.seg_idx && !own_key) my_seg = my_row = seg_lookup(a, key);
+        if (SH && a.seg_idx && !own_key) my_row = seg_lookup(a, key);
         // the linear weight (and fp8 scale, same cache line) of occurrence `lane`, one
         // lane-parallel load per 64 occurrences instead of one per row group: the w loads
         // were ~45% of the kernel's VMEM instructions with the TA 72% busy
@@ -317,12 +266,6 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
           my_w = a.w[(long long)my_row * a.w_stride];
           my_s = row_scale<TV>(a.w, my_row, a.w_stride);
           if constexpr (kNorm) my_n2 = a.w[(long long)my_row * a.w_stride + kFp8Norm];
-        }
-      }
-      if constexpr (DENSE) {
-        if (lane < m) {
-          const int h = dense_probe(dl.hkey, dl.hval, my_seg);
-          if (h >= 0) atomicAdd(&dl.dcnt[wv][h], 1u);  // integer: order-independent
         }
       }
       for (int q = 0; q < m; q += G * UNR) {
@@ -394,18 +337,6 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
         if (want_reg) rv += my_n2;
       }
     }
-    if constexpr (DENSE) {  // flush this example's dense-row counts: 4 per lane, one coalesced row
-      // (LDS instructions of one wave complete in issue order, and the compiler keeps these
-      // reads after the possibly-aliasing atomics above)
-      uint32_t packed = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        unsigned c = dl.dcnt[wv][4 * lane + j];
-        dl.dcnt[wv][4 * lane + j] = 0u;
-        packed |= (c > 255u ? 255u : c) << (8 * j);
-      }
-      reinterpret_cast<uint32_t*>(a.dense_A + (long long)i * kMaxDense)[lane] = packed;
-    }
     float part = 0.f;
 #pragma unroll
     for (int k = 0; k < EPL; ++k) {
@@ -468,22 +399,13 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
 template <int LPR, typename TV>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(fwd_local_min_waves<LPR, TV>())))
 void fm_fwd_kernel(FwdArgs a) {
-  fwd_body<LPR, TV, false, false>(a);
+  fwd_body<LPR, TV, false>(a);
 }
 
 // The row-sharded step's forward (self rows, segment lookup).
 template <int LPR, typename TV>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(fwd_min_waves<LPR, TV>())))
 void fm_fwd_shard_kernel(FwdArgs a) {
-  fwd_body<LPR, TV, false, true>(a);
-}
-
-// The forward that also counts every example's dense-row occurrences (FM_DENSE_BWD's MFMA
-// backward; fp32 r1, Kp <= 128): a separate instantiation keeps the counting's LDS and branches
-// out of the default kernel.
-template <int LPR, typename TV>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(fwd_min_waves<LPR, TV>())))
-void fm_fwd_dense_kernel(FwdArgs a) {
   fwd_body<LPR, TV, true>(a);
 }
 
@@ -530,26 +452,6 @@ int fwd_grid(int B) { return fill_grid(B, kWavesPerBlock, 4096); }
 int launch_fwd(const FwdArgs& a, int dtype, int grid, hipStream_t st) {
   if (a.B <= 0) return 0;
   const int lpr = lanes_per_row(a.Kp, dtype);
-  if (a.dense_A) {
-    if (dtype == kFP8 || lpr > 32) return -5;
-#define FM_FWD_DENSE(TV)                                                                                  \
-  switch (lpr) {                                                                                          \
-    case 1: hipLaunchKernelGGL((fm_fwd_dense_kernel<1, TV>), dim3(grid), dim3(kBlock), 0, st, a); break;   \
-    case 2: hipLaunchKernelGGL((fm_fwd_dense_kernel<2, TV>), dim3(grid), dim3(kBlock), 0, st, a); break;   \
-    case 4: hipLaunchKernelGGL((fm_fwd_dense_kernel<4, TV>), dim3(grid), dim3(kBlock), 0, st, a); break;   \
-    case 8: hipLaunchKernelGGL((fm_fwd_dense_kernel<8, TV>), dim3(grid), dim3(kBlock), 0, st, a); break;   \
-    case 16: hipLaunchKernelGGL((fm_fwd_dense_kernel<16, TV>), dim3(grid), dim3(kBlock), 0, st, a); break; \
-    case 32: hipLaunchKernelGGL((fm_fwd_dense_kernel<32, TV>), dim3(grid), dim3(kBlock), 0, st, a); break; \
-    default: return -5;                                                                                   \
-  }
-    if (dtype == kBF16) {
-      FM_FWD_DENSE(__hip_bfloat16)
-    } else {
-      FM_FWD_DENSE(float)
-    }
-#undef FM_FWD_DENSE
-    return (int)hipGetLastError();
-  }
   // (capping the forward's workgroups per CU through dynamic LDS, as the chunk backward does, tied
   // on k64 fp32: profiles/r4/wg_per_cu_ab.txt)
   // (the local fp8 forward reads [w, scale, |v|^2, pad] rows: Table's layout, w_stride 4)

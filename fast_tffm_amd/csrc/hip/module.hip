@@ -24,7 +24,6 @@ using u64 = std::uintptr_t;
 #include "fm_bwd.hip"
 #include "fm_fwd.hip"
 #include "dedup.hip"
-#include "hdedup.hip"
 #include "shard.hip"
 #include "init.hip"
 #include "parse.hip"
@@ -58,16 +57,6 @@ fm::SelfRows self_rows(const std::vector<long long>& f) {
   return r;
 }
 
-fm::HdDict hd_dict(const std::vector<long long>& f) {
-  if (f.size() != 6) throw std::invalid_argument("hot dictionary: [keys, n, ht_key, ht_idx, sel, meta]");
-  for (long long x : f)
-    if (!x) throw std::invalid_argument("hot dictionary: null buffer");
-  fm::HdDict d;
-  d.keys = P<int>((u64)f[0]); d.n = P<int>((u64)f[1]); d.ht_key = P<int>((u64)f[2]); d.ht_idx = P<int>((u64)f[3]);
-  d.sel = P<int>((u64)f[4]); d.meta = P<int>((u64)f[5]);
-  return d;
-}
-
 fm::OptParams opt_params(int type, float lr, float l1, float l2, float beta) {
   fm::OptParams o;
   o.type = type; o.lr = lr; o.l1 = l1; o.l2 = l2; o.beta = beta;
@@ -96,17 +85,13 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       "fwd",
       [](int B, u64 offsets, u64 rows, u64 vals, u64 v, long long v_stride, u64 w, long long w_stride, int Kp,
          int dtype, u64 labels, u64 weights, int loss_type, float grad_scale, u64 pred, u64 r1, u64 dpred,
-         u64 loss_partial, u64 reg_partial, int grid, u64 stream, u64 bias, u64 dense_list, u64 dense_uniq,
-         u64 dense_count, u64 dense_A, const std::vector<long long>& self, u64 seg_idx, u64 seg_keys,
-         int seg_shift) {
+         u64 loss_partial, u64 reg_partial, int grid, u64 stream, u64 bias, const std::vector<long long>& self,
+         u64 seg_idx, u64 seg_keys, int seg_shift) {
         fm::FwdArgs a{};
         a.seg_idx = P<const int>(seg_idx); a.seg_keys = P<const int>(seg_keys); a.seg_shift = seg_shift;
         if (a.seg_idx && (!a.seg_keys || seg_shift < 0 || seg_shift > 31))
           throw std::invalid_argument("fm_fwd: segment lookup needs the sorted keys and a shift in [0, 31]");
         a.self = self_rows(self);
-        a.dense_list = P<const int>(dense_list); a.dense_uniq = P<const int>(dense_uniq);
-        a.dense_count = P<const int>(dense_count); a.dense_A = P<uint8_t>(dense_A);
-        if (a.dense_A && (!a.dense_list || !a.dense_count)) throw std::runtime_error("fm_fwd: dense_A needs the dense list");
         a.B = B; a.offsets = P<const int>(offsets); a.rows = P<const int>(rows);
         a.vals = P<const float>(vals); a.v = P<const void>(v); a.v_stride = v_stride;
         a.w = P<const float>(w); a.w_stride = w_stride; a.Kp = Kp;
@@ -120,7 +105,6 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("w"), py::arg("w_stride"), py::arg("Kp"), py::arg("dtype"), py::arg("labels"), py::arg("weights"),
       py::arg("loss_type"), py::arg("grad_scale"), py::arg("pred"), py::arg("r1"), py::arg("dpred"),
       py::arg("loss_partial"), py::arg("reg_partial"), py::arg("grid"), py::arg("stream"), py::arg("bias") = 0,
-      py::arg("dense_list") = 0, py::arg("dense_uniq") = 0, py::arg("dense_count") = 0, py::arg("dense_A") = 0,
       py::arg("self_rows") = std::vector<long long>{}, py::arg("seg_idx") = 0, py::arg("seg_keys") = 0,
       py::arg("seg_shift") = 0);
 
@@ -140,10 +124,9 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
          u64 sorted_ex, int ex_shift, u64 sorted_x, u64 dpred, u64 r1, int Kp, u64 v, long long v_stride, u64 w,
          long long w_stride, u64 s0v, u64 s1v, long long s_stride, u64 s0w, u64 s1w, float reg_v, float reg_w,
          int opt_type, float lr, float l1, float l2, float beta, u64 grad_out, long long g_stride, u64 partial,
-         u64 big_list, u64 big_count, u64 multi, u64 dense_list,
-         u64 dense_part, int nex, u64 dense_stream, int dtype,
+         u64 big_list, u64 big_count, u64 multi, int nex, int dtype,
          long long max_chunks, long long max_unique, u64 stream, int g_wcol, int g_bf16, u64 sr_counter,
-         int counters_ready, u64 seg_bounds, int piece, int n_owners, u64 dense_A,
+         int counters_ready, u64 seg_bounds, int piece, int n_owners,
          const std::vector<long long>& self, int chunk_grid) {
         fm::BwdArgs a{};
         a.chunk_grid = chunk_grid;
@@ -152,7 +135,6 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
           throw std::runtime_error("fm_bwd: self-row keys must be the dedup's unique keys");
         if (a.self.u1 > a.self.u0 && (mode != 1 || !s0v || !s0w))
           throw std::runtime_error("fm_bwd: self rows are an EMIT-mode path and need the table's optimizer state");
-        a.dense_A = P<const uint8_t>(dense_A);
         a.counters_ready = counters_ready;
         a.seg_bounds = P<const int>(seg_bounds); a.piece = piece; a.n_owners = n_owners;
         a.sr_counter = P<const int>(sr_counter);
@@ -170,8 +152,8 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
         a.g_bf16 = g_bf16; a.partial = P<float>(partial);
         a.big_list = P<int>(big_list); a.big_count = P<int>(big_count); a.multi = P<int>(multi);
         a.counts_rw = P<int>(counts);
-        a.dense_list = P<const int>(dense_list); a.dense_part = P<float>(dense_part); a.nex = nex;
-        check(fm::launch_bwd(a, dtype, max_chunks, max_unique, S(stream), S(dense_stream)), "fm_bwd");
+        a.nex = nex;
+        check(fm::launch_bwd(a, dtype, max_chunks, max_unique, S(stream)), "fm_bwd");
       },
       py::arg("mode"), py::arg("counts"), py::arg("chunk_start"), py::arg("chunk_seg"), py::arg("chunk_key"),
       py::arg("seg_start"),
@@ -180,11 +162,10 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("s0v"), py::arg("s1v"), py::arg("s_stride"), py::arg("s0w"), py::arg("s1w"), py::arg("reg_v"),
       py::arg("reg_w"), py::arg("opt_type"), py::arg("lr"), py::arg("l1"), py::arg("l2"), py::arg("beta"),
       py::arg("grad_out"), py::arg("g_stride"), py::arg("partial"), py::arg("big_list"), py::arg("big_count"),
-      py::arg("multi"), py::arg("dense_list"),
-      py::arg("dense_part"), py::arg("nex"), py::arg("dense_stream"), py::arg("dtype"),
+      py::arg("multi"), py::arg("nex"), py::arg("dtype"),
       py::arg("max_chunks"), py::arg("max_unique"), py::arg("stream"), py::arg("g_wcol") = -1,
       py::arg("g_bf16") = 0, py::arg("sr_counter") = 0, py::arg("counters_ready") = 0, py::arg("seg_bounds") = 0,
-      py::arg("piece") = -1, py::arg("n_owners") = 0, py::arg("dense_A") = 0,
+      py::arg("piece") = -1, py::arg("n_owners") = 0,
       py::arg("self_rows") = std::vector<long long>{}, py::arg("chunk_grid") = 0);
 
   m.def("dedup_workspace_bytes", &fm::dedup_workspace_bytes, py::arg("n"));
@@ -192,8 +173,8 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       "dedup",
       [](int n, int end_bit, int CH, u64 keys, u64 payload, u64 skeys, u64 spay, u64 uniq, u64 seg_start,
          u64 seg_chunk, u64 chunk_start, u64 chunk_seg, u64 chunk_key, u64 counts, u64 inv, u64 ex_of_occ,
-         u64 sorted_ex, u64 vals, u64 sorted_x, int payload_is_ex, int ex_shift, u64 offsets, int dense_min,
-         u64 dense_list, u64 ws, size_t ws_bytes, u64 stream) {
+         u64 sorted_ex, u64 vals, u64 sorted_x, int payload_is_ex, int ex_shift, u64 offsets, u64 ws,
+         size_t ws_bytes, u64 stream) {
         if (CH < 1 || CH > fm::kMaxCH) throw std::invalid_argument("CH must be in [1, MAX_CH]");
         fm::DedupArgs a;
         a.n = n; a.end_bit = end_bit; a.CH = CH; a.keys = P<const uint32_t>(keys);
@@ -204,7 +185,6 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
         a.inv = P<int>(inv); a.ex_of_occ = P<const int>(ex_of_occ); a.sorted_ex = P<int>(sorted_ex);
         a.vals = P<const float>(vals); a.sorted_x = P<float>(sorted_x); a.ws = P<void>(ws);
         a.payload_is_ex = payload_is_ex; a.ex_shift = ex_shift; a.offsets = P<const int>(offsets);
-        a.dense_min = dense_min; a.dense_list = P<int>(dense_list);
         a.ws_bytes = ws_bytes;
         check(fm::launch_dedup(a, S(stream)), "dedup");
       },
@@ -213,45 +193,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("chunk_seg"), py::arg("chunk_key"), py::arg("counts"), py::arg("inv"), py::arg("ex_of_occ"),
       py::arg("sorted_ex"),
       py::arg("vals"), py::arg("sorted_x"), py::arg("payload_is_ex"), py::arg("ex_shift"), py::arg("offsets"),
-      py::arg("dense_min"), py::arg("dense_list"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"));
-  // hot-dictionary dedup (hdedup.hip): the dictionary travels as [keys, n, ht_key, ht_idx, sel, meta]
-  m.def("hd_workspace_bytes", &fm::hd_workspace_bytes, py::arg("n"));
-  m.attr("HD_MAX_H") = fm::kHdMaxH;
-  m.attr("HD_SLOTS") = fm::kHdSlots;
-  // phase 1 (classify, cold count -> hc[0], hot counts) / phase 2 (cold sort of n_c pairs, merge, plan)
-  m.def(
-      "dedup_hd",
-      [](int phase, int n_c, int n, int kb, int CH, u64 keys, u64 payload, const std::vector<long long>& dict, u64 ws,
-         size_t ws_bytes, u64 hc, u64 skeys, u64 spay, u64 uniq, u64 seg_start, u64 seg_chunk, u64 chunk_start,
-         u64 chunk_seg, u64 chunk_key, u64 counts, u64 stream) {
-        fm::HdLaunch p{};
-        p.n = n; p.kb = kb; p.CH = CH; p.keys = P<const uint32_t>(keys); p.pay = P<const int>(payload);
-        p.d = hd_dict(dict);
-        p.ws = P<void>(ws); p.ws_bytes = ws_bytes; p.hc = P<int>(hc);
-        p.skeys = P<uint32_t>(skeys); p.spay = P<int>(spay); p.uniq = P<uint32_t>(uniq);
-        p.seg_start = P<int>(seg_start); p.seg_chunk = P<int>(seg_chunk); p.chunk_start = P<int>(chunk_start);
-        p.chunk_seg = P<int>(chunk_seg); p.chunk_key = P<int>(chunk_key); p.counts = P<int>(counts);
-        if (!p.keys || !p.pay || !p.spay || !p.uniq || !p.seg_start || !p.seg_chunk || !p.chunk_start ||
-            !p.chunk_seg || !p.chunk_key || !p.counts || !p.ws || !p.hc)
-          throw std::invalid_argument("dedup_hd: null buffer");
-        if (phase == 1) check(fm::launch_hd_phase1(p, S(stream)), "dedup_hd phase 1");
-        else if (phase == 2) check(fm::launch_hd_phase2(p, n_c, S(stream)), "dedup_hd phase 2");
-        else throw std::invalid_argument("dedup_hd: phase 1 or 2");
-      },
-      py::arg("phase"), py::arg("n_c"), py::arg("n"), py::arg("kb"), py::arg("CH"), py::arg("keys"),
-      py::arg("payload"), py::arg("dict"), py::arg("ws"), py::arg("ws_bytes"), py::arg("hc"), py::arg("skeys"),
-      py::arg("spay"), py::arg("uniq"), py::arg("seg_start"), py::arg("seg_chunk"), py::arg("chunk_start"),
-      py::arg("chunk_seg"), py::arg("chunk_key"), py::arg("counts"), py::arg("stream"));
-  m.def(
-      "hd_dict_refresh",
-      [](const std::vector<long long>& dict, u64 counts, u64 seg_start, u64 uniq, int n_max, u64 stream) {
-        check(fm::launch_hd_dict_refresh(hd_dict(dict), P<const int>(counts), P<const int>(seg_start),
-                                         P<const uint32_t>(uniq), n_max, S(stream)),
-              "hd_dict_refresh");
-      },
-      py::arg("dict"), py::arg("counts"), py::arg("seg_start"), py::arg("uniq"), py::arg("n_max"), py::arg("stream"));
-  m.attr("MAX_DENSE") = fm::kMaxDense;
-  m.attr("DENSE_WG") = fm::kDenseWG;
+      py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"));
 
   m.def(
       "gather_rows",

@@ -100,9 +100,6 @@ class _Workspace:
             self.pred = torch.empty(cap, dtype=torch.float32, device=dev)
             self.dpred = torch.empty(cap, dtype=torch.float32, device=dev)
             self.r1 = torch.empty((cap, Kp), dtype=self.r1_dtype, device=dev)
-            # dense-row occurrence counts (forward -> MFMA backward), GPU only
-            self._dense_A = (torch.empty((cap, K.MAX_DENSE), dtype=torch.uint8, device=dev)
-                             if dev.type == "cuda" else None)
             self.cap_b = cap
         if nnz > self.cap_n:
             cap = max(nnz, int(self.cap_n * 1.25), 1)
@@ -111,19 +108,8 @@ class _Workspace:
             self.bwd_partial = (torch.empty((K.partial_rows(cap, self.CH), Kp + 4), dtype=torch.float32, device=dev)
                                 if dev.type == "cuda" else None)
             self.cap_n = cap
-        if not hasattr(self, "dense_part"):
-            self.dense_part = (torch.empty((K.DENSE_WG * K.MAX_DENSE, Kp + 4), dtype=torch.float32, device=dev)
-                               if dev.type == "cuda" and Kp <= 128 else None)
         if not hasattr(self, "fwd_partial"):
             self.fwd_partial = torch.zeros(3 * 4096, dtype=torch.float32, device=dev)
-
-    def dense_counts(self, B: int) -> torch.Tensor:
-        """[B, MAX_DENSE] uint8 dense-row occurrence counts (written by the forward, read by the
-        MFMA backward), grown on demand."""
-        if B > self.cap_b:
-            self.ensure(B, 0)
-        return self._dense_A[:B]
-
 
 class _LocalSlot:
     """Double-buffered dedup workspace of the local lookahead pipeline."""
@@ -303,9 +289,6 @@ class FactorizationMachine:
         self._lpending2 = None
         self._llast = 2
         self._ring = None
-        # hot-row dictionary of the GPU dedup (hip/hdedup.hip): the frequent rows of earlier plans skip
-        # the radix sort (FM_DEDUP=onesweep: every occurrence sorted); plans are the same either way
-        self._hot_dict = K.HotDict(self.device) if self.device.type == "cuda" and mode == "local" else None
         self._graph = None
         self._graph_pool: list[_GraphedStep] = []
         self._exchange = None
@@ -367,7 +350,6 @@ class FactorizationMachine:
         self._lpending = self._lpending2 = None
         self._lslots = [_LocalSlot(), _LocalSlot(), _LocalSlot()]
         self._side = None
-        self._dense_st = None
         if self.device.type == "cuda" and torch.cuda.is_initialized():
             torch.cuda.synchronize(self.device)
 
@@ -484,15 +466,6 @@ class FactorizationMachine:
         self.global_step += 1
         return out
 
-    def _dense_stream(self):
-        """Stream of the MFMA dense-row backward (forked from / joined into the compute stream);
-        None (FM_DENSE_FORK=0): it runs on the compute stream before the chunk kernel."""
-        if os.environ.get("FM_DENSE_FORK", "1") == "0":
-            return None
-        if getattr(self, "_dense_st", None) is None:
-            self._dense_st = torch.cuda.Stream(self.device)
-        return self._dense_st
-
     def _side_stream(self):
         if self._side is None:
             self._side = side_stream(self.device)
@@ -515,9 +488,7 @@ class FactorizationMachine:
                 sb = self._slot_bits(b)
                 ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz, slot_bits=sb)
                 dd = K.dedup(rows, ws=ws.dd, key_bits=bits_for(self.table.rows), ex_of_occ=ex, vals=b.vals,
-                             num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets,
-                             dense_min=0,  # (runs beside the forward, which counts dense rows: off here)
-                             hot_dict=self._hot_dict, want_skeys=False)
+                             num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets)
         else:
             ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz)
         with roctx_range("fwd"):
@@ -533,8 +504,7 @@ class FactorizationMachine:
         rv, rw = self.reg_coeffs
         with roctx_range("bwd+update"):
             K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
-                          reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, dense_part=ws.dense_part,
-                          dense_stream=self._dense_stream() if gpu else None, sr_counter=self.sr_tick())
+                          reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, sr_counter=self.sr_tick())
         return StepOut(fo.finish_loss(), b.B)
 
     # ------------------------------------------------------------------
@@ -577,29 +547,23 @@ class FactorizationMachine:
         kb = bits_for(self.table.rows)
         ex = K.csr_rows(b.offsets, out=slot.dd.ex_of_occ[: b.nnz], nnz=b.nnz, slot_bits=sb)
         dd = K.dedup(rows, ws=slot.dd, key_bits=kb, ex_of_occ=ex, vals=b.vals,
-                     num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets,
-                     dense_min=K.dense_min_for(b.B, self.Kp, cfg.dedup_chunk, table_dtype=self.table.v.dtype,
-                                               has_vals=b.vals is not None,
-                                               max_feats=b.max_feats),
-                     hot_dict=self._hot_dict, want_skeys=False)
+                     num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets)
         return rows, dd
 
     def _fwd_bwd_local(self, b: Batch, rows: torch.Tensor, dd) -> StepOut:
         """Forward + loss + backward/update of ``b`` on the current stream (dedup ``dd`` ready)."""
         ws, cfg = self.ws, self.cfg
-        dA = ws.dense_counts(b.B) if dd.dense_list is not None else None
         rv, rw = self.reg_coeffs
         with roctx_range("fwd"):
             fo = K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,
                               weights=b.weights, loss=cfg.loss_type, grad_scale=self.grad_scale(b.B), want_r1=True,
                               pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
-                              threads=cfg.threads, bias=self.gbias, dense=dd, dense_A=dA, defer_loss=True)
+                              threads=cfg.threads, bias=self.gbias, defer_loss=True)
             self.bias_step(fo.dpred)
         with roctx_range("bwd+update"):
             K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
-                          reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, dense_part=ws.dense_part,
-                          dense_stream=self._dense_stream(),
-                          sr_counter=self.sr_tick(), dense_A=dA)
+                          reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads,
+                          sr_counter=self.sr_tick())
         return StepOut(fo.finish_loss(), b.B)
 
     def _local_lookahead_step(self, b: Batch, next_batch: Batch | None, next2: Batch | None = None) -> StepOut:

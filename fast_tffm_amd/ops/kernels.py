@@ -180,10 +180,8 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
                want_r1: bool = True, want_reg: bool = False, pred: torch.Tensor | None = None,
                r1: torch.Tensor | None = None, dpred: torch.Tensor | None = None,
                partial: torch.Tensor | None = None, threads: int = 0,
-               bias: torch.Tensor | None = None, dense: "DedupOut | None" = None,
-               dense_A: torch.Tensor | None = None, dense_by_segment: bool = False,
-               self_rows: SelfRows | None = None, seg_lookup: "SegIndex | None" = None,
-               defer_loss: bool = False) -> FwdOut:
+               bias: torch.Tensor | None = None, self_rows: SelfRows | None = None,
+               seg_lookup: "SegIndex | None" = None, defer_loss: bool = False) -> FwdOut:
     """FM score of a CSR batch (reference FmScorer, cc/fm_scorer_op.h:101-140), fused with the loss.
 
     pred_i = sum_j x_j w_j + 1/2 sum_k [(sum_j x_j v_jk)^2 - sum_j x_j^2 v_jk^2]  (+ bias[0], optional
@@ -191,10 +189,6 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
     With ``loss`` in {mse, logistic} also returns the summed weighted loss and
     ``dpred = grad_scale * dL_i/dpred_i``.
 
-    ``dense`` (GPU, the batch's dedup with a dense-row list) and ``dense_A`` ([B, MAX_DENSE]
-    uint8): also count every example's occurrences of the dense rows into ``dense_A`` for the
-    MFMA backward; ``rows`` are table rows (``dense.uniq`` maps segments to them) or, with
-    ``dense_by_segment``, the segment ids themselves (the sharded step's inverse map).
     ``self_rows`` (GPU, ``rows`` = segment ids): segments in its range read this rank's table.
     ``seg_lookup`` (GPU): ``rows`` are the dedup's keys and every occurrence's segment (its
     row of ``v``) is found through the bucket index (``seg_index``) instead of an inverse map.
@@ -244,12 +238,6 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
         lp = partial[:grid]
         rp = partial[grid:3 * grid]
         dkw = {}
-        if dense is not None and dense.dense_list is not None and dense_A is not None:
-            _check(vals is None, "dense-row counts are for binary-feature batches (vals is None)")
-            _check(dense_A.dtype == torch.uint8 and dense_A.is_contiguous() and dense_A.shape[1] == MAX_DENSE
-                   and dense_A.shape[0] >= B, "dense_A: contiguous uint8 [>= B, MAX_DENSE]")
-            dkw = dict(dense_list=_p(dense.dense_list), dense_uniq=0 if dense_by_segment else _p(dense.uniq),
-                       dense_count=_p(dense.counts) + 12, dense_A=_p(dense_A))
         if self_rows is not None and self_rows.u1 > self_rows.u0:
             _self_check(self_rows, v, None)
             dkw["self_rows"] = self_rows.packed()
@@ -302,7 +290,7 @@ class DedupOut:
 
     __slots__ = ("n", "skeys", "perm", "uniq", "seg_start", "seg_chunk", "chunk_start", "chunk_seg", "chunk_key",
                  "counts", "num_unique", "inv", "sorted_ex", "sorted_x", "U_host", "CH", "big_list", "big_count",
-                 "multi", "ex_shift", "dense_list", "bwd_fresh")
+                 "multi", "ex_shift", "bwd_fresh")
 
     def __init__(self, **kw):
         for k in self.__slots__:
@@ -333,7 +321,7 @@ class DedupWorkspace:
         self.chunk_start = torch.empty(n1 + 1, **i32)
         self.chunk_seg = torch.empty(n1, **i32)   # segment id | first (bit 30) | single (bit 31)
         self.chunk_key = torch.empty(n1, **i32)
-        self.counts = torch.zeros(8, **i32)   # U, #chunks, #multi-chunk rows, #dense rows, bwd big rows, -
+        self.counts = torch.zeros(8, **i32)   # U, #chunks, #multi-chunk rows, -, bwd big rows, -
         self.multi = torch.empty(n1, **i32)
         self.inv = torch.empty(n1, **i32)
         self.sorted_ex = torch.empty(n1, **i32)
@@ -341,7 +329,6 @@ class DedupWorkspace:
         self.ex_of_occ = torch.empty(n1, **i32)
         self.big_list = torch.empty(n1, **i32)
         self.big_count = self.counts[4:5]     # zeroed with the counts by every GPU dedup
-        self.dense_list = torch.empty(MAX_DENSE, **i32)
         if device.type == "cuda":
             nbytes = native.hip().dedup_workspace_bytes(n1)
             self.ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
@@ -378,72 +365,10 @@ def csr_rows(offsets: torch.Tensor, out: torch.Tensor | None = None, nnz: int | 
     return out
 
 
-MAX_DENSE = 256            # = fm::kMaxDense: rows on the MFMA backward path
-DENSE_WG = 256             # = fm::kDenseWG: workgroups (partial rows) of the dense kernel
-
-
-def dense_min_for(num_examples: int, Kp: int, CH: int = 32, *, has_vals: bool = False,
-                  max_feats: int = 0, table_dtype: torch.dtype = torch.float32) -> int:
-    """Occurrence threshold of the MFMA backward rows (0 = off).
-
-    A row present in >= 2.5% of the batch's examples (>= B/40 occurrences; the first
-    MAX_DENSE = 256 such rows in key order) is reduced as a GEMM over example tiles on the
-    matrix cores (fm_bwd.hip, fm_bwd_dense_kernel): on a Criteo-shaped batch those rows hold
-    ~47% of the occurrences, whose r1 rows the occurrence-gather backward would fetch one by
-    one.  Needs binary features (the forward counts occurrences: x = 1), fewer than 256
-    features per example (byte counts, exact in bf16), Kp <= 128 (the tile's N) and a batch
-    that fills the 256 tile workgroups, and an fp32 r1 (not fp8 tables).  Opt-in: FM_DENSE_BWD=1."""
-    if (os.environ.get("FM_DENSE_BWD", "0") != "1" or has_vals or Kp > 128 or Kp % 4 or num_examples < 16384
-            or max_feats > 255 or r1_dtype(table_dtype) != torch.float32):
-        return 0
-    return max(8 * CH, num_examples // 40)
-class HotDict:
-    """Dictionary of the hot-dictionary GPU dedup (hip/hdedup.hip): up to HD_MAX_H frequent table
-    rows (ascending, with their LDS hash table), rebuilt on the device from a finished plan every
-    ``refresh`` plans (the first plan's included).  Its occurrences skip the radix sort; the plan
-    is the same whatever the dictionary holds, so staleness costs speed only."""
-
-    def __init__(self, device: torch.device, refresh: int | None = None):
-        h = native.hip()
-        i32 = dict(dtype=torch.int32, device=device)
-        self.keys = torch.zeros(h.HD_MAX_H, **i32)
-        self.n = torch.zeros(1, **i32)
-        self.ht_key = torch.full((h.HD_SLOTS,), -1, **i32)
-        self.ht_idx = torch.zeros(h.HD_SLOTS, **i32)
-        self.sel = torch.zeros(h.HD_MAX_H, **i32)
-        self.meta = torch.zeros(40, **i32)
-        self.refresh = max(1, int(refresh if refresh is not None else os.environ.get("FM_HD_REFRESH", "8")))
-        self.plans = 0
-
-    def packed(self) -> list[int]:
-        return [_p(self.keys), _p(self.n), _p(self.ht_key), _p(self.ht_idx), _p(self.sel), _p(self.meta)]
-
-    def rebuild(self, dd: "DedupOut") -> None:
-        """Re-derive the dictionary from plan ``dd`` (on the current stream, after the plan)."""
-        native.hip().hd_dict_refresh(dict=self.packed(), counts=_p(dd.counts), seg_start=_p(dd.seg_start),
-                                     uniq=_p(dd.uniq), n_max=int(dd.n), stream=_stream(dd.counts))
-
-    def after_plan(self, dd: "DedupOut") -> None:
-        """Count a finished plan; rebuild from it when due (plans 0, refresh, 2 * refresh, ...)."""
-        if self.plans % self.refresh == 0:
-            self.rebuild(dd)
-        self.plans += 1
-
-
-def hd_dedup_enabled() -> bool:
-    """FM_DEDUP=hd: the hot-dictionary dedup where it applies; onesweep (default): the radix sort
-    of every occurrence."""
-    v = os.environ.get("FM_DEDUP", "onesweep")
-    _check(v in ("hd", "onesweep"), "FM_DEDUP must be hd or onesweep")
-    return v == "hd"
-
-
 def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int = 32,
           ex_of_occ: torch.Tensor | None = None, vals: torch.Tensor | None = None, want_inv: bool = False,
           CH: int | None = None, want_perm: bool = False, num_examples: int | None = None,
-          Kp: int | None = None, ex_shift: int = 0, offsets: torch.Tensor | None = None,
-          dense_min: int = 0, hot_dict: HotDict | None = None,
-          want_skeys: bool = True) -> DedupOut:
+          Kp: int | None = None, ex_shift: int = 0, offsets: torch.Tensor | None = None) -> DedupOut:
     """Sort-based unique over non-negative int32 keys (reference tf.unique, fm_model.py:72).
 
     Unique keys come out in ascending order (the reference's first-occurrence
@@ -452,12 +377,6 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
     map, per-occurrence values nor the occurrence permutation are needed, the
     sort carries the example index directly (one gather pass less).
     (``num_examples`` / ``Kp`` are accepted for interface stability; the plan does not use them.)
-
-    GPU grouping: rocPRIM's onesweep radix sort of every occurrence, or -- with ``hot_dict`` and
-    ``FM_DEDUP=hd``, for the local step's plans (example payload, no per-occurrence values or
-    inverse map) -- the hot-dictionary dedup (hip/hdedup.hip: the dictionary's rows grouped by a
-    counting sort, the rest radix-sorted; the same plan bitwise).  ``want_skeys`` (hd): also write
-    the sorted keys (the backward does not read them).
     """
     dev = keys.device
     n = keys.numel()
@@ -482,34 +401,8 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
                    num_unique=ws.counts[:1], inv=ws.inv if want_inv else None,
                    sorted_ex=(ws.perm if ex_payload else ws.sorted_ex) if ex_of_occ is not None else None,
                    sorted_x=ws.sorted_x if vals is not None else None, CH=CH, big_list=ws.big_list,
-                   big_count=ws.big_count, multi=ws.multi, ex_shift=int(ex_shift),
-                   dense_list=ws.dense_list if dense_min > 0 and ex_of_occ is not None and _is_gpu(keys) else None)
-    if (_is_gpu(keys) and hot_dict is not None and ex_payload and not want_inv and vals is None
-            and out.dense_list is None and 0 < n and key_bits <= 31 and hd_dedup_enabled()
-            and not torch.cuda.is_current_stream_capturing()):  # (a host wait between its two phases)
-        # hot-dictionary dedup (hip/hdedup.hip): the same plan, sorting only the long tail
-        h = native.hip()
-        _check(1 <= CH <= h.MAX_CH, f"CH must be in [1, {h.MAX_CH}]")
-        need = h.hd_workspace_bytes(n)
-        if getattr(ws, "hd_ws", None) is None or ws.hd_ws.numel() < need:
-            ws.hd_ws = torch.empty(h.hd_workspace_bytes(max(n, ws.cap)), dtype=torch.uint8, device=dev)
-            ws.hd_hc = torch.zeros(8, dtype=torch.int32, device=dev)
-            ws.hd_hc_host = torch.zeros(8, dtype=torch.int32, pin_memory=True)
-            ws.hd_ev = torch.cuda.Event()
-        kw = dict(n=n, kb=key_bits, CH=CH, keys=_p(keys), payload=_p(ex_of_occ), dict=hot_dict.packed(),
-                  ws=_p(ws.hd_ws), ws_bytes=ws.hd_ws.numel(), hc=_p(ws.hd_hc), skeys=_p(ws.skeys) if want_skeys else 0,
-                  spay=_p(ws.perm), uniq=_p(ws.uniq), seg_start=_p(ws.seg_start), seg_chunk=_p(ws.seg_chunk),
-                  chunk_start=_p(ws.chunk_start), chunk_seg=_p(ws.chunk_seg), chunk_key=_p(ws.chunk_key),
-                  counts=_p(ws.counts), stream=_stream(keys))
-        h.dedup_hd(phase=1, n_c=0, **kw)
-        # the cold count sizes the radix sort: one host wait, on this (side) stream, for phase 1
-        ws.hd_hc_host.copy_(ws.hd_hc, non_blocking=True)
-        ws.hd_ev.record()
-        ws.hd_ev.synchronize()
-        h.dedup_hd(phase=2, n_c=int(ws.hd_hc_host[0]), **kw)
-        out.bwd_fresh = True
-        hot_dict.after_plan(out)
-    elif _is_gpu(keys):
+                   big_count=ws.big_count, multi=ws.multi, ex_shift=int(ex_shift))
+    if _is_gpu(keys):
         h = native.hip()
         _check(1 <= CH <= h.MAX_CH, f"CH must be in [1, {h.MAX_CH}]")
         h.dedup(n=n, end_bit=key_bits, CH=CH, keys=_p(keys), payload=_p(ex_of_occ if ex_payload else ws.iota),
@@ -520,7 +413,6 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
                 ex_of_occ=0 if ex_payload else _p(ex_of_occ),
                 sorted_ex=0 if ex_payload else _p(out.sorted_ex), vals=_p(vals), sorted_x=_p(out.sorted_x),
                 payload_is_ex=int(ex_payload), ex_shift=int(ex_shift), offsets=_p(offsets),
-                dense_min=int(dense_min) if out.dense_list is not None else 0, dense_list=_p(out.dense_list),
                 ws=_p(ws.ws), ws_bytes=ws.ws.numel(), stream=_stream(keys))
         out.bwd_fresh = True  # the backward counters were zeroed on this stream
     else:
@@ -635,11 +527,10 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
                 table: TableState | None = None, opt: OptConfig | None = None,
                 src_v: torch.Tensor | None = None, src_w: torch.Tensor | None = None,
                 grad_out: torch.Tensor | None = None, reg_v: float = 0.0, reg_w: float = 0.0,
-                partial: torch.Tensor | None = None, threads: int = 0,
-                dense_part: torch.Tensor | None = None, dense_stream=None,
-                grad_bf16: bool = False, sr_counter: torch.Tensor | None = None,
+                partial: torch.Tensor | None = None, threads: int = 0, grad_bf16: bool = False,
+                sr_counter: torch.Tensor | None = None,
                 seg_bounds: torch.Tensor | None = None, piece: int = -1,
-                dense_A: torch.Tensor | None = None, self_rows: SelfRows | None = None) -> torch.Tensor | None:
+                self_rows: SelfRows | None = None) -> torch.Tensor | None:
     """Segmented FM backward over the dedup grouping (reference FmGrad, cc/fm_grad_op.h:59-163).
 
     Per unique row u with occurrences (i, x):
@@ -702,21 +593,14 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
     _check(r1.dtype == r1_dtype(v.dtype), f"r1: {r1_dtype(v.dtype)} for {v.dtype} rows (the forward's r1)")
     o = opt or OptConfig()
     if piece >= 0:
-        _check(_is_gpu(dpred) and seg_bounds is not None and mode in (BWD_EMIT, BWD_EMIT_TABLE)
-               and dd.dense_list is None, "split backward pieces: GPU, EMIT / EMIT_TABLE, seg_bounds, no dense rows")
+        _check(_is_gpu(dpred) and seg_bounds is not None and mode in (BWD_EMIT, BWD_EMIT_TABLE),
+               "split backward pieces: GPU, EMIT / EMIT_TABLE, seg_bounds")
         _chk_vec(seg_bounds, torch.int32, 3, "seg_bounds", dev)
     if _is_gpu(dpred):
         h = native.hip()
         if partial is None:
             partial = torch.empty((partial_rows(dd.n, dd.CH), Kp + 4), dtype=torch.float32, device=dev)
         _check(partial.numel() >= partial_rows(dd.n, dd.CH) * (Kp + 4), "partial scratch too small")
-        dp = None
-        if dd.dense_list is not None:  # MFMA path (counts written by the forward)
-            _check(dense_A is not None and dense_A.dtype == torch.uint8 and dense_A.shape[1] == MAX_DENSE
-                   and dense_A.shape[0] >= dpred.numel(), "dense rows need the forward's dense_A counts")
-            dp = dense_part if dense_part is not None else torch.empty(
-                (DENSE_WG * MAX_DENSE, Kp + 4), dtype=torch.float32, device=dev)
-            _check(dp.numel() >= DENSE_WG * MAX_DENSE * (Kp + 4), "dense_part scratch too small")
         skw = {}
         if mode == BWD_EMIT and self_rows is not None and self_rows.u1 > self_rows.u0:
             skw = dict(self_rows=self_rows.packed())
@@ -729,16 +613,12 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               s_stride=s_stride, s0w=_p(s0w), s1w=_p(s1w), reg_v=float(reg_v), reg_w=float(reg_w),
               opt_type=o.code, lr=float(o.lr), l1=float(o.l1), l2=float(o.l2), beta=float(o.beta),
               grad_out=gptr, g_stride=gstride, partial=_p(partial), big_list=_p(dd.big_list),
-              big_count=_p(dd.big_count), multi=_p(dd.multi),
-              dense_list=_p(dd.dense_list),
-              dense_part=_p(dp), nex=int(dpred.numel()),
-              dense_stream=dense_stream.cuda_stream if dense_stream is not None else 0, dtype=dt, max_chunks=dd.n,
+              big_count=_p(dd.big_count), multi=_p(dd.multi), nex=int(dpred.numel()), dtype=dt, max_chunks=dd.n,
               max_unique=dd.n,
               stream=_stream(dpred), g_wcol=g_wcol if mode != BWD_LOCAL else -1, g_bf16=int(bool(grad_bf16)),
               sr_counter=_p(sr_counter), counters_ready=int(bool(dd.bwd_fresh)),
               seg_bounds=_p(seg_bounds), piece=int(piece),
               n_owners=(seg_bounds.numel() - 1) // 2 if seg_bounds is not None else 0,
-              dense_A=_p(dense_A) if dd.dense_list is not None else 0,
               chunk_grid=int(os.environ.get("FM_CHUNK_GRID", "0")),
               **skw)
         dd.bwd_fresh = False  # a second backward over this grouping zeroes its counters itself

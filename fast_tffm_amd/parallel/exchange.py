@@ -420,11 +420,7 @@ class ShardExchange(_Base):
                 part.dd = K.dedup(keys, ws=dws, key_bits=self.key_bits, ex_of_occ=ex,
                                   vals=sb.vals if ex is not None else None, want_inv=not (lookup or w1),
                                   num_examples=sb.B,
-                                  Kp=self.m.Kp, ex_shift=shift, offsets=sb.offsets if shift else None,
-                                  dense_min=K.dense_min_for(sb.B, self.m.Kp, m.cfg.dedup_chunk,
-                                                            table_dtype=m.table.v.dtype,
-                                                            has_vals=sb.vals is not None,
-                                                            max_feats=sb.max_feats) if train else 0)
+                                  Kp=self.m.Kp, ex_shift=shift, offsets=sb.offsets if shift else None)
                 part.seg = K.seg_index(part.dd, self.key_bits, slot.segidx_buf(k)) if lookup else None
                 counts.append(K.owner_counts(part.dd, self.Rps, self.W))
                 pl.parts.append(part)
@@ -494,7 +490,7 @@ class ShardExchange(_Base):
                 pl.run_off = slot.runs(pl.splits, self.dev)
                 pl.match = slot.match_buf(pl.R * len(pl.splits), self.dev) if len(pl.splits) > 1 else None
                 part = pl.parts[0]
-                if self.self_rows and len(pl.parts) == 1 and part.dd.dense_list is None:
+                if self.self_rows and len(pl.parts) == 1:
                     me = self.ctx.rank
                     s0, r0 = int(sum(part.sc[:me])), int(sum(part.rc[:me]))
                     pl.self_u, pl.self_r = (s0, s0 + part.sc[me]), (r0, r0 + part.rc[me])
@@ -668,8 +664,7 @@ class ShardExchange(_Base):
         return self.wire.views(e.gathered)
 
     def _split_ok(self, pl: _ShardPlan, dd) -> bool:
-        return (self.overlap_grads and len(pl.parts) == 1
-                and (dd.dense_list is None or self.dev.type != "cuda"))
+        return self.overlap_grads and len(pl.parts) == 1
 
     def _half_bounds(self, part: _Part) -> tuple[list[int], list[int], list[int], list[int]]:
         """Per owner q: start of my requests to q in unique order, and the size of their first half;
@@ -844,19 +839,15 @@ class ShardExchange(_Base):
             sb, dd, e0 = part.b, part.dd, part.e0
             if work is not None:
                 work.wait()               # the compute stream waits for this part's rows
-            dA = ws.dense_counts(ws.cap_b)[e0: e0 + sb.B] if dd.dense_list is not None else None
             if local_w1:  # (keys are table rows: the local step's forward over the table)
                 with roctx_range("fwd_local"):
                     fo = K.fm_forward(sb.offsets, part.keys, sb.vals, m.table.v, m.table.w, Kp, labels=sb.labels,
                                       weights=sb.weights, loss=cfg.loss_type, grad_scale=gscale, want_r1=True,
                                       pred=ws.pred[: sb.B], r1=ws.r1[: sb.B], dpred=ws.dpred[: sb.B],
-                                      partial=ws.fwd_partial, threads=cfg.threads, bias=m.gbias, dense=dd,
-                                      dense_A=dA, defer_loss=True)
+                                      partial=ws.fwd_partial, threads=cfg.threads, bias=m.gbias, defer_loss=True)
                 with roctx_range("bwd_local"):
                     K.fm_backward(dd, fo.dpred, fo.r1, Kp, mode=K.BWD_LOCAL, table=m.table.state, opt=cfg.opt,
-                                  reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads,
-                                  dense_part=ws.dense_part, dense_stream=m._dense_stream(), sr_counter=sr,
-                                  dense_A=dA)
+                                  reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, sr_counter=sr)
                 continue
             src_v, src_w = wf.views(buf) if buf is not None else early_views
             gs = grad_send[part.u0: part.u0 + part.U]
@@ -866,8 +857,7 @@ class ShardExchange(_Base):
                                   weights=sb.weights, loss=cfg.loss_type, grad_scale=gscale, want_r1=True,
                                   pred=ws.pred[e0: e0 + sb.B], r1=ws.r1[e0: e0 + sb.B],
                                   dpred=ws.dpred[e0: e0 + sb.B], partial=ws.fwd_partial, threads=cfg.threads,
-                                  bias=m.gbias, dense=dd, dense_A=dA, dense_by_segment=True, self_rows=srows,
-                                  seg_lookup=part.seg, defer_loss=one_part)
+                                  bias=m.gbias, self_rows=srows, seg_lookup=part.seg, defer_loss=one_part)
             if not one_part:  # (the parts share the loss partials: each part's sum before the next)
                 loss = fo.loss_sum if loss is None else loss + fo.loss_sum
             if self._split_ok(pl, dd):
@@ -877,8 +867,7 @@ class ShardExchange(_Base):
             with roctx_range("bwd"):
                 K.fm_backward(dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT, src_v=src_v, src_w=src_w, grad_out=gs,
                               reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads,
-                              dense_part=ws.dense_part, dense_stream=m._dense_stream() if gpu else None,
-                              grad_bf16=wf.grad_bf16, dense_A=dA, **skw)
+                              grad_bf16=wf.grad_bf16, **skw)
             if self.W > 1:
                 with roctx_range("a2a_grads"):
                     gworks.append(dist.all_to_all_single(grad_recv[part.r0: part.r0 + part.R], gs, part.rc, part.sc,
@@ -1145,23 +1134,21 @@ class DPDenseExchange(DPExchange):
             m._lpending = m._lpending2 = None
             pl = m._local_plan(b)
         main.wait_event(pl.ready)
-        dA = ws.dense_counts(b.B) if pl.dd.dense_list is not None else None
         with roctx_range("fwd"):
             fo = K.fm_forward(b.offsets, pl.rows, b.vals, m.table.v, m.table.w, Kp, labels=b.labels,
                               weights=b.weights, loss=cfg.loss_type, grad_scale=m.grad_scale(b.B), want_r1=True,
                               pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
-                              bias=m.gbias, dense=pl.dd, dense_A=dA)
+                              bias=m.gbias)
             m.bias_step(fo.dpred)
         rv, rw = m.reg_coeffs
         # backward pieces by key block, each block's reduce-scatter issued behind its piece
-        pieces = self.W > 1 and self.P > 1 and dA is None
+        pieces = self.W > 1 and self.P > 1
         bounds = self._block_bounds(pl.dd) if pieces else None
         rs = []
         with roctx_range("bwd_scatter+reduce_scatter"):
             for p in range(self.P if pieces else 1):
                 K.fm_backward(pl.dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT_TABLE, table=m.table.state,
                               grad_out=self.dense, reg_v=rv, reg_w=rw, partial=ws.bwd_partial,
-                              dense_part=ws.dense_part, dense_stream=m._dense_stream(), dense_A=dA,
                               piece=0 if pieces else -1, seg_bounds=bounds[p: p + 3] if pieces else None)
                 if pieces:
                     rs.append(self._reduce_scatter_block(p))

@@ -40,10 +40,12 @@ def _cfg(mode, V):
 
 
 @pytest.mark.parametrize("mode", ["shard", "dp", "dp_dense"])
-@pytest.mark.parametrize("dense", [False, True])
-def test_rccl_world1_matches_local(rccl_ctx, mode, dense, monkeypatch):
-    if dense:  # MFMA backward rows (EMIT mode on the sharded path), forced on a small batch
-        monkeypatch.setattr(K, "dense_min_for", lambda B, Kp, CH=32, **kw: 48)
+@pytest.mark.parametrize("emit", [False, True])
+def test_rccl_world1_matches_local(rccl_ctx, mode, emit, monkeypatch):
+    if emit:  # the sharded step's N > 1 compute path (EMIT backward, exchange) run at world 1
+        if mode != "shard":
+            pytest.skip("EMIT at world 1 is a row-sharded executor path")
+        monkeypatch.setenv("FM_SHARD_W1_LOCAL", "0")
     V = 50000
     gen = CriteoSynth(V, device="cuda", seed=21)
     batches = [gen.batch(2048) for _ in range(3)]

@@ -1,10 +1,9 @@
 """Dedup chain alone (csr_rows codes + grouping + chunk plan) on Criteo-shaped batches, per method.
 
-Times K.dedup back to back on a pool of batches (no step beside it): onesweep (rocPRIM radix sort
-of every occurrence) and hd (hot-dictionary dedup, hip/hdedup.hip, with a dictionary built from a
-batch outside the timed pool).  Run under ``rocprofv3 --kernel-trace --stats`` for per-kernel times.
+Times K.dedup back to back on a pool of batches (no step beside it), once per sort named in
+``--algo`` (the FM_SORT setting).  Run under ``rocprofv3 --kernel-trace --stats`` for per-kernel times.
 
-    python tools/bench_dedup.py [--algo onesweep,hd] [--iters 30]
+    python tools/bench_dedup.py [--algo onesweep] [--iters 30]
 """
 
 from __future__ import annotations
@@ -25,7 +24,7 @@ from fast_tffm_amd.ops import kernels as K  # noqa: E402
 
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--algo", default="onesweep,hd", help="onesweep | hd")
+    ap.add_argument("--algo", default="onesweep", help="comma list of FM_SORT values")
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--pool", type=int, default=4)
     ap.add_argument("--vocab", type=int, default=125_000_000)
@@ -40,21 +39,13 @@ def main() -> int:
         sb = K.slot_bits_for(b.B, b.max_feats)
         pool.append((b.ids.to(torch.int32), b.offsets, b.nnz, sb))
     for algo in a.algo.split(","):
-        os.environ["FM_DEDUP"] = algo
+        os.environ["FM_SORT"] = algo
         ws = K.DedupWorkspace(max(p[0].numel() for p in pool), dev, 32)
-        hd = None
-        if algo == "hd":  # dictionary from a batch outside the timed pool, frozen
-            hd = K.HotDict(dev, refresh=1)
-            b0 = gen.batch(131072)
-            K.dedup(b0.ids.to(torch.int32), ws=ws, key_bits=kb,
-                    ex_of_occ=K.csr_rows(b0.offsets, nnz=b0.nnz, slot_bits=pool[0][3]), hot_dict=hd)
-            hd.refresh = 10 ** 9
 
         def run(i):
             ids, off, nnz, sb = pool[i % len(pool)]
             codes = K.csr_rows(off, out=ws.ex_of_occ[:nnz], nnz=nnz, slot_bits=sb)
-            K.dedup(ids, ws=ws, key_bits=kb, ex_of_occ=codes, ex_shift=sb, offsets=off, hot_dict=hd,
-                    want_skeys=False)
+            K.dedup(ids, ws=ws, key_bits=kb, ex_of_occ=codes, ex_shift=sb, offsets=off)
 
         for i in range(3):
             run(i)
