@@ -10,4 +10,7 @@ HIP_VARIANTS: dict[str, list[str]] = {"fwdnopf": ["-DFM_FWD_PREFETCH=0"], "fwdge
                                      "allgen": ["-DFM_FWD_SPECIALIZE=0", "-DFM_BWD_SPECIALIZE=0"],
                                      "fu10w4": ["-DFM_FWD_UNR16=10", "-DFM_FWD_LOCAL_W16=4"],
                                      "f4gen": ["-DFM_FWD_UNR4=0", "-DFM_FWD_LOCAL_W4=0"],
-                                     "cu32_8": ["-DFM_CHUNK_UNR32=8"]}
+                                     "cu32_8": ["-DFM_CHUNK_UNR32=8"],
+                                     "sh16u2w7": ["-DFM_FWD_UNR16_SH=2", "-DFM_FWD_SH_W16=7"],
+                                     "sh16u4w6": ["-DFM_FWD_UNR16_SH=4", "-DFM_FWD_SH_W16=6"],
+                                     "sh16u6w5": ["-DFM_FWD_UNR16_SH=6", "-DFM_FWD_SH_W16=5"]}

@@ -49,9 +49,17 @@ constexpr int kChunkUnr = FM_CHUNK_UNR;
 #ifndef FM_CHUNK_UNR32
 #define FM_CHUNK_UNR32 12
 #endif
-template <int LPR, bool LOC>
+// The EMIT-specialised kernel of the row-sharded step: 12 for fp8 rows (bf16 r1 rows: half the
+// registers per row in flight); fp32 / bf16 rows spill 12 VGPRs at 12 under the 128-VGPR cap and
+// keep 8.  FM_CHUNK_UNR32_EMIT overrides the fp8 value.
+#ifndef FM_CHUNK_UNR32_EMIT
+#define FM_CHUNK_UNR32_EMIT FM_CHUNK_UNR32
+#endif
+template <int LPR, bool LOC, bool EMT, typename TV>
 constexpr int chunk_unr() {
-  return LOC && LPR == 32 ? FM_CHUNK_UNR32 : kChunkUnr;
+  return LOC && LPR == 32 ? FM_CHUNK_UNR32
+         : EMT && LPR == 32 ? (R1Bf16<TV>::v ? FM_CHUNK_UNR32_EMIT : kChunkUnr)
+                            : kChunkUnr;
 }
 
 struct BwdArgs {
@@ -180,6 +188,88 @@ __device__ inline void bwd_finish_local(const BwdArgs& a, int t, bool tact, RowS
   }
 }
 
+// EMIT mode known at compile time (the row-sharded step's specialised chunk kernel): segment u's
+// parameters come from gathered wire row u or -- this rank's own rows -- from table row key - base,
+// and an exclusive own row is updated in place; 32 x 32-bit row addressing throughout.
+template <typename TV, int EPL>
+__device__ inline void bwd_load_emit(const BwdArgs& a, int u, long long key, int tE, RowState<EPL>& r) {
+  using F = Frag<TV>;
+  const bool own = a.self.has(u);
+  r.apply = own && a.self.exclusive(u);
+  r.row = own ? key - a.self.base : (long long)u;
+  const TV* vsrc = reinterpret_cast<const TV*>(own ? a.self.v : a.v);
+  const float* wsrc = own ? a.self.w : a.w;
+  F::load(row_ptr(vsrc, r.row, own ? a.self.v_stride : a.v_stride) + tE * EPL, r.vv);
+  const float* wr = row_ptr(wsrc, r.row, own ? a.self.w_stride : a.w_stride);
+  r.wv = wr[0];
+  if constexpr (F::kScaled) {
+    const float s = wr[1];  // (row_scale)
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) r.vv[k] *= s;
+  }
+  if (!r.apply) return;
+  load_state<TV, EPL>(state_row<TV>(a.s0v, r.row, a.s_stride), tE * EPL, r.st0);
+  r.q0 = a.s0w[(uint32_t)r.row];
+  if (a.s1v) {
+    load_state<TV, EPL>(state_row<TV>(a.s1v, r.row, a.s_stride), tE * EPL, r.st1);
+    r.q1 = a.s1w[(uint32_t)r.row];
+  } else {
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) r.st1[k] = 0.f;
+    r.q1 = 0.f;
+  }
+}
+
+template <int LPR, typename TV, int EPL>
+__device__ inline void bwd_finish_emit(const BwdArgs& a, int u, int t, bool tact, RowState<EPL>& r,
+                                       const float (&A)[EPL], float Scx, float Sc, int n_u, uint32_t sr) {
+  const float nreg_v = a.reg_v * (float)n_u, nreg_w = a.reg_w * (float)n_u;
+  float gr[EPL];
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) gr[k] = A[k] - Scx * r.vv[k] + nreg_v * r.vv[k];
+  const float gw = Sc + nreg_w * r.wv;
+  if (!r.apply) {  // gradient row u for its owner's apply
+    float* dst = row_ptr(a.grad_out, (long long)u, a.g_stride);
+    if (tact) {
+      if (a.g_bf16) {  // EPL bf16 values per lane (EPL * 2 bytes, 8-byte aligned)
+        uint16_t* d16 = reinterpret_cast<uint16_t*>(dst) + t * EPL;
+#pragma unroll
+        for (int k = 0; k < EPL; k += 4) {
+          uint2 o;
+          o.x = f32_to_bf16_bits(gr[k]) | (f32_to_bf16_bits(gr[k + 1]) << 16);
+          o.y = f32_to_bf16_bits(gr[k + 2]) | (f32_to_bf16_bits(gr[k + 3]) << 16);
+          *reinterpret_cast<uint2*>(d16 + k) = o;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < EPL; k += 4)
+          *reinterpret_cast<float4*>(dst + t * EPL + k) = make_float4(gr[k], gr[k + 1], gr[k + 2], gr[k + 3]);
+      }
+    }
+    if (t == 0) dst[a.g_wcol] = gw;
+    return;
+  }
+  // exclusive own row: the optimizer in place on this rank's table
+  TV* tv = reinterpret_cast<TV*>(const_cast<void*>(a.self.v));
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) opt_step(a.opt, gr[k], r.vv[k], r.st0[k], r.st1[k]);
+  store_row<LPR, TV>(row_ptr(tv, r.row, a.self.v_stride) + t * EPL, r.vv, a.self.w, r.row, a.self.w_stride, t, tact,
+                     sr);
+  if (tact) {
+    store_state<TV, EPL>(state_row<TV>(a.s0v, r.row, a.s_stride), t * EPL, r.st0, sr ? sr ^ kSrSalt0 : 0u,
+                         (uint32_t)r.row, (uint32_t)(t * EPL));
+    if (a.s1v)
+      store_state<TV, EPL>(state_row<TV>(a.s1v, r.row, a.s_stride), t * EPL, r.st1, sr ? sr ^ kSrSalt1 : 0u,
+                           (uint32_t)r.row, (uint32_t)(t * EPL));
+  }
+  if (t == 0) {
+    opt_step(a.opt, gw, r.wv, r.q0, r.q1);
+    row_ptr(a.self.w, r.row, a.self.w_stride)[0] = r.wv;
+    a.s0w[(uint32_t)r.row] = r.q0;
+    if (a.s1w) a.s1w[(uint32_t)r.row] = r.q1;
+  }
+}
+
 // Parameters (and, when the row is updated here, optimizer state) of segment u with key
 // `key`: LOCAL reads table row key; EMIT reads gathered row u, or -- a self row of the
 // row-sharded step -- table row key - self.base, applied in place when exclusive;
@@ -293,11 +383,16 @@ constexpr int chunk_min_waves() {
 }
 
 // Chunk-kernel instantiations: kChunkAny runs every mode (split pieces, self rows, EMIT /
-// EMIT_TABLE gradient rows, 64-bit r1 offsets); the LOCAL ones know the mode at compile time
-// (no piece walk, no self-row or gradient-row paths, 32-bit row and r1 offsets -- the launcher
-// checks that r1 fits -- and group-relative ds_bpermute sources), kChunkLocalNoX also that the
-// occurrences carry no values (x = 1: one ds_bpermute per occurrence less, Scx = Sc).
-enum ChunkKind : int { kChunkAny = 0, kChunkLocal = 1, kChunkLocalNoX = 2 };
+// EMIT_TABLE gradient rows, 64-bit r1 offsets); the others know the mode at compile time, with
+// 32-bit row and r1 offsets (the launcher checks that r1 fits) and group-relative ds_bpermute
+// sources: LOCAL (no piece walk, no self-row or gradient-row paths), EMIT (the row-sharded step:
+// wire / own-table rows, gradient rows or in-place own-row updates; the piece walk of the split
+// backward only in the *Pc kinds), and *NoX: the occurrences carry no values (x = 1: one
+// ds_bpermute per occurrence less, Scx = Sc).
+enum ChunkKind : int {
+  kChunkAny = 0, kChunkLocal = 1, kChunkLocalNoX = 2,
+  kChunkEmit = 3, kChunkEmitNoX = 4, kChunkEmitPc = 5, kChunkEmitPcNoX = 6
+};
 #ifndef FM_BWD_SPECIALIZE
 #define FM_BWD_SPECIALIZE 1  // 0: every mode runs kChunkAny (the "bwdgen" build variant, A/B)
 #endif
@@ -305,12 +400,16 @@ enum ChunkKind : int { kChunkAny = 0, kChunkLocal = 1, kChunkLocalNoX = 2 };
 // One lane group per chunk of <= CH (<= kMaxCH) sorted occurrences of one row.
 template <int LPR, typename TV, int KV>
 __device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
-  constexpr bool LOC = KV != kChunkAny, NOX = KV == kChunkLocalNoX;
+  constexpr bool FAST = KV != kChunkAny;                                   // 32-bit offsets, bpermute
+  constexpr bool LOC = KV == kChunkLocal || KV == kChunkLocalNoX;          // local epilogue
+  constexpr bool EMT = KV >= kChunkEmit;                                   // EMIT epilogue
+  constexpr bool NOX = KV == kChunkLocalNoX || KV == kChunkEmitNoX || KV == kChunkEmitPcNoX;
+  constexpr bool PCW = KV == kChunkAny || KV == kChunkEmitPc || KV == kChunkEmitPcNoX;  // piece walk
   const uint32_t sr = sr_step_seed(a.sr_counter);  // stochastic rounding seed (0: nearest)
   constexpr int EPL = Frag<TV>::N;  // elements per lane of the table dtype
   constexpr int G = kWave / LPR;
   constexpr int PF = (kMaxCH + LPR - 1) / LPR;  // prefetched occurrences per lane
-  constexpr int UNR = LPR < chunk_unr<LPR, LOC>() ? LPR : chunk_unr<LPR, LOC>();  // r1 rows in flight per lane
+  constexpr int UNR = LPR < chunk_unr<LPR, LOC, EMT, TV>() ? LPR : chunk_unr<LPR, LOC, EMT, TV>();  // r1 rows in flight
   constexpr bool kShortPath = LPR >= 32;                          // short-chunk block (below)
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR, t = lane % LPR;
@@ -320,17 +419,17 @@ __device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
   const bool tact = t < nv;
   const int tE = tact ? t : nv - 1;
   const int nchunks = a.counts[1];
-  // r1 row of example ex, this lane's EPL columns (LOCAL: 32-bit byte offsets, one mad)
+  // r1 row of example ex, this lane's EPL columns (specialised kinds: 32-bit byte offsets, one mad)
   constexpr uint32_t kR1E = R1Bf16<TV>::v ? 2u : 4u;
   const char* r1b = reinterpret_cast<const char*>(a.r1);
   const uint32_t r1rb = (uint32_t)a.Kp * kR1E, r1cb = (uint32_t)(tE * EPL) * kR1E;
   auto r1_at = [&](int ex, float (&o)[EPL]) {
-    if constexpr (LOC) load_r1<TV, EPL>(r1b + ((uint32_t)ex * r1rb + r1cb), 0, o);
+    if constexpr (FAST) load_r1<TV, EPL>(r1b + ((uint32_t)ex * r1rb + r1cb), 0, o);
     else load_r1<TV, EPL>(a.r1, (long long)ex * a.Kp + tE * EPL, o);
   };
   // split-backward piece: this piece's chunk ranges (one per owner) and their prefix sums
-  __shared__ int pr_start[kMaxPieceOwners], pr_pre[kMaxPieceOwners + 1];
-  const bool pieced = !LOC && a.piece >= 0;
+  __shared__ int pr_start[PCW ? kMaxPieceOwners : 1], pr_pre[PCW ? kMaxPieceOwners + 1 : 1];
+  const bool pieced = PCW && a.piece >= 0;
   if (pieced) {
     if (threadIdx.x == 0) {
       int acc = 0;
@@ -379,6 +478,7 @@ __device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
     RowState<EPL> rs;
     if (single) {
       if constexpr (LOC) bwd_load_local<TV, EPL>(a, (long long)key, tE, rs);
+      else if constexpr (EMT) bwd_load_emit<TV, EPL>(a, u, (long long)key, tE, rs);
       else bwd_load<TV, EPL>(a, u, (long long)key, tE, rs);
     }
     // lane-parallel prefetch of the chunk's (example, dpred*x, x)
@@ -400,10 +500,10 @@ __device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
     for (int k = 0; k < EPL; ++k) A[k] = 0.f;
     float Scx = 0.f, Sc = 0.f;
     // occurrence li of prefetch slot q: (example, c masked by ok, x).  General kernel: __shfl from
-    // lane gbase + li (gbase when !ok); LOCAL: ds_bpermute from gb4 + 4 li (the constant folds into
+    // lane gbase + li (gbase when !ok); specialised: ds_bpermute from gb4 + 4 li (the constant folds into
     // the instruction's offset; an invalid slot reads its lane's clamped, valid example, c = 0)
     auto occ = [&](int q, int li, bool ok, int& ex, float& cs, float& xs) {
-      if constexpr (LOC) {
+      if constexpr (FAST) {
         const int sb = gb4 + (li << 2);
         ex = __builtin_amdgcn_ds_bpermute(sb, pex[q]);
         const float c0 = __int_as_float(__builtin_amdgcn_ds_bpermute(sb, __float_as_int(pc[q])));
@@ -494,6 +594,7 @@ __device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
     }
     if (single) {
       if constexpr (LOC) bwd_finish_local<LPR, TV, EPL>(a, t, tact, rs, A, Scx, Sc, len, sr);
+      else if constexpr (EMT) bwd_finish_emit<LPR, TV, EPL>(a, u, t, tact, rs, A, Scx, Sc, len, sr);
       else bwd_finish<LPR, TV, EPL>(a, u, t, tact, rs, A, Scx, Sc, len, sr);
     } else {
       float* dst = a.partial + (long long)cc * (a.Kp + 4);
@@ -521,6 +622,15 @@ void fm_bwd_chunk_local_kernel(BwdArgs a) { bwd_chunk_body<LPR, TV, kChunkLocal>
 template <int LPR, typename TV>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(chunk_min_waves<LPR, TV>())))
 void fm_bwd_chunk_local_nox_kernel(BwdArgs a) { bwd_chunk_body<LPR, TV, kChunkLocalNoX>(a); }
+#define FM_EMIT_CHUNK_KERNEL(NAME, KIND)                                                          \
+  template <int LPR, typename TV>                                                                 \
+  __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(chunk_min_waves<LPR, TV>()))) \
+  void NAME(BwdArgs a) { bwd_chunk_body<LPR, TV, KIND>(a); }
+FM_EMIT_CHUNK_KERNEL(fm_bwd_chunk_emit_kernel, kChunkEmit)
+FM_EMIT_CHUNK_KERNEL(fm_bwd_chunk_emit_nox_kernel, kChunkEmitNoX)
+FM_EMIT_CHUNK_KERNEL(fm_bwd_chunk_emit_pc_kernel, kChunkEmitPc)
+FM_EMIT_CHUNK_KERNEL(fm_bwd_chunk_emit_pc_nox_kernel, kChunkEmitPcNoX)
+#undef FM_EMIT_CHUNK_KERNEL
 
 // Rows split over 2..kSmallChunks chunks: one lane group, ordered sum of the partials.
 // Hotter rows are appended to big_list for fm_bwd_big_kernel.
@@ -651,13 +761,18 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_big_kernel(BwdArgs a) {
   }
 }
 
-static int chunk_wg_per_cu(int lpr, int mode) {
-  static const int env = [] {
-    const char* e = getenv("FM_CHUNK_WG_PER_CU");
-    return e ? atoi(e) : -1;
-  }();
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+// specialised kinds (local / EMIT) share the launch shape: EMIT runs the local step's kernel body
+static bool fast_kind(int kind) { return kind != kChunkAny; }
+
+static int chunk_wg_per_cu(int lpr, int kind) {
+  static const int env = env_int("FM_CHUNK_WG_PER_CU", -1);
   if (env >= 0) return env;
-  return mode == kBwdLocal && lpr <= 16 ? 3 : 0;
+  return fast_kind(kind) && lpr <= 16 ? 3 : 0;
 }
 
 int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_unique, hipStream_t st) {
@@ -679,9 +794,6 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   // 3 workgroups per CU (profiles/r4/chunk_grid_wg3.txt): 16-lane rows 3072 (0.616-0.618 ms) over 3840
   // (0.620-0.624), 2304 / 5120 slower; 4-lane rows 512 still best; 32-lane rows uncapped.
   // FM_CHUNK_GRID: > 0 overrides, < 0 disables.
-  const int cap = a.chunk_grid != 0 ? a.chunk_grid
-                  : a.mode != kBwdLocal ? -1 : (lpr == 16 ? 3072 : lpr == 4 ? 512 : -1);
-  if (cap > 0 && g1 > cap) g1 = (cap + 7) / 8 * 8;
   if (a.piece >= 0 && a.n_owners > kMaxPieceOwners) return -6;
   // (a software-pipelined variant that issued the next chunk's occurrence and row loads before
   // reducing the current one ran 367 -> 316 us alone but made the step slower twice:
@@ -691,24 +803,42 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   // (a split walk -- the chunks of multi-chunk rows first, their combine beside the single-chunk
   // rows' launch, or both launches concurrent -- measured slower: k64 0.669 -> 0.72-0.78 ms, each
   // launch as long as the whole walk; profiles/r3/bwd_split_ab.txt)
-  // LOCAL-mode chunk kernels (see ChunkKind) when r1 fits 32-bit offsets
+  // specialised chunk kernels (see ChunkKind) when r1 fits 32-bit offsets: LOCAL mode, and EMIT mode
+  // (the row-sharded step; FM_BWD_EMIT_FAST=0 keeps it on the general kernel, A/B)
   const long long r1_bytes = (long long)a.nex * a.Kp * (dtype == kFP8 ? 2 : 4);
-  const int kind = FM_BWD_SPECIALIZE && a.mode == kBwdLocal && a.piece < 0 && lpr >= 4 && r1_bytes < (1LL << 32)
-                       ? (a.sorted_x ? kChunkLocal : kChunkLocalNoX)
-                       : kChunkAny;
+  static const bool emit_fast = env_int("FM_BWD_EMIT_FAST", 1) != 0;
+  const bool fits = FM_BWD_SPECIALIZE && lpr >= 4 && r1_bytes < (1LL << 32);
+  int kind = kChunkAny;
+  if (fits && a.mode == kBwdLocal && a.piece < 0) {
+    kind = a.sorted_x ? kChunkLocal : kChunkLocalNoX;
+  } else if (fits && emit_fast && a.mode == kBwdEmit) {
+    kind = a.piece >= 0 ? (a.sorted_x ? kChunkEmitPc : kChunkEmitPcNoX) : (a.sorted_x ? kChunkEmit : kChunkEmitNoX);
+  }
+  const int cap = a.chunk_grid != 0 ? a.chunk_grid
+                  : !fast_kind(kind) ? -1 : (lpr == 16 ? 3072 : lpr == 4 ? 512 : -1);
+  if (cap > 0 && g1 > cap) g1 = (cap + 7) / 8 * 8;
   // Chunk workgroups resident per CU, capped through dynamic LDS the kernel does not use (a CU holds
   // floor(LDS / bytes) of them).  The side stream's radix-sort blocks then find LDS on every CU and
   // the capped grid spreads over more CUs: same-box, 3 per CU took k64 fp32 0.648 -> 0.621 ms and
   // k16 bf16 0.511 -> 0.487; 32-lane rows (k128, uncapped grid) lose (fp8 FTRL 0.887 -> 0.978)
   // (profiles/r4/wg_per_cu_ab.txt).  An earlier build's 130-VGPR k16 kernel (3 waves / SIMD) had
   // the same effect by accident.  FM_CHUNK_WG_PER_CU overrides (0: no cap).
-  const int wg_cu = chunk_wg_per_cu(lpr, a.mode);
-  const int chunk_static_lds = kind == kChunkAny ? (int)sizeof(int) * (2 * kMaxPieceOwners + 1) : 0;  // piece walk
+  const int wg_cu = chunk_wg_per_cu(lpr, kind);
+  const bool pcw = kind == kChunkAny || kind == kChunkEmitPc || kind == kChunkEmitPcNoX;
+  const int chunk_static_lds = pcw ? (int)sizeof(int) * (2 * kMaxPieceOwners + 1) : 0;  // piece walk
   const int chunk_lds = wg_cu > 0 ? lds_for_wg_per_cu(wg_cu, chunk_static_lds) : 0;
   if (kind == kChunkLocalNoX) {
     FM_DISPATCH_WIDE(dtype, lpr, fm_bwd_chunk_local_nox_kernel, g1, chunk_lds, st, a);
   } else if (kind == kChunkLocal) {
     FM_DISPATCH_WIDE(dtype, lpr, fm_bwd_chunk_local_kernel, g1, chunk_lds, st, a);
+  } else if (kind == kChunkEmit) {
+    FM_DISPATCH_WIDE(dtype, lpr, fm_bwd_chunk_emit_kernel, g1, chunk_lds, st, a);
+  } else if (kind == kChunkEmitNoX) {
+    FM_DISPATCH_WIDE(dtype, lpr, fm_bwd_chunk_emit_nox_kernel, g1, chunk_lds, st, a);
+  } else if (kind == kChunkEmitPc) {
+    FM_DISPATCH_WIDE(dtype, lpr, fm_bwd_chunk_emit_pc_kernel, g1, chunk_lds, st, a);
+  } else if (kind == kChunkEmitPcNoX) {
+    FM_DISPATCH_WIDE(dtype, lpr, fm_bwd_chunk_emit_pc_nox_kernel, g1, chunk_lds, st, a);
   } else {
     FM_DISPATCH_SHM(dtype, lpr, fm_bwd_chunk_kernel, g1, chunk_lds, st, a);
   }

@@ -55,6 +55,16 @@ __device__ inline uint32_t sr_next(uint32_t r) {
   return r;
 }
 
+// A computed address (e.g. broadcast between lanes) as a global-memory pointer: without the
+// address space hipcc emits flat loads, which count against both vmcnt and lgkmcnt and make every
+// wait a full drain (the sharded forward's row loads: profiles/r5).
+template <typename T>
+__device__ inline const __attribute__((address_space(1))) T* gptr(uint64_t addr) {
+  return reinterpret_cast<const __attribute__((address_space(1))) T*>(addr);
+}
+typedef float gf4 __attribute__((ext_vector_type(4)));      // (HIP's float4 / uint2 have no copy
+typedef uint32_t gu2 __attribute__((ext_vector_type(2)));   //  constructor from address_space(1))
+
 // ---- 16-byte row fragments ------------------------------------------------
 template <typename T> struct Frag;
 
@@ -63,6 +73,10 @@ template <> struct Frag<float> {
   static constexpr bool kScaled = false;
   __device__ static inline void load(const float* p, float (&o)[4]) {
     const float4 v = *reinterpret_cast<const float4*>(p);
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+  }
+  __device__ static inline void load_g(uint64_t a, float (&o)[4]) {
+    const gf4 v = *gptr<gf4>(a);
     o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
   }
   __device__ static inline void store(float* p, const float (&o)[4]) {
@@ -96,6 +110,13 @@ template <> struct Frag<__hip_bfloat16> {
   static constexpr bool kScaled = false;
   __device__ static inline void load(const __hip_bfloat16* p, float (&o)[4]) {
     const uint2 v = *reinterpret_cast<const uint2*>(p);
+    o[0] = bf16_bits_to_f32(v.x & 0xffffu);
+    o[1] = bf16_bits_to_f32(v.x >> 16);
+    o[2] = bf16_bits_to_f32(v.y & 0xffffu);
+    o[3] = bf16_bits_to_f32(v.y >> 16);
+  }
+  __device__ static inline void load_g(uint64_t a, float (&o)[4]) {
+    const gu2 v = *gptr<gu2>(a);
     o[0] = bf16_bits_to_f32(v.x & 0xffffu);
     o[1] = bf16_bits_to_f32(v.x >> 16);
     o[2] = bf16_bits_to_f32(v.y & 0xffffu);
@@ -144,6 +165,7 @@ template <> struct Frag<fp8e4m3> {
     o[0] = lo[0]; o[1] = lo[1]; o[2] = hi[0]; o[3] = hi[1];
   }
   __device__ static inline void load(const fp8e4m3* p, float (&o)[4]) { cvt(*reinterpret_cast<const int*>(p), o); }
+  __device__ static inline void load_g(uint64_t a, float (&o)[4]) { cvt(*gptr<int>(a), o); }
   // q * s for a power-of-two row scale s (fp8_row_scale) in the conversion instruction itself
   __device__ static inline void cvt_scaled(int u, float s, float (&o)[4]) {
     const auto lo = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(u, s, false);

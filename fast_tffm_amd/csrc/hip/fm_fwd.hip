@@ -93,11 +93,6 @@ constexpr int fwd_min_waves() {
 // k128 fp8 FTRL 0.806 -> 0.784 ms; bf16 / fp32 rows keep 12 at 4 (lower pairs spill there: k128
 // bf16 FTRL 0.95 -> 1.07-1.21 ms; profiles/r4/fwd_occupancy_ab.txt).  FM_FWD_UNR32[_FP8] /
 // FM_FWD_LOCAL_W32[_FP8]: A/B knobs.
-// Sharded fp8 forward reads the stored row norms (wire tail word 2 / the table's); 0: per-element
-// s2 as before (the "fwdshnonorm" A/B build variant)
-#ifndef FM_FWD_SH_NORM
-#define FM_FWD_SH_NORM 1
-#endif
 #ifndef FM_FWD_LOCAL_W32
 #define FM_FWD_LOCAL_W32 4
 #endif
@@ -120,49 +115,65 @@ constexpr int fwd_min_waves() {
 #ifndef FM_FWD_UNR4
 #define FM_FWD_UNR4 5
 #endif
+// The sharded forward's 16-lane rows (k = 64): its row address takes two broadcasts and a 64-bit
+// add (the local kernel's: one broadcast and a mad), a longer per-row-group chain, and 2 row groups
+// at 7 waves ran 0.70 ms EMIT (fwd 228-244 us vs the local kernel's 175): 10 in flight at 4 waves
+// instead (FM_FWD_UNR16_SH / FM_FWD_SH_W16, A/B build variants).
+#ifndef FM_FWD_UNR16_SH
+#define FM_FWD_UNR16_SH 10
+#endif
+#ifndef FM_FWD_SH_W16
+#define FM_FWD_SH_W16 4
+#endif
 template <typename TV>
 constexpr bool fwd_is_bf16() { return std::is_same<TV, __hip_bfloat16>::value; }
-template <int LPR, typename TV>
+template <int LPR, typename TV, bool SH = false>
 constexpr int fwd_local_min_waves() {
   return LPR == 4 && fwd_is_bf16<TV>() && FM_FWD_LOCAL_W4 > 0 ? FM_FWD_LOCAL_W4
-         : LPR == 16 ? FM_FWD_LOCAL_W16
+         : LPR == 16 ? (SH && !Frag<TV>::kScaled ? FM_FWD_SH_W16 : FM_FWD_LOCAL_W16)
          : LPR == 32 ? (Frag<TV>::kScaled ? FM_FWD_LOCAL_W32_FP8 : FM_FWD_LOCAL_W32)
                      : fwd_min_waves<LPR, TV>();
 }
-template <int LPR, typename TV, bool SH>
+template <int LPR, typename TV, bool SH = false>
 constexpr int fwd_unroll() {
-  return SH ? FwdUnroll<kWave / LPR>::v
+  return LPR == 16 && SH && !Frag<TV>::kScaled ? FM_FWD_UNR16_SH
          : LPR == 4 && fwd_is_bf16<TV>() && FM_FWD_UNR4 > 0 ? FM_FWD_UNR4
          : LPR == 16 ? FM_FWD_UNR16
          : LPR == 32 ? (Frag<TV>::kScaled ? FM_FWD_UNR32_FP8 : FM_FWD_UNR32)
                      : FwdUnroll<kWave / LPR>::v;
 }
 
-// SH: the row-sharded step's features (self rows, segment lookup: a tagged row index selects the
-// table, rows[] may be keys).  The local step's instantiation (SH = false) addresses every row as
-// base + row * stride with one 32 x 32 -> 64-bit multiply-add and reads the broadcast pairs with
-// precomputed ds_bpermute offsets: per row group ~5 address / index VALU instructions instead of
-// ~16 (the tag test, base / stride selects and a 64-bit stride multiply), on a kernel the PMC
-// table shows 62% (k64 fp32) / 82% (k128 fp8) VALU-busy (profiles/r4/pmc_*.txt).
+// SH: the row-sharded step's features -- rows[] may be keys (segment lookup), an occurrence's row
+// lives either in the gathered wire buffer (segment u) or, for this rank's own rows, in the table
+// (SelfRows).  Both instantiations share the mechanics measured on the local step: the example's
+// (row, value) pairs are loaded lane-parallel and broadcast with precomputed ds_bpermute offsets,
+// fp8 rows arrive raw and are converted with their power-of-two row scale (v_cvt_scalef32), s2 /
+// reg come from the stored row norms, and the occupancy / rows-in-flight pair is the local one.
+// The local kernel addresses a row as base + row * stride (one 32 x 32 -> 64-bit mad per row
+// group); the sharded one resolves each occurrence's row to a byte address once, lane-parallel
+// (source select, segment lookup, tail loads), and broadcasts the 64-bit address (two ds_bpermute
+// and one 64-bit add per row group) -- no per-row-group tag test or base / stride select.
 template <int LPR, typename TV, bool SH>
 __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
   using F = Frag<TV>;
   constexpr int EPL = F::N;
   constexpr int G = kWave / LPR;
-  // (FM_FWD_UNR16: row groups in flight of the local kernel's 16-lane instantiations, k = 64)
   constexpr int UNR = fwd_unroll<LPR, TV, SH>();
+  // fp8: raw 4-byte fragments converted with the row scale; s2 / reg from the stored norms
+  constexpr bool kRaw = F::kScaled;
+  constexpr bool kNorm = F::kScaled;
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR, t = lane % LPR;
   const int nv = a.Kp / EPL;
   const bool tact = t < nv;
   const int tE = tact ? t : nv - 1;        // clamped: loads never leave the row
   const float tmask = tact ? 1.f : 0.f;
-  const TV* vbase = reinterpret_cast<const TV*>(a.v) + tE * EPL;
+  const uint32_t coff = (uint32_t)(tE * EPL * (int)sizeof(TV));  // this lane's column byte offset
   // (local step) byte base of this lane's fragment and the row stride in bytes (< 2^32: host-checked)
-  const char* vbytes = reinterpret_cast<const char*>(vbase);
+  const char* vbytes = reinterpret_cast<const char*>(a.v) + coff;
   const uint32_t vsb = (uint32_t)(a.v_stride * (long long)sizeof(TV));
   const bool self_on = SH && a.self.u1 > a.self.u0;  // (uniform)
-  const TV* tbase = self_on ? reinterpret_cast<const TV*>(a.self.v) + tE * EPL : vbase;
+  const uint32_t tsb = self_on ? (uint32_t)(a.self.v_stride * (long long)sizeof(TV)) : vsb;
   const int wave = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   const int nwaves = gridDim.x * kWavesPerBlock;
   const bool want_reg = a.reg_partial != nullptr;
@@ -170,7 +181,6 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
   const bool self_key = SH && self_on && a.seg_idx != nullptr;
   const int self_kmin = self_key ? a.self.keys[a.self.u0] : 0;
   const int self_kmax = self_key ? a.self.keys[a.self.u1 - 1] : -1;
-
   const int wv = threadIdx.x >> 6;
 
   float loss_acc = 0.f, regv_acc = 0.f, regw_acc = 0.f;
@@ -222,86 +232,84 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
 #pragma unroll
     for (int k = 0; k < EPL; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
     float lin = 0.f, rv = 0.f, rw = 0.f;
-    // fp8 (kNorm): s2 = sum_j x_j^2 |v_j|^2 from the rows' stored norms, one occurrence per lane
-    // (sharded step: the wire row's tail carries the norm next to [w, scale], own rows the table's)
-    constexpr bool kNorm = F::kScaled && (!SH || FM_FWD_SH_NORM);
-    float s2n = 0.f;
+    float s2n = 0.f;  // (kNorm) sum_j x_j^2 |v_j|^2, one occurrence per lane
     for (int base = s; base < e; base += kWave) {
       const int m = min(kWave, e - base);
       int my_row = 0;
       float my_x = 0.f, my_w = 0.f, my_s = 1.f, my_n2 = 0.f;
+      uint64_t my_p = 0;  // (SH) byte address of the occurrence's row, column 0
       if (kPrefetch && base == s) {
         my_row = p_row;
         my_x = p_x;
       } else {
         pairs(base, m, my_row, my_x);
       }
-      if (kNorm && !SH && lane < m) {  // [w, scale, |v|^2, pad]: one 16-byte load (w_stride 4, host-checked)
-        const float4 wr = *reinterpret_cast<const float4*>(a.w + (uint64_t)(uint32_t)my_row * 4u);
-        my_w = wr.x;
-        my_s = wr.y;
-        my_n2 = wr.z;
-      } else if (!SH && lane < m) {
-        my_w = a.w[(long long)my_row * a.w_stride];
-        my_s = row_scale<TV>(a.w, my_row, a.w_stride);
-      } else if (lane < m) {
-        // segment lookup mode: rows[] are keys; an own row is known by its key alone (the self
-        // segments are exactly the batch's keys in [self_kmin, self_kmax]), so it needs neither
-        // the lookup nor the segment's key load -- at world 1 every row
-        const int key = my_row;
-        const bool own_key = self_key && key >= self_kmin && key <= self_kmax;
-        if (SH && a.seg_idx && !own_key) my_row = seg_lookup(a, key);
-        // the linear weight (and fp8 scale, same cache line) of occurrence `lane`, one
-        // lane-parallel load per 64 occurrences instead of one per row group: the w loads
-        // were ~45% of the kernel's VMEM instructions with the TA 72% busy
-        // (profiles/r2/pmc_k64_fp32_before.txt)
-        if (own_key || (self_on && !self_key && a.self.has(my_row))) {
-          // own table row: its index with the top bit set selects the table in the row loads
-          const long long trow = own_key ? (long long)key - a.self.base : a.self.row(my_row);
-          my_w = a.self.w[trow * a.self.w_stride];
-          my_s = row_scale<TV>(a.self.w, trow, a.self.w_stride);
-          if constexpr (kNorm) my_n2 = a.self.w[trow * a.self.w_stride + kFp8Norm];
-          my_row = (int)trow | kSelfBit;
-        } else {
-          my_w = a.w[(long long)my_row * a.w_stride];
-          my_s = row_scale<TV>(a.w, my_row, a.w_stride);
-          if constexpr (kNorm) my_n2 = a.w[(long long)my_row * a.w_stride + kFp8Norm];
+      if constexpr (!SH) {
+        if (lane < m) {
+          if constexpr (kNorm) {  // [w, scale, |v|^2, pad]: one 16-byte load (w_stride 4, host-checked)
+            const float4 wr = *reinterpret_cast<const float4*>(a.w + (uint64_t)(uint32_t)my_row * 4u);
+            my_w = wr.x;
+            my_s = wr.y;
+            my_n2 = wr.z;
+          } else {
+            my_w = a.w[(long long)my_row * a.w_stride];
+          }
         }
+      } else {
+        if (lane < m) {
+          // segment lookup mode: rows[] are keys; an own row is known by its key alone (the self
+          // segments are exactly the batch's keys in [self_kmin, self_kmax]), so it needs neither
+          // the lookup nor the segment's key load -- at world 1 every row
+          const int key = my_row;
+          const bool own_key = self_key && key >= self_kmin && key <= self_kmax;
+          if (a.seg_idx && !own_key) my_row = seg_lookup(a, key);
+          // the linear weight (fp8: with scale and norm, one 16-byte tail) of occurrence `lane`,
+          // one lane-parallel load per 64 occurrences instead of one per row group
+          const bool own = own_key || (self_on && !self_key && a.self.has(my_row));
+          const long long r = own ? (own_key ? (long long)key - a.self.base : a.self.row(my_row)) : my_row;
+          const char* b0 = reinterpret_cast<const char*>(own ? a.self.v : a.v);
+          my_p = reinterpret_cast<uint64_t>(b0) + (uint64_t)(uint32_t)r * (own ? tsb : vsb);
+          const uint64_t wp = reinterpret_cast<uint64_t>(own ? a.self.w + r * a.self.w_stride : a.w + r * a.w_stride);
+          if constexpr (kNorm) {  // [w, scale, |v|^2, tag] wire tails / [w, scale, |v|^2, pad] table rows
+            const gf4 wr = *gptr<gf4>(wp);
+            my_w = wr.x;
+            my_s = wr.y;
+            my_n2 = wr.z;
+          } else {
+            my_w = *gptr<float>(wp);
+          }
+        }
+        // lanes past the example take lane 0's row: the wrapped slots of a round read a valid row
+        const uint64_t p0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(my_p >> 32)) << 32) |
+                            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)my_p);
+        if (lane >= m) my_p = p0;
       }
+      const int p_lo = (int)(uint32_t)my_p, p_hi = (int)(my_p >> 32);
       for (int q = 0; q < m; q += G * UNR) {
         float fr[UNR][EPL], fx[UNR], fs[UNR];
-        // (local fp8: the raw 4-byte fragment, converted with its power-of-two row scale once that
-        // has arrived: v_cvt_scalef32_pk_f32_fp8, no per-element scale multiply)
-        constexpr bool kRaw = F::kScaled && !SH;
         int fraw[kRaw ? UNR : 1];
-        // Issue every row load of the round before the first use.  Loads are
-        // unconditional (slots past the example re-read a valid row of it and are
-        // masked to zero afterwards), so hipcc keeps all UNR loads in flight.
+        // Issue every row load of the round before the first use.  Loads are unconditional (slots
+        // past the example read a valid row -- lanes past it hold row 0 / lane 0's row -- and are
+        // masked to zero afterwards), so hipcc keeps all UNR loads in flight.  Lanes past the round
+        // wrap around the wave (ds_bpermute takes the lane modulo 64).
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
           const int f = q + u * G + g;
+          const int fb = (f & (kWave - 1)) << 2;
+          const float x = __int_as_float(__builtin_amdgcn_ds_bpermute(fb, __float_as_int(my_x)));
+          fx[u] = f < m ? x : 0.f;
           if constexpr (SH) {
-            const int src = f < m ? f : 0;
-            const int row = __shfl(my_row, src, kWave);
-            const float x = __shfl(my_x, src, kWave);
-            fx[u] = f < m ? x : 0.f;
-            // (one load either way: the tagged index selects the base, not the instruction)
-            const TV* rp = row < 0 ? tbase + (long long)(row & ~kSelfBit) * a.self.v_stride
-                                   : vbase + (long long)row * a.v_stride;
-            F::load(rp, fr[u]);
-            if constexpr (F::kScaled) fs[u] = __shfl(my_s, src, kWave);
+            const uint64_t pr = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(fb, p_hi) << 32) |
+                                (uint32_t)__builtin_amdgcn_ds_bpermute(fb, p_lo);
+            if constexpr (kRaw) fraw[u] = *gptr<int>(pr + coff);
+            else F::load_g(pr + coff, fr[u]);
           } else {
-            // lanes past the round wrap around the wave (ds_bpermute takes the lane modulo 64):
-            // a valid row of this example or row 0, masked by fx = 0
-            const int fb = (f & (kWave - 1)) << 2;
             const int row = __builtin_amdgcn_ds_bpermute(fb, my_row);
-            const float x = __int_as_float(__builtin_amdgcn_ds_bpermute(fb, __float_as_int(my_x)));
-            fx[u] = f < m ? x : 0.f;
             const char* rp = vbytes + (uint64_t)(uint32_t)row * vsb;
             if constexpr (kRaw) fraw[u] = *reinterpret_cast<const int*>(rp);
             else F::load(reinterpret_cast<const TV*>(rp), fr[u]);
-            if constexpr (F::kScaled) fs[u] = __int_as_float(__builtin_amdgcn_ds_bpermute(fb, __float_as_int(my_s)));
           }
+          if constexpr (F::kScaled) fs[u] = __int_as_float(__builtin_amdgcn_ds_bpermute(fb, __float_as_int(my_s)));
         }
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
@@ -309,12 +317,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
           // (folding the fp8 row scale into the occurrence's x instead of every element, with the
           // reg term as a per-occurrence sum times scale^2 -- fewer VALU ops -- made the k128 fp8
           // FTRL step slower, 0.888 -> 1.014 ms same-box: profiles/r4/specialize_ab.txt)
-          if constexpr (kRaw) {
-            F::cvt_scaled(fraw[u], fs[u], fv);
-          } else if constexpr (F::kScaled) {
-#pragma unroll
-            for (int k = 0; k < EPL; ++k) fv[k] *= fs[u];
-          }
+          if constexpr (kRaw) F::cvt_scaled(fraw[u], fs[u], fv);
           const float xm = fx[u] * tmask;
 #pragma unroll
           for (int k = 0; k < EPL; ++k) {
@@ -332,9 +335,9 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
       // (w is used after the row loads were issued: its load latency hides under theirs)
       lin += my_x * my_w;
       if (want_reg) rw += my_w * my_w;
-      if constexpr (kNorm) {  // (lanes past the example: x = 0, |v|^2 = 0)
+      if constexpr (kNorm) {  // (lanes past the example: x = 0; their norm is not summed)
         s2n += my_x * my_x * my_n2;
-        if (want_reg) rv += my_n2;
+        if (want_reg && lane < m) rv += my_n2;
       }
     }
     float part = 0.f;
@@ -404,7 +407,7 @@ void fm_fwd_kernel(FwdArgs a) {
 
 // The row-sharded step's forward (self rows, segment lookup).
 template <int LPR, typename TV>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(fwd_min_waves<LPR, TV>())))
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(fwd_local_min_waves<LPR, TV, true>())))
 void fm_fwd_shard_kernel(FwdArgs a) {
   fwd_body<LPR, TV, true>(a);
 }
@@ -454,9 +457,14 @@ int launch_fwd(const FwdArgs& a, int dtype, int grid, hipStream_t st) {
   const int lpr = lanes_per_row(a.Kp, dtype);
   // (capping the forward's workgroups per CU through dynamic LDS, as the chunk backward does, tied
   // on k64 fp32: profiles/r4/wg_per_cu_ab.txt)
-  // (the local fp8 forward reads [w, scale, |v|^2, pad] rows: Table's layout, w_stride 4)
-  const bool fp8_norm_ok = dtype != kFP8 || a.w_stride == 4;
-  if (a.self.u1 > a.self.u0 || a.seg_idx || !FM_FWD_SPECIALIZE || !fp8_norm_ok) {
+  // fp8 rows: [w, scale, |v|^2, .] tails read as one 16-byte load (table rows: w_stride 4; wire
+  // rows: the 16-byte tail after the factor bytes) -- for the wire / self sources as well
+  if (dtype == kFP8) {
+    auto aligned = [](const float* w, long long ws) { return ((uintptr_t)w & 15) == 0 && ws % 4 == 0; };
+    if (!aligned(a.w, a.w_stride) || (a.self.u1 > a.self.u0 && !aligned(a.self.w, a.self.w_stride))) return -7;
+  }
+  const bool table_rows = dtype != kFP8 || a.w_stride == 4;  // (the local kernel's fp8 tails: w + 4 row)
+  if (a.self.u1 > a.self.u0 || a.seg_idx || !FM_FWD_SPECIALIZE || !table_rows) {
     FM_DISPATCH(dtype, lpr, fm_fwd_shard_kernel, grid, st, a);
   } else {
     FM_DISPATCH(dtype, lpr, fm_fwd_kernel, grid, st, a);

@@ -251,13 +251,12 @@ class ShardExchange(_Base):
         # (which can then become the critical path): "auto" uses it with two batches of lookahead
         self.prefetch_depth1 = self.prefetch and forced
         # split backward: the gradient rows of every owner's first half travel (P2P on RCCL)
-        # while the second half is reduced.  On by default ("auto" = on with one part): since the
-        # segment lookup and self rows the two backward pieces are cheaper than one pass even at
-        # world 1 (0.747-0.751 -> 0.697-0.702 ms, k16 bf16 0.559-0.563 -> 0.551-0.554; round 2
-        # measured +0.1-0.19 ms before those, profiles/r2/self_rows_ab.txt; profiles/r3/shard_split_ab.txt),
-        # and at world > 1 they hide half of the gradient exchange
+        # while the second half is reduced, hiding half of the gradient exchange behind compute.
+        # "auto" = on with one part at world > 1; off at world 1, where no gradient row leaves the
+        # rank and the second pass only costs (k128 fp8 FTRL EMIT 1.121 -> 1.056 ms without it,
+        # profiles/README.md round 4; "on" forces it, the tests' way to run the pieces at world 1)
         og = str(getattr(model.cfg, "overlap_grads", "auto")).lower()
-        self.overlap_grads = self.nparts == 1 and og in ("auto", "on", "true", "1")
+        self.overlap_grads = self.nparts == 1 and (og in ("on", "true", "1") or (og == "auto" and self.W > 1))
         # self rows (hip/fm_common.h SelfRows): this rank's own rows are read from the table by the
         # forward / backward -- no owner gather, no row exchange or early copy to patch for them --
         # and the exclusive ones (requested by no other rank this step) are updated in place by

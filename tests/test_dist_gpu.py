@@ -187,13 +187,21 @@ def test_rccl_world1_early_exchange_matches_local(rccl_ctx, dtype, k, depth, sel
     torch.testing.assert_close(dm.table.reference_rows(), loc.table.reference_rows(), rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("self_rows", ["0", "1"])
+def _self_rows_env(monkeypatch, self_rows: str) -> None:
+    """"0": no self rows (every row through the wire); "1": self rows (at world 1 the step then runs
+    the local kernels); "emit": self rows on the EMIT path of world > 1 (FM_SHARD_W1_LOCAL=0)."""
+    monkeypatch.setenv("FM_SELF_ROWS", "0" if self_rows == "0" else "1")
+    if self_rows == "emit":
+        monkeypatch.setenv("FM_SHARD_W1_LOCAL", "0")
+
+
+@pytest.mark.parametrize("self_rows", ["0", "1", "emit"])
 @pytest.mark.parametrize("dtype,k", [(torch.float32, 64), (torch.bfloat16, 16), (K.FP8, 128)])
 def test_rccl_world1_split_backward_matches_local(rccl_ctx, dtype, k, self_rows, monkeypatch):
     """Backward split into every owner's first / second half of rows (overlap_grads=on, with
     the early row exchange) reduces exactly what the one-piece backward does (self rows: both
     pieces update their rows in place)."""
-    monkeypatch.setenv("FM_SELF_ROWS", self_rows)
+    _self_rows_env(monkeypatch, self_rows)
     V = 20000
     gen = CriteoSynth(V, device="cuda", seed=26)
     batches = [gen.batch(2048) for _ in range(5)]
@@ -216,13 +224,13 @@ def test_rccl_world1_split_backward_matches_local(rccl_ctx, dtype, k, self_rows,
     torch.testing.assert_close(dm.table.reference_rows(), loc.table.reference_rows(), rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("self_rows", ["0", "1"])
+@pytest.mark.parametrize("self_rows", ["0", "1", "emit"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_rccl_world1_pipelined_shard_step_is_bitwise_deterministic(rccl_ctx, dtype, self_rows, monkeypatch):
     """Race detection for the sharded pipeline: with the side-stream plan two
     batches ahead, the early row exchange + patches and the split backward all on, two runs
     of the same batches leave bit-identical tables (bf16 with stochastic rounding too)."""
-    monkeypatch.setenv("FM_SELF_ROWS", self_rows)
+    _self_rows_env(monkeypatch, self_rows)
     V = 20000
     gen = CriteoSynth(V, device="cuda", seed=27)
     batches = [gen.batch(4096) for _ in range(6)]

@@ -29,21 +29,21 @@ def _free_port() -> int:
     return free_port()
 
 
-def _cfg(mode, bcfg, **kw):
+def _cfg(mode, bcfg, vocab=V, **kw):
     from fast_tffm_amd.models.fm import FMConfig
     from fast_tffm_amd.ops import kernels as K
 
     kw = dict(kw)
     dt = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp8": K.FP8}[kw.pop("dtype", "fp32")]
-    return FMConfig(vocabulary_size=V, factor_num=KF, loss_type="logistic", factor_lambda=0.01, bias_lambda=0.01,
+    return FMConfig(vocabulary_size=vocab, factor_num=KF, loss_type="logistic", factor_lambda=0.01, bias_lambda=0.01,
                     batch_size=bcfg, init_value_range=0.05, seed=11, mode=mode, grad_reduce="mean", dtype=dt,
                     stochastic_rounding=False, opt=K.OptConfig("adagrad", lr=0.05), **kw)
 
 
-def _batch(step, rank):
+def _batch(step, rank, vocab=V, batch=B):
     from fast_tffm_amd.data.synthetic import CriteoSynth
 
-    return CriteoSynth(V, seed=1000 * step + rank, device="cuda").batch(B)
+    return CriteoSynth(vocab, seed=1000 * step + rank, device="cuda").batch(batch)
 
 
 def _worker(rank, world, port, out_dir, variant, mode="shard"):
@@ -56,35 +56,48 @@ def _worker(rank, world, port, out_dir, variant, mode="shard"):
 
     variant = dict(variant)
     os.environ.update(variant.pop("env", {}))
+    vocab, batch, steps = variant.pop("shape", (V, B, STEPS))
     ctx = fmdist.init_distributed(backend="gloo", rank=rank, world=world, device="cuda:0")
-    m = FactorizationMachine(_cfg(mode, B, **variant), device="cuda:0", dist=ctx)
-    bs = [_batch(s, rank) for s in range(STEPS)]
+    m = FactorizationMachine(_cfg(mode, batch, vocab, **variant), device="cuda:0", dist=ctx)
+    bs = [_batch(s, rank, vocab, batch) for s in range(steps)]
     losses = []
-    for s in range(STEPS):
-        nb = bs[s + 1] if s + 1 < STEPS else None
-        nb2 = bs[s + 2] if s + 2 < STEPS else None
+    for s in range(steps):
+        nb = bs[s + 1] if s + 1 < steps else None
+        nb2 = bs[s + 2] if s + 2 < steps else None
         losses.append(m.train_step(bs[s], nb, nb2).mean_loss())
     torch.cuda.synchronize()
     ex = m._exchange
-    torch.save({"gids": m.table.global_ids().cpu(), "rows": m.table.reference_rows().cpu(), "losses": losses,
+    gids = m.table.global_ids()
+    if vocab > V:  # (large tables: the rows any rank's batches touched, not the whole shard)
+        touched = torch.unique(torch.cat([_batch(s, r, vocab, batch).ids.long() for s in range(steps)
+                                          for r in range(world)]))
+        keep = (touched % world) == rank
+        gids = touched[keep]
+        rows = m.table.reference_rows(gids // world).cpu()
+    else:
+        rows = m.table.reference_rows().cpu()
+    torch.save({"gids": gids.cpu(), "rows": rows, "losses": losses,
                 "early": getattr(ex, "early_steps", 0), "split": getattr(ex, "overlap_grads", False),
                 "comm": getattr(ex, "comm_mode", None), "violations": relay.violations()},
                os.path.join(out_dir, f"rank{rank}.pt"))
     fmdist.shutdown()
 
 
-def _reference(world, dtype):
+def _reference(world, dtype, shape=(V, B, STEPS), gids=None):
     from fast_tffm_amd.data.batch import Batch
     from fast_tffm_amd.models.fm import FactorizationMachine
 
-    ref = FactorizationMachine(_cfg("local", B * world, dtype=dtype), device="cuda")
-    for s in range(STEPS):
-        parts = [_batch(s, r) for r in range(world)]
+    vocab, batch, steps = shape
+    ref = FactorizationMachine(_cfg("local", batch * world, vocab, dtype=dtype), device="cuda")
+    for s in range(steps):
+        parts = [_batch(s, r, vocab, batch) for r in range(world)]
         offs = torch.cat([parts[0].offsets] + [p.offsets[1:] + parts[0].nnz * i  # (every part: B x 39 features)
                                                for i, p in enumerate(parts[1:], 1)])
         ref.train_step(Batch(torch.cat([p.labels for p in parts]), offs, torch.cat([p.ids for p in parts]), None, None,
                              sum(p.nnz for p in parts)))
     torch.cuda.synchronize()
+    if gids is not None:
+        return ref.table.reference_rows(gids.to("cuda")).cpu()
     return ref.table.reference_rows().cpu()
 
 
@@ -132,3 +145,17 @@ def test_replicated_modes_on_one_gpu_equal_one_process(tmp_path, world, mode):
     for r in res:
         torch.testing.assert_close(r["rows"], want, rtol=1e-5, atol=1e-6)
     assert all(torch.equal(r["rows"], res[0]["rows"]) for r in res)
+
+
+def test_ranks_on_one_gpu_headline_shape(tmp_path):
+    """World 2 at a realistic row heat: 32768 examples per rank (~1.3M occurrences) over 10M rows,
+    so hot rows span many chunks and both owners (the lane-group combine and the workgroup big-row
+    kernels run under the split backward's two pieces, with self rows, early rows and patches under
+    the asynchronous relay); the touched rows equal one process on the concatenated batches."""
+    shape = (10_000_000, 32768, 3)
+    res = _run(tmp_path, 2, dict(shape=shape))
+    assert all(r["split"] and r["early"] == shape[2] - 1 for r in res)
+    gids = torch.cat([r["gids"] for r in res])
+    got = torch.cat([r["rows"] for r in res])
+    want = _reference(2, "fp32", shape, gids)
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-6)

@@ -10,5 +10,6 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $R/bench.py --steps 20 --warmup 5 "$@" > $OUT/prof.log 2>&1 || { echo "rocprof failed"; tail -30 $OUT/prof.log; exit 1; }
 grep ms/step $OUT/prof.log
 python3 $R/tools/kstats.py $OUT/prof/run_kernel_stats.csv 25 > $OUT/kernel_summary.txt
-python3 $R/tools/timeline.py $OUT/prof/run_kernel_trace.csv $MARK > $OUT/timeline.txt
+MC=$(ls $OUT/prof/*memory_copy_trace.csv 2>/dev/null | head -1)
+python3 $R/tools/timeline.py $OUT/prof/run_kernel_trace.csv $MARK $MC > $OUT/timeline.txt
 rm -f $OUT/prof/*.csv  # (per-dispatch traces: keep the summaries, stay under gpurun's merge-back limit)
