@@ -13,4 +13,5 @@ HIP_VARIANTS: dict[str, list[str]] = {"fwdnopf": ["-DFM_FWD_PREFETCH=0"], "fwdge
                                      "cu32_8": ["-DFM_CHUNK_UNR32=8"],
                                      "sh16u2w7": ["-DFM_FWD_UNR16_SH=2", "-DFM_FWD_SH_W16=7"],
                                      "sh16u4w6": ["-DFM_FWD_UNR16_SH=4", "-DFM_FWD_SH_W16=6"],
-                                     "sh16u6w5": ["-DFM_FWD_UNR16_SH=6", "-DFM_FWD_SH_W16=5"]}
+                                     "sh16u6w5": ["-DFM_FWD_UNR16_SH=6", "-DFM_FWD_SH_W16=5"],
+                                     "mfprof": ["-DFM_MF_PROF=1"]}

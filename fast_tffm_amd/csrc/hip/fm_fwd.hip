@@ -39,6 +39,7 @@ struct FwdArgs {
   const int* seg_idx;      // [nb + 1] first segment of each key bucket, or null (rows are segment ids)
   const int* seg_keys;     // [U] sorted unique keys
   int seg_shift;           // bucket = key >> seg_shift
+  int max_feats;           // host-known max occurrences per example (-1: unknown); the MFMA fp8 path needs it
 };
 
 // Segment of key k (present in the batch): the bucket's first candidate, then a scan over the
@@ -412,6 +413,8 @@ void fm_fwd_shard_kernel(FwdArgs a) {
   fwd_body<LPR, TV, true>(a);
 }
 
+#include "fm_fwd_mfma.hip"
+
 // Expand CSR offsets into the example index of every occurrence.
 // Example of every CSR occurrence; with slot_bits > 0 the packed occurrence code
 // (example << slot_bits) | (position inside the example), which the dedup sort
@@ -450,6 +453,18 @@ __global__ __launch_bounds__(kBlock) void csr_rows_kernel(int B, const int* offs
   }
 }
 
+// FM_FWD_MFMA=1 (or set_fwd_mfma(true)): fp8 k=128 batches of binary features take the matrix-core
+// kernel (fm_fwd_mfma.hip; off by default until it beats the VALU kernel: profiles/r5/fwd_mfma_ab.txt)
+static int g_fwd_mfma = -1;
+bool fwd_mfma_enabled() {
+  if (g_fwd_mfma < 0) {
+    const char* e = getenv("FM_FWD_MFMA");
+    g_fwd_mfma = e && atoi(e) != 0;
+  }
+  return g_fwd_mfma != 0;
+}
+void set_fwd_mfma(bool on) { g_fwd_mfma = on; }
+
 int fwd_grid(int B) { return fill_grid(B, kWavesPerBlock, 4096); }
 
 int launch_fwd(const FwdArgs& a, int dtype, int grid, hipStream_t st) {
@@ -464,6 +479,13 @@ int launch_fwd(const FwdArgs& a, int dtype, int grid, hipStream_t st) {
     if (!aligned(a.w, a.w_stride) || (a.self.u1 > a.self.u0 && !aligned(a.self.w, a.self.w_stride))) return -7;
   }
   const bool table_rows = dtype != kFP8 || a.w_stride == 4;  // (the local kernel's fp8 tails: w + 4 row)
+  // fp8 rows on the matrix cores (fm_fwd_mfma.hip): binary features, Kp = 128, table rows, tiles of 16
+  // examples within the kernel's LDS row capacity.
+  if (fwd_mfma_enabled() && dtype == kFP8 && a.Kp == kMfRowB && a.v_stride == kMfRowB && !a.vals && table_rows &&
+      a.self.u1 <= a.self.u0 && !a.seg_idx && a.max_feats > 0 && a.max_feats * kMfT <= kMfMaxRows) {
+    hipLaunchKernelGGL(fm_fwd_mfma_fp8_kernel, dim3(grid), dim3(kBlock), 0, st, a);
+    return (int)hipGetLastError();
+  }
   if (a.self.u1 > a.self.u0 || a.seg_idx || !FM_FWD_SPECIALIZE || !table_rows) {
     FM_DISPATCH(dtype, lpr, fm_fwd_shard_kernel, grid, st, a);
   } else {

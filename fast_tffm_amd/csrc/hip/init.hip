@@ -64,16 +64,19 @@ __global__ __launch_bounds__(kBlock) void init_rows_fp8_kernel(InitArgs a) {
 
 // |v|^2 of fp8 rows (w_row[kFp8Norm], fm_common.h fp8_norm2) from their stored bytes and scales:
 // one LPR-lane group per row, the same reduction as store_row's.  After init and after any write
-// of rows / scales from the host side (checkpoint restore, Table.set_v).
+// of rows / scales from the host side (checkpoint restore, Table.set_v).  ``idx`` (optional): the
+// rows to refresh (``rows`` of them), else rows 0 .. rows - 1.
 template <int LPR>
 __global__ __launch_bounds__(kBlock) void fp8_norms_kernel(const uint8_t* v, long long v_stride, float* w,
-                                                           long long w_stride, long long rows, int Kp) {
+                                                           long long w_stride, long long rows, int Kp,
+                                                           const long long* idx) {
   constexpr int G = kWave / LPR;
   const int lane = threadIdx.x & (kWave - 1), t = lane % LPR;
   const bool tact = t < Kp / 4;
   const long long gid = ((long long)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + lane / LPR;
   const long long stride = (long long)gridDim.x * kWavesPerBlock * G;
-  for (long long r = gid; r < rows; r += stride) {  // (uniform per group: the butterfly stays in it)
+  for (long long i = gid; i < rows; i += stride) {  // (uniform per group: the butterfly stays in it)
+    const long long r = idx ? idx[i] : i;
     const int u = tact ? *reinterpret_cast<const int*>(v + r * v_stride + 4 * t) : 0;
     const float n2 = fp8_norm2<LPR>(u, w[r * w_stride + 1], tact);
     if (t == 0) w[r * w_stride + kFp8Norm] = n2;
@@ -82,7 +85,7 @@ __global__ __launch_bounds__(kBlock) void fp8_norms_kernel(const uint8_t* v, lon
 
 // v_stride in bytes (= elements of an fp8 table)
 int launch_fp8_norms(const uint8_t* v, long long v_stride, float* w, long long w_stride, long long rows, int Kp,
-                     hipStream_t st) {
+                     hipStream_t st, const long long* idx) {
   if (rows <= 0) return 0;
   if (Kp % 4 != 0 || w_stride <= kFp8Norm) return -1;
   const int lpr = lanes_per_row(Kp, kFP8);
@@ -91,7 +94,7 @@ int launch_fp8_norms(const uint8_t* v, long long v_stride, float* w, long long w
   if (blocks > 16384) blocks = 16384;
   switch (lpr) {
 #define FM_NORMS(L) \
-  case L: hipLaunchKernelGGL(fp8_norms_kernel<L>, dim3((int)blocks), dim3(kBlock), 0, st, v, v_stride, w, w_stride, rows, Kp); break;
+  case L: hipLaunchKernelGGL(fp8_norms_kernel<L>, dim3((int)blocks), dim3(kBlock), 0, st, v, v_stride, w, w_stride, rows, Kp, idx); break;
     FM_NORMS(1) FM_NORMS(2) FM_NORMS(4) FM_NORMS(8) FM_NORMS(16) FM_NORMS(32) FM_NORMS(64)
 #undef FM_NORMS
     default: return -1;
@@ -107,7 +110,8 @@ int launch_init_rows(const InitArgs& a, hipStream_t st) {
     if (blocks > 16384) blocks = 16384;
     hipLaunchKernelGGL(init_rows_fp8_kernel, dim3((int)blocks), dim3(kBlock), 0, st, a);
     if (hipGetLastError() != hipSuccess) return -2;
-    return launch_fp8_norms(reinterpret_cast<const uint8_t*>(a.v), a.v_stride, a.w, a.w_stride, a.rows, a.Kp, st);
+    return launch_fp8_norms(reinterpret_cast<const uint8_t*>(a.v), a.v_stride, a.w, a.w_stride, a.rows, a.Kp, st,
+                            nullptr);
   }
   const long long total = a.rows * (long long)(a.Kp + 1);
   long long blocks = (total + kBlock - 1) / kBlock;

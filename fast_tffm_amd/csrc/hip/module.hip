@@ -79,6 +79,18 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
   m.attr("MAX_CH") = fm::kMaxCH;
 
   m.def("fwd_grid", &fm::fwd_grid, py::arg("B"));
+  m.def("fwd_mfma_enabled", &fm::fwd_mfma_enabled);
+  m.def("set_fwd_mfma", &fm::set_fwd_mfma, py::arg("on"));
+#if FM_MF_PROF
+  m.def("mf_prof", [] {  // (build variant "mfprof") phase clocks of the MFMA forward, then cleared
+    unsigned long long h[8] = {};
+    hipDeviceSynchronize();
+    hipMemcpyFromSymbol(h, HIP_SYMBOL(fm::g_mf_prof), sizeof(h));
+    const unsigned long long z[8] = {};
+    hipMemcpyToSymbol(HIP_SYMBOL(fm::g_mf_prof), z, sizeof(z));
+    return std::vector<unsigned long long>(h, h + 8);
+  });
+#endif
   m.def("lanes_per_row", &fm::lanes_per_row, py::arg("Kp"), py::arg("dtype"));
 
   m.def(
@@ -86,8 +98,9 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       [](int B, u64 offsets, u64 rows, u64 vals, u64 v, long long v_stride, u64 w, long long w_stride, int Kp,
          int dtype, u64 labels, u64 weights, int loss_type, float grad_scale, u64 pred, u64 r1, u64 dpred,
          u64 loss_partial, u64 reg_partial, int grid, u64 stream, u64 bias, const std::vector<long long>& self,
-         u64 seg_idx, u64 seg_keys, int seg_shift) {
+         u64 seg_idx, u64 seg_keys, int seg_shift, int max_feats) {
         fm::FwdArgs a{};
+        a.max_feats = max_feats;
         a.seg_idx = P<const int>(seg_idx); a.seg_keys = P<const int>(seg_keys); a.seg_shift = seg_shift;
         if (a.seg_idx && (!a.seg_keys || seg_shift < 0 || seg_shift > 31))
           throw std::invalid_argument("fm_fwd: segment lookup needs the sorted keys and a shift in [0, 31]");
@@ -106,7 +119,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("loss_type"), py::arg("grad_scale"), py::arg("pred"), py::arg("r1"), py::arg("dpred"),
       py::arg("loss_partial"), py::arg("reg_partial"), py::arg("grid"), py::arg("stream"), py::arg("bias") = 0,
       py::arg("self_rows") = std::vector<long long>{}, py::arg("seg_idx") = 0, py::arg("seg_keys") = 0,
-      py::arg("seg_shift") = 0);
+      py::arg("seg_shift") = 0, py::arg("max_feats") = -1);
 
   m.def(
       "seg_index",
@@ -307,12 +320,13 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("stream"));
   m.def(
       "fp8_row_norms",
-      [](u64 v, long long v_stride, u64 w, long long w_stride, long long rows, int Kp, u64 stream) {
-        check(fm::launch_fp8_norms(P<const uint8_t>(v), v_stride, P<float>(w), w_stride, rows, Kp, S(stream)),
+      [](u64 v, long long v_stride, u64 w, long long w_stride, long long rows, int Kp, u64 stream, u64 idx) {
+        check(fm::launch_fp8_norms(P<const uint8_t>(v), v_stride, P<float>(w), w_stride, rows, Kp, S(stream),
+                                   P<const long long>(idx)),
               "fp8_row_norms");
       },
       py::arg("v"), py::arg("v_stride"), py::arg("w"), py::arg("w_stride"), py::arg("rows"), py::arg("Kp"),
-      py::arg("stream"));
+      py::arg("stream"), py::arg("idx") = 0);
   m.attr("FP8_NORM_COL") = fm::kFp8Norm;
 
   m.def(

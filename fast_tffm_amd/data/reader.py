@@ -376,7 +376,7 @@ class NativeTextReader:
         tokenizer's CSR out (ids / values sized for the densest possible batch: a token takes >= 2
         bytes), its counts / status / scan workspace."""
         dev, B, nb = self._feed_dev, self.args["batch_size"], self._slot_bytes
-        cap = B * _bin_max_feats(self.args["files"]) + 1 if self.binary else nb // 2 + B + 1
+        cap = _bin_slot_cap(self.args["files"], B) if self.binary else nb // 2 + B + 1
         if self.gpu is None:
             nb = 1  # (parse mode: no raw bytes on the device)
         i32 = dict(dtype=torch.int32, device=dev)
@@ -547,17 +547,23 @@ class NativeTextReader:
         return b
 
 
-def _bin_max_feats(files: list[str]) -> int:
-    """Largest example (features) over the .fmb caches' headers (csrc/cpu/bincsr.h: i32 max_feats at
-    byte 40): a feeder slot of B times it holds any batch."""
+def _bin_slot_cap(files: list[str], B: int) -> int:
+    """ids / vals entries of a feeder slot for .fmb caches (csrc/cpu/bincsr.h header: i64 n at byte
+    16, i64 nnz at 24, i32 max_feats at 40): the caches' mean features per example x B with 50%
+    headroom, at most B x their largest example; a denser batch gets larger buffers through the
+    feeder's resize request (next() -> "resize")."""
     import struct
 
-    m = 1
+    n = nnz = 0
+    mf = 1
     for f in files:
         with open(f, "rb") as fh:
             head = fh.read(64)
-        m = max(m, struct.unpack_from("<i", head, 40)[0])
-    return m
+        fn, fnnz = struct.unpack_from("<qq", head, 16)
+        n, nnz = n + fn, nnz + fnnz
+        mf = max(mf, struct.unpack_from("<i", head, 40)[0])
+    mean = nnz / max(n, 1)
+    return min(B * mf, int(B * mean * 1.5) + 4096) + 1
 
 
 def _feeder_available() -> bool:

@@ -495,7 +495,7 @@ class FactorizationMachine:
             fo = K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,
                               weights=b.weights, loss=cfg.loss_type, grad_scale=self.grad_scale(b.B), want_r1=True,
                               pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
-                              threads=cfg.threads, bias=self.gbias, defer_loss=gpu)
+                              threads=cfg.threads, bias=self.gbias, defer_loss=gpu, max_feats=b.max_feats)
             self.bias_step(fo.dpred)
         if gpu:
             main.wait_stream(side)
@@ -558,7 +558,7 @@ class FactorizationMachine:
             fo = K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,
                               weights=b.weights, loss=cfg.loss_type, grad_scale=self.grad_scale(b.B), want_r1=True,
                               pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
-                              threads=cfg.threads, bias=self.gbias, defer_loss=True)
+                              threads=cfg.threads, bias=self.gbias, defer_loss=True, max_feats=b.max_feats)
             self.bias_step(fo.dpred)
         with roctx_range("bwd+update"):
             K.fm_backward(dd, fo.dpred, fo.r1, self.Kp, mode=K.BWD_LOCAL, table=self.table.state, opt=cfg.opt,
@@ -650,7 +650,7 @@ class FactorizationMachine:
         rows = b.ids.to(torch.int32)
         return K.fm_forward(b.offsets, rows, b.vals, self.table.v, self.table.w, self.Kp, labels=b.labels,
                             weights=b.weights, loss=loss, grad_scale=1.0, want_r1=False, want_reg=want_reg,
-                            threads=self.cfg.threads, bias=self.gbias)
+                            threads=self.cfg.threads, bias=self.gbias, max_feats=b.max_feats)
 
     def predict(self, b: Batch) -> torch.Tensor:
         """Raw scores (logits for logistic loss), like the reference's pred_ops (run_tffm.py:10-17)."""

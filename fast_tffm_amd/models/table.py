@@ -122,29 +122,39 @@ class FMTable:
                 self.scale[real:] = 1.0
                 self.norm2[real:] = 0.0
 
-    def adopt_fp8_rows(self) -> None:
+    def adopt_fp8_rows(self, local_rows: torch.Tensor | None = None) -> None:
         """After fp8 rows and scales were written as stored bytes (checkpoint restore): rows whose
         scale is not a power of two (written before scales were; the scaled conversion in the
         forward applies only a scale's exponent) are re-quantised from their dequantised values,
-        then every row's norm is recomputed."""
+        then the rows' norms are recomputed.  ``local_rows``: only these rows were written (an index
+        tensor), else all."""
         if not self.fp8:
             return
-        mant, _ = torch.frexp(self.scale)
+        rows = None if local_rows is None else _as_index(local_rows, self.device)
+        mant, _ = torch.frexp(self.scale if rows is None else self.scale[rows])
         bad = torch.nonzero(mant != 0.5).flatten()
+        if rows is not None:
+            bad = rows[bad]
         if bad.numel():
-            vals = self.dense_v(bad)[:, : self.K]
-            self.set_v(bad, vals)  # (refreshes the norms)
-        else:
-            self.refresh_norms()
+            self.set_v(bad, self.dense_v(bad)[:, : self.K])  # (refreshes the norms of these rows)
+        self.refresh_norms(rows)
 
-    def refresh_norms(self) -> None:
+    def refresh_norms(self, local_rows: torch.Tensor | None = None) -> None:
         """Recompute the fp8 rows' |v|^2 column from the stored rows and scales (after writing v or
-        the scales from the host side; the kernels keep it current themselves)."""
+        the scales from the host side; the kernels keep it current themselves) -- of every row, or
+        of ``local_rows`` (an index tensor) only."""
         if not self.fp8:
             return
-        native.hip().fp8_row_norms(v=self.v.data_ptr(), v_stride=self.v.stride(0), w=self.wx.data_ptr(),
-                                   w_stride=self.wx.stride(0), rows=self.rows, Kp=self.Kp,
-                                   stream=torch.cuda.current_stream(self.device).cuda_stream)
+        h = native.hip()
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        kw = dict(v=self.v.data_ptr(), v_stride=self.v.stride(0), w=self.wx.data_ptr(), w_stride=self.wx.stride(0),
+                  Kp=self.Kp, stream=st)
+        if local_rows is None:
+            h.fp8_row_norms(rows=self.rows, **kw)
+            return
+        idx = _as_index(local_rows, self.device)
+        if idx.numel():
+            h.fp8_row_norms(rows=idx.numel(), idx=idx.data_ptr(), **kw)
 
     def global_ids(self) -> torch.Tensor:
         return torch.arange(self.rows, device=self.device, dtype=torch.int64) * self.world + self.rank
@@ -183,9 +193,10 @@ class FMTable:
             q, s = K.quantize_fp8_rows(full)
             if local_rows is None:
                 self.v[:n], self.scale[:n] = q, s
+                self.refresh_norms(torch.arange(n, device=self.device))
             else:
                 self.v[local_rows], self.scale[local_rows] = q, s
-            self.refresh_norms()
+                self.refresh_norms(local_rows)
             return
         vals = vals.to(self.device, self.dtype)
         if local_rows is None:
@@ -208,6 +219,13 @@ class FMTable:
         gb = self.nbytes() / 2**30
         return (f"table shard rank {self.rank}/{self.world}: {self.rows} rows x K={self.K} (Kp={self.Kp}, "
                 f"{str(self.dtype).replace('torch.', '')}), opt={self.opt.name}: {gb:.2f} GiB")
+
+
+def _as_index(rows, device) -> torch.Tensor:
+    """Row selection (index tensor or slice) -> contiguous int64 indices on ``device``."""
+    if isinstance(rows, slice):
+        return torch.arange(rows.start or 0, rows.stop, device=device, dtype=torch.int64)
+    return rows.to(device=device, dtype=torch.int64).contiguous().flatten()
 
 
 def bits_for(n: int) -> int:

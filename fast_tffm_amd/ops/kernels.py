@@ -38,6 +38,15 @@ def set_debug_checks(on: bool) -> None:
     _DEBUG = bool(on)
 
 
+def set_fwd_mfma(on: bool) -> bool:
+    """Route fp8 k=128 binary-feature forwards to the matrix-core kernel (hip/fm_fwd_mfma.hip; default
+    off, FM_FWD_MFMA=1 at start-up turns it on) or the VALU kernel; returns the previous setting."""
+    h = native.hip()
+    was = bool(h.fwd_mfma_enabled())
+    h.set_fwd_mfma(bool(on))
+    return was
+
+
 FP8 = torch.float8_e4m3fn   # OCP e4m3 table storage (+ fp32 scale per row), GPU only
 FP8_MAX = 448.0
 
@@ -181,7 +190,7 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
                r1: torch.Tensor | None = None, dpred: torch.Tensor | None = None,
                partial: torch.Tensor | None = None, threads: int = 0,
                bias: torch.Tensor | None = None, self_rows: SelfRows | None = None,
-               seg_lookup: "SegIndex | None" = None, defer_loss: bool = False) -> FwdOut:
+               seg_lookup: "SegIndex | None" = None, defer_loss: bool = False, max_feats: int = -1) -> FwdOut:
     """FM score of a CSR batch (reference FmScorer, cc/fm_scorer_op.h:101-140), fused with the loss.
 
     pred_i = sum_j x_j w_j + 1/2 sum_k [(sum_j x_j v_jk)^2 - sum_j x_j^2 v_jk^2]  (+ bias[0], optional
@@ -194,6 +203,8 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
     row of ``v``) is found through the bucket index (``seg_index``) instead of an inverse map.
     (``defer_loss``, GPU: the per-workgroup loss partials are left for ``FwdOut.finish_loss``, so the
     reduction can be enqueued after the backward instead of between forward and backward.)
+    ``max_feats`` (host-known maximum occurrences per example, -1 unknown): lets fp8 k=128 batches of
+    binary features run on the matrix cores (hip/fm_fwd_mfma.hip).
     """
     dev = rows.device
     B = offsets.numel() - 1
@@ -230,6 +241,13 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
     if lt and dpred is None:
         dpred = torch.empty(B, dtype=torch.float32, device=dev)
     dt = dtype_code(v.dtype)
+    if _DEBUG and max_feats is not None and max_feats >= 0 and B > 0:
+        _check(int((offsets[1:] - offsets[:-1]).max()) <= max_feats, "max_feats: an example has more features")
+    if _DEBUG and v.dtype == FP8 and w_stride == 4 and v.shape[0] > 0:
+        # table rows [w, scale, |v|^2, .]: the kernels apply only the scale's exponent, so every host
+        # write of v / scale must keep scales powers of two (FMTable.set_v / adopt_fp8_rows do)
+        sc = torch.as_strided(w, (v.shape[0],), (4,), w.storage_offset() + 1)
+        _check(bool((torch.frexp(sc)[0] == 0.5).all()), "fp8 table: a row scale is not a power of two")
     if _is_gpu(rows):
         h = native.hip()
         grid = h.fwd_grid(max(B, 1))
@@ -248,7 +266,8 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
               stream=_stream(rows), bias=_p(bias),
               seg_idx=_p(seg_lookup.idx) if seg_lookup is not None else 0,
               seg_keys=_p(seg_lookup.keys) if seg_lookup is not None else 0,
-              seg_shift=seg_lookup.shift if seg_lookup is not None else 0, **dkw)
+              seg_shift=seg_lookup.shift if seg_lookup is not None else 0,
+              max_feats=int(max_feats) if max_feats is not None else -1, **dkw)
         # (an in-kernel last-block reduction was measured slower: the per-block agent-scope
         # release fence writes back L2 -- fwd 211 -> 412 us; a separate reduce is ~10 us; the same
         # reduce on a second stream beside the backward measured slower too: 0.668-0.671 -> 0.676 ms,

@@ -843,7 +843,8 @@ class ShardExchange(_Base):
                     fo = K.fm_forward(sb.offsets, part.keys, sb.vals, m.table.v, m.table.w, Kp, labels=sb.labels,
                                       weights=sb.weights, loss=cfg.loss_type, grad_scale=gscale, want_r1=True,
                                       pred=ws.pred[: sb.B], r1=ws.r1[: sb.B], dpred=ws.dpred[: sb.B],
-                                      partial=ws.fwd_partial, threads=cfg.threads, bias=m.gbias, defer_loss=True)
+                                      partial=ws.fwd_partial, threads=cfg.threads, bias=m.gbias, defer_loss=True,
+                                      max_feats=sb.max_feats)
                 with roctx_range("bwd_local"):
                     K.fm_backward(dd, fo.dpred, fo.r1, Kp, mode=K.BWD_LOCAL, table=m.table.state, opt=cfg.opt,
                                   reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, sr_counter=sr)
@@ -944,7 +945,7 @@ class DPExchange(_Base):
         fo = K.fm_forward(b.offsets, rows, b.vals, m.table.v, m.table.w, Kp, labels=b.labels, weights=b.weights,
                           loss=cfg.loss_type, grad_scale=m.grad_scale(b.B), want_r1=True, pred=ws.pred[: b.B],
                           r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial, threads=cfg.threads,
-                          bias=m.gbias)
+                          bias=m.gbias, max_feats=b.max_feats)
         m.bias_step(fo.dpred)
         dd = K.dedup(rows, ws=ws.dd, key_bits=bits_for(m.table.rows), ex_of_occ=ex, vals=b.vals,
                      num_examples=b.B, Kp=Kp)
@@ -991,7 +992,7 @@ class DPExchange(_Base):
         t = self.m.table
         return K.fm_forward(b.offsets, b.ids.to(torch.int32), b.vals, t.v, t.w, self.Kp, labels=b.labels,
                             weights=b.weights, loss=loss, grad_scale=1.0, want_r1=False, want_reg=want_reg,
-                            threads=self.m.cfg.threads, bias=self.m.gbias)
+                            threads=self.m.cfg.threads, bias=self.m.gbias, max_feats=b.max_feats)
 
 
 def dp_dense_blocks(world: int) -> int:
@@ -1137,7 +1138,7 @@ class DPDenseExchange(DPExchange):
             fo = K.fm_forward(b.offsets, pl.rows, b.vals, m.table.v, m.table.w, Kp, labels=b.labels,
                               weights=b.weights, loss=cfg.loss_type, grad_scale=m.grad_scale(b.B), want_r1=True,
                               pred=ws.pred[: b.B], r1=ws.r1[: b.B], dpred=ws.dpred[: b.B], partial=ws.fwd_partial,
-                              bias=m.gbias)
+                              bias=m.gbias, max_feats=b.max_feats)
             m.bias_step(fo.dpred)
         rv, rw = m.reg_coeffs
         # backward pieces by key block, each block's reduce-scatter issued behind its piece

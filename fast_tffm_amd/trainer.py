@@ -94,12 +94,16 @@ class Trainer:
                            f"every rank resumes at rank 0's position")
         self.reader_state = ReaderState(epoch=int(rs.get("epoch", 0)),
                                         batches_in_epoch=int(rs.get("batches_in_epoch", 0)))
-        if rs and int(rs.get("draw_version", 1)) != DRAW_VERSION:
+        dv = rs.get("draw_version") if rs else None
+        if rs and dv is None:
+            # (checkpoints written before the field existed: the draws may or may not be this build's)
+            self.print(f"Note: checkpoint reader position does not record its shuffle draw version; resuming "
+                       f"with this build's draws (version {DRAW_VERSION})")
+        elif rs and int(dv) != DRAW_VERSION:
             # the loader's shuffle draws changed between the builds: the same seed gives another line
             # order, so replaying batches_in_epoch batches does not land on the same examples
             self.print(f"Warning: checkpoint reader position was written with shuffle draw version "
-                       f"{rs.get('draw_version', 1)} (this build: {DRAW_VERSION}); the resumed epoch repeats "
-                       f"or skips some examples")
+                       f"{dv} (this build: {DRAW_VERSION}); the resumed epoch repeats or skips some examples")
         self.restored_from = path
         self.print(f"Restored checkpoint {path} (global step {self.model.global_step})")
         return True

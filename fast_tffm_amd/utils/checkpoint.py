@@ -283,7 +283,8 @@ def _copy_rows(table, local_rows, t: dict, K: int, dev) -> None:
     if table.fp8 and "v_fp8" in t:
         put(table.v.view(torch.uint8), t["v_fp8"])
         put(table.scale, t["v_scale"])
-        table.adopt_fp8_rows()  # (power-of-two scales + row norms)
+        # (power-of-two scales + row norms, of the rows this chunk wrote)
+        table.adopt_fp8_rows(torch.arange(t["v_scale"].shape[0], device=dev) if local_rows is None else local_rows)
     elif table.fp8:
         if isinstance(local_rows, slice):
             local_rows = torch.arange(local_rows.start, local_rows.stop, device=dev)
