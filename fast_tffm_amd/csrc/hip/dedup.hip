@@ -25,6 +25,7 @@
 // low-cardinality fields) is spread over many lane groups in the backward.
 #include "fm_common.h"
 #include <rocprim/rocprim.hpp>
+#include <string>
 
 namespace fm {
 
@@ -285,13 +286,33 @@ static size_t sort_temp_bytes(int n, hipStream_t st) {
   return align_up(best);
 }
 
-// Workspace layout: [onesweep temp | pad (8 B), tile_cnt[ntiles]]
+#include "radix_sort.hip"
+
+// Sort backend: rocPRIM onesweep (default) or the in-tree multipass radix sort (radix_sort.hip,
+// FM_SORT=fm: bitwise the same stable order; profiles/r5/sort_ab.txt)
+static int g_sort_algo = -1;
+static bool sort_in_tree() {
+  if (g_sort_algo < 0) {
+    const char* e = getenv("FM_SORT");
+    g_sort_algo = (e && std::string(e) == "fm") ? 1 : 0;
+  }
+  return g_sort_algo == 1;
+}
+void set_sort_algo(int in_tree) { g_sort_algo = in_tree ? 1 : 0; }
+int sort_algo() { return sort_in_tree() ? 1 : 0; }
+
+// Workspace layout: [sort temp (the larger of the two backends') | pad (8 B), tile_cnt[ntiles]]
 static size_t lb_bytes(int ntiles) { return 8 + 8 * (size_t)ntiles; }
+
+static size_t sort_ws_bytes(int n, hipStream_t st) {
+  const size_t a = sort_temp_bytes(n, st), b = align_up(radix_sort_ws_bytes(n));
+  return a > b ? a : b;
+}
 
 size_t dedup_workspace_bytes(int n) {
   if (n <= 0) return 256;
   const size_t ntiles = ((size_t)n + kRleTile - 1) / kRleTile;
-  return sort_temp_bytes(n, 0) + align_up(lb_bytes((int)ntiles)) + 256;
+  return sort_ws_bytes(n, 0) + align_up(lb_bytes((int)ntiles)) + 256;
 }
 
 struct DedupArgs {
@@ -365,14 +386,19 @@ int launch_dedup(const DedupArgs& a, hipStream_t st) {
   }
   const int ntiles = (a.n + kRleTile - 1) / kRleTile;
   if (ntiles > kMaxTiles) return -3;
-  const size_t tmp = sort_temp_bytes(a.n, st);
+  const size_t tmp = sort_ws_bytes(a.n, st);
   char* base = static_cast<char*>(a.ws);
   char* lb = base + tmp;
   if (tmp + align_up(lb_bytes(ntiles)) > a.ws_bytes) return -2;
 
-  size_t sort_bytes = tmp;
-  const hipError_t e = sort_pairs(a.ws, sort_bytes, a.keys, a.skeys, a.payload, a.spay, a.n, a.end_bit, st);
-  if (e != hipSuccess) return (int)e;
+  if (sort_in_tree()) {
+    const int e = launch_radix_sort(a.keys, a.payload, a.skeys, a.spay, a.n, a.end_bit, a.ws, tmp, st);
+    if (e != 0) return e;
+  } else {
+    size_t sort_bytes = tmp;
+    const hipError_t e = sort_pairs(a.ws, sort_bytes, a.keys, a.skeys, a.payload, a.spay, a.n, a.end_bit, st);
+    if (e != hipSuccess) return (int)e;
+  }
   RleArgs r{a.n, a.CH, ntiles, a.skeys, a.spay, a.ex_shift,
             a.offsets, reinterpret_cast<unsigned long long*>(lb + 8), a.uniq, a.seg_start,
             a.seg_chunk, a.chunk_start, a.chunk_seg, a.chunk_key, a.counts, a.inv, a.ex_of_occ, a.sorted_ex,

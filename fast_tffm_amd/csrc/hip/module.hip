@@ -182,6 +182,18 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("self_rows") = std::vector<long long>{}, py::arg("chunk_grid") = 0);
 
   m.def("dedup_workspace_bytes", &fm::dedup_workspace_bytes, py::arg("n"));
+  m.def("set_sort_algo", &fm::set_sort_algo, py::arg("in_tree"));  // 1: radix_sort.hip, 0: rocPRIM onesweep
+  m.def("sort_algo", &fm::sort_algo);
+  m.def(
+      "radix_sort",  // stable (key, value) sort of the in-tree backend (tests / benchmarks)
+      [](u64 keys, u64 vals, u64 kout, u64 vout, int n, int end_bit, u64 ws, size_t ws_bytes, u64 stream) {
+        check(fm::launch_radix_sort(P<const uint32_t>(keys), P<const int>(vals), P<uint32_t>(kout), P<int>(vout), n,
+                                    end_bit, P<void>(ws), ws_bytes, S(stream)),
+              "radix_sort");
+      },
+      py::arg("keys"), py::arg("vals"), py::arg("kout"), py::arg("vout"), py::arg("n"), py::arg("end_bit"),
+      py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"));
+  m.def("radix_sort_ws_bytes", &fm::radix_sort_ws_bytes, py::arg("n"));
   m.def(
       "dedup",
       [](int n, int end_bit, int CH, u64 keys, u64 payload, u64 skeys, u64 spay, u64 uniq, u64 seg_start,

@@ -2,9 +2,11 @@
 // (reference tf.unique, tffm/fm_model.py:72-73, is a hash table; this framework groups a batch's
 // occurrences by sorting them: dedup.hip).
 //
-// Per digit pass (8 or 9 bits, 2-4 passes over the key bits in use) three kernels, no atomics and
-// no spin-waits (a decoupled look-back over ~1000 tiles that start together walks back serially
-// over each other's status words, the cost the RLE kernels' comment in dedup.hip records):
+// Per digit pass (8 or 9 bits, 2-4 passes over the key bits in use) three kernels, no global
+// atomics and no spin-waits.  (A onesweep form -- one histogram kernel, one kernel per pass with a
+// decoupled look-back reading 64 predecessor tiles per load -- measured 479 us for 24-bit keys
+// against this form's 161 and rocPRIM's 148: the ~600 tiles that start together resolve their
+// prefixes over tile / 64 round trips per digit batch; profiles/r5/sort_ab.txt.)
 //   count: each 8192-element tile counts its digits -> cnt[tile][digit] (one coalesced row);
 //   scan:  per digit, exclusive prefixes over the tiles (in place) and the digit's total;
 //   scatter: each tile re-ranks its elements (stable), scans the digit totals into digit bases,
@@ -53,12 +55,21 @@ __device__ inline uint64_t rs_match(uint32_t d, uint64_t live) {
   return m;
 }
 
-// Wave-local stable ranking of the wave's 512 elements: wcnt (this wave's D counters in LDS,
+// Wave-local stable ranking of the wave's 1024 elements: wcnt (this wave's D counters in LDS,
 // zeroed by the caller) ends as the wave's digit counts; rank[i] = position of slot i's element
 // among the wave's elements of its digit.
+#ifndef FM_RS_RANK_ATOMIC
+#define FM_RS_RANK_ATOMIC 1
+#endif
 template <int DB>
-__device__ inline void rs_rank_wave(const uint32_t (&dig)[kRsItems], const bool (&ok)[kRsItems], uint16_t* wcnt,
+__device__ inline void rs_rank_wave(const uint32_t (&dig)[kRsItems], const bool (&ok)[kRsItems], unsigned* wcnt,
                                     unsigned (&rank)[kRsItems]) {
+#if FM_RS_RANK_ATOMIC
+  // ds_add_rtn_u32 per element: the LDS serves the lanes of one instruction that hit the same counter
+  // in ascending lane order (checked bitwise against a stable sort: tests/test_kernels.py, bench_fmsort)
+#pragma unroll
+  for (int i = 0; i < kRsItems; ++i) rank[i] = ok[i] ? atomicAdd(&wcnt[dig[i]], 1u) : 0u;
+#else
   const int lane = threadIdx.x & (kWave - 1);
   const uint64_t lt = rs_lanemask_lt(lane);
 #pragma unroll
@@ -69,8 +80,9 @@ __device__ inline void rs_rank_wave(const uint32_t (&dig)[kRsItems], const bool 
     unsigned base = 0;
     if (ok[i]) base = wcnt[dig[i]];
     rank[i] = base + below;
-    if (ok[i] && below == 0) wcnt[dig[i]] = (uint16_t)(base + (unsigned)__popcll(peers));
+    if (ok[i] && below == 0) wcnt[dig[i]] = base + (unsigned)__popcll(peers);
   }
+#endif
 }
 
 template <int DB>
@@ -87,20 +99,21 @@ __device__ inline void rs_load(const RsPass& p, int tile, uint32_t (&key)[kRsIte
   }
 }
 
-// 1. tile digit counts
+// 1. tile digit counts (LDS atomics into per-wave counters: no ranking needed)
 template <int DB>
 __global__ __launch_bounds__(kRsThreads) void rs_count_kernel(RsPass p) {
   constexpr int D = 1 << DB;
-  __shared__ uint16_t wc[kRsWaves][D];
+  __shared__ unsigned wc[kRsWaves][D];
   const int wv = threadIdx.x >> 6;
-  for (int t = threadIdx.x; t < kRsWaves * D; t += kRsThreads) (&wc[0][0])[t] = 0;
+  for (int t = threadIdx.x; t < kRsWaves * D; t += kRsThreads) (&wc[0][0])[t] = 0u;
   __syncthreads();
   const int tile = blockIdx.x;
   uint32_t key[kRsItems], dig[kRsItems];
   bool ok[kRsItems];
   rs_load<DB>(p, tile, key, dig, ok);
-  unsigned rank[kRsItems];
-  rs_rank_wave<DB>(dig, ok, wc[wv], rank);
+#pragma unroll
+  for (int i = 0; i < kRsItems; ++i)
+    if (ok[i]) atomicAdd(&wc[wv][dig[i]], 1u);
   __syncthreads();
   for (int d = threadIdx.x; d < D; d += kRsThreads) {
     unsigned s = 0;
@@ -167,14 +180,13 @@ __device__ inline unsigned rs_block_excl(unsigned v, unsigned* sh /*[kRsWaves]*/
 template <int DB>
 __global__ __launch_bounds__(kRsThreads) void rs_scatter_kernel(RsPass p) {
   constexpr int D = 1 << DB;
-  __shared__ uint16_t wc[kRsWaves][D];   // wave digit counts -> tile positions of the waves' digit runs
+  __shared__ unsigned wc[kRsWaves][D];   // wave digit counts -> tile positions of the waves' digit runs
   __shared__ int gofs[D];                // global position of the tile's digit-d run minus its tile position
-  __shared__ uint32_t sk[kRsTile];
-  __shared__ int sv[kRsTile];
+  __shared__ uint32_t stage[kRsTile];    // the tile in digit order: keys, then values
   __shared__ unsigned sh[kRsWaves];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
   const int tile = blockIdx.x;
-  for (int t = threadIdx.x; t < kRsWaves * D; t += kRsThreads) (&wc[0][0])[t] = 0;
+  for (int t = threadIdx.x; t < kRsWaves * D; t += kRsThreads) (&wc[0][0])[t] = 0u;
   __syncthreads();
   uint32_t key[kRsItems], dig[kRsItems];
   bool ok[kRsItems];
@@ -197,7 +209,7 @@ __global__ __launch_bounds__(kRsThreads) void rs_scatter_kernel(RsPass p) {
 #pragma unroll
       for (int w = 0; w < kRsWaves; ++w) {
         const unsigned c = wc[w][d];
-        wc[w][d] = (uint16_t)s;
+        wc[w][d] = s;
         s += c;
       }
     }
@@ -215,28 +227,37 @@ __global__ __launch_bounds__(kRsThreads) void rs_scatter_kernel(RsPass p) {
   __syncthreads();
   if (threadIdx.x < D) {
 #pragma unroll
-    for (int w = 0; w < kRsWaves; ++w) wc[w][threadIdx.x] = (uint16_t)(wc[w][threadIdx.x] + tstart);
+    for (int w = 0; w < kRsWaves; ++w) wc[w][threadIdx.x] += tstart;
   }
   __syncthreads();
+  unsigned pos[kRsItems];
 #pragma unroll
   for (int i = 0; i < kRsItems; ++i) {
-    if (ok[i]) {
-      const unsigned pos = wc[wv][dig[i]] + rank[i];
-      sk[pos] = key[i];
-      sv[pos] = val[i];
-    }
+    pos[i] = wc[wv][dig[i]] + rank[i];
+    if (ok[i]) stage[pos[i]] = key[i];
   }
   __syncthreads();
   const int tn = min(kRsTile, p.n - tile * kRsTile);
+  int gpos[kRsItems];
 #pragma unroll
   for (int i = 0; i < kRsItems; ++i) {
     const int j = threadIdx.x + i * kRsThreads;
+    gpos[i] = -1;
     if (j < tn) {
-      const uint32_t k = sk[j];
-      const int g = gofs[(k >> p.shift) & p.dmask] + j;
-      p.kout[g] = k;
-      p.vout[g] = sv[j];
+      const uint32_t k = stage[j];
+      gpos[i] = gofs[(k >> p.shift) & p.dmask] + j;
+      p.kout[gpos[i]] = k;
     }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kRsItems; ++i)
+    if (ok[i]) stage[pos[i]] = (uint32_t)val[i];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kRsItems; ++i) {
+    const int j = threadIdx.x + i * kRsThreads;
+    if (gpos[i] >= 0) p.vout[gpos[i]] = (int)stage[j];
   }
 }
 
@@ -251,11 +272,11 @@ static inline void rs_plan(int end_bit, int& passes, int& db) {
 
 static inline size_t rs_align(size_t x) { return (x + 255) & ~size_t(255); }
 
-// Workspace: [alt keys n][alt values n][cnt D x ntiles][tot D]
+// Workspace: [alt keys n][alt values n][cnt ntiles x D][tot D]
 size_t radix_sort_ws_bytes(int n) {
   if (n <= 0) return 256;
   const size_t ntiles = ((size_t)n + kRsTile - 1) / kRsTile;
-  return rs_align(4 * (size_t)n) * 2 + rs_align(4 * kRsMaxDigits * ntiles) + rs_align(4 * kRsMaxDigits);
+  return rs_align(4 * (size_t)n) * 2 + rs_align(4 * (size_t)kRsMaxDigits * ntiles) + rs_align(4 * kRsMaxDigits);
 }
 
 template <int DB>
@@ -279,7 +300,7 @@ int launch_radix_sort(const uint32_t* keys, const int* vals, uint32_t* kout, int
   uint32_t* alt_k = reinterpret_cast<uint32_t*>(b);
   int* alt_v = reinterpret_cast<int*>(b + rs_align(4 * (size_t)n));
   unsigned* cnt = reinterpret_cast<unsigned*>(b + 2 * rs_align(4 * (size_t)n));
-  unsigned* tot = reinterpret_cast<unsigned*>(b + 2 * rs_align(4 * (size_t)n) + rs_align(4 * kRsMaxDigits * (size_t)ntiles));
+  unsigned* tot = reinterpret_cast<unsigned*>(b + 2 * rs_align(4 * (size_t)n) + rs_align(4 * (size_t)kRsMaxDigits * ntiles));
   const uint32_t* kin = keys;
   const int* vin = vals;
   for (int i = 0; i < passes; ++i) {

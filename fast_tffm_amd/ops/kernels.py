@@ -355,6 +355,31 @@ class DedupWorkspace:
             self.ws = None
 
 
+def set_sort_algo(algo: str) -> str:
+    """The dedup's sort backend: "rocprim" (onesweep, default) or "fm" (in-tree multipass radix sort,
+    hip/radix_sort.hip; same stable order); returns the previous one.  FM_SORT=fm at start-up too."""
+    _check(algo in ("rocprim", "fm"), f"sort backend {algo!r}: rocprim or fm")
+    h = native.hip()
+    was = "fm" if h.sort_algo() else "rocprim"
+    h.set_sort_algo(1 if algo == "fm" else 0)
+    return was
+
+
+def radix_sort(keys: torch.Tensor, vals: torch.Tensor, key_bits: int = 32) -> tuple[torch.Tensor, torch.Tensor]:
+    """Stable sort of int32 (key, value) pairs by the keys' low ``key_bits`` bits on the in-tree
+    radix sort (GPU): returns (sorted keys, values in the same order)."""
+    n = keys.numel()
+    _chk_vec(keys, torch.int32, n, "keys", keys.device)
+    _chk_vec(vals, torch.int32, n, "vals", keys.device)
+    _check(_is_gpu(keys), "radix_sort is a GPU kernel")
+    h = native.hip()
+    ko, vo = torch.empty_like(keys), torch.empty_like(vals)
+    ws = torch.empty(max(1, int(h.radix_sort_ws_bytes(n))), dtype=torch.uint8, device=keys.device)
+    h.radix_sort(keys=_p(keys), vals=_p(vals), kout=_p(ko), vout=_p(vo), n=n, end_bit=int(key_bits), ws=_p(ws),
+                 ws_bytes=ws.numel(), stream=_stream(keys))
+    return ko, vo
+
+
 def slot_bits_for(B: int, max_feats: int) -> int:
     """Bits of the in-example slot of a packed occurrence code, or 0 when codes do not fit int32."""
     if max_feats is None or max_feats < 1:

@@ -1,9 +1,10 @@
 """Dedup chain alone (csr_rows codes + grouping + chunk plan) on Criteo-shaped batches, per method.
 
-Times K.dedup back to back on a pool of batches (no step beside it), once per sort named in
-``--algo`` (the FM_SORT setting).  Run under ``rocprofv3 --kernel-trace --stats`` for per-kernel times.
+Times K.dedup back to back on a pool of batches (no step beside it), once per sort backend named in
+``--algo`` (rocprim = onesweep, fm = in-tree radix sort).  Run under ``rocprofv3 --kernel-trace
+--stats`` for per-kernel times.
 
-    python tools/bench_dedup.py [--algo onesweep] [--iters 30]
+    python tools/bench_dedup.py [--algo rocprim,fm] [--iters 30] [--vocab 125000000]
 """
 
 from __future__ import annotations
@@ -24,7 +25,7 @@ from fast_tffm_amd.ops import kernels as K  # noqa: E402
 
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--algo", default="onesweep", help="comma list of FM_SORT values")
+    ap.add_argument("--algo", default="rocprim,fm", help="comma list of sort backends (rocprim, fm)")
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--pool", type=int, default=4)
     ap.add_argument("--vocab", type=int, default=125_000_000)
@@ -39,7 +40,7 @@ def main() -> int:
         sb = K.slot_bits_for(b.B, b.max_feats)
         pool.append((b.ids.to(torch.int32), b.offsets, b.nnz, sb))
     for algo in a.algo.split(","):
-        os.environ["FM_SORT"] = algo
+        K.set_sort_algo(algo)
         ws = K.DedupWorkspace(max(p[0].numel() for p in pool), dev, 32)
 
         def run(i):

@@ -62,6 +62,7 @@ int main(int argc, char** argv) {
     const size_t wb = fm::radix_sort_ws_bytes(n);
     void* ws;
     CK(hipMalloc(&ws, wb));
+    CK(hipMemset(ws, 0, wb));
     hipStream_t st;
     CK(hipStreamCreate(&st));
     hipEvent_t e0, e1;
