@@ -169,14 +169,9 @@ void assemble_binary(const std::vector<BinItem>& its, const BinSet& bs, bool wei
     for (int32_t j = offs[i0]; j < offs[i1]; ++j) any |= static_cast<uint32_t>(ids_out[j]) >= V;
     bad[t] = any != 0;
   };
-  if (T == 1) {
-    work(0);
-  } else {
-    std::vector<std::thread> ths;
-    for (int t = 1; t < T; ++t) ths.emplace_back(work, t);
-    work(0);
-    for (auto& th : ths) th.join();
-  }
+  // (the OpenMP team persists across batches: a std::thread per part per batch cost ~30 us each)
+#pragma omp parallel for num_threads(T) schedule(static) if (T > 1)
+  for (int t = 0; t < T; ++t) work(t);
   for (char x : bad)
     if (x) throw std::runtime_error("binary CSR cache holds a feature id outside [0, vocabulary_size)");
 }
