@@ -9,6 +9,8 @@
 #include <stdexcept>
 
 #include "bincsr.h"
+
+#include <functional>
 #include "mapped_file.h"
 
 namespace fm {
@@ -112,13 +114,47 @@ void emit_rows(const std::vector<BinItem>& its, const BinSet& bs, LoadedBatch& b
   b.has_vals = vals;
 }
 
+// Places of a kind-1 batch's arrays in one consumer-pinned buffer (256-byte aligned sections).
+struct PinLayout {
+  size_t labels, offsets, ids, vals, weights, total;
+};
+PinLayout pin_layout(size_t n, size_t nnz, bool vals, bool weights) {
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  PinLayout L{};
+  size_t o = 0;
+  L.labels = o; o += al(4 * n);
+  L.offsets = o; o += al(4 * (n + 1));
+  L.ids = o; o += al(4 * nnz);
+  L.vals = o; o += vals ? al(4 * nnz) : 0;
+  L.weights = o; o += weights ? al(4 * n) : 0;
+  L.total = o;
+  return L;
+}
+
+using PinAcquire = std::function<void*(size_t bytes, int32_t* tag)>;
+
+// Point a batch's x_* arrays into a pinned buffer laid out by pin_layout.
+void pin_batch(LoadedBatch& b, void* buf, int32_t tag, const PinLayout& L, size_t n, size_t nnz, bool vals,
+               bool weights) {
+  uint8_t* p = static_cast<uint8_t*>(buf);
+  b.pinned = tag;
+  b.x_labels = reinterpret_cast<float*>(p + L.labels);
+  b.x_offsets = reinterpret_cast<int32_t*>(p + L.offsets);
+  b.x_ids = reinterpret_cast<int32_t*>(p + L.ids);
+  b.x_vals = vals ? reinterpret_cast<float*>(p + L.vals) : nullptr;
+  b.x_weights = weights ? reinterpret_cast<float*>(p + L.weights) : nullptr;
+  b.x_n = static_cast<int64_t>(n);
+  b.x_nnz = static_cast<int64_t>(nnz);
+}
+
 // Copy n chosen binary examples into a CSR batch (offsets, ids, values, labels, weights)
-// with up to `threads` threads; ids are range-checked on the way (a corrupt cache must
-// not reach the device kernels as an out-of-bounds row).
+// with up to `threads` threads -- into a consumer's pinned buffer when `pin` yields one (the
+// host-to-device copy then needs no staging copy), else into the batch's vectors; ids are
+// range-checked on the way (a corrupt cache must not reach the device kernels as an
+// out-of-bounds row).
 void assemble_binary(const std::vector<BinItem>& its, const BinSet& bs, bool weighted, int64_t vocab, int threads,
-                     LoadedBatch& b) {
+                     LoadedBatch& b, const PinAcquire& pin) {
   const size_t n = its.size();
-  b.labels.resize(n);
   b.offsets.resize(n + 1);
   b.offsets[0] = 0;
   bool any_vals = false;
@@ -129,20 +165,38 @@ void assemble_binary(const std::vector<BinItem>& its, const BinSet& bs, bool wei
     mf = std::max(mf, c);
     any_vals |= bs.files[its[i].file]->vals != nullptr;
   }
-  if (weighted) b.weights.resize(n);
   b.max_feats = mf;
   const size_t nnz = static_cast<size_t>(b.offsets[n]);
-  b.ids.resize(nnz);
-  if (any_vals) b.vals.resize(nnz);
-  // >= 256k ids per thread; pointers hoisted so the copies are plain memcpy (no aliasing
+  int32_t* ids_out;
+  float *vals_out, *lab_out, *w_out;
+  const int32_t* offs;
+  const PinLayout PL = pin_layout(n, nnz, any_vals, weighted);
+  int32_t tag = -1;
+  void* buf = pin ? pin(PL.total, &tag) : nullptr;
+  if (buf) {
+    pin_batch(b, buf, tag, PL, n, nnz, any_vals, weighted);
+    std::memcpy(b.x_offsets, b.offsets.data(), 4 * (n + 1));
+    b.offsets.clear();
+    ids_out = b.x_ids;
+    vals_out = b.x_vals;
+    lab_out = b.x_labels;
+    w_out = b.x_weights;
+    offs = b.x_offsets;
+  } else {
+    b.labels.resize(n);
+    if (weighted) b.weights.resize(n);
+    b.ids.resize(nnz);
+    if (any_vals) b.vals.resize(nnz);
+    ids_out = b.ids.data();
+    vals_out = any_vals ? b.vals.data() : nullptr;
+    lab_out = b.labels.data();
+    w_out = weighted ? b.weights.data() : nullptr;
+    offs = b.offsets.data();
+  }
+  // >= 64k ids per thread; pointers hoisted so the copies are plain memcpy (no aliasing
   // through `b`), the range check runs over the thread's contiguous output afterwards
-  const int T = std::max(1, std::min<int>(threads, static_cast<int>(nnz >> 18)));
+  const int T = std::max(1, std::min<int>(threads, static_cast<int>(nnz >> 16)));
   std::vector<char> bad(static_cast<size_t>(T), 0);
-  int32_t* const ids_out = b.ids.data();
-  float* const vals_out = any_vals ? b.vals.data() : nullptr;
-  float* const lab_out = b.labels.data();
-  float* const w_out = weighted ? b.weights.data() : nullptr;
-  const int32_t* const offs = b.offsets.data();
   const BinItem* const items = its.data();
   const BinFile* const* const files = reinterpret_cast<const BinFile* const*>(bs.files.data());
   const int64_t* const base = bs.base.data();
@@ -198,6 +252,7 @@ int api_next(void* h, FmRawView* v, char* err, int errlen) {
     v->ids = nullptr;
     v->vals = nullptr;
     v->nnz = 0;
+    v->pinned = b->pinned;
     if (b->slot >= 0) {
       const RawSlot& rs = L->options().raw_slots[static_cast<size_t>(b->slot)];
       v->bytes = rs.bytes;
@@ -211,6 +266,18 @@ int api_next(void* h, FmRawView* v, char* err, int errlen) {
       v->nbytes = static_cast<int64_t>(b->bytes.size());
       v->nlines = static_cast<int64_t>(b->line_start.size()) - 1;
       v->weights = b->weights.empty() ? nullptr : b->weights.data();
+    } else if (b->pinned >= 0) {  // parsed / binary CSR in the consumer's pinned buffer
+      v->kind = 1;
+      v->bytes = nullptr;
+      v->line_start = nullptr;
+      v->nbytes = 0;
+      v->nlines = b->x_n;
+      v->labels = b->x_labels;
+      v->offsets = b->x_offsets;
+      v->ids = b->x_ids;
+      v->vals = b->x_vals;
+      v->nnz = b->x_nnz;
+      v->weights = b->x_weights;
     } else if (b->rows.empty() && !b->offsets.empty()) {  // parsed / binary CSR
       v->kind = 1;
       v->bytes = nullptr;
@@ -326,6 +393,7 @@ TextLoader::TextLoader(LoaderOptions o) : o_(std::move(o)) {
   api_.done = &api_done;
   api_.parse = &TextLoader::api_parse;
   api_.stop = &TextLoader::api_stop;
+  api_.set_pinned_pool = &TextLoader::api_set_pinned_pool;
   if (o_.batch_size < 1) throw std::invalid_argument("batch_size must be >= 1");
   if (!o_.weight_files.empty() && o_.weight_files.size() != o_.files.size())
     throw std::invalid_argument("The numbers of train files and weight files do not match.");
@@ -484,6 +552,7 @@ void TextLoader::run() {
       elines.reserve(2 * nf);                         // (no reallocation: references stay valid)
       std::vector<const Span*> ftab, wtab;            // per file visit: its line / weight spans
 
+      const PinAcquire pin_acquire = [this](size_t bytes, int32_t* tag) { return acquire_pinned(bytes, tag); };
       // Draw n items from the window (random when shuffling, FIFO otherwise) and build the
       // batch unless it is skipped (resume).
       auto emit = [&](size_t n) -> bool {
@@ -497,9 +566,12 @@ void TextLoader::run() {
           if (o_.rows) {
             emit_rows(bchosen, bs, b);
           } else {
-            reuse(b.labels); reuse(b.offsets); reuse(b.ids); reuse(b.vals);
-            if (weighted) reuse(b.weights);
-            assemble_binary(bchosen, bs, weighted, o_.vocab_size, o_.threads, b);
+            reuse(b.offsets);
+            if (!pinned_pool_.load(std::memory_order_acquire)) {
+              reuse(b.labels); reuse(b.ids); reuse(b.vals);
+              if (weighted) reuse(b.weights);
+            }
+            assemble_binary(bchosen, bs, weighted, o_.vocab_size, o_.threads, b, pin_acquire);
           }
           b.epoch = epoch;
           b.count = count;
@@ -614,12 +686,40 @@ void TextLoader::run() {
           ptrs[i] = rl[i].p;
           lens[i] = rl[i].len;
         }
-        reuse(csr.labels); reuse(csr.offsets); reuse(csr.ids); reuse(csr.vals);
+        const bool pool = pinned_pool_.load(std::memory_order_acquire) != nullptr;
+        if (!pool) {
+          reuse(csr.labels); reuse(csr.offsets); reuse(csr.ids); reuse(csr.vals);
+        }
+        // with a consumer pool the parser's pieces go straight into a pinned buffer (values and
+        // weights sections reserved; the values are dropped from the view when all are 1)
+        void* pbuf = nullptr;
+        int32_t ptag = -1;
+        PinLayout PL{};
+        if (pool) {
+          csr.ext = [&](size_t nn, size_t nz, float** l, int32_t** o, int32_t** ii, float** vv) {
+            PL = pin_layout(nn, nz, true, weighted);
+            pbuf = pin_acquire(PL.total, &ptag);
+            if (!pbuf) return false;
+            uint8_t* q = static_cast<uint8_t*>(pbuf);
+            *l = reinterpret_cast<float*>(q + PL.labels);
+            *o = reinterpret_cast<int32_t*>(q + PL.offsets);
+            *ii = reinterpret_cast<int32_t*>(q + PL.ids);
+            *vv = reinterpret_cast<float*>(q + PL.vals);
+            return true;
+          };
+        }
         parse_lines32(ptrs.data(), lens.data(), n, o_.vocab_size, o_.hash_feature_id, o_.threads, csr, &pws);
-        b.labels = std::move(csr.labels);
-        b.offsets = std::move(csr.offsets);
-        b.ids = std::move(csr.ids);
-        if (csr.has_vals) b.vals = std::move(csr.vals);
+        float* wdst = nullptr;
+        if (csr.in_ext) {
+          const size_t nz = static_cast<size_t>(reinterpret_cast<int32_t*>(static_cast<uint8_t*>(pbuf) + PL.offsets)[n]);
+          pin_batch(b, pbuf, ptag, PL, n, nz, csr.has_vals, weighted);
+          wdst = b.x_weights;
+        } else {
+          b.labels = std::move(csr.labels);
+          b.offsets = std::move(csr.offsets);
+          b.ids = std::move(csr.ids);
+          if (csr.has_vals) b.vals = std::move(csr.vals);
+        }
         b.max_feats = csr.max_feats;
         if (weighted) {
           wptrs.resize(n); wlens.resize(n);
@@ -627,9 +727,12 @@ void TextLoader::run() {
             wptrs[i] = rw[i].p;
             wlens[i] = rw[i].len;
           }
-          reuse(b.weights);
-          b.weights.resize(n);
-          parse_floats(wptrs.data(), wlens.data(), n, b.weights.data(), o_.threads);
+          if (!wdst) {
+            reuse(b.weights);
+            b.weights.resize(n);
+            wdst = b.weights.data();
+          }
+          parse_floats(wptrs.data(), wlens.data(), n, wdst, o_.threads);
         }
         b.epoch = epoch;
         b.count = count;

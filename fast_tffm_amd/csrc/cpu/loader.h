@@ -97,6 +97,15 @@ struct LoadedBatch {
   size_t nbytes = 0, nlines = 0;
   int epoch = 0;
   int64_t count = 0;              // batches of this epoch consumed after this one
+  // kind-1 batch in a consumer's page-locked buffer (FmPinnedPool, loader_api.h): its tag and the
+  // arrays' places there; labels / offsets / ids / vals / weights above stay empty
+  int pinned = -1;
+  float* x_labels = nullptr;
+  int32_t* x_offsets = nullptr;
+  int32_t* x_ids = nullptr;
+  float* x_vals = nullptr;         // null: every value is 1
+  float* x_weights = nullptr;
+  int64_t x_n = 0, x_nnz = 0;
 };
 
 class TextLoader {
@@ -130,6 +139,14 @@ class TextLoader {
 
  private:
   static int api_parse(void* h, const FmRawView* v, FmParsedOut* out, char* err, int errlen);
+  static void api_set_pinned_pool(void* h, const FmPinnedPool* pool) {
+    static_cast<TextLoader*>(h)->pinned_pool_.store(pool, std::memory_order_release);
+  }
+  // A pinned output buffer of >= bytes from the consumer's pool (its tag in *tag), or null.
+  void* acquire_pinned(size_t bytes, int32_t* tag) {
+    const FmPinnedPool* p = pinned_pool_.load(std::memory_order_acquire);
+    return p ? p->acquire(p->ctx, bytes, tag) : nullptr;
+  }
   static void api_stop(void* h) { static_cast<TextLoader*>(h)->close(); }
 
   void run();
@@ -149,6 +166,7 @@ class TextLoader {
   std::string error_;
   std::atomic<float> fill_{0.f};
   FmLoaderApi api_{};
+  std::atomic<const FmPinnedPool*> pinned_pool_{nullptr};
   Csr32Workspace api_ws_;     // CPU parses requested through api_ (one consumer thread)
   std::mutex pool_mu_;
   std::vector<uvector<int32_t>> pool_i32_;

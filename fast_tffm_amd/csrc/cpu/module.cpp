@@ -245,6 +245,8 @@ PYBIND11_MODULE(_fm_cpu, m) {
                ok = L.next(b);
              }
              if (!ok) return py::none();
+             if (b.pinned >= 0)  // (a native consumer's pinned pool is set: that consumer reads the batches)
+               throw std::runtime_error("TextLoader.next: the loader feeds a native consumer's pinned buffers");
              if (!b.rows.empty()) {  // rows mode: (rows, offsets, has_vals, max_feats, epoch, count)
                return py::make_tuple(to_numpy(std::move(b.rows)), to_numpy(std::move(b.offsets)), b.has_vals,
                                      b.max_feats, b.epoch, b.count);

@@ -111,7 +111,7 @@ bool parse_line_fast(const char* s, size_t len, int64_t vocab_size, bool hash_fe
   float label;
   if (!fast_parse_decimal(p, lim, &e, &label)) return false;
   p = e;
-  const size_t mark = ids.size();
+  const size_t mark = ids.size(), vmark = vals.size();  // (vals may be a line's own buffer)
   int32_t cnt = 0;
   while (p < lim) {
     if (*p != ' ') goto general;
@@ -170,7 +170,7 @@ bool parse_line_fast(const char* s, size_t len, int64_t vocab_size, bool hash_fe
   return true;
 general:
   ids.resize(mark);
-  vals.resize(mark);
+  vals.resize(vmark);
   return false;
 }
 
@@ -337,13 +337,20 @@ void parse_lines(const char* const* ptrs, const size_t* lens, size_t n, int64_t 
 
 void parse_lines32(const char* const* ptrs, const size_t* lens, size_t n, int64_t vocab_size, bool hash_feature_id,
                    int threads, Csr32& out, Csr32Workspace* ws) {
-  out.labels.resize(n);
-  out.offsets.assign(n + 1, 0);
   out.ids.clear();
   out.vals.clear();
   out.max_feats = 0;
   out.has_vals = false;
-  if (n == 0) return;
+  out.in_ext = false;
+  if (n == 0) {
+    out.labels.clear();
+    out.offsets.assign(1, 0);
+    return;
+  }
+  float* L = nullptr;    // destinations: the external buffer or the vectors (chosen once nnz is known)
+  int32_t* O = nullptr;
+  int32_t* I = nullptr;
+  float* Vd = nullptr;
   Csr32Workspace local;
   if (!ws) ws = &local;
   const int T = static_cast<int>(std::max<size_t>(1, std::min<size_t>(std::max(threads, 1), n / 512)));
@@ -352,7 +359,7 @@ void parse_lines32(const char* const* ptrs, const size_t* lens, size_t n, int64_
   std::vector<size_t> err_line(T, SIZE_MAX);
   std::vector<size_t> nz_off(T + 1, 0);
   std::vector<int> mf(T, 0);
-  std::vector<char> nonunit(T, 0);
+  bool any_vals = false;  // some value is not 1 (set once all parts are parsed)
   int nt_used = T;
   // phase 1: each thread parses a contiguous line range into its own part; phase 2 (after the
   // barrier and a serial prefix over the parts): each copies its part into place, building the
@@ -365,10 +372,11 @@ void parse_lines32(const char* const* ptrs, const size_t* lens, size_t n, int64_
     const size_t b = n * t / nt, e = n * (t + 1) / nt;
     Csr32Workspace::Part& o = ws->parts[t];
     o.labels.clear(); o.sizes.clear(); o.ids.clear(); o.vals.clear();
+    o.unit = true;
     o.labels.reserve(e - b); o.sizes.reserve(e - b);
     size_t bytes = 0;
     for (size_t i = b; i < e; ++i) bytes += lens[i];
-    o.ids.reserve(bytes / 4 + 16); o.vals.reserve(bytes / 4 + 16);
+    o.ids.reserve(bytes / 4 + 16);
     std::string scratch;
     for (size_t i = b; i < e; ++i) {
       if (i + 6 < e) {  // lines are scattered over the mapped files: fetch a few ahead
@@ -376,7 +384,21 @@ void parse_lines32(const char* const* ptrs, const size_t* lens, size_t n, int64_
         for (size_t k = 0; k < lens[i + 6]; k += 64) __builtin_prefetch(q + k);
       }
       try {
-        parse_line_into(ptrs[i], lens[i], vocab_size, hash_feature_id, o.labels, o.sizes, o.ids, o.vals, scratch);
+        // the line's values into a small buffer: the part keeps no values while all of them are 1
+        // (binary features), so the common batch writes and copies no value array at all
+        const size_t mark = o.ids.size();
+        o.line_vals.clear();
+        parse_line_into(ptrs[i], lens[i], vocab_size, hash_feature_id, o.labels, o.sizes, o.ids, o.line_vals,
+                        scratch);
+        if (o.unit) {
+          bool all1 = true;
+          for (float v : o.line_vals) all1 &= v == 1.f;
+          if (!all1) {
+            o.vals.assign(mark, 1.f);
+            o.unit = false;
+          }
+        }
+        if (!o.unit) o.vals.insert(o.vals.end(), o.line_vals.begin(), o.line_vals.end());
       } catch (const ParseError& ex) {
         errors[t] = ex.what();
         err_line[t] = i;
@@ -390,35 +412,47 @@ void parse_lines32(const char* const* ptrs, const size_t* lens, size_t n, int64_
       for (int k = 0; k < nt; ++k) nz_off[k + 1] += nz_off[k];
       bool failed = false;
       for (int k = 0; k < nt; ++k) failed |= err_line[k] != SIZE_MAX;
+      for (int k = 0; k < nt; ++k) any_vals |= !ws->parts[k].unit;
       if (!failed) {
-        out.ids.resize(nz_off[nt]);
-        out.vals.resize(nz_off[nt]);
+        if (out.ext && out.ext(n, nz_off[nt], &L, &O, &I, &Vd)) {
+          out.in_ext = true;
+        } else {
+          out.labels.resize(n);
+          out.offsets.resize(n + 1);
+          out.ids.resize(nz_off[nt]);
+          if (any_vals) out.vals.resize(nz_off[nt]);
+          L = out.labels.data();
+          O = out.offsets.data();
+          I = out.ids.data();
+          Vd = out.vals.data();
+        }
+        O[0] = 0;
       }
     }
-    if (out.ids.size() == nz_off[nt] && err_line[t] == SIZE_MAX) {
-      std::copy(o.labels.begin(), o.labels.end(), out.labels.begin() + b);
-      std::copy(o.ids.begin(), o.ids.end(), out.ids.begin() + nz_off[t]);
-      std::copy(o.vals.begin(), o.vals.end(), out.vals.begin() + nz_off[t]);
+    if (O != nullptr && err_line[t] == SIZE_MAX) {
+      std::copy(o.labels.begin(), o.labels.end(), L + b);
+      std::copy(o.ids.begin(), o.ids.end(), I + nz_off[t]);
+      if (any_vals) {  // (some value is not 1: every part's values, the unit parts' as 1s)
+        if (o.unit)
+          std::fill(Vd + nz_off[t], Vd + nz_off[t + 1], 1.f);
+        else
+          std::copy(o.vals.begin(), o.vals.end(), Vd + nz_off[t]);
+      }
       int32_t off = static_cast<int32_t>(nz_off[t]), m = 0;
       for (size_t i = b; i < e; ++i) {
         const int32_t c = o.sizes[i - b];
         off += c;
-        out.offsets[i + 1] = off;
+        O[i + 1] = off;
         m = std::max(m, c);
       }
       mf[t] = m;
-      bool nu = false;
-      for (float v : o.vals) nu |= v != 1.f;
-      nonunit[t] = nu;
     }
   }
   // the first failing line in input order (same as a sequential parse)
   for (int t = 0; t < nt_used; ++t)
     if (err_line[t] != SIZE_MAX) throw ParseError(errors[t]);
-  for (int t = 0; t < nt_used; ++t) {
-    out.max_feats = std::max(out.max_feats, mf[t]);
-    out.has_vals |= nonunit[t] != 0;
-  }
+  for (int t = 0; t < nt_used; ++t) out.max_feats = std::max(out.max_feats, mf[t]);
+  out.has_vals = any_vals;
   if (!out.has_vals) out.vals.clear();
 }
 

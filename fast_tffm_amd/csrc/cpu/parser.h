@@ -23,6 +23,7 @@
 #include <string>
 #include <type_traits>
 #include <utility>
+#include <functional>
 #include <vector>
 
 namespace fm {
@@ -89,6 +90,11 @@ struct Csr32 {
   uvector<float> vals;
   int max_feats = 0;
   bool has_vals = false;
+  // External destination (optional): called once the batch's nnz is known; when it returns true
+  // the arrays are written to *labels [n], *offsets [n + 1], *ids / *vals [nnz] instead of the
+  // vectors above (which stay empty), e.g. a consumer's page-locked buffer (loader_api.h).
+  std::function<bool(size_t n, size_t nnz, float** labels, int32_t** offsets, int32_t** ids, float** vals)> ext;
+  bool in_ext = false;  // out: the arrays went to the external destination
 };
 
 struct Csr32Workspace {
@@ -96,7 +102,9 @@ struct Csr32Workspace {
     std::vector<float> labels;
     std::vector<int32_t> sizes;
     std::vector<int32_t> ids;
-    std::vector<float> vals;
+    std::vector<float> vals;   // empty while every value so far is 1 (unit)
+    std::vector<float> line_vals;
+    bool unit = true;
   };
   std::vector<Part> parts;
 };

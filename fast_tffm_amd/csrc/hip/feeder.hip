@@ -25,6 +25,8 @@
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -63,6 +65,64 @@ struct FeederBatch {
   int64_t count = 0;
 };
 
+// A few persistent host threads for the staging copies (a std::thread per part per batch cost
+// ~50 us of creation each on the feeder's critical path)
+class CopyPool {
+ public:
+  explicit CopyPool(int n) : nth_(n < 1 ? 1 : n) {
+    for (int i = 1; i < nth_; ++i) th_.emplace_back([this, i] { loop(i); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int size() const { return nth_; }
+  // f(t) for t in [0, size()): t = 0 on the caller, the rest on the pool; returns when all are done
+  void run(const std::function<void(int)>& f) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = &f;
+      ++gen_;
+      pending_ = nth_ - 1;
+    }
+    cv_.notify_all();
+    f(0);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [&] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void loop(int i) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)>* f;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        f = job_;
+      }
+      (*f)(i);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  int nth_;
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)>* job_ = nullptr;
+  uint64_t gen_ = 0;
+  int pending_ = 0;
+  bool stop_ = false;
+};
+
 class GpuTextFeeder {
  public:
   GpuTextFeeder(const FmLoaderApi* api, int device, long long vocab, bool hash)
@@ -89,6 +149,11 @@ class GpuTextFeeder {
   void start() {
     std::lock_guard<std::mutex> lk(mu_);
     if (th_.joinable() || closed_) return;
+    // host-parsed / binary-cache batches are assembled straight into this feeder's page-locked
+    // buffers (no staging copy on the feeder thread)
+    pool_api_.ctx = this;
+    pool_api_.acquire = &GpuTextFeeder::pin_acquire_cb;
+    api_->set_pinned_pool(api_->handle, &pool_api_);
     th_ = std::thread([this] { run(); });
   }
 
@@ -161,7 +226,14 @@ class GpuTextFeeder {
     }
     cv_slot_.notify_all();
     cv_ready_.notify_all();
-    // the thread may be blocked in the loader's next(): stop the loader first
+    {  // a loader thread waiting for a pinned buffer gets none (it falls back to its own memory)
+      std::lock_guard<std::mutex> lk(pmu_);
+      pclosed_ = true;
+    }
+    pcv_.notify_all();
+    api_->set_pinned_pool(api_->handle, nullptr);
+    // the thread may be blocked in the loader's next(): stop the loader first (joins its thread:
+    // nothing writes the pinned buffers after this)
     api_->stop(api_->handle);
     if (th_.joinable()) th_.join();
     if (st_) {
@@ -176,6 +248,9 @@ class GpuTextFeeder {
       pin_ev_[i] = nullptr;
       pin_cap_[i] = 0;
     }
+    for (PinBuf& pb : pbufs_)
+      if (pb.p) (void)hipHostFree(pb.p);
+    pbufs_.clear();
     for (FeederSlot& s : slots_) {
       if (s.ready) (void)hipEventDestroy(s.ready);
       if (s.freed) (void)hipEventDestroy(s.freed);
@@ -251,11 +326,72 @@ class GpuTextFeeder {
     if (!pend_on_) return;
     pend_on_ = false;
     hip_ok(hipEventSynchronize(pin_ev_[pend_buf_]), "hipEventSynchronize");
+    if (pin_tag_[pend_buf_] >= 0) {  // its arrays were copied from a pool buffer: free it for the loader
+      pin_release(pin_tag_[pend_buf_]);
+      pin_tag_[pend_buf_] = -1;
+    }
     publish(pend_b_);
   }
 
-  // dst + offs[k] <- srcs[k] (bytes[k]) for the k with bytes: large arrays split over a few threads
-  static void parallel_copy(uint8_t* dst, const size_t* offs, const void* const* srcs, const size_t* bytes, int n) {
+  // --- pinned output pool offered to the loader (loader_api.h FmPinnedPool) ---
+  struct PinBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    bool busy = false;
+  };
+  static constexpr int kPinPoolMax = 16;  // (>= the loader's queue + the batch being built + 2 in flight)
+  static void* pin_acquire_cb(void* ctx, size_t bytes, int32_t* tag) {
+    return static_cast<GpuTextFeeder*>(ctx)->pin_acquire(bytes, tag);
+  }
+  void* pin_acquire(size_t bytes, int32_t* tag) {
+    std::unique_lock<std::mutex> lk(pmu_);
+    for (;;) {
+      if (pclosed_) return nullptr;
+      int fit = -1, small = -1;
+      for (size_t i = 0; i < pbufs_.size(); ++i) {
+        if (pbufs_[i].busy) continue;
+        if (pbufs_[i].cap >= bytes) {
+          if (fit < 0 || pbufs_[i].cap < pbufs_[fit].cap) fit = static_cast<int>(i);
+        } else if (small < 0) {
+          small = static_cast<int>(i);
+        }
+      }
+      if (fit < 0 && (small >= 0 || static_cast<int>(pbufs_.size()) < kPinPoolMax)) {
+        if (small < 0) {
+          pbufs_.emplace_back();
+          small = static_cast<int>(pbufs_.size()) - 1;
+        }
+        PinBuf& pb = pbufs_[small];
+        (void)hipSetDevice(device_);
+        if (pb.p) (void)hipHostFree(pb.p);
+        pb.p = nullptr;
+        pb.cap = 0;
+        const size_t cap = bytes + bytes / 8 + 4096;  // (room for a somewhat denser batch)
+        if (hipHostMalloc(&pb.p, cap, hipHostMallocDefault) != hipSuccess) {
+          pb.p = nullptr;
+          return nullptr;  // (no page-locked memory: the loader uses its own)
+        }
+        pb.cap = cap;
+        fit = small;
+      }
+      if (fit >= 0) {
+        pbufs_[fit].busy = true;
+        *tag = fit;
+        return pbufs_[fit].p;
+      }
+      pcv_.wait_for(lk, std::chrono::milliseconds(100));
+    }
+  }
+  void pin_release(int tag) {
+    {
+      std::lock_guard<std::mutex> lk(pmu_);
+      if (tag >= 0 && tag < static_cast<int>(pbufs_.size())) pbufs_[tag].busy = false;
+    }
+    pcv_.notify_one();
+  }
+
+  // dst + offs[k] <- srcs[k] (bytes[k]) for the k with bytes: large arrays split over the copy pool
+  void parallel_copy(uint8_t* dst, const size_t* offs, const void* const* srcs, const size_t* bytes, int n) {
     constexpr size_t kChunk = 1 << 20;
     constexpr int kThreads = 8;
     struct Piece { uint8_t* d; const uint8_t* s; size_t b; };
@@ -263,18 +399,15 @@ class GpuTextFeeder {
     for (int k = 0; k < n; ++k)
       for (size_t o = 0; o < bytes[k]; o += kChunk)
         pieces.push_back({dst + offs[k] + o, static_cast<const uint8_t*>(srcs[k]) + o, std::min(kChunk, bytes[k] - o)});
-    const int T = static_cast<int>(std::min<size_t>(kThreads, pieces.size()));
-    auto work = [&](int t) {
-      for (size_t i = t; i < pieces.size(); i += T) std::memcpy(pieces[i].d, pieces[i].s, pieces[i].b);
-    };
-    if (T <= 1) {
-      if (T == 1) work(0);
+    if (pieces.size() <= 1) {
+      for (const Piece& p : pieces) std::memcpy(p.d, p.s, p.b);
       return;
     }
-    std::vector<std::thread> ths;
-    for (int t = 1; t < T; ++t) ths.emplace_back(work, t);
-    work(0);
-    for (auto& th : ths) th.join();
+    if (!copy_pool_) copy_pool_ = std::make_unique<CopyPool>(kThreads);
+    const int T = copy_pool_->size();
+    copy_pool_->run([&](int t) {
+      for (size_t i = t; i < pieces.size(); i += T) std::memcpy(pieces[i].d, pieces[i].s, pieces[i].b);
+    });
   }
 
   void fail(const std::string& msg, bool parse) {
@@ -385,11 +518,20 @@ class GpuTextFeeder {
             }
             // two staging buffers: batch k's gather overlaps batch k-1's DMA, which is waited for (and
             // k-1 published) only after k's copies are queued
-            uint8_t* pin = staging(pin_cur_, total);  // (its previous DMA completed: flushed a batch ago)
-            parallel_copy(pin, offs, srcs, parts, 5);
-            hip_ok(hipStreamWaitEvent(st_, s.freed, 0), "hipStreamWaitEvent");
-            for (int k = 0; k < 5; ++k)
-              if (parts[k]) hip_ok(hipMemcpyAsync(dsts[k], pin + offs[k], parts[k], hipMemcpyHostToDevice, st_), "H2D");
+            if (!pin_ev_[pin_cur_])
+              hip_ok(hipEventCreateWithFlags(&pin_ev_[pin_cur_], hipEventDisableTiming), "hipEventCreate");
+            if (v.pinned >= 0) {  // assembled in one of this feeder's page-locked buffers: copy it directly
+              hip_ok(hipStreamWaitEvent(st_, s.freed, 0), "hipStreamWaitEvent");
+              for (int k = 0; k < 5; ++k)
+                if (parts[k]) hip_ok(hipMemcpyAsync(dsts[k], srcs[k], parts[k], hipMemcpyHostToDevice, st_), "H2D");
+              pin_tag_[pin_cur_] = v.pinned;  // (back to the pool once this copy has been waited for)
+            } else {
+              uint8_t* pin = staging(pin_cur_, total);  // (its previous DMA completed: flushed a batch ago)
+              parallel_copy(pin, offs, srcs, parts, 5);
+              hip_ok(hipStreamWaitEvent(st_, s.freed, 0), "hipStreamWaitEvent");
+              for (int k = 0; k < 5; ++k)
+                if (parts[k]) hip_ok(hipMemcpyAsync(dsts[k], pin + offs[k], parts[k], hipMemcpyHostToDevice, st_), "H2D");
+            }
             hip_ok(hipEventRecord(pin_ev_[pin_cur_], st_), "hipEventRecord");
             deferred = true;
             b.nnz = v.nnz;
@@ -473,6 +615,7 @@ class GpuTextFeeder {
   std::mutex mu_;
   std::condition_variable cv_slot_, cv_ready_;
   std::thread th_;
+  std::unique_ptr<CopyPool> copy_pool_;  // (the feeder thread's staging copies)
   bool stop_ = false, closed_ = false, done_ = false, starving_ = false;
   bool failed_ = false, parse_error_ = false;
   std::string error_;
@@ -486,6 +629,12 @@ class GpuTextFeeder {
   size_t pin_cap_[2] = {0, 0};
   hipEvent_t pin_ev_[2] = {nullptr, nullptr};
   int pin_cur_ = 0;
+  int pin_tag_[2] = {-1, -1};     // pool buffer whose copies pin_ev_[i] marks (-1: staging)
+  std::vector<PinBuf> pbufs_;     // (guarded by pmu_)
+  std::mutex pmu_;
+  std::condition_variable pcv_;
+  bool pclosed_ = false;
+  FmPinnedPool pool_api_{};
   bool pend_on_ = false;
   int pend_buf_ = 0;
   FeederBatch pend_b_;

@@ -8,6 +8,7 @@
 // The table lives inside the TextLoader and is valid until that loader is destroyed; the
 // Python side keeps the loader alive for as long as a feeder uses it.
 #pragma once
+#include <cstddef>
 #include <cstdint>
 
 extern "C" {
@@ -15,7 +16,10 @@ extern "C" {
 // One batch as the loader produced it, valid until handed back with FmLoaderApi::done:
 //  * kind 0 (raw mode, GPU tokenizer): '\n'-terminated lines, in page-locked memory when it came
 //    from one of the caller's slots (`slot` >= 0), else in a heap buffer owned by the loader;
-//  * kind 1 (parse mode): the CPU parser's int32 CSR in loader-owned (pageable) memory.
+//  * kind 1 (parse mode / binary caches): the CPU parser's or the cache's int32 CSR -- in a
+//    page-locked buffer of the consumer's pinned pool when one is set (`pinned` >= 0: the
+//    consumer copies it to the device directly and gives the buffer back to its pool once the
+//    copy is done), else in loader-owned pageable memory (`pinned` = -1).
 struct FmRawView {
   int32_t kind;
   int32_t slot;                 // host slot index, -1 for a heap batch
@@ -31,7 +35,17 @@ struct FmRawView {
   const int32_t* ids;           // kind 1: [nnz]
   const float* vals;            // kind 1: [nnz] or null (every value 1)
   int64_t nnz;                  // kind 1
+  int32_t pinned;               // kind 1: tag of the consumer's pinned buffer holding the arrays, or -1
   void* owner;                  // loader-private (the batch)
+};
+
+// Page-locked output buffers a consumer offers for kind-1 batches (set_pinned_pool): the loader
+// assembles a batch's CSR arrays straight into one, so the consumer's host-to-device copy needs
+// no staging copy.  acquire blocks until a buffer of >= bytes is free and returns it with its
+// tag; null (consumer closing, or no buffer that large): the loader uses its own memory.
+struct FmPinnedPool {
+  void* ctx;
+  void* (*acquire)(void* ctx, size_t bytes, int32_t* tag);
 };
 
 // Host CSR written by FmLoaderApi::parse into caller-owned arrays.
@@ -59,8 +73,11 @@ struct FmLoaderApi {
   // stop the loader (a consumer blocked in next() returns 0): lets the consumer's own shutdown
   // join a thread that is waiting for the next batch
   void (*stop)(void* handle);
+  // offer (pool != null) or withdraw (null) pinned output buffers for kind-1 batches; the pool
+  // must outlive the loader's use of it (withdraw before destroying it)
+  void (*set_pinned_pool)(void* handle, const FmPinnedPool* pool);
 };
 
 }  // extern "C"
 
-constexpr int32_t kFmLoaderApiVersion = 2;
+constexpr int32_t kFmLoaderApiVersion = 3;

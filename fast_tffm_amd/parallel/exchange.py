@@ -1047,6 +1047,7 @@ class DPDenseExchange(DPExchange):
         self.wire16 = (torch.empty((V, self.gs), dtype=torch.bfloat16, device=self.dev)
                        if self.dev.type == "cuda" and model.cfg.comm_dtype == "bf16" else None)
         self.bounds = torch.zeros(self.P + 2, dtype=torch.int32, device=self.dev)
+        self.local_w1 = (self.W == 1 and self.dev.type == "cuda" and os.environ.get("FM_DP_W1_LOCAL", "1") != "0")
 
     def close(self) -> None:
         self.dense = self.wire16 = None
@@ -1121,6 +1122,14 @@ class DPDenseExchange(DPExchange):
 
         if self.dev.type != "cuda":
             return self._train_step_reference(b)
+        if self.local_w1:
+            # world 1: the replica is the whole table and this rank owns every row, so the step is the
+            # local step (fused backward + in-place update of the touched rows only) -- the dense
+            # buffer, its scan of all V rows by dense_apply (132 us of 0.72 ms at V = 1M) and the
+            # zeroing are for the exchange (profiles/r5/dp_dense_w1.txt; FM_DP_W1_LOCAL=0: dense path)
+            if next_batch is not None or self.m._lpending is not None:
+                return self.m._local_lookahead_step(b, next_batch, next2)
+            return self.m._local_train_step(b)
         m, ws, cfg, Kp = self.m, self.m.ws, self.m.cfg, self.Kp
         main = torch.cuda.current_stream(self.dev)
         nb_ready = None

@@ -42,10 +42,13 @@ def _cfg(mode, V):
 @pytest.mark.parametrize("mode", ["shard", "dp", "dp_dense"])
 @pytest.mark.parametrize("emit", [False, True])
 def test_rccl_world1_matches_local(rccl_ctx, mode, emit, monkeypatch):
-    if emit:  # the sharded step's N > 1 compute path (EMIT backward, exchange) run at world 1
-        if mode != "shard":
-            pytest.skip("EMIT at world 1 is a row-sharded executor path")
-        monkeypatch.setenv("FM_SHARD_W1_LOCAL", "0")
+    if emit:  # the N > 1 compute path run at world 1 instead of the world-1 local step
+        if mode == "shard":  # EMIT backward + exchange
+            monkeypatch.setenv("FM_SHARD_W1_LOCAL", "0")
+        elif mode == "dp_dense":  # dense gradient buffer + dense_apply
+            monkeypatch.setenv("FM_DP_W1_LOCAL", "0")
+        else:
+            pytest.skip("dp has no separate world-1 path")
     V = 50000
     gen = CriteoSynth(V, device="cuda", seed=21)
     batches = [gen.batch(2048) for _ in range(3)]

@@ -130,7 +130,10 @@ def test_shard_world1_depth2_early_rows_matches_local(production, rccl_ctx, monk
     dm.close()
 
 
-def test_dp_dense_lookahead_matches_local(production, rccl_ctx):
+@pytest.mark.parametrize("dense", [False, True])
+def test_dp_dense_lookahead_matches_local(production, rccl_ctx, dense, monkeypatch):
+    if dense:  # the dense-buffer path of N > 1 at world 1 (else the world-1 local step)
+        monkeypatch.setenv("FM_DP_W1_LOCAL", "0")
     V = 40000
     gen = CriteoSynth(V, device="cuda", seed=63)
     pool = [gen.batch(4096) for _ in range(POOL)]

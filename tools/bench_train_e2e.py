@@ -58,6 +58,8 @@ def main():
     ap.add_argument("--batch", type=int, default=50_000)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--dir", default="/tmp/fm_e2e")
+    ap.add_argument("--paths", default="false,true,fmb,fmb_hbm",
+                    help="comma list: false (CPU parser), true (GPU tokenizer), fmb, fmb_hbm")
     a = ap.parse_args()
     data = os.path.join(a.dir, "data")
     os.makedirs(data, exist_ok=True)
@@ -71,7 +73,10 @@ def main():
             if not os.path.exists(os.path.join(data, d)):
                 shutil.copy(s, os.path.join(data, d))
     text = dict(train=f"{data}/train_*", weights=f"weight_files = {data}/weight_*")
-    for gpu in ("false", "true", "fmb", "fmb_hbm"):
+    paths = a.paths.split(",")
+    if "fmb_hbm" in paths and "fmb" not in paths:
+        paths.insert(paths.index("fmb_hbm"), "fmb")  # (the caches are converted by the fmb run)
+    for gpu in paths:
         cfg = os.path.join(a.dir, f"e2e_{gpu}.cfg")
         fmb = gpu.startswith("fmb")
         src = text if not fmb else dict(train=f"{a.dir}/fmb/*.fmb", weights="")
@@ -99,6 +104,7 @@ def main():
         steps = len(re.findall(r"Global Step", r.stdout))
         name = {"fmb": "binary .fmb caches (host assembly)",
                 "fmb_hbm": "binary .fmb caches resident in HBM"}.get(gpu, f"gpu_parse={gpu}")
+        name += f" [{a.threads} threads]"
         steady = f"{float(ms.group(1)):.4g}" if ms else "n/a"
         print(f"{name}: Average speed {float(m.group(1)):.4g} ex/s, steady state (epochs 2+) {steady} ex/s "
               f"({a.files * a.lines * a.epochs} examples, wall {time.time() - t:.1f}s incl. start-up)", flush=True)

@@ -79,6 +79,20 @@ def shard_model(N: int, B: int, slots: int, Kp: int = 64):
                 grads=grads_b, patch=patch_b, total=total, critical=critical)
 
 
+def dp_touched(N: int, B: int, V: int = 1_000_000, blocks=(16, 256, 4096)):
+    """Union over the N ranks' batches of the touched rows of the replicated V-row table, and the share
+    of row blocks (of each size) holding at least one touched row: what exchanging only touched rows
+    / touched blocks could save."""
+    t = torch.zeros(V, dtype=torch.bool)
+    for r in range(N):
+        t[CriteoSynth(V, seed=1000 + r).batch(B).ids.to(torch.int64)] = True
+    out = {"rows": float(t.float().mean())}
+    for bs in blocks:
+        tt = torch.cat([t, torch.zeros((-V) % bs, dtype=torch.bool)])
+        out[bs] = float(tt.view(-1, bs).any(1).float().mean())
+    return out
+
+
 def dp_dense_model(N: int, V: int = 1_000_000, Kp: int = 64):
     buf = V * (Kp + 4) * 4
     rows = V * (Kp + 1) * 4
@@ -136,6 +150,27 @@ def main() -> int:
         pipe = (a.dp_fwd_ms + max(a.dp_bwd_ms, a.dp_bwd_ms / P + rs) + a.dp_apply_ms / max(N, 1) / P + ag)
         print(f"{N:>2} {d['reduce_scatter'] / mb:>8.1f} {d['all_gather'] / mb:>8.1f} {d['total'] / mb:>9.1f} "
               f"{d['allreduce_equiv'] / mb:>12.1f} {t:>9.3f} {serial:>9.3f} {pipe:>8.3f} {1.1 * max(comp, t):>10.3f}")
+    print()
+    print("dp_dense: touched rows (union over the ranks' batches) and touched row blocks -- the bytes an exchange of")
+    print("only touched blocks / rows would move (RS + AG scale with the exchanged share; row-granular exchange")
+    print("needs the per-rank counts on the host before the collectives: one host sync per step)")
+    print(f"{'N':>2} {'rows':>6} {'blk16':>6} {'blk256':>7} {'blk4096':>8} {'blocks MB':>10} {'rows MB':>8} "
+          f"{'rows pipe ms':>12} {'bf16-RS rows pipe ms':>20}")
+    for N in a.ranks:
+        d = dp_dense_model(N)
+        tch = dp_touched(N, a.batch)
+        bw = max(N - 1, 1) * a.link_gbs * 1e9
+        blk_b = d["total"] * tch[4096]
+        # row-granular: the touched rows' data + one int32 id per exchanged row
+        row_b = d["total"] * tch["rows"] + 2 * 4 * (N - 1) * 1_000_000 * tch["rows"] / max(N, 1)
+        P = a.dp_blocks if N > 1 else 1
+        def pipe(rs_b, ag_b):
+            rs, ag = rs_b / bw * 1e3, ag_b / bw * 1e3
+            return a.dp_fwd_ms + max(a.dp_bwd_ms, a.dp_bwd_ms / P + rs) + a.dp_apply_ms / max(N, 1) / P + ag
+        rs_rows = d["reduce_scatter"] * tch["rows"]
+        ag_rows = d["all_gather"] * tch["rows"]
+        print(f"{N:>2} {tch['rows']:>6.3f} {tch[16]:>6.3f} {tch[256]:>7.3f} {tch[4096]:>8.3f} {blk_b / mb:>10.1f} "
+              f"{row_b / mb:>8.1f} {pipe(rs_rows, ag_rows):>12.3f} {pipe(rs_rows / 2, ag_rows):>20.3f}")
     return 0
 
 
