@@ -44,7 +44,7 @@ train_files = {train}
 parse_threads = {threads}
 gpu_parse = {gpu}
 device_cache = {dcache}
-log_steps = 1000000
+log_steps = 40
 [Predict]
 predict_files =
 """
@@ -106,6 +106,9 @@ def main():
                 "fmb_hbm": "binary .fmb caches resident in HBM"}.get(gpu, f"gpu_parse={gpu}")
         name += f" [{a.threads} threads]"
         steady = f"{float(ms.group(1)):.4g}" if ms else "n/a"
+        losses = re.findall(r"Global Step: (\d+); Avg loss: ([0-9.eE+-]+);", r.stdout)
+        if losses:  # (the same shuffle and seed on every path: the same batches, the same loss)
+            name += f" last loss {losses[-1][1]} (step {losses[-1][0]})"
         print(f"{name}: Average speed {float(m.group(1)):.4g} ex/s, steady state (epochs 2+) {steady} ex/s "
               f"({a.files * a.lines * a.epochs} examples, wall {time.time() - t:.1f}s incl. start-up)", flush=True)
 

@@ -12,5 +12,6 @@ timeout -k 10 300 python -u tools/bench_loader.py --threads 16 --epochs 5 > $OUT
 cat $OUT/loader.txt
 timeout -k 10 300 python -u tools/bench_gpu_parse_stages.py --threads 16 > $OUT/stages.txt 2>&1 || { tail -20 $OUT/stages.txt; exit 1; }
 cat $OUT/stages.txt
-timeout -k 10 600 python -u tools/bench_train_e2e.py --lines 250000 --files 4 --epochs 8 > $OUT/e2e.txt 2>&1 || { tail -20 $OUT/e2e.txt; exit 1; }
+# (8 parse threads: one per physical core of the box's 16-CPU share -- the sweep in profiles/r5/e2e.txt)
+timeout -k 10 600 python -u tools/bench_train_e2e.py --lines 250000 --files 4 --epochs 8 --threads 8 > $OUT/e2e.txt 2>&1 || { tail -20 $OUT/e2e.txt; exit 1; }
 cat $OUT/e2e.txt
