@@ -241,9 +241,10 @@ def fm_forward(offsets: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor | N
     if lt and dpred is None:
         dpred = torch.empty(B, dtype=torch.float32, device=dev)
     dt = dtype_code(v.dtype)
-    if _DEBUG and max_feats is not None and max_feats >= 0 and B > 0:
+    host_checks = _DEBUG and not (offsets.is_cuda and torch.cuda.is_current_stream_capturing())
+    if host_checks and max_feats is not None and max_feats >= 0 and B > 0:
         _check(int((offsets[1:] - offsets[:-1]).max()) <= max_feats, "max_feats: an example has more features")
-    if _DEBUG and v.dtype == FP8 and w_stride == 4 and v.shape[0] > 0:
+    if host_checks and v.dtype == FP8 and w_stride == 4 and v.shape[0] > 0:
         # table rows [w, scale, |v|^2, .]: the kernels apply only the scale's exponent, so every host
         # write of v / scale must keep scales powers of two (FMTable.set_v / adopt_fp8_rows do)
         sc = torch.as_strided(w, (v.shape[0],), (4,), w.storage_offset() + 1)
