@@ -175,6 +175,9 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
   const uint32_t vsb = (uint32_t)(a.v_stride * (long long)sizeof(TV));
   const bool self_on = SH && a.self.u1 > a.self.u0;  // (uniform)
   const uint32_t tsb = self_on ? (uint32_t)(a.self.v_stride * (long long)sizeof(TV)) : vsb;
+  // (SH) byte bases of this lane's fragment in the wire rows and in the own table rows
+  const uint64_t wbase = reinterpret_cast<uint64_t>(a.v) + coff;
+  const uint64_t sbase = self_on ? reinterpret_cast<uint64_t>(a.self.v) + coff : wbase;
   const int wave = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   const int nwaves = gridDim.x * kWavesPerBlock;
   const bool want_reg = a.reg_partial != nullptr;
@@ -238,7 +241,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
       const int m = min(kWave, e - base);
       int my_row = 0;
       float my_x = 0.f, my_w = 0.f, my_s = 1.f, my_n2 = 0.f;
-      uint64_t my_p = 0;  // (SH) byte address of the occurrence's row, column 0
+      uint32_t my_t = 0;  // (SH) the occurrence's row in its source, bit 31: an own (table) row
       if (kPrefetch && base == s) {
         my_row = p_row;
         my_x = p_x;
@@ -268,8 +271,7 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
           // one lane-parallel load per 64 occurrences instead of one per row group
           const bool own = own_key || (self_on && !self_key && a.self.has(my_row));
           const long long r = own ? (own_key ? (long long)key - a.self.base : a.self.row(my_row)) : my_row;
-          const char* b0 = reinterpret_cast<const char*>(own ? a.self.v : a.v);
-          my_p = reinterpret_cast<uint64_t>(b0) + (uint64_t)(uint32_t)r * (own ? tsb : vsb);
+          my_t = (uint32_t)r | (own ? 0x80000000u : 0u);  // (rows < 2^31: host-checked strides / counts)
           const uint64_t wp = reinterpret_cast<uint64_t>(own ? a.self.w + r * a.self.w_stride : a.w + r * a.w_stride);
           if constexpr (kNorm) {  // [w, scale, |v|^2, tag] wire tails / [w, scale, |v|^2, pad] table rows
             const gf4 wr = *gptr<gf4>(wp);
@@ -281,11 +283,10 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
           }
         }
         // lanes past the example take lane 0's row: the wrapped slots of a round read a valid row
-        const uint64_t p0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(my_p >> 32)) << 32) |
-                            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)my_p);
-        if (lane >= m) my_p = p0;
+        const uint32_t t0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)my_t);
+        if (lane >= m) my_t = t0;
       }
-      const int p_lo = (int)(uint32_t)my_p, p_hi = (int)(my_p >> 32);
+
       for (int q = 0; q < m; q += G * UNR) {
         float fr[UNR][EPL], fx[UNR], fs[UNR];
         int fraw[kRaw ? UNR : 1];
@@ -300,10 +301,14 @@ __device__ __forceinline__ void fwd_body(const FwdArgs& a) {
           const float x = __int_as_float(__builtin_amdgcn_ds_bpermute(fb, __float_as_int(my_x)));
           fx[u] = f < m ? x : 0.f;
           if constexpr (SH) {
-            const uint64_t pr = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(fb, p_hi) << 32) |
-                                (uint32_t)__builtin_amdgcn_ds_bpermute(fb, p_lo);
-            if constexpr (kRaw) fraw[u] = *gptr<int>(pr + coff);
-            else F::load_g(pr + coff, fr[u]);
+            // one broadcast per row group: the tagged row, then its source's base and stride (the
+            // 64-bit address in two broadcasts: k16 bf16 0.525 -> 0.518 ms, k128 fp8 0.864 -> 0.857,
+            // k64 tied; profiles/r5/emit_ab.txt)
+            const uint32_t tr = (uint32_t)__builtin_amdgcn_ds_bpermute(fb, (int)my_t);
+            const bool own = (tr >> 31) != 0;
+            const uint64_t pr = (own ? sbase : wbase) + (uint64_t)(tr & 0x7fffffffu) * (own ? tsb : vsb);
+            if constexpr (kRaw) fraw[u] = *gptr<int>(pr);
+            else F::load_g(pr, fr[u]);
           } else {
             const int row = __builtin_amdgcn_ds_bpermute(fb, my_row);
             const char* rp = vbytes + (uint64_t)(uint32_t)row * vsb;
