@@ -288,13 +288,13 @@ static size_t sort_temp_bytes(int n, hipStream_t st) {
 
 #include "radix_sort.hip"
 
-// Sort backend: rocPRIM onesweep (default) or the in-tree multipass radix sort (radix_sort.hip,
-// FM_SORT=fm: bitwise the same stable order; profiles/r5/sort_ab.txt)
+// Sort backend: the in-tree onesweep radix sort (radix_sort.hip, default) or rocPRIM's onesweep
+// (FM_SORT=rocprim); bitwise the same stable order (profiles/r5/sort_ab.txt)
 static int g_sort_algo = -1;
 static bool sort_in_tree() {
   if (g_sort_algo < 0) {
     const char* e = getenv("FM_SORT");
-    g_sort_algo = (e && std::string(e) == "fm") ? 1 : 0;
+    g_sort_algo = (e && std::string(e) == "rocprim") ? 0 : 1;
   }
   return g_sort_algo == 1;
 }
@@ -340,7 +340,14 @@ struct DedupArgs {
   const int* offsets;      // [B+1] (ex_shift > 0)
   void* ws;
   size_t ws_bytes;
+  // fused producers (in-tree sort: inside its histogram / first pass; rocPRIM: the separate kernels first)
+  const int* ids = nullptr;  // non-null: keys = sharded keys of ids (kW, kRps), written to the keys array
+  int kW = 1, kRps = 0;
+  int gen_codes = 0;         // payload = packed occurrence codes of the CSR offsets (written to payload)
+  int B = 0;                 // examples (gen_codes)
 };
+
+int launch_shard_keys(int n, const int* ids, int W, int Rps, int* keys, hipStream_t st);  // shard.hip
 
 // ---------------------------------------------------------------------------
 // Segment index (key -> segment id without an inverse map).  The row-sharded forward reads
@@ -391,10 +398,28 @@ int launch_dedup(const DedupArgs& a, hipStream_t st) {
   char* lb = base + tmp;
   if (tmp + align_up(lb_bytes(ntiles)) > a.ws_bytes) return -2;
 
+  if (a.gen_codes && (!a.offsets || a.B < 1)) return -4;
   if (sort_in_tree()) {
-    const int e = launch_radix_sort(a.keys, a.payload, a.skeys, a.spay, a.n, a.end_bit, a.ws, tmp, st);
+    RsSrc src;
+    src.ids = a.ids;
+    src.W = a.kW;
+    src.Rps = a.kRps;
+    if (a.gen_codes) {
+      src.offsets = a.offsets;
+      src.B = a.B;
+      src.code_shift = a.ex_shift;
+    }
+    const int e = launch_radix_sort(a.keys, a.payload, a.skeys, a.spay, a.n, a.end_bit, a.ws, tmp, st, src);
     if (e != 0) return e;
   } else {
+    if (a.ids) {
+      const int e = launch_shard_keys(a.n, a.ids, a.kW, a.kRps, const_cast<int*>(reinterpret_cast<const int*>(a.keys)), st);
+      if (e != 0) return e;
+    }
+    if (a.gen_codes) {
+      const int e = launch_csr_rows(a.B, a.offsets, const_cast<int*>(a.payload), a.ex_shift, st);
+      if (e != 0) return e;
+    }
     size_t sort_bytes = tmp;
     const hipError_t e = sort_pairs(a.ws, sort_bytes, a.keys, a.skeys, a.payload, a.spay, a.n, a.end_bit, st);
     if (e != hipSuccess) return (int)e;

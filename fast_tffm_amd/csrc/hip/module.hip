@@ -185,11 +185,19 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
   m.def("set_sort_algo", &fm::set_sort_algo, py::arg("in_tree"));  // 1: radix_sort.hip, 0: rocPRIM onesweep
   m.def("sort_algo", &fm::sort_algo);
   m.def(
-      "radix_sort",  // stable (key, value) sort of the in-tree backend (tests / benchmarks)
+      "radix_sort",  // stable (key, value) sort of the in-tree backend (tests / benchmarks; synchronous:
+                     // the look-back error word is checked)
       [](u64 keys, u64 vals, u64 kout, u64 vout, int n, int end_bit, u64 ws, size_t ws_bytes, u64 stream) {
         check(fm::launch_radix_sort(P<const uint32_t>(keys), P<const int>(vals), P<uint32_t>(kout), P<int>(vout), n,
                                     end_bit, P<void>(ws), ws_bytes, S(stream)),
               "radix_sort");
+        if (n <= 0) return;
+        int err = 0;
+        check((int)hipMemcpyAsync(&err, fm::radix_sort_error(P<void>(ws), n), sizeof(int), hipMemcpyDeviceToHost,
+                                  S(stream)),
+              "radix_sort error word");
+        check((int)hipStreamSynchronize(S(stream)), "radix_sort sync");
+        if (err) throw std::runtime_error("radix_sort: look-back spin bound hit");
       },
       py::arg("keys"), py::arg("vals"), py::arg("kout"), py::arg("vout"), py::arg("n"), py::arg("end_bit"),
       py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"));
@@ -199,7 +207,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       [](int n, int end_bit, int CH, u64 keys, u64 payload, u64 skeys, u64 spay, u64 uniq, u64 seg_start,
          u64 seg_chunk, u64 chunk_start, u64 chunk_seg, u64 chunk_key, u64 counts, u64 inv, u64 ex_of_occ,
          u64 sorted_ex, u64 vals, u64 sorted_x, int payload_is_ex, int ex_shift, u64 offsets, u64 ws,
-         size_t ws_bytes, u64 stream) {
+         size_t ws_bytes, u64 stream, u64 ids, int kW, int kRps, int gen_codes, int B) {
         if (CH < 1 || CH > fm::kMaxCH) throw std::invalid_argument("CH must be in [1, MAX_CH]");
         fm::DedupArgs a;
         a.n = n; a.end_bit = end_bit; a.CH = CH; a.keys = P<const uint32_t>(keys);
@@ -211,6 +219,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
         a.vals = P<const float>(vals); a.sorted_x = P<float>(sorted_x); a.ws = P<void>(ws);
         a.payload_is_ex = payload_is_ex; a.ex_shift = ex_shift; a.offsets = P<const int>(offsets);
         a.ws_bytes = ws_bytes;
+        a.ids = P<const int>(ids); a.kW = kW; a.kRps = kRps; a.gen_codes = gen_codes; a.B = B;
         check(fm::launch_dedup(a, S(stream)), "dedup");
       },
       py::arg("n"), py::arg("end_bit"), py::arg("CH"), py::arg("keys"), py::arg("payload"), py::arg("skeys"),
@@ -218,7 +227,8 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("chunk_seg"), py::arg("chunk_key"), py::arg("counts"), py::arg("inv"), py::arg("ex_of_occ"),
       py::arg("sorted_ex"),
       py::arg("vals"), py::arg("sorted_x"), py::arg("payload_is_ex"), py::arg("ex_shift"), py::arg("offsets"),
-      py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"));
+      py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"), py::arg("ids") = 0, py::arg("kW") = 1,
+      py::arg("kRps") = 0, py::arg("gen_codes") = 0, py::arg("B") = 0);
 
   m.def(
       "gather_rows",

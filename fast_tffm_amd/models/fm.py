@@ -486,8 +486,7 @@ class FactorizationMachine:
             side.wait_stream(main)  # inputs ready; previous step's readers of ws.dd are enqueued before
             with torch.cuda.stream(side), roctx_range("dedup"):
                 sb = self._slot_bits(b)
-                ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz, slot_bits=sb)
-                dd = K.dedup(rows, ws=ws.dd, key_bits=bits_for(self.table.rows), ex_of_occ=ex, vals=b.vals,
+                dd = K.dedup(rows, ws=ws.dd, key_bits=bits_for(self.table.rows), gen_codes=True, vals=b.vals,
                              num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets)
         else:
             ex = K.csr_rows(b.offsets, out=ws.dd.ex_of_occ[: b.nnz], nnz=b.nnz)
@@ -539,14 +538,14 @@ class FactorizationMachine:
         return _LocalPlan(b, idx, rows, dd, ev)
 
     def _plan_into(self, slot: "_LocalSlot", b: Batch):
-        """csr_rows + dedup of ``b`` into ``slot`` on the current stream; returns (rows, DedupOut)."""
+        """dedup of ``b`` (occurrence codes generated inside its sort) into ``slot`` on the current stream;
+        returns (rows, DedupOut)."""
         cfg = self.cfg
         slot.ensure(b.nnz, self.device, cfg.dedup_chunk)
         rows = b.ids if b.ids.dtype == torch.int32 else slot.rows32[: b.nnz].copy_(b.ids)
         sb = self._slot_bits(b)
         kb = bits_for(self.table.rows)
-        ex = K.csr_rows(b.offsets, out=slot.dd.ex_of_occ[: b.nnz], nnz=b.nnz, slot_bits=sb)
-        dd = K.dedup(rows, ws=slot.dd, key_bits=kb, ex_of_occ=ex, vals=b.vals,
+        dd = K.dedup(rows, ws=slot.dd, key_bits=kb, gen_codes=True, vals=b.vals,
                      num_examples=b.B, Kp=self.Kp, ex_shift=sb, offsets=b.offsets)
         return rows, dd
 

@@ -357,8 +357,9 @@ class DedupWorkspace:
 
 
 def set_sort_algo(algo: str) -> str:
-    """The dedup's sort backend: "rocprim" (onesweep, default) or "fm" (in-tree multipass radix sort,
-    hip/radix_sort.hip; same stable order); returns the previous one.  FM_SORT=fm at start-up too."""
+    """The dedup's sort backend: "fm" (in-tree onesweep radix sort, hip/radix_sort.hip, default) or
+    "rocprim" (rocPRIM's onesweep; same stable order); returns the previous one.  FM_SORT=rocprim at
+    start-up too."""
     _check(algo in ("rocprim", "fm"), f"sort backend {algo!r}: rocprim or fm")
     h = native.hip()
     was = "fm" if h.sort_algo() else "rocprim"
@@ -410,10 +411,16 @@ def csr_rows(offsets: torch.Tensor, out: torch.Tensor | None = None, nnz: int | 
     return out
 
 
+# FM_DEDUP_FUSE=0: the dedup's producers (shard_keys, csr_rows) as separate kernels (A/B switch)
+_FUSE_PRODUCERS = os.environ.get("FM_DEDUP_FUSE", "1") != "0"
+
+
 def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int = 32,
           ex_of_occ: torch.Tensor | None = None, vals: torch.Tensor | None = None, want_inv: bool = False,
           CH: int | None = None, want_perm: bool = False, num_examples: int | None = None,
-          Kp: int | None = None, ex_shift: int = 0, offsets: torch.Tensor | None = None) -> DedupOut:
+          Kp: int | None = None, ex_shift: int = 0, offsets: torch.Tensor | None = None,
+          gen_codes: bool = False, shard_ids: torch.Tensor | None = None,
+          shard: tuple[int, int] | None = None) -> DedupOut:
     """Sort-based unique over non-negative int32 keys (reference tf.unique, fm_model.py:72).
 
     Unique keys come out in ascending order (the reference's first-occurrence
@@ -422,6 +429,11 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
     map, per-occurrence values nor the occurrence permutation are needed, the
     sort carries the example index directly (one gather pass less).
     (``num_examples`` / ``Kp`` are accepted for interface stability; the plan does not use them.)
+
+    Fused producers (GPU; folded into the in-tree sort's histogram / first pass, the separate kernels
+    first under FM_SORT=rocprim): ``gen_codes`` -- the occurrence codes ``csr_rows(offsets,
+    slot_bits=ex_shift)`` (``ex_of_occ`` not given); ``shard_ids`` + ``shard = (world, rows_per_shard)``
+    -- ``keys`` is the OUTPUT buffer of ``shard_keys(shard_ids, ...)``.
     """
     dev = keys.device
     n = keys.numel()
@@ -429,6 +441,23 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
     if ws is None or ws.cap < n:
         ws = DedupWorkspace(max(n, 1), dev, CH or 32)
     CH = CH or ws.CH
+    fuse_ids = 0
+    if shard_ids is not None:
+        _check(shard is not None and shard_ids.numel() == n, "shard_ids needs shard=(world, rows_per_shard)")
+        if _FUSE_PRODUCERS and _is_gpu(keys) and shard_ids.dtype == torch.int32 and shard_ids.is_contiguous():
+            _check(shard[0] * shard[1] < 2**31, "sharded keys must fit int32")
+            fuse_ids = _p(shard_ids)
+        else:
+            shard_keys(shard_ids, shard[0], shard[1], keys)
+    fuse_codes = False
+    if gen_codes:
+        _check(ex_of_occ is None and offsets is not None, "gen_codes: offsets, no ex_of_occ")
+        in_payload = _is_gpu(keys) and not want_perm and (ex_shift > 0 or (vals is None and not want_inv))
+        ex_of_occ = ws.ex_of_occ[:n]
+        if _FUSE_PRODUCERS and in_payload and offsets.numel() > 1:
+            fuse_codes = True     # written into ex_of_occ only by the rocPRIM backend's csr_rows
+        else:
+            csr_rows(offsets, out=ex_of_occ, nnz=n, slot_bits=ex_shift)
     if ex_of_occ is not None:
         _chk_vec(ex_of_occ, torch.int32, n, "ex_of_occ", dev)
     if vals is not None:
@@ -458,7 +487,9 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
                 ex_of_occ=0 if ex_payload else _p(ex_of_occ),
                 sorted_ex=0 if ex_payload else _p(out.sorted_ex), vals=_p(vals), sorted_x=_p(out.sorted_x),
                 payload_is_ex=int(ex_payload), ex_shift=int(ex_shift), offsets=_p(offsets),
-                ws=_p(ws.ws), ws_bytes=ws.ws.numel(), stream=_stream(keys))
+                ws=_p(ws.ws), ws_bytes=ws.ws.numel(), stream=_stream(keys), ids=fuse_ids,
+                kW=int(shard[0]) if fuse_ids else 1, kRps=int(shard[1]) if fuse_ids else 0,
+                gen_codes=int(fuse_codes), B=offsets.numel() - 1 if fuse_codes else 0)
         out.bwd_fresh = True  # the backward counters were zeroed on this stream
     else:
         U = native.cpu().dedup(n=n, keys=_p(keys), skeys=_p(ws.skeys), perm=_p(ws.perm), uniq=_p(ws.uniq),

@@ -405,21 +405,19 @@ class ShardExchange(_Base):
                 dws = slot.ensure(k, sb.nnz, self.dev, m.cfg.dedup_chunk)
                 w1 = train and self.local_w1  # (world 1: keys = ids, no segment index)
                 if w1 and sb.ids.dtype == torch.int32 and sb.ids.is_contiguous():
-                    keys = sb.ids
-                else:
-                    keys = K.shard_keys(sb.ids, self.W, self.Rps, slot.keys[k])
-                ex, shift = None, 0
-                if train:
-                    shift = m._slot_bits(sb, always=True)
-                    ex = K.csr_rows(sb.offsets, out=dws.ex_of_occ[: sb.nnz], nnz=sb.nnz, slot_bits=shift)
+                    keys, sids = sb.ids, None
+                else:  # sharded keys: written by the dedup's sort (fused map)
+                    keys, sids = slot.keys[k][: sb.nnz], sb.ids
+                shift = m._slot_bits(sb, always=True) if train else 0
                 # training plans on the GPU find each occurrence's segment through a bucket index
                 # (K.seg_index) instead of the inverse map, a 5.1M-occurrence random scatter
                 lookup = train and gpu and K.seg_lookup_enabled() and not w1
                 part.keys = keys
-                part.dd = K.dedup(keys, ws=dws, key_bits=self.key_bits, ex_of_occ=ex,
-                                  vals=sb.vals if ex is not None else None, want_inv=not (lookup or w1),
-                                  num_examples=sb.B,
-                                  Kp=self.m.Kp, ex_shift=shift, offsets=sb.offsets if shift else None)
+                # (training: occurrence codes generated inside the sort -- csr_rows fused)
+                part.dd = K.dedup(keys, ws=dws, key_bits=self.key_bits, gen_codes=train,
+                                  vals=sb.vals if train else None, want_inv=not (lookup or w1),
+                                  num_examples=sb.B, Kp=self.m.Kp, ex_shift=shift,
+                                  offsets=sb.offsets if train else None, shard_ids=sids, shard=(self.W, self.Rps))
                 part.seg = K.seg_index(part.dd, self.key_bits, slot.segidx_buf(k)) if lookup else None
                 counts.append(K.owner_counts(part.dd, self.Rps, self.W))
                 pl.parts.append(part)

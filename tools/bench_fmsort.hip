@@ -1,5 +1,5 @@
 // Micro-benchmark + bitwise check of the in-tree radix sort (fast_tffm_amd/csrc/hip/radix_sort.hip)
-// against rocPRIM's onesweep (the dedup chain's previous sort; its best measured config, 1024x8
+// against rocPRIM's onesweep (the dedup chain's FM_SORT=rocprim backend; its best measured config, 1024x8
 // match ranking, 9-bit digits) on Criteo-shaped batches (n = 5.1M occurrences, ~85% on ~2k hot
 // keys, power law).  Interleaved rounds in one process.  Build (in-tree, CPU side):
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Ifast_tffm_amd/csrc tools/bench_fmsort.hip -o tools/bench_fmsort
@@ -104,7 +104,10 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(hv2.data(), vo2, n * 4, hipMemcpyDeviceToHost));
     long bad = 0;
     for (int i = 0; i < n; ++i) bad += (hk1[i] != hk2[i]) || (hv1[i] != hv2[i]);
-    bad_total += bad != 0;
+    int err = 0;
+    CK(hipMemcpy(&err, fm::radix_sort_error(ws, n), 4, hipMemcpyDeviceToHost));
+    if (err) printf("look-back error word %d\n", err);
+    bad_total += bad != 0 || err != 0;
     std::sort(a.begin(), a.end());
     std::sort(b.begin(), b.end());
     printf("n=%d bits=%d: rocPRIM onesweep 9-bit %.1f us (min %.1f) | in-tree %.1f us (min %.1f) | %s (%ld mismatches)\n",
