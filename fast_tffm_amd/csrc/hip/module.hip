@@ -353,12 +353,13 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
 
   m.def(
       "owner_counts",
-      [](u64 uniq, u64 num_unique, long long Rps, int W, u64 out, u64 stream) {
+      [](u64 uniq, u64 num_unique, long long Rps, int W, u64 out, u64 stream, long long stride, u64 out2) {
         check(fm::launch_owner_counts(P<const uint32_t>(uniq), P<const int>(num_unique), Rps, W, P<long long>(out),
-                                      S(stream)),
+                                      S(stream), stride, P<long long>(out2)),
               "owner_counts");
       },
-      py::arg("uniq"), py::arg("num_unique"), py::arg("Rps"), py::arg("W"), py::arg("out"), py::arg("stream"));
+      py::arg("uniq"), py::arg("num_unique"), py::arg("Rps"), py::arg("W"), py::arg("out"), py::arg("stream"),
+      py::arg("stride") = 1, py::arg("out2") = 0);
 
   m.def(
       "zero_listed_rows",

@@ -88,6 +88,10 @@ constexpr unsigned kOsAgg = 1u << 30, kOsInc = 2u << 30, kOsCnt = (1u << 30) - 1
 constexpr int kOsMaxPasses = 4;
 constexpr int kOsHistBlocks = 1024;
 constexpr int kOsSpinCap = 1 << 20;
+#ifndef FM_OS_LOOKBACK
+#define FM_OS_LOOKBACK 4
+#endif
+constexpr int kOsLookback = FM_OS_LOOKBACK;  // predecessor tiles read per look-back round
 
 // Fused producers of the sort's input (the dedup chain's two map kernels folded into the sort):
 // keys from row ids under the sharded-key map, written by the histogram kernel, and the payload
@@ -279,20 +283,20 @@ __global__ __launch_bounds__(kRsThreads) void os_pass_kernel(OsPass o) {
   unsigned ttot, gsum;
   const unsigned tstart = rs_block_excl(tcount, sh, ttot);
   const unsigned gbase = rs_block_excl(d < D ? o.hist[d] : 0u, sh, gsum);
-  // look-back: thread d walks back over the tiles before this one, four per round
+  // look-back: thread d walks back over the tiles before this one, kOsLookback per round
   unsigned excl = 0;
   if (d < D && tile > 0) {
     int t = tile - 1;
     for (int round = 0; t >= 0; ++round) {
-      unsigned w4[4];
+      unsigned w4[kOsLookback];
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
+      for (int k = 0; k < kOsLookback; ++k)
         w4[k] = t - k >= 0 ? __hip_atomic_load(o.status + (size_t)(t - k) * D + d, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT)
                            : kOsInc;  // (before tile 0: an inclusive prefix of 0)
       bool stop = false, wait = false;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < kOsLookback; ++k) {
         if (stop || wait) continue;
         const unsigned f = w4[k] >> 30;
         if (f == 0) {

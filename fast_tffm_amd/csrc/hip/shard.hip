@@ -612,13 +612,17 @@ __device__ __forceinline__ int wave_lower_bound(const uint32_t* uniq, int U, uns
 }
 
 __global__ __launch_bounds__(kWave) void owner_counts_kernel(const uint32_t* uniq, const int* num_unique,
-                                                             long long Rps, int W, long long* out) {
+                                                             long long Rps, int W, long long* out, long long stride,
+                                                             long long* out2) {
   const int w = blockIdx.x;
   const int lane = threadIdx.x;
   const int U = *num_unique;
   const int a = wave_lower_bound(uniq, U, (unsigned long long)w * Rps, lane);
   const int b = wave_lower_bound(uniq, U, (unsigned long long)(w + 1) * Rps, lane);
-  if (lane == 0) out[w] = b - a;
+  if (lane == 0) {
+    out[w * stride] = b - a;
+    if (out2) out2[w * stride] = b - a;
+  }
 }
 
 // Sharded key of every occurrence: owner (id % W) major, local row (id / W) minor,
@@ -636,10 +640,11 @@ int launch_shard_keys(int n, const int* ids, int W, int Rps, int* keys, hipStrea
   return (int)hipGetLastError();
 }
 
+// out[w * stride] (and out2[w * stride], nullable: the world-1 count exchange's received copy)
 int launch_owner_counts(const uint32_t* uniq, const int* num_unique, long long Rps, int W, long long* out,
-                        hipStream_t st) {
-  if (W <= 0) return 0;
-  hipLaunchKernelGGL(owner_counts_kernel, dim3(W), dim3(kWave), 0, st, uniq, num_unique, Rps, W, out);
+                        hipStream_t st, long long stride = 1, long long* out2 = nullptr) {
+  if (W <= 0 || stride < 1) return 0;
+  hipLaunchKernelGGL(owner_counts_kernel, dim3(W), dim3(kWave), 0, st, uniq, num_unique, Rps, W, out, stride, out2);
   return (int)hipGetLastError();
 }
 

@@ -754,15 +754,25 @@ def shard_keys(ids: torch.Tensor, world: int, rows_per_shard: int, out: torch.Te
     return out[:n]
 
 
-def owner_counts(dd: DedupOut, rows_per_shard: int, world: int) -> torch.Tensor:
-    """int64[world]: unique keys (owner * rows_per_shard + row) per owner, computed without a host sync."""
-    out = torch.empty(world, dtype=torch.int64, device=dd.uniq.device)
+def owner_counts(dd: DedupOut, rows_per_shard: int, world: int, out: torch.Tensor | None = None,
+                 out2: torch.Tensor | None = None) -> torch.Tensor:
+    """int64[world]: unique keys (owner * rows_per_shard + row) per owner, computed without a host sync.
+    ``out`` / ``out2``: 1-D int64 views (any stride) to write (``out2``: a second copy, GPU)."""
+    if out is None:
+        out = torch.empty(world, dtype=torch.int64, device=dd.uniq.device)
+    _check(out.dtype == torch.int64 and out.dim() == 1 and out.numel() == world, "owner_counts out: int64[world]")
     if dd.uniq.device.type == "cuda":
+        if out2 is not None:
+            _check(out2.dtype == torch.int64 and out2.shape == out.shape and out2.stride() == out.stride()
+                   and out2.device == out.device, "owner_counts out2: like out")
         native.hip().owner_counts(uniq=_p(dd.uniq), num_unique=_p(dd.num_unique), Rps=int(rows_per_shard), W=world,
-                                  out=_p(out), stream=_stream(dd.uniq))
+                                  out=_p(out), stream=_stream(dd.uniq), stride=out.stride(0),
+                                  out2=_p(out2) if out2 is not None else 0)
     else:
         owner = torch.div(dd.uniq[: dd.sync()].to(torch.int64), rows_per_shard, rounding_mode="floor")
         out.copy_(torch.bincount(owner, minlength=world))
+        if out2 is not None:
+            out2.copy_(out)
     return out
 
 

@@ -397,6 +397,9 @@ class ShardExchange(_Base):
         with self._side_ctx():
             pl.parts = []
             counts = []
+            if gpu:
+                # [0] = sent counts, [1] = received counts (world 1: written by owner_counts too), [W, P]
+                both = torch.empty((2, self.W, len(ranges)), dtype=torch.int64, device=self.dev)
             for k, (e0, e1, n0, n1) in enumerate(ranges):
                 part = _Part()
                 offs = b.offsets[e0:e1 + 1] if n0 == 0 else b.offsets[e0:e1 + 1] - n0
@@ -419,24 +422,23 @@ class ShardExchange(_Base):
                                   num_examples=sb.B, Kp=self.m.Kp, ex_shift=shift,
                                   offsets=sb.offsets if train else None, shard_ids=sids, shard=(self.W, self.Rps))
                 part.seg = K.seg_index(part.dd, self.key_bits, slot.segidx_buf(k)) if lookup else None
-                counts.append(K.owner_counts(part.dd, self.Rps, self.W))
+                if gpu:  # column k of [W, P]: row q = what goes to rank q
+                    K.owner_counts(part.dd, self.Rps, self.W, out=both[0, :, k],
+                                   out2=both[1, :, k] if self.W == 1 else None)
+                else:
+                    counts.append(K.owner_counts(part.dd, self.Rps, self.W))
                 pl.parts.append(part)
-            c = torch.stack(counts, dim=1)     # [W, P]: row q = what goes to rank q
             if gpu:
                 # the count exchange runs on the device (RCCL, plan communicator) right behind the
-                # dedup: [0] = sent counts, [1] = received counts, both copied to pinned memory
-                both = torch.empty((2,) + tuple(c.shape), dtype=c.dtype, device=self.dev)
-                both[0].copy_(c)
-                if self.W == 1:
-                    both[1].copy_(c)
-                else:
+                # dedup, both copied to pinned memory (no stack / copy kernels on the plan's chain)
+                if self.W > 1:
                     dist.all_to_all_single(both[1], both[0], group=self.plan_group)
-                pl.counts = torch.empty(both.shape, dtype=c.dtype, pin_memory=True)
+                pl.counts = torch.empty(both.shape, dtype=torch.int64, pin_memory=True)
                 pl.counts.copy_(both, non_blocking=True)
                 pl.counts_ev = torch.cuda.Event()
                 pl.counts_ev.record(torch.cuda.current_stream(self.dev))
             else:
-                pl.counts, pl.counts_ev = c, None
+                pl.counts, pl.counts_ev = torch.stack(counts, dim=1), None
         return pl
 
     def _plan_finish(self, pl: _ShardPlan, early: bool = False) -> None:
