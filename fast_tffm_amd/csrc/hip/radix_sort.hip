@@ -61,26 +61,22 @@ __device__ inline void rs_load(const RsPass& p, int tile, uint32_t (&key)[kRsIte
   }
 }
 
-// Block-wide exclusive scan of one value per thread (kRsThreads threads); returns the total too.
-__device__ inline unsigned rs_block_excl(unsigned v, unsigned* sh /*[kRsWaves]*/, unsigned& total) {
+// Block-wide exclusive scan of one 64-bit value per thread (kRsThreads threads): two 32-bit counts
+// scanned at once (neither field's sum carries into the other).
+__device__ inline uint64_t rs_block_excl(uint64_t v, uint64_t* sh /*[kRsWaves]*/) {
   const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x >> 6;
-  unsigned inc = v;
+  uint64_t inc = v;
 #pragma unroll
   for (int o = 1; o < kWave; o <<= 1) {
-    const unsigned up = __shfl_up(inc, o, kWave);
+    const uint64_t up = __shfl_up(inc, o, kWave);
     if (lane >= o) inc += up;
   }
   if (lane == kWave - 1) sh[wv] = inc;
   __syncthreads();
-  unsigned b = 0, t = 0;
+  uint64_t b = 0;
 #pragma unroll
-  for (int w = 0; w < kRsWaves; ++w) {
-    const unsigned s = sh[w];
-    if (w < wv) b += s;
-    t += s;
-  }
-  __syncthreads();
-  total = t;
+  for (int w = 0; w < kRsWaves; ++w)
+    if (w < wv) b += sh[w];
   return b + inc - v;
 }
 
@@ -219,10 +215,11 @@ __global__ __launch_bounds__(kRsThreads) void os_pass_kernel(OsPass o) {
   __shared__ unsigned wc[kRsWaves][D];
   __shared__ int gofs[D];
   __shared__ uint32_t stage[kRsTile];
-  __shared__ unsigned sh[kRsWaves];
+  __shared__ uint64_t sh[kRsWaves];
   __shared__ int tile_s;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
   if (threadIdx.x == 0) tile_s = atomicAdd(o.tile_ctr, 1);
+  const unsigned hd = threadIdx.x < D ? o.hist[threadIdx.x] : 0u;  // (loaded early: used after the ranking)
   for (int t = threadIdx.x; t < kRsWaves * D; t += kRsThreads) (&wc[0][0])[t] = 0u;
   __syncthreads();
   const int tile = tile_s;
@@ -280,9 +277,9 @@ __global__ __launch_bounds__(kRsThreads) void os_pass_kernel(OsPass o) {
     __hip_atomic_store(o.status + (size_t)tile * D + d, (tile == 0 ? kOsInc : kOsAgg) | tcount, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   }
-  unsigned ttot, gsum;
-  const unsigned tstart = rs_block_excl(tcount, sh, ttot);
-  const unsigned gbase = rs_block_excl(d < D ? o.hist[d] : 0u, sh, gsum);
+  // tile-local start of digit d's run (low half) and the global start of digit d (high half)
+  const uint64_t ex2 = rs_block_excl(((uint64_t)hd << 32) | tcount, sh);
+  const unsigned tstart = (unsigned)ex2, gbase = (unsigned)(ex2 >> 32);
   // look-back: thread d walks back over the tiles before this one, kOsLookback per round
   unsigned excl = 0;
   if (d < D && tile > 0) {

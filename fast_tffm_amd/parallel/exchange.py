@@ -746,12 +746,27 @@ class ShardExchange(_Base):
         if part.U and int(dd.uniq[part.U - 1].item()) >= self.W * self.Rps:
             raise RuntimeError("sharded key out of range")
 
+    def _drop_pending(self) -> None:
+        """The caller broke the batch order it promised (``next_batch`` / ``next2``): the pending
+        plans are for batches that are not coming next -- drop them (their slots free again; every
+        rank drops the same plans, since the call sequence is the same on all ranks)."""
+        for p in self.pending:
+            e = getattr(p, "early", None)
+            if e is not None and getattr(e, "work", None) is not None:
+                e.work.wait()
+                e.work = None
+        if self.dev.type == "cuda":
+            torch.cuda.synchronize(self.dev)  # (rare path: nothing in flight may still use the slots)
+        self.pending = []
+
     def _take_plan(self, b: Batch, train: bool) -> _ShardPlan:
+        if train and self.pending and self.pending[0].b is not b:
+            self._drop_pending()
         pl = self.pending[0] if (self.pending and train) else None
         if pl is not None and pl.b is b and (len(pl.parts) > 1) == (self.nparts > 1 and b.B >= 2 * self.nparts):
             self.pending.pop(0)
             self._plan_finish(pl)
-        else:  # (pending plans for other batches, e.g. the next training batches, stay pending)
+        else:  # (evaluation: the pending training plans stay pending)
             pl = self._plan(b, train, early=False)
         if pl.ready is not None:
             main = torch.cuda.current_stream(self.dev)

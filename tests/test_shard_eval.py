@@ -7,7 +7,10 @@ single-communicator mode.
   (regression: an eval plan used to reuse the next-but-one batch's slot and
   overwrite its dedup in place);
 * ``FM_SINGLE_COMM=1`` (every collective on one communicator, program order)
-  trains bitwise identically to the default two-communicator pipeline.
+  trains bitwise identically to the default two-communicator pipeline;
+* a caller that trains another batch than the ``next_batch`` / ``next2`` it promised gets the
+  plans of the promised batches dropped (regression: the pipeline ran out of plan slots) and
+  trains bitwise like a run whose lookahead matched.
 
 CPU, gloo, world 2 (reference C3/C4/C6 sites: /root/reference/run_tffm.py:181-226).
 """
@@ -46,10 +49,15 @@ def _worker(rank, world, port, variant, out_dir):
     bs = [random_batch(B, V, max_feats=12, seed=100 * s + rank) for s in range(STEPS)]
     vb = random_batch(B, V, max_feats=12, seed=7777 + rank)
     losses, evals = [], []
+    order = [0, 1, 2, 4, 3, 5] if variant in ("deviate", "reorder") else list(range(STEPS))
     for s in range(STEPS):
-        nb = bs[s + 1] if s + 1 < STEPS else None
-        nb2 = bs[s + 2] if s + 2 < STEPS else None
-        losses.append(m.train_step(bs[s], nb, nb2).mean_loss())
+        if variant == "deviate":  # promises the natural order, trains ``order``
+            nb = bs[s + 1] if s + 1 < STEPS else None
+            nb2 = bs[s + 2] if s + 2 < STEPS else None
+        else:
+            nb = bs[order[s + 1]] if s + 1 < STEPS else None
+            nb2 = bs[order[s + 2]] if s + 2 < STEPS else None
+        losses.append(m.train_step(bs[order[s]], nb, nb2).mean_loss())
         if variant == "eval" and s in (1, 3):
             evals.append(m.eval_loss(vb))  # every training slot is busy here
     torch.save({"rows": m.table.reference_rows(), "acc": m.table.s0v.clone(), "losses": torch.tensor(losses),
@@ -79,3 +87,12 @@ def test_single_communicator_mode_is_exact(tmp_path):
     for a, b in zip(dual, single):
         assert torch.equal(a["losses"], b["losses"])
         assert torch.equal(a["rows"], b["rows"])
+
+
+def test_broken_lookahead_promise_drops_pending_plans(tmp_path):
+    ref = _run(tmp_path, "reorder")
+    dev = _run(tmp_path, "deviate")
+    for a, b in zip(ref, dev):
+        assert torch.equal(a["losses"], b["losses"])
+        assert torch.equal(a["rows"], b["rows"])
+        assert torch.equal(a["acc"], b["acc"])
