@@ -20,8 +20,9 @@
 //    once; otherwise the chunk writes a partial row;
 //  * rows split over <= kSmallChunks chunks are combined by one lane group
 //    (ordered sum), hotter rows (Criteo's 3-value fields: ~40k occurrences per
-//    row at B=128k) are queued to a second kernel where a whole workgroup sums
-//    the partials in a fixed interleaved order and reduces through LDS.
+//    row at B=128k) by a whole workgroup that sums the partials in a fixed
+//    interleaved order and reduces through LDS; the chunk kernel lists both
+//    kinds, and both combines run in one launch (fm_bwd_combine_kernel).
 #include "fm_common.h"
 
 namespace fm {
@@ -99,6 +100,7 @@ struct BwdArgs {
   // gradient rows of piece 0 can travel while piece 1 is computed; -1 = all segments
   const int* seg_bounds;    // [2 * n_owners + 1]
   int piece, n_owners;
+  int big_blocks;           // (set by launch_bwd) fm_bwd_combine_kernel's leading hot-row workgroups
   float* partial;           // [#chunks, Kp + 4]
   int* big_list;            // [U] rows for the workgroup combine
   int* big_count;           // device scalar, zeroed by the launcher
@@ -606,8 +608,13 @@ __device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
       if (t == 0) {
         dst[a.Kp] = Scx;
         dst[a.Kp + 1] = Sc;
-        // the row's first chunk registers the row for the combine kernels
-        if (first) a.multi[atomicAdd(&a.counts_rw[2], 1)] = u;
+        // the row's first chunk registers the row for the combine: rows over <= kSmallChunks chunks
+        // for a lane group, hotter rows for a workgroup (both lists complete when this kernel ends,
+        // so the two combines run as one launch)
+        if (first) {
+          if (a.seg_chunk[u + 1] - a.seg_chunk[u] > kSmallChunks) a.big_list[atomicAdd(a.big_count, 1)] = u;
+          else a.multi[atomicAdd(&a.counts_rw[2], 1)] = u;
+        }
       }
     }
   }
@@ -633,10 +640,8 @@ FM_EMIT_CHUNK_KERNEL(fm_bwd_chunk_emit_pc_nox_kernel, kChunkEmitPcNoX)
 #undef FM_EMIT_CHUNK_KERNEL
 
 // Rows split over 2..kSmallChunks chunks: one lane group, ordered sum of the partials.
-// Hotter rows are appended to big_list for fm_bwd_big_kernel.
 template <int LPR, typename TV>
-__global__ __launch_bounds__(kBlock) void fm_bwd_combine_kernel(BwdArgs a) {
-  const uint32_t sr = sr_step_seed(a.sr_counter);  // stochastic rounding seed (0: nearest)
+__device__ inline void bwd_combine_body(const BwdArgs& a, int blk, int nblk, uint32_t sr) {
   constexpr int EPL = Frag<TV>::N;
   constexpr int G = kWave / LPR;
   const int lane = threadIdx.x & (kWave - 1);
@@ -644,16 +649,11 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_combine_kernel(BwdArgs a) {
   const int nv = a.Kp / EPL;
   const bool tact = t < nv;
   const int tE = tact ? t : nv - 1;
-  const int nmulti = a.counts[2];  // rows spanning > 1 chunk, listed by the chunk kernel
-  const int ngroups = gridDim.x * kWavesPerBlock * G;
-  for (int i = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + g; i < nmulti; i += ngroups) {
+  const int nmulti = a.counts[2];  // rows spanning 2..kSmallChunks chunks, listed by the chunk kernel
+  const int ngroups = nblk * kWavesPerBlock * G;
+  for (int i = (blk * kWavesPerBlock + (threadIdx.x >> 6)) * G + g; i < nmulti; i += ngroups) {
     const int u = a.multi[i];
     const int c0 = a.seg_chunk[u], c1 = a.seg_chunk[u + 1];
-    const int nc = c1 - c0;
-    if (nc > kSmallChunks) {
-      if (t == 0) a.big_list[atomicAdd(a.big_count, 1)] = u;
-      continue;
-    }
     float A[EPL];
 #pragma unroll
     for (int k = 0; k < EPL; ++k) A[k] = 0.f;
@@ -691,8 +691,7 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_combine_kernel(BwdArgs a) {
 // Hot rows: one workgroup per row. Lane group q of the workgroup sums chunks
 // c0+q, c0+q+NG, ... ; the NG group sums are reduced in LDS in group order.
 template <int LPR, typename TV>
-__global__ __launch_bounds__(kBlock) void fm_bwd_big_kernel(BwdArgs a) {
-  const uint32_t sr = sr_step_seed(a.sr_counter);  // stochastic rounding seed (0: nearest)
+__device__ inline void bwd_big_body(const BwdArgs& a, int blk, int nblk, uint32_t sr) {
   constexpr int EPL = Frag<TV>::N;
   constexpr int G = kWave / LPR;
   constexpr int NG = kWavesPerBlock * G;
@@ -705,7 +704,7 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_big_kernel(BwdArgs a) {
   const bool tact = t < nv;
   const int tE = tact ? t : nv - 1;
   const int nbig = *a.big_count;
-  for (int bi = blockIdx.x; bi < nbig; bi += gridDim.x) {
+  for (int bi = blk; bi < nbig; bi += nblk) {
     const int u = a.big_list[bi];
     const int c0 = a.seg_chunk[u], c1 = a.seg_chunk[u + 1];
     float A[EPL];
@@ -759,6 +758,20 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_big_kernel(BwdArgs a) {
     }
     __syncthreads();
   }
+}
+
+// Both combines in one launch (their row lists are disjoint and complete after the chunk kernel):
+// the first a.big_blocks workgroups take the hot rows (the long poles, dispatched first), the rest the
+// lane-group combine.  Two launches ran back to back (combine 35-43 us, then big 38-40 us in-step);
+// one launch, same box: k64 fp32 0.605-0.608 -> 0.592-0.596 ms, EMIT k64 0.636 -> 0.623, k16 bf16 tied;
+// 32-lane rows (k128) lost (fp8 FTRL 0.770 -> 0.778) and keep two launches of this kernel
+// (big_blocks = 0: combine only; = grid: hot rows only).
+constexpr int kBigBlocks = 1024;
+template <int LPR, typename TV>
+__global__ __launch_bounds__(kBlock) void fm_bwd_combine_kernel(BwdArgs a) {
+  const uint32_t sr = sr_step_seed(a.sr_counter);  // stochastic rounding seed (0: nearest)
+  if ((int)blockIdx.x < a.big_blocks) bwd_big_body<LPR, TV>(a, blockIdx.x, a.big_blocks, sr);
+  else bwd_combine_body<LPR, TV>(a, blockIdx.x - a.big_blocks, gridDim.x - a.big_blocks, sr);
 }
 
 static int env_int(const char* name, int dflt) {
@@ -842,8 +855,16 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   } else {
     FM_DISPATCH_SHM(dtype, lpr, fm_bwd_chunk_kernel, g1, chunk_lds, st, a);
   }
-  FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, a);
-  FM_DISPATCH(dtype, lpr, fm_bwd_big_kernel, 1024, st, a);
+  BwdArgs b = a;
+  if (lpr >= 32) {
+    b.big_blocks = 0;
+    FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, b);
+    b.big_blocks = kBigBlocks;
+    FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, kBigBlocks, st, b);
+  } else {
+    b.big_blocks = kBigBlocks;
+    FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, kBigBlocks + g2, st, b);
+  }
   return (int)hipGetLastError();
 }
 
