@@ -1,5 +1,10 @@
 #!/bin/bash
-# same-box A/B: this tree vs ab_old/ (a copy of HEAD with its own build)
+# Same-box A/B of this tree against ab_old/ -- a copy of an earlier commit with its own in-tree build:
+#   rm -rf ab_old && mkdir ab_old && git archive <commit> | tar -x -C ab_old
+#   (cd ab_old && python -c "import __graft_entry__ as g; g.build()")
+# then: gpurun -- 'bash tools/gpu_ab_tree.sh'.  GPU tests on this tree first, then the default / k16 bf16 /
+# k128 fp8 FTRL / default presets and the world-1 EMIT step, alternating new / old.  (Delete ab_old/ after:
+# every gpurun call uploads it.)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/cmb
