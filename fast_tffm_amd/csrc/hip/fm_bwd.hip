@@ -766,7 +766,7 @@ __device__ inline void bwd_big_body(const BwdArgs& a, int blk, int nblk, uint32_
 // one launch, same box: k64 fp32 0.605-0.608 -> 0.592-0.596 ms, EMIT k64 0.636 -> 0.623, k16 bf16 tied;
 // 32-lane rows (k128) lost (fp8 FTRL 0.770 -> 0.778) and keep two launches of this kernel
 // (big_blocks = 0: combine only; = grid: hot rows only).
-constexpr int kBigBlocks = 1024;
+constexpr int kBigBlocks = 1024;  // (FM_BIG_BLOCKS overrides: A/B)
 template <int LPR, typename TV>
 __global__ __launch_bounds__(kBlock) void fm_bwd_combine_kernel(BwdArgs a) {
   const uint32_t sr = sr_step_seed(a.sr_counter);  // stochastic rounding seed (0: nearest)
@@ -856,14 +856,15 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
     FM_DISPATCH_SHM(dtype, lpr, fm_bwd_chunk_kernel, g1, chunk_lds, st, a);
   }
   BwdArgs b = a;
+  static const int nbig = env_int("FM_BIG_BLOCKS", kBigBlocks) > 0 ? env_int("FM_BIG_BLOCKS", kBigBlocks) : kBigBlocks;
   if (lpr >= 32) {
     b.big_blocks = 0;
     FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, b);
-    b.big_blocks = kBigBlocks;
-    FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, kBigBlocks, st, b);
+    b.big_blocks = nbig;
+    FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, nbig, st, b);
   } else {
-    b.big_blocks = kBigBlocks;
-    FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, kBigBlocks + g2, st, b);
+    b.big_blocks = nbig;
+    FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, nbig + g2, st, b);
   }
   return (int)hipGetLastError();
 }
