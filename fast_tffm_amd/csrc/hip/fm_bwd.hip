@@ -100,7 +100,8 @@ struct BwdArgs {
   // gradient rows of piece 0 can travel while piece 1 is computed; -1 = all segments
   const int* seg_bounds;    // [2 * n_owners + 1]
   int piece, n_owners;
-  int big_blocks;           // (set by launch_bwd) fm_bwd_combine_kernel's leading hot-row workgroups
+  int big_blocks;           // (set by launch_bwd) fm_bwd_combine_kernel's hot-row workgroups
+  int big_last;             // (set by launch_bwd) 1: they follow the lane-group combine's workgroups
   float* partial;           // [#chunks, Kp + 4]
   int* big_list;            // [U] rows for the workgroup combine
   int* big_count;           // device scalar, zeroed by the launcher
@@ -770,8 +771,10 @@ constexpr int kBigBlocks = 1024;  // (FM_BIG_BLOCKS overrides: A/B)
 template <int LPR, typename TV>
 __global__ __launch_bounds__(kBlock) void fm_bwd_combine_kernel(BwdArgs a) {
   const uint32_t sr = sr_step_seed(a.sr_counter);  // stochastic rounding seed (0: nearest)
-  if ((int)blockIdx.x < a.big_blocks) bwd_big_body<LPR, TV>(a, blockIdx.x, a.big_blocks, sr);
-  else bwd_combine_body<LPR, TV>(a, blockIdx.x - a.big_blocks, gridDim.x - a.big_blocks, sr);
+  const int nsmall = gridDim.x - a.big_blocks;
+  const int b0 = a.big_last ? nsmall : 0;  // first hot-row workgroup
+  if ((int)blockIdx.x >= b0 && (int)blockIdx.x < b0 + a.big_blocks) bwd_big_body<LPR, TV>(a, blockIdx.x - b0, a.big_blocks, sr);
+  else bwd_combine_body<LPR, TV>(a, a.big_last ? blockIdx.x : blockIdx.x - a.big_blocks, nsmall, sr);
 }
 
 static int env_int(const char* name, int dflt) {
@@ -856,11 +859,14 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
     FM_DISPATCH_SHM(dtype, lpr, fm_bwd_chunk_kernel, g1, chunk_lds, st, a);
   }
   BwdArgs b = a;
+  static const int big_last = env_int("FM_BIG_LAST", 0);
+  b.big_last = big_last;
   static const int nbig = env_int("FM_BIG_BLOCKS", kBigBlocks) > 0 ? env_int("FM_BIG_BLOCKS", kBigBlocks) : kBigBlocks;
   if (lpr >= 32) {
     b.big_blocks = 0;
     FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, b);
     b.big_blocks = nbig;
+    b.big_last = 0;
     FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, nbig, st, b);
   } else {
     b.big_blocks = nbig;
