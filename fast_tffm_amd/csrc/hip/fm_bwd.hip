@@ -862,7 +862,8 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   static const int big_last = env_int("FM_BIG_LAST", 0);
   b.big_last = big_last;
   static const int nbig = env_int("FM_BIG_BLOCKS", kBigBlocks) > 0 ? env_int("FM_BIG_BLOCKS", kBigBlocks) : kBigBlocks;
-  if (lpr >= 32) {
+  static const bool one32 = env_int("FM_COMBINE_ONE32", 0) != 0;  // (A/B: one launch for 32-lane rows too)
+  if (lpr >= 32 && !one32) {
     b.big_blocks = 0;
     FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, b);
     b.big_blocks = nbig;
