@@ -194,6 +194,7 @@ def main() -> int:
     if dev.type == "cuda":
         torch.cuda.synchronize()
     elapsed_own = time.perf_counter() - t_start
+    K.check_device_errors(dev)  # (kernels' sticky error word, e.g. a failed sort look-back: exit non-zero)
     elapsed = ctx.all_reduce_scalar(elapsed_own, op="max")
     elapsed_min = ctx.all_reduce_scalar(elapsed_own, op="min")
     # bytes this rank put on the wire to OTHER ranks per timed step (all-to-all rows / ids /

@@ -52,6 +52,7 @@ struct RleArgs {
   int* sorted_ex;                 // [n] (payload = occurrence)
   const float* vals;              // [n] (payload = occurrence)
   float* sorted_x;                // [n] (payload = occurrence)
+  const int* sort_err;            // in-tree sort's look-back error word (null: rocPRIM)
 };
 
 // v[q] = p[j0 + q] (fill outside [0, n)); two 16-byte loads when in range (j0 % 8 == 0).
@@ -142,7 +143,12 @@ __global__ __launch_bounds__(kBlock) void rle_count_kernel(RleArgs a) {
     a.tile_cnt[tile] = ((unsigned long long)tot[0] << 32) | tot[1];
     if (tile == 0) {
       a.counts[3] = 0;
-      a.counts[5] = a.counts[6] = a.counts[7] = 0;
+      a.counts[5] = a.counts[6] = 0;
+      // the sort's verdict: counts[7] != 0 = this plan is invalid (DedupOut.sync raises), and the
+      // sticky device word keeps it for the host's periodic check (check_device_errors)
+      const int e = a.sort_err ? *a.sort_err : 0;
+      a.counts[7] = e;
+      if (e) atomicOr(&g_fm_dev_error, kDevErrSort);
     }
   }
 }
@@ -427,7 +433,7 @@ int launch_dedup(const DedupArgs& a, hipStream_t st) {
   RleArgs r{a.n, a.CH, ntiles, a.skeys, a.spay, a.ex_shift,
             a.offsets, reinterpret_cast<unsigned long long*>(lb + 8), a.uniq, a.seg_start,
             a.seg_chunk, a.chunk_start, a.chunk_seg, a.chunk_key, a.counts, a.inv, a.ex_of_occ, a.sorted_ex,
-            a.vals, a.sorted_x};
+            a.vals, a.sorted_x, sort_in_tree() ? radix_sort_error(a.ws, a.n) : nullptr};
   hipLaunchKernelGGL(rle_count_kernel, dim3(ntiles), dim3(kBlock), 0, st, r);
   hipLaunchKernelGGL(rle_emit_kernel, dim3(ntiles), dim3(kBlock), 0, st, r);
   return (int)hipGetLastError();

@@ -43,6 +43,9 @@ constexpr int kMaxPieceOwners = 64;  // owners of a split backward piece
 #define FM_CHUNK_UNR 8
 #endif
 constexpr int kChunkUnr = FM_CHUNK_UNR;
+#ifndef FM_R1_MASK
+#define FM_R1_MASK 1
+#endif
 // The local kernels' 32-lane rows (k = 128): 12 r1 rows in flight per lane.  Same-box A/B
 // (profiles/r4/chunk_unr_ab.txt): k128 fp8 FTRL 0.874 -> 0.807 ms with 12, 0.856 with 16; 16-lane and
 // 4-lane rows (k64 / k16) lose with 12 or 16 (k64 fp32 0.615 -> 0.625-0.640), and so does the
@@ -173,8 +176,7 @@ __device__ inline void bwd_finish_local(const BwdArgs& a, int t, bool tact, RowS
   for (int k = 0; k < EPL; ++k) gr[k] = A[k] - Scx * r.vv[k] + nreg_v * r.vv[k];
   const float gw = Sc + nreg_w * r.wv;
   TV* tv = reinterpret_cast<TV*>(a.v);
-#pragma unroll
-  for (int k = 0; k < EPL; ++k) opt_step(a.opt, gr[k], r.vv[k], r.st0[k], r.st1[k]);
+  opt_step_row<TV, EPL>(a.opt, gr, r.vv, r.st0, r.st1);
   store_row<LPR, TV>(row_ptr(tv, r.row, a.v_stride) + t * EPL, r.vv, a.w, r.row, a.w_stride, t, tact, sr);
   if (tact) {
     store_state<TV, EPL>(state_row<TV>(a.s0v, r.row, a.s_stride), t * EPL, r.st0, sr ? sr ^ kSrSalt0 : 0u,
@@ -184,7 +186,7 @@ __device__ inline void bwd_finish_local(const BwdArgs& a, int t, bool tact, RowS
                            (uint32_t)r.row, (uint32_t)(t * EPL));
   }
   if (t == 0) {
-    opt_step(a.opt, gw, r.wv, r.q0, r.q1);
+    opt_step_tv<TV>(a.opt, gw, r.wv, r.q0, r.q1);
     row_ptr(a.w, r.row, a.w_stride)[0] = r.wv;
     a.s0w[(uint32_t)r.row] = r.q0;
     if (a.s1w) a.s1w[(uint32_t)r.row] = r.q1;
@@ -254,8 +256,7 @@ __device__ inline void bwd_finish_emit(const BwdArgs& a, int u, int t, bool tact
   }
   // exclusive own row: the optimizer in place on this rank's table
   TV* tv = reinterpret_cast<TV*>(const_cast<void*>(a.self.v));
-#pragma unroll
-  for (int k = 0; k < EPL; ++k) opt_step(a.opt, gr[k], r.vv[k], r.st0[k], r.st1[k]);
+  opt_step_row<TV, EPL>(a.opt, gr, r.vv, r.st0, r.st1);
   store_row<LPR, TV>(row_ptr(tv, r.row, a.self.v_stride) + t * EPL, r.vv, a.self.w, r.row, a.self.w_stride, t, tact,
                      sr);
   if (tact) {
@@ -266,7 +267,7 @@ __device__ inline void bwd_finish_emit(const BwdArgs& a, int u, int t, bool tact
                            (uint32_t)r.row, (uint32_t)(t * EPL));
   }
   if (t == 0) {
-    opt_step(a.opt, gw, r.wv, r.q0, r.q1);
+    opt_step_tv<TV>(a.opt, gw, r.wv, r.q0, r.q1);
     row_ptr(a.self.w, r.row, a.self.w_stride)[0] = r.wv;
     a.s0w[(uint32_t)r.row] = r.q0;
     if (a.s1w) a.s1w[(uint32_t)r.row] = r.q1;
@@ -348,8 +349,7 @@ __device__ inline void bwd_finish(const BwdArgs& a, int u, int t, bool tact, Row
   TV* tv = reinterpret_cast<TV*>(own ? const_cast<void*>(a.self.v) : a.v);
   float* tw = own ? a.self.w : a.w;
   const long long tvs = own ? a.self.v_stride : a.v_stride, tws = own ? a.self.w_stride : a.w_stride;
-#pragma unroll
-  for (int k = 0; k < EPL; ++k) opt_step(a.opt, gr[k], r.vv[k], r.st0[k], r.st1[k]);
+  opt_step_row<TV, EPL>(a.opt, gr, r.vv, r.st0, r.st1);
   store_row<LPR, TV>(tv + r.row * tvs + t * EPL, r.vv, tw, r.row, tws, t, tact, sr);
   if (tact) {
     const long long off = r.row * a.s_stride + t * EPL;
@@ -358,7 +358,7 @@ __device__ inline void bwd_finish(const BwdArgs& a, int u, int t, bool tact, Row
       store_state<TV, EPL>(a.s1v, off, r.st1, sr ? sr ^ kSrSalt1 : 0u, (uint32_t)r.row, (uint32_t)(t * EPL));
   }
   if (t == 0) {
-    opt_step(a.opt, gw, r.wv, r.q0, r.q1);
+    opt_step_tv<TV>(a.opt, gw, r.wv, r.q0, r.q1);
     tw[r.row * tws] = r.wv;
     a.s0w[r.row] = r.q0;
     if (a.s1w) a.s1w[r.row] = r.q1;
@@ -429,6 +429,18 @@ __device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
   auto r1_at = [&](int ex, float (&o)[EPL]) {
     if constexpr (FAST) load_r1<TV, EPL>(r1b + ((uint32_t)ex * r1rb + r1cb), 0, o);
     else load_r1<TV, EPL>(a.r1, (long long)ex * a.Kp + tE * EPL, o);
+  };
+  // the r1 row of an occurrence slot only where the slot holds one (its c is 0 otherwise): the unused
+  // slots of the 4-slot short block -- 275k of a Criteo-shaped batch's 378k rows occur once -- issue no
+  // load (FM_R1_MASK=0: every slot loads its lane's clamped row, the A/B).  (Masking the UNR blocks'
+  // tails as well took the 32-lane fp8 kernel over 128 VGPRs into spills.)
+  auto r1_at_if = [&](bool need, int ex, float (&o)[EPL]) {
+    if (!FM_R1_MASK || need) {
+      r1_at(ex, o);
+    } else {
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) o[k] = 0.f;
+    }
   };
   // split-backward piece: this piece's chunk ranges (one per owner) and their prefix sums
   __shared__ int pr_start[PCW ? kMaxPieceOwners : 1], pr_pre[PCW ? kMaxPieceOwners + 1 : 1];
@@ -561,7 +573,7 @@ __device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
       for (int uu = 0; uu < U4; ++uu) {
         int ex;
         occ(0, uu, uu < len, ex, cc[uu], xx[uu]);
-        r1_at(ex, rr[uu]);
+        r1_at_if(uu == 0 || uu < len, ex, rr[uu]);
       }
 #pragma unroll
       for (int uu = 0; uu < U4; ++uu) {
@@ -690,12 +702,13 @@ __device__ inline void bwd_combine_body(const BwdArgs& a, int blk, int nblk, uin
 }
 
 // Hot rows: one workgroup per row. Lane group q of the workgroup sums chunks
-// c0+q, c0+q+NG, ... ; the NG group sums are reduced in LDS in group order.
-template <int LPR, typename TV>
+// c0+q, c0+q+NG, ... ; the NG group sums are reduced in LDS in group order.  (1024-thread workgroups
+// for the 32-lane rows' hot-row launch measured slower: k128 fp8 FTRL 78 -> 116 us in-step, round 6.)
+template <int LPR, typename TV, int WPB = kWavesPerBlock>
 __device__ inline void bwd_big_body(const BwdArgs& a, int blk, int nblk, uint32_t sr) {
   constexpr int EPL = Frag<TV>::N;
   constexpr int G = kWave / LPR;
-  constexpr int NG = kWavesPerBlock * G;
+  constexpr int NG = WPB * G;
   constexpr int ROW = LPR * EPL + 4;  // LDS floats per group sum (>= Kp + 2)
   __shared__ float lds[NG * ROW];
   const int lane = threadIdx.x & (kWave - 1);

@@ -25,6 +25,12 @@ constexpr int kChunkSegMask = (1 << 30) - 1;
 constexpr int kChunkFirst = 1 << 30;         // first chunk of its segment
 constexpr unsigned kChunkSingle = 1u << 31;  // the segment's only chunk
 
+// Sticky device error word (one per device; bits below), set by kernels that detect an invalid result
+// they cannot signal otherwise without a host sync; read and cleared by the host
+// (module device_errors(), ops/kernels.py check_device_errors).
+constexpr int kDevErrSort = 1;  // in-tree radix sort: a look-back spin bound was hit (dedup plan invalid)
+__device__ int g_fm_dev_error = 0;
+
 enum LossType : int { kLossNone = 0, kLossMse = 1, kLossLogistic = 2 };
 enum OptType : int { kOptAdagrad = 0, kOptFtrl = 1, kOptSgd = 2 };
 enum DType : int { kF32 = 0, kBF16 = 1, kFP8 = 2 };
@@ -53,6 +59,26 @@ __device__ inline uint32_t sr_hash(uint32_t seed, uint32_t row, uint32_t col) {
 __device__ inline uint32_t sr_next(uint32_t r) {
   r ^= r << 13; r ^= r >> 17; r ^= r << 5;
   return r;
+}
+
+// fp8 tables (factors with 3 mantissa bits, bf16 optimizer state) take a cheaper row-update
+// epilogue: FTRL's square roots and divides on v_sqrt / v_rcp (1 ulp) instead of the correctly
+// rounded expansions, and the stochastic-rounding words of a lane's 4 values as rotations of ONE
+// hash instead of a hash plus a 3-step xorshift chain (each rotation's bits are uniform on their
+// own, which is all an unbiased rounding needs).  The k128 fp8 FTRL chunk backward is VALU-bound
+// with its per-row epilogue as large as its occurrence loop (profiles/r6/fp8_epilogue_ab.txt).
+// FM_FP8_FAST_EPI=0 (build variant "fp8slow") keeps the exact forms: the A/B.
+#ifndef FM_FP8_FAST_EPI
+#define FM_FP8_FAST_EPI 1
+#endif
+__device__ inline uint32_t sr_rot(uint32_t x, int s) { return __builtin_amdgcn_alignbit(x, x, s); }
+// random word i (0..3) of a lane's 4 values from one hash
+__device__ inline uint32_t sr_word(uint32_t r0, int i) {
+  if (!FM_FP8_FAST_EPI) {
+    for (int k = 0; k < i; ++k) r0 = sr_next(r0);
+    return r0;
+  }
+  return i == 0 ? r0 : sr_rot(r0, i == 1 ? 16 : i == 2 ? 8 : 24);
 }
 
 // A computed address (e.g. broadcast between lanes) as a global-memory pointer: without the
@@ -182,11 +208,11 @@ template <> struct Frag<fp8e4m3> {
   // gfx950 v_cvt_sr_fp8_f32: hardware stochastic rounding with the given random bits
   __device__ static inline int store_sr(fp8e4m3* p, const float (&o)[4], uint32_t seed, uint32_t row,
                                         uint32_t col) {
-    const uint32_t r0 = sr_hash(seed, row, col), r1 = sr_next(r0), r2 = sr_next(r1), r3 = sr_next(r2);
+    const uint32_t r0 = sr_hash(seed, row, col);
     int u = __builtin_amdgcn_cvt_sr_fp8_f32(o[0], (int)r0, 0, 0);
-    u = __builtin_amdgcn_cvt_sr_fp8_f32(o[1], (int)r1, u, 1);
-    u = __builtin_amdgcn_cvt_sr_fp8_f32(o[2], (int)r2, u, 2);
-    u = __builtin_amdgcn_cvt_sr_fp8_f32(o[3], (int)r3, u, 3);
+    u = __builtin_amdgcn_cvt_sr_fp8_f32(o[1], (int)sr_word(r0, 1), u, 1);
+    u = __builtin_amdgcn_cvt_sr_fp8_f32(o[2], (int)sr_word(r0, 2), u, 2);
+    u = __builtin_amdgcn_cvt_sr_fp8_f32(o[3], (int)sr_word(r0, 3), u, 3);
     *reinterpret_cast<int*>(p) = u;
     return u;
   }
@@ -291,12 +317,9 @@ __device__ inline void store_state(void* s, long long off, const float (&o)[EPL]
     for (int k = 0; k < EPL; k += 4) {
       uint32_t b[4];
       if (seed) {
-        uint32_t r = sr_hash(seed, row, col + (uint32_t)k);
+        const uint32_t r = sr_hash(seed, row, col + (uint32_t)k);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          b[i] = f32_to_bf16_bits_sr(o[k + i], r);
-          r = sr_next(r);
-        }
+        for (int i = 0; i < 4; ++i) b[i] = f32_to_bf16_bits_sr(o[k + i], sr_word(r, i));
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) b[i] = f32_to_bf16_bits(o[k + i]);
@@ -430,6 +453,53 @@ __device__ inline void opt_step(const OptParams& o, float g, float& p, float& s0
     p = fabsf(s1) > o.l1 ? (copysignf(o.l1, s1) - s1) / quad : 0.f;
   } else {
     p -= o.lr * g;
+  }
+}
+
+// The same step for a table of dtype TV: fp8 tables on the hardware square root / reciprocal
+// (FM_FP8_FAST_EPI, above).  Every writer of a table row (in-place backward, owner apply, dense
+// apply) goes through this, so a row gets the same bits whichever path updates it.
+template <typename TV>
+__device__ inline void opt_step_tv(const OptParams& o, float g, float& p, float& s0, float& s1) {
+  if constexpr (FM_FP8_FAST_EPI && StateBf16<TV>::v) {
+    if (o.type == kOptFtrl) {
+      const float ilr = __builtin_amdgcn_rcpf(o.lr);  // (wave-uniform: hoisted by the compiler)
+      const float n_new = __builtin_fmaf(g, g, s0);
+      const float sq_old = __builtin_amdgcn_sqrtf(s0), sq_new = __builtin_amdgcn_sqrtf(n_new);
+      s1 += g - (sq_new - sq_old) * ilr * p;
+      s0 = n_new;
+      const float quad = __builtin_fmaf(o.beta + sq_new, ilr, 2.f * o.l2);
+      p = fabsf(s1) > o.l1 ? (copysignf(o.l1, s1) - s1) * __builtin_amdgcn_rcpf(quad) : 0.f;
+      return;
+    }
+    if (o.type == kOptAdagrad) {
+      s0 = __builtin_fmaf(g, g, s0);
+      p -= o.lr * g * __builtin_amdgcn_rsqf(s0);
+      return;
+    }
+  }
+  opt_step(o, g, p, s0, s1);
+}
+
+// A lane's N elements of one row: the optimizer switch taken once per row, not per element, so the
+// elements' dependency chains interleave (the per-element form compiled to a scalar branch ladder per
+// element).  Same per-element arithmetic as opt_step_tv: bitwise the same results.
+template <typename TV, int N>
+__device__ inline void opt_step_row(const OptParams& o, const float (&g)[N], float (&p)[N], float (&s0)[N],
+                                    float (&s1)[N]) {
+  if (o.type == kOptFtrl) {
+    OptParams f = o;
+    f.type = kOptFtrl;
+#pragma unroll
+    for (int k = 0; k < N; ++k) opt_step_tv<TV>(f, g[k], p[k], s0[k], s1[k]);
+  } else if (o.type == kOptAdagrad) {
+    OptParams f = o;
+    f.type = kOptAdagrad;
+#pragma unroll
+    for (int k = 0; k < N; ++k) opt_step_tv<TV>(f, g[k], p[k], s0[k], s1[k]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < N; ++k) p[k] -= o.lr * g[k];
   }
 }
 

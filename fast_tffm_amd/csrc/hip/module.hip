@@ -202,6 +202,20 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("keys"), py::arg("vals"), py::arg("kout"), py::arg("vout"), py::arg("n"), py::arg("end_bit"),
       py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"));
   m.def("radix_sort_ws_bytes", &fm::radix_sort_ws_bytes, py::arg("n"));
+  m.def("set_sort_spin_cap", &fm::set_sort_spin_cap, py::arg("cap"));  // (< 0: injected look-back failure)
+  m.def(
+      "device_errors",  // the current device's sticky error word (synchronous), cleared when `clear`
+      [](bool clear) {
+        int v = 0;
+        check((int)hipDeviceSynchronize(), "device_errors sync");
+        check((int)hipMemcpyFromSymbol(&v, HIP_SYMBOL(fm::g_fm_dev_error), sizeof(int)), "device_errors read");
+        if (clear && v) {
+          const int z = 0;
+          check((int)hipMemcpyToSymbol(HIP_SYMBOL(fm::g_fm_dev_error), &z, sizeof(int)), "device_errors clear");
+        }
+        return v;
+      },
+      py::arg("clear") = false);
   m.def(
       "dedup",
       [](int n, int end_bit, int CH, u64 keys, u64 payload, u64 skeys, u64 spay, u64 uniq, u64 seg_start,

@@ -18,7 +18,9 @@
 // tile's digit-d elements keep element order: the sort is stable and its output is bitwise what any
 // stable sort produces (tests/test_radix_sort_gpu.py, tools/bench_fmsort.hip against rocPRIM).
 // Memory per pass: keys and values read once and written once (+ the keys once for all passes).
-// Spins are bounded (an error word in the workspace instead of a hang).
+// Spins are bounded (an error word in the workspace instead of a hang); dedup.hip carries that word into
+// the dedup's counts[7] and the module's sticky device error word (g_fm_dev_error), which the host
+// checks (ops/kernels.py check_device_errors: bench, trainer log points, DedupOut.sync).
 // (Included by module.hip inside namespace fm.)
 
 constexpr int kRsThreads = 512;                   // threads per tile block
@@ -84,6 +86,10 @@ constexpr unsigned kOsAgg = 1u << 30, kOsInc = 2u << 30, kOsCnt = (1u << 30) - 1
 constexpr int kOsMaxPasses = 4;
 constexpr int kOsHistBlocks = 1024;
 constexpr int kOsSpinCap = 1 << 20;
+// look-back spin bound of the pass kernels (set_sort_spin_cap; < 0: every tile but the first reports
+// the error without waiting -- the tests' fault injection)
+static int g_os_spin_cap = kOsSpinCap;
+void set_sort_spin_cap(int cap) { g_os_spin_cap = cap; }
 #ifndef FM_OS_LOOKBACK
 #define FM_OS_LOOKBACK 4
 #endif
@@ -183,6 +189,7 @@ struct OsPass {
   unsigned* status;       // [ntiles][D]
   int* tile_ctr;
   int* err;
+  int spin_cap;
   const int* offsets;  // RsSrc::offsets (first pass only: generated payload)
   int B, code_shift;
 };
@@ -282,6 +289,7 @@ __global__ __launch_bounds__(kRsThreads) void os_pass_kernel(OsPass o) {
   const unsigned tstart = (unsigned)ex2, gbase = (unsigned)(ex2 >> 32);
   // look-back: thread d walks back over the tiles before this one, kOsLookback per round
   unsigned excl = 0;
+  if (d < D && tile > 0 && o.spin_cap < 0) atomicOr(o.err, 1);  // (injected failure: tests)
   if (d < D && tile > 0) {
     int t = tile - 1;
     for (int round = 0; t >= 0; ++round) {
@@ -306,7 +314,7 @@ __global__ __launch_bounds__(kRsThreads) void os_pass_kernel(OsPass o) {
       }
       if (stop) break;
       if (wait) {
-        if (round >= kOsSpinCap) {
+        if (round >= o.spin_cap) {
           atomicOr(o.err, 1);
           break;
         }
@@ -373,11 +381,12 @@ size_t radix_sort_ws_bytes(int n) {
 }
 
 // Stable sort of (keys[i], vals[i]) by keys' bits [0, end_bit) into (kout, vout); keys / vals are
-// not modified.  0 or a hip error code; -2: workspace too small.  radix_sort_error(ws, n) locates the
+// not modified.  0 or a hip error code; -2: workspace too small; -5: n >= 2^30.  radix_sort_error(ws, n) locates the
 // look-back error word (nonzero: a spin bound was hit, the output is not valid).
 int launch_radix_sort(const uint32_t* keys, const int* vals, uint32_t* kout, int* vout, int n, int end_bit,
                       void* ws, size_t ws_bytes, hipStream_t st, const RsSrc& src = RsSrc()) {
   if (n <= 0) return 0;
+  if ((unsigned)n > kOsCnt) return -5;  // (look-back words hold 30-bit prefixes)
   if (ws_bytes < radix_sort_ws_bytes(n)) return -2;
   if ((src.ids && (src.W < 1 || src.Rps < 0)) || (src.offsets && (src.B < 1 || src.code_shift < 0))) return -4;
   end_bit = end_bit < 1 ? 1 : (end_bit > 32 ? 32 : end_bit);
@@ -414,7 +423,7 @@ int launch_radix_sort(const uint32_t* keys, const int* vals, uint32_t* kout, int
     const uint32_t dmask = bits >= 32 ? 0xffffffffu : (1u << bits) - 1u;
     RsPass p{n, ntiles, shift, dmask, kin, vin, to_out ? kout : alt_k, to_out ? vout : alt_v};
     OsPass o{p, hist + (size_t)i * D, status + (size_t)i * ntiles * D, ctr + i, ctr + kOsMaxPasses,
-             src.offsets, src.B, src.code_shift};
+             g_os_spin_cap, src.offsets, src.B, src.code_shift};
     const bool gen = i == 0 && src.offsets;
     if (db == 9) {
       if (gen) hipLaunchKernelGGL((os_pass_kernel<9, true>), dim3(ntiles), dim3(kRsThreads), 0, st, o);

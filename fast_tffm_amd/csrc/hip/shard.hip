@@ -222,8 +222,7 @@ struct RowUpdate {
 
   __device__ inline void step_store(const ApplyArgs& a, const float (&gr)[EPL], float gw, long long row, int t,
                                     bool tact, uint32_t sr) {
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) opt_step(a.opt, gr[k], vv[k], st0[k], st1[k]);
+    opt_step_row<TV, EPL>(a.opt, gr, vv, st0, st1);
     store_row<LPR, TV>(vrow, vv, a.w, row, a.w_stride, t, tact, sr);
     if (tact) {
       const uint32_t col = (uint32_t)(t * EPL);
@@ -231,7 +230,7 @@ struct RowUpdate {
       if (a.s1v) store_state<TV, EPL>(a.s1v, soff, st1, sr ? sr ^ kSrSalt1 : 0u, (uint32_t)row, col);
     }
     if (t == 0) {
-      opt_step(a.opt, gw, pw, q0, q1);
+      opt_step_tv<TV>(a.opt, gw, pw, q0, q1);
       a.w[row * a.w_stride] = pw;
       a.s0w[row] = q0;
       if (a.s1w) a.s1w[row] = q1;

@@ -318,7 +318,12 @@ class DedupOut:
 
     def sync(self) -> int:
         if self.U_host is None:
-            self.U_host = int(self.num_unique.item())
+            # counts[7]: the in-tree sort's look-back verdict (nonzero: this grouping is invalid)
+            u, err = self.counts[0:8:7].tolist() if self.counts.numel() >= 8 else (int(self.num_unique.item()), 0)
+            if err:
+                raise RuntimeError(f"dedup: the radix sort's look-back spin bound was hit (error word {err}); "
+                                   "this batch's grouping is invalid")
+            self.U_host = int(u)
         return self.U_host
 
     def unique_keys(self) -> torch.Tensor:
@@ -354,6 +359,55 @@ class DedupWorkspace:
             self.ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
         else:
             self.ws = None
+
+
+DEV_ERR_SORT = 1  # hip/fm_common.h kDevErrSort
+
+
+def check_device_errors(device: torch.device | None = None, clear: bool = True) -> None:
+    """Raise if a kernel on ``device`` (default: the current GPU) flagged an invalid result in the
+    module's sticky error word since the last check (synchronises the device).  Kernels that cannot
+    fail loudly without a host sync set it -- the in-tree radix sort when a look-back spin bound is
+    hit -- and the bench / trainer check it at their reporting points.  No-op without a GPU."""
+    if device is not None and device.type != "cuda":
+        return
+    if not torch.cuda.is_available() or not torch.cuda.is_initialized():
+        return
+    with torch.cuda.device(device if device is not None else torch.cuda.current_device()):
+        err = int(native.hip().device_errors(clear))
+    if err:
+        what = ["radix sort look-back spin bound hit (a dedup plan was invalid)"] if err & DEV_ERR_SORT else []
+        raise RuntimeError(f"device error word {err:#x}: {'; '.join(what) or 'unknown'}")
+
+
+_SORT_CHECKED: set = set()
+
+
+def _sort_selfcheck(dev: torch.device) -> None:
+    """Once per device and process, before the in-tree sort first groups a batch: its passes are
+    stable only if the LDS returns ds_add_rtn ranks in ascending lane order for lanes of one
+    instruction that hit the same counter (radix_sort.hip rs_rank_wave) -- measured on gfx950, not
+    documented.  Sort a digit-colliding pattern against torch's stable sort; on a mismatch switch the
+    dedup to rocPRIM's sort (bitwise the same order) and warn."""
+    if dev.index in _SORT_CHECKED or torch.cuda.is_current_stream_capturing():
+        return
+    _SORT_CHECKED.add(dev.index)
+    h = native.hip()
+    if not h.sort_algo():
+        return
+    g = torch.Generator(device="cpu").manual_seed(7)
+    n = 3 * 8192 + 77  # several tiles, a partial last one
+    keys = (torch.randint(0, 6, (n,), generator=g) * 0x01010101 + torch.randint(0, 2, (n,), generator=g)).to(
+        torch.int32).to(dev)  # every digit of every pass collides heavily
+    vals = torch.arange(n, dtype=torch.int32, device=dev)
+    ko, vo = radix_sort(keys, vals, key_bits=32)
+    ref_k, ref_v = torch.sort(keys.long(), stable=True)
+    if not (torch.equal(ko.long(), ref_k) and torch.equal(vo, ref_v.to(torch.int32))):
+        import warnings
+
+        h.set_sort_algo(0)
+        warnings.warn("in-tree radix sort failed its stability self-check on this device: the dedup uses "
+                      "rocPRIM's sort (FM_SORT=rocprim)")
 
 
 def set_sort_algo(algo: str) -> str:
@@ -479,6 +533,7 @@ def dedup(keys: torch.Tensor, *, ws: DedupWorkspace | None = None, key_bits: int
     if _is_gpu(keys):
         h = native.hip()
         _check(1 <= CH <= h.MAX_CH, f"CH must be in [1, {h.MAX_CH}]")
+        _sort_selfcheck(dev)
         h.dedup(n=n, end_bit=key_bits, CH=CH, keys=_p(keys), payload=_p(ex_of_occ if ex_payload else ws.iota),
                 skeys=_p(ws.skeys), spay=_p(ws.perm), uniq=_p(ws.uniq), seg_start=_p(ws.seg_start),
                 seg_chunk=_p(ws.seg_chunk), chunk_start=_p(ws.chunk_start), chunk_seg=_p(ws.chunk_seg),

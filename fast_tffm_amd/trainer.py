@@ -31,6 +31,7 @@ from .utils.fault import maybe_inject
 from .utils.trace import roctx_range
 from .data.reader import NativeTextReader, Prefetcher, ReaderState, TextBatchReader, load_file_batch
 from .models.fm import FactorizationMachine
+from .ops.kernels import check_device_errors
 from .parallel.dist import DistContext
 from .utils import checkpoint as ckpt
 from .utils.metrics import MetricsLogger
@@ -254,6 +255,7 @@ class Trainer:
                     if c.tolerance is not None and v_loss < c.tolerance:
                         self.print("Loss on validation data set is below tolerance. Training completed.")
                         ended_early = True
+                check_device_errors(self.device)  # (kernels' sticky error word: fail before saving)
                 if c.log_dir:
                     self.save()
             maybe_inject(step_num, self.rank)
@@ -268,6 +270,7 @@ class Trainer:
         pf.close()
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
+        check_device_errors(self.device)
         total = time.time() - st
         speed = (step_num - start_step) * c.batch_size * self.world / max(total, 1e-9)
         self.print("Average speed: ", speed, " ex/s")

@@ -126,3 +126,41 @@ def test_dedup_fused_shard_keys(algo, misalign):
     assert torch.equal(buf, keys_ref)
     for a, c in zip(ref, got):
         assert torch.equal(a, c)
+
+
+def test_lookback_failure_is_loud():
+    """A look-back that hits its spin bound (injected: spin cap < 0) must not pass silently: the
+    dedup's counts[7] makes DedupOut.sync raise, and the sticky device word makes
+    check_device_errors raise (the bench / trainer reporting points); cleared, the next plan is fine."""
+    from fast_tffm_amd.ops import native
+
+    h = native.hip()
+    was = K.set_sort_algo("fm")
+    keys = _keys(100_000, 24, seed=5)
+    K.dedup(keys.clone(), key_bits=24).sync()  # (first use: the sort's self-check runs outside the injection)
+    K.check_device_errors()  # (clean start)
+    try:
+        h.set_sort_spin_cap(-1)
+        dd = K.dedup(keys.clone(), key_bits=24)
+        with pytest.raises(RuntimeError, match="spin bound"):
+            dd.sync()
+        with pytest.raises(RuntimeError, match="radix sort"):
+            K.check_device_errors()
+        K.check_device_errors()  # cleared by the raising check
+    finally:
+        h.set_sort_spin_cap(1 << 20)
+        K.set_sort_algo(was)
+    dd = K.dedup(keys.clone(), key_bits=24)
+    assert dd.sync() == int(torch.unique(keys).numel())
+    K.check_device_errors()
+
+
+def test_radix_sort_rejects_oversized_n():
+    """n >= 2^30 would overflow the 30-bit look-back prefixes: the launcher refuses it (no launch)."""
+    from fast_tffm_amd.ops import native
+
+    h = native.hip()
+    t = torch.empty(1, dtype=torch.int32, device="cuda")
+    with pytest.raises(RuntimeError, match="code -5"):
+        h.radix_sort(keys=t.data_ptr(), vals=t.data_ptr(), kout=t.data_ptr(), vout=t.data_ptr(), n=(1 << 30) + 1,
+                     end_bit=32, ws=t.data_ptr(), ws_bytes=1 << 62, stream=torch.cuda.current_stream().cuda_stream)
