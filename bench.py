@@ -86,6 +86,9 @@ def main() -> int:
                     help="row-sharded step: split backward, first half's gradient rows sent early (auto: off)")
     ap.add_argument("--comm-dtype", default="auto", choices=["auto", "fp32", "bf16"],
                     help="row-sharded wire rows (auto = table storage dtype; bf16 rounds fp32 rows for transport)")
+    ap.add_argument("--staleness", type=int, default=0, choices=[0, 1],
+                    help="row-sharded step: 0 = synchronous (default), 1 = bounded staleness (the reference's "
+                         "asynchronous updates, deterministic: rows read one step stale, exchange + apply overlap)")
     ap.add_argument("--stochastic-rounding", default="on", choices=["on", "off"],
                     help="bf16 / fp8 tables: stochastically rounded row stores (the training default)")
     ap.add_argument("--profile-steps", type=int, default=0, help="also emit a torch.profiler trace")
@@ -120,7 +123,8 @@ def main() -> int:
     cfg = FMConfig(vocabulary_size=vocab, factor_num=p["k"], loss_type="logistic", batch_size=a.batch,
                    init_value_range=0.01, seed=42, dtype=dtype, opt=opt, mode=mode, comm_dtype=a.comm_dtype,
                    microbatches=a.microbatches, prefetch_rows=a.prefetch_rows,
-                   overlap_grads=a.overlap_grads, stochastic_rounding=a.stochastic_rounding == "on")
+                   overlap_grads=a.overlap_grads, stochastic_rounding=a.stochastic_rounding == "on",
+                   staleness=a.staleness)
     t0 = time.time()
     model = FactorizationMachine(cfg, device=dev, dist=ctx if W > 1 or mode not in ("auto", "local") else None)
     if dev.type == "cuda":
@@ -248,6 +252,7 @@ def main() -> int:
                 "early_rows": bool(model._exchange.prefetch) if model.mode == "shard" else None,
                 "split_grads": bool(model._exchange.overlap_grads) if model.mode == "shard" else None,
                 "comm": getattr(model._exchange, "comm_mode", None),
+                "staleness": getattr(model._exchange, "staleness", 0) if model.mode == "shard" else None,
                 "seg_lookup": K.seg_lookup_enabled() if model.mode == "shard" else None,
                 "lookahead": (2 if os.environ.get("FM_LOCAL_DEPTH2", "1") != "0" and len(pool) > 2 else 1)
                 if model.mode == "local" and dev.type == "cuda" and not graphed else None,

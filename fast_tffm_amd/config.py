@@ -29,7 +29,10 @@ Extensions (new keys, all optional):
                 microbatches = 1|2|... (row-sharded step parts overlapping the exchange; default 1),
                 prefetch_rows = auto|on|off (exchange the next step's rows early, re-send updated ones),
                 overlap_grads = auto|on|off (split backward; first half's gradients sent while the rest runs;
-                                auto = on with one microbatch)
+                                auto = on with one microbatch),
+                staleness = 0|1 (row-sharded step: 0 = synchronous; 1 = bounded staleness, the reference's
+                                asynchronous updates made deterministic: step t reads every row with the
+                                gradients of steps <= t-2 applied, step t-1's exchange + apply overlap it)
 """
 
 from __future__ import annotations
@@ -113,6 +116,7 @@ class FMRunConfig:
     microbatches: int = 0
     prefetch_rows: str = "auto"
     overlap_grads: str = "auto"
+    staleness: int = 0
     config_file: str | None = None
 
     # ------------------------------------------------------------------
@@ -135,7 +139,7 @@ class FMRunConfig:
                                "fp8": torch.float8_e4m3fn}[self.dtype], opt=opt, mode=self.mode,
                         grad_reduce=self.grad_reduce, comm_dtype=self.comm_dtype, microbatches=self.microbatches,
                         prefetch_rows=self.prefetch_rows,
-                        overlap_grads=self.overlap_grads,
+                        overlap_grads=self.overlap_grads, staleness=self.staleness,
                         stochastic_rounding=self.stochastic_rounding, dedup_chunk=self.dedup_chunk,
                         global_bias=self.global_bias)
 
@@ -250,6 +254,9 @@ def load_config(config_file: str, *, echo: bool = True, printer=print) -> FMRunC
     c.microbatches = opt(DISTRIBUTED, "microbatches", int, c.microbatches)
     c.prefetch_rows = opt(DISTRIBUTED, "prefetch_rows", lambda s: s.strip().lower(), c.prefetch_rows)
     c.overlap_grads = opt(DISTRIBUTED, "overlap_grads", lambda s: s.strip().lower(), c.overlap_grads)
+    c.staleness = opt(DISTRIBUTED, "staleness", int, c.staleness)
     if c.comm_dtype not in ("auto", "storage", "fp32", "bf16"):
         raise ConfigError(f"[Distributed] comm_dtype must be auto, fp32 or bf16, got {c.comm_dtype}")
+    if c.staleness not in (0, 1):
+        raise ConfigError(f"[Distributed] staleness must be 0 or 1, got {c.staleness}")
     return c

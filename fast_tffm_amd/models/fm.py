@@ -71,6 +71,7 @@ class FMConfig:
     microbatches: int = 0             # row-sharded step: parts per batch overlapping the exchange (0/1 = one)
     prefetch_rows: str = "auto"       # row-sharded step: early row exchange + patch (auto = on when world > 1)
     overlap_grads: str = "auto"       # row-sharded step: split backward, first half's grads sent early (auto: on)
+    staleness: int = 0                # row-sharded step: 0 = synchronous, 1 = bounded staleness (ShardExchange)
     dedup_chunk: int = 32             # CH of the segmented backward
     threads: int = 0                  # CPU kernels (0 = OpenMP default)
     global_bias: bool = False         # learned global bias b0 (extension; the reference has none)
@@ -465,6 +466,13 @@ class FactorizationMachine:
                 out = self._local_train_step(b)
         self.global_step += 1
         return out
+
+    def flush(self) -> None:
+        """Make every training update visible in the table (bounded-staleness sharded steps apply each
+        gradient one step late: the pending one is applied now); no-op otherwise."""
+        fl = getattr(self._exchange, "flush", None)
+        if fl is not None:
+            fl()
 
     def _side_stream(self):
         if self._side is None:

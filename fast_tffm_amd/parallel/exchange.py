@@ -99,7 +99,7 @@ class _ShardPlan:
     part 1's, ...; ``run_off`` the W * parts run boundaries)."""
 
     __slots__ = ("b", "slot", "parts", "U", "R", "req_recv", "run_off", "splits", "match", "ready", "early",
-                 "train", "counts", "counts_ev", "self_u", "self_r", "self_excl")
+                 "train", "counts", "counts_ev", "self_u", "self_r", "self_excl", "sb", "pieces")
 
 
 class _Early:
@@ -270,6 +270,32 @@ class ShardExchange(_Base):
         # (profiles/r4/shard_w1_local.txt); world > 1 keeps EMIT + the exchange
         self.local_w1 = (self.self_rows and self.W == 1
                          and os.environ.get("FM_SHARD_W1_LOCAL", "1") != "0")  # (0: EMIT path, A/B)
+        # Bounded staleness (FMConfig.staleness = 1): the reference trains asynchronously -- workers push
+        # their sparse gradients to the parameter servers without waiting for each other and read
+        # whatever the servers hold (run_tffm.py:204-211, fm_model.py:345-348).  Made deterministic here:
+        # step t reads EVERY row (own rows included) as the table is with the gradients of steps <= t-2
+        # applied, gathered from the owners and exchanged during step t-1 (no dirty-row patch); step t's
+        # gradient all-to-all and the owners' apply run on their own streams beside step t+1's compute
+        # (the apply of step t-1 between the gather of step t+1's rows and the apply of step t).  The
+        # compute stream never touches the table, so no own-row shortcut (self rows, in-place updates)
+        # and no split backward.  Equal to one process applying each step's merged gradient one step late
+        # (tests/test_staleness.py).  0 = synchronous (default).
+        self.staleness = int(getattr(model.cfg, "staleness", 0) or 0)
+        if self.staleness not in (0, 1):
+            raise ValueError(f"staleness must be 0 or 1, got {self.staleness}")
+        if self.staleness:
+            if self.nparts != 1:
+                raise ValueError("staleness = 1 runs one part per batch (microbatches <= 1)")
+            self.self_rows = self.local_w1 = self.overlap_grads = False
+            self.prefetch = True
+        self._pend = None             # staleness: (plan, gradient rows, works, sr seed, bwd event) to apply
+        self.applied_ev = None        # staleness: the last enqueued apply (apply stream)
+        self._gather_ev = None        # staleness: the last gather of a step's rows (the next apply follows it)
+        self._apply_st = None
+        self._ded = None
+        self._main = None             # the compute stream of the current step (starvation check)
+        self.host_blocks = self.starved_waits = 0
+        self.host_wait_s = 0.0
         self.cur_plan: _ShardPlan | None = None
         self.step_start = None
         self.early_steps = 0          # steps that took the early-exchange + patch path
@@ -306,7 +332,10 @@ class ShardExchange(_Base):
     def close(self) -> None:
         """Wait for in-flight exchange works, drop every plan (device buffers, pinned
         staging, events) and destroy the plan communicator (dual mode) while the main
-        process group is still alive."""
+        process group is still alive.  With staleness the pending gradient is applied first (the table
+        stays complete and readable after close)."""
+        if self.staleness and self._pend is not None:
+            self.flush()
         for pl in [self.cur_plan] + list(self.pending):
             e = getattr(pl, "early", None) if pl is not None else None
             if e is not None and getattr(e, "work", None) is not None:
@@ -319,15 +348,44 @@ class ShardExchange(_Base):
         if self.comm_mode == "dual" and self.plan_group is not None and dist.is_initialized():
             dist.destroy_process_group(self.plan_group)
         self.plan_group = None
-        self._prep = None
+        self._prep = self._apply_st = self._ded = self._main = None
+        self.applied_ev = self._gather_ev = None
         super().close()
 
     def _prep_stream(self):
+        """Stream of the plan finish (id all-to-all, run offsets, early row exchange)."""
         if self._prep is None:
             from ..models.fm import side_stream
 
             self._prep = side_stream(self.dev)
         return self._prep
+
+    def _dedup_stream(self):
+        """Stream of the plan start (dedup, owner counts, count exchange): its own, so the next plan's
+        dedup never queues behind this plan's early row gather, which waits for the previous step's
+        update (one stream for both tied the count read of plan t+2 to step t's start)."""
+        if self._ded is None:
+            from ..models.fm import side_stream
+
+            self._ded = side_stream(self.dev)
+        return self._ded
+
+    def _await(self, ev) -> None:
+        """Host read of a plan's device-produced counts (pinned copy behind ``ev``).  Normally the event
+        finished long ago (no wait).  Otherwise the host blocks -- back-pressure when the host is more
+        than a step ahead, counted in ``host_blocks`` -- and, if the compute stream has run dry while the
+        host waits, in ``starved_waits`` (a host wait on the critical path)."""
+        if ev.query():
+            return
+        self.host_blocks += 1
+        main = self._main
+        if main is not None and main.query():
+            self.starved_waits += 1
+        import time
+
+        t0 = time.perf_counter()
+        ev.synchronize()
+        self.host_wait_s += time.perf_counter() - t0
 
     def _split(self, b: Batch, nparts: int) -> list[tuple[int, int, int, int]]:
         """(e0, e1, n0, n1) example / occurrence ranges of the micro-batches of ``b``."""
@@ -379,10 +437,10 @@ class ShardExchange(_Base):
         pl = _ShardPlan()
         pl.b, pl.slot, pl.train = b, idx, train
         pl.early = pl.splits = pl.run_off = pl.match = pl.ready = None
-        pl.self_u = pl.self_r = pl.self_excl = None
+        pl.self_u = pl.self_r = pl.self_excl = pl.sb = pl.pieces = None
         gpu = self.dev.type == "cuda"
         if gpu:
-            st = self._prep_stream()
+            st = self._dedup_stream()
             if slot.done is not None:
                 st.wait_event(slot.done)      # the last step that used these buffers is over
             ready = getattr(b, "ready", None) or inputs_ready
@@ -394,7 +452,7 @@ class ShardExchange(_Base):
                 if t is not None:
                     t.record_stream(st)
         ranges = self._split(b, self.nparts if train else 1)
-        with self._side_ctx():
+        with (torch.cuda.stream(st) if gpu else self._side_ctx()):
             pl.parts = []
             counts = []
             if gpu:
@@ -451,7 +509,8 @@ class ShardExchange(_Base):
         slot = self.slots[pl.slot]
         with self._side_ctx():
             if pl.counts_ev is not None:  # GPU: both count matrices exchanged on the device
-                pl.counts_ev.synchronize()
+                torch.cuda.current_stream(self.dev).wait_event(pl.counts_ev)  # (the dedup stream's outputs)
+                self._await(pl.counts_ev)
                 sc, rc = pl.counts[0].clone(), pl.counts[1].clone()
             else:
                 sc = pl.counts.clone()
@@ -496,6 +555,8 @@ class ShardExchange(_Base):
                     if self.W > 1 and part.rc[me]:
                         pl.self_excl = K.self_excl(pl.req_recv, self.W, pl.run_off, me, part.rc[me],
                                                    slot.excl_buf(part.rc[me], self.dev))
+            if pl.train and self._split_ok(pl, None):
+                self._split_plan(pl)
             if early and pl.train and self._early_ok(pl, self.cur_plan):
                 pl.early = self._early(pl, self.cur_plan)
             if gpu:
@@ -504,6 +565,8 @@ class ShardExchange(_Base):
 
     def _early_ok(self, pl: _ShardPlan, cur: _ShardPlan | None) -> bool:
         gpu = self.dev.type == "cuda"
+        if self.staleness:  # (no dirty scan against the current plan: every row is read stale)
+            return pl.train and len(pl.parts) == 1 and pl.splits is not None and (pl.run_off is not None or not gpu)
         if self.local_w1 or (pl.self_r is not None and pl.self_r[1] - pl.self_r[0] == pl.R):
             return False  # every request is this rank's own row (world 1): nothing to exchange early
         return (self.prefetch and len(pl.parts) == 1 and pl.splits is not None and cur is not None
@@ -511,7 +574,189 @@ class ShardExchange(_Base):
                 and (pl.run_off is not None or not gpu))
 
     def _early(self, pl: _ShardPlan, cur: _ShardPlan) -> _Early:
+        if self.staleness:
+            return self._early_stale(pl)
         return self._early_gpu(pl, cur) if self.dev.type == "cuda" else self._early_cpu(pl, cur)
+
+    # ---- bounded staleness -------------------------------------------------------------------
+    def _note_gather(self) -> None:
+        """Staleness: the gather of a step's rows was enqueued on the current stream; the next apply
+        (step t-1's, when these are step t's rows) must follow it."""
+        if self.dev.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.dev))
+            self._gather_ev = ev
+
+    def _early_stale(self, pl: _ShardPlan) -> _Early:
+        """Staleness: every row ``pl`` requests (own rows included), gathered from the table as it is after
+        the apply enqueued last -- step t-1's, when ``pl`` is step t+1's plan -- and before the next one,
+        and exchanged now, on the plan stream and communicator; no dirty rows, no patch."""
+        dev, W = self.dev, self.W
+        gpu = dev.type == "cuda"
+        part = pl.parts[0]
+        e = _Early()
+        e.work = e.rows_send = e.didx = e.sc_start = e.dsend = e.ev = None
+        if gpu and self.applied_ev is not None:
+            torch.cuda.current_stream(dev).wait_event(self.applied_ev)
+        rows_send = self.wire.empty(pl.R, dev)
+        K.gather_wire(pl.req_recv[: pl.R], self.m.table.state, self.wire, rows_send, threads=self.m.cfg.threads)
+        self._note_gather()
+        if W == 1:
+            e.gathered = rows_send
+            return e
+        e.gathered = self.wire.empty(pl.U, dev)
+        if gpu:
+            e.rows_send = rows_send
+            e.work = dist.all_to_all_single(e.gathered, rows_send, part.sc, part.rc, group=self.plan_group,
+                                            async_op=True)
+        else:
+            _a2a(e.gathered, rows_send, part.sc, part.rc, self.plan_group)
+        self.bytes_sent += self.wire.rb * self._to_others(part.rc)
+        return e
+
+    def _apply_stream(self):
+        if self._apply_st is None:
+            from ..models.fm import side_stream
+
+            self._apply_st = side_stream(self.dev)
+        return self._apply_st
+
+    def _apply_pending(self) -> None:
+        """Staleness: enqueue the owners' apply of the pending (previous step's) gradient rows on the apply
+        stream, behind the last gather of a step's rows (they keep the table as it was before this apply)
+        and behind the gradient all-to-all; its event gates the next gather and the plan slot's reuse."""
+        p, self._pend = self._pend, None
+        if p is None:
+            return
+        pl, grad_recv, works, sr, bwd_ev = p
+        m, cfg = self.m, self.m.cfg
+        gpu = self.dev.type == "cuda"
+        if gpu:
+            st = self._apply_stream()
+            cm = torch.cuda.stream(st)
+        else:
+            import contextlib
+
+            cm = contextlib.nullcontext()
+        with cm:
+            if gpu:
+                st.wait_event(bwd_ev)                # (world 1: no all-to-all orders it after the backward)
+                if self._gather_ev is not None:
+                    st.wait_event(self._gather_ev)
+            for w in works:
+                w.wait()                             # GPU: this stream waits for the communicator's
+            with roctx_range("apply_stale"):
+                K.apply_runs(pl.req_recv, pl.run_off, pl.splits, grad_recv, m.table.state, cfg.opt, self.Kp,
+                             match=pl.match, threads=cfg.threads,
+                             ws=self.slots[pl.slot].ensure2(pl.R, self.dev) if not gpu else None,
+                             grad_bf16=self.wire.grad_bf16, sr_counter=sr, self_run=-1, self_excl=None)
+            if gpu:
+                for t in (grad_recv, pl.req_recv) + ((sr,) if sr is not None else ()):
+                    t.record_stream(st)
+                ev = torch.cuda.Event()
+                ev.record(st)
+                self.applied_ev = ev
+                self.slots[pl.slot].done = ev        # (the plan's run offsets / match scratch were read)
+
+    def flush(self) -> None:
+        """Staleness: apply the pending gradient now and make the current stream wait for it -- the table
+        then holds every step's update (evaluation, checkpoints, teardown).  A step whose rows were not
+        gathered yet (no lookahead) then reads them as fresh as a synchronous step would.  No-op when
+        synchronous."""
+        if not self.staleness:
+            return
+        self._apply_pending()
+        if self.dev.type == "cuda" and self.applied_ev is not None:
+            torch.cuda.current_stream(self.dev).wait_event(self.applied_ev)
+
+    def sync_state(self) -> None:
+        """Checkpoint hook (utils/checkpoint.py): every update applied."""
+        self.flush()
+
+    def _train_step_stale(self, b: Batch, next_batch: Batch | None = None, next2: Batch | None = None):
+        """One bounded-staleness step (see __init__).  Host order: take this step's plan (its rows were
+        gathered and sent during the previous step, or are gathered now without lookahead), apply the
+        previous step's gradient (apply stream), forward + backward on the exchanged rows only, gradient
+        all-to-all (pending: applied during the next step), then the next plans and the next step's rows
+        (gathered right behind the apply just enqueued)."""
+        from ..models.fm import StepOut
+
+        m, ws, cfg, Kp = self.m, self.m.ws, self.m.cfg, self.Kp
+        gpu = self.dev.type == "cuda"
+        wf = self.wire
+        build = next2 if next2 is not None else next_batch
+        nb_ready = None
+        if build is not None and gpu and getattr(build, "ready", None) is None:
+            nb_ready = torch.cuda.Event()
+            nb_ready.record(torch.cuda.current_stream(self.dev))
+        with roctx_range("plan"):
+            pl = self._take_plan(b, True)
+        self.cur_plan = pl
+        part = pl.parts[0]
+        with roctx_range("rows"):
+            if pl.early is not None:
+                e = pl.early
+                if e.work is not None:
+                    e.work.wait()
+                    e.work = e.rows_send = None
+                buf = e.gathered
+                self.early_steps += 1
+            else:  # (no lookahead: gathered now, after the last apply and before the pending one)
+                if gpu and self.applied_ev is not None:
+                    torch.cuda.current_stream(self.dev).wait_event(self.applied_ev)
+                buf, work = self._gather_part(pl, part, async_op=True)
+                self._note_gather()
+                if work is not None:
+                    work.wait()
+        self._apply_pending()  # step t-1's gradient (after the gather of this step's rows)
+        src_v, src_w = wf.views(buf)
+        grad_send = wf.empty_grads(max(pl.U, 1), self.dev)
+        grad_recv = grad_send if self.W == 1 else wf.empty_grads(max(pl.R, 1), self.dev)
+        rv, rw = m.reg_coeffs
+        sr = m.sr_tick()
+        if sr is not None:
+            sr = sr.clone()  # (this step's seed, read by its apply during the next step)
+        sb, dd = part.b, part.dd
+        with roctx_range("fwd"):
+            fo = K.fm_forward(sb.offsets, part.keys if part.seg is not None else dd.inv[: sb.nnz], sb.vals, src_v,
+                              src_w, Kp, labels=sb.labels, weights=sb.weights, loss=cfg.loss_type,
+                              grad_scale=m.grad_scale(b.B), want_r1=True, pred=ws.pred[: sb.B], r1=ws.r1[: sb.B],
+                              dpred=ws.dpred[: sb.B], partial=ws.fwd_partial, threads=cfg.threads, bias=m.gbias,
+                              seg_lookup=part.seg, defer_loss=True)
+        with roctx_range("bwd"):
+            K.fm_backward(dd, fo.dpred, fo.r1, Kp, mode=K.BWD_EMIT, src_v=src_v, src_w=src_w,
+                          grad_out=grad_send[: max(pl.U, 1)], reg_v=rv, reg_w=rw, partial=ws.bwd_partial,
+                          threads=cfg.threads, grad_bf16=wf.grad_bf16)
+        m.bias_step(ws.dpred[: b.B])
+        loss = fo.finish_loss()
+        works, bwd_ev = [], None
+        if gpu:
+            bwd_ev = torch.cuda.Event()
+            bwd_ev.record(torch.cuda.current_stream(self.dev))
+        if self.W > 1:
+            with roctx_range("a2a_grads"):
+                works.append(dist.all_to_all_single(grad_recv[: pl.R], grad_send[: pl.U], part.rc, part.sc,
+                                                    group=self.group, async_op=True))
+                self.bytes_sent += 4 * wf.g_words * self._to_others(part.sc)
+        self._pend = (pl, grad_recv, works, sr, bwd_ev)
+        # the next plans; the next step's rows are gathered behind the apply enqueued above
+        if self.pending and next_batch is not None and self.pending[0].b is next_batch:
+            nxt_pl = self.pending[0]
+            with roctx_range("plan_finish_next"):
+                self._plan_finish(nxt_pl)
+            if nxt_pl.early is None and self._early_ok(nxt_pl, pl):
+                with roctx_range("early_rows_next"):
+                    self._early_ahead(nxt_pl, pl)
+        if next2 is not None and not any(p.b is next2 for p in self.pending):
+            if next_batch is not None and not any(p.b is next_batch for p in self.pending):
+                with roctx_range("plan_next"):
+                    self.pending.append(self._plan(next_batch, True, nb_ready, early=True))
+            with roctx_range("plan_next2"):
+                self.pending.append(self._plan_start(next2, True, nb_ready))
+        elif next2 is None and next_batch is not None and not any(p.b is next_batch for p in self.pending):
+            with roctx_range("plan_next"):
+                self.pending.append(self._plan(next_batch, True, nb_ready, early=True))
+        return StepOut(loss, b.B)
 
     def _early_ahead(self, pl: _ShardPlan, cur: _ShardPlan) -> None:
         """Depth-2 pipeline: at the start of step t, the early row exchange of the (already
@@ -578,7 +823,7 @@ class ShardExchange(_Base):
         """GPU version of ``_patch_cpu``: one tagged gather of the dirty rows, the patch
         all-to-all, one scatter kernel into the early copies."""
         e, dev, W = pl.early, self.dev, self.W
-        e.ev.synchronize()  # dirty counts (sent, received) on the host -- long done by now
+        self._await(e.ev)  # dirty counts (sent, received) on the host -- long done by now
         ds, dr = e.dsend[0].tolist(), e.dsend[1].tolist()
         D, Dr = int(sum(ds)), int(sum(dr))
         patch = self.wire.empty(D, dev)
@@ -674,19 +919,44 @@ class ShardExchange(_Base):
         r_start = np.concatenate([[0], np.cumsum(rc)[:-1]]).astype(np.int64).tolist()
         return s_start, [(n + 1) // 2 for n in sc], r_start, [(n + 1) // 2 for n in rc]
 
-    def _p2p_piece(self, piece: int, part: _Part, bounds, grad_send: torch.Tensor, grad_recv: torch.Tensor):
+    def _split_plan(self, pl: _ShardPlan) -> None:
+        """Once per plan (in its finish, off the step): the split backward's per-owner segment bounds
+        (device int32 [2W + 1], staged on the finish stream) and, per piece, every peer's send / receive
+        row ranges -- the step only wraps them in P2P ops."""
+        part = pl.parts[0]
+        s_start, s_half, r_start, r_half = self._half_bounds(part)
+        pieces = []
+        for piece in (0, 1):
+            rng = []
+            for q in range(self.W):
+                a0 = s_start[q] + (0 if piece == 0 else s_half[q])
+                a1 = s_start[q] + (s_half[q] if piece == 0 else part.sc[q])
+                b0 = r_start[q] + (0 if piece == 0 else r_half[q])
+                b1 = r_start[q] + (r_half[q] if piece == 0 else part.rc[q])
+                rng.append((q, a0, a1, b0, b1))
+            pieces.append(rng)
+        pl.pieces = pieces
+        if self.dev.type == "cuda":
+            sb = []
+            for q in range(self.W):
+                sb += [s_start[q], s_start[q] + s_half[q]]
+            sb.append(part.U)
+            slot = self.slots[pl.slot]
+            if getattr(slot, "sb_h", None) is None or slot.sb_h.numel() != len(sb):
+                slot.sb_h = torch.empty(len(sb), dtype=torch.int32, pin_memory=True)
+                slot.sb = torch.empty(len(sb), dtype=torch.int32, device=self.dev)
+            slot.sb_h.numpy()[:] = sb  # (this slot's previous copy finished: its plan's step is over)
+            slot.sb.copy_(slot.sb_h, non_blocking=True)
+            pl.sb = slot.sb
+
+    def _p2p_piece(self, pl: _ShardPlan, piece: int, grad_send: torch.Tensor, grad_recv: torch.Tensor):
         """Send every owner its rows of ``piece`` (0: first halves, 1: second halves) and receive
         the matching rows of every source into their place in ``grad_recv`` (rank-major runs);
         the own rank's rows are a local copy.  Returns the pending works."""
         if self.W == 1:
             return []  # (grad_recv is grad_send)
-        s_start, s_half, r_start, r_half = bounds
         ops, me = [], self.ctx.rank
-        for q in range(self.W):
-            a0 = s_start[q] + (0 if piece == 0 else s_half[q])
-            a1 = s_start[q] + (s_half[q] if piece == 0 else part.sc[q])
-            b0 = r_start[q] + (0 if piece == 0 else r_half[q])
-            b1 = r_start[q] + (r_half[q] if piece == 0 else part.rc[q])
+        for q, a0, a1, b0, b1 in pl.pieces[piece]:
             if q == me:
                 if b1 > b0:
                     grad_recv[b0:b1].copy_(grad_send[a0:a1])
@@ -705,29 +975,19 @@ class ShardExchange(_Base):
         """Backward in two pieces (every owner's first half of rows, then the second half) with
         the first piece's gradient rows sent while the second is reduced."""
         m, ws, cfg, Kp, wf = self.m, self.m.ws, self.m.cfg, self.Kp, self.wire
-        bounds = self._half_bounds(part)
+        if pl.pieces is None:  # (a plan finished before its split ranges existed)
+            self._split_plan(pl)
         if self.W > 1:
             self.bytes_sent += 4 * wf.g_words * self._to_others(part.sc)
         kw = dict(mode=K.BWD_EMIT, src_v=src_v, src_w=src_w, grad_out=gs, reg_v=rv, reg_w=rw,
                   partial=ws.bwd_partial, threads=cfg.threads, grad_bf16=wf.grad_bf16, **skw)
         if self.dev.type != "cuda":  # CPU reference: one backward, the exchange still in two pieces
             K.fm_backward(dd, fo.dpred, fo.r1, Kp, **kw)
-            return self._p2p_piece(0, part, bounds, gs, grad_recv) + self._p2p_piece(1, part, bounds, gs, grad_recv)
-        s_start, s_half = bounds[0], bounds[1]
-        sb = []
-        for q in range(self.W):
-            sb += [s_start[q], s_start[q] + s_half[q]]
-        sb.append(part.U)
-        slot = self.slots[pl.slot]
-        if getattr(slot, "sb_h", None) is None or slot.sb_h.numel() != len(sb):
-            slot.sb_h = torch.empty(len(sb), dtype=torch.int32, pin_memory=True)
-            slot.sb = torch.empty(len(sb), dtype=torch.int32, device=self.dev)
-        slot.sb_h.numpy()[:] = sb
-        slot.sb.copy_(slot.sb_h, non_blocking=True)
-        K.fm_backward(dd, fo.dpred, fo.r1, Kp, seg_bounds=slot.sb, piece=0, **kw)
-        works = self._p2p_piece(0, part, bounds, gs, grad_recv)
-        K.fm_backward(dd, fo.dpred, fo.r1, Kp, seg_bounds=slot.sb, piece=1, **kw)
-        return works + self._p2p_piece(1, part, bounds, gs, grad_recv)
+            return self._p2p_piece(pl, 0, gs, grad_recv) + self._p2p_piece(pl, 1, gs, grad_recv)
+        K.fm_backward(dd, fo.dpred, fo.r1, Kp, seg_bounds=pl.sb, piece=0, **kw)
+        works = self._p2p_piece(pl, 0, gs, grad_recv)
+        K.fm_backward(dd, fo.dpred, fo.r1, Kp, seg_bounds=pl.sb, piece=1, **kw)
+        return works + self._p2p_piece(pl, 1, gs, grad_recv)
 
     def _check_splits(self, part: _Part) -> None:
         """FM_DEBUG_CHECKS=1: the split lists of every rank must form a consistent W x W
@@ -807,6 +1067,10 @@ class ShardExchange(_Base):
         whole table-independent half of a step and its row exchange have a full step of slack."""
         from ..models.fm import StepOut
 
+        if self.dev.type == "cuda":
+            self._main = torch.cuda.current_stream(self.dev)
+        if self.staleness:
+            return self._train_step_stale(b, next_batch, next2)
         m, ws, cfg, Kp = self.m, self.m.ws, self.m.cfg, self.Kp
         gpu = self.dev.type == "cuda"
         build = next2 if next2 is not None else next_batch
@@ -934,6 +1198,7 @@ class ShardExchange(_Base):
 
     @torch.no_grad()
     def forward(self, b: Batch, *, loss: str = "none", want_reg: bool = False) -> K.FwdOut:
+        self.flush()  # (staleness: evaluate the table with every update applied)
         self.m.ws.ensure(b.B, b.nnz)
         pl = self._take_plan(b, False)
         part = pl.parts[0]

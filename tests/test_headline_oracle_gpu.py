@@ -14,7 +14,15 @@ touched rows only, gathered per occurrence on the GPU.
 (b) k=128 fp8 table + FTRL (BASELINE config 5): the fp32 linear weights tightly, the fp8 factors
     within the requantisation bound (one e4m3 step at the row's stored power-of-two scale, plus
     the bf16 r1 cache's 2^-9 relative error carried into the FTRL closed form).
+
+Both on the local step and on the row-sharded step's N > 1 compute path run at world 1 ("emit":
+RCCL world 1, FM_SHARD_W1_LOCAL=0 -- the sharded forward with self rows and the segment lookup, the
+EMIT-specialised chunk kernels with in-place self-row updates, the plan chain with the fused
+sharded-key sort).
 """
+
+import os
+
 
 import pytest
 import torch
@@ -27,6 +35,31 @@ pytestmark = pytest.mark.gpu
 
 V, B = 10_000_000, 131072
 LAMBDA_F, LAMBDA_B = 0.01, 0.01
+
+
+@pytest.fixture(scope="module")
+def rccl_ctx():
+    from ports import free_port
+
+    from fast_tffm_amd.parallel import dist as fmdist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(free_port())
+    ctx = fmdist.init_distributed(backend="nccl", rank=0, world=1, device="cuda:0", force_pg=True)
+    yield ctx
+    fmdist.shutdown()
+
+
+def _model(cfg, path, request, monkeypatch):
+    """The local step, or ("emit") the row-sharded N > 1 compute path at RCCL world 1."""
+    if path == "local":
+        return FactorizationMachine(cfg, device="cuda")
+    monkeypatch.setenv("FM_SHARD_W1_LOCAL", "0")
+    ctx = request.getfixturevalue("rccl_ctx")
+    cfg.mode = "shard"
+    m = FactorizationMachine(cfg, device="cuda", dist=ctx)
+    assert not m._exchange.local_w1 and m._exchange.self_rows
+    return m
 
 
 @pytest.fixture
@@ -64,13 +97,14 @@ def _touched(b):
     return uniq, loc
 
 
-def test_headline_step_k64_fp32_adagrad_matches_fp64_oracle(production):
+@pytest.mark.parametrize("path", ["local", "emit"])
+def test_headline_step_k64_fp32_adagrad_matches_fp64_oracle(production, path, request, monkeypatch):
     K_ = 64
     lr, acc0 = 0.01, 0.1
     cfg = FMConfig(vocabulary_size=V, factor_num=K_, loss_type="logistic", batch_size=B, init_value_range=0.01,
                    seed=42, factor_lambda=LAMBDA_F, bias_lambda=LAMBDA_B, mode="local",
                    opt=K.OptConfig("adagrad", lr=lr, initial_accumulator=acc0))
-    m = FactorizationMachine(cfg, device="cuda")
+    m = _model(cfg, path, request, monkeypatch)
     gen = CriteoSynth(V, seed=1000, device="cuda")
     b, nb = gen.batch(B), gen.batch(B)
     uniq, loc = _touched(b)
@@ -93,6 +127,7 @@ def test_headline_step_k64_fp32_adagrad_matches_fp64_oracle(production):
     # untouched rows stay put (a sample of them)
     rest = torch.randint(0, V, (100000,), device="cuda")
     rest = rest[~torch.isin(rest, uniq)]
+    cfg.mode = "local"
     fresh = FactorizationMachine(cfg, device="cuda")
     assert torch.equal(m.table.reference_rows(rest), fresh.table.reference_rows(rest))
     m.close()
@@ -108,12 +143,13 @@ def _ftrl(p, n, z, g, alpha, l1, l2, beta):
     return p, n_new, z
 
 
-def test_headline_step_k128_fp8_ftrl_matches_oracle(production):
+@pytest.mark.parametrize("path", ["local", "emit"])
+def test_headline_step_k128_fp8_ftrl_matches_oracle(production, path, request, monkeypatch):
     K_ = 128
     o = K.OptConfig("ftrl", lr=0.05, l1=0.001, l2=0.001, beta=1.0, initial_accumulator=0.1)
     cfg = FMConfig(vocabulary_size=V, factor_num=K_, loss_type="logistic", batch_size=B, init_value_range=0.01,
                    seed=42, factor_lambda=LAMBDA_F, bias_lambda=LAMBDA_B, mode="local", dtype=K.FP8, opt=o)
-    m = FactorizationMachine(cfg, device="cuda")
+    m = _model(cfg, path, request, monkeypatch)
     gen = CriteoSynth(V, seed=1001, device="cuda")
     b, nb = gen.batch(B), gen.batch(B)
     uniq, loc = _touched(b)

@@ -108,6 +108,9 @@ def main() -> int:
     ap.add_argument("--ranks", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--link-gbs", type=float, default=64.0, help="unidirectional GB/s per xGMI link (effective)")
     ap.add_argument("--step-ms", type=float, default=0.67, help="measured 1-GPU step (compute) time")
+    ap.add_argument("--stale-step-ms", type=float, default=None,
+                    help="measured world-1 step of the bounded-staleness executor (bench.py --mode shard "
+                         "--staleness 1): its compute, every row through the owner gather / apply")
     ap.add_argument("--dp-fwd-ms", type=float, default=0.20, help="dp_dense forward at world 1")
     ap.add_argument("--dp-bwd-ms", type=float, default=0.45, help="dp_dense backward (EMIT_TABLE) at world 1")
     ap.add_argument("--dp-apply-ms", type=float, default=0.10, help="dp_dense dense_apply of all V rows at world 1")
@@ -128,6 +131,20 @@ def main() -> int:
         print(f"{N:>2} {d['U']:>8} {d['to_others']:>8} {d['recv_others']:>8} {d['dirty']:>8} {d['ids'] / mb:>7.1f} "
               f"{d['rows'] / mb:>8.1f} {d['grads'] / mb:>9.1f} {d['patch'] / mb:>9.1f} {d['total'] / mb:>9.1f} "
               f"{d['critical'] / mb:>8.1f} {t_crit:>9.3f} {pred:>8.3f} {a.step_ms / pred:>8.2f}")
+    print()
+    stale_ms = a.stale_step_ms or a.step_ms
+    print(f"bounded staleness (staleness = 1): no dirty patch; step t-1's gradient all-to-all + owner apply and the "
+          f"gather + all-to-all of step t+1's rows run beside step t's compute ({stale_ms:.3f} ms/step at world 1, "
+          f"every row through the owner gather / apply), so no exchange byte is on the critical path while that "
+          f"chain fits a step:  pred = max(compute, bytes / links)")
+    print(f"{'N':>2} {'total MB':>9} {'t_all ms':>9} {'pred ms':>8} {'eff vs sync N=1':>15} {'eff vs stale N=1':>16}")
+    for N in a.ranks:
+        d = shard_model(N, a.batch, a.slots)
+        links = max(N - 1, 1)
+        tot = d["ids"] + d["rows"] + d["grads"]  # (no patch)
+        t_all = tot / (links * a.link_gbs * 1e9) * 1e3 if N > 1 else 0.0
+        pred = max(stale_ms, t_all)
+        print(f"{N:>2} {tot / mb:>9.1f} {t_all:>9.3f} {pred:>8.3f} {a.step_ms / pred:>15.2f} {stale_ms / pred:>16.2f}")
     print()
     print("dp_dense k=64 (V = 1M replicated, fp32 gradient buffer): reduce-scatter + sharded apply + all-gather")
     print(f"  compute at world 1: forward {a.dp_fwd_ms:.3f} ms, backward {a.dp_bwd_ms:.3f} ms, "
