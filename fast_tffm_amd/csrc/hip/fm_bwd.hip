@@ -103,8 +103,7 @@ struct BwdArgs {
   // gradient rows of piece 0 can travel while piece 1 is computed; -1 = all segments
   const int* seg_bounds;    // [2 * n_owners + 1]
   int piece, n_owners;
-  int big_blocks;           // (set by launch_bwd) fm_bwd_combine_kernel's hot-row workgroups
-  int big_last;             // (set by launch_bwd) 1: they follow the lane-group combine's workgroups
+  int big_blocks;           // (set by launch_bwd) fm_bwd_combine_kernel's hot-row workgroups (its first ones)
   float* partial;           // [#chunks, Kp + 4]
   int* big_list;            // [U] rows for the workgroup combine
   int* big_count;           // device scalar, zeroed by the launcher
@@ -112,7 +111,6 @@ struct BwdArgs {
   int* counts_rw;           // == counts, writable (counts[2] = #multi, zeroed by the launcher)
   int nex;                  // examples in the batch (r1 rows)
   SelfRows self;            // EMIT (row-sharded step): segments that are this rank's own table rows
-  int chunk_grid;           // chunk kernel workgroup cap: 0 = per-row-width default, > 0 = this, < 0 = none
 };
 
 // Parameter row + optimizer slots of one segment, read before its gradient is
@@ -779,30 +777,20 @@ __device__ inline void bwd_big_body(const BwdArgs& a, int blk, int nblk, uint32_
 // lane-group combine.  Two launches ran back to back (combine 35-43 us, then big 38-40 us in-step);
 // one launch, same box: k64 fp32 0.605-0.608 -> 0.592-0.596 ms, EMIT k64 0.636 -> 0.623, k16 bf16 tied;
 // 32-lane rows (k128) lost (fp8 FTRL 0.770 -> 0.778) and keep two launches of this kernel
-// (big_blocks = 0: combine only; = grid: hot rows only).
-constexpr int kBigBlocks = 1024;  // (FM_BIG_BLOCKS overrides: A/B)
+// (big_blocks = 0: combine only; = grid: hot rows only).  (Placing the hot-row workgroups last, and
+// 256-8192 of them, measured no better: the A/B knobs were removed in round 6.)
+constexpr int kBigBlocks = 1024;
 template <int LPR, typename TV>
 __global__ __launch_bounds__(kBlock) void fm_bwd_combine_kernel(BwdArgs a) {
   const uint32_t sr = sr_step_seed(a.sr_counter);  // stochastic rounding seed (0: nearest)
-  const int nsmall = gridDim.x - a.big_blocks;
-  const int b0 = a.big_last ? nsmall : 0;  // first hot-row workgroup
-  if ((int)blockIdx.x >= b0 && (int)blockIdx.x < b0 + a.big_blocks) bwd_big_body<LPR, TV>(a, blockIdx.x - b0, a.big_blocks, sr);
-  else bwd_combine_body<LPR, TV>(a, a.big_last ? blockIdx.x : blockIdx.x - a.big_blocks, nsmall, sr);
-}
-
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
+  if ((int)blockIdx.x < a.big_blocks) bwd_big_body<LPR, TV>(a, blockIdx.x, a.big_blocks, sr);
+  else bwd_combine_body<LPR, TV>(a, blockIdx.x - a.big_blocks, gridDim.x - a.big_blocks, sr);
 }
 
 // specialised kinds (local / EMIT) share the launch shape: EMIT runs the local step's kernel body
 static bool fast_kind(int kind) { return kind != kChunkAny; }
 
-static int chunk_wg_per_cu(int lpr, int kind) {
-  static const int env = env_int("FM_CHUNK_WG_PER_CU", -1);
-  if (env >= 0) return env;
-  return fast_kind(kind) && lpr <= 16 ? 3 : 0;
-}
+static int chunk_wg_per_cu(int lpr, int kind) { return fast_kind(kind) && lpr <= 16 ? 3 : 0; }
 
 int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_unique, hipStream_t st) {
   if (max_chunks <= 0) return 0;
@@ -812,8 +800,7 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
     (void)hipMemsetAsync(a.big_count, 0, sizeof(int), st);
     (void)hipMemsetAsync(a.counts_rw + 2, 0, sizeof(int), st);  // #multi-chunk rows, appended by the chunk kernel
   }
-  // (an explicit FM_CHUNK_GRID above fill_grid's 8192 cap raises the grid: A/B knob)
-  int g1 = (fill_grid(max_chunks, kWavesPerBlock * G, a.chunk_grid > 8192 ? a.chunk_grid : 8192) + 7) / 8 * 8;
+  int g1 = (fill_grid(max_chunks, kWavesPerBlock * G, 8192) + 7) / 8 * 8;
   // Cap on the chunk kernel's workgroups (the grid-stride walk covers every chunk either way).
   // Same-box sweeps (profiles/r2/chunk_grid_ab.txt): 16-lane rows (k=64 fp32 / bf16) 3456-4608
   // blocks beat the 8192 fill cap by 2.5-3% (k64 fp32 0.677-0.685 -> 0.661-0.662 ms), 4-lane
@@ -822,7 +809,6 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   // steadiest without a cap (0.701-0.702 ms vs 0.68-0.73 with 3840; chunk_grid_ab.txt).  Re-swept with
   // 3 workgroups per CU (profiles/r4/chunk_grid_wg3.txt): 16-lane rows 3072 (0.616-0.618 ms) over 3840
   // (0.620-0.624), 2304 / 5120 slower; 4-lane rows 512 still best; 32-lane rows uncapped.
-  // FM_CHUNK_GRID: > 0 overrides, < 0 disables.
   if (a.piece >= 0 && a.n_owners > kMaxPieceOwners) return -6;
   // (a software-pipelined variant that issued the next chunk's occurrence and row loads before
   // reducing the current one ran 367 -> 316 us alone but made the step slower twice:
@@ -833,25 +819,23 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   // rows' launch, or both launches concurrent -- measured slower: k64 0.669 -> 0.72-0.78 ms, each
   // launch as long as the whole walk; profiles/r3/bwd_split_ab.txt)
   // specialised chunk kernels (see ChunkKind) when r1 fits 32-bit offsets: LOCAL mode, and EMIT mode
-  // (the row-sharded step; FM_BWD_EMIT_FAST=0 keeps it on the general kernel, A/B)
+  // (the row-sharded step; the "bwdgen" build variant keeps every mode on the general kernel, A/B)
   const long long r1_bytes = (long long)a.nex * a.Kp * (dtype == kFP8 ? 2 : 4);
-  static const bool emit_fast = env_int("FM_BWD_EMIT_FAST", 1) != 0;
   const bool fits = FM_BWD_SPECIALIZE && lpr >= 4 && r1_bytes < (1LL << 32);
   int kind = kChunkAny;
   if (fits && a.mode == kBwdLocal && a.piece < 0) {
     kind = a.sorted_x ? kChunkLocal : kChunkLocalNoX;
-  } else if (fits && emit_fast && a.mode == kBwdEmit) {
+  } else if (fits && a.mode == kBwdEmit) {
     kind = a.piece >= 0 ? (a.sorted_x ? kChunkEmitPc : kChunkEmitPcNoX) : (a.sorted_x ? kChunkEmit : kChunkEmitNoX);
   }
-  const int cap = a.chunk_grid != 0 ? a.chunk_grid
-                  : !fast_kind(kind) ? -1 : (lpr == 16 ? 3072 : lpr == 4 ? 512 : -1);
+  const int cap = !fast_kind(kind) ? -1 : (lpr == 16 ? 3072 : lpr == 4 ? 512 : -1);
   if (cap > 0 && g1 > cap) g1 = (cap + 7) / 8 * 8;
   // Chunk workgroups resident per CU, capped through dynamic LDS the kernel does not use (a CU holds
   // floor(LDS / bytes) of them).  The side stream's radix-sort blocks then find LDS on every CU and
   // the capped grid spreads over more CUs: same-box, 3 per CU took k64 fp32 0.648 -> 0.621 ms and
   // k16 bf16 0.511 -> 0.487; 32-lane rows (k128, uncapped grid) lose (fp8 FTRL 0.887 -> 0.978)
   // (profiles/r4/wg_per_cu_ab.txt).  An earlier build's 130-VGPR k16 kernel (3 waves / SIMD) had
-  // the same effect by accident.  FM_CHUNK_WG_PER_CU overrides (0: no cap).
+  // the same effect by accident.
   const int wg_cu = chunk_wg_per_cu(lpr, kind);
   const bool pcw = kind == kChunkAny || kind == kChunkEmitPc || kind == kChunkEmitPcNoX;
   const int chunk_static_lds = pcw ? (int)sizeof(int) * (2 * kMaxPieceOwners + 1) : 0;  // piece walk
@@ -872,19 +856,14 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
     FM_DISPATCH_SHM(dtype, lpr, fm_bwd_chunk_kernel, g1, chunk_lds, st, a);
   }
   BwdArgs b = a;
-  static const int big_last = env_int("FM_BIG_LAST", 0);
-  b.big_last = big_last;
-  static const int nbig = env_int("FM_BIG_BLOCKS", kBigBlocks) > 0 ? env_int("FM_BIG_BLOCKS", kBigBlocks) : kBigBlocks;
-  static const bool one32 = env_int("FM_COMBINE_ONE32", 0) != 0;  // (A/B: one launch for 32-lane rows too)
-  if (lpr >= 32 && !one32) {
+  if (lpr >= 32) {  // (one launch lost for 32-lane rows: above)
     b.big_blocks = 0;
     FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, b);
-    b.big_blocks = nbig;
-    b.big_last = 0;
-    FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, nbig, st, b);
+    b.big_blocks = kBigBlocks;
+    FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, kBigBlocks, st, b);
   } else {
-    b.big_blocks = nbig;
-    FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, nbig + g2, st, b);
+    b.big_blocks = kBigBlocks;
+    FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, kBigBlocks + g2, st, b);
   }
   return (int)hipGetLastError();
 }

@@ -418,7 +418,15 @@ void fm_fwd_shard_kernel(FwdArgs a) {
   fwd_body<LPR, TV, true>(a);
 }
 
+// The matrix-core form of the fp8 k=128 forward is a build variant ("mfma": -DFM_WITH_MFMA=1), not part
+// of the default module: built, correct, and slower than the VALU kernel twice over -- the forward is
+// bound by its random row gathers, not by its arithmetic (profiles/r5/fwd_mfma_ab.txt).
+#ifndef FM_WITH_MFMA
+#define FM_WITH_MFMA 0
+#endif
+#if FM_WITH_MFMA
 #include "fm_fwd_mfma.hip"
+#endif
 
 // Expand CSR offsets into the example index of every occurrence.
 // Example of every CSR occurrence; with slot_bits > 0 the packed occurrence code
@@ -458,17 +466,11 @@ __global__ __launch_bounds__(kBlock) void csr_rows_kernel(int B, const int* offs
   }
 }
 
-// FM_FWD_MFMA=1 (or set_fwd_mfma(true)): fp8 k=128 batches of binary features take the matrix-core
-// kernel (fm_fwd_mfma.hip; off by default until it beats the VALU kernel: profiles/r5/fwd_mfma_ab.txt)
-static int g_fwd_mfma = -1;
-bool fwd_mfma_enabled() {
-  if (g_fwd_mfma < 0) {
-    const char* e = getenv("FM_FWD_MFMA");
-    g_fwd_mfma = e && atoi(e) != 0;
-  }
-  return g_fwd_mfma != 0;
-}
-void set_fwd_mfma(bool on) { g_fwd_mfma = on; }
+// "mfma" build variant: fp8 k=128 batches of binary features take the matrix-core kernel
+// (fm_fwd_mfma.hip) while set_fwd_mfma(true) (its default); the default module has no such kernel.
+static bool g_fwd_mfma = FM_WITH_MFMA;
+bool fwd_mfma_enabled() { return g_fwd_mfma; }
+void set_fwd_mfma(bool on) { g_fwd_mfma = FM_WITH_MFMA && on; }
 
 int fwd_grid(int B) { return fill_grid(B, kWavesPerBlock, 4096); }
 
@@ -484,6 +486,7 @@ int launch_fwd(const FwdArgs& a, int dtype, int grid, hipStream_t st) {
     if (!aligned(a.w, a.w_stride) || (a.self.u1 > a.self.u0 && !aligned(a.self.w, a.self.w_stride))) return -7;
   }
   const bool table_rows = dtype != kFP8 || a.w_stride == 4;  // (the local kernel's fp8 tails: w + 4 row)
+#if FM_WITH_MFMA
   // fp8 rows on the matrix cores (fm_fwd_mfma.hip): binary features, Kp = 128, table rows, tiles of 16
   // examples within the kernel's LDS row capacity.
   if (fwd_mfma_enabled() && dtype == kFP8 && a.Kp == kMfRowB && a.v_stride == kMfRowB && !a.vals && table_rows &&
@@ -491,6 +494,8 @@ int launch_fwd(const FwdArgs& a, int dtype, int grid, hipStream_t st) {
     hipLaunchKernelGGL(fm_fwd_mfma_fp8_kernel, dim3(grid), dim3(kBlock), 0, st, a);
     return (int)hipGetLastError();
   }
+#endif
+
   if (a.self.u1 > a.self.u0 || a.seg_idx || !FM_FWD_SPECIALIZE || !table_rows) {
     FM_DISPATCH(dtype, lpr, fm_fwd_shard_kernel, grid, st, a);
   } else {

@@ -140,9 +140,8 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
          u64 big_list, u64 big_count, u64 multi, int nex, int dtype,
          long long max_chunks, long long max_unique, u64 stream, int g_wcol, int g_bf16, u64 sr_counter,
          int counters_ready, u64 seg_bounds, int piece, int n_owners,
-         const std::vector<long long>& self, int chunk_grid) {
+         const std::vector<long long>& self) {
         fm::BwdArgs a{};
-        a.chunk_grid = chunk_grid;
         a.self = self_rows(self);
         if (a.self.u1 > a.self.u0 && a.self.keys != P<const int>(uniq))
           throw std::runtime_error("fm_bwd: self-row keys must be the dedup's unique keys");
@@ -179,7 +178,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("max_chunks"), py::arg("max_unique"), py::arg("stream"), py::arg("g_wcol") = -1,
       py::arg("g_bf16") = 0, py::arg("sr_counter") = 0, py::arg("counters_ready") = 0, py::arg("seg_bounds") = 0,
       py::arg("piece") = -1, py::arg("n_owners") = 0,
-      py::arg("self_rows") = std::vector<long long>{}, py::arg("chunk_grid") = 0);
+      py::arg("self_rows") = std::vector<long long>{});
 
   m.def("dedup_workspace_bytes", &fm::dedup_workspace_bytes, py::arg("n"));
   m.def("set_sort_algo", &fm::set_sort_algo, py::arg("in_tree"));  // 1: radix_sort.hip, 0: rocPRIM onesweep

@@ -39,8 +39,9 @@ def set_debug_checks(on: bool) -> None:
 
 
 def set_fwd_mfma(on: bool) -> bool:
-    """Route fp8 k=128 binary-feature forwards to the matrix-core kernel (hip/fm_fwd_mfma.hip; default
-    off, FM_FWD_MFMA=1 at start-up turns it on) or the VALU kernel; returns the previous setting."""
+    """Route fp8 k=128 binary-feature forwards to the matrix-core kernel (hip/fm_fwd_mfma.hip: the "mfma"
+    build variant only, where it is the default; the default module has no such kernel and stays on the
+    VALU kernel) or the VALU kernel; returns the previous setting."""
     h = native.hip()
     was = bool(h.fwd_mfma_enabled())
     h.set_fwd_mfma(bool(on))
@@ -749,9 +750,7 @@ def fm_backward(dd: DedupOut, dpred: torch.Tensor, r1: torch.Tensor, Kp: int, *,
               stream=_stream(dpred), g_wcol=g_wcol if mode != BWD_LOCAL else -1, g_bf16=int(bool(grad_bf16)),
               sr_counter=_p(sr_counter), counters_ready=int(bool(dd.bwd_fresh)),
               seg_bounds=_p(seg_bounds), piece=int(piece),
-              n_owners=(seg_bounds.numel() - 1) // 2 if seg_bounds is not None else 0,
-              chunk_grid=int(os.environ.get("FM_CHUNK_GRID", "0")),
-              **skw)
+              n_owners=(seg_bounds.numel() - 1) // 2 if seg_bounds is not None else 0, **skw)
         dd.bwd_fresh = False  # a second backward over this grouping zeroes its counters itself
     else:
         _check(self_rows is None, "self rows are a GPU path")

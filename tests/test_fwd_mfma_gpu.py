@@ -25,6 +25,19 @@ from oracle import fm_scores
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def mfma_variant(monkeypatch):
+    """The matrix-core forward lives in the "mfma" build variant (python -m fast_tffm_amd.build_native
+    --variant mfma), not in the default module; skipped where that variant is not built."""
+    from fast_tffm_amd.ops import native
+
+    monkeypatch.setenv("FM_HIP_VARIANT", "mfma")
+    try:
+        native.hip()
+    except native.NativeExtensionError as e:
+        pytest.skip(f"mfma build variant not available: {e}")
+
+
 def _table(V: int, seed: int) -> FMTable:
     t = FMTable(V, 128, dtype=K.FP8, device="cuda", seed=seed, init_range=0.05)
     g = torch.Generator(device="cuda").manual_seed(seed)
