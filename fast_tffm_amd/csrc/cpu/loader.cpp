@@ -571,7 +571,12 @@ void TextLoader::run() {
               reuse(b.labels); reuse(b.ids); reuse(b.vals);
               if (weighted) reuse(b.weights);
             }
-            assemble_binary(bchosen, bs, weighted, o_.vocab_size, o_.threads, b, pin_acquire);
+            try {
+              assemble_binary(bchosen, bs, weighted, o_.vocab_size, o_.threads, b, pin_acquire);
+            } catch (...) {  // (an out-of-range id: the pinned buffer goes back before the error does)
+              release_pinned(b.pinned);
+              throw;
+            }
           }
           b.epoch = epoch;
           b.count = count;
@@ -708,6 +713,16 @@ void TextLoader::run() {
             return true;
           };
         }
+        // (a parse / weight error after the pinned buffer was acquired gives it back before the error
+        // propagates: the consumer's pool must not shrink by a failed batch)
+        struct PinGuard {
+          TextLoader* ld;
+          const int32_t* tag;
+          bool armed = true;
+          ~PinGuard() {
+            if (armed) ld->release_pinned(*tag);
+          }
+        } pin_guard{this, &ptag};
         parse_lines32(ptrs.data(), lens.data(), n, o_.vocab_size, o_.hash_feature_id, o_.threads, csr, &pws);
         float* wdst = nullptr;
         if (csr.in_ext) {
@@ -737,6 +752,7 @@ void TextLoader::run() {
         b.epoch = epoch;
         b.count = count;
         csr = Csr32();
+        pin_guard.armed = false;  // (the batch owns the buffer now: its consumer frees it)
         return push(std::move(b));
       };
 

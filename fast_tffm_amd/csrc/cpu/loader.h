@@ -147,6 +147,11 @@ class TextLoader {
     const FmPinnedPool* p = pinned_pool_.load(std::memory_order_acquire);
     return p ? p->acquire(p->ctx, bytes, tag) : nullptr;
   }
+  // Give an acquired, undelivered pinned buffer back (the batch being built failed).
+  void release_pinned(int32_t tag) {
+    const FmPinnedPool* p = pinned_pool_.load(std::memory_order_acquire);
+    if (p && p->release && tag >= 0) p->release(p->ctx, tag);
+  }
   static void api_stop(void* h) { static_cast<TextLoader*>(h)->close(); }
 
   void run();

@@ -153,6 +153,7 @@ class GpuTextFeeder {
     // buffers (no staging copy on the feeder thread)
     pool_api_.ctx = this;
     pool_api_.acquire = &GpuTextFeeder::pin_acquire_cb;
+    pool_api_.release = &GpuTextFeeder::pin_release_cb;
     api_->set_pinned_pool(api_->handle, &pool_api_);
     th_ = std::thread([this] { run(); });
   }
@@ -343,6 +344,11 @@ class GpuTextFeeder {
   static void* pin_acquire_cb(void* ctx, size_t bytes, int32_t* tag) {
     return static_cast<GpuTextFeeder*>(ctx)->pin_acquire(bytes, tag);
   }
+  static void pin_release_cb(void* ctx, int32_t tag) { static_cast<GpuTextFeeder*>(ctx)->pin_release(tag); }
+  // Smallest idle buffer of >= bytes; else a NEW buffer while the pool has room (an idle smaller one
+  // -- an epoch's short last batch -- is kept for later small batches), else an idle smaller one grown.
+  // The page-locked allocation runs outside pmu_ (hipHostMalloc / hipHostFree can wait for device
+  // work): the slot is reserved busy first.
   void* pin_acquire(size_t bytes, int32_t* tag) {
     std::unique_lock<std::mutex> lk(pmu_);
     for (;;) {
@@ -356,30 +362,42 @@ class GpuTextFeeder {
           small = static_cast<int>(i);
         }
       }
-      if (fit < 0 && (small >= 0 || static_cast<int>(pbufs_.size()) < kPinPoolMax)) {
-        if (small < 0) {
-          pbufs_.emplace_back();
-          small = static_cast<int>(pbufs_.size()) - 1;
-        }
-        PinBuf& pb = pbufs_[small];
-        (void)hipSetDevice(device_);
-        if (pb.p) (void)hipHostFree(pb.p);
-        pb.p = nullptr;
-        pb.cap = 0;
-        const size_t cap = bytes + bytes / 8 + 4096;  // (room for a somewhat denser batch)
-        if (hipHostMalloc(&pb.p, cap, hipHostMallocDefault) != hipSuccess) {
-          pb.p = nullptr;
-          return nullptr;  // (no page-locked memory: the loader uses its own)
-        }
-        pb.cap = cap;
-        fit = small;
-      }
       if (fit >= 0) {
         pbufs_[fit].busy = true;
         *tag = fit;
         return pbufs_[fit].p;
       }
-      pcv_.wait_for(lk, std::chrono::milliseconds(100));
+      int slot = -1;
+      if (static_cast<int>(pbufs_.size()) < kPinPoolMax) {
+        pbufs_.emplace_back();
+        slot = static_cast<int>(pbufs_.size()) - 1;
+      } else if (small >= 0) {
+        slot = small;
+      }
+      if (slot < 0) {
+        pcv_.wait_for(lk, std::chrono::milliseconds(100));
+        continue;
+      }
+      pbufs_[slot].busy = true;  // (reserved: no other acquire takes it while it is reallocated)
+      void* old = pbufs_[slot].p;
+      pbufs_[slot].p = nullptr;
+      pbufs_[slot].cap = 0;
+      lk.unlock();
+      (void)hipSetDevice(device_);
+      if (old) (void)hipHostFree(old);
+      const size_t cap = bytes + bytes / 8 + 4096;  // (room for a somewhat denser batch)
+      void* p = nullptr;
+      const bool ok = hipHostMalloc(&p, cap, hipHostMallocDefault) == hipSuccess;
+      lk.lock();
+      if (!ok) {
+        pbufs_[slot].busy = false;  // (an empty idle slot: a later acquire allocates it again)
+        pcv_.notify_one();
+        return nullptr;  // (no page-locked memory: the loader uses its own)
+      }
+      pbufs_[slot].p = p;
+      pbufs_[slot].cap = cap;
+      *tag = slot;
+      return p;
     }
   }
   void pin_release(int tag) {

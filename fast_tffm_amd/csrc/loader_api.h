@@ -42,10 +42,13 @@ struct FmRawView {
 // Page-locked output buffers a consumer offers for kind-1 batches (set_pinned_pool): the loader
 // assembles a batch's CSR arrays straight into one, so the consumer's host-to-device copy needs
 // no staging copy.  acquire blocks until a buffer of >= bytes is free and returns it with its
-// tag; null (consumer closing, or no buffer that large): the loader uses its own memory.
+// tag; null (consumer closing, or no buffer that large): the loader uses its own memory.  release
+// hands a tag back unused (a batch that failed after its buffer was acquired); a delivered batch's
+// buffer is freed by its consumer.
 struct FmPinnedPool {
   void* ctx;
   void* (*acquire)(void* ctx, size_t bytes, int32_t* tag);
+  void (*release)(void* ctx, int32_t tag);
 };
 
 // Host CSR written by FmLoaderApi::parse into caller-owned arrays.
@@ -80,4 +83,4 @@ struct FmLoaderApi {
 
 }  // extern "C"
 
-constexpr int32_t kFmLoaderApiVersion = 3;
+constexpr int32_t kFmLoaderApiVersion = 4;
