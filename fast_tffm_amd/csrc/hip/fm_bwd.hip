@@ -430,8 +430,9 @@ __device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
   };
   // the r1 row of an occurrence slot only where the slot holds one (its c is 0 otherwise): the unused
   // slots of the 4-slot short block -- 275k of a Criteo-shaped batch's 378k rows occur once -- issue no
-  // load (FM_R1_MASK=0: every slot loads its lane's clamped row, the A/B).  (Masking the UNR blocks'
-  // tails as well took the 32-lane fp8 kernel over 128 VGPRs into spills.)
+  // load (FM_R1_MASK=0: every slot loads its lane's clamped row, the A/B).  Masking the UNR blocks'
+  // tails too was much slower (k64 fp32 0.592-0.597 -> 0.701-0.704 ms, EMIT 0.624 -> 0.736: each masked
+  // load became its own branch, so the block's loads no longer went out together; round 6).
   auto r1_at_if = [&](bool need, int ex, float (&o)[EPL]) {
     if (!FM_R1_MASK || need) {
       r1_at(ex, o);
