@@ -494,7 +494,7 @@ class ShardExchange(_Base):
                 pl.counts = torch.empty(both.shape, dtype=torch.int64, pin_memory=True)
                 pl.counts.copy_(both, non_blocking=True)
                 pl.counts_ev = torch.cuda.Event()
-                pl.counts_ev.record(torch.cuda.current_stream(self.dev))
+                pl.counts_ev.record(st)
             else:
                 pl.counts, pl.counts_ev = torch.stack(counts, dim=1), None
         return pl
@@ -509,7 +509,7 @@ class ShardExchange(_Base):
         slot = self.slots[pl.slot]
         with self._side_ctx():
             if pl.counts_ev is not None:  # GPU: both count matrices exchanged on the device
-                torch.cuda.current_stream(self.dev).wait_event(pl.counts_ev)  # (the dedup stream's outputs)
+                self._prep_stream().wait_event(pl.counts_ev)  # (the dedup stream's outputs)
                 self._await(pl.counts_ev)
                 sc, rc = pl.counts[0].clone(), pl.counts[1].clone()
             else:
@@ -561,7 +561,7 @@ class ShardExchange(_Base):
                 pl.early = self._early(pl, self.cur_plan)
             if gpu:
                 pl.ready = torch.cuda.Event()
-                pl.ready.record(torch.cuda.current_stream(self.dev))
+                pl.ready.record(self._prep_stream())
 
     def _early_ok(self, pl: _ShardPlan, cur: _ShardPlan | None) -> bool:
         gpu = self.dev.type == "cuda"
@@ -597,7 +597,7 @@ class ShardExchange(_Base):
         e = _Early()
         e.work = e.rows_send = e.didx = e.sc_start = e.dsend = e.ev = None
         if gpu and self.applied_ev is not None:
-            torch.cuda.current_stream(dev).wait_event(self.applied_ev)
+            self._prep_stream().wait_event(self.applied_ev)
         rows_send = self.wire.empty(pl.R, dev)
         K.gather_wire(pl.req_recv[: pl.R], self.m.table.state, self.wire, rows_send, threads=self.m.cfg.threads)
         self._note_gather()
@@ -688,7 +688,7 @@ class ShardExchange(_Base):
         nb_ready = None
         if build is not None and gpu and getattr(build, "ready", None) is None:
             nb_ready = torch.cuda.Event()
-            nb_ready.record(torch.cuda.current_stream(self.dev))
+            nb_ready.record(self._main)
         with roctx_range("plan"):
             pl = self._take_plan(b, True)
         self.cur_plan = pl
@@ -703,7 +703,7 @@ class ShardExchange(_Base):
                 self.early_steps += 1
             else:  # (no lookahead: gathered now, after the last apply and before the pending one)
                 if gpu and self.applied_ev is not None:
-                    torch.cuda.current_stream(self.dev).wait_event(self.applied_ev)
+                    self._main.wait_event(self.applied_ev)
                 buf, work = self._gather_part(pl, part, async_op=True)
                 self._note_gather()
                 if work is not None:
@@ -732,7 +732,7 @@ class ShardExchange(_Base):
         works, bwd_ev = [], None
         if gpu:
             bwd_ev = torch.cuda.Event()
-            bwd_ev.record(torch.cuda.current_stream(self.dev))
+            bwd_ev.record(self._main)
         if self.W > 1:
             with roctx_range("a2a_grads"):
                 works.append(dist.all_to_all_single(grad_recv[: pl.R], grad_send[: pl.U], part.rc, part.sc,
@@ -767,7 +767,7 @@ class ShardExchange(_Base):
             pl.early = self._early(pl, cur)
             if gpu:
                 pl.ready = torch.cuda.Event()
-                pl.ready.record(torch.cuda.current_stream(self.dev))
+                pl.ready.record(self._prep_stream())
 
     def _patch(self, pl: _ShardPlan) -> tuple[torch.Tensor, torch.Tensor]:
         return self._patch_gpu(pl) if self.dev.type == "cuda" else self._patch_cpu(pl)
@@ -796,14 +796,14 @@ class ShardExchange(_Base):
         e.dsend[0].copy_(dcount[:W], non_blocking=True)
         e.dsend[1].copy_(drecv, non_blocking=True)
         e.ev = torch.cuda.Event()
-        e.ev.record(torch.cuda.current_stream(dev))
+        e.ev.record(self._prep_stream())
         h = ew["sc_h"].numpy()
         h[0] = 0
         np.cumsum(part.sc[:-1], out=h[1:W])
         e.sc_start = ew["sc"]
         e.sc_start.copy_(ew["sc_h"], non_blocking=True)
         if self.step_start is not None:
-            torch.cuda.current_stream(dev).wait_event(self.step_start)
+            self._prep_stream().wait_event(self.step_start)
         rows_send = self.wire.empty(R, dev)
         K.gather_wire(req, self.m.table.state, self.wire, rows_send, threads=self.m.cfg.threads, skip=pl.self_r)
         e.work = None
@@ -1077,10 +1077,10 @@ class ShardExchange(_Base):
         nb_ready = None
         if build is not None and gpu and getattr(build, "ready", None) is None:
             nb_ready = torch.cuda.Event()  # the batch's producers: all work enqueued before this step
-            nb_ready.record(torch.cuda.current_stream(self.dev))
+            nb_ready.record(self._main)
         if gpu:
             self.step_start = torch.cuda.Event()  # after the previous step's apply (early gathers wait on it)
-            self.step_start.record(torch.cuda.current_stream(self.dev))
+            self.step_start.record(self._main)
         with roctx_range("plan"):
             pl = self._take_plan(b, True)
         self.cur_plan = pl
@@ -1166,7 +1166,7 @@ class ShardExchange(_Base):
                              self_excl=pl.self_excl)
         if gpu:
             done = torch.cuda.Event()
-            done.record(torch.cuda.current_stream(self.dev))
+            done.record(self._main)
             self.slots[pl.slot].done = done
         if self.pending and next_batch is not None and self.pending[0].b is next_batch:
             # Finish the next batch's plan only now, with this whole step already enqueued: the
