@@ -169,9 +169,31 @@ def install(delay_cycles: int = 2_000_000) -> None:
         n = out.numel()
         return _deliver(group, cur, [inp], snaps, [(out, full.reshape(-1)[r * n:(r + 1) * n])], async_op)
 
-    tdist.all_to_all_single = a2a
-    tdist.batch_isend_irecv = batch_isend_irecv
-    tdist.all_reduce = all_reduce
-    tdist.all_gather = all_gather
-    tdist.all_gather_into_tensor = all_gather_into_tensor
-    tdist.reduce_scatter_tensor = reduce_scatter_tensor
+    import functools
+    import time
+
+    _STATE["t"] = 0.0
+
+    def timed(fn):
+        """Host seconds spent inside the relay (its staging, host syncs and gloo transfers): excluded
+        when the executor's own host time is measured under the relay."""
+        @functools.wraps(fn)
+        def f(*a, **kw):
+            t0 = time.perf_counter()
+            try:
+                return fn(*a, **kw)
+            finally:
+                _STATE["t"] += time.perf_counter() - t0
+        return f
+
+    tdist.all_to_all_single = timed(a2a)
+    tdist.batch_isend_irecv = timed(batch_isend_irecv)
+    tdist.all_reduce = timed(all_reduce)
+    tdist.all_gather = timed(all_gather)
+    tdist.all_gather_into_tensor = timed(all_gather_into_tensor)
+    tdist.reduce_scatter_tensor = timed(reduce_scatter_tensor)
+
+
+def relay_seconds() -> float:
+    """Host time spent inside relayed collectives so far."""
+    return float(_STATE.get("t", 0.0))

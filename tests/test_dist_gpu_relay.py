@@ -67,10 +67,19 @@ def _worker(rank, world, port, out_dir, variant, mode="shard"):
     else:
         bs = [_batch(s, rank, vocab, batch) for s in range(steps)]
     losses = []
+    import time
+
+    t_loop = r_loop = w_loop = 0.0
     for s in range(steps):
         nb = bs[s + 1] if s + 1 < steps else None
         nb2 = bs[s + 2] if s + 2 < steps else None
-        losses.append(m.train_step(bs[s], nb, nb2).mean_loss())
+        t0, r0, w0 = time.perf_counter(), relay.relay_seconds(), getattr(m._exchange, "host_wait_s", 0.0)
+        out = m.train_step(bs[s], nb, nb2)
+        if s >= 1:  # (the executor's own host time: the step's wall time minus the relay and the blocked waits)
+            t_loop += time.perf_counter() - t0
+            r_loop += relay.relay_seconds() - r0
+            w_loop += getattr(m._exchange, "host_wait_s", 0.0) - w0
+        losses.append(out.mean_loss())
     m.flush()  # (staleness: the last step's gradient applied)
     torch.cuda.synchronize()
     ex = m._exchange
@@ -85,7 +94,8 @@ def _worker(rank, world, port, out_dir, variant, mode="shard"):
         rows = m.table.reference_rows().cpu()
     torch.save({"gids": gids.cpu(), "rows": rows, "losses": losses,
                 "early": getattr(ex, "early_steps", 0), "split": getattr(ex, "overlap_grads", False),
-                "comm": getattr(ex, "comm_mode", None), "violations": relay.violations()},
+                "comm": getattr(ex, "comm_mode", None), "violations": relay.violations(),
+                "host_us": (t_loop - r_loop - w_loop) / max(steps - 1, 1) * 1e6},
                os.path.join(out_dir, f"rank{rank}.pt"))
     fmdist.shutdown()
 
@@ -131,6 +141,9 @@ def test_ranks_on_one_gpu_equal_one_process(tmp_path, world, variant):
     World 8 (the node size of the scaling runs): 8 owners in the split-backward piece walk, the
     segment lookup and the dirty scan, with the dual (default) and the single communicator."""
     res = _run(tmp_path, world, variant)
+    print(f"[relay host] world {world} {variant}: executor host time per step (relay staging and blocked "
+          f"waits excluded) "
+          f"{', '.join('%.0f' % r['host_us'] for r in res)} us")
     if "prefetch_rows" not in variant:  # default at world > 1: early row exchange on
         assert all(r["early"] == STEPS - 1 for r in res)
     assert all(r["split"] == (variant.get("overlap_grads", "auto") != "off") for r in res)  # (split: default on)
