@@ -46,6 +46,9 @@ constexpr int kChunkUnr = FM_CHUNK_UNR;
 #ifndef FM_R1_MASK
 #define FM_R1_MASK 1
 #endif
+#ifndef FM_CHUNK_PERM
+#define FM_CHUNK_PERM 0
+#endif
 // The local kernels' 32-lane rows (k = 128): 12 r1 rows in flight per lane.  Same-box A/B
 // (profiles/r4/chunk_unr_ab.txt): k128 fp8 FTRL 0.874 -> 0.807 ms with 12, 0.856 with 16; 16-lane and
 // 4-lane rows (k64 / k16) lose with 12 or 16 (k64 fp32 0.615 -> 0.625-0.640), and so does the
@@ -470,6 +473,13 @@ __device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
       while (q + 1 < a.n_owners && pr_pre[q + 1] <= i) ++q;
       return pr_start[q] + (i - pr_pre[q]);
     }
+#if FM_CHUNK_PERM
+    // (probe variant "chunkperm": the walk interleaves 8 far-apart streams of chunks -- lane groups
+    // working together reduce rows ~n/8 apart instead of consecutive ones -- to measure what the
+    // read-modify-write's page locality is worth: profiles/r6/rmw_locality.txt)
+    const int q8 = nchunks / 8;
+    if (i < 8 * q8) return (i & 7) * q8 + (i >> 3);
+#endif
     return i;
   };
   int c = ii < i1 ? chunk_at(ii) : 0;
