@@ -454,7 +454,8 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("ws_bytes"), py::arg("stream"), py::arg("require_vals") = 0);
 
   // GPU-tokenizer feeder (feeder.hip): a native thread from the loader's raw batches to device CSR
-  py::class_<fm::GpuTextFeeder>(m, "GpuTextFeeder")
+  // (module_local: a build variant of this module can be loaded beside it in one process)
+  py::class_<fm::GpuTextFeeder>(m, "GpuTextFeeder", py::module_local())
       .def(py::init([](u64 api, int device, long long vocab, bool hash) {
              return new fm::GpuTextFeeder(P<const FmLoaderApi>(api), device, vocab, hash);
            }),
