@@ -922,7 +922,7 @@ class ShardExchange(_Base):
     def _split_plan(self, pl: _ShardPlan) -> None:
         """Once per plan (in its finish, off the step): the split backward's per-owner segment bounds
         (device int32 [2W + 1], staged on the finish stream) and, per piece, every peer's send / receive
-        row ranges -- the step only wraps them in P2P ops."""
+        row ranges -- the step only wraps them in one all-to-all (P2P ops on CPU)."""
         part = pl.parts[0]
         s_start, s_half, r_start, r_half = self._half_bounds(part)
         pieces = []
@@ -951,10 +951,18 @@ class ShardExchange(_Base):
 
     def _p2p_piece(self, pl: _ShardPlan, piece: int, grad_send: torch.Tensor, grad_recv: torch.Tensor):
         """Send every owner its rows of ``piece`` (0: first halves, 1: second halves) and receive
-        the matching rows of every source into their place in ``grad_recv`` (rank-major runs);
-        the own rank's rows are a local copy.  Returns the pending works."""
+        the matching rows of every source into their place in ``grad_recv`` (rank-major runs).
+        Returns the pending works."""
         if self.W == 1:
             return []  # (grad_recv is grad_send)
+        if self.dev.type == "cuda":
+            # one all-to-all over per-peer views (the own chunk included): a single C++ call issues the
+            # RCCL group of sends / receives, where 2 (W - 1) Python P2P ops per piece cost host time
+            # that grows with W
+            ins = [grad_send[a0:a1] for _, a0, a1, _, _ in pl.pieces[piece]]
+            outs = [grad_recv[b0:b1] for _, _, _, b0, b1 in pl.pieces[piece]]
+            w = dist.all_to_all(outs, ins, group=self.group, async_op=True)
+            return [w] if w is not None else []
         ops, me = [], self.ctx.rank
         for q, a0, a1, b0, b1 in pl.pieces[piece]:
             if q == me:
@@ -967,9 +975,7 @@ class ShardExchange(_Base):
                 ops.append(dist.P2POp(dist.irecv, grad_recv[b0:b1], q, group=self.group))
         if not ops:
             return []
-        if self.dev.type == "cuda":
-            return list(dist.batch_isend_irecv(ops))
-        return [op.op(op.tensor, op.peer, group=op.group) for op in ops]
+        return [op.op(op.tensor, op.peer, group=op.group) for op in ops]  # (CPU / gloo)
 
     def _bwd_split_exchange(self, pl, part, dd, fo, src_v, src_w, gs, grad_recv, rv, rw, skw) -> list:
         """Backward in two pieces (every owner's first half of rows, then the second half) with

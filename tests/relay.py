@@ -101,7 +101,7 @@ def install(delay_cycles: int = 2_000_000) -> None:
     real = dict(a2a=tdist.all_to_all_single, isend=tdist.isend, irecv=tdist.irecv,
                 all_reduce=tdist.all_reduce, all_gather=tdist.all_gather,
                 agit=tdist.all_gather_into_tensor, rst=tdist.reduce_scatter_tensor,
-                bir=tdist.batch_isend_irecv)
+                bir=tdist.batch_isend_irecv, a2a_list=tdist.all_to_all)
     _STATE.update(streams={}, delay=int(delay_cycles), real=real, flag=None)
 
     def a2a(out, inp, output_split_sizes=None, input_split_sizes=None, group=None, async_op=False):
@@ -111,6 +111,19 @@ def install(delay_cycles: int = 2_000_000) -> None:
         o = torch.empty(out.shape, dtype=out.dtype)
         real["a2a"](o, host[0], output_split_sizes, input_split_sizes, group=group)
         return _deliver(group, cur, [inp], snaps, [(out, o)], async_op)
+
+    def all_to_all(out_list, in_list, group=None, async_op=False):
+        """List all-to-all (per-peer views) over gloo's all_to_all_single on the flattened chunks."""
+        if not any(t.is_cuda for t in list(in_list) + list(out_list)):
+            return real["a2a_list"](out_list, in_list, group=group, async_op=async_op)
+        cur, snaps, host = _begin(list(in_list))
+        in_splits = [h.numel() for h in host]
+        out_splits = [o.numel() for o in out_list]
+        flat = torch.cat([h.reshape(-1) for h in host]) if host else torch.empty(0)
+        o = torch.empty(sum(out_splits), dtype=out_list[0].dtype)
+        real["a2a"](o, flat, out_splits, in_splits, group=group)
+        outs = [(d, part.view(d.shape)) for d, part in zip(out_list, o.split(out_splits))]
+        return _deliver(group, cur, list(in_list), snaps, outs, async_op)
 
     def batch_isend_irecv(ops):
         sends = [op for op in ops if op.op in (tdist.isend, real["isend"])]
@@ -187,6 +200,7 @@ def install(delay_cycles: int = 2_000_000) -> None:
         return f
 
     tdist.all_to_all_single = timed(a2a)
+    tdist.all_to_all = timed(all_to_all)
     tdist.batch_isend_irecv = timed(batch_isend_irecv)
     tdist.all_reduce = timed(all_reduce)
     tdist.all_gather = timed(all_gather)
