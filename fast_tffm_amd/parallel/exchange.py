@@ -264,10 +264,10 @@ class ShardExchange(_Base):
         self.self_rows = (self.dev.type == "cuda" and self.wire.dtype == tdt and self.nparts == 1
                           and os.environ.get("FM_SELF_ROWS", "1") != "0")
         # world 1 with self rows: every row is this rank's and exclusive and a key is its table
-        # row (owner 0), so training steps run the local step's forward and backward (table rows,
-        # LOCAL-mode in-place update: the specialised kernels, one backward pass, no gradient rows,
-        # no apply) and their plans skip the key transform and the segment index
-        # (profiles/r4/shard_w1_local.txt); world > 1 keeps EMIT + the exchange
+        # row (owner 0), so a training step IS the local step -- the model's own executor runs it
+        # (its dedup lookahead, the fused in-place backward: no plan, gradient rows or apply; the
+        # table is the local table) -- as dp_dense does at world 1 (profiles/r4/shard_w1_local.txt);
+        # world > 1 keeps EMIT + the exchange
         self.local_w1 = (self.self_rows and self.W == 1
                          and os.environ.get("FM_SHARD_W1_LOCAL", "1") != "0")  # (0: EMIT path, A/B)
         # Bounded staleness (FMConfig.staleness = 1): the reference trains asynchronously -- workers push
@@ -464,19 +464,15 @@ class ShardExchange(_Base):
                 part.b = sb = b if len(ranges) == 1 else _sub_batch(b, e0, e1, n0, n1, offs)
                 part.e0 = e0
                 dws = slot.ensure(k, sb.nnz, self.dev, m.cfg.dedup_chunk)
-                w1 = train and self.local_w1  # (world 1: keys = ids, no segment index)
-                if w1 and sb.ids.dtype == torch.int32 and sb.ids.is_contiguous():
-                    keys, sids = sb.ids, None
-                else:  # sharded keys: written by the dedup's sort (fused map)
-                    keys, sids = slot.keys[k][: sb.nnz], sb.ids
+                keys, sids = slot.keys[k][: sb.nnz], sb.ids  # sharded keys: written by the dedup's sort
                 shift = m._slot_bits(sb, always=True) if train else 0
                 # training plans on the GPU find each occurrence's segment through a bucket index
                 # (K.seg_index) instead of the inverse map, a 5.1M-occurrence random scatter
-                lookup = train and gpu and K.seg_lookup_enabled() and not w1
+                lookup = train and gpu and K.seg_lookup_enabled()
                 part.keys = keys
                 # (training: occurrence codes generated inside the sort -- csr_rows fused)
                 part.dd = K.dedup(keys, ws=dws, key_bits=self.key_bits, gen_codes=train,
-                                  vals=sb.vals if train else None, want_inv=not (lookup or w1),
+                                  vals=sb.vals if train else None, want_inv=not lookup,
                                   num_examples=sb.B, Kp=self.m.Kp, ex_shift=shift,
                                   offsets=sb.offsets if train else None, shard_ids=sids, shard=(self.W, self.Rps))
                 part.seg = K.seg_index(part.dd, self.key_bits, slot.segidx_buf(k)) if lookup else None
@@ -567,7 +563,7 @@ class ShardExchange(_Base):
         gpu = self.dev.type == "cuda"
         if self.staleness:  # (no dirty scan against the current plan: every row is read stale)
             return pl.train and len(pl.parts) == 1 and pl.splits is not None and (pl.run_off is not None or not gpu)
-        if self.local_w1 or (pl.self_r is not None and pl.self_r[1] - pl.self_r[0] == pl.R):
+        if pl.self_r is not None and pl.self_r[1] - pl.self_r[0] == pl.R:
             return False  # every request is this rank's own row (world 1): nothing to exchange early
         return (self.prefetch and len(pl.parts) == 1 and pl.splits is not None and cur is not None
                 and cur.splits is not None and (cur.run_off is not None or not gpu) and len(cur.parts) == 1
@@ -1077,6 +1073,10 @@ class ShardExchange(_Base):
             self._main = torch.cuda.current_stream(self.dev)
         if self.staleness:
             return self._train_step_stale(b, next_batch, next2)
+        if self.local_w1:  # (see __init__)
+            if next_batch is not None or self.m._lpending is not None:
+                return self.m._local_lookahead_step(b, next_batch, next2)
+            return self.m._local_train_step(b)
         m, ws, cfg, Kp = self.m, self.m.ws, self.m.cfg, self.Kp
         gpu = self.dev.type == "cuda"
         build = next2 if next2 is not None else next_batch
@@ -1094,9 +1094,7 @@ class ShardExchange(_Base):
         # every part's rows are gathered first and their all-to-alls queued on RCCL's stream
         # (async): part k+1's rows travel while part k computes
         with roctx_range("gather+a2a_rows"):
-            if self.local_w1:  # (the forward reads the table)
-                rows = [(None, None)] * len(pl.parts)
-            elif pl.early is not None:
+            if pl.early is not None:
                 rows = [(None, None)]
                 early_views = self._patch(pl)
                 self.early_steps += 1
@@ -1116,24 +1114,12 @@ class ShardExchange(_Base):
             srows = K.SelfRows(pl.self_u[0], pl.self_u[1], self.ctx.rank * self.Rps, pl.parts[0].dd.uniq,
                                m.table.state, pl.self_excl)
             skw = dict(self_rows=srows, opt=cfg.opt, sr_counter=sr)
-        local_w1 = self.local_w1  # (see __init__; its plans were built for it: keys = ids, no inverse map)
         # one part: the loss reduction is enqueued after the backward, as in the local step
         one_part = len(pl.parts) == 1
         for part, (buf, work) in zip(pl.parts, rows):
             sb, dd, e0 = part.b, part.dd, part.e0
             if work is not None:
                 work.wait()               # the compute stream waits for this part's rows
-            if local_w1:  # (keys are table rows: the local step's forward over the table)
-                with roctx_range("fwd_local"):
-                    fo = K.fm_forward(sb.offsets, part.keys, sb.vals, m.table.v, m.table.w, Kp, labels=sb.labels,
-                                      weights=sb.weights, loss=cfg.loss_type, grad_scale=gscale, want_r1=True,
-                                      pred=ws.pred[: sb.B], r1=ws.r1[: sb.B], dpred=ws.dpred[: sb.B],
-                                      partial=ws.fwd_partial, threads=cfg.threads, bias=m.gbias, defer_loss=True,
-                                      max_feats=sb.max_feats)
-                with roctx_range("bwd_local"):
-                    K.fm_backward(dd, fo.dpred, fo.r1, Kp, mode=K.BWD_LOCAL, table=m.table.state, opt=cfg.opt,
-                                  reg_v=rv, reg_w=rw, partial=ws.bwd_partial, threads=cfg.threads, sr_counter=sr)
-                continue
             src_v, src_w = wf.views(buf) if buf is not None else early_views
             gs = grad_send[part.u0: part.u0 + part.U]
             with roctx_range("fwd"):
@@ -1164,7 +1150,7 @@ class ShardExchange(_Base):
         for w in gworks:
             w.wait()
         with roctx_range("apply"):
-            if not local_w1 and not (srows is not None and self.W == 1):  # (world 1: updated in place)
+            if not (srows is not None and self.W == 1):  # (world 1: updated in place)
                 K.apply_runs(pl.req_recv, pl.run_off, pl.splits, grad_recv, m.table.state, cfg.opt, Kp,
                              match=pl.match, threads=cfg.threads,
                              ws=self.slots[pl.slot].ensure2(pl.R, self.dev) if not gpu else None,
