@@ -62,6 +62,19 @@ constexpr int kChunkUnr = FM_CHUNK_UNR;
 #ifndef FM_CHUNK_UNR32_EMIT
 #define FM_CHUNK_UNR32_EMIT FM_CHUNK_UNR32
 #endif
+// The wide fp8 kernel (8 values per lane, below): 5 r1 rows in flight per lane (6 spills 6 VGPRs under
+// the 128-VGPR cap, 4 one) -- about the bytes in flight of the 4-value kernel's 12.  FM_CHUNK_UNR_W8 overrides.
+#ifndef FM_CHUNK_UNR_W8
+#define FM_CHUNK_UNR_W8 5
+#endif
+// Wide fp8 chunk kernel (FM_FP8_WIDE=1, default): the local step's fp8 rows reduced with 8 values per
+// lane -- 8-byte row loads, 16-byte r1 / optimizer-state loads and stores, LPR = Kp / 8 -- instead of
+// 4 (4-, 8- and 8-byte accesses): the same bytes with half the per-lane addresses, which the gather-
+// bound kernel spends its texture-address time on.  Bitwise the same results (fm_common.h
+// store_row_fp8x8); 0 keeps the 4-value kernel (the "fp8narrow" build variant, A/B).
+#ifndef FM_FP8_WIDE
+#define FM_FP8_WIDE 1
+#endif
 template <int LPR, bool LOC, bool EMT, typename TV>
 constexpr int chunk_unr() {
   return LOC && LPR == 32 ? FM_CHUNK_UNR32
@@ -141,6 +154,39 @@ __device__ inline void* state_row(void* s, long long row, long long stride) {
   return row_ptr(reinterpret_cast<float*>(s), row, stride);
 }
 
+// g_v of one element, A - Scx v + reg n_u v, in a fixed fma order: the rounding is not left to the
+// compiler's contraction, which differed between instantiations of different lane widths (1 ulp on
+// rare elements: the wide fp8 kernel against the 4-value one)
+__device__ __forceinline__ float row_grad(float A, float Scx, float nreg_v, float v) {
+  return __builtin_fmaf(nreg_v, v, __builtin_fmaf(-Scx, v, A));
+}
+
+// EPL values of a table row for this lane: one Frag, or -- the wide fp8 kernel -- 8 fp8 values in
+// one 8-byte load.
+template <typename TV, int EPL>
+__device__ inline void frag_load(const TV* p, float (&o)[EPL]) {
+  if constexpr (EPL == Frag<TV>::N) {
+    Frag<TV>::load(p, o);
+  } else {
+    static_assert(std::is_same<TV, fp8e4m3>::value && EPL == 8, "wide rows: fp8, 8 values per lane");
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    float lo[4], hi[4];
+    Frag<TV>::cvt((int)u.x, lo);
+    Frag<TV>::cvt((int)u.y, hi);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o[k] = lo[k];
+      o[k + 4] = hi[k];
+    }
+  }
+}
+template <int LPR, typename TV, int EPL>
+__device__ inline void store_row_e(TV* lane_ptr, const float (&o)[EPL], float* w, long long row, long long w_stride,
+                                   int t, bool tact, uint32_t sr) {
+  if constexpr (EPL == Frag<TV>::N) store_row<LPR, TV>(lane_ptr, o, w, row, w_stride, t, tact, sr);
+  else store_row_fp8x8<LPR>(lane_ptr, o, w, row, w_stride, t, tact, sr);
+}
+
 // LOCAL mode known at compile time (the chunk kernel's local instantiations): table row `key`,
 // optimizer applied in place, 32 x 32-bit row addressing.
 template <typename TV, int EPL>
@@ -148,7 +194,7 @@ __device__ inline void bwd_load_local(const BwdArgs& a, long long key, int tE, R
   using F = Frag<TV>;
   r.apply = true;
   r.row = key;
-  F::load(row_ptr(reinterpret_cast<const TV*>(a.v), r.row, a.v_stride) + tE * EPL, r.vv);
+  frag_load<TV, EPL>(row_ptr(reinterpret_cast<const TV*>(a.v), r.row, a.v_stride) + tE * EPL, r.vv);
   const float* wr = row_ptr(static_cast<const float*>(a.w), r.row, a.w_stride);
   r.wv = wr[0];
   if constexpr (F::kScaled) {
@@ -174,11 +220,11 @@ __device__ inline void bwd_finish_local(const BwdArgs& a, int t, bool tact, RowS
   const float nreg_v = a.reg_v * (float)n_u, nreg_w = a.reg_w * (float)n_u;
   float gr[EPL];
 #pragma unroll
-  for (int k = 0; k < EPL; ++k) gr[k] = A[k] - Scx * r.vv[k] + nreg_v * r.vv[k];
+  for (int k = 0; k < EPL; ++k) gr[k] = row_grad(A[k], Scx, nreg_v, r.vv[k]);
   const float gw = Sc + nreg_w * r.wv;
   TV* tv = reinterpret_cast<TV*>(a.v);
   opt_step_row<TV, EPL>(a.opt, gr, r.vv, r.st0, r.st1);
-  store_row<LPR, TV>(row_ptr(tv, r.row, a.v_stride) + t * EPL, r.vv, a.w, r.row, a.w_stride, t, tact, sr);
+  store_row_e<LPR, TV, EPL>(row_ptr(tv, r.row, a.v_stride) + t * EPL, r.vv, a.w, r.row, a.w_stride, t, tact, sr);
   if (tact) {
     store_state<TV, EPL>(state_row<TV>(a.s0v, r.row, a.s_stride), t * EPL, r.st0, sr ? sr ^ kSrSalt0 : 0u,
                          (uint32_t)r.row, (uint32_t)(t * EPL));
@@ -232,7 +278,7 @@ __device__ inline void bwd_finish_emit(const BwdArgs& a, int u, int t, bool tact
   const float nreg_v = a.reg_v * (float)n_u, nreg_w = a.reg_w * (float)n_u;
   float gr[EPL];
 #pragma unroll
-  for (int k = 0; k < EPL; ++k) gr[k] = A[k] - Scx * r.vv[k] + nreg_v * r.vv[k];
+  for (int k = 0; k < EPL; ++k) gr[k] = row_grad(A[k], Scx, nreg_v, r.vv[k]);
   const float gw = Sc + nreg_w * r.wv;
   if (!r.apply) {  // gradient row u for its owner's apply
     float* dst = row_ptr(a.grad_out, (long long)u, a.g_stride);
@@ -319,7 +365,7 @@ __device__ inline void bwd_finish(const BwdArgs& a, int u, int t, bool tact, Row
   const float nreg_v = a.reg_v * (float)n_u, nreg_w = a.reg_w * (float)n_u;
   float gr[EPL];
 #pragma unroll
-  for (int k = 0; k < EPL; ++k) gr[k] = A[k] - Scx * r.vv[k] + nreg_v * r.vv[k];
+  for (int k = 0; k < EPL; ++k) gr[k] = row_grad(A[k], Scx, nreg_v, r.vv[k]);
   const float gw = Sc + nreg_w * r.wv;
   if (!r.apply) {
     float* dst = a.grad_out + (a.mode == kBwdEmitTable ? r.row : (long long)u) * a.g_stride;
@@ -402,7 +448,7 @@ enum ChunkKind : int {
 #endif
 
 // One lane group per chunk of <= CH (<= kMaxCH) sorted occurrences of one row.
-template <int LPR, typename TV, int KV>
+template <int LPR, typename TV, int KV, int EW = 0>
 __device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
   constexpr bool FAST = KV != kChunkAny;                                   // 32-bit offsets, bpermute
   constexpr bool LOC = KV == kChunkLocal || KV == kChunkLocalNoX;          // local epilogue
@@ -410,11 +456,13 @@ __device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
   constexpr bool NOX = KV == kChunkLocalNoX || KV == kChunkEmitNoX || KV == kChunkEmitPcNoX;
   constexpr bool PCW = KV == kChunkAny || KV == kChunkEmitPc || KV == kChunkEmitPcNoX;  // piece walk
   const uint32_t sr = sr_step_seed(a.sr_counter);  // stochastic rounding seed (0: nearest)
-  constexpr int EPL = Frag<TV>::N;  // elements per lane of the table dtype
+  constexpr int EPL = EW ? EW : Frag<TV>::N;  // elements per lane: the table dtype's, or the wide kernel's 8
+  static_assert(EW == 0 || LOC, "the wide kernel is a local-step kernel");
   constexpr int G = kWave / LPR;
   constexpr int PF = (kMaxCH + LPR - 1) / LPR;  // prefetched occurrences per lane
-  constexpr int UNR = LPR < chunk_unr<LPR, LOC, EMT, TV>() ? LPR : chunk_unr<LPR, LOC, EMT, TV>();  // r1 rows in flight
-  constexpr bool kShortPath = LPR >= 32;                          // short-chunk block (below)
+  constexpr int UNR0 = EW ? FM_CHUNK_UNR_W8 : chunk_unr<LPR, LOC, EMT, TV>();
+  constexpr int UNR = LPR < UNR0 ? LPR : UNR0;  // r1 rows in flight
+  constexpr bool kShortPath = LPR * EPL >= 128;                   // short-chunk block (below): k = 128 rows
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR, t = lane % LPR;
   const int gbase = g * LPR;
@@ -519,6 +567,8 @@ __device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
       px[q] = x;
       pc[q] = ok ? a.dpred[ex] * x : 0.f;
     }
+    // (the sums below are explicit fma chains: contraction left to the compiler fused some multiply-adds
+    // and not others depending on the instantiation -- 1-ulp differences between lane widths)
     float A[EPL];
 #pragma unroll
     for (int k = 0; k < EPL; ++k) A[k] = 0.f;
@@ -565,8 +615,8 @@ __device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
 #pragma unroll
         for (int uu = 0; uu < UNRF; ++uu) {
 #pragma unroll
-          for (int k = 0; k < EPL; ++k) A[k] += cc[uu] * rr[uu][k];
-          Scx += cc[uu] * xx[uu];
+          for (int k = 0; k < EPL; ++k) A[k] = __builtin_fmaf(cc[uu], rr[uu][k], A[k]);
+          Scx = __builtin_fmaf(cc[uu], xx[uu], Scx);
           Sc += cc[uu];
         }
       }
@@ -587,8 +637,8 @@ __device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
 #pragma unroll
       for (int uu = 0; uu < U4; ++uu) {
 #pragma unroll
-        for (int k = 0; k < EPL; ++k) A[k] += cc[uu] * rr[uu][k];
-        Scx += cc[uu] * xx[uu];
+        for (int k = 0; k < EPL; ++k) A[k] = __builtin_fmaf(cc[uu], rr[uu][k], A[k]);
+        Scx = __builtin_fmaf(cc[uu], xx[uu], Scx);
         Sc += cc[uu];
       }
     } else {
@@ -608,8 +658,8 @@ __device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
 #pragma unroll
             for (int uu = 0; uu < UNR; ++uu) {
 #pragma unroll
-              for (int k = 0; k < EPL; ++k) A[k] += cc[uu] * rr[uu][k];
-              Scx += cc[uu] * xx[uu];
+              for (int k = 0; k < EPL; ++k) A[k] = __builtin_fmaf(cc[uu], rr[uu][k], A[k]);
+              Scx = __builtin_fmaf(cc[uu], xx[uu], Scx);
               Sc += cc[uu];
             }
           }
@@ -651,6 +701,15 @@ void fm_bwd_chunk_local_kernel(BwdArgs a) { bwd_chunk_body<LPR, TV, kChunkLocal>
 template <int LPR, typename TV>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(chunk_min_waves<LPR, TV>())))
 void fm_bwd_chunk_local_nox_kernel(BwdArgs a) { bwd_chunk_body<LPR, TV, kChunkLocalNoX>(a); }
+#if FM_FP8_WIDE
+// the wide fp8 kernels (8 values per lane; LPR = Kp / 8): 128-VGPR cap as the 32-lane fp8 kernels
+template <int LPR>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+void fm_bwd_chunk_local_w8_kernel(BwdArgs a) { bwd_chunk_body<LPR, fp8e4m3, kChunkLocal, 8>(a); }
+template <int LPR>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+void fm_bwd_chunk_local_nox_w8_kernel(BwdArgs a) { bwd_chunk_body<LPR, fp8e4m3, kChunkLocalNoX, 8>(a); }
+#endif
 #define FM_EMIT_CHUNK_KERNEL(NAME, KIND)                                                          \
   template <int LPR, typename TV>                                                                 \
   __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(chunk_min_waves<LPR, TV>()))) \
@@ -803,6 +862,9 @@ static bool fast_kind(int kind) { return kind != kChunkAny; }
 
 static int chunk_wg_per_cu(int lpr, int kind) { return fast_kind(kind) && lpr <= 16 ? 3 : 0; }
 
+static long long g_bwd_wide_launches = 0;  // (host counter: tests check the wide kernel ran)
+long long bwd_wide_launches() { return g_bwd_wide_launches; }
+
 int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_unique, hipStream_t st) {
   if (max_chunks <= 0) return 0;
   const int lpr = lanes_per_row(a.Kp, dtype);
@@ -851,6 +913,22 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   const bool pcw = kind == kChunkAny || kind == kChunkEmitPc || kind == kChunkEmitPcNoX;
   const int chunk_static_lds = pcw ? (int)sizeof(int) * (2 * kMaxPieceOwners + 1) : 0;  // piece walk
   const int chunk_lds = wg_cu > 0 ? lds_for_wg_per_cu(wg_cu, chunk_static_lds) : 0;
+  // wide fp8 rows (k = 128, 16 lanes x 8 values): rows, r1 rows and state rows 16-byte aligned
+  const bool wide = FM_FP8_WIDE && dtype == kFP8 && lpr == 32 && a.Kp % 8 == 0 &&
+                    (kind == kChunkLocal || kind == kChunkLocalNoX) && a.v_stride % 8 == 0 && a.s_stride % 8 == 0 &&
+                    ((uintptr_t)a.v % 8 == 0) && ((uintptr_t)a.r1 % 16 == 0) && ((uintptr_t)a.s0v % 16 == 0) &&
+                    ((uintptr_t)a.s1v % 16 == 0);
+  (void)wide;
+#if FM_FP8_WIDE
+  if (wide) {
+    ++g_bwd_wide_launches;
+    const int gw = (fill_grid(max_chunks, kWavesPerBlock * (kWave / 16), 8192) + 7) / 8 * 8;
+    if (kind == kChunkLocalNoX)
+      hipLaunchKernelGGL(fm_bwd_chunk_local_nox_w8_kernel<16>, dim3(gw), dim3(kBlock), chunk_lds, st, a);
+    else
+      hipLaunchKernelGGL(fm_bwd_chunk_local_w8_kernel<16>, dim3(gw), dim3(kBlock), chunk_lds, st, a);
+  } else
+#endif
   if (kind == kChunkLocalNoX) {
     FM_DISPATCH_WIDE(dtype, lpr, fm_bwd_chunk_local_nox_kernel, g1, chunk_lds, st, a);
   } else if (kind == kChunkLocal) {

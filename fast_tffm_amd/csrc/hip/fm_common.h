@@ -198,21 +198,29 @@ template <> struct Frag<fp8e4m3> {
     const auto hi = __builtin_amdgcn_cvt_scalef32_pk_f32_fp8(u, s, true);
     o[0] = lo[0]; o[1] = lo[1]; o[2] = hi[0]; o[3] = hi[1];
   }
-  // (store / store_sr return the 4 stored bytes: the row norm is taken from them)
-  __device__ static inline int store(fp8e4m3* p, const float (&o)[4]) {
+  // the 4 bytes of 4 values (round to nearest even)
+  __device__ static inline int pack(const float (&o)[4]) {
     int u = __builtin_amdgcn_cvt_pk_fp8_f32(o[0], o[1], 0, false);
-    u = __builtin_amdgcn_cvt_pk_fp8_f32(o[2], o[3], u, true);
-    *reinterpret_cast<int*>(p) = u;
-    return u;
+    return __builtin_amdgcn_cvt_pk_fp8_f32(o[2], o[3], u, true);
   }
-  // gfx950 v_cvt_sr_fp8_f32: hardware stochastic rounding with the given random bits
-  __device__ static inline int store_sr(fp8e4m3* p, const float (&o)[4], uint32_t seed, uint32_t row,
-                                        uint32_t col) {
+  // gfx950 v_cvt_sr_fp8_f32: hardware stochastic rounding with the given random bits (values of
+  // columns col .. col + 3 of `row`)
+  __device__ static inline int pack_sr(const float (&o)[4], uint32_t seed, uint32_t row, uint32_t col) {
     const uint32_t r0 = sr_hash(seed, row, col);
     int u = __builtin_amdgcn_cvt_sr_fp8_f32(o[0], (int)r0, 0, 0);
     u = __builtin_amdgcn_cvt_sr_fp8_f32(o[1], (int)sr_word(r0, 1), u, 1);
     u = __builtin_amdgcn_cvt_sr_fp8_f32(o[2], (int)sr_word(r0, 2), u, 2);
-    u = __builtin_amdgcn_cvt_sr_fp8_f32(o[3], (int)sr_word(r0, 3), u, 3);
+    return __builtin_amdgcn_cvt_sr_fp8_f32(o[3], (int)sr_word(r0, 3), u, 3);
+  }
+  // (store / store_sr return the 4 stored bytes: the row norm is taken from them)
+  __device__ static inline int store(fp8e4m3* p, const float (&o)[4]) {
+    const int u = pack(o);
+    *reinterpret_cast<int*>(p) = u;
+    return u;
+  }
+  __device__ static inline int store_sr(fp8e4m3* p, const float (&o)[4], uint32_t seed, uint32_t row,
+                                        uint32_t col) {
+    const int u = pack_sr(o, seed, row, col);
     *reinterpret_cast<int*>(p) = u;
     return u;
   }
@@ -241,16 +249,33 @@ __device__ inline float group_max(float v) {
 template <typename TV> struct R1Bf16 { static constexpr bool v = false; };
 template <> struct R1Bf16<fp8e4m3> { static constexpr bool v = true; };
 
-template <typename TV, int EPL>
-__device__ inline void load_r1(const void* r1, long long off, float (&o)[EPL]) {
-  if constexpr (R1Bf16<TV>::v) {
-    const uint16_t* p = reinterpret_cast<const uint16_t*>(r1) + off;
+// EPL bf16 values (8-byte aligned; 16-byte loads when EPL is a multiple of 8 -- the wide fp8 chunk kernel,
+// whose rows and r1 rows are then 16-byte aligned: half the address work per byte of the 8-byte form)
+template <int EPL>
+__device__ inline void load_bf16x(const uint16_t* p, float (&o)[EPL]) {
+  if constexpr (EPL % 8 == 0) {
+#pragma unroll
+    for (int k = 0; k < EPL; k += 8) {
+      const uint4 h = *reinterpret_cast<const uint4*>(p + k);
+      o[k] = bf16_bits_to_f32(h.x & 0xffffu); o[k + 1] = bf16_bits_to_f32(h.x >> 16);
+      o[k + 2] = bf16_bits_to_f32(h.y & 0xffffu); o[k + 3] = bf16_bits_to_f32(h.y >> 16);
+      o[k + 4] = bf16_bits_to_f32(h.z & 0xffffu); o[k + 5] = bf16_bits_to_f32(h.z >> 16);
+      o[k + 6] = bf16_bits_to_f32(h.w & 0xffffu); o[k + 7] = bf16_bits_to_f32(h.w >> 16);
+    }
+  } else {
 #pragma unroll
     for (int k = 0; k < EPL; k += 4) {
       const uint2 h = *reinterpret_cast<const uint2*>(p + k);
       o[k] = bf16_bits_to_f32(h.x & 0xffffu); o[k + 1] = bf16_bits_to_f32(h.x >> 16);
       o[k + 2] = bf16_bits_to_f32(h.y & 0xffffu); o[k + 3] = bf16_bits_to_f32(h.y >> 16);
     }
+  }
+}
+
+template <typename TV, int EPL>
+__device__ inline void load_r1(const void* r1, long long off, float (&o)[EPL]) {
+  if constexpr (R1Bf16<TV>::v) {
+    load_bf16x<EPL>(reinterpret_cast<const uint16_t*>(r1) + off, o);
   } else {
     const float* p = reinterpret_cast<const float*>(r1) + off;
 #pragma unroll
@@ -290,13 +315,7 @@ template <> struct StateBf16<fp8e4m3> { static constexpr bool v = true; };
 template <typename TV, int EPL>
 __device__ inline void load_state(const void* s, long long off, float (&o)[EPL]) {
   if constexpr (StateBf16<TV>::v) {
-    const uint16_t* p = reinterpret_cast<const uint16_t*>(s) + off;
-#pragma unroll
-    for (int k = 0; k < EPL; k += 4) {
-      const uint2 h = *reinterpret_cast<const uint2*>(p + k);
-      o[k] = bf16_bits_to_f32(h.x & 0xffffu); o[k + 1] = bf16_bits_to_f32(h.x >> 16);
-      o[k + 2] = bf16_bits_to_f32(h.y & 0xffffu); o[k + 3] = bf16_bits_to_f32(h.y >> 16);
-    }
+    load_bf16x<EPL>(reinterpret_cast<const uint16_t*>(s) + off, o);
   } else {
     const float* p = reinterpret_cast<const float*>(s) + off;
 #pragma unroll
@@ -313,18 +332,28 @@ __device__ inline void store_state(void* s, long long off, const float (&o)[EPL]
                                    uint32_t col) {
   if constexpr (StateBf16<TV>::v) {
     uint16_t* p = reinterpret_cast<uint16_t*>(s) + off;
+    // (random bits per 4 values, salted by their first column: the same bits for any EPL)
+    uint32_t b[EPL];
 #pragma unroll
     for (int k = 0; k < EPL; k += 4) {
-      uint32_t b[4];
       if (seed) {
         const uint32_t r = sr_hash(seed, row, col + (uint32_t)k);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) b[i] = f32_to_bf16_bits_sr(o[k + i], sr_word(r, i));
+        for (int i = 0; i < 4; ++i) b[k + i] = f32_to_bf16_bits_sr(o[k + i], sr_word(r, i));
       } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) b[i] = f32_to_bf16_bits(o[k + i]);
+        for (int i = 0; i < 4; ++i) b[k + i] = f32_to_bf16_bits(o[k + i]);
       }
-      *reinterpret_cast<uint2*>(p + k) = make_uint2(b[0] | (b[1] << 16), b[2] | (b[3] << 16));
+    }
+    if constexpr (EPL % 8 == 0) {
+#pragma unroll
+      for (int k = 0; k < EPL; k += 8)
+        *reinterpret_cast<uint4*>(p + k) = make_uint4(b[k] | (b[k + 1] << 16), b[k + 2] | (b[k + 3] << 16),
+                                                      b[k + 4] | (b[k + 5] << 16), b[k + 6] | (b[k + 7] << 16));
+    } else {
+#pragma unroll
+      for (int k = 0; k < EPL; k += 4)
+        *reinterpret_cast<uint2*>(p + k) = make_uint2(b[k] | (b[k + 1] << 16), b[k + 2] | (b[k + 3] << 16));
     }
   } else {
     float* p = reinterpret_cast<float*>(s) + off;
@@ -386,6 +415,47 @@ __device__ inline void store_row(TV* lane_ptr, const float (&o)[Frag<TV>::N], fl
       if (sr_seed) F::store_sr(lane_ptr, o, sr_seed, (uint32_t)row, col);
       else F::store(lane_ptr, o);
     }
+  }
+}
+
+// store_row for fp8 rows held 8 values per lane (the wide chunk kernel, LPR = Kp / 8): the same bytes,
+// row scale and norm as store_row<2 LPR, fp8> over 4-value lanes -- lane t's halves are the 4-value
+// lanes 2t and 2t + 1 (their stochastic-rounding columns), and the norm's butterfly is theirs: over the
+// halves' partner lanes first, the two halves added last (the 4-value butterfly's last step).
+template <int LPR>
+__device__ inline void store_row_fp8x8(fp8e4m3* lane_ptr, const float (&o)[8], float* w, long long row,
+                                       long long w_stride, int t, bool tact, uint32_t sr_seed) {
+  using F = Frag<fp8e4m3>;
+  float m = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) m = fmaxf(m, fabsf(o[k]));
+  m = group_max<LPR>(m);
+  const float s = fp8_row_scale(m);
+  const float inv = 1.f / s;  // (exact: s is a power of two)
+  float qa[4], qb[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    qa[k] = fminf(fmaxf(o[k] * inv, -kFp8Max), kFp8Max);
+    qb[k] = fminf(fmaxf(o[k + 4] * inv, -kFp8Max), kFp8Max);
+  }
+  const uint32_t col = (uint32_t)(t * 8);
+  int ua = 0, ub = 0;
+  if (tact) {
+    ua = sr_seed ? F::pack_sr(qa, sr_seed, (uint32_t)row, col) : F::pack(qa);
+    ub = sr_seed ? F::pack_sr(qb, sr_seed, (uint32_t)row, col + 4) : F::pack(qb);
+    *reinterpret_cast<uint2*>(lane_ptr) = make_uint2((uint32_t)ua, (uint32_t)ub);
+  }
+  float pa[4], pb[4];
+  F::cvt(ua, pa);
+  F::cvt(ub, pb);
+  float na = tact ? __fmaf_rn(pa[0], pa[0], __fmaf_rn(pa[1], pa[1], __fmaf_rn(pa[2], pa[2], pa[3] * pa[3]))) : 0.f;
+  float nb = tact ? __fmaf_rn(pb[0], pb[0], __fmaf_rn(pb[1], pb[1], __fmaf_rn(pb[2], pb[2], pb[3] * pb[3]))) : 0.f;
+  na = group_sum<LPR>(na);
+  nb = group_sum<LPR>(nb);
+  const float n2 = (na + nb) * (s * s);
+  if (t == 0) {
+    w[row * w_stride + 1] = s;
+    w[row * w_stride + kFp8Norm] = n2;
   }
 }
 
@@ -466,7 +536,9 @@ __device__ inline void opt_step_tv(const OptParams& o, float g, float& p, float&
       const float ilr = __builtin_amdgcn_rcpf(o.lr);  // (wave-uniform: hoisted by the compiler)
       const float n_new = __builtin_fmaf(g, g, s0);
       const float sq_old = __builtin_amdgcn_sqrtf(s0), sq_new = __builtin_amdgcn_sqrtf(n_new);
-      s1 += g - (sq_new - sq_old) * ilr * p;
+      // (explicit fma / mul order: the rounding is fixed, not left to contraction, so every writer and
+      // every lane width -- the wide fp8 chunk kernel -- produces the same bits)
+      s1 += __builtin_fmaf(-((sq_new - sq_old) * ilr), p, g);
       s0 = n_new;
       const float quad = __builtin_fmaf(o.beta + sq_new, ilr, 2.f * o.l2);
       p = fabsf(s1) > o.l1 ? (copysignf(o.l1, s1) - s1) * __builtin_amdgcn_rcpf(quad) : 0.f;
@@ -474,7 +546,7 @@ __device__ inline void opt_step_tv(const OptParams& o, float g, float& p, float&
     }
     if (o.type == kOptAdagrad) {
       s0 = __builtin_fmaf(g, g, s0);
-      p -= o.lr * g * __builtin_amdgcn_rsqf(s0);
+      p = __builtin_fmaf(-(o.lr * g), __builtin_amdgcn_rsqf(s0), p);
       return;
     }
   }

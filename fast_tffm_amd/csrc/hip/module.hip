@@ -201,6 +201,7 @@ PYBIND11_MODULE(FM_HIP_MODULE, m) {
       py::arg("keys"), py::arg("vals"), py::arg("kout"), py::arg("vout"), py::arg("n"), py::arg("end_bit"),
       py::arg("ws"), py::arg("ws_bytes"), py::arg("stream"));
   m.def("radix_sort_ws_bytes", &fm::radix_sort_ws_bytes, py::arg("n"));
+  m.def("bwd_wide_launches", &fm::bwd_wide_launches);  // launches of the wide fp8 chunk kernel so far
   m.def("set_sort_spin_cap", &fm::set_sort_spin_cap, py::arg("cap"));  // (< 0: injected look-back failure)
   m.def(
       "device_errors",  // the current device's sticky error word (synchronous), cleared when `clear`
