@@ -38,11 +38,14 @@ for sr, va, vb in ((False, None, None), (False, "fp8narrow", "fp8narrow"), (True
     print(f"== {va} vs {vb}")
     a, n = run(va, sr), run(vb, sr)
     for name, x, y in zip(("v", "s0v", "s1v"), a, n):
-        d = (x.view(torch.uint8 if x.dtype == K.FP8 else torch.int16) != y.view(torch.uint8 if y.dtype == K.FP8 else torch.int16))
+        bits = torch.uint8 if x.dtype == K.FP8 else torch.int16
+        d = x.view(bits) != y.view(bits)
         idx = d.nonzero()
         print(f"sr={sr} {name}: {idx.shape[0]} mismatches", flush=True)
         for r, c in idx[:12].tolist():
-            print(f"   row {r} col {c} count {int(cnt[r])}  wide {float(x[r, c].float()):.9e}  narrow {float(y[r, c].float()):.9e}")
+            print(f"   row {r} col {c} count {int(cnt[r])}  a {float(x[r, c].float()):.9e}  "
+                  f"b {float(y[r, c].float()):.9e}")
         if idx.shape[0]:
             rows = idx[:, 0].unique()
-            print("   occurrence counts of mismatching rows:", torch.bincount(cnt[rows].clamp(max=40)).nonzero().flatten().tolist())
+            print("   occurrence counts of mismatching rows:",
+                  torch.bincount(cnt[rows].clamp(max=40)).nonzero().flatten().tolist())
