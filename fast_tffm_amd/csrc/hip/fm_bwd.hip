@@ -251,7 +251,7 @@ __device__ inline void bwd_load_emit(const BwdArgs& a, int u, long long key, int
   r.row = own ? key - a.self.base : (long long)u;
   const TV* vsrc = reinterpret_cast<const TV*>(own ? a.self.v : a.v);
   const float* wsrc = own ? a.self.w : a.w;
-  F::load(row_ptr(vsrc, r.row, own ? a.self.v_stride : a.v_stride) + tE * EPL, r.vv);
+  frag_load<TV, EPL>(row_ptr(vsrc, r.row, own ? a.self.v_stride : a.v_stride) + tE * EPL, r.vv);
   const float* wr = row_ptr(wsrc, r.row, own ? a.self.w_stride : a.w_stride);
   r.wv = wr[0];
   if constexpr (F::kScaled) {
@@ -304,8 +304,8 @@ __device__ inline void bwd_finish_emit(const BwdArgs& a, int u, int t, bool tact
   // exclusive own row: the optimizer in place on this rank's table
   TV* tv = reinterpret_cast<TV*>(const_cast<void*>(a.self.v));
   opt_step_row<TV, EPL>(a.opt, gr, r.vv, r.st0, r.st1);
-  store_row<LPR, TV>(row_ptr(tv, r.row, a.self.v_stride) + t * EPL, r.vv, a.self.w, r.row, a.self.w_stride, t, tact,
-                     sr);
+  store_row_e<LPR, TV, EPL>(row_ptr(tv, r.row, a.self.v_stride) + t * EPL, r.vv, a.self.w, r.row, a.self.w_stride, t,
+                            tact, sr);
   if (tact) {
     store_state<TV, EPL>(state_row<TV>(a.s0v, r.row, a.s_stride), t * EPL, r.st0, sr ? sr ^ kSrSalt0 : 0u,
                          (uint32_t)r.row, (uint32_t)(t * EPL));
@@ -457,7 +457,7 @@ __device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
   constexpr bool PCW = KV == kChunkAny || KV == kChunkEmitPc || KV == kChunkEmitPcNoX;  // piece walk
   const uint32_t sr = sr_step_seed(a.sr_counter);  // stochastic rounding seed (0: nearest)
   constexpr int EPL = EW ? EW : Frag<TV>::N;  // elements per lane: the table dtype's, or the wide kernel's 8
-  static_assert(EW == 0 || LOC, "the wide kernel is a local-step kernel");
+  static_assert(EW == 0 || LOC || EMT, "the wide kernels: local and EMIT kinds");
   constexpr int G = kWave / LPR;
   constexpr int PF = (kMaxCH + LPR - 1) / LPR;  // prefetched occurrences per lane
   constexpr int UNR0 = EW ? FM_CHUNK_UNR_W8 : chunk_unr<LPR, LOC, EMT, TV>();
@@ -719,6 +719,12 @@ FM_EMIT_CHUNK_KERNEL(fm_bwd_chunk_emit_nox_kernel, kChunkEmitNoX)
 FM_EMIT_CHUNK_KERNEL(fm_bwd_chunk_emit_pc_kernel, kChunkEmitPc)
 FM_EMIT_CHUNK_KERNEL(fm_bwd_chunk_emit_pc_nox_kernel, kChunkEmitPcNoX)
 #undef FM_EMIT_CHUNK_KERNEL
+#if FM_FP8_WIDE
+// (the row-sharded step's wide fp8 kernels: wire / own-table rows, gradient rows or in-place own rows)
+template <int KIND>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+void fm_bwd_chunk_emit_w8_kernel(BwdArgs a) { bwd_chunk_body<16, fp8e4m3, KIND, 8>(a); }
+#endif
 
 // Rows split over 2..kSmallChunks chunks: one lane group, ordered sum of the partials.
 template <int LPR, typename TV>
@@ -914,19 +920,37 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   const int chunk_static_lds = pcw ? (int)sizeof(int) * (2 * kMaxPieceOwners + 1) : 0;  // piece walk
   const int chunk_lds = wg_cu > 0 ? lds_for_wg_per_cu(wg_cu, chunk_static_lds) : 0;
   // wide fp8 rows (k = 128, 16 lanes x 8 values): rows, r1 rows and state rows 16-byte aligned
-  const bool wide = FM_FP8_WIDE && dtype == kFP8 && lpr == 32 && a.Kp % 8 == 0 &&
-                    (kind == kChunkLocal || kind == kChunkLocalNoX) && a.v_stride % 8 == 0 && a.s_stride % 8 == 0 &&
-                    ((uintptr_t)a.v % 8 == 0) && ((uintptr_t)a.r1 % 16 == 0) && ((uintptr_t)a.s0v % 16 == 0) &&
-                    ((uintptr_t)a.s1v % 16 == 0);
+  // (EMIT: wire rows and own table rows 8-byte aligned too)
+  const bool emit_kind = kind >= kChunkEmit;
+  const bool wide = FM_FP8_WIDE && dtype == kFP8 && lpr == 32 && a.Kp % 8 == 0 && fast_kind(kind) &&
+                    a.v_stride % 8 == 0 && a.s_stride % 8 == 0 && ((uintptr_t)a.v % 8 == 0) &&
+                    ((uintptr_t)a.r1 % 16 == 0) && ((uintptr_t)a.s0v % 16 == 0) && ((uintptr_t)a.s1v % 16 == 0) &&
+                    (!emit_kind || (a.self.v_stride % 8 == 0 && (uintptr_t)a.self.v % 8 == 0));
   (void)wide;
 #if FM_FP8_WIDE
   if (wide) {
     ++g_bwd_wide_launches;
     const int gw = (fill_grid(max_chunks, kWavesPerBlock * (kWave / 16), 8192) + 7) / 8 * 8;
-    if (kind == kChunkLocalNoX)
-      hipLaunchKernelGGL(fm_bwd_chunk_local_nox_w8_kernel<16>, dim3(gw), dim3(kBlock), chunk_lds, st, a);
-    else
-      hipLaunchKernelGGL(fm_bwd_chunk_local_w8_kernel<16>, dim3(gw), dim3(kBlock), chunk_lds, st, a);
+    switch (kind) {
+      case kChunkLocalNoX:
+        hipLaunchKernelGGL(fm_bwd_chunk_local_nox_w8_kernel<16>, dim3(gw), dim3(kBlock), chunk_lds, st, a);
+        break;
+      case kChunkLocal:
+        hipLaunchKernelGGL(fm_bwd_chunk_local_w8_kernel<16>, dim3(gw), dim3(kBlock), chunk_lds, st, a);
+        break;
+      case kChunkEmit:
+        hipLaunchKernelGGL(fm_bwd_chunk_emit_w8_kernel<kChunkEmit>, dim3(gw), dim3(kBlock), chunk_lds, st, a);
+        break;
+      case kChunkEmitNoX:
+        hipLaunchKernelGGL(fm_bwd_chunk_emit_w8_kernel<kChunkEmitNoX>, dim3(gw), dim3(kBlock), chunk_lds, st, a);
+        break;
+      case kChunkEmitPc:
+        hipLaunchKernelGGL(fm_bwd_chunk_emit_w8_kernel<kChunkEmitPc>, dim3(gw), dim3(kBlock), chunk_lds, st, a);
+        break;
+      default:
+        hipLaunchKernelGGL(fm_bwd_chunk_emit_w8_kernel<kChunkEmitPcNoX>, dim3(gw), dim3(kBlock), chunk_lds, st, a);
+        break;
+    }
   } else
 #endif
   if (kind == kChunkLocalNoX) {

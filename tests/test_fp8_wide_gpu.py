@@ -6,6 +6,8 @@ butterfly: fm_common.h store_row_fp8x8).  Adagrad and FTRL, with and without fea
 with single-occurrence rows (short block), mid-length chunks and hot rows (partials + combines).
 """
 
+import os
+
 import pytest
 import torch
 
@@ -32,13 +34,14 @@ def _batches(with_vals: bool):
     return out
 
 
-def _train(opt: str, batches):
+def _train(opt: str, batches, dist=None, split="auto"):
     o = K.OptConfig("ftrl", lr=0.05, l1=0.01, l2=0.01, beta=1.0) if opt == "ftrl" else K.OptConfig("adagrad", lr=0.05)
     cfg = FMConfig(vocabulary_size=V, factor_num=128, loss_type="logistic", batch_size=B, init_value_range=0.05, seed=3,
-                   opt=o, dtype=K.FP8, factor_lambda=0.001, bias_lambda=0.001)
-    m = FactorizationMachine(cfg, device="cuda")
-    for b in batches:
-        m.train_step(b)
+                   opt=o, dtype=K.FP8, factor_lambda=0.001, bias_lambda=0.001, mode="shard" if dist else "local",
+                   overlap_grads=split)
+    m = FactorizationMachine(cfg, device="cuda", dist=dist)
+    for i, b in enumerate(batches):
+        m.train_step(b, *batches[i + 1: i + 3]) if dist else m.train_step(b)
     torch.cuda.synchronize()
     t = m.table  # (wx: [w, scale, |v|^2, pad] per fp8 row)
     out = [x.clone() for x in (t.v, t.wx, t.s0v, t.s0w, t.s1v, t.s1w) if x is not None]
@@ -73,3 +76,41 @@ def test_wide_fp8_backward_is_bitwise_the_narrow_one(opt, with_vals, monkeypatch
             fa, fb = a.float(), b.float()
             bad[n] = (int(d.sum()), float((fa - fb).abs().max()), float(fa.abs().max()))
     assert not bad, bad
+
+
+@pytest.fixture(scope="module")
+def rccl_ctx():
+    from ports import free_port
+
+    from fast_tffm_amd.parallel import dist as fmdist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(free_port())
+    ctx = fmdist.init_distributed(backend="nccl", rank=0, world=1, device="cuda:0", force_pg=True)
+    yield ctx
+    fmdist.shutdown()
+
+
+@pytest.mark.parametrize("self_rows", ["1", "0"])
+@pytest.mark.parametrize("split", ["on", "off"])
+def test_wide_fp8_emit_backward_is_bitwise_the_narrow_one(rccl_ctx, self_rows, split, monkeypatch):
+    """The row-sharded step's EMIT kernels (RCCL world 1 on the N > 1 compute path): own rows updated in
+    place (self rows) or every row as a gradient row through the owner's apply, one pass or the split
+    backward's two pieces."""
+    from fast_tffm_amd.ops import native
+
+    monkeypatch.setenv("FM_SHARD_W1_LOCAL", "0")
+    monkeypatch.setenv("FM_SELF_ROWS", self_rows)
+    batches = _batches(True)
+    monkeypatch.delenv("FM_HIP_VARIANT", raising=False)
+    n0 = native.hip().bwd_wide_launches()
+    wide = _train("ftrl", batches, rccl_ctx, split)
+    assert native.hip().bwd_wide_launches() > n0
+    monkeypatch.setenv("FM_HIP_VARIANT", "fp8narrow")
+    try:
+        native.hip()
+    except native.NativeExtensionError as e:
+        pytest.skip(f"fp8narrow build variant not available: {e}")
+    narrow = _train("ftrl", batches, rccl_ctx, split)
+    for n, a, b in zip(["v", "wx", "s0v", "s0w", "s1v", "s1w"], wide, narrow):
+        assert torch.equal(a.view(torch.uint8), b.view(torch.uint8)), n
