@@ -154,11 +154,26 @@ __device__ inline void* state_row(void* s, long long row, long long stride) {
   return row_ptr(reinterpret_cast<float*>(s), row, stride);
 }
 
-// g_v of one element, A - Scx v + reg n_u v, in a fixed fma order: the rounding is not left to the
-// compiler's contraction, which differed between instantiations of different lane widths (1 ulp on
-// rare elements: the wide fp8 kernel against the 4-value one)
+// g_v of one element, A - Scx v + reg n_u v, and the occurrence sums, as fixed fma chains for the 16-bit
+// and fp8 tables: the rounding is not left to the compiler's contraction, which differed between
+// instantiations of different lane widths (1 ulp on rare elements: the wide fp8 kernel against the
+// 4-value one) -- and the fused forms made the k = 128 bf16 FTRL step 1.025 -> 0.94 ms.  fp32 tables
+// keep the plain expressions: pinned, the row-sharded step's k = 64 fp32 EMIT kernels ran 0.620 ->
+// 0.666 ms (profiles/r6/fp8_wide_ab.txt); no wide fp32 kernel needs the pinned bits.
+#ifndef FM_FMA_PIN
+#define FM_FMA_PIN 1  // 0: plain expressions for every dtype (A/B build variant "nopin")
+#endif
+template <typename TV>
+constexpr bool fma_pinned() { return FM_FMA_PIN && !std::is_same<TV, float>::value; }
+template <typename TV>
 __device__ __forceinline__ float row_grad(float A, float Scx, float nreg_v, float v) {
-  return __builtin_fmaf(nreg_v, v, __builtin_fmaf(-Scx, v, A));
+  if constexpr (fma_pinned<TV>()) return __builtin_fmaf(nreg_v, v, __builtin_fmaf(-Scx, v, A));
+  return A - Scx * v + nreg_v * v;
+}
+template <typename TV>
+__device__ __forceinline__ float fma_acc(float a, float b, float c) {
+  if constexpr (fma_pinned<TV>()) return __builtin_fmaf(a, b, c);
+  return c + a * b;
 }
 
 // EPL values of a table row for this lane: one Frag, or -- the wide fp8 kernel -- 8 fp8 values in
@@ -220,7 +235,7 @@ __device__ inline void bwd_finish_local(const BwdArgs& a, int t, bool tact, RowS
   const float nreg_v = a.reg_v * (float)n_u, nreg_w = a.reg_w * (float)n_u;
   float gr[EPL];
 #pragma unroll
-  for (int k = 0; k < EPL; ++k) gr[k] = row_grad(A[k], Scx, nreg_v, r.vv[k]);
+  for (int k = 0; k < EPL; ++k) gr[k] = row_grad<TV>(A[k], Scx, nreg_v, r.vv[k]);
   const float gw = Sc + nreg_w * r.wv;
   TV* tv = reinterpret_cast<TV*>(a.v);
   opt_step_row<TV, EPL>(a.opt, gr, r.vv, r.st0, r.st1);
@@ -278,7 +293,7 @@ __device__ inline void bwd_finish_emit(const BwdArgs& a, int u, int t, bool tact
   const float nreg_v = a.reg_v * (float)n_u, nreg_w = a.reg_w * (float)n_u;
   float gr[EPL];
 #pragma unroll
-  for (int k = 0; k < EPL; ++k) gr[k] = row_grad(A[k], Scx, nreg_v, r.vv[k]);
+  for (int k = 0; k < EPL; ++k) gr[k] = row_grad<TV>(A[k], Scx, nreg_v, r.vv[k]);
   const float gw = Sc + nreg_w * r.wv;
   if (!r.apply) {  // gradient row u for its owner's apply
     float* dst = row_ptr(a.grad_out, (long long)u, a.g_stride);
@@ -365,7 +380,7 @@ __device__ inline void bwd_finish(const BwdArgs& a, int u, int t, bool tact, Row
   const float nreg_v = a.reg_v * (float)n_u, nreg_w = a.reg_w * (float)n_u;
   float gr[EPL];
 #pragma unroll
-  for (int k = 0; k < EPL; ++k) gr[k] = row_grad(A[k], Scx, nreg_v, r.vv[k]);
+  for (int k = 0; k < EPL; ++k) gr[k] = row_grad<TV>(A[k], Scx, nreg_v, r.vv[k]);
   const float gw = Sc + nreg_w * r.wv;
   if (!r.apply) {
     float* dst = a.grad_out + (a.mode == kBwdEmitTable ? r.row : (long long)u) * a.g_stride;
@@ -615,8 +630,8 @@ __device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
 #pragma unroll
         for (int uu = 0; uu < UNRF; ++uu) {
 #pragma unroll
-          for (int k = 0; k < EPL; ++k) A[k] = __builtin_fmaf(cc[uu], rr[uu][k], A[k]);
-          Scx = __builtin_fmaf(cc[uu], xx[uu], Scx);
+          for (int k = 0; k < EPL; ++k) A[k] = fma_acc<TV>(cc[uu], rr[uu][k], A[k]);
+          Scx = fma_acc<TV>(cc[uu], xx[uu], Scx);
           Sc += cc[uu];
         }
       }
@@ -637,8 +652,8 @@ __device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
 #pragma unroll
       for (int uu = 0; uu < U4; ++uu) {
 #pragma unroll
-        for (int k = 0; k < EPL; ++k) A[k] = __builtin_fmaf(cc[uu], rr[uu][k], A[k]);
-        Scx = __builtin_fmaf(cc[uu], xx[uu], Scx);
+        for (int k = 0; k < EPL; ++k) A[k] = fma_acc<TV>(cc[uu], rr[uu][k], A[k]);
+        Scx = fma_acc<TV>(cc[uu], xx[uu], Scx);
         Sc += cc[uu];
       }
     } else {
@@ -658,8 +673,8 @@ __device__ __forceinline__ void bwd_chunk_body(const BwdArgs& a) {
 #pragma unroll
             for (int uu = 0; uu < UNR; ++uu) {
 #pragma unroll
-              for (int k = 0; k < EPL; ++k) A[k] = __builtin_fmaf(cc[uu], rr[uu][k], A[k]);
-              Scx = __builtin_fmaf(cc[uu], xx[uu], Scx);
+              for (int k = 0; k < EPL; ++k) A[k] = fma_acc<TV>(cc[uu], rr[uu][k], A[k]);
+              Scx = fma_acc<TV>(cc[uu], xx[uu], Scx);
               Sc += cc[uu];
             }
           }
