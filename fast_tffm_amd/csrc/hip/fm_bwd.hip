@@ -67,14 +67,6 @@ constexpr int kChunkUnr = FM_CHUNK_UNR;
 #ifndef FM_CHUNK_UNR_W8
 #define FM_CHUNK_UNR_W8 5
 #endif
-// Wide fp8 chunk kernel (FM_FP8_WIDE=1, default): the local step's fp8 rows reduced with 8 values per
-// lane -- 8-byte row loads, 16-byte r1 / optimizer-state loads and stores, LPR = Kp / 8 -- instead of
-// 4 (4-, 8- and 8-byte accesses): the same bytes with half the per-lane addresses, which the gather-
-// bound kernel spends its texture-address time on.  Bitwise the same results (fm_common.h
-// store_row_fp8x8); 0 keeps the 4-value kernel (the "fp8narrow" build variant, A/B).
-#ifndef FM_FP8_WIDE
-#define FM_FP8_WIDE 1
-#endif
 template <int LPR, bool LOC, bool EMT, typename TV>
 constexpr int chunk_unr() {
   return LOC && LPR == 32 ? FM_CHUNK_UNR32
@@ -174,32 +166,6 @@ template <typename TV>
 __device__ __forceinline__ float fma_acc(float a, float b, float c) {
   if constexpr (fma_pinned<TV>()) return __builtin_fmaf(a, b, c);
   return c + a * b;
-}
-
-// EPL values of a table row for this lane: one Frag, or -- the wide fp8 kernel -- 8 fp8 values in
-// one 8-byte load.
-template <typename TV, int EPL>
-__device__ inline void frag_load(const TV* p, float (&o)[EPL]) {
-  if constexpr (EPL == Frag<TV>::N) {
-    Frag<TV>::load(p, o);
-  } else {
-    static_assert(std::is_same<TV, fp8e4m3>::value && EPL == 8, "wide rows: fp8, 8 values per lane");
-    const uint2 u = *reinterpret_cast<const uint2*>(p);
-    float lo[4], hi[4];
-    Frag<TV>::cvt((int)u.x, lo);
-    Frag<TV>::cvt((int)u.y, hi);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      o[k] = lo[k];
-      o[k + 4] = hi[k];
-    }
-  }
-}
-template <int LPR, typename TV, int EPL>
-__device__ inline void store_row_e(TV* lane_ptr, const float (&o)[EPL], float* w, long long row, long long w_stride,
-                                   int t, bool tact, uint32_t sr) {
-  if constexpr (EPL == Frag<TV>::N) store_row<LPR, TV>(lane_ptr, o, w, row, w_stride, t, tact, sr);
-  else store_row_fp8x8<LPR>(lane_ptr, o, w, row, w_stride, t, tact, sr);
 }
 
 // LOCAL mode known at compile time (the chunk kernel's local instantiations): table row `key`,

@@ -459,6 +459,42 @@ __device__ inline void store_row_fp8x8(fp8e4m3* lane_ptr, const float (&o)[8], f
   }
 }
 
+// Wide fp8 kernels (FM_FP8_WIDE=1, default): k = 128 fp8 rows reduced / updated with 8 values per lane --
+// 8-byte row loads, 16-byte r1 / optimizer-state / bf16-gradient accesses, LPR = Kp / 8 -- instead of 4
+// (4-, 8- and 8-byte accesses): the same bytes with half the per-lane addresses, which the gather-bound
+// kernels spend their texture-address time on, and twice the rows per wave.  The chunk backward (local and
+// EMIT kinds) and the owner apply; bitwise the same results (store_row_fp8x8).  0 keeps the 4-value kernels
+// (the "fp8narrow" build variant, A/B).
+#ifndef FM_FP8_WIDE
+#define FM_FP8_WIDE 1
+#endif
+
+// EPL values of a table row for this lane: one Frag, or -- the wide fp8 kernel -- 8 fp8 values in
+// one 8-byte load.
+template <typename TV, int EPL>
+__device__ inline void frag_load(const TV* p, float (&o)[EPL]) {
+  if constexpr (EPL == Frag<TV>::N) {
+    Frag<TV>::load(p, o);
+  } else {
+    static_assert(std::is_same<TV, fp8e4m3>::value && EPL == 8, "wide rows: fp8, 8 values per lane");
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    float lo[4], hi[4];
+    Frag<TV>::cvt((int)u.x, lo);
+    Frag<TV>::cvt((int)u.y, hi);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o[k] = lo[k];
+      o[k + 4] = hi[k];
+    }
+  }
+}
+template <int LPR, typename TV, int EPL>
+__device__ inline void store_row_e(TV* lane_ptr, const float (&o)[EPL], float* w, long long row, long long w_stride,
+                                   int t, bool tact, uint32_t sr) {
+  if constexpr (EPL == Frag<TV>::N) store_row<LPR, TV>(lane_ptr, o, w, row, w_stride, t, tact, sr);
+  else store_row_fp8x8<LPR>(lane_ptr, o, w, row, w_stride, t, tact, sr);
+}
+
 // Per-step seed of the stochastic rounding (device counter ticked once per training
 // step, so hipGraph replays draw fresh bits); 0 = round to nearest even.
 __device__ inline uint32_t sr_step_seed(const int* counter) {

@@ -190,10 +190,10 @@ struct ApplyArgs {
 // One table row's parameters + optimizer state in registers (this lane's EPL
 // columns; lane t == 0 also holds w and its state).  load() is issued before the
 // gradient sum so that the row's loads overlap it.
-template <int LPR, typename TV>
+template <int LPR, typename TV, int EW = 0>
 struct RowUpdate {
   using F = Frag<TV>;
-  static constexpr int EPL = F::N;
+  static constexpr int EPL = EW ? EW : F::N;  // (EW: the wide fp8 apply's 8 values per lane)
   float vv[EPL], st0[EPL], st1[EPL];
   float pw, q0, q1;
   TV* vrow;
@@ -201,7 +201,7 @@ struct RowUpdate {
 
   __device__ inline void load(const ApplyArgs& a, long long row, int tE) {
     vrow = reinterpret_cast<TV*>(a.v) + row * a.v_stride + tE * EPL;
-    F::load(vrow, vv);
+    frag_load<TV, EPL>(vrow, vv);
     if constexpr (F::kScaled) {
       const float s = row_scale<TV>(a.w, row, a.w_stride);
 #pragma unroll
@@ -223,7 +223,7 @@ struct RowUpdate {
   __device__ inline void step_store(const ApplyArgs& a, const float (&gr)[EPL], float gw, long long row, int t,
                                     bool tact, uint32_t sr) {
     opt_step_row<TV, EPL>(a.opt, gr, vv, st0, st1);
-    store_row<LPR, TV>(vrow, vv, a.w, row, a.w_stride, t, tact, sr);
+    store_row_e<LPR, TV, EPL>(vrow, vv, a.w, row, a.w_stride, t, tact, sr);
     if (tact) {
       const uint32_t col = (uint32_t)(t * EPL);
       store_state<TV, EPL>(a.s0v, soff, st0, sr ? sr ^ kSrSalt0 : 0u, (uint32_t)row, col);
@@ -241,13 +241,10 @@ struct RowUpdate {
 template <int EPL>
 __device__ inline void add_grad_row(const ApplyArgs& a, const float* src, int tE, float (&gr)[EPL], float& gw) {
   if (a.g_bf16) {
-    const uint16_t* s16 = reinterpret_cast<const uint16_t*>(src) + tE * EPL;
+    float h[EPL];
+    load_bf16x<EPL>(reinterpret_cast<const uint16_t*>(src) + tE * EPL, h);
 #pragma unroll
-    for (int k = 0; k < EPL; k += 4) {
-      const uint2 f = *reinterpret_cast<const uint2*>(s16 + k);
-      gr[k] += bf16_bits_to_f32(f.x & 0xffffu); gr[k + 1] += bf16_bits_to_f32(f.x >> 16);
-      gr[k + 2] += bf16_bits_to_f32(f.y & 0xffffu); gr[k + 3] += bf16_bits_to_f32(f.y >> 16);
-    }
+    for (int k = 0; k < EPL; ++k) gr[k] += h[k];
   } else {
 #pragma unroll
     for (int k = 0; k < EPL; k += 4) {
@@ -469,10 +466,10 @@ int launch_run_member(int R, const int* req, int W, const int* run_off, const in
   return (int)hipGetLastError();
 }
 
-template <int LPR, typename TV>
+template <int LPR, typename TV, int EW = 0>
 __global__ __launch_bounds__(kBlock) void apply_runs_kernel(ApplyArgs a) {
   const uint32_t sr = sr_step_seed(a.sr_counter);  // stochastic rounding seed (0: nearest)
-  constexpr int EPL = Frag<TV>::N;
+  constexpr int EPL = EW ? EW : Frag<TV>::N;
   constexpr int G = kWave / LPR;
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR, t = lane % LPR;
@@ -492,7 +489,7 @@ __global__ __launch_bounds__(kBlock) void apply_runs_kernel(ApplyArgs a) {
       if (!led) continue;  // an earlier run holds this row: its leader applies it
     }
     const long long row = a.req[i];
-    RowUpdate<LPR, TV> ru;
+    RowUpdate<LPR, TV, EW> ru;
     ru.load(a, row, tE);
     float gr[EPL];
 #pragma unroll
@@ -568,6 +565,19 @@ int launch_apply_runs(const ApplyArgs& a, int* match, int dtype, hipStream_t st)
                        a.run_off, a.req, match);
   }
   const int lpr = lanes_per_row(a.Kp, dtype);
+#ifndef FM_FP8_WIDE_APPLY
+#define FM_FP8_WIDE_APPLY FM_FP8_WIDE  // (the owner apply alone: the "fp8narrowapply" variant, A/B)
+#endif
+#if FM_FP8_WIDE_APPLY
+  // wide fp8 rows (k = 128: 16 lanes x 8 values; rows, state and gradient rows 8 / 16-byte aligned)
+  if (dtype == kFP8 && lpr == 32 && a.Kp % 8 == 0 && a.v_stride % 8 == 0 && a.s_stride % 8 == 0 && a.g_stride % 4 == 0 &&
+      (uintptr_t)a.v % 8 == 0 && (uintptr_t)a.s0v % 16 == 0 && (uintptr_t)a.s1v % 16 == 0 &&
+      (uintptr_t)a.grad_in % 16 == 0) {
+    const int grid = fill_grid(a.R, kWavesPerBlock * (kWave / 16));
+    hipLaunchKernelGGL((apply_runs_kernel<16, fp8e4m3, 8>), dim3(grid), dim3(kBlock), 0, st, a);
+    return (int)hipGetLastError();
+  }
+#endif
   const int grid = fill_grid(a.R, kWavesPerBlock * (kWave / lpr));
   FM_DISPATCH(dtype, lpr, apply_runs_kernel, grid, st, a);
   return (int)hipGetLastError();
