@@ -319,7 +319,7 @@ __device__ inline void bwd_load(const BwdArgs& a, int u, long long key, int tE, 
     r.apply = a.self.exclusive(u);
     vsrc = a.self.v; wsrc = a.self.w; vst = a.self.v_stride; wst = a.self.w_stride;
   }
-  F::load(reinterpret_cast<const TV*>(vsrc) + r.row * vst + tE * EPL, r.vv);
+  frag_load<TV, EPL>(reinterpret_cast<const TV*>(vsrc) + r.row * vst + tE * EPL, r.vv);
   r.wv = wsrc[r.row * wst];
   if constexpr (F::kScaled) {
     const float s = row_scale<TV>(wsrc, r.row, wst);
@@ -378,7 +378,7 @@ __device__ inline void bwd_finish(const BwdArgs& a, int u, int t, bool tact, Row
   float* tw = own ? a.self.w : a.w;
   const long long tvs = own ? a.self.v_stride : a.v_stride, tws = own ? a.self.w_stride : a.w_stride;
   opt_step_row<TV, EPL>(a.opt, gr, r.vv, r.st0, r.st1);
-  store_row<LPR, TV>(tv + r.row * tvs + t * EPL, r.vv, tw, r.row, tws, t, tact, sr);
+  store_row_e<LPR, TV, EPL>(tv + r.row * tvs + t * EPL, r.vv, tw, r.row, tws, t, tact, sr);
   if (tact) {
     const long long off = r.row * a.s_stride + t * EPL;
     store_state<TV, EPL>(a.s0v, off, r.st0, sr ? sr ^ kSrSalt0 : 0u, (uint32_t)r.row, (uint32_t)(t * EPL));
@@ -707,10 +707,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
 void fm_bwd_chunk_emit_w8_kernel(BwdArgs a) { bwd_chunk_body<16, fp8e4m3, KIND, 8>(a); }
 #endif
 
-// Rows split over 2..kSmallChunks chunks: one lane group, ordered sum of the partials.
-template <int LPR, typename TV>
+// Rows split over 2..kSmallChunks chunks: one lane group, ordered sum of the partials (EW: the wide fp8
+// form, 8 values per lane -- the same sums in the same order).
+template <int LPR, typename TV, int EW = 0>
 __device__ inline void bwd_combine_body(const BwdArgs& a, int blk, int nblk, uint32_t sr) {
-  constexpr int EPL = Frag<TV>::N;
+  constexpr int EPL = EW ? EW : Frag<TV>::N;
   constexpr int G = kWave / LPR;
   const int lane = threadIdx.x & (kWave - 1);
   const int g = lane / LPR, t = lane % LPR;
@@ -843,6 +844,14 @@ __global__ __launch_bounds__(kBlock) void fm_bwd_combine_kernel(BwdArgs a) {
   if ((int)blockIdx.x < a.big_blocks) bwd_big_body<LPR, TV>(a, blockIdx.x, a.big_blocks, sr);
   else bwd_combine_body<LPR, TV>(a, blockIdx.x - a.big_blocks, gridDim.x - a.big_blocks, sr);
 }
+#if FM_FP8_WIDE
+// the lane-group combine of the wide fp8 rows (the hot-row workgroup combine keeps 4 values per lane: its
+// group count fixes the summation order)
+template <int LPR>
+__global__ __launch_bounds__(kBlock) void fm_bwd_combine_w8_kernel(BwdArgs a) {
+  bwd_combine_body<LPR, fp8e4m3, 8>(a, blockIdx.x, gridDim.x, sr_step_seed(a.sr_counter));
+}
+#endif
 
 // specialised kinds (local / EMIT) share the launch shape: EMIT runs the local step's kernel body
 static bool fast_kind(int kind) { return kind != kChunkAny; }
@@ -952,6 +961,15 @@ int launch_bwd(const BwdArgs& a, int dtype, long long max_chunks, long long max_
   BwdArgs b = a;
   if (lpr >= 32) {  // (one launch lost for 32-lane rows: above)
     b.big_blocks = 0;
+#ifndef FM_FP8_WIDE_COMBINE
+#define FM_FP8_WIDE_COMBINE 1  // (0: the 4-value lane-group combine beside the wide chunk kernel, A/B)
+#endif
+#if FM_FP8_WIDE
+    if (wide && FM_FP8_WIDE_COMBINE)
+      hipLaunchKernelGGL(fm_bwd_combine_w8_kernel<16>, dim3(fill_grid(max_unique, kWavesPerBlock * (kWave / 16), 2048)),
+                         dim3(kBlock), 0, st, b);
+    else
+#endif
     FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, g2, st, b);
     b.big_blocks = kBigBlocks;
     FM_DISPATCH(dtype, lpr, fm_bwd_combine_kernel, kBigBlocks, st, b);
