@@ -16,6 +16,7 @@ HIP_VARIANTS: dict[str, list[str]] = {"fwdnopf": ["-DFM_FWD_PREFETCH=0"], "fwdge
                                      "sh16u6w5": ["-DFM_FWD_UNR16_SH=6", "-DFM_FWD_SH_W16=5"],
                                      "mfma": ["-DFM_WITH_MFMA=1"], "mfprof": ["-DFM_WITH_MFMA=1", "-DFM_MF_PROF=1"],
                                      "fp8slow": ["-DFM_FP8_FAST_EPI=0"], "r1nomask": ["-DFM_R1_MASK=0"],
-                                     "chunkperm": ["-DFM_CHUNK_PERM=1"], "fp8narrow": ["-DFM_FP8_WIDE=0"], "fp8narrowapply": ["-DFM_FP8_WIDE_APPLY=0"],
+                                     "chunkperm": ["-DFM_CHUNK_PERM=1"], "fp8narrow": ["-DFM_FP8_WIDE=0"],
+                                     "fp8narrowapply": ["-DFM_FP8_WIDE_APPLY=0"],
                                      "fp8narrowcomb": ["-DFM_FP8_WIDE_COMBINE=0"],
                                      "nopin": ["-DFM_FMA_PIN=0"]}
